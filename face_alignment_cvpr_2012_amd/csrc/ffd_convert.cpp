@@ -1,0 +1,353 @@
+// ffd_convert.cpp — offline converter: reference Boost text archives -> FFDMODEL.
+//
+// Replaces the run-time archive load of the reference:
+//   FaceForest::FaceForest            /root/reference/src/FaceForest.cpp:15-58
+//   Forest<S>::load / load_tree       /root/reference/include/Forest.hpp:103-153
+//   Tree<S>::load / serialize         /root/reference/include/Tree.hpp:193-237,336-343
+//   TreeNode<S>::serialize            /root/reference/include/TreeNode.hpp:150-164
+//   ThresholdSplit / SimplePatchFeature serializers
+//                                     ThresholdSplit.hpp:60-67, ImageSample.hpp:83-90
+//   MPLeaf / HeadPoseLeaf serializers MPSample.hpp:149-158, HeadPoseSample.hpp:154-161
+//   loadConfigFile                    /root/reference/src/face_utils.cpp:50-140
+// Archive grammar: SURVEY.md Appendix A.  Trees whose i_node != m_num_nodes are
+// rejected exactly like Forest::load_tree (Forest.hpp:142-152).
+//
+// usage: ffd_convert <reference_root> <out.bin>
+//   reads <root>/data/config_headpose.txt and <root>/data/config_ffd.txt, then
+//   the tree directories they name (relative to <root>); the FFD directory is
+//   scanned for sub-directories which are sorted (FaceForest.cpp:39-45).
+#include <dirent.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "model_io.hpp"
+
+namespace {
+
+struct ForestParam {  // Constants.hpp:24-60
+  int max_depth = 15, min_patches = 20, ntests = 250, ntrees = 10, nimages = 500, npatches = 200,
+      face_size = 100;
+  float patch_size_ratio = 0.25f;
+  std::string tree_path, image_path;
+  std::vector<int> features;
+};
+
+// loadConfigFile (face_utils.cpp:50-140): fixed order of (comment line, value line) pairs.
+bool load_config(const std::string& path, ForestParam& p) {
+  std::ifstream f(path);
+  if (!f.is_open()) return false;
+  std::string line;
+  auto next_value = [&](std::string& out) {
+    if (!std::getline(f, line)) return false;  // "____..." label line
+    if (!std::getline(f, out)) return false;
+    while (!out.empty() && (out.back() == '\r' || out.back() == ' ')) out.pop_back();
+    return true;
+  };
+  std::string v;
+  if (!next_value(p.image_path)) return false;
+  if (!next_value(p.tree_path)) return false;
+  if (!next_value(v)) return false; p.ntrees = std::stoi(v);
+  if (!next_value(v)) return false; p.ntests = std::stoi(v);
+  if (!next_value(v)) return false; p.max_depth = std::stoi(v);
+  if (!next_value(v)) return false; p.min_patches = std::stoi(v);
+  if (!next_value(v)) return false; p.nimages = std::stoi(v);
+  if (!next_value(v)) return false; p.npatches = std::stoi(v);
+  if (!next_value(v)) return false; p.face_size = std::stoi(v);
+  if (!next_value(v)) return false; p.patch_size_ratio = std::stof(v);
+  if (!next_value(v)) return false;
+  std::istringstream ss(v);
+  std::string tok;
+  while (ss >> tok) p.features.push_back((int)std::stof(tok));  // lexical_cast<float> then int
+  return true;
+}
+
+// Whitespace tokenizer over a memory-mapped archive.
+class Tokens {
+ public:
+  explicit Tokens(const std::string& path) : path_(path) {
+    fd_ = ::open(path.c_str(), O_RDONLY);
+    if (fd_ < 0) throw std::runtime_error("File not found: " + path);
+    struct stat st;
+    fstat(fd_, &st);
+    size_ = (size_t)st.st_size;
+    data_ = (const char*)mmap(nullptr, size_, PROT_READ, MAP_PRIVATE, fd_, 0);
+    if (data_ == MAP_FAILED) throw std::runtime_error("mmap failed: " + path);
+  }
+  ~Tokens() {
+    munmap((void*)data_, size_);
+    ::close(fd_);
+  }
+  std::string next() {
+    while (pos_ < size_ && isspace((unsigned char)data_[pos_])) pos_++;
+    if (pos_ >= size_) throw std::runtime_error("unexpected end of archive " + path_);
+    size_t s = pos_;
+    while (pos_ < size_ && !isspace((unsigned char)data_[pos_])) pos_++;
+    return std::string(data_ + s, pos_ - s);
+  }
+  long i() {
+    std::string t = next();
+    char* e = nullptr;
+    long v = std::strtol(t.c_str(), &e, 10);
+    if (*e) throw std::runtime_error("expected int, got '" + t + "' in " + path_);
+    return v;
+  }
+  float f() {  // text_iarchive reads float via istream >> float (correctly rounded)
+    std::string t = next();
+    char* e = nullptr;
+    float v = std::strtof(t.c_str(), &e);
+    if (*e) throw std::runtime_error("expected float, got '" + t + "' in " + path_);
+    return v;
+  }
+  double d() {
+    std::string t = next();
+    char* e = nullptr;
+    double v = std::strtod(t.c_str(), &e);
+    if (*e) throw std::runtime_error("expected double, got '" + t + "' in " + path_);
+    return v;
+  }
+  std::string str() {  // length-prefixed string; our paths contain no spaces
+    long n = i();
+    if (n == 0) return std::string();
+    std::string s = next();
+    if ((long)s.size() != n) throw std::runtime_error("string length mismatch in " + path_);
+    return s;
+  }
+  void expect(long v, const char* what) {
+    long g = i();
+    if (g != v)
+      throw std::runtime_error(std::string("archive grammar: expected ") + what + " in " + path_);
+  }
+  bool at_end() {
+    while (pos_ < size_ && isspace((unsigned char)data_[pos_])) pos_++;
+    return pos_ >= size_;
+  }
+
+ private:
+  std::string path_;
+  int fd_ = -1;
+  const char* data_ = nullptr;
+  size_t size_ = 0, pos_ = 0;
+};
+
+enum Kind { HP, MP };
+
+struct ForestOut {
+  std::vector<int64_t> tree_node_off{0}, tree_leaf_off{0};
+  std::vector<int32_t> node_leaf;
+  std::vector<int16_t> node_split;
+  std::vector<int32_t> leaf_n;
+  std::vector<float> leaf_fg;
+  std::vector<int32_t> hp_labels;
+  std::vector<int16_t> mp_offset;
+  std::vector<float> mp_var, mp_pf;
+};
+
+struct TreeParseState {
+  bool first_leaf = true, first_split = true, first_vec_point = true;
+  long next_object_id = 0;
+  long nodes = 0;
+};
+
+void parse_node(Tokens& tk, Kind kind, TreeParseState& st, ForestOut& out, int depth) {
+  long oid = tk.i();
+  if (oid != st.next_object_id)
+    throw std::runtime_error("archive grammar: unexpected object id");
+  st.next_object_id++;
+  st.nodes++;
+  long d = tk.i();
+  long is_leaf = tk.i();
+  long has_split = tk.i();
+  if (d != depth) throw std::runtime_error("archive grammar: depth mismatch");
+  int16_t split[FFD_SPLIT_FIELDS] = {0};
+  if (is_leaf) {
+    if (st.first_leaf) { tk.expect(0, "leaf class tracking"); tk.expect(0, "leaf class version"); st.first_leaf = false; }
+    out.node_leaf.push_back((int32_t)out.leaf_n.size());
+    if (kind == HP) {
+      out.leaf_n.push_back((int32_t)tk.i());
+      out.leaf_fg.push_back(tk.f());
+      long cnt = tk.i();
+      tk.expect(0, "vector<int> item_version");
+      if (cnt != FFD_NUM_HP_LABELS) throw std::runtime_error("HP leaf: expected 5 labels");
+      for (long j = 0; j < cnt; j++) out.hp_labels.push_back((int32_t)tk.i());
+    } else {
+      out.leaf_n.push_back((int32_t)tk.i());
+      if (st.first_vec_point) { tk.expect(0, "vector<Point> tracking"); tk.expect(0, "vector<Point> version"); }
+      long cnt = tk.i();
+      tk.expect(0, "vector<Point> item_version");
+      if (st.first_vec_point) { tk.expect(0, "Point tracking"); tk.expect(0, "Point version"); st.first_vec_point = false; }
+      if (cnt != FFD_NUM_PARTS) throw std::runtime_error("MP leaf: expected 10 parts");
+      for (long j = 0; j < cnt; j++) {
+        long x = tk.i(), y = tk.i();
+        if (x < -32768 || x > 32767 || y < -32768 || y > 32767) throw std::runtime_error("offset out of int16");
+        out.mp_offset.push_back((int16_t)x);
+        out.mp_offset.push_back((int16_t)y);
+      }
+      cnt = tk.i();
+      tk.expect(0, "vector<float> item_version");
+      if (cnt != FFD_NUM_PARTS) throw std::runtime_error("MP leaf: expected 10 variances");
+      for (long j = 0; j < cnt; j++) out.mp_var.push_back(tk.f());
+      cnt = tk.i();
+      tk.expect(0, "vector<float> item_version");
+      if (cnt != FFD_NUM_PARTS) throw std::runtime_error("MP leaf: expected 10 probabilities");
+      for (long j = 0; j < cnt; j++) out.mp_pf.push_back(tk.f());
+      out.leaf_fg.push_back(tk.f());
+    }
+  } else {
+    out.node_leaf.push_back(-1);
+  }
+  if (has_split) {
+    if (st.first_split) {
+      tk.expect(0, "ThresholdSplit tracking"); tk.expect(0, "ThresholdSplit version");
+      tk.expect(0, "SimplePatchFeature tracking"); tk.expect(0, "SimplePatchFeature version");
+    }
+    split[0] = (int16_t)tk.i();  // feature_channel
+    if (st.first_split) { tk.expect(0, "Rect tracking"); tk.expect(0, "Rect version"); st.first_split = false; }
+    for (int j = 0; j < 8; j++) split[1 + j] = (int16_t)tk.i();  // rect1, rect2 (x y w h)
+    (void)tk.d();                                                 // info (unused at test time)
+    long thr = tk.i();
+    if (thr < -32768 || thr > 32767) throw std::runtime_error("threshold out of int16");
+    split[9] = (int16_t)thr;
+  }
+  if (is_leaf && has_split) throw std::runtime_error("node is both leaf and split");
+  if (!is_leaf && !has_split) throw std::runtime_error("internal node without split");
+  for (int j = 0; j < FFD_SPLIT_FIELDS; j++) out.node_split.push_back(is_leaf ? 0 : split[j]);
+  if (!is_leaf) {
+    tk.expect(3, "TreeNode pointer class id");
+    parse_node(tk, kind, st, out, depth + 1);
+    tk.expect(3, "TreeNode pointer class id");
+    parse_node(tk, kind, st, out, depth + 1);
+  }
+}
+
+void parse_tree(const std::string& path, Kind kind, ForestOut& out) {
+  Tokens tk(path);
+  tk.expect(22, "signature length");
+  if (tk.next() != "serialization::archive") throw std::runtime_error("not a boost archive: " + path);
+  tk.expect(10, "library version");
+  tk.expect(0, "Tree tracking");
+  tk.expect(0, "Tree version");
+  long num_nodes = tk.i(), i_node = tk.i();
+  // ForestParam (Constants.hpp:44-59)
+  tk.expect(0, "ForestParam tracking");
+  tk.expect(0, "ForestParam version");
+  for (int j = 0; j < 7; j++) (void)tk.i();
+  (void)tk.f();
+  (void)tk.str();
+  (void)tk.str();
+  long nf = tk.i();
+  tk.expect(0, "features item_version");
+  for (long j = 0; j < nf; j++) (void)tk.i();
+  (void)tk.str();  // m_save_path
+  // root pointer: class id 3, tracking 1, version 0
+  tk.expect(3, "root class id");
+  tk.expect(1, "TreeNode tracking");
+  tk.expect(0, "TreeNode version");
+  TreeParseState st;
+  parse_node(tk, kind, st, out, 0);
+  if (!tk.at_end()) throw std::runtime_error("trailing tokens in " + path);
+  // Tree::isFinished (Tree.hpp:72-79) gate of Forest::load_tree (Forest.hpp:142-152)
+  if (i_node != num_nodes) throw std::runtime_error("Tree is not finished successfully: " + path);
+  out.tree_node_off.push_back((int64_t)out.node_leaf.size());
+  out.tree_leaf_off.push_back((int64_t)out.leaf_n.size());
+}
+
+std::vector<std::string> sorted_subdirs(const std::string& dir) {
+  std::vector<std::string> v;
+  DIR* d = opendir(dir.c_str());
+  if (!d) throw std::runtime_error("cannot open directory " + dir);
+  while (struct dirent* e = readdir(d)) {
+    std::string n = e->d_name;
+    if (n == "." || n == "..") continue;
+    std::string full = dir + "/" + n;
+    struct stat st;
+    if (stat(full.c_str(), &st) == 0 && S_ISDIR(st.st_mode)) v.push_back(full);
+  }
+  closedir(d);
+  std::sort(v.begin(), v.end());
+  return v;
+}
+
+void put_params(ffd::ModelFile& m, const std::string& p, const ForestParam& fp, int n_forests) {
+  m.put<int32_t>(p + ".param", "i32", {8},
+                 {fp.max_depth, fp.min_patches, fp.ntests, fp.ntrees, fp.nimages, fp.npatches,
+                  fp.face_size, n_forests});
+  m.put<float>(p + ".patch_ratio", "f32", {1}, {fp.patch_size_ratio});
+  std::vector<int32_t> feats(fp.features.begin(), fp.features.end());
+  m.put<int32_t>(p + ".features", "i32", {(uint64_t)feats.size()}, feats);
+}
+
+void put_forest(ffd::ModelFile& m, const std::string& p, Kind kind, const ForestOut& o) {
+  uint64_t T = o.tree_node_off.size() - 1, N = o.node_leaf.size(), L = o.leaf_n.size();
+  m.put<int64_t>(p + ".tree_node_off", "i64", {T + 1}, o.tree_node_off);
+  m.put<int64_t>(p + ".tree_leaf_off", "i64", {T + 1}, o.tree_leaf_off);
+  m.put<int32_t>(p + ".node_leaf", "i32", {N}, o.node_leaf);
+  m.put<int16_t>(p + ".node_split", "i16", {N, FFD_SPLIT_FIELDS}, o.node_split);
+  m.put<int32_t>(p + ".leaf_n", "i32", {L}, o.leaf_n);
+  m.put<float>(p + ".leaf_fg", "f32", {L}, o.leaf_fg);
+  if (kind == HP) {
+    m.put<int32_t>(p + ".leaf_labels", "i32", {L, FFD_NUM_HP_LABELS}, o.hp_labels);
+  } else {
+    m.put<int16_t>(p + ".leaf_offset", "i16", {L, FFD_NUM_PARTS, 2}, o.mp_offset);
+    m.put<float>(p + ".leaf_var", "f32", {L, FFD_NUM_PARTS}, o.mp_var);
+    m.put<float>(p + ".leaf_pf", "f32", {L, FFD_NUM_PARTS}, o.mp_pf);
+  }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc != 3) {
+    std::fprintf(stderr, "usage: %s <reference_root> <out.bin>\n", argv[0]);
+    return 2;
+  }
+  std::string root = argv[1], outp = argv[2];
+  try {
+    ForestParam hp, mp;
+    if (!load_config(root + "/data/config_headpose.txt", hp))
+      throw std::runtime_error("cannot parse config_headpose.txt");
+    if (!load_config(root + "/data/config_ffd.txt", mp))
+      throw std::runtime_error("cannot parse config_ffd.txt");
+    ffd::ModelFile m;
+    ForestOut hpo;
+    char buf[512];
+    for (int i = 0; i < hp.ntrees; i++) {  // Forest::load (Forest.hpp:116-127)
+      std::snprintf(buf, sizeof buf, "%s/%s/tree_%03d.txt", root.c_str(), hp.tree_path.c_str(), i);
+      parse_tree(buf, HP, hpo);
+    }
+    put_params(m, "hp", hp, 1);
+    put_forest(m, "hp", HP, hpo);
+    std::vector<std::string> dirs = sorted_subdirs(root + "/" + mp.tree_path);
+    if (dirs.empty()) throw std::runtime_error("no FFD forest directories");
+    ForestOut mpo;
+    for (auto& d : dirs)
+      for (int i = 0; i < mp.ntrees; i++) {
+        std::snprintf(buf, sizeof buf, "%s/tree_%03d.txt", d.c_str(), i);
+        parse_tree(buf, MP, mpo);
+      }
+    put_params(m, "mp", mp, (int)dirs.size());
+    put_forest(m, "mp", MP, mpo);
+    std::string tmp = outp + ".tmp";
+    m.save(tmp);
+    if (std::rename(tmp.c_str(), outp.c_str()) != 0) throw std::runtime_error("rename failed");
+    std::printf("ffd_convert: hp %zu trees %zu nodes %zu leaves; mp %zu forests %zu trees %zu nodes %zu leaves -> %s\n",
+                hpo.tree_node_off.size() - 1, hpo.node_leaf.size(), hpo.leaf_n.size(), dirs.size(),
+                mpo.tree_node_off.size() - 1, mpo.node_leaf.size(), mpo.leaf_n.size(), outp.c_str());
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "ffd_convert: ERROR: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}

@@ -1,0 +1,71 @@
+/*
+ * ffd_numerics.h — the numeric definitions shared by the CPU oracle and the
+ * HIP kernels so both produce identical bits.
+ *
+ * The reference calls libm `exp` inside areaUnderCurve
+ * (/root/reference/src/face_utils.cpp:304-323) and `expf` inside
+ * MeanShift::getWeightedMean (/root/reference/include/MeanShift.hpp:106-135).
+ * glibc's and the GPU's (ocml) exponentials are both faithful (<1 ulp) but not
+ * bitwise identical, and the head-pose tree selection takes floor(area*20)
+ * (FaceForest.cpp:243), so a 1-ulp difference could flip a tree choice.  The
+ * restatement therefore DEFINES exp as the deterministic routine below
+ * (Cody-Waite reduction + degree-13 Taylor/Horner, no FMA contraction), used
+ * by both sides.  Its accuracy against libm is checked in
+ * tests/test_numerics.py (|err| <= 2 ulp).
+ *
+ * Everything here is IEEE binary64/binary32 arithmetic with round-to-nearest
+ * and no contraction; both the oracle (g++ -ffp-contract=off) and the kernels
+ * (hipcc -ffp-contract=off) are compiled that way.
+ */
+#ifndef FFD_NUMERICS_H
+#define FFD_NUMERICS_H
+
+#if defined(__HIPCC__)
+#define FFD_HD __host__ __device__ __forceinline__
+#else
+#define FFD_HD static inline
+#endif
+
+#ifdef __cplusplus
+#include <cmath>
+#define FFD_RINT(x) std::rint(x)
+#define FFD_LDEXP(x, k) std::ldexp((x), (k))
+#else
+#include <math.h>
+#define FFD_RINT(x) rint(x)
+#define FFD_LDEXP(x, k) ldexp((x), (k))
+#endif
+
+/* exp(x) in binary64. */
+FFD_HD double ffd_exp(double x) {
+  if (x != x) return x;                               /* NaN */
+  if (x > 709.782712893384) return HUGE_VAL;           /* overflow */
+  if (x < -745.1332191019412) return 0.0;              /* underflow */
+  const double log2e = 1.4426950408889634074;
+  const double ln2_hi = 6.93147180369123816490e-01;   /* 0x3FE62E42FEE00000 */
+  const double ln2_lo = 1.90821492927058770002e-10;   /* 0x3DEA39EF35793C76 */
+  double kd = FFD_RINT(x * log2e);
+  int k = (int)kd;
+  double hi = x - kd * ln2_hi; /* exact: kd*ln2_hi has <= 43 significant bits */
+  double r = hi - kd * ln2_lo;
+  double p = 1.0 / 6227020800.0;           /* 1/13! */
+  p = p * r + 1.0 / 479001600.0;           /* 1/12! */
+  p = p * r + 1.0 / 39916800.0;            /* 1/11! */
+  p = p * r + 1.0 / 3628800.0;             /* 1/10! */
+  p = p * r + 1.0 / 362880.0;              /* 1/9!  */
+  p = p * r + 1.0 / 40320.0;               /* 1/8!  */
+  p = p * r + 1.0 / 5040.0;                /* 1/7!  */
+  p = p * r + 1.0 / 720.0;                 /* 1/6!  */
+  p = p * r + 1.0 / 120.0;                 /* 1/5!  */
+  p = p * r + 1.0 / 24.0;                  /* 1/4!  */
+  p = p * r + 1.0 / 6.0;                   /* 1/3!  */
+  p = p * r + 0.5;                         /* 1/2!  */
+  p = p * r + 1.0;
+  p = p * r + 1.0;
+  return FFD_LDEXP(p, k);
+}
+
+/* expf(x) in binary32, defined as the binary32 rounding of ffd_exp. */
+FFD_HD float ffd_expf(float x) { return (float)ffd_exp((double)x); }
+
+#endif /* FFD_NUMERICS_H */

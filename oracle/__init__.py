@@ -1,0 +1,173 @@
+"""ctypes wrapper for the CPU restatement (oracle/ffd_oracle.cpp).
+
+TEST INFRASTRUCTURE: only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this package.  The product (the HIP engine behind
+include/ffd.h) never links, calls or falls back to it.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libffd_oracle.so")
+MAX_TREES = 32
+
+
+class OracleFace(ctypes.Structure):
+    _fields_ = [
+        ("headpose", ctypes.c_float),
+        ("pose_variance", ctypes.c_float),
+        ("face_w", ctypes.c_int32),
+        ("face_h", ctypes.c_int32),
+        ("n_trees", ctypes.c_int32),
+        ("points", (ctypes.c_int32 * 2) * 10),
+    ]
+
+
+class OracleTrace(ctypes.Structure):
+    _fields_ = [
+        ("face", ctypes.c_void_p),
+        ("channels", ctypes.c_void_p),
+        ("hp_leaves", ctypes.c_void_p),
+        ("mp_leaves", ctypes.c_void_p),
+        ("trees", ctypes.c_void_p),
+        ("pose_freq", ctypes.c_void_p),
+        ("vote_counts", ctypes.c_void_p),
+        ("ms_mean", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"oracle library missing: {LIB_PATH} (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        L.oracle_load_model.argtypes = [ctypes.c_char_p]
+        L.oracle_last_error.restype = ctypes.c_char_p
+        L.oracle_analyze_face.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 8 + [
+            ctypes.POINTER(OracleFace), ctypes.POINTER(OracleTrace)]
+        L.oracle_face_geometry.argtypes = [ctypes.c_int32, ctypes.c_int32] + [ctypes.POINTER(ctypes.c_int32)] * 4
+        L.oracle_bgr2gray.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 3 + [ctypes.c_void_p]
+        L.oracle_resize.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 5 + [ctypes.c_void_p]
+        L.oracle_channels.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
+        L.oracle_gabor_kernel.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]
+        L.oracle_gabor_mag.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
+        L.oracle_area_under_curve.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_double, ctypes.c_double]
+        L.oracle_area_under_curve.restype = ctypes.c_double
+        L.oracle_exp.argtypes = [ctypes.c_double]
+        L.oracle_exp.restype = ctypes.c_double
+        _lib = L
+    return _lib
+
+
+_loaded_model = None
+
+
+def load_model(path):
+    global _loaded_model
+    if _loaded_model == path:
+        return
+    if lib().oracle_load_model(path.encode()) != 0:
+        raise RuntimeError("oracle_load_model: " + lib().oracle_last_error().decode())
+    _loaded_model = path
+
+
+def _p(a):
+    return a.ctypes.data if a is not None else None
+
+
+def geometry(bw, bh):
+    v = [ctypes.c_int32() for _ in range(4)]
+    if lib().oracle_face_geometry(bw, bh, *[ctypes.byref(x) for x in v]) != 0:
+        raise RuntimeError(lib().oracle_last_error().decode())
+    return tuple(x.value for x in v)  # face_w, face_h, n_hp_patches, n_mp_patches
+
+
+def analyze_face(img, bbox, threads=1, trace=False):
+    """img: HxWx3 uint8 BGR; bbox (x, y, w, h). Returns (face dict, trace dict|None)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape[:2]
+    x, y, bw, bh = [int(v) for v in bbox]
+    out = OracleFace()
+    tr = None
+    bufs = None
+    if trace:
+        fw, fh, nhp, nmp = geometry(bw, bh)
+        bufs = dict(
+            face=np.zeros((fh, fw), np.uint8),
+            channels=np.zeros((38, fh + 1, fw + 1), np.uint32),
+            hp_leaves=np.zeros((nhp, 15), np.int32),
+            mp_leaves=np.zeros(nmp * MAX_TREES, np.int32),
+            trees=np.full(MAX_TREES, -1, np.int32),
+            pose_freq=np.zeros(5, np.float32),
+            vote_counts=np.zeros(10, np.int32),
+            ms_mean=np.zeros((10, 2), np.float32),
+        )
+        tr = OracleTrace(*[_p(bufs[k]) for k, _ in OracleTrace._fields_])
+    rc = lib().oracle_analyze_face(img.ctypes.data, w, h, img.strides[0], x, y, bw, bh, threads,
+                                   ctypes.byref(out), ctypes.byref(tr) if tr is not None else None)
+    if rc != 0:
+        raise RuntimeError("oracle_analyze_face: " + lib().oracle_last_error().decode())
+    face = dict(headpose=out.headpose, pose_variance=out.pose_variance, face_w=out.face_w,
+                face_h=out.face_h, n_trees=out.n_trees,
+                points=np.array([[out.points[i][0], out.points[i][1]] for i in range(10)], np.int32))
+    if bufs is not None:
+        nt = out.n_trees
+        bufs["mp_leaves"] = bufs["mp_leaves"][: bufs["mp_leaves"].size // MAX_TREES * nt].reshape(-1, nt)
+        bufs["trees"] = bufs["trees"][:nt]
+    return face, bufs
+
+
+def bgr2gray(img):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape[:2]
+    out = np.zeros((h, w), np.uint8)
+    lib().oracle_bgr2gray(img.ctypes.data, w, h, img.strides[0], out.ctypes.data)
+    return out
+
+
+def resize(src, dw, dh):
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.zeros((dh, dw), np.uint8)
+    lib().oracle_resize(src.ctypes.data, src.shape[1], src.shape[0], src.strides[0], dw, dh, out.ctypes.data)
+    return out
+
+
+def channels(face):
+    face = np.ascontiguousarray(face, np.uint8)
+    h, w = face.shape
+    out = np.zeros((38, h + 1, w + 1), np.uint32)
+    if lib().oracle_channels(face.ctypes.data, w, h, out.ctypes.data) != 0:
+        raise RuntimeError(lib().oracle_last_error().decode())
+    return out
+
+
+def gabor_kernel(index):
+    w = ctypes.c_int32()
+    re = np.zeros(25 * 25, np.float32)
+    im = np.zeros(25 * 25, np.float32)
+    if lib().oracle_gabor_kernel(index, re.ctypes.data, im.ctypes.data, ctypes.byref(w)) != 0:
+        raise RuntimeError(lib().oracle_last_error().decode())
+    n = w.value
+    return re[: n * n].reshape(n, n), im[: n * n].reshape(n, n)
+
+
+def gabor_mag(face, index):
+    face = np.ascontiguousarray(face, np.uint8)
+    h, w = face.shape
+    out = np.zeros((h, w), np.float32)
+    lib().oracle_gabor_mag(face.ctypes.data, w, h, index, out.ctypes.data)
+    return out
+
+
+def area_under_curve(x1, x2, mean, std):
+    return lib().oracle_area_under_curve(x1, x2, mean, std)
+
+
+def exp(x):
+    return lib().oracle_exp(x)

@@ -1,0 +1,705 @@
+// ffd_oracle.cpp — CPU restatement of the reference hot path. TEST INFRASTRUCTURE.
+//
+// This file is the parity oracle for the HIP engine: a plain C++17 (no OpenCV,
+// no Boost) restatement of FaceForest::analyzeFace and everything below it, in
+// reference order, with the numeric semantics of SURVEY.md Appendix B.  Only
+// tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+//
+// Parity status:
+//   * PINNED  — model loader: node/leaf counts and threshold sums of every tree
+//               equal the known-answer values computed from the reference's own
+//               archives (tests/test_model.py).
+//   * SANITY  — end-to-end accuracy on the 20 annotated faces the reference
+//               ships (data/imgs/index_random_subset.txt) is checked against
+//               the band of the reference's published errors (output/errors.txt).
+//   * UNPINNED — every value at the OpenCV 2.4.9 boundary (cvtColor, resize,
+//               filter2D, normalize, convertTo, Sobel, cvRound): OpenCV is not
+//               in this image and the reference ships no intermediate values,
+//               so these follow OpenCV 2.4.9's documented/x86-SSE2 behaviour as
+//               restated here ("parity unpinned" for channel values and exact
+//               landmark positions).
+//
+// Reference files followed (paths relative to /root/reference):
+//   src/FaceForest.cpp:183-258           analyzeFace
+//   src/face_utils.cpp:183-323           getHeadPoseVotesMT, getFacialFeaturesVotesMT, areaUnderCurve
+//   include/MeanShift.hpp:16-135         MeanShift
+//   src/ImageSample.cpp:11-90            ImageSample, evalTest (integral branch)
+//   include/FeatureChannelFactory.hpp:35-286  channels, Gabor kernels
+//   include/Forest.hpp:80-90, Tree.hpp:173-191, TreeNode.hpp:54-66,129-136  traversal
+//   src/MPSample.cpp:77-84, src/HeadPoseSample.cpp:39-46  eval: test <= threshold -> left
+//   include/FaceForest.hpp:34-58, include/Constants.hpp:24-30,65-68  options/constants
+//   include/ThreadPool.hpp:24-64         per-call pools (CPU-baseline shape)
+#include "ffd_oracle.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../include/ffd_model_format.h"
+#include "../include/ffd_numerics.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+// ------------------------------------------------------------------ model ----
+struct Node {           // TreeNode<S> (TreeNode.hpp:138-146), pointer-free
+  int32_t left = -1, right = -1, leaf = -1;
+  int16_t ch = 0, r1[4] = {0, 0, 0, 0}, r2[4] = {0, 0, 0, 0};
+  int32_t thr = 0;
+};
+
+struct Forest {
+  std::vector<int32_t> roots;  // global node index of each tree's root
+  std::vector<Node> nodes;
+  int ntrees_per_forest = 0, n_forests = 0, face_size = 125;
+  float patch_ratio = 0.25f;
+  // HP leaf payload
+  std::vector<int32_t> hp_n, hp_labels;
+  std::vector<float> hp_fg;
+  // MP leaf payload
+  std::vector<int32_t> mp_n;
+  std::vector<float> mp_fg, mp_var, mp_pf;
+  std::vector<int16_t> mp_off;
+};
+
+Forest g_hp, g_mp;
+bool g_loaded = false;
+std::mutex g_mu;
+
+struct Arr {
+  std::string dtype;
+  std::vector<uint64_t> shape;
+  std::vector<uint8_t> data;
+  template <class T> const T* p() const { return (const T*)data.data(); }
+  uint64_t n() const { uint64_t v = 1; for (auto s : shape) v *= s; return v; }
+};
+
+std::map<std::string, Arr> read_container(const char* path) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) throw std::runtime_error(std::string("cannot open ") + path);
+  char magic[8];
+  uint32_t ver, n;
+  if (std::fread(magic, 1, 8, f) != 8 || std::memcmp(magic, FFD_MODEL_MAGIC, 8) ||
+      std::fread(&ver, 4, 1, f) != 1 || std::fread(&n, 4, 1, f) != 1 || ver != FFD_MODEL_VERSION) {
+    std::fclose(f);
+    throw std::runtime_error("bad model header");
+  }
+  std::vector<ffd_array_entry> e(n);
+  if (std::fread(e.data(), sizeof(ffd_array_entry), n, f) != n) { std::fclose(f); throw std::runtime_error("bad model table"); }
+  std::map<std::string, Arr> out;
+  for (auto& x : e) {
+    Arr a;
+    a.dtype = x.dtype;
+    for (uint32_t i = 0; i < x.ndim; i++) a.shape.push_back(x.shape[i]);
+    a.data.resize(x.nbytes);
+    std::fseek(f, (long)x.offset, SEEK_SET);
+    if (x.nbytes && std::fread(a.data.data(), 1, x.nbytes, f) != x.nbytes) { std::fclose(f); throw std::runtime_error("truncated model"); }
+    out[std::string(x.name)] = std::move(a);
+  }
+  std::fclose(f);
+  return out;
+}
+
+// Rebuild pointer structure from pre-order records (TreeNode::serialize order:
+// node, then full left subtree, then right subtree; TreeNode.hpp:150-164).
+void build_forest(const std::map<std::string, Arr>& m, const std::string& p, Forest& F, bool hp) {
+  auto get = [&](const std::string& k) -> const Arr& {
+    auto it = m.find(p + "." + k);
+    if (it == m.end()) throw std::runtime_error("missing array " + p + "." + k);
+    return it->second;
+  };
+  const Arr& prm = get("param");
+  F.ntrees_per_forest = prm.p<int32_t>()[3];
+  F.face_size = prm.p<int32_t>()[6];
+  F.n_forests = prm.p<int32_t>()[7];
+  F.patch_ratio = get("patch_ratio").p<float>()[0];
+  const Arr& off = get("tree_node_off");
+  const Arr& nl = get("node_leaf");
+  const Arr& ns = get("node_split");
+  uint64_t T = off.n() - 1, N = nl.n();
+  F.nodes.assign(N, Node());
+  F.roots.clear();
+  for (uint64_t t = 0; t < T; t++) {
+    int64_t b = off.p<int64_t>()[t], e = off.p<int64_t>()[t + 1];
+    F.roots.push_back((int32_t)b);
+    std::vector<int64_t> stack;  // nodes awaiting children
+    for (int64_t i = b; i < e; i++) {
+      Node& nd = F.nodes[i];
+      const int16_t* s = ns.p<int16_t>() + i * FFD_SPLIT_FIELDS;
+      nd.leaf = nl.p<int32_t>()[i];
+      nd.ch = s[0];
+      for (int k = 0; k < 4; k++) { nd.r1[k] = s[1 + k]; nd.r2[k] = s[5 + k]; }
+      nd.thr = s[9];
+      if (i > b) {  // attach to the most recent parent still missing a child
+        if (stack.empty()) throw std::runtime_error("malformed pre-order tree");
+        Node& par = F.nodes[stack.back()];
+        if (par.left < 0) par.left = (int32_t)i;
+        else { par.right = (int32_t)i; stack.pop_back(); }
+      }
+      if (nd.leaf < 0) stack.push_back(i);
+    }
+    if (!stack.empty()) throw std::runtime_error("incomplete tree");
+  }
+  if (hp) {
+    const Arr& n = get("leaf_n"); const Arr& fg = get("leaf_fg"); const Arr& lb = get("leaf_labels");
+    F.hp_n.assign(n.p<int32_t>(), n.p<int32_t>() + n.n());
+    F.hp_fg.assign(fg.p<float>(), fg.p<float>() + fg.n());
+    F.hp_labels.assign(lb.p<int32_t>(), lb.p<int32_t>() + lb.n());
+  } else {
+    const Arr& n = get("leaf_n"); const Arr& fg = get("leaf_fg"); const Arr& o = get("leaf_offset");
+    const Arr& v = get("leaf_var"); const Arr& pf = get("leaf_pf");
+    F.mp_n.assign(n.p<int32_t>(), n.p<int32_t>() + n.n());
+    F.mp_fg.assign(fg.p<float>(), fg.p<float>() + fg.n());
+    F.mp_off.assign(o.p<int16_t>(), o.p<int16_t>() + o.n());
+    F.mp_var.assign(v.p<float>(), v.p<float>() + v.n());
+    F.mp_pf.assign(pf.p<float>(), pf.p<float>() + pf.n());
+  }
+}
+
+// ------------------------------------------------------------ thread pool ----
+// Per-call pool of n threads, one task per unit, joined before returning —
+// the shape of boost::thread_pool::ThreadPool (ThreadPool.hpp:24-64) at its
+// call sites FeatureChannelFactory.hpp:82-86 and face_utils.cpp:210-216,267-274.
+void run_pool(int threads, int ntasks, const std::function<void(int)>& fn) {
+  if (threads <= 1) {
+    for (int i = 0; i < ntasks; i++) fn(i);
+    return;
+  }
+  std::atomic<int> next{0};
+  std::vector<std::thread> pool;
+  pool.reserve(threads);
+  for (int t = 0; t < threads; t++)
+    pool.emplace_back([&] {
+      for (;;) {
+        int i = next.fetch_add(1);
+        if (i >= ntasks) break;
+        fn(i);
+      }
+    });
+  for (auto& th : pool) th.join();
+}
+
+// ---------------------------------------------------------- OpenCV 2.4.9 ----
+inline int cv_round(float v) {  // cvRound: SSE2 cvtss2si, round-half-even; NaN/overflow -> INT_MIN
+  if (!(v >= -2147483648.0f && v < 2147483648.0f)) return INT_MIN;
+  return (int)std::nearbyint(v);
+}
+inline int cv_round_d(double v) {
+  if (!(v >= -2147483648.0 && v < 2147483648.0)) return INT_MIN;
+  return (int)std::nearbyint(v);
+}
+inline uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+inline int16_t sat_s16(int v) { return (int16_t)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v)); }
+inline int cv_floor(double v) { return (int)std::floor(v); }
+inline int reflect101(int i, int n) {  // BORDER_REFLECT_101 for n >= 2
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) {
+    if (i < 0) i = -i;
+    if (i >= n) i = 2 * n - 2 - i;
+  }
+  return i;
+}
+
+// cvtColor(BGR2GRAY) 8U: fixed point, yuv_shift 14 (B 1868, G 9617, R 4899).
+inline uint8_t gray_px(const uint8_t* p) {
+  return (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14);
+}
+
+// resize(INTER_LINEAR) 8U, OpenCV 2.4.9 resizeGeneric_ with HResizeLinear<uchar,int,short,2048>
+// and VResizeLinear<uchar,int,short,FixedPtCast<int,uchar,22>, VResizeLinearVec_32s8u> (SSE2).
+// Exact 2x down-scales take the INTER_AREA fast path; equal sizes copy.
+void cv_resize(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dw, int dh) {
+  if (sw == dw && sh == dh) {
+    for (int y = 0; y < dh; y++) std::memcpy(dst + y * dw, src + y * sstride, dw);
+    return;
+  }
+  double inv_scale_x = (double)dw / sw, inv_scale_y = (double)dh / sh;
+  double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+  int iscale_x = (int)cv_round_d(scale_x), iscale_y = (int)cv_round_d(scale_y);
+  bool is_area_fast = std::fabs(scale_x - iscale_x) < DBL_EPSILON && std::fabs(scale_y - iscale_y) < DBL_EPSILON;
+  if (is_area_fast && iscale_x == 2 && iscale_y == 2) {
+    // resizeAreaFast_ 2x2: (a+b+c+d+2)>>2
+    for (int y = 0; y < dh; y++)
+      for (int x = 0; x < dw; x++) {
+        const uint8_t* s0 = src + (2 * y) * sstride + 2 * x;
+        const uint8_t* s1 = s0 + sstride;
+        dst[y * dw + x] = (uint8_t)((s0[0] + s0[1] + s1[0] + s1[1] + 2) >> 2);
+      }
+    return;
+  }
+  const int ONE = 2048;
+  std::vector<int> xofs(dw), yofs(dh);
+  std::vector<int16_t> ialpha(dw * 2), ibeta(dh * 2);
+  int xmax = dw;
+  for (int dx = 0; dx < dw; dx++) {
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = cv_floor(fx);
+    fx -= sx;
+    if (sx < 0) fx = 0, sx = 0;
+    if (sx + 1 >= sw) {
+      xmax = std::min(xmax, dx);
+      if (sx >= sw - 1) fx = 0, sx = sw - 1;
+    }
+    xofs[dx] = sx;
+    ialpha[dx * 2] = sat_s16(cv_round((1.f - fx) * ONE));
+    ialpha[dx * 2 + 1] = sat_s16(cv_round(fx * ONE));
+  }
+  for (int dy = 0; dy < dh; dy++) {  // rows are NOT clamped here; resizeGeneric_ clips row indices
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    int sy = cv_floor(fy);
+    fy -= sy;
+    yofs[dy] = sy;
+    ibeta[dy * 2] = sat_s16(cv_round((1.f - fy) * ONE));
+    ibeta[dy * 2 + 1] = sat_s16(cv_round(fy * ONE));
+  }
+  // columns covered by the SSE2 vertical pass (VResizeLinearVec_32s8u loop bounds)
+  int xv = 0;
+  while (xv <= dw - 16) xv += 16;
+  while (xv < dw - 4) xv += 4;
+  std::vector<int> r0(dw), r1(dw);
+  auto hresize = [&](const uint8_t* S, int* D) {
+    int dx = 0;
+    for (; dx < xmax; dx++) D[dx] = S[xofs[dx]] * ialpha[dx * 2] + S[xofs[dx] + 1] * ialpha[dx * 2 + 1];
+    for (; dx < dw; dx++) D[dx] = S[xofs[dx]] * ONE;
+  };
+  for (int dy = 0; dy < dh; dy++) {
+    // clip(sy0 - ksize2 + 1 + k, 0, sh) for k = 0, 1
+    int sy0 = std::max(0, std::min(yofs[dy], sh - 1));
+    int sy1 = std::max(0, std::min(yofs[dy] + 1, sh - 1));
+    hresize(src + sy0 * sstride, r0.data());
+    hresize(src + sy1 * sstride, r1.data());
+    int b0 = ibeta[dy * 2], b1 = ibeta[dy * 2 + 1];
+    uint8_t* D = dst + dy * dw;
+    for (int x = 0; x < dw; x++) {
+      if (x < xv) {
+        // _mm_packs_epi32(srai(S,4)) -> _mm_mulhi_epi16 -> _mm_adds_epi16 -> +2 >> 2 -> packus
+        int s0 = std::max(-32768, std::min(32767, r0[x] >> 4));
+        int s1 = std::max(-32768, std::min(32767, r1[x] >> 4));
+        int m0 = (s0 * b0) >> 16, m1 = (s1 * b1) >> 16;
+        int a = std::max(-32768, std::min(32767, m0 + m1));
+        a = std::max(-32768, std::min(32767, a + 2)) >> 2;
+        D[x] = sat_u8(a);
+      } else {
+        D[x] = sat_u8((b0 * r0[x] + b1 * r1[x] + (1 << 21)) >> 22);
+      }
+    }
+  }
+}
+
+// cv::integral(img, sum, CV_32F): exact integer sums (< 2^24), stored as u32.
+void integral(const uint8_t* img, int w, int h, uint32_t* out) {
+  int W1 = w + 1;
+  for (int x = 0; x <= w; x++) out[x] = 0;
+  for (int y = 0; y < h; y++) {
+    uint32_t s = 0;
+    out[(y + 1) * W1] = 0;
+    for (int x = 0; x < w; x++) {
+      s += img[y * w + x];
+      out[(y + 1) * W1 + x + 1] = out[y * W1 + x + 1] + s;
+    }
+  }
+}
+
+// ------------------------------------------------------------ Gabor bank ----
+struct GaborKernel { int width; std::vector<float> re, im; };  // [row j = y+off][col i = x+off]
+std::vector<GaborKernel> g_gabor;
+
+// FeatureChannelFactory::createKernel / initGaborKernels (FeatureChannelFactory.hpp:186-251)
+void init_gabor() {
+  if (!g_gabor.empty()) return;
+  const double CV_PI = 3.1415926535897932384626433832795;
+  double sigma = 1.0 / 2.0 * CV_PI;
+  double dF = std::sqrt(2.0);
+  for (int iNu = 0; iNu <= 4; iNu++)
+    for (int iMu = 0; iMu < 7; iMu++) {
+      double F = dF;
+      double k = (CV_PI / 2) / std::pow(F, (double)iNu);
+      double phi = CV_PI * iMu / 8;
+      double width = std::round((sigma / k) * 6 + 1);
+      if (std::fmod(width, 2.0) == 0.0) width++;
+      GaborKernel g;
+      g.width = (int)width;
+      g.re.assign(g.width * g.width, 0.f);
+      g.im.assign(g.width * g.width, 0.f);
+      int off_set = (int)((width - 1) / 2);
+      for (int i = 0; i < g.width; i++)
+        for (int j = 0; j < g.width; j++) {
+          int x = i - off_set, y = j - off_set;
+          double dTemp1 = (std::pow(k, 2) / std::pow(sigma, 2)) *
+                          std::exp(-(std::pow((double)x, 2) + std::pow((double)y, 2)) * std::pow(k, 2) /
+                                   (2 * std::pow(sigma, 2)));
+          double dTemp2 = std::cos(k * std::cos(phi) * x + k * std::sin(phi) * y) - std::exp(-(std::pow(sigma, 2) / 2));
+          double dTemp3 = std::sin(k * std::cos(phi) * x + k * std::sin(phi) * y);
+          g.re[j * g.width + i] = (float)(dTemp1 * dTemp2);
+          g.im[j * g.width + i] = (float)(dTemp1 * dTemp3);
+        }
+      // point symmetry required by the folded correlation below
+      int n = g.width * g.width;
+      for (int t = 0; t < n; t++)
+        if (g.re[t] != g.re[n - 1 - t] || g.im[t] != -g.im[n - 1 - t])
+          throw std::runtime_error("Gabor kernel not point-symmetric");
+      g_gabor.push_back(std::move(g));
+    }
+}
+
+// One Gabor magnitude plane (gaborTransform, FeatureChannelFactory.hpp:253-286).
+//  * 7x7 kernels (49 taps < OpenCV's dft_filter_size 50): OpenCV's direct
+//    Filter2D, row-major taps, s = 0; s += k*p (no FMA) — bit-exact restatement.
+//  * >= 9x9 kernels: OpenCV 2.4.9 switches to a DFT (crossCorr) whose rounding
+//    cannot be reproduced; the restatement DEFINES the correlation as the
+//    point-symmetric folded sum: for the first (W*W-1)/2 taps t in row-major
+//    order, S = p(+t)+p(-t), D = p(+t)-p(-t) (exact), re = fma(kre_t, S, re),
+//    im = fma(kim_t, D, im); then re = fma(kre_centre, p(0), re).
+void gabor_mag(const uint8_t* img, int w, int h, int index, float* mag) {
+  const GaborKernel& g = g_gabor[index];
+  int W = g.width, R = (W - 1) / 2, n = W * W, half = (n - 1) / 2;
+  std::vector<int> rx(w + 2 * R), ry(h + 2 * R);
+  for (int i = 0; i < w + 2 * R; i++) rx[i] = reflect101(i - R, w);
+  for (int i = 0; i < h + 2 * R; i++) ry[i] = reflect101(i - R, h);
+  auto P = [&](int y, int x) -> float { return (float)img[ry[y + R] * w + rx[x + R]]; };
+  for (int py = 0; py < h; py++)
+    for (int px = 0; px < w; px++) {
+      float re = 0.f, im = 0.f;
+      if (W == 7) {
+        for (int r = 0; r < W; r++)
+          for (int c = 0; c < W; c++) {
+            float p = P(py + r - R, px + c - R);
+            re = re + g.re[r * W + c] * p;
+            im = im + g.im[r * W + c] * p;
+          }
+      } else {
+        for (int t = 0; t < half; t++) {
+          int dy = t / W - R, dx = t % W - R;
+          float a = P(py + dy, px + dx), b = P(py - dy, px - dx);
+          re = std::fmaf(g.re[t], a + b, re);
+          im = std::fmaf(g.im[t], a - b, im);
+        }
+        re = std::fmaf(g.re[half], P(py, px), re);
+      }
+      // pow(r,2), pow(i,2), add(i,r), pow(.,0.5) == sqrt
+      float r2 = re * re, i2 = im * im;
+      mag[py * w + px] = std::sqrt(i2 + r2);
+    }
+}
+
+// normalize(NORM_MINMAX, 0, 1) then convertTo(CV_8U, 255) (FeatureChannelFactory.hpp:271-276).
+void quantize(const float* mag, int n, uint8_t* out) {
+  float mn = mag[0], mx = mag[0];
+  for (int i = 1; i < n; i++) { mn = std::min(mn, mag[i]); mx = std::max(mx, mag[i]); }
+  double smin = mn, smax = mx, dmin = 0, dmax = 1;
+  double scale = (dmax - dmin) * (smax - smin > DBL_EPSILON ? 1. / (smax - smin) : 0);
+  double shift = dmin - smin * scale;
+  float sf = (float)scale, hf = (float)shift;
+  for (int i = 0; i < n; i++) {
+    float v = mag[i] * sf + hf;
+    out[i] = sat_u8(cv_round(v * 255.f + 0.f));
+  }
+}
+
+// Sobel 3x3, CV_8U output (saturated), BORDER_REFLECT_101. dy -> channel 36, dx -> 37.
+void sobel(const uint8_t* img, int w, int h, bool dy, uint8_t* out) {
+  auto I = [&](int y, int x) { return (int)img[reflect101(y, h) * w + reflect101(x, w)]; };
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      int v;
+      if (dy)
+        v = (I(y + 1, x - 1) + 2 * I(y + 1, x) + I(y + 1, x + 1)) - (I(y - 1, x - 1) + 2 * I(y - 1, x) + I(y - 1, x + 1));
+      else
+        v = (I(y - 1, x + 1) + 2 * I(y, x + 1) + I(y + 1, x + 1)) - (I(y - 1, x - 1) + 2 * I(y, x - 1) + I(y + 1, x - 1));
+      out[y * w + x] = sat_u8(v);
+    }
+}
+
+constexpr int NCH = 38;
+
+// ImageSample(img, {0,1,2}, true) -> 38 integral channels (ImageSample.cpp:77-90).
+void extract_channels(const uint8_t* face, int w, int h, uint32_t* ch, int threads) {
+  size_t plane = (size_t)(w + 1) * (h + 1);
+  integral(face, w, h, ch);  // FC_GRAY
+  init_gabor();
+  run_pool(threads, 35, [&](int i) {  // FC_GABOR: 35 tasks
+    std::vector<float> mag((size_t)w * h);
+    std::vector<uint8_t> q((size_t)w * h);
+    gabor_mag(face, w, h, i, mag.data());
+    quantize(mag.data(), w * h, q.data());
+    integral(q.data(), w, h, ch + plane * (1 + i));
+  });
+  std::vector<uint8_t> s((size_t)w * h);  // FC_SOBEL
+  sobel(face, w, h, true, s.data());
+  integral(s.data(), w, h, ch + plane * 36);
+  sobel(face, w, h, false, s.data());
+  integral(s.data(), w, h, ch + plane * 37);
+}
+
+// ImageSample::evalTest integral branch (ImageSample.cpp:48-63).
+inline int eval_test(const uint32_t* ch, int w, int h, const Node& nd, int px, int py) {
+  int W1 = w + 1;
+  const uint32_t* I = ch + (size_t)nd.ch * (W1) * (h + 1);
+  auto at = [&](int y, int x) { return (int)(float)I[y * W1 + x]; };
+  int x1 = px + nd.r1[0], y1 = py + nd.r1[1], w1 = nd.r1[2], h1 = nd.r1[3];
+  int x2 = px + nd.r2[0], y2 = py + nd.r2[1], w2 = nd.r2[2], h2 = nd.r2[3];
+  int a = at(y1, x1), b = at(y1, x1 + w1), c = at(y1 + h1, x1), d = at(y1 + h1, x1 + w1);
+  int p1 = (int)((float)(d - b - c + a) / (float)(w1 * h1));
+  a = at(y2, x2); b = at(y2, x2 + w2); c = at(y2 + h2, x2); d = at(y2 + h2, x2 + w2);
+  int p2 = (int)((float)(d - b - c + a) / (float)(w2 * h2));
+  return p1 - p2;
+}
+
+// Tree<S>::evaluateMT (Tree.hpp:173-191): eval true (test <= threshold) -> left.
+int walk(const Forest& F, int root, const uint32_t* ch, int w, int h, int px, int py) {
+  int i = root;
+  while (F.nodes[i].leaf < 0) {
+    const Node& nd = F.nodes[i];
+    i = (eval_test(ch, w, h, nd, px, py) <= nd.thr) ? nd.left : nd.right;
+  }
+  return F.nodes[i].leaf;
+}
+
+// areaUnderCurve (face_utils.cpp:304-323) with exp := ffd_exp (ffd_numerics.h).
+double area_under_curve(float x1, float x2, double mean, double std_) {
+  double sum = 0, step = 0.01, t;
+  for (double x = x1; x < x2; x += step) {
+    t = (x - mean) / std_;
+    sum += ffd_exp(-0.5 * (t * t)) * step;
+  }
+  const double sqrt_2pi = 2.5066282746310002;  // sqrt(2 * M_PI), constant-folded
+  return sum * 1.0 / (std_ * sqrt_2pi);
+}
+
+inline int to_int_trunc(float v) {  // static_cast<int>(float) on x86-64 (cvttss2si)
+  if (!(v > -2147483649.0f && v < 2147483648.0f)) return INT_MIN;
+  return (int)v;
+}
+
+struct Geometry { int W, H, patch, nhx, nhy, nmx, nmy; float scale; };
+
+bool geometry(int bw, int bh, Geometry& g) {
+  if (bw <= 0 || bh <= 0) return false;
+  // FaceForest.cpp:202-204: scale = 125.f/cols; Size(cols*scale, rows*scale) truncates
+  g.scale = (float)g_hp.face_size / (float)bw;
+  g.W = (int)((float)bw * g.scale);
+  g.H = (int)((float)bh * g.scale);
+  g.patch = (int)std::round(g_hp.face_size * g_hp.patch_ratio);  // getPatchSize (Constants.hpp:27-30)
+  auto cnt = [](int extent, int patch, int step) { int n = 0; for (int x = 0; x < extent - patch; x += step) n++; return n; };
+  g.nhx = cnt(g.W, g.patch, 4); g.nhy = cnt(g.H, g.patch, 4);   // HeadPoseEstimatorOption step 4
+  g.nmx = cnt(g.W, g.patch, 3); g.nmy = cnt(g.H, g.patch, 3);   // MultiPartEstimatorOption step 3
+  return g.W > 0 && g.H > 0;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------- C API --
+extern "C" {
+
+const char* oracle_last_error(void) { return g_err.c_str(); }
+
+int oracle_load_model(const char* path) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  try {
+    auto m = read_container(path);
+    build_forest(m, "hp", g_hp, true);
+    build_forest(m, "mp", g_mp, false);
+    init_gabor();
+    g_loaded = true;
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+int oracle_face_geometry(int32_t bw, int32_t bh, int32_t* fw, int32_t* fh, int32_t* nhp, int32_t* nmp) {
+  if (!g_loaded) { g_err = "model not loaded"; return -1; }
+  Geometry g;
+  if (!geometry(bw, bh, g)) { g_err = "degenerate box"; return -1; }
+  *fw = g.W; *fh = g.H; *nhp = g.nhx * g.nhy; *nmp = g.nmx * g.nmy;
+  return 0;
+}
+
+int oracle_bgr2gray(const uint8_t* bgr, int32_t w, int32_t h, int32_t stride, uint8_t* gray) {
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) gray[y * w + x] = gray_px(bgr + y * stride + 3 * x);
+  return 0;
+}
+
+int oracle_resize(const uint8_t* src, int32_t sw, int32_t sh, int32_t sstride, int32_t dw, int32_t dh, uint8_t* dst) {
+  cv_resize(src, sw, sh, sstride, dst, dw, dh);
+  return 0;
+}
+
+int oracle_channels(const uint8_t* face, int32_t w, int32_t h, uint32_t* channels) {
+  try { extract_channels(face, w, h, channels, 1); return 0; }
+  catch (const std::exception& e) { g_err = e.what(); return -1; }
+}
+
+int oracle_gabor_kernel(int32_t index, float* re, float* im, int32_t* width) {
+  try { init_gabor(); } catch (const std::exception& e) { g_err = e.what(); return -1; }
+  if (index < 0 || index >= (int)g_gabor.size()) return -1;
+  const auto& g = g_gabor[index];
+  *width = g.width;
+  if (re) std::memcpy(re, g.re.data(), g.re.size() * 4);
+  if (im) std::memcpy(im, g.im.data(), g.im.size() * 4);
+  return 0;
+}
+
+int oracle_gabor_mag(const uint8_t* face, int32_t w, int32_t h, int32_t index, float* mag) {
+  try { init_gabor(); } catch (const std::exception& e) { g_err = e.what(); return -1; }
+  gabor_mag(face, w, h, index, mag);
+  return 0;
+}
+
+double oracle_area_under_curve(float x1, float x2, double mean, double std_) {
+  return area_under_curve(x1, x2, mean, std_);
+}
+
+double oracle_exp(double x) { return ffd_exp(x); }
+
+int oracle_analyze_face(const uint8_t* bgr, int32_t iw, int32_t ih, int32_t stride, int32_t bx, int32_t by,
+                        int32_t bw, int32_t bh, int32_t threads, oracle_face* out, oracle_trace* tr) {
+  if (!g_loaded) { g_err = "model not loaded"; return -1; }
+  if (bx < 0 || by < 0 || bw <= 0 || bh <= 0 || bx + bw > iw || by + bh > ih) {
+    g_err = "bbox outside image";  // cv::Mat ROI assertion in the reference
+    return -2;
+  }
+  Geometry g;
+  if (!geometry(bw, bh, g)) { g_err = "degenerate box"; return -2; }
+  const int W = g.W, H = g.H, P = g.patch;
+  std::memset(out, 0, sizeof(*out));
+  out->face_w = W; out->face_h = H;
+
+  // a2: gray of the ROI (cvtColor is per-pixel, so ROI-only is identical) + resize
+  std::vector<uint8_t> roi((size_t)bw * bh), face((size_t)W * H);
+  for (int y = 0; y < bh; y++)
+    for (int x = 0; x < bw; x++) roi[y * bw + x] = gray_px(bgr + (size_t)(by + y) * stride + 3 * (bx + x));
+  cv_resize(roi.data(), bw, bh, bw, face.data(), W, H);
+  if (tr && tr->face) std::memcpy(tr->face, face.data(), face.size());
+
+  // a3-a6: channels
+  size_t plane = (size_t)(W + 1) * (H + 1);
+  std::vector<uint32_t> ch(plane * NCH);
+  try { extract_channels(face.data(), W, H, ch.data(), threads); }
+  catch (const std::exception& e) { g_err = e.what(); return -1; }
+  if (tr && tr->channels) std::memcpy(tr->channels, ch.data(), ch.size() * 4);
+
+  // a13: getHeadPoseVotesMT (face_utils.cpp:183-242), grid x outer / y inner, step 4
+  const int HT = (int)g_hp.roots.size();
+  std::vector<std::pair<int, int>> hp_patches;
+  for (int x = 0; x < W - P; x += 4)
+    for (int y = 0; y < H - P; y += 4) hp_patches.push_back({x, y});
+  std::vector<int> hp_leafs(hp_patches.size() * HT);
+  run_pool(threads, (int)hp_patches.size(), [&](int i) {
+    for (int t = 0; t < HT; t++)
+      hp_leafs[i * HT + t] = walk(g_hp, g_hp.roots[t], ch.data(), W, H, hp_patches[i].first, hp_patches[i].second);
+  });
+  if (tr && tr->hp_leaves) std::memcpy(tr->hp_leaves, hp_leafs.data(), hp_leafs.size() * 4);
+  float n = 0, sum = 0, sum_sq = 0;
+  for (size_t i = 0; i < hp_leafs.size(); ++i) {
+    int L = hp_leafs[i];
+    if (g_hp.hp_fg[L] > 0.5f) {  // HeadPoseEstimatorOption::min_foreground_probability
+      float m = 0;
+      for (int j = 0; j < FFD_NUM_HP_LABELS; j++) m += g_hp.hp_labels[L * 5 + j] * j;
+      m /= (g_hp.hp_n[L] * g_hp.hp_fg[L]);
+      sum += m;
+      sum_sq += m * m;
+      n++;
+    }
+  }
+  float mean = sum / n;
+  float var = (sum_sq / n) - (mean * mean);
+  mean -= 2;
+  var *= 0.05f;  // NORM_HEADPOSE_VARIANCE_FACTOR (Constants.hpp:67)
+  out->headpose = mean;
+  out->pose_variance = var;
+
+  // a15: pose histogram + tree selection (FaceForest.cpp:214-250)
+  const int NF = g_mp.n_forests, NT = g_mp.ntrees_per_forest;
+  std::vector<float> poseT = {-2.5f, -0.35f, -0.20f, 0.20f, 0.35f, 2.5f};
+  std::vector<float> pose_freq(NF);
+  float max_area = 0;
+  int dominant = 0;
+  for (int j = 0; j < NF; j++) {
+    float area = (float)area_under_curve(poseT[j], poseT[j + 1], mean, std::sqrt((double)var));
+    pose_freq[j] = area;
+    if (max_area < area) { max_area = area; dominant = j; }
+  }
+  if (tr && tr->pose_freq) std::memcpy(tr->pose_freq, pose_freq.data(), NF * 4);
+  std::vector<int> trees;
+  for (int i = 0; i < NF; i++) {
+    int nt = to_int_trunc(std::floor(pose_freq[i] * NT));
+    nt = std::min(nt, NT);  // getTree(j >= NT) is out of range in the reference
+    for (int j = 0; j < nt && (int)trees.size() < ORACLE_MAX_TREES; j++) trees.push_back(i * NT + j);
+  }
+  for (int i = (int)trees.size(); i < NT; i++) trees.push_back(dominant * NT + i);
+  out->n_trees = (int)trees.size();
+  if (tr && tr->trees) std::memcpy(tr->trees, trees.data(), trees.size() * 4);
+
+  // a16: getFacialFeaturesVotesMT (face_utils.cpp:244-302), step 3
+  const int MT = (int)trees.size();
+  std::vector<std::pair<int, int>> mp_patches;
+  for (int x = 0; x < W - P; x += 3)
+    for (int y = 0; y < H - P; y += 3) mp_patches.push_back({x, y});
+  std::vector<int> mp_leafs(mp_patches.size() * MT);
+  run_pool(threads, (int)mp_patches.size(), [&](int i) {
+    for (int t = 0; t < MT; t++)
+      mp_leafs[i * MT + t] = walk(g_mp, g_mp.roots[trees[t]], ch.data(), W, H, mp_patches[i].first, mp_patches[i].second);
+  });
+  if (tr && tr->mp_leaves) std::memcpy(tr->mp_leaves, mp_leafs.data(), mp_leafs.size() * 4);
+  struct Vote { int x, y; float w; };
+  std::vector<std::vector<Vote>> votes(FFD_NUM_PARTS);
+  for (size_t k = 0; k < mp_leafs.size(); k++) {
+    int L = mp_leafs[k];
+    int ox = mp_patches[k / MT].first + P / 2, oy = mp_patches[k / MT].second + P / 2;
+    for (int i = 0; i < FFD_NUM_PARTS; i++) {
+      float min_pf = 0.25f;             // MultiPartEstimatorOption::min_pf
+      if (i == 0 || i == 7) min_pf *= 1.5;
+      if (g_mp.mp_fg[L] > 0.5f && g_mp.mp_pf[L * 10 + i] > min_pf && g_mp.mp_var[L * 10 + i] < 25.f &&
+          g_mp.mp_n[L] > 2)
+        votes[i].push_back({g_mp.mp_off[(L * 10 + i) * 2] + ox, g_mp.mp_off[(L * 10 + i) * 2 + 1] + oy, g_mp.mp_fg[L]});
+    }
+  }
+  // a18: MeanShift::shift per part (MeanShift.hpp:41-135), kernel 10, 7 iterations, 0.05
+  float inv_scale = 1.0f / g.scale;
+  for (int i = 0; i < FFD_NUM_PARTS; i++) {
+    const auto& V = votes[i];
+    if (tr && tr->vote_counts) tr->vote_counts[i] = (int)V.size();
+    float mx = 0, my = 0, sw = 0;
+    for (const auto& v : V) { float w = v.w; mx += v.x * w; my += v.y * w; sw += w; }
+    if (sw > 0) { mx /= sw; my /= sw; }
+    bool conv = false;
+    const float lamda = 10.f, stop = 0.05f;
+    for (int it = 0; it < 7 && !conv; it++) {
+      float sx = 0, sy = 0, s = 0;
+      for (const auto& v : V) {
+        float dx = mx - (float)v.x, dy = my - (float)v.y;
+        float d = (float)std::sqrt((double)dx * dx + (double)dy * dy);
+        d = ffd_expf(-d / lamda);
+        float w = v.w * d;
+        sx += v.x * w; sy += v.y * w; s += w;
+      }
+      if (s > 0) { sx /= s; sy /= s; }
+      float ddx = sx - mx, ddy = sy - my;
+      if (std::sqrt((double)ddx * ddx + (double)ddy * ddy) < stop) conv = true;
+      mx = sx; my = sy;
+    }
+    if (tr && tr->ms_mean) { tr->ms_mean[2 * i] = mx; tr->ms_mean[2 * i + 1] = my; }
+    int px = cv_round(mx), py = cv_round(my);
+    // FaceForest.cpp:255-257: Point_<int> *= 1.0f/scale -> cvRound(x * inv)
+    out->points[i][0] = cv_round((float)px * inv_scale);
+    out->points[i][1] = cv_round((float)py * inv_scale);
+  }
+  return 0;
+}
+
+}  // extern "C"

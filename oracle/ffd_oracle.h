@@ -1,0 +1,75 @@
+/*
+ * ffd_oracle.h — C API of the CPU restatement (TEST INFRASTRUCTURE ONLY).
+ *
+ * The oracle is the checker for the HIP product path.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg load it; the
+ * product library never links or calls it.
+ */
+#ifndef FFD_ORACLE_H
+#define FFD_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORACLE_MAX_TREES 32
+
+typedef struct {
+  float headpose;       /* FaceForest::analyzeFace face.headpose */
+  float pose_variance;  /* variance from getHeadPoseVotesMT */
+  int32_t face_w, face_h;  /* scaled face size */
+  int32_t n_trees;      /* MP trees selected */
+  int32_t points[10][2];   /* bbox-relative landmarks (Face::ffd_cordinates) */
+} oracle_face;
+
+/* Optional per-stage outputs; any pointer may be NULL. Sizes (caller allocates):
+ *   face        face_w*face_h u8
+ *   channels    38*(face_h+1)*(face_w+1) u32
+ *   hp_leaves   n_hp_patches*15 i32 (global HP leaf ordinal, [patch][tree], reference order)
+ *   mp_leaves   n_mp_patches*n_trees i32 (global MP leaf ordinal, [patch][tree])
+ *   trees       ORACLE_MAX_TREES i32 (global MP tree id = forest*20+tree)
+ *   pose_freq   5 f32
+ *   vote_counts 10 i32
+ *   ms_mean     20 f32 (MeanShift result before cvRound, x,y per part)
+ */
+typedef struct {
+  uint8_t* face;
+  uint32_t* channels;
+  int32_t* hp_leaves;
+  int32_t* mp_leaves;
+  int32_t* trees;
+  float* pose_freq;
+  int32_t* vote_counts;
+  float* ms_mean;
+} oracle_trace;
+
+int oracle_load_model(const char* path);
+const char* oracle_last_error(void);
+
+/* analyzeFace (FaceForest.cpp:183-258). threads<=1: serial; >1: reference-shaped
+ * per-stage thread pools of that many threads (ThreadPool.hpp:24-64). */
+int oracle_analyze_face(const uint8_t* bgr, int32_t w, int32_t h, int32_t stride,
+                        int32_t bx, int32_t by, int32_t bw, int32_t bh, int32_t threads,
+                        oracle_face* out, oracle_trace* trace);
+
+/* Geometry of the scaled face for a bbox of bw x bh. */
+int oracle_face_geometry(int32_t bw, int32_t bh, int32_t* face_w, int32_t* face_h,
+                         int32_t* n_hp_patches, int32_t* n_mp_patches);
+
+/* Stage hooks for known-answer tests. */
+int oracle_bgr2gray(const uint8_t* bgr, int32_t w, int32_t h, int32_t stride, uint8_t* gray);
+int oracle_resize(const uint8_t* src, int32_t sw, int32_t sh, int32_t sstride, int32_t dw,
+                  int32_t dh, uint8_t* dst);
+int oracle_channels(const uint8_t* face, int32_t w, int32_t h, uint32_t* channels);
+int oracle_gabor_kernel(int32_t index, float* real, float* imag, int32_t* width);
+int oracle_gabor_mag(const uint8_t* face, int32_t w, int32_t h, int32_t index, float* mag);
+double oracle_area_under_curve(float x1, float x2, double mean, double std_);
+double oracle_exp(double x);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif
