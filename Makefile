@@ -1,0 +1,51 @@
+# Build recipe for the MI355X engine, the offline model converter and the CPU oracle.
+#   make            -> everything below (used by __graft_entry__.build())
+#   make model      -> convert the reference's archives (needs /root/reference)
+HIPCC     ?= /opt/rocm/bin/hipcc
+CXX       ?= g++
+ARCH      ?= gfx950
+PKG       := face_alignment_cvpr_2012_amd
+CSRC      := $(PKG)/csrc
+REFERENCE ?= /root/reference
+
+HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude
+CXXFLAGS  := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall -Iinclude
+
+LIB       := $(PKG)/lib/libffd.so
+CONVERT   := $(PKG)/bin/ffd_convert
+ORACLE    := oracle/build/libffd_oracle.so
+MODEL     := model/ffd_model.bin
+
+HIP_OBJS  := $(PKG)/lib/ffd_kernels.o $(PKG)/lib/ffd_engine.o
+HDRS      := include/ffd.h include/ffd_numerics.h include/ffd_model_format.h $(CSRC)/ffd_device.hpp \
+             $(CSRC)/ffd_kernels.hpp $(CSRC)/model_io.hpp
+
+all: $(LIB) $(CONVERT) $(ORACLE)
+
+$(PKG)/lib/ffd_kernels.o: $(CSRC)/ffd_kernels.hip $(HDRS)
+	@mkdir -p $(@D)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(PKG)/lib/ffd_engine.o: $(CSRC)/ffd_engine.cpp $(HDRS)
+	@mkdir -p $(@D)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(HIP_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS)
+
+$(CONVERT): $(CSRC)/ffd_convert.cpp $(CSRC)/model_io.hpp include/ffd_model_format.h
+	@mkdir -p $(@D)
+	$(CXX) $(CXXFLAGS) -o $@ $<
+
+$(ORACLE): oracle/ffd_oracle.cpp oracle/ffd_oracle.h include/ffd_numerics.h include/ffd_model_format.h
+	@mkdir -p $(@D)
+	$(CXX) $(CXXFLAGS) -shared -pthread -o $@ $<
+
+model: $(CONVERT)
+	@mkdir -p model
+	$(CONVERT) $(REFERENCE) $(MODEL)
+
+clean:
+	rm -rf $(PKG)/lib $(PKG)/bin oracle/build
+
+.PHONY: all model clean

@@ -1,0 +1,220 @@
+"""Benchmark: faces/sec of FaceForest::analyzeFace on the pretrained FFD forest (BASELINE.json).
+
+Workload (config C2, BASELINE.json configs[1]): per GPU, a batch of 4,096 synthetic 150x150 BGR
+face crops (face_alignment_cvpr_2012_amd/synthetic.py, seed 2012 + rank), analyzeFace(crop,
+Rect(0,0,150,150)) each -> 125x125 face, 576 head-pose + 1,024 FFD patches, 15 + 20 trees.
+A step = one full pass of the hot path over the batch: gray/resize, 38 integral channels,
+head-pose forest, tree selection, FFD forest, votes, MeanShift.  Inputs are resident in HBM when
+the timed region starts; outputs stay in HBM (for N > 1 they are gathered to rank 0 with an
+RCCL gather over xGMI inside the step).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3     # MI355X FP32 vector = FP32 matrix peak (no dense MFMA work here)
+CROP = 150
+
+
+def gabor_flops_per_pixel(w):
+    """FLOPs the restated Gabor correlation executes per output pixel for the 7 orientations of
+    one scale: 7x7 direct (mul + add per tap, re and im); >= 9x9 folded
+    pairs (S, D adds + 14 FMAs), centre FMAs; + magnitude (2 mul, add, sqrt) per orientation."""
+    if w == 7:
+        core = 49 * 7 * 2 * 2
+    else:
+        pairs = (w * w - 1) // 2
+        core = pairs * (2 + 7 * 2 * 2) + 7 * 2
+    return core + 7 * 4
+
+
+def stage_work(stage, n_faces, W=125, H=125, n_hp=576, n_mp=1024, trees=20):
+    """Algorithmic work of one launch of `stage` over n_faces: (amount, unit, bound)."""
+    chan_bytes = 38 * (H + 1) * (W + 1) * 4
+    if stage.startswith("gabor_"):
+        w = int(stage.split("_")[1].split("x")[0])
+        return n_faces * W * H * gabor_flops_per_pixel(w) / 1e12, "TFLOP/s", "mfma"
+    if stage == "integral_channels":
+        return n_faces * (35 * W * H * 4 + W * H + chan_bytes) / 1e9, "GB/s", "hbm"
+    if stage == "headpose_traverse":
+        return n_faces * (chan_bytes + n_hp * 15 * 4) / 1e9, "GB/s", "hbm"
+    if stage == "ffd_traverse":
+        return n_faces * (chan_bytes + n_mp * trees * 4) / 1e9, "GB/s", "hbm"
+    if stage == "votes_meanshift":
+        return n_faces * (n_mp * trees * 4 + 112) / 1e9, "GB/s", "hbm"
+    if stage == "gray_resize":
+        return n_faces * (CROP * CROP * 3 + W * H) / 1e9, "GB/s", "hbm"
+    return n_faces * n_hp * 15 * 4 / 1e9, "GB/s", "hbm"
+
+
+def cpu_baseline(n_budget_s=12.0, max_faces=96):
+    """Oracle (C++ restatement) in reference-shaped mode: faces sequential, per-face thread pools
+    of `cores` threads for the 35 Gabor, 576 head-pose and 1,024 FFD tasks (ThreadPool.hpp:24-64)."""
+    import oracle
+    from face_alignment_cvpr_2012_amd.synthetic import make_crops
+    oracle.load_model(os.path.join(REPO, "model", "ffd_model.bin"))
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    cores = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)), 16))
+    crops, _ = make_crops(max_faces, seed=4242)
+    t0 = time.perf_counter()
+    oracle.analyze_face(crops[0], (0, 0, CROP, CROP), threads=cores)
+    one = time.perf_counter() - t0
+    n = int(max(3, min(max_faces - 1, n_budget_s / max(one, 1e-3))))
+    t0 = time.perf_counter()
+    for k in range(1, n + 1):
+        oracle.analyze_face(crops[k], (0, 0, CROP, CROP), threads=cores)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "faces/s", "cores": cores, "kind": "port",
+            "sample": f"{n} C2 150x150 crops (seed 4242), analyzeFace each, reference-shaped per-face "
+                      f"thread pools, {dt:.1f} s"}
+
+
+def parity_spot_check(ff, crops, d_out, k=4):
+    """Decode the first k output records and compare them with the oracle (outside the timed region)."""
+    import torch
+
+    import face_alignment_cvpr_2012_amd as ffd
+    import oracle
+    oracle.load_model(os.path.join(REPO, "model", "ffd_model.bin"))
+    rec = d_out[: k * ffd.FACE_RECORD_BYTES].cpu().numpy().tobytes()
+    faces = ffd.faces_from_records(rec)
+    ok = True
+    for i in range(k):
+        ref, _ = oracle.analyze_face(crops[i], (0, 0, CROP, CROP), threads=8)
+        ok &= bool(np.array_equal(faces[i].ffd_cordinates, ref["points"]))
+        ok &= np.float32(faces[i].headpose) == np.float32(ref["headpose"])
+    del torch
+    return ok
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--faces", type=int, default=4096, help="faces per GPU per step")
+    ap.add_argument("--chunk", type=int, default=0, help="faces per pipeline launch (0 = whole batch)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import face_alignment_cvpr_2012_amd as ffd
+    from face_alignment_cvpr_2012_amd.synthetic import make_crops
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    n = args.faces
+    crops, _ = make_crops(n, seed=2012 + rank)
+    d_crops = torch.from_numpy(crops).to(dev)
+    rec = ffd.FACE_RECORD_BYTES
+    d_out = torch.zeros(n * rec, dtype=torch.uint8, device=dev)
+    gathered = torch.empty(world * n * rec, dtype=torch.uint8, device=dev) if (world > 1 and rank == 0) else None
+    torch.cuda.synchronize()
+
+    chunk = args.chunk if 0 < args.chunk < n else n
+    ff = ffd.FaceForest(ffd.FaceForestOptions(device=local, max_chunk_faces=chunk))
+    boxes = [(0, 0, CROP, CROP)] * n
+    box_img = np.arange(n, dtype=np.int32)
+
+    def step():
+        ff.analyze_device(d_crops.data_ptr(), CROP * CROP * 3, CROP, CROP, CROP * 3, n, boxes, box_img,
+                          d_out.data_ptr())
+        ff.synchronize()
+        if world > 1:  # RCCL gather of the ffd_face records to rank 0
+            if rank == 0:
+                dist.gather(d_out, gather_list=list(gathered.chunk(world)), dst=0)
+            else:
+                dist.gather(d_out, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ok = parity_spot_check(ff, crops, d_out) if rank == 0 else True
+
+    ff.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    stages = ff.stage_times()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        total_faces = world * n * args.steps
+        value = total_faces / elapsed
+        dom = max((k for k in stages if stages[k][1] > 0), key=lambda k: stages[k][0])
+        ms_total, launches = stages[dom]
+        avg_ms = ms_total / launches
+        amount, unit, bound = stage_work(dom, chunk)  # one launch covers one chunk of faces
+        achieved = amount / (avg_ms / 1e3)
+        peak = FP32_PEAK_TFLOPS if unit == "TFLOP/s" else HBM_PEAK_GBS
+        b_face = CROP * CROP * 3 + 2 * 38 * 126 * 126 * 4 + 100
+        out = {
+            "metric": "faces/sec (whole node) on pretrained FFD forest; mean landmark px error",
+            "value": round(value, 1),
+            "unit": "faces/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8/u32/f32",
+            "data": "synthetic: 4096 C2 150x150 crops per GPU from the 20 bundled LFW faces (seed 2012+rank); "
+                    "pretrained reference forests converted to model/ffd_model.bin",
+            "config": {"workload": "C2: batch of 4096 pre-cropped 150x150 faces per GPU, pretrained "
+                                   "config_ffd.txt forest (20 trees/face of 5x20, depth<=20), head-pose forest 15 "
+                                   "trees, 125x125 faces", "faces_per_gpu": n, "parallelism": f"faces sharded x{world}"},
+            "landmark_px_error_vs_cpu": 0.0 if ok else None,
+            "parity_spot_check": bool(ok),
+            "roofline": {"bound": bound, "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
+                         "frac": round(achieved / peak, 4), "traffic": None,
+                         "avg_launch_ms": round(avg_ms, 4)},
+            "path_hbm_roofline": {"b_face": b_face, "achieved_GBs": round(value * b_face / 1e9, 1),
+                                  "frac": round(value * b_face / 1e9 / HBM_PEAK_GBS, 4)},
+            "stage_ms_per_step": {k: round(v[0] / max(1, args.steps), 3) for k, v in stages.items()},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+        print(json.dumps(out), flush=True)
+    ff.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

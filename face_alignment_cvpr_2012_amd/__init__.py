@@ -1,0 +1,354 @@
+"""MI355X-native conditional-regression-forest facial-landmark engine.
+
+Python host mirror of the reference's public API over the C-ABI in include/ffd.h
+(libffd.so, HIP kernels for gfx950).  Names follow the reference
+(/root/reference/include/FaceForest.hpp): FaceForestOptions, Face, FaceForest with
+analyzeFace / analyzeImage, and Forest.evaluate (Forest<S>::evaluateMT,
+include/Forest.hpp:80-90).
+
+The product path is the HIP engine only: if libffd.so is missing or no HIP
+device is usable, construction raises (there is no CPU fallback; the CPU
+restatement in oracle/ is test infrastructure).
+"""
+import ctypes
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+__all__ = [
+    "FaceForestOptions", "HeadPoseEstimatorOption", "MultiPartEstimatorOption", "MeanShiftOption",
+    "Face", "FaceForest", "Forest", "FFDError", "default_model_path", "library_path",
+    "FOREST_HEADPOSE", "FOREST_FFD", "LANDMARK_NAMES",
+]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+FOREST_HEADPOSE = 0
+FOREST_FFD = 1
+MAX_TREES = 32
+NUM_CHANNELS = 38
+LANDMARK_NAMES = ("left eye (l)", "left eye (r)", "mouth (l)", "mouth (r)", "mouth (b)", "mouth (t)",
+                  "right eye (l)", "right eye (r)", "nose (l)", "nose (r)")  # output/generate_report.m:13-15
+
+
+def library_path():
+    return os.environ.get("FFD_LIBRARY", os.path.join(HERE, "lib", "libffd.so"))
+
+
+def default_model_path():
+    return os.environ.get("FFD_MODEL", os.path.join(REPO, "model", "ffd_model.bin"))
+
+
+class FFDError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"ffd status {status}: {msg}")
+        self.status = status
+
+
+# ------------------------------------------------------------------ ctypes --
+class _Rect(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_int32), ("y", ctypes.c_int32), ("width", ctypes.c_int32), ("height", ctypes.c_int32)]
+
+
+class _Image(ctypes.Structure):
+    _fields_ = [("bgr", ctypes.c_void_p), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("stride", ctypes.c_int32)]
+
+
+class _Face(ctypes.Structure):
+    _fields_ = [("headpose", ctypes.c_float), ("pose_variance", ctypes.c_float), ("bbox", _Rect),
+                ("points", (ctypes.c_int32 * 2) * 10), ("n_trees", ctypes.c_int32), ("status", ctypes.c_int32)]
+
+
+FACE_RECORD_BYTES = ctypes.sizeof(_Face)
+
+
+class _HpOpt(ctypes.Structure):
+    _fields_ = [("num_head_pose_labels", ctypes.c_int32), ("step_size", ctypes.c_int32),
+                ("min_foreground_probability", ctypes.c_float)]
+
+
+class _MpOpt(ctypes.Structure):
+    _fields_ = [("num_parts", ctypes.c_int32), ("step_size", ctypes.c_int32), ("min_samples", ctypes.c_int32),
+                ("min_forground", ctypes.c_float), ("min_pf", ctypes.c_float), ("max_variance", ctypes.c_float)]
+
+
+class _MsOpt(ctypes.Structure):
+    _fields_ = [("kernel_size", ctypes.c_int32), ("max_iterations", ctypes.c_int32),
+                ("stopping_criteria", ctypes.c_float)]
+
+
+class _Desc(ctypes.Structure):
+    _fields_ = [("model_path", ctypes.c_char_p), ("device", ctypes.c_int32), ("max_chunk_faces", ctypes.c_int32),
+                ("hp_option", _HpOpt), ("mp_option", _MpOpt), ("ms_option", _MsOpt)]
+
+
+class _Trace(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in
+                ("face", "channels", "hp_leaves", "mp_leaves", "trees", "pose_freq", "vote_counts", "ms_mean")]
+
+
+_lib = None
+
+# Every symbol include/ffd.h declares (tests check the library exports them all).
+EXPORTED_SYMBOLS = (
+    "ffd_engine_desc_init", "ffd_engine_create", "ffd_engine_destroy", "ffd_last_error", "ffd_face_geometry",
+    "ffd_analyze_faces", "ffd_analyze_faces_device", "ffd_synchronize", "ffd_stream", "ffd_extract_channels",
+    "ffd_forest_eval_leaves", "ffd_get_trace", "ffd_version", "ffd_set_profiling", "ffd_get_stage_times",
+    "ffd_stage_name",
+)
+NUM_STAGES = 11
+
+
+def lib():
+    """Load libffd.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = library_path()
+    if not os.path.exists(path):
+        raise FFDError(-1, f"HIP engine library not built: {path} (run __graft_entry__.build())")
+    L = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    L.ffd_engine_desc_init.argtypes = [P(_Desc)]
+    L.ffd_engine_create.argtypes = [P(_Desc), P(ctypes.c_void_p)]
+    L.ffd_engine_destroy.argtypes = [ctypes.c_void_p]
+    L.ffd_last_error.argtypes = [ctypes.c_void_p]
+    L.ffd_last_error.restype = ctypes.c_char_p
+    L.ffd_version.restype = ctypes.c_char_p
+    L.ffd_face_geometry.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32] + [P(ctypes.c_int32)] * 4
+    L.ffd_analyze_faces.argtypes = [ctypes.c_void_p, P(_Image), ctypes.c_int32, P(_Rect), ctypes.c_void_p,
+                                    ctypes.c_int32, P(_Face)]
+    L.ffd_analyze_faces_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P(_Rect),
+                                           ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+    L.ffd_synchronize.argtypes = [ctypes.c_void_p]
+    L.ffd_stream.argtypes = [ctypes.c_void_p]
+    L.ffd_stream.restype = ctypes.c_void_p
+    L.ffd_extract_channels.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_void_p]
+    L.ffd_forest_eval_leaves.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                         ctypes.c_int32, ctypes.c_void_p]
+    L.ffd_get_trace.argtypes = [ctypes.c_void_p, ctypes.c_int32, P(_Trace)]
+    L.ffd_set_profiling.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    L.ffd_get_stage_times.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
+    L.ffd_stage_name.argtypes = [ctypes.c_int32]
+    L.ffd_stage_name.restype = ctypes.c_char_p
+    for name in ("ffd_engine_create", "ffd_face_geometry", "ffd_analyze_faces", "ffd_analyze_faces_device",
+                 "ffd_synchronize", "ffd_extract_channels", "ffd_forest_eval_leaves", "ffd_get_trace",
+                 "ffd_set_profiling", "ffd_get_stage_times"):
+        getattr(L, name).restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+# ----------------------------------------------------------------- options --
+@dataclass
+class HeadPoseEstimatorOption:          # include/FaceForest.hpp:34-43
+    num_head_pose_labels: int = 5
+    step_size: int = 4
+    min_foreground_probability: float = 0.5
+
+
+@dataclass
+class MultiPartEstimatorOption:         # include/FaceForest.hpp:45-58
+    num_parts: int = 10
+    step_size: int = 3
+    min_samples: int = 2
+    min_forground: float = 0.5
+    min_pf: float = 0.25
+    max_variance: float = 25.0
+
+
+@dataclass
+class MeanShiftOption:                  # include/MeanShift.hpp:16-25
+    kernel_size: int = 10
+    max_iterations: int = 7
+    stopping_criteria: float = 0.05
+
+
+@dataclass
+class FaceForestOptions:                # include/FaceForest.hpp:60-68
+    model_path: str = field(default_factory=default_model_path)
+    device: int = 0
+    max_chunk_faces: int = 0
+    hp_option: HeadPoseEstimatorOption = field(default_factory=HeadPoseEstimatorOption)
+    mp_option: MultiPartEstimatorOption = field(default_factory=MultiPartEstimatorOption)
+    ms_option: MeanShiftOption = field(default_factory=MeanShiftOption)
+
+
+@dataclass
+class Face:                             # include/FaceForest.hpp:70-75
+    headpose: float
+    bbox: tuple
+    ffd_cordinates: np.ndarray          # 10 x 2 int, bbox-relative
+    pose_variance: float = 0.0
+    n_trees: int = 0
+    status: int = 0
+
+
+def _face_from_record(r):
+    return Face(headpose=float(r.headpose), bbox=(r.bbox.x, r.bbox.y, r.bbox.width, r.bbox.height),
+                ffd_cordinates=np.array([[r.points[i][0], r.points[i][1]] for i in range(10)], np.int32),
+                pose_variance=float(r.pose_variance), n_trees=int(r.n_trees), status=int(r.status))
+
+
+def faces_from_records(buf):
+    """Decode a bytes/uint8 buffer of ffd_face records (e.g. copied back from the device)."""
+    arr = (_Face * (len(buf) // FACE_RECORD_BYTES)).from_buffer_copy(bytes(buf))
+    return [_face_from_record(r) for r in arr]
+
+
+def _check(status, handle=None):
+    if status != 0:
+        msg = lib().ffd_last_error(handle).decode(errors="replace")
+        raise FFDError(status, msg)
+
+
+# --------------------------------------------------------------- FaceForest --
+class FaceForest:
+    """FaceForest (include/FaceForest.hpp:81-157) on one MI355X device."""
+
+    def __init__(self, options=None):
+        self.options = options or FaceForestOptions()
+        L = lib()
+        d = _Desc()
+        L.ffd_engine_desc_init(ctypes.byref(d))
+        o = self.options
+        self._model_path_bytes = os.fspath(o.model_path).encode()
+        d.model_path = self._model_path_bytes
+        d.device = o.device
+        d.max_chunk_faces = o.max_chunk_faces
+        d.hp_option = _HpOpt(o.hp_option.num_head_pose_labels, o.hp_option.step_size,
+                             o.hp_option.min_foreground_probability)
+        d.mp_option = _MpOpt(o.mp_option.num_parts, o.mp_option.step_size, o.mp_option.min_samples,
+                             o.mp_option.min_forground, o.mp_option.min_pf, o.mp_option.max_variance)
+        d.ms_option = _MsOpt(o.ms_option.kernel_size, o.ms_option.max_iterations, o.ms_option.stopping_criteria)
+        h = ctypes.c_void_p()
+        st = L.ffd_engine_create(ctypes.byref(d), ctypes.byref(h))
+        if st != 0:
+            raise FFDError(st, L.ffd_last_error(None).decode(errors="replace"))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ffd_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ---- reference API ------------------------------------------------------
+    def analyzeFace(self, img, face_bbox):
+        """FaceForest::analyzeFace(img, bbox, face) (src/FaceForest.cpp:183-258)."""
+        return self.analyzeFaces([img], [face_bbox])[0]
+
+    def analyzeImage(self, img, faces_bboxes):
+        """FaceForest::analyzeImage (src/FaceForest.cpp:161-181) with the face boxes supplied by
+        the caller's detector (the Haar cascade stays outside this engine)."""
+        return self.analyzeFaces([img], list(faces_bboxes), [0] * len(faces_bboxes))
+
+    # ---- batched API --------------------------------------------------------
+    def analyzeFaces(self, images, boxes, box_img=None):
+        imgs = [np.ascontiguousarray(im, dtype=np.uint8) for im in images]
+        n = len(boxes)
+        if n == 0:
+            return []
+        cim = (_Image * len(imgs))()
+        for i, im in enumerate(imgs):
+            if im.ndim != 3 or im.shape[2] != 3:
+                raise ValueError("images must be HxWx3 BGR uint8")
+            cim[i] = _Image(im.ctypes.data, im.shape[1], im.shape[0], im.strides[0])
+        crect = (_Rect * n)(*[_Rect(*[int(v) for v in b]) for b in boxes])
+        cmap = None
+        if box_img is not None:
+            cmap = np.ascontiguousarray(box_img, np.int32)
+        out = (_Face * n)()
+        _check(lib().ffd_analyze_faces(self._h, cim, len(imgs), crect,
+                                       cmap.ctypes.data if cmap is not None else None, n, out), self._h)
+        return [_face_from_record(r) for r in out]
+
+    def analyze_device(self, d_images, image_bytes, width, height, stride, n_img, boxes, box_img, d_out):
+        """Enqueue a batch whose images (and output records) live in device memory."""
+        n = len(boxes)
+        crect = (_Rect * n)(*[_Rect(*[int(v) for v in b]) for b in boxes])
+        cmap = np.ascontiguousarray(box_img, np.int32) if box_img is not None else None
+        _check(lib().ffd_analyze_faces_device(self._h, d_images, image_bytes, width, height, stride, n_img, crect,
+                                              cmap.ctypes.data if cmap is not None else None, n, d_out), self._h)
+        self._keep = cmap
+
+    def synchronize(self):
+        _check(lib().ffd_synchronize(self._h), self._h)
+
+    def stream(self):
+        return lib().ffd_stream(self._h)
+
+    def set_profiling(self, enable=True):
+        _check(lib().ffd_set_profiling(self._h, 1 if enable else 0), self._h)
+
+    def stage_times(self):
+        """{stage name: (total device ms, launches)} since set_profiling(True)."""
+        ms = np.zeros(NUM_STAGES, np.float64)
+        n = np.zeros(NUM_STAGES, np.int64)
+        _check(lib().ffd_get_stage_times(self._h, ms.ctypes.data, n.ctypes.data, NUM_STAGES), self._h)
+        return {lib().ffd_stage_name(i).decode(): (float(ms[i]), int(n[i])) for i in range(NUM_STAGES)}
+
+    def geometry(self, box_w, box_h):
+        v = [ctypes.c_int32() for _ in range(4)]
+        _check(lib().ffd_face_geometry(self._h, box_w, box_h, *[ctypes.byref(x) for x in v]), self._h)
+        return tuple(x.value for x in v)  # face_w, face_h, n_hp_patches, n_mp_patches
+
+    def extract_channels(self, gray_face):
+        """ImageSample(img, {0,1,2}, true).m_feature_channels as 38 x (h+1) x (w+1) uint32."""
+        g = np.ascontiguousarray(gray_face, np.uint8)
+        h, w = g.shape
+        out = np.zeros((NUM_CHANNELS, h + 1, w + 1), np.uint32)
+        _check(lib().ffd_extract_channels(self._h, g.ctypes.data, w, h, out.ctypes.data), self._h)
+        return out
+
+    def trace(self, index, box_w, box_h):
+        """Per-stage intermediates of face `index` of the last batch."""
+        fw, fh, nhp, nmp = self.geometry(box_w, box_h)
+        bufs = dict(face=np.zeros((fh, fw), np.uint8), channels=np.zeros((NUM_CHANNELS, fh + 1, fw + 1), np.uint32),
+                    hp_leaves=np.zeros((nhp, 15), np.int32), mp_leaves=np.zeros(nmp * MAX_TREES, np.int32),
+                    trees=np.zeros(MAX_TREES, np.int32), pose_freq=np.zeros(5, np.float32),
+                    vote_counts=np.zeros(10, np.int32), ms_mean=np.zeros((10, 2), np.float32))
+        tr = _Trace(*[bufs[k].ctypes.data for k, _ in _Trace._fields_])
+        _check(lib().ffd_get_trace(self._h, index, ctypes.byref(tr)), self._h)
+        nt = int((bufs["trees"] >= 0).sum())
+        bufs["trees"] = bufs["trees"][:nt]
+        bufs["mp_leaves"] = bufs["mp_leaves"][: nmp * nt].reshape(nmp, nt)
+        return bufs
+
+
+class Forest:
+    """Forest<S>::evaluateMT over a batch of patches (include/Forest.hpp:80-90)."""
+
+    def __init__(self, face_forest, kind):
+        self.ff = face_forest
+        self.kind = kind
+
+    def evaluate(self, channels, patches_xy, tree_ids):
+        ch = np.ascontiguousarray(channels, np.uint32)
+        _, h1, w1 = ch.shape
+        p = np.ascontiguousarray(patches_xy, np.int32).reshape(-1, 2)
+        t = np.ascontiguousarray(tree_ids, np.int32)
+        out = np.zeros((p.shape[0], t.size), np.int32)
+        _check(lib().ffd_forest_eval_leaves(self.ff.handle, self.kind, ch.ctypes.data, w1 - 1, h1 - 1, p.ctypes.data,
+                                            p.shape[0], t.ctypes.data, t.size, out.ctypes.data), self.ff.handle)
+        return out

@@ -1,0 +1,79 @@
+// ffd_device.hpp — data layout shared by the host engine and the HIP kernels.
+//
+// HBM layout (per face, row pitch PITCH elements, see DESIGN.md §Data layout):
+//   gray   u8  [H][PITCH]                  scaled gray face (FaceForest.cpp:195-204)
+//   mag    f32 [35][H][PITCH]              Gabor magnitudes before min-max normalisation
+//   chan   u32 [38][H+1][PITCH]            integral channels (ImageSample m_feature_channels)
+//   hpleaf i32 [15][n_hp]                  head-pose leaf ordinal per (tree, patch lane-order)
+//   mpleaf i32 [T][n_mp]                   FFD leaf ordinal per (tree slot, patch lane-order)
+//   votes  {i16 x,y; f32 w} [10][T*n_mp]   compacted votes per landmark (MeanShift input)
+// "lane order" enumerates the patch grid y-major (q = yi*nx + xi) so that the 64 lanes
+// of a traversal wave read horizontally adjacent patches; the reference order is
+// x-major (i = xi*ny + yi, face_utils.cpp:200-207) and every consumer that depends on
+// order (head-pose sums, vote lists) walks the reference order.
+#pragma once
+
+#include <stdint.h>
+
+namespace ffd {
+
+constexpr int PITCH = 128;        // row pitch (elements) of gray/mag/channel planes; W <= 125
+constexpr int NCH = 38;           // 1 gray + 35 Gabor + 2 Sobel (config "0 1 2")
+constexpr int NGABOR = 35;
+constexpr int NPARTS = 10;
+constexpr int NHP_LABELS = 5;
+constexpr int MAX_TREES = 32;     // FFD_MAX_TREES
+constexpr int MAX_FACE_H = 320;   // scaled face height limit (aspect <= 2.56)
+constexpr uint32_t LEAF_BIT = 0x80000000u;
+
+// Flattened tree node (16 B), breadth-first per tree, children adjacent:
+//   x: internal -> global index of the left child (right = left + 1); leaf -> LEAF_BIT | ordinal
+//   y: ch | r1w<<6 | r1h<<11 | r2w<<16 | r2h<<21
+//   z: threshold (int32)
+//   w: off1 | off2<<16, off = ry*PITCH + rx (patch-relative integral-image offsets)
+// Source fields: ThresholdSplit<SimplePatchFeature> (ThresholdSplit.hpp:51-67,
+// ImageSample.hpp:462-464) and TreeNode::left/right (TreeNode.hpp:138-141).
+
+struct FaceDesc {
+  int64_t img_off;        // byte offset of the source image
+  int32_t img_w, img_h, img_stride;
+  int32_t bx, by, bw, bh; // face box in the image
+  int32_t W, H;           // scaled face size
+  float scale;            // 125.f / bw
+  int32_t mode;           // 0 copy, 1 bilinear, 2 area 2x
+  double scale_x, scale_y;// resize source/dest ratios (resize(), OpenCV 2.4.9)
+  int32_t xv;             // columns covered by the SSE2 vertical pass
+  int32_t nhx, nhy, nmx, nmy;  // patch grid sizes (step 4 / step 3)
+  int64_t gray_off;       // byte offset into the gray buffer
+  int64_t mag_off;        // element offset into the mag buffer
+  int64_t ch_off;         // element offset into the channel buffer
+  int64_t plane;          // channel plane stride (elements) = (H+1)*PITCH
+  int64_t hp_off;         // element offset into the head-pose leaf buffer
+  int64_t mp_off;         // element offset into the FFD leaf buffer
+  int64_t vote_off;       // element offset into the vote buffer
+  int32_t valid;          // 0: box rejected, face skipped
+  int32_t pad_;
+};
+
+struct FaceOut {          // == ffd_face
+  float headpose;
+  float pose_variance;
+  int32_t bbox[4];
+  int32_t points[NPARTS][2];
+  int32_t n_trees;
+  int32_t status;
+};
+
+struct Vote {
+  int16_t x, y;
+  float w;
+};
+
+struct HpState {          // per-face head-pose result + tree selection
+  float headpose, variance;
+  float pose_freq[8];
+  int32_t n_trees;
+  int32_t trees[MAX_TREES];
+};
+
+}  // namespace ffd

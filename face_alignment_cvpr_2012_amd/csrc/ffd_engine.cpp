@@ -1,0 +1,836 @@
+// ffd_engine.cpp — host side of the MI355X engine behind include/ffd.h.
+//
+// Owns the device-resident model (flattened forests + leaf tables), the workspace
+// and one HIP stream; orchestrates the kernel pipeline of ffd_kernels.hip for a batch
+// of faces.  Replaces, per reference file (paths relative to /root/reference):
+//   FaceForest::FaceForest / Forest::load      src/FaceForest.cpp:15-58, include/Forest.hpp:103-153
+//   FaceForest::analyzeFace (batched)          src/FaceForest.cpp:183-258
+//   FeatureChannelFactory::initGaborKernels    include/FeatureChannelFactory.hpp:186-251
+// The product never calls the CPU oracle; when no HIP device is usable every entry
+// point fails with FFD_ERR_DEVICE (no CPU fallback).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/ffd.h"
+#include "ffd_device.hpp"
+#include "ffd_kernels.hpp"
+#include "model_io.hpp"
+
+#define FFD_VERSION_STR "ffd-mi355x 0.1.0 (gfx950)"
+
+namespace {
+
+using namespace ffd;
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIP_CHECK(expr)                                                                        \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      throw HipError(std::string(#expr) + ": " + hipGetErrorString(e_) + " (" __FILE__ ":" +  \
+                     std::to_string(__LINE__) + ")");                                         \
+  } while (0)
+
+// Device buffer that grows on demand (never shrinks).
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  void* ensure(size_t bytes) {
+    if (bytes <= n) return p;
+    if (p) { (void)hipFree(p); p = nullptr; n = 0; }
+    size_t want = std::max<size_t>(bytes, 256);
+    HIP_CHECK(hipMalloc(&p, want));
+    n = want;
+    return p;
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+template <class T> void upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
+  b.ensure(v.size() * sizeof(T));
+  if (!v.empty()) HIP_CHECK(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+}
+
+int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+struct Geometry {
+  int W = 0, H = 0, nhx = 0, nhy = 0, nmx = 0, nmy = 0;
+  float scale = 0;
+};
+
+}  // namespace
+
+struct ffd_engine {
+  std::string err;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  ffd_engine_desc desc{};
+  int max_chunk = 1024;
+
+  // model parameters
+  int face_size = 125, patch = 31, hp_trees = 0, n_forests = 0, ntrees_per_forest = 0;
+  int64_t hp_leaves = 0, mp_leaves = 0;
+
+  // device model
+  DevBuf hp_nodes, hp_roots, hp_m, mp_nodes, mp_roots, mp_mask, mp_fg, mp_offs;
+
+  // workspace
+  DevBuf faces, wave_hp, wave_mp, images, gray, mag, minmax, chan, hpleaf, mpleaf, votes, state, out,
+      ms_mean, vote_counts, maxtrees, scratch_a, scratch_b, scratch_c;
+  std::vector<uint8_t> pinned_dummy;
+
+  // stage profiler (hipEvents on the engine stream)
+  struct Pending { int stage; hipEvent_t a, b; };
+  bool profiling = false;
+  std::vector<hipEvent_t> event_pool;
+  std::vector<Pending> pending;
+  double stage_ms[FFD_NUM_STAGES] = {0};
+  int64_t stage_n[FFD_NUM_STAGES] = {0};
+
+  hipEvent_t get_event() {
+    if (!event_pool.empty()) { hipEvent_t e = event_pool.back(); event_pool.pop_back(); return e; }
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    return e;
+  }
+  // Run `fn` (one kernel launch) bracketed by events when profiling.
+  template <class F> void stage(int id, F&& fn) {
+    if (!profiling) { fn(); return; }
+    Pending p{id, get_event(), get_event()};
+    HIP_CHECK(hipEventRecord(p.a, stream));
+    fn();
+    HIP_CHECK(hipEventRecord(p.b, stream));
+    pending.push_back(p);
+  }
+  void resolve() {
+    if (pending.empty()) return;
+    HIP_CHECK(hipStreamSynchronize(stream));
+    for (auto& p : pending) {
+      float ms = 0;
+      HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
+      stage_ms[p.stage] += ms;
+      stage_n[p.stage] += 1;
+      event_pool.push_back(p.a);
+      event_pool.push_back(p.b);
+    }
+    pending.clear();
+  }
+
+  // last batch bookkeeping (for ffd_get_trace)
+  std::vector<FaceDesc> last_desc;
+  int last_first = 0, last_count = 0, last_tslots = 0;
+
+  ~ffd_engine() {
+    for (auto& p : pending) { event_pool.push_back(p.a); event_pool.push_back(p.b); }
+    for (auto e : event_pool) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  Geometry geometry(int bw, int bh) const {
+    Geometry g;
+    if (bw <= 0 || bh <= 0) return g;
+    g.scale = (float)face_size / (float)bw;  // FaceForest.cpp:202
+    g.W = (int)((float)bw * g.scale);        // cv::Size(cols*scale, rows*scale) truncation
+    g.H = (int)((float)bh * g.scale);
+    auto cnt = [&](int extent, int step) {
+      int n = 0;
+      for (int x = 0; x < extent - patch; x += step) n++;
+      return n;
+    };
+    g.nhx = cnt(g.W, desc.hp_option.step_size);
+    g.nhy = cnt(g.H, desc.hp_option.step_size);
+    g.nmx = cnt(g.W, desc.mp_option.step_size);
+    g.nmy = cnt(g.H, desc.mp_option.step_size);
+    return g;
+  }
+
+  void load_model(const std::string& path);
+  void build_gabor();
+  void run_chunk(std::vector<FaceDesc>& fds, const uint8_t* d_images, FaceOut* d_out);
+  void analyze(const uint8_t* d_images, const std::vector<FaceDesc>& all, FaceOut* d_out);
+};
+
+namespace {
+
+thread_local std::string g_create_err;
+
+// Flatten the pre-order archive records of every tree into breadth-first node arrays
+// with adjacent children (see ffd_device.hpp for the 16-byte node encoding).
+void flatten_forest(const ModelFile& m, const std::string& p, std::vector<uint4>& nodes, std::vector<int32_t>& roots) {
+  const auto& off = m.get(p + ".tree_node_off");
+  const auto& nl = m.get(p + ".node_leaf");
+  const auto& ns = m.get(p + ".node_split");
+  const int64_t* to = off.as<int64_t>();
+  const int32_t* leaf = nl.as<int32_t>();
+  const int16_t* sp = ns.as<int16_t>();
+  const int64_t T = (int64_t)off.count() - 1;
+  nodes.clear();
+  roots.clear();
+  nodes.reserve(nl.count());
+  for (int64_t t = 0; t < T; t++) {
+    const int64_t b = to[t], e = to[t + 1];
+    const int64_t n = e - b;
+    std::vector<int64_t> left(n, -1), right(n, -1), stack;
+    for (int64_t i = 0; i < n; i++) {
+      if (i > 0) {
+        if (stack.empty()) throw std::runtime_error("malformed tree in model");
+        int64_t par = stack.back();
+        if (left[par] < 0) left[par] = i;
+        else { right[par] = i; stack.pop_back(); }
+      }
+      if (leaf[b + i] < 0) stack.push_back(i);
+    }
+    if (!stack.empty()) throw std::runtime_error("incomplete tree in model");
+    std::vector<int64_t> order{0}, newidx(n, -1);
+    for (size_t k = 0; k < order.size(); k++) {
+      int64_t v = order[k];
+      if (leaf[b + v] < 0) { order.push_back(left[v]); order.push_back(right[v]); }
+    }
+    const int64_t base = (int64_t)nodes.size();
+    for (size_t k = 0; k < order.size(); k++) newidx[order[k]] = base + (int64_t)k;
+    roots.push_back((int32_t)base);
+    for (size_t k = 0; k < order.size(); k++) {
+      const int64_t v = order[k];
+      uint4 nd;
+      if (leaf[b + v] >= 0) {
+        nd.x = LEAF_BIT | (uint32_t)leaf[b + v];
+        nd.y = nd.z = nd.w = 0;
+      } else {
+        const int16_t* s = sp + (b + v) * FFD_SPLIT_FIELDS;
+        const int ch = s[0], x1 = s[1], y1 = s[2], w1 = s[3], h1 = s[4], x2 = s[5], y2 = s[6], w2 = s[7], h2 = s[8];
+        if (ch < 0 || ch >= NCH) throw std::runtime_error("split channel out of range");
+        for (int q : {w1, h1, w2, h2})
+          if (q < 1 || q > 31) throw std::runtime_error("split rectangle size out of range");
+        for (int q : {x1, y1, x2, y2})
+          if (q < 0 || q > 31) throw std::runtime_error("split rectangle offset out of range");
+        if (x1 + w1 > 31 || y1 + h1 > 31 || x2 + w2 > 31 || y2 + h2 > 31)
+          throw std::runtime_error("split rectangle leaves the patch");
+        nd.x = (uint32_t)newidx[left[v]];
+        if (newidx[right[v]] != newidx[left[v]] + 1) throw std::runtime_error("BFS layout error");
+        nd.y = (uint32_t)ch | (uint32_t)w1 << 6 | (uint32_t)h1 << 11 | (uint32_t)w2 << 16 | (uint32_t)h2 << 21;
+        nd.z = (uint32_t)(int32_t)s[9];
+        nd.w = (uint32_t)(y1 * PITCH + x1) | (uint32_t)(y2 * PITCH + x2) << 16;
+      }
+      nodes.push_back(nd);
+    }
+  }
+  if ((int64_t)nodes.size() != (int64_t)nl.count()) throw std::runtime_error("node count mismatch");
+}
+
+}  // namespace
+
+void ffd_engine::load_model(const std::string& path) {
+  ModelFile m;
+  m.load(path);
+  const int32_t* hp_param = m.get("hp.param").as<int32_t>();
+  const int32_t* mp_param = m.get("mp.param").as<int32_t>();
+  face_size = hp_param[6];
+  const float ratio = m.get("hp.patch_ratio").as<float>()[0];
+  patch = (int)std::round(face_size * ratio);  // ForestParam::getPatchSize (Constants.hpp:27-30)
+  n_forests = mp_param[7];
+  ntrees_per_forest = mp_param[3];
+  if (patch != 31) throw std::runtime_error("unsupported patch size (engine is built for 31x31 patches)");
+  if (face_size > 125) throw std::runtime_error("unsupported face size (> 125)");
+  for (const char* p : {"hp", "mp"}) {
+    const auto& feats = m.get(std::string(p) + ".features");
+    std::vector<int> f(feats.as<int32_t>(), feats.as<int32_t>() + feats.count());
+    std::sort(f.begin(), f.end());
+    if (f != std::vector<int>({0, 1, 2})) throw std::runtime_error("engine supports feature channels {0,1,2} only");
+  }
+  if (n_forests < 1 || n_forests > 5) throw std::runtime_error("engine supports 1..5 pose forests (poseT has 5 bins)");
+
+  std::vector<uint4> nodes;
+  std::vector<int32_t> roots;
+  flatten_forest(m, "hp", nodes, roots);
+  hp_trees = (int)roots.size();
+  upload(hp_nodes, nodes, stream);
+  upload(hp_roots, roots, stream);
+  flatten_forest(m, "mp", nodes, roots);
+  if ((int)roots.size() != n_forests * ntrees_per_forest) throw std::runtime_error("FFD tree count mismatch");
+  upload(mp_nodes, nodes, stream);
+  upload(mp_roots, roots, stream);
+
+  // head-pose leaf value m (face_utils.cpp:223-228), -1 when the leaf is filtered out
+  {
+    const auto& n = m.get("hp.leaf_n");
+    const auto& fg = m.get("hp.leaf_fg");
+    const auto& lb = m.get("hp.leaf_labels");
+    hp_leaves = (int64_t)n.count();
+    std::vector<float> mv(hp_leaves);
+    const int nl = std::min(desc.hp_option.num_head_pose_labels, (int)FFD_NUM_HP_LABELS);
+    for (int64_t L = 0; L < hp_leaves; L++) {
+      const float f = fg.as<float>()[L];
+      if (f > desc.hp_option.min_foreground_probability) {
+        float v = 0;
+        for (int j = 0; j < nl; j++) v += lb.as<int32_t>()[L * 5 + j] * j;
+        v /= (n.as<int32_t>()[L] * f);
+        mv[L] = v;
+      } else {
+        mv[L] = -1.f;
+      }
+    }
+    upload(hp_m, mv, stream);
+  }
+  // FFD leaf vote mask / weight / offsets (face_utils.cpp:283-298)
+  {
+    const auto& n = m.get("mp.leaf_n");
+    const auto& fg = m.get("mp.leaf_fg");
+    const auto& off = m.get("mp.leaf_offset");
+    const auto& var = m.get("mp.leaf_var");
+    const auto& pf = m.get("mp.leaf_pf");
+    mp_leaves = (int64_t)n.count();
+    std::vector<uint32_t> mask(mp_leaves);
+    std::vector<float> w(mp_leaves);
+    std::vector<int32_t> o(mp_leaves * NPARTS);
+    const auto& op = desc.mp_option;
+    const int np = std::min(op.num_parts, NPARTS);
+    for (int64_t L = 0; L < mp_leaves; L++) {
+      uint32_t mk = 0;
+      const float f = fg.as<float>()[L];
+      for (int i = 0; i < np; i++) {
+        float min_pf = op.min_pf;
+        if (i == 0 || i == 7) min_pf *= 1.5;  // outer eye corners
+        if (f > op.min_forground && pf.as<float>()[L * 10 + i] > min_pf && var.as<float>()[L * 10 + i] < op.max_variance &&
+            n.as<int32_t>()[L] > op.min_samples)
+          mk |= 1u << i;
+      }
+      mask[L] = mk;
+      w[L] = f;
+      for (int i = 0; i < NPARTS; i++) {
+        const int16_t x = off.as<int16_t>()[(L * 10 + i) * 2], y = off.as<int16_t>()[(L * 10 + i) * 2 + 1];
+        o[L * NPARTS + i] = (int32_t)((uint32_t)(uint16_t)x | (uint32_t)(uint16_t)y << 16);
+      }
+    }
+    upload(mp_mask, mask, stream);
+    upload(mp_fg, w, stream);
+    upload(mp_offs, o, stream);
+  }
+  HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+// createKernel / initGaborKernels (FeatureChannelFactory.hpp:186-251), packed for k_gabor.
+void ffd_engine::build_gabor() {
+  std::vector<float> coef(GABOR_COEF_TOTAL, 0.f);
+  const double CV_PI = 3.1415926535897932384626433832795;
+  const double sigma = 1.0 / 2.0 * CV_PI, dF = std::sqrt(2.0);
+  for (int iNu = 0; iNu <= 4; iNu++) {
+    std::vector<std::vector<float>> re(7), im(7);
+    int Wk = 0;
+    for (int iMu = 0; iMu < 7; iMu++) {
+      double F = dF;
+      double k = (CV_PI / 2) / std::pow(F, (double)iNu);
+      double phi = CV_PI * iMu / 8;
+      double width = std::round((sigma / k) * 6 + 1);
+      if (std::fmod(width, 2.0) == 0.0) width++;
+      Wk = (int)width;
+      if (Wk != GABOR_WIDTHS[iNu]) throw std::runtime_error("unexpected Gabor kernel width");
+      re[iMu].assign(Wk * Wk, 0.f);
+      im[iMu].assign(Wk * Wk, 0.f);
+      int off_set = (int)((width - 1) / 2);
+      for (int i = 0; i < Wk; i++)
+        for (int j = 0; j < Wk; j++) {
+          int x = i - off_set, y = j - off_set;
+          double dTemp1 = (std::pow(k, 2) / std::pow(sigma, 2)) *
+                          std::exp(-(std::pow((double)x, 2) + std::pow((double)y, 2)) * std::pow(k, 2) /
+                                   (2 * std::pow(sigma, 2)));
+          double dTemp2 = std::cos(k * std::cos(phi) * x + k * std::sin(phi) * y) - std::exp(-(std::pow(sigma, 2) / 2));
+          double dTemp3 = std::sin(k * std::cos(phi) * x + k * std::sin(phi) * y);
+          re[iMu][j * Wk + i] = (float)(dTemp1 * dTemp2);
+          im[iMu][j * Wk + i] = (float)(dTemp1 * dTemp3);
+        }
+      const int n = Wk * Wk;
+      for (int t = 0; t < n; t++)
+        if (re[iMu][t] != re[iMu][n - 1 - t] || im[iMu][t] != -im[iMu][n - 1 - t])
+          throw std::runtime_error("Gabor kernel not point-symmetric on this libm");
+    }
+    const int OFF = GABOR_OFFS[iNu];
+    if (Wk == 7) {
+      for (int t = 0; t < 49; t++)
+        for (int o = 0; o < 7; o++) {
+          coef[OFF + t * 14 + o] = re[o][t];
+          coef[OFF + t * 14 + 7 + o] = im[o][t];
+        }
+    } else {
+      const int half = (Wk * Wk - 1) / 2;
+      for (int t = 0; t < half; t++)
+        for (int o = 0; o < 7; o++) {
+          coef[OFF + t * 14 + o] = re[o][t];
+          coef[OFF + t * 14 + 7 + o] = im[o][t];
+        }
+      for (int o = 0; o < 7; o++) coef[OFF + half * 14 + o] = re[o][half];
+    }
+  }
+  HIP_CHECK(upload_gabor(coef.data(), stream));
+  HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+// Run the whole pipeline for one chunk of faces (desc offsets relative to the chunk
+// workspace).  d_out points at the chunk's first output record.
+void ffd_engine::run_chunk(std::vector<FaceDesc>& fds, const uint8_t* d_images, FaceOut* d_out) {
+  const int n = (int)fds.size();
+  if (n == 0) return;
+  resolve();
+  int64_t gray_b = 0, mag_e = 0, ch_e = 0, hp_e = 0, mp_e = 0, vote_e = 0;
+  int max_w = 0, max_h = 0;
+  for (auto& f : fds) {
+    if (!f.valid) continue;
+    f.gray_off = gray_b;
+    gray_b += align_up((int64_t)f.H * PITCH, 256);
+    f.mag_off = mag_e;
+    mag_e += (int64_t)NGABOR * f.H * PITCH;
+    f.plane = (int64_t)(f.H + 1) * PITCH;
+    f.ch_off = ch_e;
+    ch_e += NCH * f.plane;
+    f.hp_off = hp_e;
+    hp_e += (int64_t)hp_trees * f.nhx * f.nhy;
+    f.mp_off = mp_e;
+    mp_e += (int64_t)MAX_TREES * f.nmx * f.nmy;
+    f.vote_off = vote_e;
+    vote_e += (int64_t)NPARTS * MAX_TREES * f.nmx * f.nmy;
+    max_w = std::max(max_w, f.W);
+    max_h = std::max(max_h, f.H);
+  }
+  gray.ensure(gray_b + 256);
+  mag.ensure((mag_e + 64) * 4);
+  chan.ensure((ch_e + 64) * 4);
+  hpleaf.ensure((hp_e + 64) * 4);
+  mpleaf.ensure((mp_e + 64) * 4);
+  votes.ensure((vote_e + 64) * sizeof(Vote));
+  minmax.ensure((size_t)n * NGABOR * 2 * 4);
+  state.ensure((size_t)n * sizeof(HpState));
+  ms_mean.ensure((size_t)n * NPARTS * 2 * 4);
+  vote_counts.ensure((size_t)n * NPARTS * 4);
+
+  // traversal wave tables (face-major; HP: 15 trees; FFD: filled after the tree count is known)
+  std::vector<int64_t> ws_hp(n + 1, 0);
+  for (int i = 0; i < n; i++) {
+    const auto& f = fds[i];
+    int64_t w = f.valid ? (int64_t)hp_trees * ((f.nhx * f.nhy + 63) / 64) : 0;
+    ws_hp[i + 1] = ws_hp[i] + w;
+  }
+  upload(faces, fds, stream);
+  upload(wave_hp, ws_hp, stream);
+  HIP_CHECK(hipMemsetAsync(minmax.p, 0xFF, (size_t)n * NGABOR * 2 * 4, stream));
+  HIP_CHECK(hipMemsetAsync(d_out, 0, (size_t)n * sizeof(FaceOut), stream));
+  maxtrees.ensure(4);
+
+  const FaceDesc* dfd = faces.as<FaceDesc>();
+  stage(0, [&] { launch_gray_resize(dfd, n, d_images, gray.as<uint8_t>(), stream); });
+  for (int nu = 4; nu >= 0; nu--)  // largest kernels first
+    stage(1 + (4 - nu), [&] {
+      launch_gabor(nu, dfd, n, max_w, max_h, gray.as<uint8_t>(), mag.as<float>(), minmax.as<uint32_t>(), stream);
+    });
+  stage(6, [&] {
+    launch_integral(dfd, n, gray.as<uint8_t>(), mag.as<float>(), minmax.as<uint32_t>(), chan.as<uint32_t>(), stream);
+  });
+  stage(7, [&] {
+    launch_traverse(true, dfd, wave_hp.as<int64_t>(), n, ws_hp[n], hp_nodes.as<uint4>(), hp_roots.as<int32_t>(),
+                    nullptr, hp_trees, desc.hp_option.step_size, chan.as<uint32_t>(), hpleaf.as<int32_t>(), stream);
+  });
+  stage(8, [&] {
+    launch_hp_pose(dfd, n, hpleaf.as<int32_t>(), hp_m.as<float>(), hp_trees, n_forests, ntrees_per_forest,
+                   state.as<HpState>(), d_out, stream);
+  });
+  HIP_CHECK(hipGetLastError());
+
+  // per-face tree counts decide the FFD traversal grid: read them back (small sync)
+  std::vector<HpState> hs(n);
+  HIP_CHECK(hipMemcpyAsync(hs.data(), state.p, (size_t)n * sizeof(HpState), hipMemcpyDeviceToHost, stream));
+  HIP_CHECK(hipStreamSynchronize(stream));
+  int tslots = 0;
+  std::vector<int64_t> ws_mp(n + 1, 0);
+  for (int i = 0; i < n; i++) {
+    const auto& f = fds[i];
+    int nt = f.valid ? hs[i].n_trees : 0;
+    tslots = std::max(tslots, nt);
+    int64_t w = f.valid ? (int64_t)nt * ((f.nmx * f.nmy + 63) / 64) : 0;
+    ws_mp[i + 1] = ws_mp[i] + w;
+  }
+  upload(wave_mp, ws_mp, stream);
+  stage(9, [&] {
+    launch_traverse(false, dfd, wave_mp.as<int64_t>(), n, ws_mp[n], mp_nodes.as<uint4>(), mp_roots.as<int32_t>(),
+                    state.as<HpState>(), tslots, desc.mp_option.step_size, chan.as<uint32_t>(), mpleaf.as<int32_t>(),
+                    stream);
+  });
+  stage(10, [&] {
+    launch_votes_meanshift(dfd, n, mpleaf.as<int32_t>(), mp_mask.as<uint32_t>(), mp_fg.as<float>(),
+                           mp_offs.as<int32_t>(), state.as<HpState>(), MAX_TREES, desc.mp_option.step_size, patch / 2,
+                           std::min(desc.mp_option.num_parts, NPARTS), (float)desc.ms_option.kernel_size,
+                           desc.ms_option.max_iterations, desc.ms_option.stopping_criteria, votes.as<Vote>(),
+                           ms_mean.as<float>(), vote_counts.as<int32_t>(), d_out, stream);
+  });
+  HIP_CHECK(hipGetLastError());
+  last_tslots = tslots;
+}
+
+void ffd_engine::analyze(const uint8_t* d_images, const std::vector<FaceDesc>& all, FaceOut* d_out) {
+  const int n = (int)all.size();
+  for (int first = 0; first < n; first += max_chunk) {
+    const int cnt = std::min(max_chunk, n - first);
+    std::vector<FaceDesc> fds(all.begin() + first, all.begin() + first + cnt);
+    run_chunk(fds, d_images, d_out + first);
+    last_desc = fds;
+    last_first = first;
+    last_count = cnt;
+  }
+}
+
+namespace {
+
+ffd_status fail(ffd_engine* e, ffd_status s, const std::string& msg) {
+  if (e) e->err = msg;
+  else g_create_err = msg;
+  return s;
+}
+
+// Fill the per-face descriptor (geometry + resize parameters) for a box on an image.
+bool make_desc(const ffd_engine* e, int64_t img_off, int iw, int ih, int stride, const ffd_rect& b, FaceDesc& f) {
+  std::memset(&f, 0, sizeof(f));
+  f.img_off = img_off;
+  f.img_w = iw; f.img_h = ih; f.img_stride = stride;
+  f.bx = b.x; f.by = b.y; f.bw = b.width; f.bh = b.height;
+  if (b.x < 0 || b.y < 0 || b.width <= 0 || b.height <= 0 || b.x + b.width > iw || b.y + b.height > ih) return false;
+  Geometry g = e->geometry(b.width, b.height);
+  if (g.W < 2 || g.H < 2 || g.W > PITCH - 3 || g.H > MAX_FACE_H) return false;
+  f.W = g.W; f.H = g.H; f.scale = g.scale;
+  f.nhx = g.nhx; f.nhy = g.nhy; f.nmx = g.nmx; f.nmy = g.nmy;
+  if (f.nhx * f.nhy == 0) return false;  // no head-pose patches: the reference divides 0/0
+  if (g.W == b.width && g.H == b.height) {
+    f.mode = 0;
+  } else {
+    double inv_x = (double)g.W / b.width, inv_y = (double)g.H / b.height;
+    f.scale_x = 1. / inv_x;
+    f.scale_y = 1. / inv_y;
+    int ix = (int)std::nearbyint(f.scale_x), iy = (int)std::nearbyint(f.scale_y);
+    bool area_fast = std::fabs(f.scale_x - ix) < DBL_EPSILON && std::fabs(f.scale_y - iy) < DBL_EPSILON;
+    f.mode = (area_fast && ix == 2 && iy == 2) ? 2 : 1;
+  }
+  int xv = 0;
+  while (xv <= g.W - 16) xv += 16;
+  while (xv < g.W - 4) xv += 4;
+  f.xv = xv;
+  f.valid = 1;
+  return true;
+}
+
+template <class F> ffd_status guarded(ffd_engine* e, F&& fn) {
+  if (!e) return FFD_ERR_INVALID_ARGUMENT;
+  try {
+    HIP_CHECK(hipSetDevice(e->device));
+    return fn();
+  } catch (const HipError& x) {
+    return fail(e, FFD_ERR_DEVICE, x.what());
+  } catch (const std::bad_alloc&) {
+    return fail(e, FFD_ERR_OUT_OF_MEMORY, "host allocation failed");
+  } catch (const std::exception& x) {
+    return fail(e, FFD_ERR_INTERNAL, x.what());
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ffd_version(void) { return FFD_VERSION_STR; }
+
+void ffd_engine_desc_init(ffd_engine_desc* d) {
+  if (!d) return;
+  std::memset(d, 0, sizeof(*d));
+  d->model_path = nullptr;
+  d->device = 0;
+  d->max_chunk_faces = 0;
+  d->hp_option.num_head_pose_labels = 5;        // NUM_HEADPOSE_CLASSES
+  d->hp_option.step_size = 4;
+  d->hp_option.min_foreground_probability = 0.5f;
+  d->mp_option.num_parts = 10;
+  d->mp_option.step_size = 3;
+  d->mp_option.min_samples = 2;
+  d->mp_option.min_forground = 0.5f;
+  d->mp_option.min_pf = 0.25f;
+  d->mp_option.max_variance = 25.f;
+  d->ms_option.kernel_size = 10;
+  d->ms_option.max_iterations = 7;
+  d->ms_option.stopping_criteria = 0.05f;
+}
+
+ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
+  if (!out) return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "out is NULL");
+  *out = nullptr;
+  if (!d || !d->model_path) return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "desc/model_path is NULL");
+  if (d->hp_option.step_size <= 0 || d->mp_option.step_size <= 0 || d->ms_option.kernel_size == 0)
+    return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "invalid estimator options");
+  std::unique_ptr<ffd_engine> e(new ffd_engine());
+  e->desc = *d;
+  e->device = d->device;
+  if (d->max_chunk_faces > 0) e->max_chunk = d->max_chunk_faces;
+  try {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+      return fail(nullptr, FFD_ERR_DEVICE, "no HIP device available (the engine has no CPU fallback)");
+    if (d->device < 0 || d->device >= ndev) return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "bad device ordinal");
+    HIP_CHECK(hipSetDevice(d->device));
+    HIP_CHECK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    e->load_model(d->model_path);
+    e->build_gabor();
+  } catch (const HipError& x) {
+    return fail(nullptr, FFD_ERR_DEVICE, x.what());
+  } catch (const std::exception& x) {
+    return fail(nullptr, FFD_ERR_MODEL, x.what());
+  }
+  *out = e.release();
+  return FFD_OK;
+}
+
+void ffd_engine_destroy(ffd_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  delete e;
+}
+
+const char* ffd_last_error(const ffd_engine* e) { return e ? e->err.c_str() : g_create_err.c_str(); }
+
+void* ffd_stream(ffd_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+ffd_status ffd_synchronize(ffd_engine* e) {
+  return guarded(e, [&] {
+    HIP_CHECK(hipStreamSynchronize(e->stream));
+    e->resolve();
+    return FFD_OK;
+  });
+}
+
+static const char* const kStageNames[FFD_NUM_STAGES] = {
+    "gray_resize", "gabor_25x25", "gabor_19x19", "gabor_13x13", "gabor_9x9", "gabor_7x7",
+    "integral_channels", "headpose_traverse", "headpose_reduce_select", "ffd_traverse", "votes_meanshift"};
+
+const char* ffd_stage_name(int32_t i) { return (i >= 0 && i < FFD_NUM_STAGES) ? kStageNames[i] : ""; }
+
+ffd_status ffd_set_profiling(ffd_engine* e, int32_t enable) {
+  return guarded(e, [&] {
+    e->resolve();
+    e->profiling = enable != 0;
+    for (int i = 0; i < FFD_NUM_STAGES; i++) { e->stage_ms[i] = 0; e->stage_n[i] = 0; }
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_get_stage_times(ffd_engine* e, double* ms, int64_t* launches, int32_t n) {
+  return guarded(e, [&] {
+    e->resolve();
+    for (int i = 0; i < n && i < FFD_NUM_STAGES; i++) {
+      if (ms) ms[i] = e->stage_ms[i];
+      if (launches) launches[i] = e->stage_n[i];
+    }
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_face_geometry(const ffd_engine* e, int32_t bw, int32_t bh, int32_t* fw, int32_t* fh, int32_t* nhp,
+                             int32_t* nmp) {
+  if (!e) return FFD_ERR_INVALID_ARGUMENT;
+  Geometry g = e->geometry(bw, bh);
+  if (g.W <= 0 || g.H <= 0) return FFD_ERR_INVALID_ARGUMENT;
+  if (fw) *fw = g.W;
+  if (fh) *fh = g.H;
+  if (nhp) *nhp = g.nhx * g.nhy;
+  if (nmp) *nmp = g.nmx * g.nmy;
+  return FFD_OK;
+}
+
+ffd_status ffd_analyze_faces(ffd_engine* e, const ffd_image* imgs, int32_t n_img, const ffd_rect* boxes,
+                             const int32_t* box_img, int32_t n_faces, ffd_face* out) {
+  return guarded(e, [&]() -> ffd_status {
+    if (n_faces < 0 || (n_faces > 0 && (!imgs || !boxes || !out)) || n_img < 0)
+      return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (!box_img && n_img != n_faces) return fail(e, FFD_ERR_INVALID_ARGUMENT, "box_img NULL requires n_img == n_faces");
+    if (n_faces == 0) return FFD_OK;
+    // pack the images into one device buffer
+    std::vector<int64_t> img_off(n_img);
+    int64_t total = 0;
+    for (int i = 0; i < n_img; i++) {
+      if (!imgs[i].bgr || imgs[i].width <= 0 || imgs[i].height <= 0 || imgs[i].stride < 3 * imgs[i].width)
+        return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad image " + std::to_string(i));
+      img_off[i] = total;
+      total += align_up((int64_t)imgs[i].stride * imgs[i].height, 256);
+    }
+    e->images.ensure(total);
+    for (int i = 0; i < n_img; i++)
+      HIP_CHECK(hipMemcpyAsync(e->images.as<uint8_t>() + img_off[i], imgs[i].bgr, (size_t)imgs[i].stride * imgs[i].height,
+                               hipMemcpyHostToDevice, e->stream));
+    std::vector<FaceDesc> fds(n_faces);
+    for (int i = 0; i < n_faces; i++) {
+      int k = box_img ? box_img[i] : i;
+      if (k < 0 || k >= n_img) return fail(e, FFD_ERR_INVALID_ARGUMENT, "box_img out of range");
+      make_desc(e, img_off[k], imgs[k].width, imgs[k].height, imgs[k].stride, boxes[i], fds[i]);
+    }
+    e->out.ensure((size_t)n_faces * sizeof(FaceOut));
+    e->analyze(e->images.as<uint8_t>(), fds, e->out.as<FaceOut>());
+    static_assert(sizeof(FaceOut) == sizeof(ffd_face), "FaceOut must mirror ffd_face");
+    HIP_CHECK(hipMemcpyAsync(out, e->out.p, (size_t)n_faces * sizeof(ffd_face), hipMemcpyDeviceToHost, e->stream));
+    HIP_CHECK(hipStreamSynchronize(e->stream));
+    for (int i = 0; i < n_faces; i++)
+      if (out[i].status != FFD_OK) out[i].status = FFD_ERR_INVALID_ARGUMENT;
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_analyze_faces_device(ffd_engine* e, const void* d_images, int64_t image_bytes, int32_t width,
+                                    int32_t height, int32_t stride, int32_t n_img, const ffd_rect* boxes,
+                                    const int32_t* box_img, int32_t n_faces, void* d_out) {
+  return guarded(e, [&]() -> ffd_status {
+    if (n_faces < 0 || (n_faces > 0 && (!d_images || !boxes || !d_out)) || width <= 0 || height <= 0 ||
+        stride < 3 * width || image_bytes < (int64_t)stride * height)
+      return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (!box_img && n_img != n_faces) return fail(e, FFD_ERR_INVALID_ARGUMENT, "box_img NULL requires n_img == n_faces");
+    std::vector<FaceDesc> fds(n_faces);
+    for (int i = 0; i < n_faces; i++) {
+      int k = box_img ? box_img[i] : i;
+      if (k < 0 || k >= n_img) return fail(e, FFD_ERR_INVALID_ARGUMENT, "box_img out of range");
+      make_desc(e, (int64_t)k * image_bytes, width, height, stride, boxes[i], fds[i]);
+    }
+    e->analyze(static_cast<const uint8_t*>(d_images), fds, static_cast<FaceOut*>(d_out));
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_get_trace(ffd_engine* e, int32_t index, ffd_trace* tr) {
+  return guarded(e, [&]() -> ffd_status {
+    if (!tr) return fail(e, FFD_ERR_INVALID_ARGUMENT, "trace is NULL");
+    const int k = index - e->last_first;
+    if (k < 0 || k >= e->last_count) return fail(e, FFD_ERR_INVALID_ARGUMENT, "index not in the last chunk");
+    const FaceDesc& f = e->last_desc[k];
+    if (!f.valid) return fail(e, FFD_ERR_INVALID_ARGUMENT, "face was rejected");
+    HIP_CHECK(hipStreamSynchronize(e->stream));
+    const int W = f.W, H = f.H;
+    if (tr->face)
+      HIP_CHECK(hipMemcpy2D(tr->face, W, e->gray.as<uint8_t>() + f.gray_off, PITCH, W, H, hipMemcpyDeviceToHost));
+    if (tr->channels)
+      for (int c = 0; c < NCH; c++)
+        HIP_CHECK(hipMemcpy2D(tr->channels + (size_t)c * (H + 1) * (W + 1), (W + 1) * 4,
+                              e->chan.as<uint32_t>() + f.ch_off + c * f.plane, PITCH * 4, (W + 1) * 4, H + 1,
+                              hipMemcpyDeviceToHost));
+    HpState hs;
+    HIP_CHECK(hipMemcpy(&hs, e->state.as<HpState>() + k, sizeof(hs), hipMemcpyDeviceToHost));
+    if (tr->hp_leaves) {
+      const int nh = f.nhx * f.nhy;
+      std::vector<int32_t> v((size_t)e->hp_trees * nh);
+      HIP_CHECK(hipMemcpy(v.data(), e->hpleaf.as<int32_t>() + f.hp_off, v.size() * 4, hipMemcpyDeviceToHost));
+      for (int xi = 0; xi < f.nhx; xi++)
+        for (int yi = 0; yi < f.nhy; yi++)
+          for (int t = 0; t < e->hp_trees; t++)
+            tr->hp_leaves[(xi * f.nhy + yi) * e->hp_trees + t] = v[(size_t)t * nh + yi * f.nhx + xi];
+    }
+    if (tr->mp_leaves) {
+      const int nm = f.nmx * f.nmy, T = hs.n_trees;
+      std::vector<int32_t> v((size_t)std::max(T, 1) * nm);
+      HIP_CHECK(hipMemcpy(v.data(), e->mpleaf.as<int32_t>() + f.mp_off, (size_t)T * nm * 4, hipMemcpyDeviceToHost));
+      for (int xi = 0; xi < f.nmx; xi++)
+        for (int yi = 0; yi < f.nmy; yi++)
+          for (int t = 0; t < T; t++) tr->mp_leaves[(xi * f.nmy + yi) * T + t] = v[(size_t)t * nm + yi * f.nmx + xi];
+    }
+    if (tr->trees)
+      for (int t = 0; t < MAX_TREES; t++) tr->trees[t] = t < hs.n_trees ? hs.trees[t] : -1;
+    if (tr->pose_freq)
+      for (int j = 0; j < 5; j++) tr->pose_freq[j] = j < e->n_forests ? hs.pose_freq[j] : 0.f;
+    if (tr->vote_counts)
+      HIP_CHECK(hipMemcpy(tr->vote_counts, e->vote_counts.as<int32_t>() + (size_t)k * NPARTS, NPARTS * 4,
+                          hipMemcpyDeviceToHost));
+    if (tr->ms_mean)
+      HIP_CHECK(hipMemcpy(tr->ms_mean, e->ms_mean.as<float>() + (size_t)k * NPARTS * 2, NPARTS * 2 * 4,
+                          hipMemcpyDeviceToHost));
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t W, int32_t H, uint32_t* out) {
+  return guarded(e, [&]() -> ffd_status {
+    if (!gray_face || !out || W < 2 || H < 2 || W > PITCH - 3 || H > MAX_FACE_H)
+      return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    // the face itself is the "image" (copy mode): one BGR image whose gray equals the input
+    std::vector<uint8_t> bgr((size_t)W * H * 3);
+    // BGR2GRAY of (v,v,v) is v: (1868+9617+4899)*v + 8192 >> 14 == v for v in [0,255]
+    for (int i = 0; i < W * H; i++) bgr[3 * i] = bgr[3 * i + 1] = bgr[3 * i + 2] = gray_face[i];
+    e->scratch_a.ensure(bgr.size());
+    HIP_CHECK(hipMemcpyAsync(e->scratch_a.p, bgr.data(), bgr.size(), hipMemcpyHostToDevice, e->stream));
+    FaceDesc f;
+    std::memset(&f, 0, sizeof(f));
+    f.img_w = W; f.img_h = H; f.img_stride = 3 * W; f.bw = W; f.bh = H; f.W = W; f.H = H;
+    f.scale = 1.f; f.mode = 0; f.valid = 1;
+    f.plane = (int64_t)(H + 1) * PITCH;
+    e->gray.ensure((size_t)H * PITCH + 256);
+    e->mag.ensure((size_t)NGABOR * H * PITCH * 4 + 256);
+    e->chan.ensure((size_t)NCH * f.plane * 4 + 256);
+    e->minmax.ensure(NGABOR * 2 * 4);
+    std::vector<FaceDesc> one{f};
+    upload(e->faces, one, e->stream);
+    HIP_CHECK(hipMemsetAsync(e->minmax.p, 0xFF, NGABOR * 2 * 4, e->stream));
+    const FaceDesc* dfd = e->faces.as<FaceDesc>();
+    launch_gray_resize(dfd, 1, e->scratch_a.as<uint8_t>(), e->gray.as<uint8_t>(), e->stream);
+    for (int nu = 4; nu >= 0; nu--)
+      launch_gabor(nu, dfd, 1, W, H, e->gray.as<uint8_t>(), e->mag.as<float>(), e->minmax.as<uint32_t>(), e->stream);
+    launch_integral(dfd, 1, e->gray.as<uint8_t>(), e->mag.as<float>(), e->minmax.as<uint32_t>(), e->chan.as<uint32_t>(),
+                    e->stream);
+    HIP_CHECK(hipGetLastError());
+    for (int c = 0; c < NCH; c++)
+      HIP_CHECK(hipMemcpy2DAsync(out + (size_t)c * (H + 1) * (W + 1), (W + 1) * 4, e->chan.as<uint32_t>() + c * f.plane,
+                                 PITCH * 4, (W + 1) * 4, H + 1, hipMemcpyDeviceToHost, e->stream));
+    HIP_CHECK(hipStreamSynchronize(e->stream));
+    e->last_count = 0;  // workspace no longer holds a batch
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* channels, int32_t W, int32_t H,
+                                  const int32_t* patches_xy, int32_t n_patches, const int32_t* tree_ids, int32_t n_trees,
+                                  int32_t* leaf_ids) {
+  return guarded(e, [&]() -> ffd_status {
+    if (!channels || (!patches_xy && n_patches) || (!tree_ids && n_trees) || (!leaf_ids && n_patches * n_trees) ||
+        W < 1 || H < 1 || W > PITCH - 3 || H > MAX_FACE_H || n_patches < 0 || n_trees < 0)
+      return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (kind != FFD_FOREST_HEADPOSE && kind != FFD_FOREST_FFD) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad forest kind");
+    const int ntot = kind == FFD_FOREST_HEADPOSE ? e->hp_trees : e->n_forests * e->ntrees_per_forest;
+    for (int t = 0; t < n_trees; t++)
+      if (tree_ids[t] < 0 || tree_ids[t] >= ntot) return fail(e, FFD_ERR_INVALID_ARGUMENT, "tree id out of range");
+    for (int p = 0; p < n_patches; p++) {
+      const int x = patches_xy[2 * p], y = patches_xy[2 * p + 1];
+      if (x < 0 || y < 0 || x + e->patch > W || y + e->patch > H)
+        return fail(e, FFD_ERR_INVALID_ARGUMENT, "patch outside the image sample");
+    }
+    if (n_patches == 0 || n_trees == 0) return FFD_OK;
+    const int64_t plane = (int64_t)(H + 1) * PITCH;
+    e->scratch_a.ensure((size_t)NCH * plane * 4);
+    for (int c = 0; c < NCH; c++)
+      HIP_CHECK(hipMemcpy2DAsync(e->scratch_a.as<uint32_t>() + c * plane, PITCH * 4, channels + (size_t)c * (H + 1) * (W + 1),
+                                 (W + 1) * 4, (W + 1) * 4, H + 1, hipMemcpyHostToDevice, e->stream));
+    std::vector<int32_t> pv(patches_xy, patches_xy + 2 * n_patches), tv(tree_ids, tree_ids + n_trees);
+    upload(e->scratch_b, pv, e->stream);
+    upload(e->scratch_c, tv, e->stream);
+    DevBuf outb;
+    outb.ensure((size_t)n_patches * n_trees * 4);
+    const bool hp = kind == FFD_FOREST_HEADPOSE;
+    launch_eval_patches(hp ? e->hp_nodes.as<uint4>() : e->mp_nodes.as<uint4>(),
+                        hp ? e->hp_roots.as<int32_t>() : e->mp_roots.as<int32_t>(), e->scratch_c.as<int32_t>(), n_trees,
+                        e->scratch_b.as<int32_t>(), n_patches, e->scratch_a.as<uint32_t>(), plane, outb.as<int32_t>(),
+                        e->stream);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(leaf_ids, outb.p, (size_t)n_patches * n_trees * 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_CHECK(hipStreamSynchronize(e->stream));
+    return FFD_OK;
+  });
+}
+
+}  // extern "C"

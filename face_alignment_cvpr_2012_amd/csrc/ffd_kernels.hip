@@ -1,0 +1,584 @@
+// ffd_kernels.hip — CDNA4 (gfx950) kernels of the analyzeFace hot path.
+//
+// Compiled with -ffp-contract=off: every float/double expression rounds exactly
+// as written (explicit fmaf() only where the restatement defines a fused op), so
+// the results are bit-identical to the CPU restatement in oracle/.
+//
+// Kernel map (reference -> kernel):
+//   cvtColor + ROI + resize      FaceForest.cpp:195-204              k_gray_resize
+//   Gabor filter2D + magnitude   FeatureChannelFactory.hpp:253-270   k_gabor<W>
+//   normalize/convertTo/integral FeatureChannelFactory.hpp:271-286,  k_integral (+ gray, Sobel
+//                                46-57, 120-141                       channels fused in)
+//   Forest::evaluateMT           Forest.hpp:80-90, Tree.hpp:173-191,  k_traverse<HP/FFD>
+//                                ImageSample.cpp:48-63
+//   head-pose reduction + tree   face_utils.cpp:218-241,304-323,      k_hp_pose
+//   selection                    FaceForest.cpp:214-250
+//   vote filter + MeanShift      face_utils.cpp:276-301,              k_votes_meanshift
+//                                MeanShift.hpp:41-135, FaceForest.cpp:255-257
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/ffd_numerics.h"
+#include "ffd_device.hpp"
+#include "ffd_kernels.hpp"
+
+namespace ffd {
+
+// ----------------------------------------------------------------- helpers --
+__device__ __forceinline__ int reflect101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) {
+    if (i < 0) i = -i;
+    if (i >= n) i = 2 * n - 2 - i;
+  }
+  return i;
+}
+
+__device__ __forceinline__ int sat_u8(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+__device__ __forceinline__ int sat_s16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+
+// cvRound(float): round half to even, NaN / out of range -> INT_MIN (cvtss2si).
+__device__ __forceinline__ int cv_round(float v) {
+  if (!(v >= -2147483648.0f && v < 2147483648.0f)) return (int)0x80000000;
+  return (int)__builtin_rintf(v);
+}
+
+__device__ __forceinline__ uint8_t gray_px(const uint8_t* p) {  // BGR2GRAY, yuv_shift 14
+  return (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14);
+}
+
+// Map a dispatch block index to a logical block so that every XCD (blocks are dealt
+// round-robin over the 8 XCDs) works on a contiguous logical range: consecutive
+// faces' data then shares one XCD's L2.  Speed only, never correctness.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
+  uint32_t xcd = b & 7u, q = nb >> 3, r = nb & 7u;
+  uint32_t start = xcd * q + (xcd < r ? xcd : r);
+  return start + (b >> 3);
+}
+
+// ------------------------------------------------------ gray + ROI + resize --
+// One workgroup per face; OpenCV 2.4.9 resize(INTER_LINEAR) 8U fixed-point path
+// (HResizeLinear + VResizeLinearVec_32s8u SSE2 columns [0, xv) + scalar tail).
+__global__ __launch_bounds__(256) void k_gray_resize(const FaceDesc* __restrict__ faces,
+                                                     const uint8_t* __restrict__ images,
+                                                     uint8_t* __restrict__ gray) {
+  const FaceDesc fd = faces[blockIdx.x];
+  if (!fd.valid) return;
+  const uint8_t* img = images + fd.img_off;
+  uint8_t* out = gray + fd.gray_off;
+  auto G = [&](int y, int x) -> int {
+    return gray_px(img + (int64_t)(fd.by + y) * fd.img_stride + 3 * (fd.bx + x));
+  };
+  const int sw = fd.bw, sh = fd.bh;
+  for (int i = threadIdx.x; i < fd.W * fd.H; i += blockDim.x) {
+    int dy = i / fd.W, dx = i % fd.W;
+    int v;
+    if (fd.mode == 0) {
+      v = G(dy, dx);
+    } else if (fd.mode == 2) {
+      v = (G(2 * dy, 2 * dx) + G(2 * dy, 2 * dx + 1) + G(2 * dy + 1, 2 * dx) + G(2 * dy + 1, 2 * dx + 1) + 2) >> 2;
+    } else {
+      float fx = (float)((dx + 0.5) * fd.scale_x - 0.5);
+      int sx = (int)floorf(fx);
+      fx -= sx;
+      if (sx < 0) fx = 0, sx = 0;
+      bool right = false;
+      if (sx + 1 >= sw) {
+        right = true;
+        if (sx >= sw - 1) fx = 0, sx = sw - 1;
+      }
+      int a0 = sat_s16(cv_round((1.f - fx) * 2048.f)), a1 = sat_s16(cv_round(fx * 2048.f));
+      float fy = (float)((dy + 0.5) * fd.scale_y - 0.5);
+      int sy = (int)floorf(fy);
+      fy -= sy;
+      int b0 = sat_s16(cv_round((1.f - fy) * 2048.f)), b1 = sat_s16(cv_round(fy * 2048.f));
+      int y0 = min(max(sy, 0), sh - 1), y1 = min(max(sy + 1, 0), sh - 1);
+      int r0, r1;
+      if (right) {
+        r0 = G(y0, sx) * 2048;
+        r1 = G(y1, sx) * 2048;
+      } else {
+        r0 = G(y0, sx) * a0 + G(y0, sx + 1) * a1;
+        r1 = G(y1, sx) * a0 + G(y1, sx + 1) * a1;
+      }
+      if (dx < fd.xv) {
+        int s0 = max(-32768, min(32767, r0 >> 4)), s1 = max(-32768, min(32767, r1 >> 4));
+        int m = max(-32768, min(32767, ((s0 * b0) >> 16) + ((s1 * b1) >> 16)));
+        m = max(-32768, min(32767, m + 2)) >> 2;
+        v = sat_u8(m);
+      } else {
+        v = sat_u8((b0 * r0 + b1 * r1 + (1 << 21)) >> 22);
+      }
+    }
+    out[dy * PITCH + dx] = (uint8_t)v;
+  }
+}
+
+// ------------------------------------------------------------------ Gabor --
+// Coefficients (host-built from createKernel, FeatureChannelFactory.hpp:186-251):
+//   scale 0 (7x7): [49 taps row-major][7 re | 7 im]
+//   scale >= 1   : [half pairs][7 re | 7 im], then [7 re centre]
+__constant__ float c_gabor[GABOR_COEF_TOTAL];
+
+template <int W> struct GaborCfg;
+template <> struct GaborCfg<7>  { static constexpr int nu = 0, off = GABOR_OFF0; };
+template <> struct GaborCfg<9>  { static constexpr int nu = 1, off = GABOR_OFF1; };
+template <> struct GaborCfg<13> { static constexpr int nu = 2, off = GABOR_OFF2; };
+template <> struct GaborCfg<19> { static constexpr int nu = 3, off = GABOR_OFF3; };
+template <> struct GaborCfg<25> { static constexpr int nu = 4, off = GABOR_OFF4; };
+
+// One workgroup = one 16x16 output tile of one face for the 7 orientations of one
+// scale.  Pixel pair sums S/D are shared by the 7 orientations (the point symmetry
+// of the Gabor kernels), halving the FMAs of a direct correlation.
+template <int W>
+__global__ __launch_bounds__(256) void k_gabor(const FaceDesc* __restrict__ faces,
+                                               const uint8_t* __restrict__ gray,
+                                               float* __restrict__ mag,
+                                               uint32_t* __restrict__ minmax) {
+  constexpr int R = (W - 1) / 2, TS = 16, LW = 48, TW = TS + 2 * R;
+  constexpr int NU = GaborCfg<W>::nu, OFF = GaborCfg<W>::off;
+  __shared__ float tile[TW * LW];
+  __shared__ uint32_t red[4][14];
+  const FaceDesc fd = faces[blockIdx.y];
+  if (!fd.valid) return;
+  const int tiles_x = (fd.W + TS - 1) / TS;
+  const int tx0 = (blockIdx.x % tiles_x) * TS, ty0 = (blockIdx.x / tiles_x) * TS;
+  if (ty0 >= fd.H) return;  // grid is sized for the batch's tallest face
+  const uint8_t* g = gray + fd.gray_off;
+  for (int i = threadIdx.x; i < TW * TW; i += 256) {
+    int ly = i / TW, lx = i % TW;
+    int y = reflect101(ty0 - R + ly, fd.H), x = reflect101(tx0 - R + lx, fd.W);
+    tile[ly * LW + lx] = (float)g[y * PITCH + x];
+  }
+  __syncthreads();
+  const int lx = threadIdx.x & 15, ly = threadIdx.x >> 4;
+  const float* base = &tile[(ly + R) * LW + lx + R];
+  float re[7], im[7];
+#pragma unroll
+  for (int o = 0; o < 7; o++) re[o] = im[o] = 0.f;
+  if constexpr (W == 7) {
+    // OpenCV Filter2D direct path: s = 0; s += k*p over taps in row-major order.
+#pragma unroll 7
+    for (int t = 0; t < 49; t++) {
+      const float p = base[(t / 7 - 3) * LW + (t % 7 - 3)];
+#pragma unroll
+      for (int o = 0; o < 7; o++) {
+        re[o] = re[o] + c_gabor[OFF + t * 14 + o] * p;
+        im[o] = im[o] + c_gabor[OFF + t * 14 + 7 + o] * p;
+      }
+    }
+  } else {
+    constexpr int HALF = (W * W - 1) / 2;
+#pragma unroll 4
+    for (int t = 0; t < HALF; t++) {
+      const int dy = t / W - R, dx = t % W - R;
+      const float a = base[dy * LW + dx], b = base[-dy * LW - dx];
+      const float S = a + b, D = a - b;
+#pragma unroll
+      for (int o = 0; o < 7; o++) {
+        re[o] = fmaf(c_gabor[OFF + t * 14 + o], S, re[o]);
+        im[o] = fmaf(c_gabor[OFF + t * 14 + 7 + o], D, im[o]);
+      }
+    }
+    const float p0 = base[0];
+#pragma unroll
+    for (int o = 0; o < 7; o++) re[o] = fmaf(c_gabor[OFF + HALF * 14 + o], p0, re[o]);
+  }
+  const int x = tx0 + lx, y = ty0 + ly;
+  const bool in = x < fd.W && y < fd.H;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t mn[7], mx[7];
+#pragma unroll
+  for (int o = 0; o < 7; o++) {
+    const float i2 = im[o] * im[o], r2 = re[o] * re[o];
+    const float m = __builtin_sqrtf(i2 + r2);
+    if (in) mag[fd.mag_off + ((int64_t)(NU * 7 + o) * fd.H + y) * PITCH + x] = m;
+    // m >= +0, so unsigned order == float order; the max is kept as min(~bits) so one
+    // atomicMin per slot serves both and the table is initialised to all-ones.
+    uint32_t bits = __float_as_uint(m);
+    mn[o] = in ? bits : 0xFFFFFFFFu;
+    mx[o] = in ? ~bits : 0xFFFFFFFFu;
+  }
+#pragma unroll
+  for (int o = 0; o < 7; o++) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+      mn[o] = min(mn[o], (uint32_t)__shfl_xor((int)mn[o], s));
+      mx[o] = min(mx[o], (uint32_t)__shfl_xor((int)mx[o], s));
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int o = 0; o < 7; o++) { red[wv][o] = mn[o]; red[wv][7 + o] = mx[o]; }
+  }
+  __syncthreads();
+  if (threadIdx.x < 14) {
+    int k = threadIdx.x;
+    uint32_t v = red[0][k];
+    for (int w = 1; w < 4; w++) v = min(v, red[w][k]);
+    uint32_t* slot = minmax + ((int64_t)blockIdx.y * NGABOR + NU * 7 + (k % 7)) * 2;
+    atomicMin(slot + (k < 7 ? 0 : 1), v);
+  }
+}
+
+// ---------------------------------------------------------------- integral --
+// One wave per (face, channel): the wave walks the rows top to bottom; lane l owns
+// columns 2l, 2l+1, keeps their running column sums and a 64-lane prefix scan turns
+// them into integral-image rows.  Integer-exact, so order does not matter.
+__device__ __forceinline__ int chan_value(int c, const uint8_t* g, const float* m, int W, int H, int y, int x,
+                                          float sf, float hf) {
+  if (x >= W) return 0;
+  if (c == 0) return g[y * PITCH + x];
+  if (c <= NGABOR) {
+    float v = m[y * PITCH + x] * sf + hf;  // normalize: v*scale + shift (float, no FMA)
+    return sat_u8(cv_round(v * 255.f + 0.f));
+  }
+  int ym = reflect101(y - 1, H), yp = reflect101(y + 1, H), xm = reflect101(x - 1, W), xp = reflect101(x + 1, W);
+  auto I = [&](int yy, int xx) { return (int)g[yy * PITCH + xx]; };
+  int v;
+  if (c == 36)  // Sobel(0,1): d/dy
+    v = (I(yp, xm) + 2 * I(yp, x) + I(yp, xp)) - (I(ym, xm) + 2 * I(ym, x) + I(ym, xp));
+  else          // Sobel(1,0): d/dx
+    v = (I(ym, xp) + 2 * I(y, xp) + I(yp, xp)) - (I(ym, xm) + 2 * I(y, xm) + I(yp, xm));
+  return sat_u8(v);
+}
+
+__global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ faces,
+                                                  const uint8_t* __restrict__ gray,
+                                                  const float* __restrict__ mag,
+                                                  const uint32_t* __restrict__ minmax,
+                                                  uint32_t* __restrict__ chan) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const FaceDesc fd = faces[blockIdx.y];
+  if (!fd.valid || c >= NCH) return;
+  const int W = fd.W, H = fd.H;
+  const uint8_t* g = gray + fd.gray_off;
+  const float* m = mag + fd.mag_off + (c >= 1 && c <= NGABOR ? (int64_t)(c - 1) * H * PITCH : 0);
+  float sf = 0.f, hf = 0.f;
+  if (c >= 1 && c <= NGABOR) {
+    // cv::normalize(NORM_MINMAX, 0, 1) -> convertTo(scale, shift) (OpenCV 2.4.9)
+    const uint32_t* mm = minmax + ((int64_t)blockIdx.y * NGABOR + (c - 1)) * 2;
+    double smin = (double)__uint_as_float(mm[0]), smax = (double)__uint_as_float(~mm[1]);
+    double dmin = 0, dmax = 1;
+    double scale = (dmax - dmin) * (smax - smin > 2.220446049250313e-16 ? 1. / (smax - smin) : 0);
+    double shift = dmin - smin * scale;
+    sf = (float)scale;
+    hf = (float)shift;
+  }
+  uint32_t* out = chan + fd.ch_off + (int64_t)c * fd.plane;
+  const int x0 = 2 * lane, x1 = 2 * lane + 1;
+  // row 0 of the integral image is zero
+  for (int x = lane; x <= W; x += 64) out[x] = 0;
+  uint32_t c0 = 0, c1 = 0;
+  for (int y = 0; y < H; y++) {
+    c0 += (uint32_t)chan_value(c, g, m, W, H, y, x0, sf, hf);
+    c1 += (uint32_t)chan_value(c, g, m, W, H, y, x1, sf, hf);
+    uint32_t s = c0 + c1, incl = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+      if (lane >= d) incl += o;
+    }
+    uint32_t excl = incl - s;
+    uint32_t* row = out + (int64_t)(y + 1) * PITCH;
+    if (lane == 0) row[0] = 0;
+    if (x0 + 1 <= W) row[x0 + 1] = excl + c0;
+    if (x1 + 1 <= W) row[x1 + 1] = excl + c0 + c1;
+  }
+}
+
+// --------------------------------------------------------------- traversal --
+// ImageSample::evalTest integral branch (ImageSample.cpp:48-63): p = (int)(R / (float)area)
+// equals the integer quotient for R in [0, 255*484] (tests/test_numerics.py checks all
+// pairs); computed as rcp estimate + one integer correction step.
+__device__ __forceinline__ int rect_mean(const uint32_t* __restrict__ I, uint32_t off, int w, int h) {
+  const uint32_t a = I[off], b = I[off + w], c = I[off + h * PITCH], d = I[off + h * PITCH + w];
+  const int R = (int)(d - b - c + a);
+  const int area = w * h;
+  int q = (int)((float)R * __builtin_amdgcn_rcpf((float)area));
+  const int r = R - q * area;
+  q += (r >= area) ? 1 : 0;
+  q -= (r < 0) ? 1 : 0;
+  return q;
+}
+
+// Tree<S>::evaluateMT: walk from `node` to a leaf; TreeNode::eval -> (test <= threshold) -> left.
+__device__ __forceinline__ uint32_t walk(const uint4* __restrict__ nodes, uint32_t node,
+                                         const uint32_t* __restrict__ chan, int64_t plane) {
+  uint4 nd = nodes[node];
+  while (!(nd.x & LEAF_BIT)) {
+    const uint32_t* I = chan + (int64_t)(nd.y & 63u) * plane;
+    const int p1 = rect_mean(I, nd.w & 0xFFFFu, (nd.y >> 6) & 31u, (nd.y >> 11) & 31u);
+    const int p2 = rect_mean(I, nd.w >> 16, (nd.y >> 16) & 31u, (nd.y >> 21) & 31u);
+    node = nd.x + ((p1 - p2) <= (int)nd.z ? 0u : 1u);
+    nd = nodes[node];
+  }
+  return nd.x & ~LEAF_BIT;
+}
+
+// One wave = 64 patches (lane order) x one tree of one face.  Wave ids are laid out
+// face-major, then tree slot, then patch chunk; wave_start[f] is the first wave of f.
+template <bool HP>
+__global__ __launch_bounds__(256) void k_traverse(const FaceDesc* __restrict__ faces,
+                                                  const int64_t* __restrict__ wave_start, int n_faces,
+                                                  int64_t total_waves, const uint4* __restrict__ nodes,
+                                                  const int32_t* __restrict__ roots,
+                                                  const HpState* __restrict__ hp_state, int tslots, int step,
+                                                  const uint32_t* __restrict__ chan,
+                                                  int32_t* __restrict__ leaf_out) {
+  const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t wave = (int64_t)lb * 4 + (threadIdx.x >> 6);
+  if (wave >= total_waves) return;
+  int lo = 0, hi = n_faces - 1;
+  while (lo < hi) {  // last f with wave_start[f] <= wave
+    int mid = (lo + hi + 1) >> 1;
+    if (wave_start[mid] <= wave) lo = mid; else hi = mid - 1;
+  }
+  const int f = lo;
+  const FaceDesc& fd = faces[f];
+  const int nx = HP ? fd.nhx : fd.nmx, ny = HP ? fd.nhy : fd.nmy, n = nx * ny;
+  const int chunks = (n + 63) >> 6;
+  const int local = (int)(wave - wave_start[f]);
+  const int t = local / chunks, ck = local % chunks;
+  const int q = ck * 64 + (threadIdx.x & 63);
+  if (q >= n) return;
+  int tree;
+  if (HP) {
+    tree = t;
+  } else {
+    if (t >= hp_state[f].n_trees) return;
+    tree = hp_state[f].trees[t];
+  }
+  const int px = (q % nx) * step, py = (q / nx) * step;
+  const uint32_t* I = chan + fd.ch_off + py * PITCH + px;
+  const uint32_t leaf = walk(nodes, (uint32_t)roots[tree], I, fd.plane);
+  leaf_out[(HP ? fd.hp_off : fd.mp_off) + (int64_t)t * n + q] = (int32_t)leaf;
+  (void)tslots;
+}
+
+// Forest<S>::evaluateMT over an explicit patch list (ffd_forest_eval_leaves hook).
+__global__ void k_eval_patches(const uint4* __restrict__ nodes, const int32_t* __restrict__ roots,
+                               const int32_t* __restrict__ tree_ids, int n_trees,
+                               const int32_t* __restrict__ patches, int n_patches,
+                               const uint32_t* __restrict__ chan, int64_t plane,
+                               int32_t* __restrict__ leaf_ids) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_patches * n_trees) return;
+  const int p = i / n_trees, t = i % n_trees;
+  const uint32_t* I = chan + patches[2 * p + 1] * PITCH + patches[2 * p];
+  leaf_ids[i] = (int32_t)walk(nodes, (uint32_t)roots[tree_ids[t]], I, plane);
+}
+
+// -------------------------------------------------- head pose + tree choice --
+// getHeadPoseVotesMT reduction (face_utils.cpp:218-241), sequential in the reference
+// (patch-major, tree-minor) order; then areaUnderCurve (face_utils.cpp:304-323) and the
+// tree selection of FaceForest.cpp:214-250.  One thread per face.
+__global__ void k_hp_pose(const FaceDesc* __restrict__ faces, int n_faces, const int32_t* __restrict__ hp_leaf,
+                          const float* __restrict__ hp_m, int hp_trees, int n_forests, int ntrees_per_forest,
+                          HpState* __restrict__ state, FaceOut* __restrict__ out) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n_faces) return;
+  const FaceDesc& fd = faces[f];
+  FaceOut& o = out[f];
+  o.bbox[0] = fd.bx; o.bbox[1] = fd.by; o.bbox[2] = fd.bw; o.bbox[3] = fd.bh;
+  if (!fd.valid) {
+    o.status = 1;
+    o.n_trees = 0;
+    state[f].n_trees = 0;
+    return;
+  }
+  o.status = 0;
+  const int nx = fd.nhx, ny = fd.nhy, n = nx * ny;
+  const int32_t* L = hp_leaf + fd.hp_off;
+  float cnt = 0, sum = 0, sum_sq = 0;
+  for (int xi = 0; xi < nx; xi++)
+    for (int yi = 0; yi < ny; yi++) {
+      const int q = yi * nx + xi;
+      for (int t = 0; t < hp_trees; t++) {
+        const float m = hp_m[L[(int64_t)t * n + q]];
+        if (m >= 0.f) {
+          sum += m;
+          sum_sq += m * m;
+          cnt++;
+        }
+      }
+    }
+  float mean = sum / cnt;
+  float var = (sum_sq / cnt) - (mean * mean);
+  mean -= 2;
+  var *= 0.05f;  // NORM_HEADPOSE_VARIANCE_FACTOR
+  o.headpose = mean;
+  o.pose_variance = var;
+  HpState& s = state[f];
+  s.headpose = mean;
+  s.variance = var;
+  const float poseT[6] = {-2.5f, -0.35f, -0.20f, 0.20f, 0.35f, 2.5f};
+  const double dmean = (double)mean, dstd = __builtin_sqrt((double)var);
+  float max_area = 0;
+  int dominant = 0;
+  for (int j = 0; j < n_forests; j++) {
+    double acc = 0, step = 0.01, tt;
+    for (double x = poseT[j]; x < (double)poseT[j + 1]; x += step) {
+      tt = (x - dmean) / dstd;
+      acc += ffd_exp(-0.5 * (tt * tt)) * step;
+    }
+    const float area = (float)(acc * 1.0 / (dstd * 2.5066282746310002));
+    s.pose_freq[j] = area;
+    if (max_area < area) { max_area = area; dominant = j; }
+  }
+  int nt_total = 0;
+  for (int i = 0; i < n_forests; i++) {
+    const float v = floorf(s.pose_freq[i] * (float)ntrees_per_forest);
+    int k = (v > -2147483649.0f && v < 2147483648.0f) ? (int)v : (int)0x80000000;
+    k = min(k, ntrees_per_forest);
+    for (int j = 0; j < k && nt_total < MAX_TREES; j++) s.trees[nt_total++] = i * ntrees_per_forest + j;
+  }
+  for (int i = nt_total; i < ntrees_per_forest; i++) s.trees[nt_total++] = dominant * ntrees_per_forest + i;
+  s.n_trees = nt_total;
+  o.n_trees = nt_total;
+}
+
+// ----------------------------------------------------- votes + MeanShift ----
+// One thread per (face, landmark).  Pass 1 walks the FFD leaves in reference order
+// (patch-major x-outer, tree-minor; face_utils.cpp:277-301), compacts the landmark's
+// votes and accumulates MeanShift::getMean in the same order; then up to
+// max_iterations getWeightedMean passes (MeanShift.hpp:41-76,106-135).
+__global__ void k_votes_meanshift(const FaceDesc* __restrict__ faces, int n_faces,
+                                  const int32_t* __restrict__ mp_leaf, const uint32_t* __restrict__ mask,
+                                  const float* __restrict__ fg, const int32_t* __restrict__ offs,
+                                  const HpState* __restrict__ state, int tslots, int step, int half_patch,
+                                  int n_parts, float lamda, int max_iter, float stop, Vote* __restrict__ votes,
+                                  float* __restrict__ ms_mean, int32_t* __restrict__ vote_counts,
+                                  FaceOut* __restrict__ out) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int f = gid / NPARTS, part = gid % NPARTS;
+  if (f >= n_faces) return;
+  const FaceDesc& fd = faces[f];
+  if (!fd.valid) return;
+  if (part >= n_parts) {
+    out[f].points[part][0] = 0;
+    out[f].points[part][1] = 0;
+    return;
+  }
+  const int nx = fd.nmx, ny = fd.nmy, n = nx * ny, T = state[f].n_trees;
+  const int32_t* L = mp_leaf + fd.mp_off;
+  Vote* V = votes + fd.vote_off + (int64_t)part * tslots * n;
+  int cnt = 0;
+  float mx = 0, my = 0, sw = 0;
+  const uint32_t bit = 1u << part;
+  for (int xi = 0; xi < nx; xi++)
+    for (int yi = 0; yi < ny; yi++) {
+      const int q = yi * nx + xi;
+      const int ox = xi * step + half_patch, oy = yi * step + half_patch;
+      for (int t = 0; t < T; t++) {
+        const int leaf = L[(int64_t)t * n + q];
+        if (mask[leaf] & bit) {
+          const int32_t o = offs[(int64_t)leaf * NPARTS + part];
+          const int vx = (int)(int16_t)(o & 0xFFFF) + ox, vy = (int)(int16_t)(o >> 16) + oy;
+          const float w = fg[leaf];
+          V[cnt++] = Vote{(int16_t)vx, (int16_t)vy, w};
+          mx += vx * w;
+          my += vy * w;
+          sw += w;
+        }
+      }
+    }
+  if (sw > 0) { mx /= sw; my /= sw; }
+  bool conv = false;
+  for (int it = 0; it < max_iter && !conv; it++) {
+    float sx = 0, sy = 0, s = 0;
+    for (int k = 0; k < cnt; k++) {
+      const Vote v = V[k];
+      const float dx = mx - (float)v.x, dy = my - (float)v.y;
+      float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
+      d = ffd_expf(-d / lamda);
+      const float w = v.w * d;
+      sx += v.x * w;
+      sy += v.y * w;
+      s += w;
+    }
+    if (s > 0) { sx /= s; sy /= s; }
+    const float ddx = sx - mx, ddy = sy - my;
+    if (__builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) conv = true;
+    mx = sx;
+    my = sy;
+  }
+  ms_mean[((int64_t)f * NPARTS + part) * 2] = mx;
+  ms_mean[((int64_t)f * NPARTS + part) * 2 + 1] = my;
+  vote_counts[(int64_t)f * NPARTS + part] = cnt;
+  const float inv = 1.0f / fd.scale;  // FaceForest.cpp:255-257
+  out[f].points[part][0] = cv_round((float)cv_round(mx) * inv);
+  out[f].points[part][1] = cv_round((float)cv_round(my) * inv);
+}
+
+// ------------------------------------------------------------------ launch --
+hipError_t upload_gabor(const float* coef, hipStream_t s) {
+  return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_gabor), coef, sizeof(float) * GABOR_COEF_TOTAL, 0,
+                                hipMemcpyHostToDevice, s);
+}
+
+void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s) {
+  k_gray_resize<<<n, 256, 0, s>>>(faces, images, gray);
+}
+
+void launch_gabor(int nu, const FaceDesc* faces, int n, int max_w, int max_h, const uint8_t* gray, float* mag,
+                  uint32_t* minmax, hipStream_t s) {
+  const int tiles = ((max_w + 15) / 16) * ((max_h + 15) / 16);
+  if (tiles <= 0 || n <= 0) return;
+  dim3 grid(tiles, n);
+  switch (nu) {
+    case 4: k_gabor<25><<<grid, 256, 0, s>>>(faces, gray, mag, minmax); break;
+    case 3: k_gabor<19><<<grid, 256, 0, s>>>(faces, gray, mag, minmax); break;
+    case 2: k_gabor<13><<<grid, 256, 0, s>>>(faces, gray, mag, minmax); break;
+    case 1: k_gabor<9><<<grid, 256, 0, s>>>(faces, gray, mag, minmax); break;
+    default: k_gabor<7><<<grid, 256, 0, s>>>(faces, gray, mag, minmax); break;
+  }
+}
+
+void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, const float* mag, const uint32_t* minmax,
+                     uint32_t* chan, hipStream_t s) {
+  dim3 grid((NCH + 3) / 4, n);
+  k_integral<<<grid, 256, 0, s>>>(faces, gray, mag, minmax, chan);
+}
+
+void launch_traverse(bool hp, const FaceDesc* faces, const int64_t* wave_start, int n, int64_t total_waves,
+                     const uint4* nodes, const int32_t* roots, const HpState* state, int tslots, int step,
+                     const uint32_t* chan, int32_t* leaf_out, hipStream_t s) {
+  if (total_waves <= 0) return;
+  const unsigned blocks = (unsigned)((total_waves + 3) / 4);
+  if (hp)
+    k_traverse<true><<<blocks, 256, 0, s>>>(faces, wave_start, n, total_waves, nodes, roots, state, tslots, step,
+                                            chan, leaf_out);
+  else
+    k_traverse<false><<<blocks, 256, 0, s>>>(faces, wave_start, n, total_waves, nodes, roots, state, tslots, step,
+                                             chan, leaf_out);
+}
+
+void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
+                         const int32_t* patches, int n_patches, const uint32_t* chan, int64_t plane,
+                         int32_t* leaf_ids, hipStream_t s) {
+  const int total = n_patches * n_trees;
+  if (total <= 0) return;
+  k_eval_patches<<<(total + 255) / 256, 256, 0, s>>>(nodes, roots, tree_ids, n_trees, patches, n_patches, chan,
+                                                     plane, leaf_ids);
+}
+
+void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const float* hp_m, int hp_trees,
+                    int n_forests, int ntrees_per_forest, HpState* state, FaceOut* out, hipStream_t s) {
+  k_hp_pose<<<(n + 63) / 64, 64, 0, s>>>(faces, n, hp_leaf, hp_m, hp_trees, n_forests, ntrees_per_forest, state,
+                                         out);
+}
+
+void launch_votes_meanshift(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint32_t* mask,
+                            const float* fg, const int32_t* offs, const HpState* state, int tslots, int step,
+                            int half_patch, int n_parts, float lamda, int max_iter, float stop, Vote* votes,
+                            float* ms_mean, int32_t* vote_counts, FaceOut* out, hipStream_t s) {
+  const int total = n * NPARTS;
+  k_votes_meanshift<<<(total + 63) / 64, 64, 0, s>>>(faces, n, mp_leaf, mask, fg, offs, state, tslots, step,
+                                                     half_patch, n_parts, lamda, max_iter, stop, votes, ms_mean,
+                                                     vote_counts, out);
+}
+
+}  // namespace ffd

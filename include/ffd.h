@@ -1,0 +1,182 @@
+/*
+ * ffd.h — C-ABI of the MI355X conditional-regression-forest facial-landmark
+ * engine (drop-in for the reference's FaceForest::analyzeFace hot path).
+ *
+ * Every entry point replaces a reference interface (paths relative to
+ * /root/reference):
+ *
+ *   ffd_engine_create      FaceForest::FaceForest(FaceForestOptions)      src/FaceForest.cpp:15-58
+ *                          (+ Forest<S>::load, include/Forest.hpp:103-153)
+ *   ffd_analyze_faces      FaceForest::analyzeFace(img, bbox, Face&) per  src/FaceForest.cpp:183-258
+ *                          box, batched (the reference loops faces at     src/FaceForest.cpp:175-180)
+ *   ffd_analyze_faces_device  same, inputs/outputs resident in HBM (no PCIe in the timed path)
+ *   ffd_extract_channels   ImageSample(img, features, true)               src/ImageSample.cpp:11-20,77-90
+ *                          -> FeatureChannelFactory::extractChannel       include/FeatureChannelFactory.hpp:35-183
+ *   ffd_forest_eval_leaves Forest<S>::evaluateMT over a batch of patches  include/Forest.hpp:80-90
+ *                          (Tree<S>::evaluateMT, include/Tree.hpp:173-191)
+ *   ffd_get_trace          per-stage intermediates of the last batch (test hook; the reference has
+ *                          plotVotes/show for the same purpose, src/face_utils.cpp:348-376)
+ *   ffd_engine_destroy     FaceForest::~FaceForest                        include/FaceForest.hpp:351-353
+ *   ffd_last_error         the reference prints ERROR(...) and leaves is_inizialized=false
+ *                          (src/FaceForest.cpp:23-56); here a status code + message
+ *
+ * Conventions (same as the reference):
+ *   - images are BGR 8UC3 (cvtColor BGR2GRAY at src/FaceForest.cpp:196), row stride in bytes;
+ *   - boxes are in image pixels and must lie inside the image (cv::Mat ROI rule);
+ *   - landmarks are bbox-relative integer pixels in the order l-eye-l, l-eye-r, mouth-l,
+ *     mouth-r, mouth-b, mouth-t, r-eye-l, r-eye-r, nose-l, nose-r (output/generate_report.m:13-15);
+ *   - headpose is the predicted label in [-2, 2] (src/face_utils.cpp:237).
+ * No exceptions cross the ABI; no allocation is visible to the caller.  One
+ * engine owns one HIP stream on one device; concurrent calls need separate
+ * engines (the reference's analyzeFace is not reentrant either).
+ */
+#ifndef FFD_H
+#define FFD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  FFD_OK = 0,
+  FFD_ERR_INVALID_ARGUMENT = 1,
+  FFD_ERR_MODEL = 2,
+  FFD_ERR_DEVICE = 3,
+  FFD_ERR_OUT_OF_MEMORY = 4,
+  FFD_ERR_NOT_INITIALIZED = 5,
+  FFD_ERR_INTERNAL = 6
+} ffd_status;
+
+typedef struct ffd_engine ffd_engine;
+
+typedef struct { int32_t x, y, width, height; } ffd_rect;              /* cv::Rect */
+
+typedef struct {                                                       /* cv::Mat 8UC3 */
+  const uint8_t* bgr;
+  int32_t width, height, stride;
+} ffd_image;
+
+#define FFD_NUM_LANDMARKS 10
+#define FFD_MAX_TREES 32
+
+typedef struct {                                                       /* struct Face */
+  float headpose;            /* Face::headpose                       FaceForest.hpp:330 */
+  float pose_variance;       /* variance from getHeadPoseVotesMT    face_utils.cpp:235-238 */
+  ffd_rect bbox;             /* Face::bbox = input box              FaceForest.cpp:192 */
+  int32_t points[FFD_NUM_LANDMARKS][2]; /* Face::ffd_cordinates (bbox-relative) */
+  int32_t n_trees;           /* FFD trees selected for this face (20 except edge cases) */
+  int32_t status;            /* FFD_OK, or FFD_ERR_INVALID_ARGUMENT for a rejected box */
+} ffd_face;
+
+typedef struct {             /* HeadPoseEstimatorOption, include/FaceForest.hpp:34-43 */
+  int32_t num_head_pose_labels;      /* 5   */
+  int32_t step_size;                 /* 4   */
+  float min_foreground_probability;  /* 0.5 */
+} ffd_headpose_option;
+
+typedef struct {             /* MultiPartEstimatorOption, include/FaceForest.hpp:45-58 */
+  int32_t num_parts;                 /* 10   */
+  int32_t step_size;                 /* 3    */
+  int32_t min_samples;               /* 2    */
+  float min_forground;               /* 0.5  */
+  float min_pf;                      /* 0.25 */
+  float max_variance;                /* 25   */
+} ffd_multipart_option;
+
+typedef struct {             /* MeanShiftOption, include/MeanShift.hpp:16-25 */
+  int32_t kernel_size;               /* 10   */
+  int32_t max_iterations;            /* 7    */
+  float stopping_criteria;           /* 0.05 */
+} ffd_meanshift_option;
+
+typedef struct {
+  const char* model_path;    /* FFDMODEL file written by ffd_convert (replaces tree_path dirs) */
+  int32_t device;            /* HIP device ordinal */
+  int32_t max_chunk_faces;   /* faces per pipeline chunk; 0 = default */
+  ffd_headpose_option hp_option;
+  ffd_multipart_option mp_option;
+  ffd_meanshift_option ms_option;
+} ffd_engine_desc;
+
+/* Fill desc with the reference defaults (identical values to the option structs' ctors). */
+void ffd_engine_desc_init(ffd_engine_desc* desc);
+
+ffd_status ffd_engine_create(const ffd_engine_desc* desc, ffd_engine** out);
+void ffd_engine_destroy(ffd_engine* engine);
+/* Last error message for this engine (or for a failed create when engine == NULL). */
+const char* ffd_last_error(const ffd_engine* engine);
+
+/* Scaled-face geometry of a box (FaceForest.cpp:202-204; face_utils.cpp:197-207,255-265). */
+ffd_status ffd_face_geometry(const ffd_engine* engine, int32_t box_w, int32_t box_h, int32_t* face_w,
+                             int32_t* face_h, int32_t* n_hp_patches, int32_t* n_mp_patches);
+
+/* analyzeFace for n_faces boxes; face i uses imgs[box_img[i]] (box_img may be NULL when
+ * n_img == n_faces: face i on image i).  Host buffers in, host results out. */
+ffd_status ffd_analyze_faces(ffd_engine* engine, const ffd_image* imgs, int32_t n_img,
+                             const ffd_rect* boxes, const int32_t* box_img, int32_t n_faces,
+                             ffd_face* out);
+
+/* Same with device-resident data: d_images holds n_img images of identical geometry
+ * (width, height, stride; image k at byte offset k*image_bytes); boxes/box_img are host
+ * metadata; results are written to the device array d_out (n_faces ffd_face).  The call
+ * is enqueued on the engine's stream and returns when the work has been queued, except
+ * for one small device->host read of the per-batch tree count.  ffd_synchronize waits. */
+ffd_status ffd_analyze_faces_device(ffd_engine* engine, const void* d_images, int64_t image_bytes,
+                                    int32_t width, int32_t height, int32_t stride, int32_t n_img,
+                                    const ffd_rect* boxes, const int32_t* box_img, int32_t n_faces,
+                                    void* d_out);
+ffd_status ffd_synchronize(ffd_engine* engine);
+/* Opaque hipStream_t of the engine (for callers that order their own work after it). */
+void* ffd_stream(ffd_engine* engine);
+
+/* ImageSample channels for one scaled gray face (face_w x face_h, row-major, no padding):
+ * out receives 38 integral planes of (face_h+1) x (face_w+1) u32 (same values as the
+ * reference's CV_32F integrals, which are exact integers). */
+ffd_status ffd_extract_channels(ffd_engine* engine, const uint8_t* gray_face, int32_t face_w,
+                                int32_t face_h, uint32_t* out);
+
+#define FFD_FOREST_HEADPOSE 0
+#define FFD_FOREST_FFD 1
+
+/* Forest<S>::evaluateMT over n_patches patches (top-left x,y pairs; 31x31 patches) of one
+ * image sample given as 38 integral planes (layout of ffd_extract_channels).  tree_ids:
+ * head-pose tree index (0..14) or FFD global tree id (forest*20 + tree).  leaf_ids[p*n_trees+t]
+ * receives the global leaf ordinal reached (model file order). */
+ffd_status ffd_forest_eval_leaves(ffd_engine* engine, int32_t forest_kind, const uint32_t* channels,
+                                  int32_t face_w, int32_t face_h, const int32_t* patches_xy,
+                                  int32_t n_patches, const int32_t* tree_ids, int32_t n_trees,
+                                  int32_t* leaf_ids);
+
+/* Intermediates of face `index` of the most recent ffd_analyze_faces[_device] batch.
+ * Any pointer may be NULL; sizes as documented per field (from ffd_face_geometry). */
+typedef struct {
+  uint8_t* face;         /* face_w*face_h scaled gray face                          */
+  uint32_t* channels;    /* 38*(face_h+1)*(face_w+1) integral channels              */
+  int32_t* hp_leaves;    /* n_hp_patches*15, [patch][tree], reference patch order   */
+  int32_t* mp_leaves;    /* n_mp_patches*n_trees, [patch][tree]                     */
+  int32_t* trees;        /* FFD_MAX_TREES selected global FFD tree ids (n_trees used) */
+  float* pose_freq;      /* 5 areaUnderCurve values                                 */
+  int32_t* vote_counts;  /* 10 votes per landmark                                   */
+  float* ms_mean;        /* 20: MeanShift mode (x,y) per landmark before rounding   */
+} ffd_trace;
+
+ffd_status ffd_get_trace(ffd_engine* engine, int32_t index, ffd_trace* trace);
+
+/* Per-stage device time of the pipeline, measured with hipEvents on the engine stream
+ * (kernel boundaries only; used by bench.py for the roofline of the dominant kernel).
+ * ffd_set_profiling(e, 1) enables and resets the accumulators. */
+#define FFD_NUM_STAGES 11
+ffd_status ffd_set_profiling(ffd_engine* engine, int32_t enable);
+ffd_status ffd_get_stage_times(ffd_engine* engine, double* total_ms, int64_t* launches, int32_t n_stages);
+const char* ffd_stage_name(int32_t stage);
+
+/* Library version string. */
+const char* ffd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FFD_H */

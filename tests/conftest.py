@@ -1,0 +1,57 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+MODEL = os.path.join(REPO, "model", "ffd_model.bin")
+REFERENCE = os.environ.get("FFD_REFERENCE", "/root/reference")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+    config.addinivalue_line("markers", "reference: needs the read-only reference tree at /root/reference")
+
+
+@pytest.fixture(scope="session")
+def model_path():
+    if not os.path.exists(MODEL):
+        pytest.fail(f"model not converted: {MODEL} (run __graft_entry__.build())")
+    return MODEL
+
+
+@pytest.fixture(scope="session")
+def fixtures():
+    from face_alignment_cvpr_2012_amd.synthetic import load_fixtures
+    return load_fixtures()
+
+
+@pytest.fixture(scope="session")
+def oracle_mod(model_path):
+    import oracle
+    oracle.load_model(model_path)
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def engine(model_path):
+    import face_alignment_cvpr_2012_amd as ffd
+    ff = ffd.FaceForest(ffd.FaceForestOptions(model_path=model_path))
+    yield ff
+    ff.close()
+
+
+@pytest.fixture(scope="session")
+def reference_root():
+    if not os.path.isdir(os.path.join(REFERENCE, "data")):
+        pytest.skip("reference tree not present (only in the build container)")
+    return REFERENCE
+
+
+def crops(n, seed=2012):
+    from face_alignment_cvpr_2012_amd.synthetic import make_crops
+    return make_crops(n, seed=seed)[0]
