@@ -59,7 +59,7 @@ def stage_work(stage, n_faces, W=125, H=125, n_hp=576, n_mp=1024, trees=20):
     return n_faces * n_hp * 15 * 4 / 1e9, "GB/s", "hbm"
 
 
-def cpu_baseline(n_budget_s=12.0, max_faces=96):
+def cpu_baseline(n_budget_s=12.0, max_faces=512):
     """Oracle (C++ restatement) in reference-shaped mode: faces sequential, per-face thread pools
     of `cores` threads for the 35 Gabor, 576 head-pose and 1,024 FFD tasks (ThreadPool.hpp:24-64)."""
     import oracle

@@ -1,0 +1,55 @@
+"""Numeric premises the restatement and the kernels rely on (CPU-only)."""
+import math
+
+import numpy as np
+import pytest
+
+
+def test_float_division_truncation_equals_integer_division():
+    """ImageSample::evalTest computes p = (int)(R / (float)(w*h)) (ImageSample.cpp:347,353); the
+    kernels use the exact integer quotient.  Equal for every rectangle sum R in [0, 255*484] and
+    area in [1, 484] (rect sides 1..22)."""
+    R = np.arange(0, 255 * 484 + 1, dtype=np.int64)
+    Rf = R.astype(np.float32)
+    for a in range(1, 485):
+        q = (Rf / np.float32(a)).astype(np.int64)  # IEEE float32 division, then trunc toward 0
+        assert np.array_equal(q, R // a), a
+
+
+def test_ffd_exp_matches_libm(oracle_mod):
+    """ffd_exp (include/ffd_numerics.h) is within 2 ulp of libm exp over the argument ranges the
+    path uses (areaUnderCurve: -0.5 t^2 <= 0; MeanShift: -d/10 in [-30, 0])."""
+    rng = np.random.default_rng(0)
+    xs = np.concatenate([rng.uniform(-745, 709, 4000), rng.uniform(-40, 0, 4000), rng.uniform(-1, 1, 2000),
+                         [0.0, -0.0, 1e-300, -1e-300, 709.7, -708.3, -744.0]])
+    for x in xs:
+        got, ref = oracle_mod.exp(float(x)), math.exp(float(x))
+        if ref == 0.0 or got == 0.0:
+            assert abs(got - ref) <= 5e-324 * 4
+            continue
+        ulp = math.ulp(ref)
+        if ref < 2.2250738585072014e-308:  # subnormal results: absolute tolerance
+            assert abs(got - ref) <= 2 * 5e-324
+        else:
+            assert abs(got - ref) <= 2 * ulp, (x, got, ref)
+    assert math.isnan(oracle_mod.exp(float("nan")))
+    assert oracle_mod.exp(-1e6) == 0.0 and oracle_mod.exp(1e6) == math.inf
+
+
+def test_sqrt_2pi_literal():
+    assert 2.5066282746310002 == math.sqrt(2 * math.pi)
+
+
+def test_area_under_curve_partition(oracle_mod):
+    """areaUnderCurve (face_utils.cpp:304-323) over the 5 pose bins of FaceForest.cpp:216-222
+    integrates the Gaussian: for a moderate sigma the bins sum to ~1 (left Riemann sums)."""
+    poseT = np.array([-2.5, -0.35, -0.20, 0.20, 0.35, 2.5], np.float32)
+    for mean, std in [(0.0, 0.4), (0.3, 0.2), (-1.0, 0.5)]:
+        s = sum(oracle_mod.area_under_curve(float(poseT[j]), float(poseT[j + 1]), mean, std) for j in range(5))
+        assert abs(s - 1.0) < 0.03, (mean, std, s)
+
+
+@pytest.mark.parametrize("w", [7, 9, 13, 19, 25])
+def test_gabor_flop_model(w):
+    import bench
+    assert bench.gabor_flops_per_pixel(w) > 0
