@@ -98,7 +98,7 @@ EXPORTED_SYMBOLS = (
     "ffd_forest_eval_leaves", "ffd_get_trace", "ffd_version", "ffd_set_profiling", "ffd_get_stage_times",
     "ffd_stage_name",
 )
-NUM_STAGES = 11
+NUM_STAGES = 12
 
 
 def lib():

@@ -85,12 +85,14 @@ struct ffd_engine {
   int64_t hp_leaves = 0, mp_leaves = 0;
 
   // device model
-  DevBuf hp_nodes, hp_roots, hp_m, mp_nodes, mp_roots, mp_mask, mp_fg, mp_offs;
+  DevBuf gabor_coef, hp_nodes, hp_roots, hp_sizes, hp_m, mp_nodes, mp_roots, mp_sizes, mp_mask, mp_fg, mp_offs;
 
   // workspace
   DevBuf faces, wave_hp, wave_mp, images, gray, mag, minmax, chan, hpleaf, mpleaf, votes, state, out,
       ms_mean, vote_counts, maxtrees, scratch_a, scratch_b, scratch_c;
-  std::vector<uint8_t> pinned_dummy;
+  // host staging of per-batch tables (kept alive until the next batch: async H2D copies)
+  std::vector<FaceDesc> h_fds;
+  std::vector<int32_t> h_ws_hp, h_ws_mp;
 
   // stage profiler (hipEvents on the engine stream)
   struct Pending { int stage; hipEvent_t a, b; };
@@ -169,7 +171,8 @@ thread_local std::string g_create_err;
 
 // Flatten the pre-order archive records of every tree into breadth-first node arrays
 // with adjacent children (see ffd_device.hpp for the 16-byte node encoding).
-void flatten_forest(const ModelFile& m, const std::string& p, std::vector<uint4>& nodes, std::vector<int32_t>& roots) {
+void flatten_forest(const ModelFile& m, const std::string& p, std::vector<uint4>& nodes, std::vector<int32_t>& roots,
+                    std::vector<int32_t>& sizes) {
   const auto& off = m.get(p + ".tree_node_off");
   const auto& nl = m.get(p + ".node_leaf");
   const auto& ns = m.get(p + ".node_split");
@@ -179,6 +182,7 @@ void flatten_forest(const ModelFile& m, const std::string& p, std::vector<uint4>
   const int64_t T = (int64_t)off.count() - 1;
   nodes.clear();
   roots.clear();
+  sizes.clear();
   nodes.reserve(nl.count());
   for (int64_t t = 0; t < T; t++) {
     const int64_t b = to[t], e = to[t + 1];
@@ -202,6 +206,7 @@ void flatten_forest(const ModelFile& m, const std::string& p, std::vector<uint4>
     const int64_t base = (int64_t)nodes.size();
     for (size_t k = 0; k < order.size(); k++) newidx[order[k]] = base + (int64_t)k;
     roots.push_back((int32_t)base);
+    sizes.push_back((int32_t)order.size());
     for (size_t k = 0; k < order.size(); k++) {
       const int64_t v = order[k];
       uint4 nd;
@@ -253,15 +258,18 @@ void ffd_engine::load_model(const std::string& path) {
   if (n_forests < 1 || n_forests > 5) throw std::runtime_error("engine supports 1..5 pose forests (poseT has 5 bins)");
 
   std::vector<uint4> nodes;
-  std::vector<int32_t> roots;
-  flatten_forest(m, "hp", nodes, roots);
+  std::vector<int32_t> roots, sizes;
+  flatten_forest(m, "hp", nodes, roots, sizes);
   hp_trees = (int)roots.size();
   upload(hp_nodes, nodes, stream);
   upload(hp_roots, roots, stream);
-  flatten_forest(m, "mp", nodes, roots);
+  upload(hp_sizes, sizes, stream);
+  flatten_forest(m, "mp", nodes, roots, sizes);
   if ((int)roots.size() != n_forests * ntrees_per_forest) throw std::runtime_error("FFD tree count mismatch");
   upload(mp_nodes, nodes, stream);
   upload(mp_roots, roots, stream);
+  upload(mp_sizes, sizes, stream);
+  HIP_CHECK(hipStreamSynchronize(stream));  // host vectors are reused below
 
   // head-pose leaf value m (face_utils.cpp:223-228), -1 when the leaf is filtered out
   {
@@ -357,23 +365,16 @@ void ffd_engine::build_gabor() {
           throw std::runtime_error("Gabor kernel not point-symmetric on this libm");
     }
     const int OFF = GABOR_OFFS[iNu];
-    if (Wk == 7) {
-      for (int t = 0; t < 49; t++)
-        for (int o = 0; o < 7; o++) {
-          coef[OFF + t * 14 + o] = re[o][t];
-          coef[OFF + t * 14 + 7 + o] = im[o][t];
-        }
-    } else {
-      const int half = (Wk * Wk - 1) / 2;
-      for (int t = 0; t < half; t++)
-        for (int o = 0; o < 7; o++) {
-          coef[OFF + t * 14 + o] = re[o][t];
-          coef[OFF + t * 14 + 7 + o] = im[o][t];
-        }
-      for (int o = 0; o < 7; o++) coef[OFF + half * 14 + o] = re[o][half];
-    }
+    const int ntap = Wk == 7 ? 49 : (Wk * Wk - 1) / 2;  // taps (7x7) or folded pairs
+    for (int t = 0; t < ntap; t++)
+      for (int o = 0; o < 7; o++) {
+        coef[OFF + t * 16 + o] = re[o][t];
+        coef[OFF + t * 16 + 8 + o] = im[o][t];
+      }
+    if (Wk != 7)
+      for (int o = 0; o < 7; o++) coef[OFF + ntap * 16 + o] = re[o][ntap];  // centre tap
   }
-  HIP_CHECK(upload_gabor(coef.data(), stream));
+  upload(gabor_coef, coef, stream);
   HIP_CHECK(hipStreamSynchronize(stream));
 }
 
@@ -414,14 +415,12 @@ void ffd_engine::run_chunk(std::vector<FaceDesc>& fds, const uint8_t* d_images, 
   ms_mean.ensure((size_t)n * NPARTS * 2 * 4);
   vote_counts.ensure((size_t)n * NPARTS * 4);
 
-  // traversal wave tables (face-major; HP: 15 trees; FFD: filled after the tree count is known)
-  std::vector<int64_t> ws_hp(n + 1, 0);
-  for (int i = 0; i < n; i++) {
-    const auto& f = fds[i];
-    int64_t w = f.valid ? (int64_t)hp_trees * ((f.nhx * f.nhy + 63) / 64) : 0;
-    ws_hp[i + 1] = ws_hp[i] + w;
-  }
-  upload(faces, fds, stream);
+  // traversal block tables: one block per (face, tree), face-major (FFD: after the tree count is known)
+  std::vector<int32_t>& ws_hp = h_ws_hp;
+  ws_hp.assign(n + 1, 0);
+  for (int i = 0; i < n; i++) ws_hp[i + 1] = ws_hp[i] + (fds[i].valid ? hp_trees : 0);
+  h_fds = fds;
+  upload(faces, h_fds, stream);
   upload(wave_hp, ws_hp, stream);
   HIP_CHECK(hipMemsetAsync(minmax.p, 0xFF, (size_t)n * NGABOR * 2 * 4, stream));
   HIP_CHECK(hipMemsetAsync(d_out, 0, (size_t)n * sizeof(FaceOut), stream));
@@ -431,14 +430,16 @@ void ffd_engine::run_chunk(std::vector<FaceDesc>& fds, const uint8_t* d_images, 
   stage(0, [&] { launch_gray_resize(dfd, n, d_images, gray.as<uint8_t>(), stream); });
   for (int nu = 4; nu >= 0; nu--)  // largest kernels first
     stage(1 + (4 - nu), [&] {
-      launch_gabor(nu, dfd, n, max_w, max_h, gray.as<uint8_t>(), mag.as<float>(), minmax.as<uint32_t>(), stream);
+      launch_gabor(nu, dfd, n, max_w, max_h, gray.as<uint8_t>(), gabor_coef.as<float4>(), mag.as<float>(),
+                   minmax.as<uint32_t>(), stream);
     });
   stage(6, [&] {
     launch_integral(dfd, n, gray.as<uint8_t>(), mag.as<float>(), minmax.as<uint32_t>(), chan.as<uint32_t>(), stream);
   });
   stage(7, [&] {
-    launch_traverse(true, dfd, wave_hp.as<int64_t>(), n, ws_hp[n], hp_nodes.as<uint4>(), hp_roots.as<int32_t>(),
-                    nullptr, hp_trees, desc.hp_option.step_size, chan.as<uint32_t>(), hpleaf.as<int32_t>(), stream);
+    launch_traverse(true, dfd, wave_hp.as<int32_t>(), n, ws_hp[n], hp_nodes.as<uint4>(), hp_roots.as<int32_t>(),
+                    hp_sizes.as<int32_t>(), nullptr, desc.hp_option.step_size, chan.as<uint32_t>(),
+                    hpleaf.as<int32_t>(), stream);
   });
   stage(8, [&] {
     launch_hp_pose(dfd, n, hpleaf.as<int32_t>(), hp_m.as<float>(), hp_trees, n_forests, ntrees_per_forest,
@@ -451,26 +452,29 @@ void ffd_engine::run_chunk(std::vector<FaceDesc>& fds, const uint8_t* d_images, 
   HIP_CHECK(hipMemcpyAsync(hs.data(), state.p, (size_t)n * sizeof(HpState), hipMemcpyDeviceToHost, stream));
   HIP_CHECK(hipStreamSynchronize(stream));
   int tslots = 0;
-  std::vector<int64_t> ws_mp(n + 1, 0);
+  std::vector<int32_t>& ws_mp = h_ws_mp;
+  ws_mp.assign(n + 1, 0);
   for (int i = 0; i < n; i++) {
-    const auto& f = fds[i];
-    int nt = f.valid ? hs[i].n_trees : 0;
+    const int nt = fds[i].valid ? hs[i].n_trees : 0;
     tslots = std::max(tslots, nt);
-    int64_t w = f.valid ? (int64_t)nt * ((f.nmx * f.nmy + 63) / 64) : 0;
-    ws_mp[i + 1] = ws_mp[i] + w;
+    ws_mp[i + 1] = ws_mp[i] + nt;
   }
   upload(wave_mp, ws_mp, stream);
   stage(9, [&] {
-    launch_traverse(false, dfd, wave_mp.as<int64_t>(), n, ws_mp[n], mp_nodes.as<uint4>(), mp_roots.as<int32_t>(),
-                    state.as<HpState>(), tslots, desc.mp_option.step_size, chan.as<uint32_t>(), mpleaf.as<int32_t>(),
-                    stream);
+    launch_traverse(false, dfd, wave_mp.as<int32_t>(), n, ws_mp[n], mp_nodes.as<uint4>(), mp_roots.as<int32_t>(),
+                    mp_sizes.as<int32_t>(), state.as<HpState>(), desc.mp_option.step_size, chan.as<uint32_t>(),
+                    mpleaf.as<int32_t>(), stream);
   });
+  const int n_parts = std::min(desc.mp_option.num_parts, NPARTS);
   stage(10, [&] {
-    launch_votes_meanshift(dfd, n, mpleaf.as<int32_t>(), mp_mask.as<uint32_t>(), mp_fg.as<float>(),
-                           mp_offs.as<int32_t>(), state.as<HpState>(), MAX_TREES, desc.mp_option.step_size, patch / 2,
-                           std::min(desc.mp_option.num_parts, NPARTS), (float)desc.ms_option.kernel_size,
-                           desc.ms_option.max_iterations, desc.ms_option.stopping_criteria, votes.as<Vote>(),
-                           ms_mean.as<float>(), vote_counts.as<int32_t>(), d_out, stream);
+    launch_votes(dfd, n, mpleaf.as<int32_t>(), mp_mask.as<uint32_t>(), mp_fg.as<float>(), mp_offs.as<int32_t>(),
+                 state.as<HpState>(), MAX_TREES, desc.mp_option.step_size, patch / 2, n_parts, votes.as<Vote>(),
+                 vote_counts.as<int32_t>(), stream);
+  });
+  stage(11, [&] {
+    launch_meanshift(dfd, n, state.as<HpState>(), MAX_TREES, n_parts, (float)desc.ms_option.kernel_size,
+                     desc.ms_option.max_iterations, desc.ms_option.stopping_criteria, votes.as<Vote>(),
+                     vote_counts.as<int32_t>(), ms_mean.as<float>(), d_out, stream);
   });
   HIP_CHECK(hipGetLastError());
   last_tslots = tslots;
@@ -615,7 +619,7 @@ ffd_status ffd_synchronize(ffd_engine* e) {
 
 static const char* const kStageNames[FFD_NUM_STAGES] = {
     "gray_resize", "gabor_25x25", "gabor_19x19", "gabor_13x13", "gabor_9x9", "gabor_7x7",
-    "integral_channels", "headpose_traverse", "headpose_reduce_select", "ffd_traverse", "votes_meanshift"};
+    "integral_channels", "headpose_traverse", "headpose_reduce_select", "ffd_traverse", "votes", "meanshift"};
 
 const char* ffd_stage_name(int32_t i) { return (i >= 0 && i < FFD_NUM_STAGES) ? kStageNames[i] : ""; }
 
@@ -781,7 +785,8 @@ ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t
     const FaceDesc* dfd = e->faces.as<FaceDesc>();
     launch_gray_resize(dfd, 1, e->scratch_a.as<uint8_t>(), e->gray.as<uint8_t>(), e->stream);
     for (int nu = 4; nu >= 0; nu--)
-      launch_gabor(nu, dfd, 1, W, H, e->gray.as<uint8_t>(), e->mag.as<float>(), e->minmax.as<uint32_t>(), e->stream);
+      launch_gabor(nu, dfd, 1, W, H, e->gray.as<uint8_t>(), e->gabor_coef.as<float4>(), e->mag.as<float>(),
+                   e->minmax.as<uint32_t>(), e->stream);
     launch_integral(dfd, 1, e->gray.as<uint8_t>(), e->mag.as<float>(), e->minmax.as<uint32_t>(), e->chan.as<uint32_t>(),
                     e->stream);
     HIP_CHECK(hipGetLastError());

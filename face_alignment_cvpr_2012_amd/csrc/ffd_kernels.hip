@@ -116,10 +116,16 @@ __global__ __launch_bounds__(256) void k_gray_resize(const FaceDesc* __restrict_
 }
 
 // ------------------------------------------------------------------ Gabor --
-// Coefficients (host-built from createKernel, FeatureChannelFactory.hpp:186-251):
-//   scale 0 (7x7): [49 taps row-major][7 re | 7 im]
-//   scale >= 1   : [half pairs][7 re | 7 im], then [7 re centre]
-__constant__ float c_gabor[GABOR_COEF_TOTAL];
+// Coefficient table (host-built from createKernel, FeatureChannelFactory.hpp:186-251), 16 floats
+// per tap/pair: [re0..re6, 0, im0..im6, 0]:
+//   scale 0 (7x7): 49 taps in row-major order
+//   scale >= 1   : (W*W-1)/2 pairs in row-major order, then the centre [re0..re6, 0]
+// One 512-thread workgroup computes a 64x32 output tile of one face for the 7 orientations of
+// one scale; each thread owns 4 horizontally adjacent pixels and slides a 4-wide window along
+// each kernel row, so one new LDS value per tap feeds 56 FMAs.  The per-pixel operation order is
+// the restatement's (oracle/ffd_oracle.cpp gabor_mag): 7x7 = OpenCV's direct row-major mul+add;
+// larger = folded pairs S = a+b, D = a-b, fma in row-major pair order, then the centre.
+constexpr int GB_TX = 64, GB_TY = 32, GB_THREADS = 512;
 
 template <int W> struct GaborCfg;
 template <> struct GaborCfg<7>  { static constexpr int nu = 0, off = GABOR_OFF0; };
@@ -128,84 +134,132 @@ template <> struct GaborCfg<13> { static constexpr int nu = 2, off = GABOR_OFF2;
 template <> struct GaborCfg<19> { static constexpr int nu = 3, off = GABOR_OFF3; };
 template <> struct GaborCfg<25> { static constexpr int nu = 4, off = GABOR_OFF4; };
 
-// One workgroup = one 16x16 output tile of one face for the 7 orientations of one
-// scale.  Pixel pair sums S/D are shared by the 7 orientations (the point symmetry
-// of the Gabor kernels), halving the FMAs of a direct correlation.
 template <int W>
-__global__ __launch_bounds__(256) void k_gabor(const FaceDesc* __restrict__ faces,
-                                               const uint8_t* __restrict__ gray,
-                                               float* __restrict__ mag,
-                                               uint32_t* __restrict__ minmax) {
-  constexpr int R = (W - 1) / 2, TS = 16, LW = 48, TW = TS + 2 * R;
+__global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict__ faces,
+                                                      const uint8_t* __restrict__ gray,
+                                                      const float4* __restrict__ coef_g,
+                                                      float* __restrict__ mag,
+                                                      uint32_t* __restrict__ minmax) {
+  constexpr int R = (W - 1) / 2;
+  constexpr int LW = GB_TX + 2 * R + 4;  // row stride (floats), multiple of 4
+  constexpr int LH = GB_TY + 2 * R;
   constexpr int NU = GaborCfg<W>::nu, OFF = GaborCfg<W>::off;
-  __shared__ float tile[TW * LW];
-  __shared__ uint32_t red[4][14];
+  constexpr int NTAP = (W == 7) ? 49 : (W * W - 1) / 2 + 1;  // incl. centre
+  __shared__ __attribute__((aligned(16))) float tile[LH * LW];
+  __shared__ float4 coef[NTAP * 4];
+  __shared__ uint32_t red[8][14];
   const FaceDesc fd = faces[blockIdx.y];
   if (!fd.valid) return;
-  const int tiles_x = (fd.W + TS - 1) / TS;
-  const int tx0 = (blockIdx.x % tiles_x) * TS, ty0 = (blockIdx.x / tiles_x) * TS;
+  const int tiles_x = (fd.W + GB_TX - 1) / GB_TX;
+  const int tx0 = (blockIdx.x % tiles_x) * GB_TX, ty0 = (blockIdx.x / tiles_x) * GB_TY;
   if (ty0 >= fd.H) return;  // grid is sized for the batch's tallest face
+  for (int i = threadIdx.x; i < NTAP * 4; i += GB_THREADS) coef[i] = coef_g[OFF / 4 + i];
   const uint8_t* g = gray + fd.gray_off;
-  for (int i = threadIdx.x; i < TW * TW; i += 256) {
-    int ly = i / TW, lx = i % TW;
-    int y = reflect101(ty0 - R + ly, fd.H), x = reflect101(tx0 - R + lx, fd.W);
+  for (int i = threadIdx.x; i < LH * (GB_TX + 2 * R); i += GB_THREADS) {
+    const int ly = i / (GB_TX + 2 * R), lx = i % (GB_TX + 2 * R);
+    const int y = reflect101(ty0 - R + ly, fd.H), x = reflect101(tx0 - R + lx, fd.W);
     tile[ly * LW + lx] = (float)g[y * PITCH + x];
   }
   __syncthreads();
-  const int lx = threadIdx.x & 15, ly = threadIdx.x >> 4;
-  const float* base = &tile[(ly + R) * LW + lx + R];
-  float re[7], im[7];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;  // 16 x 32 threads, 4 px each
+  float re[4][7], im[4][7];
 #pragma unroll
-  for (int o = 0; o < 7; o++) re[o] = im[o] = 0.f;
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int o = 0; o < 7; o++) re[k][o] = im[k][o] = 0.f;
+
   if constexpr (W == 7) {
-    // OpenCV Filter2D direct path: s = 0; s += k*p over taps in row-major order.
-#pragma unroll 7
-    for (int t = 0; t < 49; t++) {
-      const float p = base[(t / 7 - 3) * LW + (t % 7 - 3)];
+    for (int r = 0; r < 7; r++) {
+      const float* row = &tile[(ty + r) * LW + 4 * tx];  // image row py + r - 3, cols px - 3 ..
+      float win[10];
 #pragma unroll
-      for (int o = 0; o < 7; o++) {
-        re[o] = re[o] + c_gabor[OFF + t * 14 + o] * p;
-        im[o] = im[o] + c_gabor[OFF + t * 14 + 7 + o] * p;
+      for (int j = 0; j < 10; j++) win[j] = row[j];
+#pragma unroll
+      for (int c = 0; c < 7; c++) {
+        const float4 c0 = coef[(r * 7 + c) * 4 + 0], c1 = coef[(r * 7 + c) * 4 + 1];
+        const float4 c2 = coef[(r * 7 + c) * 4 + 2], c3 = coef[(r * 7 + c) * 4 + 3];
+        const float kr[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
+        const float ki[7] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const float p = win[c + k];
+#pragma unroll
+          for (int o = 0; o < 7; o++) {
+            re[k][o] = re[k][o] + kr[o] * p;
+            im[k][o] = im[k][o] + ki[o] * p;
+          }
+        }
       }
     }
   } else {
-    constexpr int HALF = (W * W - 1) / 2;
-#pragma unroll 4
-    for (int t = 0; t < HALF; t++) {
-      const int dy = t / W - R, dx = t % W - R;
-      const float a = base[dy * LW + dx], b = base[-dy * LW - dx];
-      const float S = a + b, D = a - b;
+    // rows dy = -R .. 0 (row 0 only dx < 0); pair t = (dy + R) * W + (dx + R)
+    for (int r = 0; r <= R; r++) {
+      const int dy = r - R;
+      const float* rowA = &tile[(ty + R + dy) * LW + 4 * tx];  // a(k, dx) = rowA[dx + R + k]
+      const float* rowB = &tile[(ty + R - dy) * LW + 4 * tx];  // b(k, dx) = rowB[R - dx + k]
+      float a[4], b[4];
 #pragma unroll
-      for (int o = 0; o < 7; o++) {
-        re[o] = fmaf(c_gabor[OFF + t * 14 + o], S, re[o]);
-        im[o] = fmaf(c_gabor[OFF + t * 14 + 7 + o], D, im[o]);
+      for (int k = 0; k < 4; k++) { a[k] = rowA[k]; b[k] = rowB[2 * R + k]; }
+      const int ncol = (r < R) ? W : R;
+#pragma unroll
+      for (int j = 0; j < W; j++) {  // dx = j - R
+        if (j >= ncol) break;
+        const int t = r * W + j;
+        const float4 c0 = coef[t * 4 + 0], c1 = coef[t * 4 + 1], c2 = coef[t * 4 + 2], c3 = coef[t * 4 + 3];
+        const float kr[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
+        const float ki[7] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const float S = a[k] + b[k], D = a[k] - b[k];
+#pragma unroll
+          for (int o = 0; o < 7; o++) {
+            re[k][o] = fmaf(kr[o], S, re[k][o]);
+            im[k][o] = fmaf(ki[o], D, im[k][o]);
+          }
+        }
+        if (j + 1 < W) {  // slide: a moves right, b moves left
+          a[0] = a[1]; a[1] = a[2]; a[2] = a[3]; a[3] = rowA[j + 4];
+          b[3] = b[2]; b[2] = b[1]; b[1] = b[0]; b[0] = rowB[2 * R - j - 1];
+        }
       }
     }
-    const float p0 = base[0];
+    constexpr int TC = (W * W - 1) / 2;
+    const float4 c0 = coef[TC * 4 + 0], c1 = coef[TC * 4 + 1];
+    const float kr[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
+    const float* rowC = &tile[(ty + R) * LW + 4 * tx + R];
 #pragma unroll
-    for (int o = 0; o < 7; o++) re[o] = fmaf(c_gabor[OFF + HALF * 14 + o], p0, re[o]);
+    for (int k = 0; k < 4; k++) {
+      const float p0 = rowC[k];
+#pragma unroll
+      for (int o = 0; o < 7; o++) re[k][o] = fmaf(kr[o], p0, re[k][o]);
+    }
   }
-  const int x = tx0 + lx, y = ty0 + ly;
-  const bool in = x < fd.W && y < fd.H;
+  const int x0 = tx0 + 4 * tx, y = ty0 + ty;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t mn[7], mx[7];
 #pragma unroll
   for (int o = 0; o < 7; o++) {
-    const float i2 = im[o] * im[o], r2 = re[o] * re[o];
-    const float m = __builtin_sqrtf(i2 + r2);
-    if (in) mag[fd.mag_off + ((int64_t)(NU * 7 + o) * fd.H + y) * PITCH + x] = m;
-    // m >= +0, so unsigned order == float order; the max is kept as min(~bits) so one
-    // atomicMin per slot serves both and the table is initialised to all-ones.
-    uint32_t bits = __float_as_uint(m);
-    mn[o] = in ? bits : 0xFFFFFFFFu;
-    mx[o] = in ? ~bits : 0xFFFFFFFFu;
+    float m4[4];
+    mn[o] = 0xFFFFFFFFu;
+    mx[o] = 0xFFFFFFFFu;  // max kept as min(~bits): one atomicMin serves both
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const float i2 = im[k][o] * im[k][o], r2 = re[k][o] * re[k][o];
+      m4[k] = __builtin_sqrtf(i2 + r2);
+      const bool in = (x0 + k) < fd.W && y < fd.H;
+      const uint32_t bits = __float_as_uint(m4[k]);  // m >= +0: unsigned order == float order
+      if (in) { mn[o] = min(mn[o], bits); mx[o] = min(mx[o], ~bits); }
+    }
+    if (y < fd.H)  // columns >= W land in the row's pitch padding, never read
+      *reinterpret_cast<float4*>(&mag[fd.mag_off + ((int64_t)(NU * 7 + o) * fd.H + y) * PITCH + x0]) =
+          make_float4(m4[0], m4[1], m4[2], m4[3]);
   }
 #pragma unroll
   for (int o = 0; o < 7; o++) {
 #pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) {
-      mn[o] = min(mn[o], (uint32_t)__shfl_xor((int)mn[o], s));
-      mx[o] = min(mx[o], (uint32_t)__shfl_xor((int)mx[o], s));
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+      mn[o] = min(mn[o], (uint32_t)__shfl_xor((int)mn[o], sh));
+      mx[o] = min(mx[o], (uint32_t)__shfl_xor((int)mx[o], sh));
     }
   }
   if (lane == 0) {
@@ -214,9 +268,9 @@ __global__ __launch_bounds__(256) void k_gabor(const FaceDesc* __restrict__ face
   }
   __syncthreads();
   if (threadIdx.x < 14) {
-    int k = threadIdx.x;
+    const int k = threadIdx.x;
     uint32_t v = red[0][k];
-    for (int w = 1; w < 4; w++) v = min(v, red[w][k]);
+    for (int w = 1; w < GB_THREADS / 64; w++) v = min(v, red[w][k]);
     uint32_t* slot = minmax + ((int64_t)blockIdx.y * NGABOR + NU * 7 + (k % 7)) * 2;
     atomicMin(slot + (k < 7 ? 0 : 1), v);
   }
@@ -318,44 +372,82 @@ __device__ __forceinline__ uint32_t walk(const uint4* __restrict__ nodes, uint32
   return nd.x & ~LEAF_BIT;
 }
 
-// One wave = 64 patches (lane order) x one tree of one face.  Wave ids are laid out
-// face-major, then tree slot, then patch chunk; wave_start[f] is the first wave of f.
+// One workgroup = one (face, tree): the tree's first TOP_NODES breadth-first nodes (its top
+// ~10 levels, which every walk visits) are staged in LDS; each thread then walks two patches
+// at a time (lane order, so a wave's 64 lanes read horizontally adjacent patches) to keep two
+// independent gather chains in flight.  block_start[f] = first block of face f.
+constexpr int TOP_NODES = 1024;
+
+struct WalkCtx {
+  const uint4* __restrict__ nodes;
+  const uint4* top;       // LDS copy of nodes[root .. root+ntop)
+  uint32_t root, ntop;
+  const uint32_t* __restrict__ chan;  // face's channel base (uniform)
+  uint32_t plane;
+};
+
+__device__ __forceinline__ uint4 fetch_node(const WalkCtx& c, uint32_t node) {
+  const uint32_t r = node - c.root;
+  return r < c.ntop ? c.top[r] : c.nodes[node];
+}
+
+__device__ __forceinline__ uint32_t split_child(const WalkCtx& c, const uint4& nd, uint32_t poff) {
+  const uint32_t* I = c.chan + (nd.y & 63u) * c.plane + poff;
+  const int p1 = rect_mean(I, nd.w & 0xFFFFu, (nd.y >> 6) & 31u, (nd.y >> 11) & 31u);
+  const int p2 = rect_mean(I, nd.w >> 16, (nd.y >> 16) & 31u, (nd.y >> 21) & 31u);
+  return nd.x + ((p1 - p2) <= (int)nd.z ? 0u : 1u);
+}
+
 template <bool HP>
 __global__ __launch_bounds__(256) void k_traverse(const FaceDesc* __restrict__ faces,
-                                                  const int64_t* __restrict__ wave_start, int n_faces,
-                                                  int64_t total_waves, const uint4* __restrict__ nodes,
-                                                  const int32_t* __restrict__ roots,
-                                                  const HpState* __restrict__ hp_state, int tslots, int step,
+                                                  const int32_t* __restrict__ block_start, int n_faces,
+                                                  const uint4* __restrict__ nodes, const int32_t* __restrict__ roots,
+                                                  const int32_t* __restrict__ tree_nodes,
+                                                  const HpState* __restrict__ hp_state, int step,
                                                   const uint32_t* __restrict__ chan,
                                                   int32_t* __restrict__ leaf_out) {
-  const uint32_t lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t wave = (int64_t)lb * 4 + (threadIdx.x >> 6);
-  if (wave >= total_waves) return;
+  __shared__ uint4 top[TOP_NODES];
+  const int lb = (int)xcd_remap(blockIdx.x, gridDim.x);
   int lo = 0, hi = n_faces - 1;
-  while (lo < hi) {  // last f with wave_start[f] <= wave
-    int mid = (lo + hi + 1) >> 1;
-    if (wave_start[mid] <= wave) lo = mid; else hi = mid - 1;
+  while (lo < hi) {  // last f with block_start[f] <= lb
+    const int mid = (lo + hi + 1) >> 1;
+    if (block_start[mid] <= lb) lo = mid; else hi = mid - 1;
   }
   const int f = lo;
+  const int t = lb - block_start[f];
   const FaceDesc& fd = faces[f];
+  const int tree = HP ? t : hp_state[f].trees[t];
+  WalkCtx c;
+  c.nodes = nodes;
+  c.top = top;
+  c.root = (uint32_t)roots[tree];
+  c.ntop = (uint32_t)min(TOP_NODES, tree_nodes[tree]);
+  c.chan = chan + fd.ch_off;
+  c.plane = (uint32_t)fd.plane;
+  for (uint32_t i = threadIdx.x; i < c.ntop; i += 256) top[i] = nodes[c.root + i];
+  __syncthreads();
   const int nx = HP ? fd.nhx : fd.nmx, ny = HP ? fd.nhy : fd.nmy, n = nx * ny;
-  const int chunks = (n + 63) >> 6;
-  const int local = (int)(wave - wave_start[f]);
-  const int t = local / chunks, ck = local % chunks;
-  const int q = ck * 64 + (threadIdx.x & 63);
-  if (q >= n) return;
-  int tree;
-  if (HP) {
-    tree = t;
-  } else {
-    if (t >= hp_state[f].n_trees) return;
-    tree = hp_state[f].trees[t];
+  int32_t* out = leaf_out + (HP ? fd.hp_off : fd.mp_off) + (int64_t)t * n;
+  for (int q0 = threadIdx.x; q0 < n; q0 += 512) {
+    const int q1 = q0 + 256;
+    const bool va = true, vb = q1 < n;
+    const uint32_t pa = (uint32_t)(((q0 / nx) * PITCH + (q0 % nx)) * step);
+    const uint32_t pb = vb ? (uint32_t)(((q1 / nx) * PITCH + (q1 % nx)) * step) : pa;
+    uint4 A = c.top[0], B = c.top[0];
+    bool da = !va, db = !vb;
+    for (;;) {
+      da = da || (A.x & LEAF_BIT);
+      db = db || (B.x & LEAF_BIT);
+      if (da && db) break;
+      uint32_t na = 0, nb = 0;
+      if (!da) na = split_child(c, A, pa);
+      if (!db) nb = split_child(c, B, pb);
+      if (!da) A = fetch_node(c, na);
+      if (!db) B = fetch_node(c, nb);
+    }
+    out[q0] = (int32_t)(A.x & ~LEAF_BIT);
+    if (vb) out[q1] = (int32_t)(B.x & ~LEAF_BIT);
   }
-  const int px = (q % nx) * step, py = (q / nx) * step;
-  const uint32_t* I = chan + fd.ch_off + py * PITCH + px;
-  const uint32_t leaf = walk(nodes, (uint32_t)roots[tree], I, fd.plane);
-  leaf_out[(HP ? fd.hp_off : fd.mp_off) + (int64_t)t * n + q] = (int32_t)leaf;
-  (void)tslots;
 }
 
 // Forest<S>::evaluateMT over an explicit patch list (ffd_forest_eval_leaves hook).
@@ -372,61 +464,79 @@ __global__ void k_eval_patches(const uint4* __restrict__ nodes, const int32_t* _
 }
 
 // -------------------------------------------------- head pose + tree choice --
-// getHeadPoseVotesMT reduction (face_utils.cpp:218-241), sequential in the reference
-// (patch-major, tree-minor) order; then areaUnderCurve (face_utils.cpp:304-323) and the
-// tree selection of FaceForest.cpp:214-250.  One thread per face.
-__global__ void k_hp_pose(const FaceDesc* __restrict__ faces, int n_faces, const int32_t* __restrict__ hp_leaf,
-                          const float* __restrict__ hp_m, int hp_trees, int n_forests, int ntrees_per_forest,
-                          HpState* __restrict__ state, FaceOut* __restrict__ out) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+// getHeadPoseVotesMT reduction (face_utils.cpp:218-241) + areaUnderCurve (face_utils.cpp:304-323)
+// + tree selection (FaceForest.cpp:214-250).  One wave per face: the 64 lanes gather the leaf
+// values of 64 consecutive (patch, tree) pairs in the reference order (patch-major x-outer,
+// tree-minor) and compute m and m*m per element (element-wise, same rounding as the serial
+// loop); the running sums are then advanced IN ORDER with one add per element (readlane), so
+// they equal the reference's sequential float sums bit for bit.  Filtered-out leaves add +0,
+// which leaves a non-negative float sum unchanged.
+__device__ __forceinline__ float lane_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+__global__ __launch_bounds__(256) void k_hp_pose(const FaceDesc* __restrict__ faces, int n_faces,
+                                                 const int32_t* __restrict__ hp_leaf, const float* __restrict__ hp_m,
+                                                 int hp_trees, int n_forests, int ntrees_per_forest,
+                                                 HpState* __restrict__ state, FaceOut* __restrict__ out) {
+  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (f >= n_faces) return;
   const FaceDesc& fd = faces[f];
   FaceOut& o = out[f];
-  o.bbox[0] = fd.bx; o.bbox[1] = fd.by; o.bbox[2] = fd.bw; o.bbox[3] = fd.bh;
+  if (lane == 0) { o.bbox[0] = fd.bx; o.bbox[1] = fd.by; o.bbox[2] = fd.bw; o.bbox[3] = fd.bh; }
   if (!fd.valid) {
-    o.status = 1;
-    o.n_trees = 0;
-    state[f].n_trees = 0;
+    if (lane == 0) { o.status = 1; o.n_trees = 0; state[f].n_trees = 0; }
     return;
   }
-  o.status = 0;
-  const int nx = fd.nhx, ny = fd.nhy, n = nx * ny;
+  const int nx = fd.nhx, ny = fd.nhy, n = nx * ny, T = hp_trees, total = n * T;
   const int32_t* L = hp_leaf + fd.hp_off;
   float cnt = 0, sum = 0, sum_sq = 0;
-  for (int xi = 0; xi < nx; xi++)
-    for (int yi = 0; yi < ny; yi++) {
-      const int q = yi * nx + xi;
-      for (int t = 0; t < hp_trees; t++) {
-        const float m = hp_m[L[(int64_t)t * n + q]];
-        if (m >= 0.f) {
-          sum += m;
-          sum_sq += m * m;
-          cnt++;
-        }
-      }
+  for (int base = 0; base < total; base += 64) {
+    const int k = base + lane;
+    float m = 0.f, mm = 0.f, one = 0.f;
+    if (k < total) {
+      const int pr = k / T, t = k - pr * T;
+      const int xi = pr / ny, yi = pr - xi * ny;
+      const float v = hp_m[L[(int64_t)t * n + yi * nx + xi]];
+      if (v >= 0.f) { m = v; mm = v * v; one = 1.f; }
     }
+    const int lim = min(64, total - base);
+    for (int j = 0; j < lim; j++) {
+      sum += lane_f(m, j);
+      sum_sq += lane_f(mm, j);
+      cnt += lane_f(one, j);
+    }
+  }
   float mean = sum / cnt;
   float var = (sum_sq / cnt) - (mean * mean);
   mean -= 2;
   var *= 0.05f;  // NORM_HEADPOSE_VARIANCE_FACTOR
+  // areaUnderCurve per pose bin: lane j < n_forests integrates bin j
+  const float poseT[6] = {-2.5f, -0.35f, -0.20f, 0.20f, 0.35f, 2.5f};
+  float area = 0.f;
+  if (lane < n_forests) {
+    const double dmean = (double)mean, dstd = __builtin_sqrt((double)var);
+    double acc = 0, step = 0.01, tt;
+    for (double x = poseT[lane]; x < (double)poseT[lane + 1]; x += step) {
+      tt = (x - dmean) / dstd;
+      acc += ffd_exp(-0.5 * (tt * tt)) * step;
+    }
+    area = (float)(acc * 1.0 / (dstd * 2.5066282746310002));
+  }
+  if (lane != 0) return;
+  o.status = 0;
   o.headpose = mean;
   o.pose_variance = var;
   HpState& s = state[f];
   s.headpose = mean;
   s.variance = var;
-  const float poseT[6] = {-2.5f, -0.35f, -0.20f, 0.20f, 0.35f, 2.5f};
-  const double dmean = (double)mean, dstd = __builtin_sqrt((double)var);
   float max_area = 0;
   int dominant = 0;
   for (int j = 0; j < n_forests; j++) {
-    double acc = 0, step = 0.01, tt;
-    for (double x = poseT[j]; x < (double)poseT[j + 1]; x += step) {
-      tt = (x - dmean) / dstd;
-      acc += ffd_exp(-0.5 * (tt * tt)) * step;
-    }
-    const float area = (float)(acc * 1.0 / (dstd * 2.5066282746310002));
-    s.pose_freq[j] = area;
-    if (max_area < area) { max_area = area; dominant = j; }
+    const float a = lane_f(area, j);
+    s.pose_freq[j] = a;
+    if (max_area < a) { max_area = a; dominant = j; }
   }
   int nt_total = 0;
   for (int i = 0; i < n_forests; i++) {
@@ -440,18 +550,71 @@ __global__ void k_hp_pose(const FaceDesc* __restrict__ faces, int n_faces, const
   o.n_trees = nt_total;
 }
 
-// ----------------------------------------------------- votes + MeanShift ----
-// One thread per (face, landmark).  Pass 1 walks the FFD leaves in reference order
-// (patch-major x-outer, tree-minor; face_utils.cpp:277-301), compacts the landmark's
-// votes and accumulates MeanShift::getMean in the same order; then up to
-// max_iterations getWeightedMean passes (MeanShift.hpp:41-76,106-135).
-__global__ void k_votes_meanshift(const FaceDesc* __restrict__ faces, int n_faces,
-                                  const int32_t* __restrict__ mp_leaf, const uint32_t* __restrict__ mask,
-                                  const float* __restrict__ fg, const int32_t* __restrict__ offs,
-                                  const HpState* __restrict__ state, int tslots, int step, int half_patch,
-                                  int n_parts, float lamda, int max_iter, float stop, Vote* __restrict__ votes,
-                                  float* __restrict__ ms_mean, int32_t* __restrict__ vote_counts,
-                                  FaceOut* __restrict__ out) {
+// ------------------------------------------------------------ vote lists ----
+// getFacialFeaturesVotesMT vote filter (face_utils.cpp:276-301).  One wave per face walks the
+// FFD leaves in reference order (patch-major x-outer, tree-minor), 64 at a time; for each
+// landmark a ballot + popcount gives every voting lane its slot, so the compacted list keeps
+// the reference's vote order exactly.
+__global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ faces, int n_faces,
+                                               const int32_t* __restrict__ mp_leaf,
+                                               const uint32_t* __restrict__ mask, const float* __restrict__ fg,
+                                               const int32_t* __restrict__ offs, const HpState* __restrict__ state,
+                                               int tslots, int step, int half_patch, int n_parts,
+                                               Vote* __restrict__ votes, int32_t* __restrict__ vote_counts) {
+  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (f >= n_faces) return;
+  const FaceDesc& fd = faces[f];
+  if (!fd.valid) return;
+  const int nx = fd.nmx, ny = fd.nmy, n = nx * ny, T = state[f].n_trees, total = n * T;
+  const int64_t cap = (int64_t)tslots * n;
+  const int32_t* L = mp_leaf + fd.mp_off;
+  Vote* V = votes + fd.vote_off;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int cnt[NPARTS];
+#pragma unroll
+  for (int i = 0; i < NPARTS; i++) cnt[i] = 0;
+  for (int base = 0; base < total; base += 64) {
+    const int k = base + lane;
+    uint32_t mk = 0;
+    int leaf = 0, vx0 = 0, vy0 = 0;
+    if (k < total) {
+      const int pr = k / T, t = k - pr * T;
+      const int xi = pr / ny, yi = pr - xi * ny;
+      leaf = L[(int64_t)t * n + yi * nx + xi];
+      mk = mask[leaf];
+      vx0 = xi * step + half_patch;
+      vy0 = yi * step + half_patch;
+    }
+    const float w = mk ? fg[leaf] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NPARTS; i++) {  // mask bits >= n_parts are never set (engine load)
+      const bool vote = (mk >> i) & 1u;
+      const uint64_t bal = __ballot(vote);
+      if (vote) {
+        const int pos = cnt[i] + __popcll(bal & below);
+        const int32_t o = offs[(int64_t)leaf * NPARTS + i];
+        V[i * cap + pos] = Vote{(int16_t)((int)(int16_t)(o & 0xFFFF) + vx0), (int16_t)((int)(int16_t)(o >> 16) + vy0), w};
+      }
+      cnt[i] += __popcll(bal);
+    }
+  }
+  if (lane < n_parts) {
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < NPARTS; i++)
+      if (i == lane) c = cnt[i];
+    vote_counts[(int64_t)f * NPARTS + lane] = c;
+  }
+}
+
+// -------------------------------------------------------------- MeanShift ----
+// MeanShift::shift (MeanShift.hpp:41-135) over one landmark's compacted vote list, in list
+// order; then the rescale of FaceForest.cpp:255-257.  One thread per (face, landmark).
+__global__ void k_meanshift(const FaceDesc* __restrict__ faces, int n_faces, const HpState* __restrict__ state,
+                            int tslots, int n_parts, float lamda, int max_iter, float stop,
+                            const Vote* __restrict__ votes, const int32_t* __restrict__ vote_counts,
+                            float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int f = gid / NPARTS, part = gid % NPARTS;
   if (f >= n_faces) return;
@@ -462,32 +625,19 @@ __global__ void k_votes_meanshift(const FaceDesc* __restrict__ faces, int n_face
     out[f].points[part][1] = 0;
     return;
   }
-  const int nx = fd.nmx, ny = fd.nmy, n = nx * ny, T = state[f].n_trees;
-  const int32_t* L = mp_leaf + fd.mp_off;
-  Vote* V = votes + fd.vote_off + (int64_t)part * tslots * n;
-  int cnt = 0;
+  const int n = fd.nmx * fd.nmy;
+  const Vote* V = votes + fd.vote_off + (int64_t)part * tslots * n;
+  const int cnt = vote_counts[(int64_t)f * NPARTS + part];
   float mx = 0, my = 0, sw = 0;
-  const uint32_t bit = 1u << part;
-  for (int xi = 0; xi < nx; xi++)
-    for (int yi = 0; yi < ny; yi++) {
-      const int q = yi * nx + xi;
-      const int ox = xi * step + half_patch, oy = yi * step + half_patch;
-      for (int t = 0; t < T; t++) {
-        const int leaf = L[(int64_t)t * n + q];
-        if (mask[leaf] & bit) {
-          const int32_t o = offs[(int64_t)leaf * NPARTS + part];
-          const int vx = (int)(int16_t)(o & 0xFFFF) + ox, vy = (int)(int16_t)(o >> 16) + oy;
-          const float w = fg[leaf];
-          V[cnt++] = Vote{(int16_t)vx, (int16_t)vy, w};
-          mx += vx * w;
-          my += vy * w;
-          sw += w;
-        }
-      }
-    }
+  for (int k = 0; k < cnt; k++) {  // getMean
+    const Vote v = V[k];
+    mx += v.x * v.w;
+    my += v.y * v.w;
+    sw += v.w;
+  }
   if (sw > 0) { mx /= sw; my /= sw; }
   bool conv = false;
-  for (int it = 0; it < max_iter && !conv; it++) {
+  for (int it = 0; it < max_iter && !conv; it++) {  // getWeightedMean
     float sx = 0, sy = 0, s = 0;
     for (int k = 0; k < cnt; k++) {
       const Vote v = V[k];
@@ -507,33 +657,27 @@ __global__ void k_votes_meanshift(const FaceDesc* __restrict__ faces, int n_face
   }
   ms_mean[((int64_t)f * NPARTS + part) * 2] = mx;
   ms_mean[((int64_t)f * NPARTS + part) * 2 + 1] = my;
-  vote_counts[(int64_t)f * NPARTS + part] = cnt;
   const float inv = 1.0f / fd.scale;  // FaceForest.cpp:255-257
   out[f].points[part][0] = cv_round((float)cv_round(mx) * inv);
   out[f].points[part][1] = cv_round((float)cv_round(my) * inv);
 }
 
 // ------------------------------------------------------------------ launch --
-hipError_t upload_gabor(const float* coef, hipStream_t s) {
-  return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_gabor), coef, sizeof(float) * GABOR_COEF_TOTAL, 0,
-                                hipMemcpyHostToDevice, s);
-}
-
 void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s) {
   k_gray_resize<<<n, 256, 0, s>>>(faces, images, gray);
 }
 
-void launch_gabor(int nu, const FaceDesc* faces, int n, int max_w, int max_h, const uint8_t* gray, float* mag,
-                  uint32_t* minmax, hipStream_t s) {
-  const int tiles = ((max_w + 15) / 16) * ((max_h + 15) / 16);
+void launch_gabor(int nu, const FaceDesc* faces, int n, int max_w, int max_h, const uint8_t* gray,
+                  const float4* coef, float* mag, uint32_t* minmax, hipStream_t s) {
+  const int tiles = ((max_w + GB_TX - 1) / GB_TX) * ((max_h + GB_TY - 1) / GB_TY);
   if (tiles <= 0 || n <= 0) return;
   dim3 grid(tiles, n);
   switch (nu) {
-    case 4: k_gabor<25><<<grid, 256, 0, s>>>(faces, gray, mag, minmax); break;
-    case 3: k_gabor<19><<<grid, 256, 0, s>>>(faces, gray, mag, minmax); break;
-    case 2: k_gabor<13><<<grid, 256, 0, s>>>(faces, gray, mag, minmax); break;
-    case 1: k_gabor<9><<<grid, 256, 0, s>>>(faces, gray, mag, minmax); break;
-    default: k_gabor<7><<<grid, 256, 0, s>>>(faces, gray, mag, minmax); break;
+    case 4: k_gabor<25><<<grid, GB_THREADS, 0, s>>>(faces, gray, coef, mag, minmax); break;
+    case 3: k_gabor<19><<<grid, GB_THREADS, 0, s>>>(faces, gray, coef, mag, minmax); break;
+    case 2: k_gabor<13><<<grid, GB_THREADS, 0, s>>>(faces, gray, coef, mag, minmax); break;
+    case 1: k_gabor<9><<<grid, GB_THREADS, 0, s>>>(faces, gray, coef, mag, minmax); break;
+    default: k_gabor<7><<<grid, GB_THREADS, 0, s>>>(faces, gray, coef, mag, minmax); break;
   }
 }
 
@@ -543,17 +687,16 @@ void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, const fl
   k_integral<<<grid, 256, 0, s>>>(faces, gray, mag, minmax, chan);
 }
 
-void launch_traverse(bool hp, const FaceDesc* faces, const int64_t* wave_start, int n, int64_t total_waves,
-                     const uint4* nodes, const int32_t* roots, const HpState* state, int tslots, int step,
-                     const uint32_t* chan, int32_t* leaf_out, hipStream_t s) {
-  if (total_waves <= 0) return;
-  const unsigned blocks = (unsigned)((total_waves + 3) / 4);
+void launch_traverse(bool hp, const FaceDesc* faces, const int32_t* block_start, int n, int total_blocks,
+                     const uint4* nodes, const int32_t* roots, const int32_t* tree_nodes, const HpState* state,
+                     int step, const uint32_t* chan, int32_t* leaf_out, hipStream_t s) {
+  if (total_blocks <= 0) return;
   if (hp)
-    k_traverse<true><<<blocks, 256, 0, s>>>(faces, wave_start, n, total_waves, nodes, roots, state, tslots, step,
-                                            chan, leaf_out);
+    k_traverse<true><<<total_blocks, 256, 0, s>>>(faces, block_start, n, nodes, roots, tree_nodes, state, step, chan,
+                                                  leaf_out);
   else
-    k_traverse<false><<<blocks, 256, 0, s>>>(faces, wave_start, n, total_waves, nodes, roots, state, tslots, step,
-                                             chan, leaf_out);
+    k_traverse<false><<<total_blocks, 256, 0, s>>>(faces, block_start, n, nodes, roots, tree_nodes, state, step, chan,
+                                                   leaf_out);
 }
 
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
@@ -567,18 +710,22 @@ void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t
 
 void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const float* hp_m, int hp_trees,
                     int n_forests, int ntrees_per_forest, HpState* state, FaceOut* out, hipStream_t s) {
-  k_hp_pose<<<(n + 63) / 64, 64, 0, s>>>(faces, n, hp_leaf, hp_m, hp_trees, n_forests, ntrees_per_forest, state,
-                                         out);
+  k_hp_pose<<<(n + 3) / 4, 256, 0, s>>>(faces, n, hp_leaf, hp_m, hp_trees, n_forests, ntrees_per_forest, state, out);
 }
 
-void launch_votes_meanshift(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint32_t* mask,
-                            const float* fg, const int32_t* offs, const HpState* state, int tslots, int step,
-                            int half_patch, int n_parts, float lamda, int max_iter, float stop, Vote* votes,
-                            float* ms_mean, int32_t* vote_counts, FaceOut* out, hipStream_t s) {
+void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint32_t* mask, const float* fg,
+                  const int32_t* offs, const HpState* state, int tslots, int step, int half_patch, int n_parts,
+                  Vote* votes, int32_t* vote_counts, hipStream_t s) {
+  k_votes<<<(n + 3) / 4, 256, 0, s>>>(faces, n, mp_leaf, mask, fg, offs, state, tslots, step, half_patch, n_parts,
+                                      votes, vote_counts);
+}
+
+void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int tslots, int n_parts, float lamda,
+                      int max_iter, float stop, const Vote* votes, const int32_t* vote_counts, float* ms_mean,
+                      FaceOut* out, hipStream_t s) {
   const int total = n * NPARTS;
-  k_votes_meanshift<<<(total + 63) / 64, 64, 0, s>>>(faces, n, mp_leaf, mask, fg, offs, state, tslots, step,
-                                                     half_patch, n_parts, lamda, max_iter, stop, votes, ms_mean,
-                                                     vote_counts, out);
+  k_meanshift<<<(total + 63) / 64, 64, 0, s>>>(faces, n, state, tslots, n_parts, lamda, max_iter, stop, votes,
+                                               vote_counts, ms_mean, out);
 }
 
 }  // namespace ffd

@@ -9,9 +9,9 @@
 
 namespace ffd {
 
-// Gabor coefficient table layout in __constant__ memory (see k_gabor).
+// Gabor coefficient table layout (see k_gabor): 16 floats per tap / pair (+ centre for W >= 9).
 constexpr int GABOR_WIDTHS[5] = {7, 9, 13, 19, 25};
-constexpr int gabor_block(int w) { return w == 7 ? 49 * 14 : ((w * w - 1) / 2) * 14 + 7; }
+constexpr int gabor_block(int w) { return w == 7 ? 49 * 16 : ((w * w - 1) / 2 + 1) * 16; }
 constexpr int GABOR_OFF0 = 0;
 constexpr int GABOR_OFF1 = GABOR_OFF0 + gabor_block(7);
 constexpr int GABOR_OFF2 = GABOR_OFF1 + gabor_block(9);
@@ -20,23 +20,24 @@ constexpr int GABOR_OFF4 = GABOR_OFF3 + gabor_block(19);
 constexpr int GABOR_COEF_TOTAL = GABOR_OFF4 + gabor_block(25);
 constexpr int GABOR_OFFS[5] = {GABOR_OFF0, GABOR_OFF1, GABOR_OFF2, GABOR_OFF3, GABOR_OFF4};
 
-hipError_t upload_gabor(const float* coef, hipStream_t s);
 void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s);
-void launch_gabor(int nu, const FaceDesc* faces, int n, int max_w, int max_h, const uint8_t* gray, float* mag,
-                  uint32_t* minmax, hipStream_t s);
+void launch_gabor(int nu, const FaceDesc* faces, int n, int max_w, int max_h, const uint8_t* gray,
+                  const float4* coef, float* mag, uint32_t* minmax, hipStream_t s);
 void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, const float* mag, const uint32_t* minmax,
                      uint32_t* chan, hipStream_t s);
-void launch_traverse(bool hp, const FaceDesc* faces, const int64_t* wave_start, int n, int64_t total_waves,
-                     const uint4* nodes, const int32_t* roots, const HpState* state, int tslots, int step,
-                     const uint32_t* chan, int32_t* leaf_out, hipStream_t s);
+void launch_traverse(bool hp, const FaceDesc* faces, const int32_t* block_start, int n, int total_blocks,
+                     const uint4* nodes, const int32_t* roots, const int32_t* tree_nodes, const HpState* state,
+                     int step, const uint32_t* chan, int32_t* leaf_out, hipStream_t s);
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
                          const int32_t* patches, int n_patches, const uint32_t* chan, int64_t plane,
                          int32_t* leaf_ids, hipStream_t s);
 void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const float* hp_m, int hp_trees,
                     int n_forests, int ntrees_per_forest, HpState* state, FaceOut* out, hipStream_t s);
-void launch_votes_meanshift(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint32_t* mask,
-                            const float* fg, const int32_t* offs, const HpState* state, int tslots, int step,
-                            int half_patch, int n_parts, float lamda, int max_iter, float stop, Vote* votes,
-                            float* ms_mean, int32_t* vote_counts, FaceOut* out, hipStream_t s);
+void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint32_t* mask, const float* fg,
+                  const int32_t* offs, const HpState* state, int tslots, int step, int half_patch, int n_parts,
+                  Vote* votes, int32_t* vote_counts, hipStream_t s);
+void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int tslots, int n_parts, float lamda,
+                      int max_iter, float stop, const Vote* votes, const int32_t* vote_counts, float* ms_mean,
+                      FaceOut* out, hipStream_t s);
 
 }  // namespace ffd

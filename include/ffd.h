@@ -167,7 +167,7 @@ ffd_status ffd_get_trace(ffd_engine* engine, int32_t index, ffd_trace* trace);
 /* Per-stage device time of the pipeline, measured with hipEvents on the engine stream
  * (kernel boundaries only; used by bench.py for the roofline of the dominant kernel).
  * ffd_set_profiling(e, 1) enables and resets the accumulators. */
-#define FFD_NUM_STAGES 11
+#define FFD_NUM_STAGES 12
 ffd_status ffd_set_profiling(ffd_engine* engine, int32_t enable);
 ffd_status ffd_get_stage_times(ffd_engine* engine, double* total_ms, int64_t* launches, int32_t n_stages);
 const char* ffd_stage_name(int32_t stage);
