@@ -14,6 +14,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -79,6 +80,9 @@ struct ffd_engine {
   hipStream_t stream = nullptr;
   ffd_engine_desc desc{};
   int max_chunk = 1024;
+  // traversal tuning: LDS bytes per (face, tree) workgroup (staged tree top; also caps occupancy)
+  // and interleaved walks per thread.  Overridable with FFD_TRAV_LDS_KB_{HP,FFD} / FFD_TRAV_WALKS.
+  int trav_lds_hp = 16 * 1024, trav_lds_mp = 16 * 1024, trav_walks = 2;
 
   // model parameters
   int face_size = 125, patch = 31, hp_trees = 0, n_forests = 0, ntrees_per_forest = 0;
@@ -439,7 +443,7 @@ void ffd_engine::run_chunk(std::vector<FaceDesc>& fds, const uint8_t* d_images, 
   stage(7, [&] {
     launch_traverse(true, dfd, wave_hp.as<int32_t>(), n, ws_hp[n], hp_nodes.as<uint4>(), hp_roots.as<int32_t>(),
                     hp_sizes.as<int32_t>(), nullptr, desc.hp_option.step_size, chan.as<uint32_t>(),
-                    hpleaf.as<int32_t>(), stream);
+                    hpleaf.as<int32_t>(), trav_lds_hp, trav_walks, stream);
   });
   stage(8, [&] {
     launch_hp_pose(dfd, n, hpleaf.as<int32_t>(), hp_m.as<float>(), hp_trees, n_forests, ntrees_per_forest,
@@ -463,7 +467,7 @@ void ffd_engine::run_chunk(std::vector<FaceDesc>& fds, const uint8_t* d_images, 
   stage(9, [&] {
     launch_traverse(false, dfd, wave_mp.as<int32_t>(), n, ws_mp[n], mp_nodes.as<uint4>(), mp_roots.as<int32_t>(),
                     mp_sizes.as<int32_t>(), state.as<HpState>(), desc.mp_option.step_size, chan.as<uint32_t>(),
-                    mpleaf.as<int32_t>(), stream);
+                    mpleaf.as<int32_t>(), trav_lds_mp, trav_walks, stream);
   });
   const int n_parts = std::min(desc.mp_option.num_parts, NPARTS);
   stage(10, [&] {
@@ -579,6 +583,9 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   std::unique_ptr<ffd_engine> e(new ffd_engine());
   e->desc = *d;
   e->device = d->device;
+  if (const char* v = std::getenv("FFD_TRAV_LDS_KB_HP")) e->trav_lds_hp = std::max(1, std::atoi(v)) * 1024;
+  if (const char* v = std::getenv("FFD_TRAV_LDS_KB_FFD")) e->trav_lds_mp = std::max(1, std::atoi(v)) * 1024;
+  if (const char* v = std::getenv("FFD_TRAV_WALKS")) e->trav_walks = std::atoi(v);
   if (d->max_chunk_faces > 0) e->max_chunk = d->max_chunk_faces;
   try {
     int ndev = 0;

@@ -372,12 +372,12 @@ __device__ __forceinline__ uint32_t walk(const uint4* __restrict__ nodes, uint32
   return nd.x & ~LEAF_BIT;
 }
 
-// One workgroup = one (face, tree): the tree's first TOP_NODES breadth-first nodes (its top
-// ~10 levels, which every walk visits) are staged in LDS; each thread then walks two patches
-// at a time (lane order, so a wave's 64 lanes read horizontally adjacent patches) to keep two
-// independent gather chains in flight.  block_start[f] = first block of face f.
-constexpr int TOP_NODES = 1024;
-
+// One workgroup = one (face, tree).  The tree's first `top_nodes` breadth-first nodes (its top
+// levels, which every walk visits) are staged in LDS; the LDS size is a launch parameter, so it
+// also caps the workgroups per CU and with them the number of faces whose 2.4 MB channel sets
+// are live in one XCD's 4 MB L2 (face-major block order + XCD remap keep a face on one XCD).
+// Each thread walks NW patches at once (lane order: a wave's lanes read horizontally adjacent
+// patches) so NW independent gather chains are in flight per lane.
 struct WalkCtx {
   const uint4* __restrict__ nodes;
   const uint4* top;       // LDS copy of nodes[root .. root+ntop)
@@ -398,15 +398,15 @@ __device__ __forceinline__ uint32_t split_child(const WalkCtx& c, const uint4& n
   return nd.x + ((p1 - p2) <= (int)nd.z ? 0u : 1u);
 }
 
-template <bool HP>
+template <bool HP, int NW>
 __global__ __launch_bounds__(256) void k_traverse(const FaceDesc* __restrict__ faces,
                                                   const int32_t* __restrict__ block_start, int n_faces,
                                                   const uint4* __restrict__ nodes, const int32_t* __restrict__ roots,
                                                   const int32_t* __restrict__ tree_nodes,
-                                                  const HpState* __restrict__ hp_state, int step,
+                                                  const HpState* __restrict__ hp_state, int step, int top_cap,
                                                   const uint32_t* __restrict__ chan,
                                                   int32_t* __restrict__ leaf_out) {
-  __shared__ uint4 top[TOP_NODES];
+  extern __shared__ uint4 top[];
   const int lb = (int)xcd_remap(blockIdx.x, gridDim.x);
   int lo = 0, hi = n_faces - 1;
   while (lo < hi) {  // last f with block_start[f] <= lb
@@ -421,32 +421,44 @@ __global__ __launch_bounds__(256) void k_traverse(const FaceDesc* __restrict__ f
   c.nodes = nodes;
   c.top = top;
   c.root = (uint32_t)roots[tree];
-  c.ntop = (uint32_t)min(TOP_NODES, tree_nodes[tree]);
+  c.ntop = (uint32_t)min(top_cap, tree_nodes[tree]);
   c.chan = chan + fd.ch_off;
   c.plane = (uint32_t)fd.plane;
   for (uint32_t i = threadIdx.x; i < c.ntop; i += 256) top[i] = nodes[c.root + i];
   __syncthreads();
   const int nx = HP ? fd.nhx : fd.nmx, ny = HP ? fd.nhy : fd.nmy, n = nx * ny;
   int32_t* out = leaf_out + (HP ? fd.hp_off : fd.mp_off) + (int64_t)t * n;
-  for (int q0 = threadIdx.x; q0 < n; q0 += 512) {
-    const int q1 = q0 + 256;
-    const bool va = true, vb = q1 < n;
-    const uint32_t pa = (uint32_t)(((q0 / nx) * PITCH + (q0 % nx)) * step);
-    const uint32_t pb = vb ? (uint32_t)(((q1 / nx) * PITCH + (q1 % nx)) * step) : pa;
-    uint4 A = c.top[0], B = c.top[0];
-    bool da = !va, db = !vb;
-    for (;;) {
-      da = da || (A.x & LEAF_BIT);
-      db = db || (B.x & LEAF_BIT);
-      if (da && db) break;
-      uint32_t na = 0, nb = 0;
-      if (!da) na = split_child(c, A, pa);
-      if (!db) nb = split_child(c, B, pb);
-      if (!da) A = fetch_node(c, na);
-      if (!db) B = fetch_node(c, nb);
+  for (int q0 = threadIdx.x; q0 < n; q0 += 256 * NW) {
+    uint32_t poff[NW];
+    uint4 nd[NW];
+    bool done[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      const int q = q0 + w * 256;
+      done[w] = q >= n;
+      poff[w] = done[w] ? 0u : (uint32_t)(((q / nx) * PITCH + (q % nx)) * step);
+      nd[w] = c.top[0];
     }
-    out[q0] = (int32_t)(A.x & ~LEAF_BIT);
-    if (vb) out[q1] = (int32_t)(B.x & ~LEAF_BIT);
+    for (;;) {
+      bool all = true;
+#pragma unroll
+      for (int w = 0; w < NW; w++) {
+        done[w] = done[w] || (nd[w].x & LEAF_BIT);
+        all = all && done[w];
+      }
+      if (all) break;
+      uint32_t nxt[NW];
+#pragma unroll
+      for (int w = 0; w < NW; w++) nxt[w] = done[w] ? 0u : split_child(c, nd[w], poff[w]);
+#pragma unroll
+      for (int w = 0; w < NW; w++)
+        if (!done[w]) nd[w] = fetch_node(c, nxt[w]);
+    }
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      const int q = q0 + w * 256;
+      if (q < n) out[q] = (int32_t)(nd[w].x & ~LEAF_BIT);
+    }
   }
 }
 
@@ -628,26 +640,49 @@ __global__ void k_meanshift(const FaceDesc* __restrict__ faces, int n_faces, con
   const int n = fd.nmx * fd.nmy;
   const Vote* V = votes + fd.vote_off + (int64_t)part * tslots * n;
   const int cnt = vote_counts[(int64_t)f * NPARTS + part];
+  // Votes are read 8 at a time (independent loads, independent per-vote weights: ILP across the
+  // 8 chains); the three running sums still advance strictly in list order.
+  constexpr int G = 8;
   float mx = 0, my = 0, sw = 0;
-  for (int k = 0; k < cnt; k++) {  // getMean
-    const Vote v = V[k];
-    mx += v.x * v.w;
-    my += v.y * v.w;
-    sw += v.w;
+  for (int k0 = 0; k0 < cnt; k0 += G) {  // getMean
+    Vote v[G];
+#pragma unroll
+    for (int j = 0; j < G; j++) v[j] = (k0 + j < cnt) ? V[k0 + j] : Vote{0, 0, 0.f};
+#pragma unroll
+    for (int j = 0; j < G; j++) {
+      if (k0 + j < cnt) {
+        mx += v[j].x * v[j].w;
+        my += v[j].y * v[j].w;
+        sw += v[j].w;
+      }
+    }
   }
   if (sw > 0) { mx /= sw; my /= sw; }
   bool conv = false;
   for (int it = 0; it < max_iter && !conv; it++) {  // getWeightedMean
     float sx = 0, sy = 0, s = 0;
-    for (int k = 0; k < cnt; k++) {
-      const Vote v = V[k];
-      const float dx = mx - (float)v.x, dy = my - (float)v.y;
-      float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
-      d = ffd_expf(-d / lamda);
-      const float w = v.w * d;
-      sx += v.x * w;
-      sy += v.y * w;
-      s += w;
+    for (int k0 = 0; k0 < cnt; k0 += G) {
+      Vote v[G];
+#pragma unroll
+      for (int j = 0; j < G; j++) v[j] = (k0 + j < cnt) ? V[k0 + j] : Vote{0, 0, 0.f};
+      float w[G], px[G], py[G];
+#pragma unroll
+      for (int j = 0; j < G; j++) {
+        const float dx = mx - (float)v[j].x, dy = my - (float)v[j].y;
+        float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
+        d = ffd_expf(-d / lamda);
+        w[j] = v[j].w * d;
+        px[j] = v[j].x * w[j];
+        py[j] = v[j].y * w[j];
+      }
+#pragma unroll
+      for (int j = 0; j < G; j++) {
+        if (k0 + j < cnt) {
+          sx += px[j];
+          sy += py[j];
+          s += w[j];
+        }
+      }
     }
     if (s > 0) { sx /= s; sy /= s; }
     const float ddx = sx - mx, ddy = sy - my;
@@ -689,14 +724,18 @@ void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, const fl
 
 void launch_traverse(bool hp, const FaceDesc* faces, const int32_t* block_start, int n, int total_blocks,
                      const uint4* nodes, const int32_t* roots, const int32_t* tree_nodes, const HpState* state,
-                     int step, const uint32_t* chan, int32_t* leaf_out, hipStream_t s) {
+                     int step, const uint32_t* chan, int32_t* leaf_out, int lds_bytes, int walks, hipStream_t s) {
   if (total_blocks <= 0) return;
-  if (hp)
-    k_traverse<true><<<total_blocks, 256, 0, s>>>(faces, block_start, n, nodes, roots, tree_nodes, state, step, chan,
-                                                  leaf_out);
-  else
-    k_traverse<false><<<total_blocks, 256, 0, s>>>(faces, block_start, n, nodes, roots, tree_nodes, state, step, chan,
-                                                   leaf_out);
+  const int cap = lds_bytes / (int)sizeof(uint4);
+#define FFD_TRAV(HPV, NWV)                                                                                   \
+  k_traverse<HPV, NWV><<<total_blocks, 256, lds_bytes, s>>>(faces, block_start, n, nodes, roots, tree_nodes, \
+                                                            state, step, cap, chan, leaf_out)
+  if (hp) {
+    if (walks >= 4) FFD_TRAV(true, 4); else if (walks == 1) FFD_TRAV(true, 1); else FFD_TRAV(true, 2);
+  } else {
+    if (walks >= 4) FFD_TRAV(false, 4); else if (walks == 1) FFD_TRAV(false, 1); else FFD_TRAV(false, 2);
+  }
+#undef FFD_TRAV
 }
 
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
