@@ -378,24 +378,23 @@ __device__ __forceinline__ uint32_t walk(const uint4* __restrict__ nodes, uint32
 // are live in one XCD's 4 MB L2 (face-major block order + XCD remap keep a face on one XCD).
 // Each thread walks NW patches at once (lane order: a wave's lanes read horizontally adjacent
 // patches) so NW independent gather chains are in flight per lane.
-struct WalkCtx {
-  const uint4* __restrict__ nodes;
-  const uint4* top;       // LDS copy of nodes[root .. root+ntop)
-  uint32_t root, ntop;
-  const uint32_t* __restrict__ chan;  // face's channel base (uniform)
-  uint32_t plane;
-};
+// gfx9 raw buffer resource word 3 (as CK uses for gfx94x/gfx950).
+constexpr int BUF_WORD3 = 0x00020000;
 
-__device__ __forceinline__ uint4 fetch_node(const WalkCtx& c, uint32_t node) {
-  const uint32_t r = node - c.root;
-  return r < c.ntop ? c.top[r] : c.nodes[node];
-}
-
-__device__ __forceinline__ uint32_t split_child(const WalkCtx& c, const uint4& nd, uint32_t poff) {
-  const uint32_t* I = c.chan + (nd.y & 63u) * c.plane + poff;
-  const int p1 = rect_mean(I, nd.w & 0xFFFFu, (nd.y >> 6) & 31u, (nd.y >> 11) & 31u);
-  const int p2 = rect_mean(I, nd.w >> 16, (nd.y >> 16) & 31u, (nd.y >> 21) & 31u);
-  return nd.x + ((p1 - p2) <= (int)nd.z ? 0u : 1u);
+// ImageSample::evalTest on a buffer resource covering one face's 38 integral planes (byte
+// offsets are 32-bit; one VGPR per gather address).
+__device__ __forceinline__ int rect_mean_buf(__amdgpu_buffer_rsrc_t rs, uint32_t boff, uint32_t w, uint32_t h) {
+  const uint32_t a = __builtin_amdgcn_raw_buffer_load_b32(rs, boff, 0, 0);
+  const uint32_t b = __builtin_amdgcn_raw_buffer_load_b32(rs, boff + 4 * w, 0, 0);
+  const uint32_t c = __builtin_amdgcn_raw_buffer_load_b32(rs, boff + 4 * PITCH * h, 0, 0);
+  const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rs, boff + 4 * (PITCH * h + w), 0, 0);
+  const int R = (int)(d - b - c + a);
+  const int area = (int)(w * h);
+  int q = (int)((float)R * __builtin_amdgcn_rcpf((float)area));
+  const int r = R - q * area;
+  q += (r >= area) ? 1 : 0;
+  q -= (r < 0) ? 1 : 0;
+  return q;
 }
 
 template <bool HP, int NW>
@@ -417,47 +416,78 @@ __global__ __launch_bounds__(256) void k_traverse(const FaceDesc* __restrict__ f
   const int t = lb - block_start[f];
   const FaceDesc& fd = faces[f];
   const int tree = HP ? t : hp_state[f].trees[t];
-  WalkCtx c;
-  c.nodes = nodes;
-  c.top = top;
-  c.root = (uint32_t)roots[tree];
-  c.ntop = (uint32_t)min(top_cap, tree_nodes[tree]);
-  c.chan = chan + fd.ch_off;
-  c.plane = (uint32_t)fd.plane;
-  for (uint32_t i = threadIdx.x; i < c.ntop; i += 256) top[i] = nodes[c.root + i];
+  const uint32_t root = (uint32_t)roots[tree];
+  const uint32_t ntop = (uint32_t)min(top_cap, tree_nodes[tree]);
+  const uint32_t plane_b = (uint32_t)fd.plane * 4u;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(chan + fd.ch_off), (short)0, (int)(NCH * plane_b), BUF_WORD3);
+  for (uint32_t i = threadIdx.x; i < ntop; i += 256) top[i] = nodes[root + i];
   __syncthreads();
   const int nx = HP ? fd.nhx : fd.nmx, ny = HP ? fd.nhy : fd.nmy, n = nx * ny;
   int32_t* out = leaf_out + (HP ? fd.hp_off : fd.mp_off) + (int64_t)t * n;
+  // Walk state per interleaved walk (named scalars: keeps everything in VGPRs).
+  struct Walk {
+    uint4 nd;
+    uint32_t pb;  // patch byte offset in a plane
+    bool done;
+  };
+  auto step_child = [&](const Walk& k) -> uint32_t {
+    const uint4 v = k.nd;
+    const uint32_t base = (v.y & 63u) * plane_b + k.pb;
+    const int p1 = rect_mean_buf(rs, base + 4u * (v.w & 0xFFFFu), (v.y >> 6) & 31u, (v.y >> 11) & 31u);
+    const int p2 = rect_mean_buf(rs, base + 4u * (v.w >> 16), (v.y >> 16) & 31u, (v.y >> 21) & 31u);
+    return v.x + ((p1 - p2) <= (int)v.z ? 0u : 1u);
+  };
+  auto init = [&](Walk& k, int q) {
+    k.done = q >= n;
+    k.pb = k.done ? 0u : 4u * (uint32_t)(((q / nx) * PITCH + (q % nx)) * step);
+    k.nd = top[0];
+  };
   for (int q0 = threadIdx.x; q0 < n; q0 += 256 * NW) {
-    uint32_t poff[NW];
-    uint4 nd[NW];
-    bool done[NW];
-#pragma unroll
-    for (int w = 0; w < NW; w++) {
-      const int q = q0 + w * 256;
-      done[w] = q >= n;
-      poff[w] = done[w] ? 0u : (uint32_t)(((q / nx) * PITCH + (q % nx)) * step);
-      nd[w] = c.top[0];
-    }
+    Walk A, B, C, D;
+    init(A, q0);
+    init(B, q0 + 256);
+    if (NW > 2) { init(C, q0 + 512); init(D, q0 + 768); } else { C.done = D.done = true; C.nd = D.nd = A.nd; C.pb = D.pb = 0; }
     for (;;) {
-      bool all = true;
-#pragma unroll
-      for (int w = 0; w < NW; w++) {
-        done[w] = done[w] || (nd[w].x & LEAF_BIT);
-        all = all && done[w];
+      A.done = A.done || (A.nd.x & LEAF_BIT);
+      B.done = B.done || (B.nd.x & LEAF_BIT);
+      if (NW > 2) { C.done = C.done || (C.nd.x & LEAF_BIT); D.done = D.done || (D.nd.x & LEAF_BIT); }
+      if (A.done && B.done && (NW <= 2 || (C.done && D.done))) break;
+      // branch-free: every walk issues its 8 gathers before any is consumed (a finished walk
+      // re-evaluates its leaf record: channel 0, offset 0 -> in-range reads, result ignored)
+      const uint32_t na = step_child(A), nb = step_child(B);
+      uint32_t nc = 0, ndd = 0;
+      if (NW > 2) { nc = step_child(C); ndd = step_child(D); }
+      // next node: LDS for the staged top levels, else global; both reads issued for every walk
+      const uint32_t ra = na - root, rb = nb - root, rc = nc - root, rd = ndd - root;
+      const bool ta = ra < ntop, tb = rb < ntop, tc = rc < ntop, td = rd < ntop;
+      const uint4 ga = nodes[(A.done || ta) ? root : na];
+      const uint4 gb = nodes[(B.done || tb) ? root : nb];
+      const uint4 la = top[ta ? ra : 0u];
+      const uint4 lb2 = top[tb ? rb : 0u];
+      uint4 gc = ga, gd = ga, lc = la, ld = la;
+      if (NW > 2) {
+        gc = nodes[(C.done || tc) ? root : nc];
+        gd = nodes[(D.done || td) ? root : ndd];
+        lc = top[tc ? rc : 0u];
+        ld = top[td ? rd : 0u];
       }
-      if (all) break;
-      uint32_t nxt[NW];
-#pragma unroll
-      for (int w = 0; w < NW; w++) nxt[w] = done[w] ? 0u : split_child(c, nd[w], poff[w]);
-#pragma unroll
-      for (int w = 0; w < NW; w++)
-        if (!done[w]) nd[w] = fetch_node(c, nxt[w]);
+      auto pick = [](bool keep, const uint4& cur, bool t, const uint4& l, const uint4& g) {
+        const uint4 nv = t ? l : g;  // selects, not branches: keeps the walks' work unconditional
+        return make_uint4(keep ? cur.x : nv.x, keep ? cur.y : nv.y, keep ? cur.z : nv.z, keep ? cur.w : nv.w);
+      };
+      A.nd = pick(A.done, A.nd, ta, la, ga);
+      B.nd = pick(B.done, B.nd, tb, lb2, gb);
+      if (NW > 2) {
+        C.nd = pick(C.done, C.nd, tc, lc, gc);
+        D.nd = pick(D.done, D.nd, td, ld, gd);
+      }
     }
-#pragma unroll
-    for (int w = 0; w < NW; w++) {
-      const int q = q0 + w * 256;
-      if (q < n) out[q] = (int32_t)(nd[w].x & ~LEAF_BIT);
+    if (q0 < n) out[q0] = (int32_t)(A.nd.x & ~LEAF_BIT);
+    if (q0 + 256 < n) out[q0 + 256] = (int32_t)(B.nd.x & ~LEAF_BIT);
+    if (NW > 2) {
+      if (q0 + 512 < n) out[q0 + 512] = (int32_t)(C.nd.x & ~LEAF_BIT);
+      if (q0 + 768 < n) out[q0 + 768] = (int32_t)(D.nd.x & ~LEAF_BIT);
     }
   }
 }
@@ -731,9 +761,9 @@ void launch_traverse(bool hp, const FaceDesc* faces, const int32_t* block_start,
   k_traverse<HPV, NWV><<<total_blocks, 256, lds_bytes, s>>>(faces, block_start, n, nodes, roots, tree_nodes, \
                                                             state, step, cap, chan, leaf_out)
   if (hp) {
-    if (walks >= 4) FFD_TRAV(true, 4); else if (walks == 1) FFD_TRAV(true, 1); else FFD_TRAV(true, 2);
+    if (walks >= 4) FFD_TRAV(true, 4); else FFD_TRAV(true, 2);
   } else {
-    if (walks >= 4) FFD_TRAV(false, 4); else if (walks == 1) FFD_TRAV(false, 1); else FFD_TRAV(false, 2);
+    if (walks >= 4) FFD_TRAV(false, 4); else FFD_TRAV(false, 2);
   }
 #undef FFD_TRAV
 }
