@@ -137,7 +137,7 @@ def main():
     gathered = torch.empty(world * n * rec, dtype=torch.uint8, device=dev) if (world > 1 and rank == 0) else None
     torch.cuda.synchronize()
 
-    chunk = args.chunk if 0 < args.chunk < n else n
+    chunk = args.chunk if 0 < args.chunk < n else 0  # 0: engine default (FFD_CHUNK)
     ff = ffd.FaceForest(ffd.FaceForestOptions(device=local, max_chunk_faces=chunk))
     boxes = [(0, 0, CROP, CROP)] * n
     box_img = np.arange(n, dtype=np.int32)
@@ -180,7 +180,8 @@ def main():
         dom = max((k for k in stages if stages[k][1] > 0), key=lambda k: stages[k][0])
         ms_total, launches = stages[dom]
         avg_ms = ms_total / launches
-        amount, unit, bound = stage_work(dom, chunk)  # one launch covers one chunk of faces
+        faces_per_launch = n * args.steps / launches  # one launch covers one chunk of faces
+        amount, unit, bound = stage_work(dom, faces_per_launch)
         achieved = amount / (avg_ms / 1e3)
         peak = FP32_PEAK_TFLOPS if unit == "TFLOP/s" else HBM_PEAK_GBS
         b_face = CROP * CROP * 3 + 2 * 38 * 126 * 126 * 4 + 100
@@ -205,7 +206,7 @@ def main():
             "parity_spot_check": bool(ok),
             "roofline": {"bound": bound, "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
                          "frac": round(achieved / peak, 4), "traffic": None,
-                         "avg_launch_ms": round(avg_ms, 4)},
+                         "avg_launch_ms": round(avg_ms, 4), "faces_per_launch": faces_per_launch},
             "path_hbm_roofline": {"b_face": b_face, "achieved_GBs": round(value * b_face / 1e9, 1),
                                   "frac": round(value * b_face / 1e9 / HBM_PEAK_GBS, 4)},
             "stage_ms_per_step": {k: round(v[0] / max(1, args.steps), 3) for k, v in stages.items()},

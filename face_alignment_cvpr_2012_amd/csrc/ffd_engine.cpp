@@ -74,15 +74,34 @@ struct Geometry {
 
 }  // namespace
 
+// Per-stream workspace: a chunk of faces runs its whole pipeline on one stream; consecutive
+// chunks alternate streams so one chunk's memory-bound traversal overlaps the next chunk's
+// VALU-bound Gabor stage, and a chunk's channel planes stay in the Infinity Cache between the
+// kernel that writes them and the traversals that read them.
+struct Workspace {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  bool pending = false;
+  DevBuf faces, gray, mag, minmax, chan, hpleaf, mpleaf, votes, state, ms_mean, vote_counts;
+  std::vector<FaceDesc> h_fds;  // host staging, reused only after `done`
+  std::vector<FaceDesc> desc;   // descriptors of the chunk last run here (ffd_get_trace)
+  int first = 0, count = 0;
+  ~Workspace() {
+    if (done) (void)hipEventDestroy(done);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
 struct ffd_engine {
   std::string err;
   int device = 0;
-  hipStream_t stream = nullptr;
   ffd_engine_desc desc{};
-  int max_chunk = 1024;
-  // traversal tuning: LDS bytes per (face, tree) workgroup (staged tree top; also caps occupancy)
-  // and interleaved walks per thread.  Overridable with FFD_TRAV_LDS_KB_{HP,FFD} / FFD_TRAV_WALKS.
-  int trav_lds_hp = 16 * 1024, trav_lds_mp = 16 * 1024, trav_walks = 2;
+  int max_chunk = 512;
+  int n_streams = 2;
+  // traversal tuning: LDS bytes per (face, tree) workgroup (staged tree top; also caps occupancy,
+  // hence the faces whose channel sets share one XCD's L2) and interleaved walks per thread.
+  // Overridable with FFD_TRAV_LDS_KB_{HP,FFD} / FFD_TRAV_WALKS / FFD_CHUNK / FFD_STREAMS.
+  int trav_lds_hp = 64 * 1024, trav_lds_mp = 64 * 1024, trav_walks = 2;
 
   // model parameters
   int face_size = 125, patch = 31, hp_trees = 0, n_forests = 0, ntrees_per_forest = 0;
@@ -91,14 +110,13 @@ struct ffd_engine {
   // device model
   DevBuf gabor_coef, hp_nodes, hp_roots, hp_sizes, hp_m, mp_nodes, mp_roots, mp_sizes, mp_mask, mp_fg, mp_offs;
 
-  // workspace
-  DevBuf faces, wave_hp, wave_mp, images, gray, mag, minmax, chan, hpleaf, mpleaf, votes, state, out,
-      ms_mean, vote_counts, maxtrees, scratch_a, scratch_b, scratch_c;
-  // host staging of per-batch tables (kept alive until the next batch: async H2D copies)
-  std::vector<FaceDesc> h_fds;
-  std::vector<int32_t> h_ws_hp, h_ws_mp;
+  std::vector<std::unique_ptr<Workspace>> ws;
+  DevBuf images, out, scratch_a, scratch_b, scratch_c;  // host-API staging (ws[0] stream)
+  int last_ws = -1;
 
-  // stage profiler (hipEvents on the engine stream)
+  hipStream_t main_stream() const { return ws[0]->stream; }
+
+  // stage profiler (hipEvents around each launch, on the launching stream)
   struct Pending { int stage; hipEvent_t a, b; };
   bool profiling = false;
   std::vector<hipEvent_t> event_pool;
@@ -112,18 +130,20 @@ struct ffd_engine {
     HIP_CHECK(hipEventCreate(&e));
     return e;
   }
-  // Run `fn` (one kernel launch) bracketed by events when profiling.
-  template <class F> void stage(int id, F&& fn) {
+  template <class F> void stage(int id, hipStream_t s, F&& fn) {
     if (!profiling) { fn(); return; }
     Pending p{id, get_event(), get_event()};
-    HIP_CHECK(hipEventRecord(p.a, stream));
+    HIP_CHECK(hipEventRecord(p.a, s));
     fn();
-    HIP_CHECK(hipEventRecord(p.b, stream));
+    HIP_CHECK(hipEventRecord(p.b, s));
     pending.push_back(p);
+  }
+  void sync_all() {
+    for (auto& w : ws) HIP_CHECK(hipStreamSynchronize(w->stream));
   }
   void resolve() {
     if (pending.empty()) return;
-    HIP_CHECK(hipStreamSynchronize(stream));
+    sync_all();
     for (auto& p : pending) {
       float ms = 0;
       HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
@@ -135,14 +155,9 @@ struct ffd_engine {
     pending.clear();
   }
 
-  // last batch bookkeeping (for ffd_get_trace)
-  std::vector<FaceDesc> last_desc;
-  int last_first = 0, last_count = 0, last_tslots = 0;
-
   ~ffd_engine() {
     for (auto& p : pending) { event_pool.push_back(p.a); event_pool.push_back(p.b); }
     for (auto e : event_pool) (void)hipEventDestroy(e);
-    if (stream) (void)hipStreamDestroy(stream);
   }
 
   Geometry geometry(int bw, int bh) const {
@@ -165,7 +180,7 @@ struct ffd_engine {
 
   void load_model(const std::string& path);
   void build_gabor();
-  void run_chunk(std::vector<FaceDesc>& fds, const uint8_t* d_images, FaceOut* d_out);
+  void run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out);
   void analyze(const uint8_t* d_images, const std::vector<FaceDesc>& all, FaceOut* d_out);
 };
 
@@ -265,15 +280,15 @@ void ffd_engine::load_model(const std::string& path) {
   std::vector<int32_t> roots, sizes;
   flatten_forest(m, "hp", nodes, roots, sizes);
   hp_trees = (int)roots.size();
-  upload(hp_nodes, nodes, stream);
-  upload(hp_roots, roots, stream);
-  upload(hp_sizes, sizes, stream);
+  upload(hp_nodes, nodes, main_stream());
+  upload(hp_roots, roots, main_stream());
+  upload(hp_sizes, sizes, main_stream());
   flatten_forest(m, "mp", nodes, roots, sizes);
   if ((int)roots.size() != n_forests * ntrees_per_forest) throw std::runtime_error("FFD tree count mismatch");
-  upload(mp_nodes, nodes, stream);
-  upload(mp_roots, roots, stream);
-  upload(mp_sizes, sizes, stream);
-  HIP_CHECK(hipStreamSynchronize(stream));  // host vectors are reused below
+  upload(mp_nodes, nodes, main_stream());
+  upload(mp_roots, roots, main_stream());
+  upload(mp_sizes, sizes, main_stream());
+  HIP_CHECK(hipStreamSynchronize(main_stream()));  // host vectors are reused below
 
   // head-pose leaf value m (face_utils.cpp:223-228), -1 when the leaf is filtered out
   {
@@ -294,7 +309,7 @@ void ffd_engine::load_model(const std::string& path) {
         mv[L] = -1.f;
       }
     }
-    upload(hp_m, mv, stream);
+    upload(hp_m, mv, main_stream());
   }
   // FFD leaf vote mask / weight / offsets (face_utils.cpp:283-298)
   {
@@ -326,11 +341,11 @@ void ffd_engine::load_model(const std::string& path) {
         o[L * NPARTS + i] = (int32_t)((uint32_t)(uint16_t)x | (uint32_t)(uint16_t)y << 16);
       }
     }
-    upload(mp_mask, mask, stream);
-    upload(mp_fg, w, stream);
-    upload(mp_offs, o, stream);
+    upload(mp_mask, mask, main_stream());
+    upload(mp_fg, w, main_stream());
+    upload(mp_offs, o, main_stream());
   }
-  HIP_CHECK(hipStreamSynchronize(stream));
+  HIP_CHECK(hipStreamSynchronize(main_stream()));
 }
 
 // createKernel / initGaborKernels (FeatureChannelFactory.hpp:186-251), packed for k_gabor.
@@ -378,16 +393,17 @@ void ffd_engine::build_gabor() {
     if (Wk != 7)
       for (int o = 0; o < 7; o++) coef[OFF + ntap * 16 + o] = re[o][ntap];  // centre tap
   }
-  upload(gabor_coef, coef, stream);
-  HIP_CHECK(hipStreamSynchronize(stream));
+  upload(gabor_coef, coef, main_stream());
+  HIP_CHECK(hipStreamSynchronize(main_stream()));
 }
 
-// Run the whole pipeline for one chunk of faces (desc offsets relative to the chunk
-// workspace).  d_out points at the chunk's first output record.
-void ffd_engine::run_chunk(std::vector<FaceDesc>& fds, const uint8_t* d_images, FaceOut* d_out) {
+// Run the whole pipeline for the chunk staged in w.h_fds (descriptor offsets are filled in
+// here, relative to w's buffers).  Everything is enqueued on w.stream; nothing waits.
+void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out) {
+  std::vector<FaceDesc>& fds = w.h_fds;
   const int n = (int)fds.size();
   if (n == 0) return;
-  resolve();
+  const hipStream_t st = w.stream;
   int64_t gray_b = 0, mag_e = 0, ch_e = 0, hp_e = 0, mp_e = 0, vote_e = 0;
   int max_w = 0, max_h = 0;
   for (auto& f : fds) {
@@ -408,92 +424,79 @@ void ffd_engine::run_chunk(std::vector<FaceDesc>& fds, const uint8_t* d_images, 
     max_w = std::max(max_w, f.W);
     max_h = std::max(max_h, f.H);
   }
-  gray.ensure(gray_b + 256);
-  mag.ensure((mag_e + 64) * 4);
-  chan.ensure((ch_e + 64) * 4);
-  hpleaf.ensure((hp_e + 64) * 4);
-  mpleaf.ensure((mp_e + 64) * 4);
-  votes.ensure((vote_e + 64) * sizeof(Vote));
-  minmax.ensure((size_t)n * NGABOR * 2 * 4);
-  state.ensure((size_t)n * sizeof(HpState));
-  ms_mean.ensure((size_t)n * NPARTS * 2 * 4);
-  vote_counts.ensure((size_t)n * NPARTS * 4);
+  w.gray.ensure(gray_b + 256);
+  w.mag.ensure((mag_e + 64) * 4);
+  w.chan.ensure((ch_e + 64) * 4);
+  w.hpleaf.ensure((hp_e + 64) * 4);
+  w.mpleaf.ensure((mp_e + 64) * 4);
+  w.votes.ensure((vote_e + 64) * sizeof(Vote));
+  w.minmax.ensure((size_t)n * NGABOR * 2 * 4);
+  w.state.ensure((size_t)n * sizeof(HpState));
+  w.ms_mean.ensure((size_t)n * NPARTS * 2 * 4);
+  w.vote_counts.ensure((size_t)n * NPARTS * 4);
+  upload(w.faces, fds, st);
+  HIP_CHECK(hipMemsetAsync(w.minmax.p, 0xFF, (size_t)n * NGABOR * 2 * 4, st));
+  HIP_CHECK(hipMemsetAsync(d_out, 0, (size_t)n * sizeof(FaceOut), st));
 
-  // traversal block tables: one block per (face, tree), face-major (FFD: after the tree count is known)
-  std::vector<int32_t>& ws_hp = h_ws_hp;
-  ws_hp.assign(n + 1, 0);
-  for (int i = 0; i < n; i++) ws_hp[i + 1] = ws_hp[i] + (fds[i].valid ? hp_trees : 0);
-  h_fds = fds;
-  upload(faces, h_fds, stream);
-  upload(wave_hp, ws_hp, stream);
-  HIP_CHECK(hipMemsetAsync(minmax.p, 0xFF, (size_t)n * NGABOR * 2 * 4, stream));
-  HIP_CHECK(hipMemsetAsync(d_out, 0, (size_t)n * sizeof(FaceOut), stream));
-  maxtrees.ensure(4);
-
-  const FaceDesc* dfd = faces.as<FaceDesc>();
-  stage(0, [&] { launch_gray_resize(dfd, n, d_images, gray.as<uint8_t>(), stream); });
+  const FaceDesc* dfd = w.faces.as<FaceDesc>();
+  stage(0, st, [&] { launch_gray_resize(dfd, n, d_images, w.gray.as<uint8_t>(), st); });
   for (int nu = 4; nu >= 0; nu--)  // largest kernels first
-    stage(1 + (4 - nu), [&] {
-      launch_gabor(nu, dfd, n, max_w, max_h, gray.as<uint8_t>(), gabor_coef.as<float4>(), mag.as<float>(),
-                   minmax.as<uint32_t>(), stream);
+    stage(1 + (4 - nu), st, [&] {
+      launch_gabor(nu, dfd, n, max_w, max_h, w.gray.as<uint8_t>(), gabor_coef.as<float4>(), w.mag.as<float>(),
+                   w.minmax.as<uint32_t>(), st);
     });
-  stage(6, [&] {
-    launch_integral(dfd, n, gray.as<uint8_t>(), mag.as<float>(), minmax.as<uint32_t>(), chan.as<uint32_t>(), stream);
+  stage(6, st, [&] {
+    launch_integral(dfd, n, w.gray.as<uint8_t>(), w.mag.as<float>(), w.minmax.as<uint32_t>(), w.chan.as<uint32_t>(),
+                    st);
   });
-  stage(7, [&] {
-    launch_traverse(true, dfd, wave_hp.as<int32_t>(), n, ws_hp[n], hp_nodes.as<uint4>(), hp_roots.as<int32_t>(),
-                    hp_sizes.as<int32_t>(), nullptr, desc.hp_option.step_size, chan.as<uint32_t>(),
-                    hpleaf.as<int32_t>(), trav_lds_hp, trav_walks, stream);
+  stage(7, st, [&] {
+    launch_traverse(true, dfd, n, hp_trees, hp_nodes.as<uint4>(), hp_roots.as<int32_t>(), hp_sizes.as<int32_t>(),
+                    nullptr, desc.hp_option.step_size, w.chan.as<uint32_t>(), w.hpleaf.as<int32_t>(), trav_lds_hp,
+                    trav_walks, st);
   });
-  stage(8, [&] {
-    launch_hp_pose(dfd, n, hpleaf.as<int32_t>(), hp_m.as<float>(), hp_trees, n_forests, ntrees_per_forest,
-                   state.as<HpState>(), d_out, stream);
+  stage(8, st, [&] {
+    launch_hp_pose(dfd, n, w.hpleaf.as<int32_t>(), hp_m.as<float>(), hp_trees, n_forests, ntrees_per_forest,
+                   w.state.as<HpState>(), d_out, st);
   });
-  HIP_CHECK(hipGetLastError());
-
-  // per-face tree counts decide the FFD traversal grid: read them back (small sync)
-  std::vector<HpState> hs(n);
-  HIP_CHECK(hipMemcpyAsync(hs.data(), state.p, (size_t)n * sizeof(HpState), hipMemcpyDeviceToHost, stream));
-  HIP_CHECK(hipStreamSynchronize(stream));
-  int tslots = 0;
-  std::vector<int32_t>& ws_mp = h_ws_mp;
-  ws_mp.assign(n + 1, 0);
-  for (int i = 0; i < n; i++) {
-    const int nt = fds[i].valid ? hs[i].n_trees : 0;
-    tslots = std::max(tslots, nt);
-    ws_mp[i + 1] = ws_mp[i] + nt;
-  }
-  upload(wave_mp, ws_mp, stream);
-  stage(9, [&] {
-    launch_traverse(false, dfd, wave_mp.as<int32_t>(), n, ws_mp[n], mp_nodes.as<uint4>(), mp_roots.as<int32_t>(),
-                    mp_sizes.as<int32_t>(), state.as<HpState>(), desc.mp_option.step_size, chan.as<uint32_t>(),
-                    mpleaf.as<int32_t>(), trav_lds_mp, trav_walks, stream);
+  stage(9, st, [&] {
+    launch_traverse(false, dfd, n, MAX_TREES, mp_nodes.as<uint4>(), mp_roots.as<int32_t>(), mp_sizes.as<int32_t>(),
+                    w.state.as<HpState>(), desc.mp_option.step_size, w.chan.as<uint32_t>(), w.mpleaf.as<int32_t>(),
+                    trav_lds_mp, trav_walks, st);
   });
   const int n_parts = std::min(desc.mp_option.num_parts, NPARTS);
-  stage(10, [&] {
-    launch_votes(dfd, n, mpleaf.as<int32_t>(), mp_mask.as<uint32_t>(), mp_fg.as<float>(), mp_offs.as<int32_t>(),
-                 state.as<HpState>(), MAX_TREES, desc.mp_option.step_size, patch / 2, n_parts, votes.as<Vote>(),
-                 vote_counts.as<int32_t>(), stream);
+  stage(10, st, [&] {
+    launch_votes(dfd, n, w.mpleaf.as<int32_t>(), mp_mask.as<uint32_t>(), mp_fg.as<float>(), mp_offs.as<int32_t>(),
+                 w.state.as<HpState>(), MAX_TREES, desc.mp_option.step_size, patch / 2, n_parts, w.votes.as<Vote>(),
+                 w.vote_counts.as<int32_t>(), st);
   });
-  stage(11, [&] {
-    launch_meanshift(dfd, n, state.as<HpState>(), MAX_TREES, n_parts, (float)desc.ms_option.kernel_size,
-                     desc.ms_option.max_iterations, desc.ms_option.stopping_criteria, votes.as<Vote>(),
-                     vote_counts.as<int32_t>(), ms_mean.as<float>(), d_out, stream);
+  stage(11, st, [&] {
+    launch_meanshift(dfd, n, w.state.as<HpState>(), MAX_TREES, n_parts, (float)desc.ms_option.kernel_size,
+                     desc.ms_option.max_iterations, desc.ms_option.stopping_criteria, w.votes.as<Vote>(),
+                     w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(), d_out, st);
   });
   HIP_CHECK(hipGetLastError());
-  last_tslots = tslots;
 }
 
+// Split the batch into chunks, round-robin over the stream workspaces.  On return every chunk
+// is enqueued and main_stream() is ordered after all of them.
 void ffd_engine::analyze(const uint8_t* d_images, const std::vector<FaceDesc>& all, FaceOut* d_out) {
   const int n = (int)all.size();
-  for (int first = 0; first < n; first += max_chunk) {
+  int k = 0;
+  for (int first = 0; first < n; first += max_chunk, k++) {
     const int cnt = std::min(max_chunk, n - first);
-    std::vector<FaceDesc> fds(all.begin() + first, all.begin() + first + cnt);
-    run_chunk(fds, d_images, d_out + first);
-    last_desc = fds;
-    last_first = first;
-    last_count = cnt;
+    Workspace& w = *ws[k % ws.size()];
+    if (w.pending) HIP_CHECK(hipEventSynchronize(w.done));  // its host staging is free again
+    w.h_fds.assign(all.begin() + first, all.begin() + first + cnt);
+    run_chunk(w, d_images, d_out + first);
+    w.desc = w.h_fds;
+    w.first = first;
+    w.count = cnt;
+    HIP_CHECK(hipEventRecord(w.done, w.stream));
+    w.pending = true;
+    last_ws = (int)(k % ws.size());
   }
+  for (size_t i = 1; i < ws.size(); i++)
+    if (ws[i]->pending) HIP_CHECK(hipStreamWaitEvent(main_stream(), ws[i]->done, 0));
 }
 
 namespace {
@@ -583,9 +586,11 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   std::unique_ptr<ffd_engine> e(new ffd_engine());
   e->desc = *d;
   e->device = d->device;
-  if (const char* v = std::getenv("FFD_TRAV_LDS_KB_HP")) e->trav_lds_hp = std::max(1, std::atoi(v)) * 1024;
-  if (const char* v = std::getenv("FFD_TRAV_LDS_KB_FFD")) e->trav_lds_mp = std::max(1, std::atoi(v)) * 1024;
+  if (const char* v = std::getenv("FFD_TRAV_LDS_KB_HP")) e->trav_lds_hp = std::max(1, std::min(160, std::atoi(v))) * 1024;
+  if (const char* v = std::getenv("FFD_TRAV_LDS_KB_FFD")) e->trav_lds_mp = std::max(1, std::min(160, std::atoi(v))) * 1024;
   if (const char* v = std::getenv("FFD_TRAV_WALKS")) e->trav_walks = std::atoi(v);
+  if (const char* v = std::getenv("FFD_CHUNK")) e->max_chunk = std::max(1, std::atoi(v));
+  if (const char* v = std::getenv("FFD_STREAMS")) e->n_streams = std::max(1, std::min(8, std::atoi(v)));
   if (d->max_chunk_faces > 0) e->max_chunk = d->max_chunk_faces;
   try {
     int ndev = 0;
@@ -593,7 +598,13 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
       return fail(nullptr, FFD_ERR_DEVICE, "no HIP device available (the engine has no CPU fallback)");
     if (d->device < 0 || d->device >= ndev) return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "bad device ordinal");
     HIP_CHECK(hipSetDevice(d->device));
-    HIP_CHECK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    for (int i = 0; i < std::max(1, e->n_streams); i++) {
+      auto w = std::make_unique<Workspace>();
+      HIP_CHECK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
+      HIP_CHECK(hipEventCreateWithFlags(&w->done, hipEventDisableTiming));
+      e->ws.push_back(std::move(w));
+    }
+    HIP_CHECK(set_traverse_lds_limit(std::max(e->trav_lds_hp, e->trav_lds_mp)));
     e->load_model(d->model_path);
     e->build_gabor();
   } catch (const HipError& x) {
@@ -608,17 +619,17 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
 void ffd_engine_destroy(ffd_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
-  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (auto& w : e->ws) (void)hipStreamSynchronize(w->stream);
   delete e;
 }
 
 const char* ffd_last_error(const ffd_engine* e) { return e ? e->err.c_str() : g_create_err.c_str(); }
 
-void* ffd_stream(ffd_engine* e) { return e ? (void*)e->stream : nullptr; }
+void* ffd_stream(ffd_engine* e) { return (e && !e->ws.empty()) ? (void*)e->main_stream() : nullptr; }
 
 ffd_status ffd_synchronize(ffd_engine* e) {
   return guarded(e, [&] {
-    HIP_CHECK(hipStreamSynchronize(e->stream));
+    e->sync_all();
     e->resolve();
     return FFD_OK;
   });
@@ -681,7 +692,10 @@ ffd_status ffd_analyze_faces(ffd_engine* e, const ffd_image* imgs, int32_t n_img
     e->images.ensure(total);
     for (int i = 0; i < n_img; i++)
       HIP_CHECK(hipMemcpyAsync(e->images.as<uint8_t>() + img_off[i], imgs[i].bgr, (size_t)imgs[i].stride * imgs[i].height,
-                               hipMemcpyHostToDevice, e->stream));
+                               hipMemcpyHostToDevice, e->main_stream()));
+    // the other streams must see the uploaded images
+    HIP_CHECK(hipEventRecord(e->ws[0]->done, e->main_stream()));
+    for (size_t i = 1; i < e->ws.size(); i++) HIP_CHECK(hipStreamWaitEvent(e->ws[i]->stream, e->ws[0]->done, 0));
     std::vector<FaceDesc> fds(n_faces);
     for (int i = 0; i < n_faces; i++) {
       int k = box_img ? box_img[i] : i;
@@ -691,8 +705,9 @@ ffd_status ffd_analyze_faces(ffd_engine* e, const ffd_image* imgs, int32_t n_img
     e->out.ensure((size_t)n_faces * sizeof(FaceOut));
     e->analyze(e->images.as<uint8_t>(), fds, e->out.as<FaceOut>());
     static_assert(sizeof(FaceOut) == sizeof(ffd_face), "FaceOut must mirror ffd_face");
-    HIP_CHECK(hipMemcpyAsync(out, e->out.p, (size_t)n_faces * sizeof(ffd_face), hipMemcpyDeviceToHost, e->stream));
-    HIP_CHECK(hipStreamSynchronize(e->stream));
+    HIP_CHECK(hipMemcpyAsync(out, e->out.p, (size_t)n_faces * sizeof(ffd_face), hipMemcpyDeviceToHost,
+                             e->main_stream()));
+    HIP_CHECK(hipStreamSynchronize(e->main_stream()));
     for (int i = 0; i < n_faces; i++)
       if (out[i].status != FFD_OK) out[i].status = FFD_ERR_INVALID_ARGUMENT;
     return FFD_OK;
@@ -721,25 +736,27 @@ ffd_status ffd_analyze_faces_device(ffd_engine* e, const void* d_images, int64_t
 ffd_status ffd_get_trace(ffd_engine* e, int32_t index, ffd_trace* tr) {
   return guarded(e, [&]() -> ffd_status {
     if (!tr) return fail(e, FFD_ERR_INVALID_ARGUMENT, "trace is NULL");
-    const int k = index - e->last_first;
-    if (k < 0 || k >= e->last_count) return fail(e, FFD_ERR_INVALID_ARGUMENT, "index not in the last chunk");
-    const FaceDesc& f = e->last_desc[k];
+    if (e->last_ws < 0) return fail(e, FFD_ERR_INVALID_ARGUMENT, "no batch has run");
+    Workspace& w = *e->ws[e->last_ws];
+    const int k = index - w.first;
+    if (k < 0 || k >= w.count) return fail(e, FFD_ERR_INVALID_ARGUMENT, "index not in the last chunk");
+    const FaceDesc& f = w.desc[k];
     if (!f.valid) return fail(e, FFD_ERR_INVALID_ARGUMENT, "face was rejected");
-    HIP_CHECK(hipStreamSynchronize(e->stream));
+    e->sync_all();
     const int W = f.W, H = f.H;
     if (tr->face)
-      HIP_CHECK(hipMemcpy2D(tr->face, W, e->gray.as<uint8_t>() + f.gray_off, PITCH, W, H, hipMemcpyDeviceToHost));
+      HIP_CHECK(hipMemcpy2D(tr->face, W, w.gray.as<uint8_t>() + f.gray_off, PITCH, W, H, hipMemcpyDeviceToHost));
     if (tr->channels)
       for (int c = 0; c < NCH; c++)
         HIP_CHECK(hipMemcpy2D(tr->channels + (size_t)c * (H + 1) * (W + 1), (W + 1) * 4,
-                              e->chan.as<uint32_t>() + f.ch_off + c * f.plane, PITCH * 4, (W + 1) * 4, H + 1,
+                              w.chan.as<uint32_t>() + f.ch_off + c * f.plane, PITCH * 4, (W + 1) * 4, H + 1,
                               hipMemcpyDeviceToHost));
     HpState hs;
-    HIP_CHECK(hipMemcpy(&hs, e->state.as<HpState>() + k, sizeof(hs), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(&hs, w.state.as<HpState>() + k, sizeof(hs), hipMemcpyDeviceToHost));
     if (tr->hp_leaves) {
       const int nh = f.nhx * f.nhy;
       std::vector<int32_t> v((size_t)e->hp_trees * nh);
-      HIP_CHECK(hipMemcpy(v.data(), e->hpleaf.as<int32_t>() + f.hp_off, v.size() * 4, hipMemcpyDeviceToHost));
+      HIP_CHECK(hipMemcpy(v.data(), w.hpleaf.as<int32_t>() + f.hp_off, v.size() * 4, hipMemcpyDeviceToHost));
       for (int xi = 0; xi < f.nhx; xi++)
         for (int yi = 0; yi < f.nhy; yi++)
           for (int t = 0; t < e->hp_trees; t++)
@@ -748,7 +765,7 @@ ffd_status ffd_get_trace(ffd_engine* e, int32_t index, ffd_trace* tr) {
     if (tr->mp_leaves) {
       const int nm = f.nmx * f.nmy, T = hs.n_trees;
       std::vector<int32_t> v((size_t)std::max(T, 1) * nm);
-      HIP_CHECK(hipMemcpy(v.data(), e->mpleaf.as<int32_t>() + f.mp_off, (size_t)T * nm * 4, hipMemcpyDeviceToHost));
+      HIP_CHECK(hipMemcpy(v.data(), w.mpleaf.as<int32_t>() + f.mp_off, (size_t)T * nm * 4, hipMemcpyDeviceToHost));
       for (int xi = 0; xi < f.nmx; xi++)
         for (int yi = 0; yi < f.nmy; yi++)
           for (int t = 0; t < T; t++) tr->mp_leaves[(xi * f.nmy + yi) * T + t] = v[(size_t)t * nm + yi * f.nmx + xi];
@@ -758,10 +775,10 @@ ffd_status ffd_get_trace(ffd_engine* e, int32_t index, ffd_trace* tr) {
     if (tr->pose_freq)
       for (int j = 0; j < 5; j++) tr->pose_freq[j] = j < e->n_forests ? hs.pose_freq[j] : 0.f;
     if (tr->vote_counts)
-      HIP_CHECK(hipMemcpy(tr->vote_counts, e->vote_counts.as<int32_t>() + (size_t)k * NPARTS, NPARTS * 4,
+      HIP_CHECK(hipMemcpy(tr->vote_counts, w.vote_counts.as<int32_t>() + (size_t)k * NPARTS, NPARTS * 4,
                           hipMemcpyDeviceToHost));
     if (tr->ms_mean)
-      HIP_CHECK(hipMemcpy(tr->ms_mean, e->ms_mean.as<float>() + (size_t)k * NPARTS * 2, NPARTS * 2 * 4,
+      HIP_CHECK(hipMemcpy(tr->ms_mean, w.ms_mean.as<float>() + (size_t)k * NPARTS * 2, NPARTS * 2 * 4,
                           hipMemcpyDeviceToHost));
     return FFD_OK;
   });
@@ -772,36 +789,40 @@ ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t
     if (!gray_face || !out || W < 2 || H < 2 || W > PITCH - 3 || H > MAX_FACE_H)
       return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     // the face itself is the "image" (copy mode): one BGR image whose gray equals the input
+    e->sync_all();
+    Workspace& w = *e->ws[0];
     std::vector<uint8_t> bgr((size_t)W * H * 3);
     // BGR2GRAY of (v,v,v) is v: (1868+9617+4899)*v + 8192 >> 14 == v for v in [0,255]
     for (int i = 0; i < W * H; i++) bgr[3 * i] = bgr[3 * i + 1] = bgr[3 * i + 2] = gray_face[i];
     e->scratch_a.ensure(bgr.size());
-    HIP_CHECK(hipMemcpyAsync(e->scratch_a.p, bgr.data(), bgr.size(), hipMemcpyHostToDevice, e->stream));
+    HIP_CHECK(hipMemcpyAsync(e->scratch_a.p, bgr.data(), bgr.size(), hipMemcpyHostToDevice, w.stream));
     FaceDesc f;
     std::memset(&f, 0, sizeof(f));
     f.img_w = W; f.img_h = H; f.img_stride = 3 * W; f.bw = W; f.bh = H; f.W = W; f.H = H;
     f.scale = 1.f; f.mode = 0; f.valid = 1;
     f.plane = (int64_t)(H + 1) * PITCH;
-    e->gray.ensure((size_t)H * PITCH + 256);
-    e->mag.ensure((size_t)NGABOR * H * PITCH * 4 + 256);
-    e->chan.ensure((size_t)NCH * f.plane * 4 + 256);
-    e->minmax.ensure(NGABOR * 2 * 4);
+    w.gray.ensure((size_t)H * PITCH + 256);
+    w.mag.ensure((size_t)NGABOR * H * PITCH * 4 + 256);
+    w.chan.ensure((size_t)NCH * f.plane * 4 + 256);
+    w.minmax.ensure(NGABOR * 2 * 4);
     std::vector<FaceDesc> one{f};
-    upload(e->faces, one, e->stream);
-    HIP_CHECK(hipMemsetAsync(e->minmax.p, 0xFF, NGABOR * 2 * 4, e->stream));
-    const FaceDesc* dfd = e->faces.as<FaceDesc>();
-    launch_gray_resize(dfd, 1, e->scratch_a.as<uint8_t>(), e->gray.as<uint8_t>(), e->stream);
+    upload(w.faces, one, w.stream);
+    HIP_CHECK(hipMemsetAsync(w.minmax.p, 0xFF, NGABOR * 2 * 4, w.stream));
+    const FaceDesc* dfd = w.faces.as<FaceDesc>();
+    launch_gray_resize(dfd, 1, e->scratch_a.as<uint8_t>(), w.gray.as<uint8_t>(), w.stream);
     for (int nu = 4; nu >= 0; nu--)
-      launch_gabor(nu, dfd, 1, W, H, e->gray.as<uint8_t>(), e->gabor_coef.as<float4>(), e->mag.as<float>(),
-                   e->minmax.as<uint32_t>(), e->stream);
-    launch_integral(dfd, 1, e->gray.as<uint8_t>(), e->mag.as<float>(), e->minmax.as<uint32_t>(), e->chan.as<uint32_t>(),
-                    e->stream);
+      launch_gabor(nu, dfd, 1, W, H, w.gray.as<uint8_t>(), e->gabor_coef.as<float4>(), w.mag.as<float>(),
+                   w.minmax.as<uint32_t>(), w.stream);
+    launch_integral(dfd, 1, w.gray.as<uint8_t>(), w.mag.as<float>(), w.minmax.as<uint32_t>(), w.chan.as<uint32_t>(),
+                    w.stream);
     HIP_CHECK(hipGetLastError());
     for (int c = 0; c < NCH; c++)
-      HIP_CHECK(hipMemcpy2DAsync(out + (size_t)c * (H + 1) * (W + 1), (W + 1) * 4, e->chan.as<uint32_t>() + c * f.plane,
-                                 PITCH * 4, (W + 1) * 4, H + 1, hipMemcpyDeviceToHost, e->stream));
-    HIP_CHECK(hipStreamSynchronize(e->stream));
-    e->last_count = 0;  // workspace no longer holds a batch
+      HIP_CHECK(hipMemcpy2DAsync(out + (size_t)c * (H + 1) * (W + 1), (W + 1) * 4, w.chan.as<uint32_t>() + c * f.plane,
+                                 PITCH * 4, (W + 1) * 4, H + 1, hipMemcpyDeviceToHost, w.stream));
+    HIP_CHECK(hipStreamSynchronize(w.stream));
+    w.count = 0;  // workspace no longer holds a batch
+    w.pending = false;
+    if (e->last_ws == 0) e->last_ws = -1;
     return FFD_OK;
   });
 }
@@ -827,20 +848,20 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* c
     e->scratch_a.ensure((size_t)NCH * plane * 4);
     for (int c = 0; c < NCH; c++)
       HIP_CHECK(hipMemcpy2DAsync(e->scratch_a.as<uint32_t>() + c * plane, PITCH * 4, channels + (size_t)c * (H + 1) * (W + 1),
-                                 (W + 1) * 4, (W + 1) * 4, H + 1, hipMemcpyHostToDevice, e->stream));
+                                 (W + 1) * 4, (W + 1) * 4, H + 1, hipMemcpyHostToDevice, e->main_stream()));
     std::vector<int32_t> pv(patches_xy, patches_xy + 2 * n_patches), tv(tree_ids, tree_ids + n_trees);
-    upload(e->scratch_b, pv, e->stream);
-    upload(e->scratch_c, tv, e->stream);
+    upload(e->scratch_b, pv, e->main_stream());
+    upload(e->scratch_c, tv, e->main_stream());
     DevBuf outb;
     outb.ensure((size_t)n_patches * n_trees * 4);
     const bool hp = kind == FFD_FOREST_HEADPOSE;
     launch_eval_patches(hp ? e->hp_nodes.as<uint4>() : e->mp_nodes.as<uint4>(),
                         hp ? e->hp_roots.as<int32_t>() : e->mp_roots.as<int32_t>(), e->scratch_c.as<int32_t>(), n_trees,
                         e->scratch_b.as<int32_t>(), n_patches, e->scratch_a.as<uint32_t>(), plane, outb.as<int32_t>(),
-                        e->stream);
+                        e->main_stream());
     HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipMemcpyAsync(leaf_ids, outb.p, (size_t)n_patches * n_trees * 4, hipMemcpyDeviceToHost, e->stream));
-    HIP_CHECK(hipStreamSynchronize(e->stream));
+    HIP_CHECK(hipMemcpyAsync(leaf_ids, outb.p, (size_t)n_patches * n_trees * 4, hipMemcpyDeviceToHost, e->main_stream()));
+    HIP_CHECK(hipStreamSynchronize(e->main_stream()));
     return FFD_OK;
   });
 }

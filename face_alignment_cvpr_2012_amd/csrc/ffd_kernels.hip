@@ -398,22 +398,19 @@ __device__ __forceinline__ int rect_mean_buf(__amdgpu_buffer_rsrc_t rs, uint32_t
 }
 
 template <bool HP, int NW>
-__global__ __launch_bounds__(256) void k_traverse(const FaceDesc* __restrict__ faces,
-                                                  const int32_t* __restrict__ block_start, int n_faces,
+__global__ __launch_bounds__(256) void k_traverse(const FaceDesc* __restrict__ faces, int slots,
                                                   const uint4* __restrict__ nodes, const int32_t* __restrict__ roots,
                                                   const int32_t* __restrict__ tree_nodes,
                                                   const HpState* __restrict__ hp_state, int step, int top_cap,
                                                   const uint32_t* __restrict__ chan,
                                                   int32_t* __restrict__ leaf_out) {
   extern __shared__ uint4 top[];
+  // blocks are face-major: `slots` consecutive blocks per face (HP: one per tree; FFD: FFD_MAX_TREES
+  // slots, those beyond the face's selected tree count exit at once)
   const int lb = (int)xcd_remap(blockIdx.x, gridDim.x);
-  int lo = 0, hi = n_faces - 1;
-  while (lo < hi) {  // last f with block_start[f] <= lb
-    const int mid = (lo + hi + 1) >> 1;
-    if (block_start[mid] <= lb) lo = mid; else hi = mid - 1;
-  }
-  const int f = lo;
-  const int t = lb - block_start[f];
+  const int f = lb / slots, t = lb - f * slots;
+  if (!faces[f].valid) return;
+  if (!HP && t >= hp_state[f].n_trees) return;
   const FaceDesc& fd = faces[f];
   const int tree = HP ? t : hp_state[f].trees[t];
   const uint32_t root = (uint32_t)roots[tree];
@@ -752,20 +749,32 @@ void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, const fl
   k_integral<<<grid, 256, 0, s>>>(faces, gray, mag, minmax, chan);
 }
 
-void launch_traverse(bool hp, const FaceDesc* faces, const int32_t* block_start, int n, int total_blocks,
-                     const uint4* nodes, const int32_t* roots, const int32_t* tree_nodes, const HpState* state,
-                     int step, const uint32_t* chan, int32_t* leaf_out, int lds_bytes, int walks, hipStream_t s) {
+void launch_traverse(bool hp, const FaceDesc* faces, int n, int slots, const uint4* nodes, const int32_t* roots,
+                     const int32_t* tree_nodes, const HpState* state, int step, const uint32_t* chan,
+                     int32_t* leaf_out, int lds_bytes, int walks, hipStream_t s) {
+  const int total_blocks = n * slots;
   if (total_blocks <= 0) return;
   const int cap = lds_bytes / (int)sizeof(uint4);
-#define FFD_TRAV(HPV, NWV)                                                                                   \
-  k_traverse<HPV, NWV><<<total_blocks, 256, lds_bytes, s>>>(faces, block_start, n, nodes, roots, tree_nodes, \
-                                                            state, step, cap, chan, leaf_out)
+#define FFD_TRAV(HPV, NWV)                                                                                    \
+  k_traverse<HPV, NWV><<<total_blocks, 256, lds_bytes, s>>>(faces, slots, nodes, roots, tree_nodes, state, step, \
+                                                            cap, chan, leaf_out)
   if (hp) {
     if (walks >= 4) FFD_TRAV(true, 4); else FFD_TRAV(true, 2);
   } else {
     if (walks >= 4) FFD_TRAV(false, 4); else FFD_TRAV(false, 2);
   }
 #undef FFD_TRAV
+}
+
+hipError_t set_traverse_lds_limit(int bytes) {
+  hipError_t e = hipSuccess;
+  const void* fns[] = {(const void*)k_traverse<true, 2>, (const void*)k_traverse<true, 4>,
+                       (const void*)k_traverse<false, 2>, (const void*)k_traverse<false, 4>};
+  for (const void* f : fns) {
+    hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (r != hipSuccess) e = r;
+  }
+  return e;
 }
 
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
