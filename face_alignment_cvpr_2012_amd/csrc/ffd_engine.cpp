@@ -96,8 +96,8 @@ struct ffd_engine {
   std::string err;
   int device = 0;
   ffd_engine_desc desc{};
-  int max_chunk = 512;
-  int n_streams = 2;
+  int max_chunk = 4096;
+  int n_streams = 1;
   // traversal tuning: LDS bytes per (face, tree) workgroup (staged tree top; also caps occupancy,
   // hence the faces whose channel sets share one XCD's L2) and interleaved walks per thread.
   // Overridable with FFD_TRAV_LDS_KB_{HP,FFD} / FFD_TRAV_WALKS / FFD_CHUNK / FFD_STREAMS.

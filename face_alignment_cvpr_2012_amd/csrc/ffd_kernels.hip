@@ -648,67 +648,68 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
 }
 
 // -------------------------------------------------------------- MeanShift ----
-// MeanShift::shift (MeanShift.hpp:41-135) over one landmark's compacted vote list, in list
-// order; then the rescale of FaceForest.cpp:255-257.  One thread per (face, landmark).
-__global__ void k_meanshift(const FaceDesc* __restrict__ faces, int n_faces, const HpState* __restrict__ state,
-                            int tslots, int n_parts, float lamda, int max_iter, float stop,
-                            const Vote* __restrict__ votes, const int32_t* __restrict__ vote_counts,
-                            float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+// MeanShift::shift (MeanShift.hpp:41-135) over one landmark's compacted vote list, then the
+// rescale of FaceForest.cpp:255-257.  One wave per (face, landmark): the 64 lanes compute the
+// per-vote terms of 64 consecutive votes in parallel (distance, exp kernel, products — each an
+// element-wise op with the reference's rounding), then the three running sums advance over the
+// 64 terms strictly in list order (readlane + add), so they equal the sequential float sums.
+__global__ __launch_bounds__(256) void k_meanshift(const FaceDesc* __restrict__ faces, int n_faces,
+                                                   const HpState* __restrict__ state, int tslots, int n_parts,
+                                                   float lamda, int max_iter, float stop,
+                                                   const Vote* __restrict__ votes,
+                                                   const int32_t* __restrict__ vote_counts,
+                                                   float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
+  const int gid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   const int f = gid / NPARTS, part = gid % NPARTS;
   if (f >= n_faces) return;
   const FaceDesc& fd = faces[f];
   if (!fd.valid) return;
   if (part >= n_parts) {
-    out[f].points[part][0] = 0;
-    out[f].points[part][1] = 0;
+    if (lane == 0) { out[f].points[part][0] = 0; out[f].points[part][1] = 0; }
     return;
   }
   const int n = fd.nmx * fd.nmy;
   const Vote* V = votes + fd.vote_off + (int64_t)part * tslots * n;
   const int cnt = vote_counts[(int64_t)f * NPARTS + part];
-  // Votes are read 8 at a time (independent loads, independent per-vote weights: ILP across the
-  // 8 chains); the three running sums still advance strictly in list order.
-  constexpr int G = 8;
   float mx = 0, my = 0, sw = 0;
-  for (int k0 = 0; k0 < cnt; k0 += G) {  // getMean
-    Vote v[G];
-#pragma unroll
-    for (int j = 0; j < G; j++) v[j] = (k0 + j < cnt) ? V[k0 + j] : Vote{0, 0, 0.f};
-#pragma unroll
-    for (int j = 0; j < G; j++) {
-      if (k0 + j < cnt) {
-        mx += v[j].x * v[j].w;
-        my += v[j].y * v[j].w;
-        sw += v[j].w;
-      }
+  for (int k0 = 0; k0 < cnt; k0 += 64) {  // getMean
+    const int k = k0 + lane;
+    float px = 0.f, py = 0.f, w = 0.f;
+    if (k < cnt) {
+      const Vote v = V[k];
+      px = v.x * v.w;
+      py = v.y * v.w;
+      w = v.w;
+    }
+    const int lim = min(64, cnt - k0);
+    for (int j = 0; j < lim; j++) {
+      mx += lane_f(px, j);
+      my += lane_f(py, j);
+      sw += lane_f(w, j);
     }
   }
   if (sw > 0) { mx /= sw; my /= sw; }
   bool conv = false;
   for (int it = 0; it < max_iter && !conv; it++) {  // getWeightedMean
     float sx = 0, sy = 0, s = 0;
-    for (int k0 = 0; k0 < cnt; k0 += G) {
-      Vote v[G];
-#pragma unroll
-      for (int j = 0; j < G; j++) v[j] = (k0 + j < cnt) ? V[k0 + j] : Vote{0, 0, 0.f};
-      float w[G], px[G], py[G];
-#pragma unroll
-      for (int j = 0; j < G; j++) {
-        const float dx = mx - (float)v[j].x, dy = my - (float)v[j].y;
+    for (int k0 = 0; k0 < cnt; k0 += 64) {
+      const int k = k0 + lane;
+      float px = 0.f, py = 0.f, w = 0.f;
+      if (k < cnt) {
+        const Vote v = V[k];
+        const float dx = mx - (float)v.x, dy = my - (float)v.y;
         float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
         d = ffd_expf(-d / lamda);
-        w[j] = v[j].w * d;
-        px[j] = v[j].x * w[j];
-        py[j] = v[j].y * w[j];
+        w = v.w * d;
+        px = v.x * w;
+        py = v.y * w;
       }
-#pragma unroll
-      for (int j = 0; j < G; j++) {
-        if (k0 + j < cnt) {
-          sx += px[j];
-          sy += py[j];
-          s += w[j];
-        }
+      const int lim = min(64, cnt - k0);
+      for (int j = 0; j < lim; j++) {
+        sx += lane_f(px, j);
+        sy += lane_f(py, j);
+        s += lane_f(w, j);
       }
     }
     if (s > 0) { sx /= s; sy /= s; }
@@ -717,11 +718,13 @@ __global__ void k_meanshift(const FaceDesc* __restrict__ faces, int n_faces, con
     mx = sx;
     my = sy;
   }
-  ms_mean[((int64_t)f * NPARTS + part) * 2] = mx;
-  ms_mean[((int64_t)f * NPARTS + part) * 2 + 1] = my;
-  const float inv = 1.0f / fd.scale;  // FaceForest.cpp:255-257
-  out[f].points[part][0] = cv_round((float)cv_round(mx) * inv);
-  out[f].points[part][1] = cv_round((float)cv_round(my) * inv);
+  if (lane == 0) {
+    ms_mean[((int64_t)f * NPARTS + part) * 2] = mx;
+    ms_mean[((int64_t)f * NPARTS + part) * 2 + 1] = my;
+    const float inv = 1.0f / fd.scale;  // FaceForest.cpp:255-257
+    out[f].points[part][0] = cv_round((float)cv_round(mx) * inv);
+    out[f].points[part][1] = cv_round((float)cv_round(my) * inv);
+  }
 }
 
 // ------------------------------------------------------------------ launch --
@@ -801,9 +804,9 @@ void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const ui
 void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int tslots, int n_parts, float lamda,
                       int max_iter, float stop, const Vote* votes, const int32_t* vote_counts, float* ms_mean,
                       FaceOut* out, hipStream_t s) {
-  const int total = n * NPARTS;
-  k_meanshift<<<(total + 63) / 64, 64, 0, s>>>(faces, n, state, tslots, n_parts, lamda, max_iter, stop, votes,
-                                               vote_counts, ms_mean, out);
+  const int total = n * NPARTS;  // one wave per (face, landmark), 4 per workgroup
+  k_meanshift<<<(total + 3) / 4, 256, 0, s>>>(faces, n, state, tslots, n_parts, lamda, max_iter, stop, votes,
+                                             vote_counts, ms_mean, out);
 }
 
 }  // namespace ffd
