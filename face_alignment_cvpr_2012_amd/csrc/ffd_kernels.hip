@@ -141,11 +141,12 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
                                                       float* __restrict__ mag,
                                                       uint32_t* __restrict__ minmax) {
   constexpr int R = (W - 1) / 2;
-  constexpr int LW = GB_TX + 2 * R + 4;  // row stride (floats), multiple of 4
+  // row stride (floats) == 1 mod 4: the 4 rows a 32-lane group touches fall on disjoint banks
+  constexpr int LW = ((GB_TX + 2 * R + 3) / 4) * 4 + 1;
   constexpr int LH = GB_TY + 2 * R;
   constexpr int NU = GaborCfg<W>::nu, OFF = GaborCfg<W>::off;
   constexpr int NTAP = (W == 7) ? 49 : (W * W - 1) / 2 + 1;  // incl. centre
-  __shared__ __attribute__((aligned(16))) float tile[LH * LW];
+  __shared__ float tile[LH * LW];
   __shared__ float4 coef[NTAP * 4];
   __shared__ uint32_t red[8][14];
   const FaceDesc fd = faces[blockIdx.y];
@@ -161,81 +162,68 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
     tile[ly * LW + lx] = (float)g[y * PITCH + x];
   }
   __syncthreads();
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;  // 16 x 32 threads, 4 px each
+  // wave w covers threads tx in [8*(w&1), +8) x ty in [8*(w>>1), +8); 4 px per thread
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  const int tx = (wv & 1) * 8 + (ln & 7), ty = (wv >> 1) * 8 + (ln >> 3);
   float re[4][7], im[4][7];
 #pragma unroll
   for (int k = 0; k < 4; k++)
 #pragma unroll
     for (int o = 0; o < 7; o++) re[k][o] = im[k][o] = 0.f;
+  // centre pixel (ty, 4tx + k) sits at tile (ty + R, 4tx + R + k)
+  const float* ctr = &tile[(ty + R) * LW + 4 * tx + R];
 
   if constexpr (W == 7) {
-    for (int r = 0; r < 7; r++) {
-      const float* row = &tile[(ty + r) * LW + 4 * tx];  // image row py + r - 3, cols px - 3 ..
-      float win[10];
+    // OpenCV Filter2D direct path: s = 0; s += k*p over taps in row-major order
+#pragma unroll 1
+    for (int t = 0; t < 49; t++) {
+      const int dy = t / 7 - 3, dx = t % 7 - 3;
+      const float* pa = ctr + dy * LW + dx;
+      const float4 c0 = coef[t * 4 + 0], c1 = coef[t * 4 + 1], c2 = coef[t * 4 + 2], c3 = coef[t * 4 + 3];
+      const float kr[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
+      const float ki[7] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z};
 #pragma unroll
-      for (int j = 0; j < 10; j++) win[j] = row[j];
+      for (int k = 0; k < 4; k++) {
+        const float p = pa[k];
 #pragma unroll
-      for (int c = 0; c < 7; c++) {
-        const float4 c0 = coef[(r * 7 + c) * 4 + 0], c1 = coef[(r * 7 + c) * 4 + 1];
-        const float4 c2 = coef[(r * 7 + c) * 4 + 2], c3 = coef[(r * 7 + c) * 4 + 3];
-        const float kr[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
-        const float ki[7] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z};
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const float p = win[c + k];
-#pragma unroll
-          for (int o = 0; o < 7; o++) {
-            re[k][o] = re[k][o] + kr[o] * p;
-            im[k][o] = im[k][o] + ki[o] * p;
-          }
+        for (int o = 0; o < 7; o++) {
+          re[k][o] = re[k][o] + kr[o] * p;
+          im[k][o] = im[k][o] + ki[o] * p;
         }
       }
     }
   } else {
-    // rows dy = -R .. 0 (row 0 only dx < 0); pair t = (dy + R) * W + (dx + R)
-    for (int r = 0; r <= R; r++) {
-      const int dy = r - R;
-      const float* rowA = &tile[(ty + R + dy) * LW + 4 * tx];  // a(k, dx) = rowA[dx + R + k]
-      const float* rowB = &tile[(ty + R - dy) * LW + 4 * tx];  // b(k, dx) = rowB[R - dx + k]
-      float a[4], b[4];
+    // folded pairs t = (dy + R) * W + (dx + R), rows dy = -R .. 0, row 0 only dx < 0
+    constexpr int HALF = (W * W - 1) / 2;
+#pragma unroll 1
+    for (int t = 0; t < HALF; t++) {
+      const int dy = t / W - R, dx = t % W - R;
+      const float* pa = ctr + dy * LW + dx;   // a(k) = pa[k]
+      const float* pb = ctr - dy * LW - dx;   // b(k) = pb[k]
+      const float4 c0 = coef[t * 4 + 0], c1 = coef[t * 4 + 1], c2 = coef[t * 4 + 2], c3 = coef[t * 4 + 3];
+      const float kr[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
+      const float ki[7] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z};
 #pragma unroll
-      for (int k = 0; k < 4; k++) { a[k] = rowA[k]; b[k] = rowB[2 * R + k]; }
-      const int ncol = (r < R) ? W : R;
+      for (int k = 0; k < 4; k++) {
+        const float av = pa[k], bv = pb[k];
+        const float S = av + bv, D = av - bv;
 #pragma unroll
-      for (int j = 0; j < W; j++) {  // dx = j - R
-        if (j >= ncol) break;
-        const int t = r * W + j;
-        const float4 c0 = coef[t * 4 + 0], c1 = coef[t * 4 + 1], c2 = coef[t * 4 + 2], c3 = coef[t * 4 + 3];
-        const float kr[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
-        const float ki[7] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z};
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const float S = a[k] + b[k], D = a[k] - b[k];
-#pragma unroll
-          for (int o = 0; o < 7; o++) {
-            re[k][o] = fmaf(kr[o], S, re[k][o]);
-            im[k][o] = fmaf(ki[o], D, im[k][o]);
-          }
-        }
-        if (j + 1 < W) {  // slide: a moves right, b moves left
-          a[0] = a[1]; a[1] = a[2]; a[2] = a[3]; a[3] = rowA[j + 4];
-          b[3] = b[2]; b[2] = b[1]; b[1] = b[0]; b[0] = rowB[2 * R - j - 1];
+        for (int o = 0; o < 7; o++) {
+          re[k][o] = fmaf(kr[o], S, re[k][o]);
+          im[k][o] = fmaf(ki[o], D, im[k][o]);
         }
       }
     }
-    constexpr int TC = (W * W - 1) / 2;
-    const float4 c0 = coef[TC * 4 + 0], c1 = coef[TC * 4 + 1];
+    const float4 c0 = coef[HALF * 4 + 0], c1 = coef[HALF * 4 + 1];
     const float kr[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
-    const float* rowC = &tile[(ty + R) * LW + 4 * tx + R];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const float p0 = rowC[k];
+      const float p0 = ctr[k];
 #pragma unroll
       for (int o = 0; o < 7; o++) re[k][o] = fmaf(kr[o], p0, re[k][o]);
     }
   }
   const int x0 = tx0 + 4 * tx, y = ty0 + ty;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t mn[7], mx[7];
 #pragma unroll
   for (int o = 0; o < 7; o++) {
@@ -262,7 +250,7 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
       mx[o] = min(mx[o], (uint32_t)__shfl_xor((int)mx[o], sh));
     }
   }
-  if (lane == 0) {
+  if (ln == 0) {
 #pragma unroll
     for (int o = 0; o < 7; o++) { red[wv][o] = mn[o]; red[wv][7 + o] = mx[o]; }
   }
@@ -648,82 +636,116 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
 }
 
 // -------------------------------------------------------------- MeanShift ----
-// MeanShift::shift (MeanShift.hpp:41-135) over one landmark's compacted vote list, then the
-// rescale of FaceForest.cpp:255-257.  One wave per (face, landmark): the 64 lanes compute the
-// per-vote terms of 64 consecutive votes in parallel (distance, exp kernel, products — each an
-// element-wise op with the reference's rounding), then the three running sums advance over the
-// 64 terms strictly in list order (readlane + add), so they equal the sequential float sums.
+// MeanShift::shift (MeanShift.hpp:41-135) for one landmark of 64 faces per workgroup, then the
+// rescale of FaceForest.cpp:255-257.  Each pass walks the vote lists in tiles of MS_TILE votes:
+//   parallel phase: all 256 threads compute the per-vote terms (x*w, y*w, w) — element-wise ops
+//                   with the reference's rounding — into LDS;
+//   serial phase:   lane p (one per face) adds its face's MS_TILE terms in list order,
+// so every running sum equals the reference's sequential float sum bit for bit.
+constexpr int MS_FACES = 64, MS_TILE = 32, MS_LD = MS_FACES + 1;
+
 __global__ __launch_bounds__(256) void k_meanshift(const FaceDesc* __restrict__ faces, int n_faces,
-                                                   const HpState* __restrict__ state, int tslots, int n_parts,
-                                                   float lamda, int max_iter, float stop,
-                                                   const Vote* __restrict__ votes,
+                                                   int tslots, int n_parts, float lamda, int max_iter,
+                                                   float stop, const Vote* __restrict__ votes,
                                                    const int32_t* __restrict__ vote_counts,
                                                    float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
-  const int gid = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int f = gid / NPARTS, part = gid % NPARTS;
-  if (f >= n_faces) return;
-  const FaceDesc& fd = faces[f];
-  if (!fd.valid) return;
-  if (part >= n_parts) {
-    if (lane == 0) { out[f].points[part][0] = 0; out[f].points[part][1] = 0; }
-    return;
-  }
-  const int n = fd.nmx * fd.nmy;
-  const Vote* V = votes + fd.vote_off + (int64_t)part * tslots * n;
-  const int cnt = vote_counts[(int64_t)f * NPARTS + part];
-  float mx = 0, my = 0, sw = 0;
-  for (int k0 = 0; k0 < cnt; k0 += 64) {  // getMean
-    const int k = k0 + lane;
-    float px = 0.f, py = 0.f, w = 0.f;
-    if (k < cnt) {
-      const Vote v = V[k];
-      px = v.x * v.w;
-      py = v.y * v.w;
-      w = v.w;
+  __shared__ float tx[MS_TILE * MS_LD], ty[MS_TILE * MS_LD], tw[MS_TILE * MS_LD];
+  __shared__ float s_mx[MS_FACES], s_my[MS_FACES];
+  __shared__ int s_cnt[MS_FACES], s_live[MS_FACES];
+  __shared__ int64_t s_vb[MS_FACES];
+  __shared__ int s_maxcnt, s_nlive;
+  const int part = blockIdx.y, f0 = blockIdx.x * MS_FACES, tid = threadIdx.x;
+  if (tid == 0) { s_maxcnt = 0; s_nlive = 0; }
+  __syncthreads();
+  if (tid < MS_FACES) {
+    const int f = f0 + tid;
+    int cnt = 0;
+    int64_t vb = 0;
+    if (f < n_faces && faces[f].valid) {
+      const FaceDesc& fd = faces[f];
+      cnt = vote_counts[(int64_t)f * NPARTS + part];
+      vb = fd.vote_off + (int64_t)part * tslots * fd.nmx * fd.nmy;
+      if (part >= n_parts) cnt = 0;
     }
-    const int lim = min(64, cnt - k0);
-    for (int j = 0; j < lim; j++) {
-      mx += lane_f(px, j);
-      my += lane_f(py, j);
-      sw += lane_f(w, j);
-    }
+    s_cnt[tid] = cnt;
+    s_vb[tid] = vb;
+    s_live[tid] = (f < n_faces && faces[f].valid) ? 1 : 0;
+    s_mx[tid] = 0.f;
+    s_my[tid] = 0.f;
+    atomicMax(&s_maxcnt, cnt);
   }
-  if (sw > 0) { mx /= sw; my /= sw; }
-  bool conv = false;
-  for (int it = 0; it < max_iter && !conv; it++) {  // getWeightedMean
-    float sx = 0, sy = 0, s = 0;
-    for (int k0 = 0; k0 < cnt; k0 += 64) {
-      const int k = k0 + lane;
-      float px = 0.f, py = 0.f, w = 0.f;
-      if (k < cnt) {
-        const Vote v = V[k];
-        const float dx = mx - (float)v.x, dy = my - (float)v.y;
-        float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
-        d = ffd_expf(-d / lamda);
-        w = v.w * d;
-        px = v.x * w;
-        py = v.y * w;
+  __syncthreads();
+  const int maxcnt = s_maxcnt;
+  // lane p of wave 0 owns face f0 + p; its sums live in registers
+  float ax = 0, ay = 0, aw = 0;
+  // pass = -1: getMean (terms x*w, y*w, w); pass >= 0: getWeightedMean iteration
+  for (int pass = -1; pass < max_iter; pass++) {
+    if (pass >= 0) {
+      if (tid == 0) s_nlive = 0;
+      __syncthreads();
+      if (tid < MS_FACES && s_live[tid]) atomicAdd(&s_nlive, 1);
+      __syncthreads();
+      if (s_nlive == 0) break;
+    }
+    ax = ay = aw = 0;
+    for (int k0 = 0; k0 < maxcnt; k0 += MS_TILE) {
+      for (int i = tid; i < MS_TILE * MS_FACES; i += 256) {  // parallel phase
+        const int j = i % MS_TILE, p = i / MS_TILE, k = k0 + j;
+        float px = 0.f, py = 0.f, w = 0.f;
+        if (k < s_cnt[p] && s_live[p]) {
+          const Vote v = votes[s_vb[p] + k];
+          if (pass < 0) {
+            w = v.w;
+          } else {
+            const float dx = s_mx[p] - (float)v.x, dy = s_my[p] - (float)v.y;
+            float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
+            d = ffd_expf(-d / lamda);
+            w = v.w * d;
+          }
+          px = v.x * w;
+          py = v.y * w;
+        }
+        tx[j * MS_LD + p] = px;
+        ty[j * MS_LD + p] = py;
+        tw[j * MS_LD + p] = w;
       }
-      const int lim = min(64, cnt - k0);
-      for (int j = 0; j < lim; j++) {
-        sx += lane_f(px, j);
-        sy += lane_f(py, j);
-        s += lane_f(w, j);
+      __syncthreads();
+      if (tid < MS_FACES && s_live[tid]) {  // serial phase, in list order
+        const int lim = min(MS_TILE, s_cnt[tid] - k0);
+        for (int j = 0; j < lim; j++) {
+          ax += tx[j * MS_LD + tid];
+          ay += ty[j * MS_LD + tid];
+          aw += tw[j * MS_LD + tid];
+        }
+      }
+      __syncthreads();
+    }
+    if (tid < MS_FACES && s_live[tid]) {
+      if (aw > 0) { ax /= aw; ay /= aw; }
+      if (pass < 0) {
+        s_mx[tid] = ax;
+        s_my[tid] = ay;
+      } else {
+        const float ddx = ax - s_mx[tid], ddy = ay - s_my[tid];
+        if (__builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) s_live[tid] = 0;  // converged
+        s_mx[tid] = ax;
+        s_my[tid] = ay;
       }
     }
-    if (s > 0) { sx /= s; sy /= s; }
-    const float ddx = sx - mx, ddy = sy - my;
-    if (__builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) conv = true;
-    mx = sx;
-    my = sy;
+    __syncthreads();
   }
-  if (lane == 0) {
-    ms_mean[((int64_t)f * NPARTS + part) * 2] = mx;
-    ms_mean[((int64_t)f * NPARTS + part) * 2 + 1] = my;
-    const float inv = 1.0f / fd.scale;  // FaceForest.cpp:255-257
-    out[f].points[part][0] = cv_round((float)cv_round(mx) * inv);
-    out[f].points[part][1] = cv_round((float)cv_round(my) * inv);
+  if (tid < MS_FACES) {
+    const int f = f0 + tid;
+    if (f < n_faces && faces[f].valid) {
+      const float mx = s_mx[tid], my = s_my[tid];
+      if (part < n_parts) {
+        ms_mean[((int64_t)f * NPARTS + part) * 2] = mx;
+        ms_mean[((int64_t)f * NPARTS + part) * 2 + 1] = my;
+      }
+      const float inv = 1.0f / faces[f].scale;  // FaceForest.cpp:255-257
+      out[f].points[part][0] = part < n_parts ? cv_round((float)cv_round(mx) * inv) : 0;
+      out[f].points[part][1] = part < n_parts ? cv_round((float)cv_round(my) * inv) : 0;
+    }
   }
 }
 
@@ -804,9 +826,10 @@ void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const ui
 void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int tslots, int n_parts, float lamda,
                       int max_iter, float stop, const Vote* votes, const int32_t* vote_counts, float* ms_mean,
                       FaceOut* out, hipStream_t s) {
-  const int total = n * NPARTS;  // one wave per (face, landmark), 4 per workgroup
-  k_meanshift<<<(total + 3) / 4, 256, 0, s>>>(faces, n, state, tslots, n_parts, lamda, max_iter, stop, votes,
-                                             vote_counts, ms_mean, out);
+  (void)state;
+  dim3 grid((n + MS_FACES - 1) / MS_FACES, NPARTS);
+  k_meanshift<<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, max_iter, stop, votes, vote_counts, ms_mean,
+                                   out);
 }
 
 }  // namespace ffd
