@@ -8,7 +8,7 @@ PKG       := face_alignment_cvpr_2012_amd
 CSRC      := $(PKG)/csrc
 REFERENCE ?= /root/reference
 
-HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude
+HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Iinclude $(EXTRA)
 CXXFLAGS  := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall -Iinclude
 
 LIB       := $(PKG)/lib/libffd.so

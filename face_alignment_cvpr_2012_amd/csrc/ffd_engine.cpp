@@ -67,6 +67,38 @@ template <class T> void upload(DevBuf& b, const std::vector<T>& v, hipStream_t s
 
 int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
+// Device integrals are kept modulo 2^16; the u8 plane is the exact mod-2^16 second difference,
+// from which the full 32-bit integral ([NCH][H+1][W+1], the reference's layout) is rebuilt.
+void widen_integrals(const uint16_t* J, int64_t plane, int W, int H, uint32_t* out) {
+  const size_t ow = (size_t)W + 1, oplane = ((size_t)H + 1) * ow;
+  for (int c = 0; c < NCH; c++) {
+    const uint16_t* j = J + c * plane;
+    uint32_t* o = out + c * oplane;
+    for (int x = 0; x <= W; x++) o[x] = 0;
+    for (int y = 0; y < H; y++) {
+      uint32_t run = 0;
+      o[(y + 1) * ow] = 0;
+      for (int x = 0; x < W; x++) {
+        const uint16_t v = (uint16_t)(j[(y + 1) * PITCH + x + 1] - j[y * PITCH + x + 1] - j[(y + 1) * PITCH + x] +
+                                      j[y * PITCH + x]);
+        run += v;
+        o[(y + 1) * ow + x + 1] = o[y * ow + x + 1] + run;
+      }
+    }
+  }
+}
+
+// Traversal workgroups per face: one per G x G block of the face's patch grid (max over the chunk).
+int blocks_per_face(const std::vector<FaceDesc>& fds, bool hp, int G) {
+  int m = 0;
+  for (const auto& f : fds)
+    if (f.valid) {
+      const int nx = hp ? f.nhx : f.nmx, ny = hp ? f.nhy : f.nmy;
+      m = std::max(m, ((nx + G - 1) / G) * ((ny + G - 1) / G));
+    }
+  return m;
+}
+
 struct Geometry {
   int W = 0, H = 0, nhx = 0, nhy = 0, nmx = 0, nmy = 0;
   float scale = 0;
@@ -98,10 +130,10 @@ struct ffd_engine {
   ffd_engine_desc desc{};
   int max_chunk = 4096;
   int n_streams = 1;
-  // traversal tuning: LDS bytes per (face, tree) workgroup (staged tree top; also caps occupancy,
-  // hence the faces whose channel sets share one XCD's L2) and interleaved walks per thread.
-  // Overridable with FFD_TRAV_LDS_KB_{HP,FFD} / FFD_TRAV_WALKS / FFD_CHUNK / FFD_STREAMS.
-  int trav_lds_hp = 64 * 1024, trav_lds_mp = 64 * 1024, trav_walks = 2;
+  // traversal tuning: patch block edge G (a workgroup walks all trees of a G x G block of patches
+  // over an LDS copy of the block's integral window) and the breadth-first nodes per tree staged in
+  // LDS.  Overridable with FFD_TRAV_G_{HP,FFD} / FFD_TRAV_KTOP / FFD_CHUNK / FFD_STREAMS.
+  int trav_g_hp = 4, trav_g_mp = 5, trav_ktop = 31;
 
   // model parameters
   int face_size = 125, patch = 31, hp_trees = 0, n_forests = 0, ntrees_per_forest = 0;
@@ -180,6 +212,23 @@ struct ffd_engine {
 
   void load_model(const std::string& path);
   void build_gabor();
+  // Fit the traversal's LDS footprint (window + staged tree tops) into the CU's 160 KB, shrinking
+  // the staged tops first and then the patch block, and raise the kernels' dynamic-LDS limit.
+  void check_traverse_lds() {
+    const int cap = 160 * 1024;
+    auto fit = [&](int& G, int step, int maxT) {
+      for (;;) {
+        int k = trav_ktop;
+        while (k > 1 && traverse_lds_bytes(G, step, k, maxT) > cap) k--;
+        if (traverse_lds_bytes(G, step, k, maxT) <= cap) { trav_ktop = k; return; }
+        if (G <= 3) throw std::runtime_error("traversal window does not fit in LDS (step size too large)");
+        G--;
+      }
+    };
+    fit(trav_g_hp, desc.hp_option.step_size, hp_trees);
+    fit(trav_g_mp, desc.mp_option.step_size, MAX_TREES);
+    HIP_CHECK(set_traverse_lds_limit(cap));
+  }
   void run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out);
   void analyze(const uint8_t* d_images, const std::vector<FaceDesc>& all, FaceOut* d_out);
 };
@@ -426,7 +475,7 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   }
   w.gray.ensure(gray_b + 256);
   w.mag.ensure((mag_e + 64) * 4);
-  w.chan.ensure((ch_e + 64) * 4);
+  w.chan.ensure((ch_e + 256) * 2);  // slack: traversal windows read up to 7 columns past a row
   w.hpleaf.ensure((hp_e + 64) * 4);
   w.mpleaf.ensure((mp_e + 64) * 4);
   w.votes.ensure((vote_e + 64) * sizeof(Vote));
@@ -446,22 +495,22 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
                    w.minmax.as<uint32_t>(), st);
     });
   stage(6, st, [&] {
-    launch_integral(dfd, n, w.gray.as<uint8_t>(), w.mag.as<float>(), w.minmax.as<uint32_t>(), w.chan.as<uint32_t>(),
+    launch_integral(dfd, n, w.gray.as<uint8_t>(), w.mag.as<float>(), w.minmax.as<uint32_t>(), w.chan.as<uint16_t>(),
                     st);
   });
   stage(7, st, [&] {
-    launch_traverse(true, dfd, n, hp_trees, hp_nodes.as<uint4>(), hp_roots.as<int32_t>(), hp_sizes.as<int32_t>(),
-                    nullptr, desc.hp_option.step_size, w.chan.as<uint32_t>(), w.hpleaf.as<int32_t>(), trav_lds_hp,
-                    trav_walks, st);
+    launch_traverse(true, dfd, n, blocks_per_face(fds, true, trav_g_hp), trav_g_hp, hp_nodes.as<uint4>(),
+                    hp_roots.as<int32_t>(), hp_sizes.as<int32_t>(), nullptr, hp_trees, desc.hp_option.step_size,
+                    trav_ktop, hp_trees, w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), st);
   });
   stage(8, st, [&] {
     launch_hp_pose(dfd, n, w.hpleaf.as<int32_t>(), hp_m.as<float>(), hp_trees, n_forests, ntrees_per_forest,
                    w.state.as<HpState>(), d_out, st);
   });
   stage(9, st, [&] {
-    launch_traverse(false, dfd, n, MAX_TREES, mp_nodes.as<uint4>(), mp_roots.as<int32_t>(), mp_sizes.as<int32_t>(),
-                    w.state.as<HpState>(), desc.mp_option.step_size, w.chan.as<uint32_t>(), w.mpleaf.as<int32_t>(),
-                    trav_lds_mp, trav_walks, st);
+    launch_traverse(false, dfd, n, blocks_per_face(fds, false, trav_g_mp), trav_g_mp, mp_nodes.as<uint4>(),
+                    mp_roots.as<int32_t>(), mp_sizes.as<int32_t>(), w.state.as<HpState>(), 0,
+                    desc.mp_option.step_size, trav_ktop, MAX_TREES, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), st);
   });
   const int n_parts = std::min(desc.mp_option.num_parts, NPARTS);
   stage(10, st, [&] {
@@ -586,9 +635,9 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   std::unique_ptr<ffd_engine> e(new ffd_engine());
   e->desc = *d;
   e->device = d->device;
-  if (const char* v = std::getenv("FFD_TRAV_LDS_KB_HP")) e->trav_lds_hp = std::max(1, std::min(160, std::atoi(v))) * 1024;
-  if (const char* v = std::getenv("FFD_TRAV_LDS_KB_FFD")) e->trav_lds_mp = std::max(1, std::min(160, std::atoi(v))) * 1024;
-  if (const char* v = std::getenv("FFD_TRAV_WALKS")) e->trav_walks = std::atoi(v);
+  if (const char* v = std::getenv("FFD_TRAV_G_HP")) e->trav_g_hp = std::max(3, std::min(5, std::atoi(v)));
+  if (const char* v = std::getenv("FFD_TRAV_G_FFD")) e->trav_g_mp = std::max(3, std::min(5, std::atoi(v)));
+  if (const char* v = std::getenv("FFD_TRAV_KTOP")) e->trav_ktop = std::max(1, std::min(255, std::atoi(v)));
   if (const char* v = std::getenv("FFD_CHUNK")) e->max_chunk = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("FFD_STREAMS")) e->n_streams = std::max(1, std::min(8, std::atoi(v)));
   if (d->max_chunk_faces > 0) e->max_chunk = d->max_chunk_faces;
@@ -604,8 +653,8 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
       HIP_CHECK(hipEventCreateWithFlags(&w->done, hipEventDisableTiming));
       e->ws.push_back(std::move(w));
     }
-    HIP_CHECK(set_traverse_lds_limit(std::max(e->trav_lds_hp, e->trav_lds_mp)));
     e->load_model(d->model_path);
+    e->check_traverse_lds();
     e->build_gabor();
   } catch (const HipError& x) {
     return fail(nullptr, FFD_ERR_DEVICE, x.what());
@@ -746,11 +795,11 @@ ffd_status ffd_get_trace(ffd_engine* e, int32_t index, ffd_trace* tr) {
     const int W = f.W, H = f.H;
     if (tr->face)
       HIP_CHECK(hipMemcpy2D(tr->face, W, w.gray.as<uint8_t>() + f.gray_off, PITCH, W, H, hipMemcpyDeviceToHost));
-    if (tr->channels)
-      for (int c = 0; c < NCH; c++)
-        HIP_CHECK(hipMemcpy2D(tr->channels + (size_t)c * (H + 1) * (W + 1), (W + 1) * 4,
-                              w.chan.as<uint32_t>() + f.ch_off + c * f.plane, PITCH * 4, (W + 1) * 4, H + 1,
-                              hipMemcpyDeviceToHost));
+    if (tr->channels) {
+      std::vector<uint16_t> v((size_t)NCH * f.plane);
+      HIP_CHECK(hipMemcpy(v.data(), w.chan.as<uint16_t>() + f.ch_off, v.size() * 2, hipMemcpyDeviceToHost));
+      widen_integrals(v.data(), f.plane, W, H, tr->channels);
+    }
     HpState hs;
     HIP_CHECK(hipMemcpy(&hs, w.state.as<HpState>() + k, sizeof(hs), hipMemcpyDeviceToHost));
     if (tr->hp_leaves) {
@@ -803,7 +852,7 @@ ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t
     f.plane = (int64_t)(H + 1) * PITCH;
     w.gray.ensure((size_t)H * PITCH + 256);
     w.mag.ensure((size_t)NGABOR * H * PITCH * 4 + 256);
-    w.chan.ensure((size_t)NCH * f.plane * 4 + 256);
+    w.chan.ensure((size_t)NCH * f.plane * 2 + 256);
     w.minmax.ensure(NGABOR * 2 * 4);
     std::vector<FaceDesc> one{f};
     upload(w.faces, one, w.stream);
@@ -813,13 +862,13 @@ ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t
     for (int nu = 4; nu >= 0; nu--)
       launch_gabor(nu, dfd, 1, W, H, w.gray.as<uint8_t>(), e->gabor_coef.as<float4>(), w.mag.as<float>(),
                    w.minmax.as<uint32_t>(), w.stream);
-    launch_integral(dfd, 1, w.gray.as<uint8_t>(), w.mag.as<float>(), w.minmax.as<uint32_t>(), w.chan.as<uint32_t>(),
+    launch_integral(dfd, 1, w.gray.as<uint8_t>(), w.mag.as<float>(), w.minmax.as<uint32_t>(), w.chan.as<uint16_t>(),
                     w.stream);
     HIP_CHECK(hipGetLastError());
-    for (int c = 0; c < NCH; c++)
-      HIP_CHECK(hipMemcpy2DAsync(out + (size_t)c * (H + 1) * (W + 1), (W + 1) * 4, w.chan.as<uint32_t>() + c * f.plane,
-                                 PITCH * 4, (W + 1) * 4, H + 1, hipMemcpyDeviceToHost, w.stream));
+    std::vector<uint16_t> v((size_t)NCH * f.plane);
+    HIP_CHECK(hipMemcpyAsync(v.data(), w.chan.p, v.size() * 2, hipMemcpyDeviceToHost, w.stream));
     HIP_CHECK(hipStreamSynchronize(w.stream));
+    widen_integrals(v.data(), f.plane, W, H, out);
     w.count = 0;  // workspace no longer holds a batch
     w.pending = false;
     if (e->last_ws == 0) e->last_ws = -1;
@@ -845,10 +894,13 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* c
     }
     if (n_patches == 0 || n_trees == 0) return FFD_OK;
     const int64_t plane = (int64_t)(H + 1) * PITCH;
-    e->scratch_a.ensure((size_t)NCH * plane * 4);
+    // the device keeps integrals modulo 2^16 (exact for every rectangle the trees read)
+    std::vector<uint16_t> narrow((size_t)NCH * plane, 0);
     for (int c = 0; c < NCH; c++)
-      HIP_CHECK(hipMemcpy2DAsync(e->scratch_a.as<uint32_t>() + c * plane, PITCH * 4, channels + (size_t)c * (H + 1) * (W + 1),
-                                 (W + 1) * 4, (W + 1) * 4, H + 1, hipMemcpyHostToDevice, e->main_stream()));
+      for (int y = 0; y <= H; y++)
+        for (int x = 0; x <= W; x++)
+          narrow[(size_t)c * plane + (size_t)y * PITCH + x] = (uint16_t)channels[((size_t)c * (H + 1) + y) * (W + 1) + x];
+    upload(e->scratch_a, narrow, e->main_stream());
     std::vector<int32_t> pv(patches_xy, patches_xy + 2 * n_patches), tv(tree_ids, tree_ids + n_trees);
     upload(e->scratch_b, pv, e->main_stream());
     upload(e->scratch_c, tv, e->main_stream());
@@ -857,11 +909,11 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* c
     const bool hp = kind == FFD_FOREST_HEADPOSE;
     launch_eval_patches(hp ? e->hp_nodes.as<uint4>() : e->mp_nodes.as<uint4>(),
                         hp ? e->hp_roots.as<int32_t>() : e->mp_roots.as<int32_t>(), e->scratch_c.as<int32_t>(), n_trees,
-                        e->scratch_b.as<int32_t>(), n_patches, e->scratch_a.as<uint32_t>(), plane, outb.as<int32_t>(),
+                        e->scratch_b.as<int32_t>(), n_patches, e->scratch_a.as<uint16_t>(), plane, outb.as<int32_t>(),
                         e->main_stream());
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipMemcpyAsync(leaf_ids, outb.p, (size_t)n_patches * n_trees * 4, hipMemcpyDeviceToHost, e->main_stream()));
-    HIP_CHECK(hipStreamSynchronize(e->main_stream()));
+    HIP_CHECK(hipStreamSynchronize(e->main_stream()));  // `narrow` outlives the upload
     return FFD_OK;
   });
 }

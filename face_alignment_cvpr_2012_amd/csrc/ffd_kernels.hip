@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ f
                                                   const uint8_t* __restrict__ gray,
                                                   const float* __restrict__ mag,
                                                   const uint32_t* __restrict__ minmax,
-                                                  uint32_t* __restrict__ chan) {
+                                                  uint16_t* __restrict__ chan) {
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const FaceDesc fd = faces[blockIdx.y];
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ f
     sf = (float)scale;
     hf = (float)shift;
   }
-  uint32_t* out = chan + fd.ch_off + (int64_t)c * fd.plane;
+  uint16_t* out = chan + fd.ch_off + (int64_t)c * fd.plane;  // integral mod 2^16 (see rect_sum16)
   const int x0 = 2 * lane, x1 = 2 * lane + 1;
   // row 0 of the integral image is zero
   for (int x = lane; x <= W; x += 64) out[x] = 0;
@@ -324,21 +324,22 @@ __global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ f
       if (lane >= d) incl += o;
     }
     uint32_t excl = incl - s;
-    uint32_t* row = out + (int64_t)(y + 1) * PITCH;
+    uint16_t* row = out + (int64_t)(y + 1) * PITCH;
     if (lane == 0) row[0] = 0;
-    if (x0 + 1 <= W) row[x0 + 1] = excl + c0;
-    if (x1 + 1 <= W) row[x1 + 1] = excl + c0 + c1;
+    if (x0 + 1 <= W) row[x0 + 1] = (uint16_t)(excl + c0);
+    if (x1 + 1 <= W) row[x1 + 1] = (uint16_t)(excl + c0 + c1);
   }
 }
 
 // --------------------------------------------------------------- traversal --
-// ImageSample::evalTest integral branch (ImageSample.cpp:48-63): p = (int)(R / (float)area)
-// equals the integer quotient for R in [0, 255*484] (tests/test_numerics.py checks all
-// pairs); computed as rcp estimate + one integer correction step.
-__device__ __forceinline__ int rect_mean(const uint32_t* __restrict__ I, uint32_t off, int w, int h) {
-  const uint32_t a = I[off], b = I[off + w], c = I[off + h * PITCH], d = I[off + h * PITCH + w];
-  const int R = (int)(d - b - c + a);
-  const int area = w * h;
+// Integral channels are stored modulo 2^16 (u16).  A rectangle sum R = d - b - c + a of a u8
+// plane is computed as the sum of its top (h>>1 rows) and bottom halves, each taken mod 2^16:
+// a half covers at most 22 x 11 pixels, so its true sum is <= 255*242 = 61,710 < 2^16 and the
+// modular value is exact; R (<= 123,420) is then exact in 32 bits.
+// ImageSample::evalTest (ImageSample.cpp:48-63): p = (int)(R / (float)area) equals the integer
+// quotient for R in [0, 255*484] (tests/test_numerics.py checks all pairs); computed as an rcp
+// estimate plus one integer correction step.
+__device__ __forceinline__ int idiv_small(int R, int area) {
   int q = (int)((float)R * __builtin_amdgcn_rcpf((float)area));
   const int r = R - q * area;
   q += (r >= area) ? 1 : 0;
@@ -346,134 +347,177 @@ __device__ __forceinline__ int rect_mean(const uint32_t* __restrict__ I, uint32_
   return q;
 }
 
-// Tree<S>::evaluateMT: walk from `node` to a leaf; TreeNode::eval -> (test <= threshold) -> left.
-__device__ __forceinline__ uint32_t walk(const uint4* __restrict__ nodes, uint32_t node,
-                                         const uint32_t* __restrict__ chan, int64_t plane) {
+// I: integral (mod 2^16) at the rectangle's top-left corner; ld: row pitch (elements).
+template <class P>
+__device__ __forceinline__ int rect_mean16(P I, int ld, int w, int h) {
+  const int h1 = h >> 1;
+  const uint32_t a = I[0], b = I[w], c = I[h1 * ld], d = I[h1 * ld + w];
+  const uint32_t e = I[h * ld], f = I[h * ld + w];
+  const uint32_t top = (d - c - b + a) & 0xFFFFu, bot = (f - e - d + c) & 0xFFFFu;
+  return idiv_small((int)(top + bot), w * h);
+}
+
+// Node fields (ffd_device.hpp): rect offsets are encoded for PITCH; re-derive for a pitch `ld`.
+__device__ __forceinline__ int node_off(uint32_t enc, int ld) { return (int)(enc >> 7) * ld + (int)(enc & 127u); }
+
+// Tree<S>::evaluateMT over global u16 planes (ffd_forest_eval_leaves hook).
+__device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint32_t node,
+                                           const uint16_t* __restrict__ chan, int64_t plane) {
   uint4 nd = nodes[node];
   while (!(nd.x & LEAF_BIT)) {
-    const uint32_t* I = chan + (int64_t)(nd.y & 63u) * plane;
-    const int p1 = rect_mean(I, nd.w & 0xFFFFu, (nd.y >> 6) & 31u, (nd.y >> 11) & 31u);
-    const int p2 = rect_mean(I, nd.w >> 16, (nd.y >> 16) & 31u, (nd.y >> 21) & 31u);
+    const uint16_t* I = chan + (int64_t)(nd.y & 63u) * plane;
+    const int p1 = rect_mean16(I + node_off(nd.w & 0xFFFFu, PITCH), PITCH, (nd.y >> 6) & 31u, (nd.y >> 11) & 31u);
+    const int p2 = rect_mean16(I + node_off(nd.w >> 16, PITCH), PITCH, (nd.y >> 16) & 31u, (nd.y >> 21) & 31u);
     node = nd.x + ((p1 - p2) <= (int)nd.z ? 0u : 1u);
     nd = nodes[node];
   }
   return nd.x & ~LEAF_BIT;
 }
 
-// One workgroup = one (face, tree).  The tree's first `top_nodes` breadth-first nodes (its top
-// levels, which every walk visits) are staged in LDS; the LDS size is a launch parameter, so it
-// also caps the workgroups per CU and with them the number of faces whose 2.4 MB channel sets
-// are live in one XCD's 4 MB L2 (face-major block order + XCD remap keep a face on one XCD).
-// Each thread walks NW patches at once (lane order: a wave's lanes read horizontally adjacent
-// patches) so NW independent gather chains are in flight per lane.
-// gfx9 raw buffer resource word 3 (as CK uses for gfx94x/gfx950).
-constexpr int BUF_WORD3 = 0x00020000;
+// One workgroup = one G x G block of patches of one face, ALL its trees.  The block's 38-channel
+// u16 integral window ((32 + step*(G-1))^2 values per channel) and the first `ktop` breadth-first
+// nodes of every tree are staged in LDS, so every rectangle read and the top tree levels are LDS
+// hits; only the deeper node records come from L2.  Items (patch, tree) are assigned tree-major so
+// the lanes of a wave walk one tree over adjacent patches; each thread walks two items at once.
+#ifndef FFD_TRAV_PROBE
+#define FFD_TRAV_PROBE 0
+#endif
+#ifndef FFD_TRAV_NT
+#define FFD_TRAV_NT 1024
+#endif
+constexpr int TRAV_NT = FFD_TRAV_NT;  // threads per traversal workgroup (one workgroup per CU: LDS-bound)
 
-// ImageSample::evalTest on a buffer resource covering one face's 38 integral planes (byte
-// offsets are 32-bit; one VGPR per gather address).
-__device__ __forceinline__ int rect_mean_buf(__amdgpu_buffer_rsrc_t rs, uint32_t boff, uint32_t w, uint32_t h) {
-  const uint32_t a = __builtin_amdgcn_raw_buffer_load_b32(rs, boff, 0, 0);
-  const uint32_t b = __builtin_amdgcn_raw_buffer_load_b32(rs, boff + 4 * w, 0, 0);
-  const uint32_t c = __builtin_amdgcn_raw_buffer_load_b32(rs, boff + 4 * PITCH * h, 0, 0);
-  const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rs, boff + 4 * (PITCH * h + w), 0, 0);
-  const int R = (int)(d - b - c + a);
-  const int area = (int)(w * h);
-  int q = (int)((float)R * __builtin_amdgcn_rcpf((float)area));
-  const int r = R - q * area;
-  q += (r >= area) ? 1 : 0;
-  q -= (r < 0) ? 1 : 0;
-  return q;
-}
+// LDS row pitch (u16) of a traversal window WW columns wide staged from a 4-element aligned column.
+__host__ __device__ __forceinline__ int trav_row_pitch(int WW) { return (WW + 3 + 3) & ~3; }
 
-template <bool HP, int NW>
-__global__ __launch_bounds__(256) void k_traverse(const FaceDesc* __restrict__ faces, int slots,
-                                                  const uint4* __restrict__ nodes, const int32_t* __restrict__ roots,
-                                                  const int32_t* __restrict__ tree_nodes,
-                                                  const HpState* __restrict__ hp_state, int step, int top_cap,
-                                                  const uint32_t* __restrict__ chan,
-                                                  int32_t* __restrict__ leaf_out) {
-  extern __shared__ uint4 top[];
-  // blocks are face-major: `slots` consecutive blocks per face (HP: one per tree; FFD: FFD_MAX_TREES
-  // slots, those beyond the face's selected tree count exit at once)
+struct TravArgs {
+  const FaceDesc* faces;
+  int bpf;                 // blocks per face (grid = n_faces * bpf)
+  const uint4* nodes;
+  const int32_t* roots;
+  const int32_t* tree_nodes;
+  const HpState* hp_state; // FFD pass: selected trees; nullptr for the head-pose pass
+  int ntrees_hp;           // head-pose pass: number of trees
+  int step, ktop, maxT;
+  const uint16_t* chan;
+  int32_t* leaf_out;
+};
+
+template <bool HP, int G, int NT>
+__global__ __launch_bounds__(NT) void k_traverse(TravArgs A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lb = (int)xcd_remap(blockIdx.x, gridDim.x);
-  const int f = lb / slots, t = lb - f * slots;
-  if (!faces[f].valid) return;
-  if (!HP && t >= hp_state[f].n_trees) return;
-  const FaceDesc& fd = faces[f];
-  const int tree = HP ? t : hp_state[f].trees[t];
-  const uint32_t root = (uint32_t)roots[tree];
-  const uint32_t ntop = (uint32_t)min(top_cap, tree_nodes[tree]);
-  const uint32_t plane_b = (uint32_t)fd.plane * 4u;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(chan + fd.ch_off), (short)0, (int)(NCH * plane_b), BUF_WORD3);
-  for (uint32_t i = threadIdx.x; i < ntop; i += 256) top[i] = nodes[root + i];
-  __syncthreads();
+  const int f = lb / A.bpf, b = lb - f * A.bpf;
+  const FaceDesc& fd = A.faces[f];
+  if (!fd.valid) return;
   const int nx = HP ? fd.nhx : fd.nmx, ny = HP ? fd.nhy : fd.nmy, n = nx * ny;
-  int32_t* out = leaf_out + (HP ? fd.hp_off : fd.mp_off) + (int64_t)t * n;
-  // Walk state per interleaved walk (named scalars: keeps everything in VGPRs).
+  const int gbx = (nx + G - 1) / G, gby = (ny + G - 1) / G;
+  if (b >= gbx * gby) return;
+  const int xi0 = (b % gbx) * G, yi0 = (b / gbx) * G;
+  const int step = A.step, px0 = xi0 * step, py0 = yi0 * step;
+  const int WW = 32 + step * (G - 1);              // window: integral cols/rows [p0, p0 + WW)
+  const int sh = px0 & 3, LW = trav_row_pitch(WW);  // LDS row starts at column px0 - sh
+  const int T = HP ? A.ntrees_hp : A.hp_state[f].n_trees;
+  uint4* top = reinterpret_cast<uint4*>(smem);
+  uint16_t* win = reinterpret_cast<uint16_t*>(smem + (size_t)A.maxT * A.ktop * sizeof(uint4));
+  const int tid = threadIdx.x;
+  // stage tree tops
+  for (int i = tid; i < T * A.ktop; i += NT) {
+    const int t = i / A.ktop, k = i - t * A.ktop;
+    const int tree = HP ? t : A.hp_state[f].trees[t];
+    if (k < A.tree_nodes[tree]) top[i] = A.nodes[A.roots[tree] + k];
+  }
+#if FFD_TRAV_PROBE != 2  // timing probes (tools/probe.sh): 1 = stage only, 2 = walk only
+  // Stage the u16 window [c][r][0, LW) in 8-byte chunks from the 8-byte aligned column
+  // px0 - sh (flattened over (c, r, chunk), NT chunks apart per thread, coordinates advanced
+  // incrementally).  Rows beyond the face's integral image are never read.
+  {
+    const int wr = min(WW, fd.H + 1 - py0);
+    const uint2* src = reinterpret_cast<const uint2*>(A.chan + fd.ch_off + (int64_t)py0 * PITCH + (px0 - sh));
+    uint2* dst = reinterpret_cast<uint2*>(win);
+    const int nq = LW >> 2, total = NCH * WW * nq;
+    const int dq = NT % nq, dr = (NT / nq) % WW, dc = NT / (nq * WW);
+    int q = tid % nq, r = (tid / nq) % WW, c = tid / (nq * WW);
+    constexpr int U = 8;
+    for (int base = 0; base < total; base += NT * U) {
+      uint2 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        v[u] = (base + u * NT + tid < total && r < wr) ? src[(c * (int)fd.plane + r * PITCH) / 4 + q] : make_uint2(0, 0);
+        q += dq;
+        int cr = q >= nq;
+        q -= cr ? nq : 0;
+        r += dr + cr;
+        cr = r >= WW;
+        r -= cr ? WW : 0;
+        c += dc + cr;
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (base + u * NT + tid < total) dst[base + u * NT + tid] = v[u];
+    }
+  }
+#endif
+  __syncthreads();
+#if FFD_TRAV_PROBE == 1
+  return;
+#endif
+  const int GG = G * G, items = GG * T;
+  int32_t* out = A.leaf_out + (HP ? fd.hp_off : fd.mp_off);
+
   struct Walk {
     uint4 nd;
-    uint32_t pb;  // patch byte offset in a plane
+    uint32_t root, ktop_t;
+    const uint4* tp;
+    int wbase;   // window offset of the patch's top-left corner
+    int oidx;    // output index
     bool done;
   };
-  auto step_child = [&](const Walk& k) -> uint32_t {
+  auto init = [&](Walk& k, int item) {
+    k.done = true;
+    k.oidx = -1;
+    k.root = 0;
+    k.ktop_t = 0;
+    k.tp = top;
+    k.wbase = 0;
+    k.nd = make_uint4(LEAF_BIT, 0, 0, 0);
+    if (item >= items) return;
+    const int t = item / GG, pl = item - t * GG;
+    const int xi = xi0 + pl % G, yi = yi0 + pl / G;
+    if (xi >= nx || yi >= ny) return;
+    const int tree = HP ? t : A.hp_state[f].trees[t];
+    k.root = (uint32_t)A.roots[tree];
+    k.ktop_t = (uint32_t)min(A.ktop, A.tree_nodes[tree]);
+    k.tp = top + t * A.ktop;
+    k.wbase = (yi - yi0) * step * LW + (xi - xi0) * step + sh;
+    k.oidx = t * n + yi * nx + xi;
+    k.nd = k.tp[0];
+    k.done = false;
+  };
+  auto child = [&](const Walk& k) -> uint32_t {
     const uint4 v = k.nd;
-    const uint32_t base = (v.y & 63u) * plane_b + k.pb;
-    const int p1 = rect_mean_buf(rs, base + 4u * (v.w & 0xFFFFu), (v.y >> 6) & 31u, (v.y >> 11) & 31u);
-    const int p2 = rect_mean_buf(rs, base + 4u * (v.w >> 16), (v.y >> 16) & 31u, (v.y >> 21) & 31u);
+    const uint16_t* I = win + (int)(v.y & 63u) * WW * LW + k.wbase;
+    const int p1 = rect_mean16(I + node_off(v.w & 0xFFFFu, LW), LW, (v.y >> 6) & 31u, (v.y >> 11) & 31u);
+    const int p2 = rect_mean16(I + node_off(v.w >> 16, LW), LW, (v.y >> 16) & 31u, (v.y >> 21) & 31u);
     return v.x + ((p1 - p2) <= (int)v.z ? 0u : 1u);
   };
-  auto init = [&](Walk& k, int q) {
-    k.done = q >= n;
-    k.pb = k.done ? 0u : 4u * (uint32_t)(((q / nx) * PITCH + (q % nx)) * step);
-    k.nd = top[0];
+  auto fetch = [&](const Walk& k, uint32_t nxt) -> uint4 {
+    const uint32_t r = nxt - k.root;
+    return r < k.ktop_t ? k.tp[r] : A.nodes[nxt];
   };
-  for (int q0 = threadIdx.x; q0 < n; q0 += 256 * NW) {
-    Walk A, B, C, D;
-    init(A, q0);
-    init(B, q0 + 256);
-    if (NW > 2) { init(C, q0 + 512); init(D, q0 + 768); } else { C.done = D.done = true; C.nd = D.nd = A.nd; C.pb = D.pb = 0; }
+  for (int i0 = tid; i0 < items; i0 += 2 * NT) {
+    Walk P, Q;
+    init(P, i0);
+    init(Q, i0 + NT);
     for (;;) {
-      A.done = A.done || (A.nd.x & LEAF_BIT);
-      B.done = B.done || (B.nd.x & LEAF_BIT);
-      if (NW > 2) { C.done = C.done || (C.nd.x & LEAF_BIT); D.done = D.done || (D.nd.x & LEAF_BIT); }
-      if (A.done && B.done && (NW <= 2 || (C.done && D.done))) break;
-      // branch-free: every walk issues its 8 gathers before any is consumed (a finished walk
-      // re-evaluates its leaf record: channel 0, offset 0 -> in-range reads, result ignored)
-      const uint32_t na = step_child(A), nb = step_child(B);
-      uint32_t nc = 0, ndd = 0;
-      if (NW > 2) { nc = step_child(C); ndd = step_child(D); }
-      // next node: LDS for the staged top levels, else global; both reads issued for every walk
-      const uint32_t ra = na - root, rb = nb - root, rc = nc - root, rd = ndd - root;
-      const bool ta = ra < ntop, tb = rb < ntop, tc = rc < ntop, td = rd < ntop;
-      const uint4 ga = nodes[(A.done || ta) ? root : na];
-      const uint4 gb = nodes[(B.done || tb) ? root : nb];
-      const uint4 la = top[ta ? ra : 0u];
-      const uint4 lb2 = top[tb ? rb : 0u];
-      uint4 gc = ga, gd = ga, lc = la, ld = la;
-      if (NW > 2) {
-        gc = nodes[(C.done || tc) ? root : nc];
-        gd = nodes[(D.done || td) ? root : ndd];
-        lc = top[tc ? rc : 0u];
-        ld = top[td ? rd : 0u];
-      }
-      auto pick = [](bool keep, const uint4& cur, bool t, const uint4& l, const uint4& g) {
-        const uint4 nv = t ? l : g;  // selects, not branches: keeps the walks' work unconditional
-        return make_uint4(keep ? cur.x : nv.x, keep ? cur.y : nv.y, keep ? cur.z : nv.z, keep ? cur.w : nv.w);
-      };
-      A.nd = pick(A.done, A.nd, ta, la, ga);
-      B.nd = pick(B.done, B.nd, tb, lb2, gb);
-      if (NW > 2) {
-        C.nd = pick(C.done, C.nd, tc, lc, gc);
-        D.nd = pick(D.done, D.nd, td, ld, gd);
-      }
+      P.done = P.done || (P.nd.x & LEAF_BIT);
+      Q.done = Q.done || (Q.nd.x & LEAF_BIT);
+      if (P.done && Q.done) break;
+      if (!P.done) P.nd = fetch(P, child(P));
+      if (!Q.done) Q.nd = fetch(Q, child(Q));
     }
-    if (q0 < n) out[q0] = (int32_t)(A.nd.x & ~LEAF_BIT);
-    if (q0 + 256 < n) out[q0 + 256] = (int32_t)(B.nd.x & ~LEAF_BIT);
-    if (NW > 2) {
-      if (q0 + 512 < n) out[q0 + 512] = (int32_t)(C.nd.x & ~LEAF_BIT);
-      if (q0 + 768 < n) out[q0 + 768] = (int32_t)(D.nd.x & ~LEAF_BIT);
-    }
+    if (P.oidx >= 0) out[P.oidx] = (int32_t)(P.nd.x & ~LEAF_BIT);
+    if (Q.oidx >= 0) out[Q.oidx] = (int32_t)(Q.nd.x & ~LEAF_BIT);
   }
 }
 
@@ -481,13 +525,13 @@ __global__ __launch_bounds__(256) void k_traverse(const FaceDesc* __restrict__ f
 __global__ void k_eval_patches(const uint4* __restrict__ nodes, const int32_t* __restrict__ roots,
                                const int32_t* __restrict__ tree_ids, int n_trees,
                                const int32_t* __restrict__ patches, int n_patches,
-                               const uint32_t* __restrict__ chan, int64_t plane,
+                               const uint16_t* __restrict__ chan, int64_t plane,
                                int32_t* __restrict__ leaf_ids) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_patches * n_trees) return;
   const int p = i / n_trees, t = i % n_trees;
-  const uint32_t* I = chan + patches[2 * p + 1] * PITCH + patches[2 * p];
-  leaf_ids[i] = (int32_t)walk(nodes, (uint32_t)roots[tree_ids[t]], I, plane);
+  const uint16_t* I = chan + patches[2 * p + 1] * PITCH + patches[2 * p];
+  leaf_ids[i] = (int32_t)walk16(nodes, (uint32_t)roots[tree_ids[t]], I, plane);
 }
 
 // -------------------------------------------------- head pose + tree choice --
@@ -769,32 +813,37 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_w, int max_h, co
 }
 
 void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, const float* mag, const uint32_t* minmax,
-                     uint32_t* chan, hipStream_t s) {
+                     uint16_t* chan, hipStream_t s) {
   dim3 grid((NCH + 3) / 4, n);
   k_integral<<<grid, 256, 0, s>>>(faces, gray, mag, minmax, chan);
 }
 
-void launch_traverse(bool hp, const FaceDesc* faces, int n, int slots, const uint4* nodes, const int32_t* roots,
-                     const int32_t* tree_nodes, const HpState* state, int step, const uint32_t* chan,
-                     int32_t* leaf_out, int lds_bytes, int walks, hipStream_t s) {
-  const int total_blocks = n * slots;
+int traverse_lds_bytes(int G, int step, int ktop, int maxT) {
+  const int WW = 32 + step * (G - 1);
+  return maxT * ktop * (int)sizeof(uint4) + NCH * WW * trav_row_pitch(WW) * 2;
+}
+
+void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* nodes, const int32_t* roots,
+                     const int32_t* tree_nodes, const HpState* state, int ntrees_hp, int step, int ktop, int maxT,
+                     const uint16_t* chan, int32_t* leaf_out, hipStream_t s) {
+  const int total_blocks = n * bpf;
   if (total_blocks <= 0) return;
-  const int cap = lds_bytes / (int)sizeof(uint4);
-#define FFD_TRAV(HPV, NWV)                                                                                    \
-  k_traverse<HPV, NWV><<<total_blocks, 256, lds_bytes, s>>>(faces, slots, nodes, roots, tree_nodes, state, step, \
-                                                            cap, chan, leaf_out)
+  TravArgs A{faces, bpf, nodes, roots, tree_nodes, state, ntrees_hp, step, ktop, maxT, chan, leaf_out};
+  const int lds = traverse_lds_bytes(G, step, ktop, maxT);
+#define FFD_TRAV(HPV, GV) k_traverse<HPV, GV, TRAV_NT><<<total_blocks, TRAV_NT, lds, s>>>(A)
   if (hp) {
-    if (walks >= 4) FFD_TRAV(true, 4); else FFD_TRAV(true, 2);
+    if (G == 3) FFD_TRAV(true, 3); else if (G == 5) FFD_TRAV(true, 5); else FFD_TRAV(true, 4);
   } else {
-    if (walks >= 4) FFD_TRAV(false, 4); else FFD_TRAV(false, 2);
+    if (G == 3) FFD_TRAV(false, 3); else if (G == 5) FFD_TRAV(false, 5); else FFD_TRAV(false, 4);
   }
 #undef FFD_TRAV
 }
 
 hipError_t set_traverse_lds_limit(int bytes) {
   hipError_t e = hipSuccess;
-  const void* fns[] = {(const void*)k_traverse<true, 2>, (const void*)k_traverse<true, 4>,
-                       (const void*)k_traverse<false, 2>, (const void*)k_traverse<false, 4>};
+  const void* fns[] = {(const void*)k_traverse<true, 3, TRAV_NT>, (const void*)k_traverse<true, 4, TRAV_NT>,
+                       (const void*)k_traverse<true, 5, TRAV_NT>, (const void*)k_traverse<false, 3, TRAV_NT>,
+                       (const void*)k_traverse<false, 4, TRAV_NT>, (const void*)k_traverse<false, 5, TRAV_NT>};
   for (const void* f : fns) {
     hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (r != hipSuccess) e = r;
@@ -803,7 +852,7 @@ hipError_t set_traverse_lds_limit(int bytes) {
 }
 
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
-                         const int32_t* patches, int n_patches, const uint32_t* chan, int64_t plane,
+                         const int32_t* patches, int n_patches, const uint16_t* chan, int64_t plane,
                          int32_t* leaf_ids, hipStream_t s) {
   const int total = n_patches * n_trees;
   if (total <= 0) return;

@@ -24,13 +24,14 @@ void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uin
 void launch_gabor(int nu, const FaceDesc* faces, int n, int max_w, int max_h, const uint8_t* gray,
                   const float4* coef, float* mag, uint32_t* minmax, hipStream_t s);
 void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, const float* mag, const uint32_t* minmax,
-                     uint32_t* chan, hipStream_t s);
-void launch_traverse(bool hp, const FaceDesc* faces, int n, int slots, const uint4* nodes, const int32_t* roots,
-                     const int32_t* tree_nodes, const HpState* state, int step, const uint32_t* chan,
-                     int32_t* leaf_out, int lds_bytes, int walks, hipStream_t s);
+                     uint16_t* chan, hipStream_t s);
+int traverse_lds_bytes(int G, int step, int ktop, int maxT);
+void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* nodes, const int32_t* roots,
+                     const int32_t* tree_nodes, const HpState* state, int ntrees_hp, int step, int ktop, int maxT,
+                     const uint16_t* chan, int32_t* leaf_out, hipStream_t s);
 hipError_t set_traverse_lds_limit(int bytes);
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
-                         const int32_t* patches, int n_patches, const uint32_t* chan, int64_t plane,
+                         const int32_t* patches, int n_patches, const uint16_t* chan, int64_t plane,
                          int32_t* leaf_ids, hipStream_t s);
 void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const float* hp_m, int hp_trees,
                     int n_forests, int ntrees_per_forest, HpState* state, FaceOut* out, hipStream_t s);
