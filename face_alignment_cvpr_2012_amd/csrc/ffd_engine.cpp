@@ -131,9 +131,9 @@ struct ffd_engine {
   int max_chunk = 4096;
   int n_streams = 1;
   // traversal tuning: patch block edge G (a workgroup walks all trees of a G x G block of patches
-  // over an LDS copy of the block's integral window) and the breadth-first nodes per tree staged in
-  // LDS.  Overridable with FFD_TRAV_G_{HP,FFD} / FFD_TRAV_KTOP / FFD_CHUNK / FFD_STREAMS.
-  int trav_g_hp = 4, trav_g_mp = 5, trav_ktop = 31;
+  // over an LDS copy of the block's integral window) and the persistent workgroups (one per CU).
+  // Overridable with FFD_TRAV_G_{HP,FFD} / FFD_TRAV_WG / FFD_CHUNK / FFD_STREAMS.
+  int trav_g_hp = 4, trav_g_mp = 5, trav_wg = 256;
 
   // model parameters
   int face_size = 125, patch = 31, hp_trees = 0, n_forests = 0, ntrees_per_forest = 0;
@@ -212,22 +212,22 @@ struct ffd_engine {
 
   void load_model(const std::string& path);
   void build_gabor();
-  // Fit the traversal's LDS footprint (window + staged tree tops) into the CU's 160 KB, shrinking
-  // the staged tops first and then the patch block, and raise the kernels' dynamic-LDS limit.
+  // Fit the traversal window into the CU's 160 KB of LDS (and the staging registers), shrinking
+  // the patch block if needed, and raise the kernels' dynamic-LDS limit.
   void check_traverse_lds() {
     const int cap = 160 * 1024;
-    auto fit = [&](int& G, int step, int maxT) {
-      for (;;) {
-        int k = trav_ktop;
-        while (k > 1 && traverse_lds_bytes(G, step, k, maxT) > cap) k--;
-        if (traverse_lds_bytes(G, step, k, maxT) <= cap) { trav_ktop = k; return; }
+    auto fit = [&](int& G, int step) {
+      while (!traverse_window_fits(G, step, cap)) {
         if (G <= 3) throw std::runtime_error("traversal window does not fit in LDS (step size too large)");
         G--;
       }
     };
-    fit(trav_g_hp, desc.hp_option.step_size, hp_trees);
-    fit(trav_g_mp, desc.mp_option.step_size, MAX_TREES);
+    fit(trav_g_hp, desc.hp_option.step_size);
+    fit(trav_g_mp, desc.mp_option.step_size);
     HIP_CHECK(set_traverse_lds_limit(cap));
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    if (!std::getenv("FFD_TRAV_WG")) trav_wg = std::max(8, prop.multiProcessorCount);
   }
   void run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out);
   void analyze(const uint8_t* d_images, const std::vector<FaceDesc>& all, FaceOut* d_out);
@@ -434,13 +434,13 @@ void ffd_engine::build_gabor() {
     }
     const int OFF = GABOR_OFFS[iNu];
     const int ntap = Wk == 7 ? 49 : (Wk * Wk - 1) / 2;  // taps (7x7) or folded pairs
-    for (int t = 0; t < ntap; t++)
+    for (int t = 0; t < ntap; t++)  // interleaved (re, im) per orientation: one packed operand each
       for (int o = 0; o < 7; o++) {
-        coef[OFF + t * 16 + o] = re[o][t];
-        coef[OFF + t * 16 + 8 + o] = im[o][t];
+        coef[OFF + t * 16 + 2 * o] = re[o][t];
+        coef[OFF + t * 16 + 2 * o + 1] = im[o][t];
       }
     if (Wk != 7)
-      for (int o = 0; o < 7; o++) coef[OFF + ntap * 16 + o] = re[o][ntap];  // centre tap
+      for (int o = 0; o < 7; o++) coef[OFF + ntap * 16 + 2 * o] = re[o][ntap];  // centre tap
   }
   upload(gabor_coef, coef, main_stream());
   HIP_CHECK(hipStreamSynchronize(main_stream()));
@@ -500,8 +500,8 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   });
   stage(7, st, [&] {
     launch_traverse(true, dfd, n, blocks_per_face(fds, true, trav_g_hp), trav_g_hp, hp_nodes.as<uint4>(),
-                    hp_roots.as<int32_t>(), hp_sizes.as<int32_t>(), nullptr, hp_trees, desc.hp_option.step_size,
-                    trav_ktop, hp_trees, w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), st);
+                    hp_roots.as<int32_t>(), nullptr, hp_trees, desc.hp_option.step_size, w.chan.as<uint16_t>(),
+                    w.hpleaf.as<int32_t>(), trav_wg, st);
   });
   stage(8, st, [&] {
     launch_hp_pose(dfd, n, w.hpleaf.as<int32_t>(), hp_m.as<float>(), hp_trees, n_forests, ntrees_per_forest,
@@ -509,8 +509,8 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   });
   stage(9, st, [&] {
     launch_traverse(false, dfd, n, blocks_per_face(fds, false, trav_g_mp), trav_g_mp, mp_nodes.as<uint4>(),
-                    mp_roots.as<int32_t>(), mp_sizes.as<int32_t>(), w.state.as<HpState>(), 0,
-                    desc.mp_option.step_size, trav_ktop, MAX_TREES, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), st);
+                    mp_roots.as<int32_t>(), w.state.as<HpState>(), 0, desc.mp_option.step_size,
+                    w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), trav_wg, st);
   });
   const int n_parts = std::min(desc.mp_option.num_parts, NPARTS);
   stage(10, st, [&] {
@@ -637,7 +637,7 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   e->device = d->device;
   if (const char* v = std::getenv("FFD_TRAV_G_HP")) e->trav_g_hp = std::max(3, std::min(5, std::atoi(v)));
   if (const char* v = std::getenv("FFD_TRAV_G_FFD")) e->trav_g_mp = std::max(3, std::min(5, std::atoi(v)));
-  if (const char* v = std::getenv("FFD_TRAV_KTOP")) e->trav_ktop = std::max(1, std::min(255, std::atoi(v)));
+  if (const char* v = std::getenv("FFD_TRAV_WG")) e->trav_wg = std::max(8, std::atoi(v));
   if (const char* v = std::getenv("FFD_CHUNK")) e->max_chunk = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("FFD_STREAMS")) e->n_streams = std::max(1, std::min(8, std::atoi(v)));
   if (d->max_chunk_faces > 0) e->max_chunk = d->max_chunk_faces;

@@ -17,6 +17,7 @@
 //                                MeanShift.hpp:41-135, FaceForest.cpp:255-257
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "../../include/ffd_numerics.h"
@@ -126,6 +127,7 @@ __global__ __launch_bounds__(256) void k_gray_resize(const FaceDesc* __restrict_
 // the restatement's (oracle/ffd_oracle.cpp gabor_mag): 7x7 = OpenCV's direct row-major mul+add;
 // larger = folded pairs S = a+b, D = a-b, fma in row-major pair order, then the centre.
 constexpr int GB_TX = 64, GB_TY = 32, GB_THREADS = 512;
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <int W> struct GaborCfg;
 template <> struct GaborCfg<7>  { static constexpr int nu = 0, off = GABOR_OFF0; };
@@ -165,13 +167,20 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
   // wave w covers threads tx in [8*(w&1), +8) x ty in [8*(w>>1), +8); 4 px per thread
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int tx = (wv & 1) * 8 + (ln & 7), ty = (wv >> 1) * 8 + (ln >> 3);
-  float re[4][7], im[4][7];
+  // acc[k][o] = (re, im): one v_pk_fma_f32 / v_pk_mul+v_pk_add per (pixel, orientation), each
+  // half of which is exactly the scalar fmaf / mul+add of the restatement
+  f2 acc[4][7];
 #pragma unroll
   for (int k = 0; k < 4; k++)
 #pragma unroll
-    for (int o = 0; o < 7; o++) re[k][o] = im[k][o] = 0.f;
+    for (int o = 0; o < 7; o++) acc[k][o] = f2{0.f, 0.f};
   // centre pixel (ty, 4tx + k) sits at tile (ty + R, 4tx + R + k)
   const float* ctr = &tile[(ty + R) * LW + 4 * tx + R];
+  auto load_coef = [&](int t, f2* c) {
+    const float4 c0 = coef[t * 4 + 0], c1 = coef[t * 4 + 1], c2 = coef[t * 4 + 2], c3 = coef[t * 4 + 3];
+    c[0] = f2{c0.x, c0.y}; c[1] = f2{c0.z, c0.w}; c[2] = f2{c1.x, c1.y}; c[3] = f2{c1.z, c1.w};
+    c[4] = f2{c2.x, c2.y}; c[5] = f2{c2.z, c2.w}; c[6] = f2{c3.x, c3.y};
+  };
 
   if constexpr (W == 7) {
     // OpenCV Filter2D direct path: s = 0; s += k*p over taps in row-major order
@@ -179,17 +188,14 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
     for (int t = 0; t < 49; t++) {
       const int dy = t / 7 - 3, dx = t % 7 - 3;
       const float* pa = ctr + dy * LW + dx;
-      const float4 c0 = coef[t * 4 + 0], c1 = coef[t * 4 + 1], c2 = coef[t * 4 + 2], c3 = coef[t * 4 + 3];
-      const float kr[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
-      const float ki[7] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z};
+      f2 c[7];
+      load_coef(t, c);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const float p = pa[k];
+        const f2 pp = f2{p, p};
 #pragma unroll
-        for (int o = 0; o < 7; o++) {
-          re[k][o] = re[k][o] + kr[o] * p;
-          im[k][o] = im[k][o] + ki[o] * p;
-        }
+        for (int o = 0; o < 7; o++) acc[k][o] = acc[k][o] + c[o] * pp;
       }
     }
   } else {
@@ -200,27 +206,23 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
       const int dy = t / W - R, dx = t % W - R;
       const float* pa = ctr + dy * LW + dx;   // a(k) = pa[k]
       const float* pb = ctr - dy * LW - dx;   // b(k) = pb[k]
-      const float4 c0 = coef[t * 4 + 0], c1 = coef[t * 4 + 1], c2 = coef[t * 4 + 2], c3 = coef[t * 4 + 3];
-      const float kr[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
-      const float ki[7] = {c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z};
+      f2 c[7];
+      load_coef(t, c);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const float av = pa[k], bv = pb[k];
-        const float S = av + bv, D = av - bv;
+        const f2 sd = f2{av, av} + f2{bv, -bv};  // (S, D) = (a + b, a - b)
 #pragma unroll
-        for (int o = 0; o < 7; o++) {
-          re[k][o] = fmaf(kr[o], S, re[k][o]);
-          im[k][o] = fmaf(ki[o], D, im[k][o]);
-        }
+        for (int o = 0; o < 7; o++) acc[k][o] = __builtin_elementwise_fma(c[o], sd, acc[k][o]);
       }
     }
-    const float4 c0 = coef[HALF * 4 + 0], c1 = coef[HALF * 4 + 1];
-    const float kr[7] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z};
+    const float4 c0 = coef[HALF * 4 + 0], c1 = coef[HALF * 4 + 1], c2 = coef[HALF * 4 + 2], c3 = coef[HALF * 4 + 3];
+    const float kr[7] = {c0.x, c0.z, c1.x, c1.z, c2.x, c2.z, c3.x};
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const float p0 = ctr[k];
 #pragma unroll
-      for (int o = 0; o < 7; o++) re[k][o] = fmaf(kr[o], p0, re[k][o]);
+      for (int o = 0; o < 7; o++) acc[k][o].x = fmaf(kr[o], p0, acc[k][o].x);
     }
   }
   const int x0 = tx0 + 4 * tx, y = ty0 + ty;
@@ -232,7 +234,7 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
     mx[o] = 0xFFFFFFFFu;  // max kept as min(~bits): one atomicMin serves both
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const float i2 = im[k][o] * im[k][o], r2 = re[k][o] * re[k][o];
+      const float i2 = acc[k][o].y * acc[k][o].y, r2 = acc[k][o].x * acc[k][o].x;
       m4[k] = __builtin_sqrtf(i2 + r2);
       const bool in = (x0 + k) < fd.W && y < fd.H;
       const uint32_t bits = __float_as_uint(m4[k]);  // m >= +0: unsigned order == float order
@@ -374,150 +376,197 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
   return nd.x & ~LEAF_BIT;
 }
 
-// One workgroup = one G x G block of patches of one face, ALL its trees.  The block's 38-channel
-// u16 integral window ((32 + step*(G-1))^2 values per channel) and the first `ktop` breadth-first
-// nodes of every tree are staged in LDS, so every rectangle read and the top tree levels are LDS
-// hits; only the deeper node records come from L2.  Items (patch, tree) are assigned tree-major so
-// the lanes of a wave walk one tree over adjacent patches; each thread walks two items at once.
+// Traversal of all (patch, tree) pairs of a batch.  Work unit = a G x G block of one face's patch
+// grid with ALL the face's trees: the block's 38-channel u16 integral window (WW = 32 + step*(G-1)
+// rows and columns) sits in LDS, so every rectangle read is an LDS read and only node records come
+// from L2.  The window fills the CU's LDS, so the kernel is persistent (one workgroup per CU) and
+// software-pipelined: waves [NW/64, NT/64) load the NEXT block's window into registers while waves
+// [0, NW/64) walk the current block; the registers are committed to LDS between blocks.  Blocks
+// are dealt XCD-contiguously and face-major, so the 32 workgroups of an XCD share one or two faces'
+// planes in that XCD's L2.
 #ifndef FFD_TRAV_PROBE
-#define FFD_TRAV_PROBE 0
+#define FFD_TRAV_PROBE 0  // timing probes (tools/probe.sh): 1 = stage only, 2 = walk only
 #endif
-#ifndef FFD_TRAV_NT
-#define FFD_TRAV_NT 1024
+#ifndef FFD_TRAV_NW
+#define FFD_TRAV_NW 384
 #endif
-constexpr int TRAV_NT = FFD_TRAV_NT;  // threads per traversal workgroup (one workgroup per CU: LDS-bound)
+#ifndef FFD_TRAV_WALKS
+#define FFD_TRAV_WALKS 1
+#endif
+constexpr int TRAV_NT = 1024, TRAV_NW = FFD_TRAV_NW, TRAV_NS = TRAV_NT - TRAV_NW;
+constexpr int TRAV_U = (20480 + TRAV_NS - 1) / TRAV_NS;  // 8-byte window chunks held in registers per staging thread
 
 // LDS row pitch (u16) of a traversal window WW columns wide staged from a 4-element aligned column.
 __host__ __device__ __forceinline__ int trav_row_pitch(int WW) { return (WW + 3 + 3) & ~3; }
 
+constexpr int BUF_WORD3 = 0x00020000;  // raw buffer resource word 3 (gfx950: 32-bit data format)
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
 struct TravArgs {
   const FaceDesc* faces;
-  int bpf;                 // blocks per face (grid = n_faces * bpf)
+  int n_faces, bpf;        // blocks per face: ceil(nx/G) * ceil(ny/G) (max over the batch)
   const uint4* nodes;
   const int32_t* roots;
-  const int32_t* tree_nodes;
   const HpState* hp_state; // FFD pass: selected trees; nullptr for the head-pose pass
   int ntrees_hp;           // head-pose pass: number of trees
-  int step, ktop, maxT;
+  int step;
   const uint16_t* chan;
   int32_t* leaf_out;
 };
 
-template <bool HP, int G, int NT>
-__global__ __launch_bounds__(NT) void k_traverse(TravArgs A) {
+template <bool HP, int G>
+__global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int lb = (int)xcd_remap(blockIdx.x, gridDim.x);
-  const int f = lb / A.bpf, b = lb - f * A.bpf;
-  const FaceDesc& fd = A.faces[f];
-  if (!fd.valid) return;
-  const int nx = HP ? fd.nhx : fd.nmx, ny = HP ? fd.nhy : fd.nmy, n = nx * ny;
-  const int gbx = (nx + G - 1) / G, gby = (ny + G - 1) / G;
-  if (b >= gbx * gby) return;
-  const int xi0 = (b % gbx) * G, yi0 = (b / gbx) * G;
-  const int step = A.step, px0 = xi0 * step, py0 = yi0 * step;
-  const int WW = 32 + step * (G - 1);              // window: integral cols/rows [p0, p0 + WW)
-  const int sh = px0 & 3, LW = trav_row_pitch(WW);  // LDS row starts at column px0 - sh
-  const int T = HP ? A.ntrees_hp : A.hp_state[f].n_trees;
-  uint4* top = reinterpret_cast<uint4*>(smem);
-  uint16_t* win = reinterpret_cast<uint16_t*>(smem + (size_t)A.maxT * A.ktop * sizeof(uint4));
+  uint16_t* win = reinterpret_cast<uint16_t*>(smem);
+  constexpr int NW = TRAV_NW, NS = TRAV_NS, U = TRAV_U, GG = G * G;
   const int tid = threadIdx.x;
-  // stage tree tops
-  for (int i = tid; i < T * A.ktop; i += NT) {
-    const int t = i / A.ktop, k = i - t * A.ktop;
-    const int tree = HP ? t : A.hp_state[f].trees[t];
-    if (k < A.tree_nodes[tree]) top[i] = A.nodes[A.roots[tree] + k];
-  }
-#if FFD_TRAV_PROBE != 2  // timing probes (tools/probe.sh): 1 = stage only, 2 = walk only
-  // Stage the u16 window [c][r][0, LW) in 8-byte chunks from the 8-byte aligned column
-  // px0 - sh (flattened over (c, r, chunk), NT chunks apart per thread, coordinates advanced
-  // incrementally).  Rows beyond the face's integral image are never read.
-  {
-    const int wr = min(WW, fd.H + 1 - py0);
-    const uint2* src = reinterpret_cast<const uint2*>(A.chan + fd.ch_off + (int64_t)py0 * PITCH + (px0 - sh));
-    uint2* dst = reinterpret_cast<uint2*>(win);
-    const int nq = LW >> 2, total = NCH * WW * nq;
-    const int dq = NT % nq, dr = (NT / nq) % WW, dc = NT / (nq * WW);
-    int q = tid % nq, r = (tid / nq) % WW, c = tid / (nq * WW);
-    constexpr int U = 8;
-    for (int base = 0; base < total; base += NT * U) {
-      uint2 v[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        v[u] = (base + u * NT + tid < total && r < wr) ? src[(c * (int)fd.plane + r * PITCH) / 4 + q] : make_uint2(0, 0);
-        q += dq;
-        int cr = q >= nq;
-        q -= cr ? nq : 0;
-        r += dr + cr;
-        cr = r >= WW;
-        r -= cr ? WW : 0;
-        c += dc + cr;
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++)
-        if (base + u * NT + tid < total) dst[base + u * NT + tid] = v[u];
+  const int step = A.step, WW = 32 + step * (G - 1), LW = trav_row_pitch(WW), nq = LW >> 2;
+  const int total = NCH * WW * nq;  // 8-byte chunks per window (host guarantees <= NS * U)
+  // XCD-contiguous, face-major block range of this workgroup's XCD; workgroups of one XCD stride it
+  const int N = A.n_faces * A.bpf, xcd = blockIdx.x & 7, k = blockIdx.x >> 3, nk = gridDim.x >> 3;
+  const int q8 = N >> 3, r8 = N & 7;
+  const int start = xcd * q8 + min(xcd, r8), end = start + q8 + (xcd < r8 ? 1 : 0);
+
+  struct Blk {
+    int f, xi0, yi0, px0, py0, nx, ny, T;
+    bool ok;
+  };
+  auto block = [&](int lb) {
+    Blk B;
+    B.ok = false;
+    B.f = lb / A.bpf;
+    const int b = lb - B.f * A.bpf;
+    const FaceDesc& fd = A.faces[B.f];
+    B.nx = HP ? fd.nhx : fd.nmx;
+    B.ny = HP ? fd.nhy : fd.nmy;
+    const int gbx = (B.nx + G - 1) / G, gby = (B.ny + G - 1) / G;
+    B.xi0 = (b % gbx) * G;
+    B.yi0 = (b / gbx) * G;
+    B.px0 = B.xi0 * step;
+    B.py0 = B.yi0 * step;
+    B.T = 0;
+    if (fd.valid && b < gbx * gby) {
+      B.ok = true;
+      B.T = HP ? A.ntrees_hp : A.hp_state[B.f].n_trees;
     }
-  }
-#endif
-  __syncthreads();
-#if FFD_TRAV_PROBE == 1
-  return;
-#endif
-  const int GG = G * G, items = GG * T;
-  int32_t* out = A.leaf_out + (HP ? fd.hp_off : fd.mp_off);
+    return B;
+  };
+
+  // staging registers: window chunks (c, r, q) of the next block, NS chunks apart
+  // (buffer loads: 32-bit offsets, and reads past the face's planes return 0; window rows below
+  // the face's integral image are never referenced by a patch)
+  v2u st[U];
+  auto prefetch = [&](const Blk& B) {
+    if (tid < NW || !B.ok) return;
+    const FaceDesc& fd = A.faces[B.f];
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(A.chan + fd.ch_off), (short)0, (int)(NCH * fd.plane * 2), BUF_WORD3);
+    const int base_b = (B.py0 * PITCH + (B.px0 & ~3)) * 2, plane_b = (int)fd.plane * 2;
+    int s = tid - NW;
+    asm volatile("" : "+v"(s));  // keep the per-chunk offsets out of loop-invariant hoisting (VGPRs)
+    const int dq = NS % nq, dr = (NS / nq) % WW, dc = NS / (nq * WW);
+    int q = s % nq, r = (s / nq) % WW, c = s / (nq * WW);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, base_b + c * plane_b + r * (PITCH * 2) + q * 8, 0, 0);
+      q += dq;
+      int cr = q >= nq;
+      q -= cr ? nq : 0;
+      r += dr + cr;
+      cr = r >= WW;
+      r -= cr ? WW : 0;
+      c += dc + cr;
+    }
+  };
+  auto commit = [&](const Blk& B) {
+    if (tid < NW || !B.ok) return;
+    v2u* dst = reinterpret_cast<v2u*>(win);
+    const int s = tid - NW;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (u * NS + s < total) dst[u * NS + s] = st[u];
+  };
 
   struct Walk {
     uint4 nd;
-    uint32_t root, ktop_t;
-    const uint4* tp;
-    int wbase;   // window offset of the patch's top-left corner
-    int oidx;    // output index
+    int wbase;  // window offset of the patch's top-left corner
+    int oidx;   // output index
     bool done;
   };
-  auto init = [&](Walk& k, int item) {
-    k.done = true;
-    k.oidx = -1;
-    k.root = 0;
-    k.ktop_t = 0;
-    k.tp = top;
-    k.wbase = 0;
-    k.nd = make_uint4(LEAF_BIT, 0, 0, 0);
-    if (item >= items) return;
-    const int t = item / GG, pl = item - t * GG;
-    const int xi = xi0 + pl % G, yi = yi0 + pl / G;
-    if (xi >= nx || yi >= ny) return;
-    const int tree = HP ? t : A.hp_state[f].trees[t];
-    k.root = (uint32_t)A.roots[tree];
-    k.ktop_t = (uint32_t)min(A.ktop, A.tree_nodes[tree]);
-    k.tp = top + t * A.ktop;
-    k.wbase = (yi - yi0) * step * LW + (xi - xi0) * step + sh;
-    k.oidx = t * n + yi * nx + xi;
-    k.nd = k.tp[0];
-    k.done = false;
-  };
-  auto child = [&](const Walk& k) -> uint32_t {
-    const uint4 v = k.nd;
-    const uint16_t* I = win + (int)(v.y & 63u) * WW * LW + k.wbase;
-    const int p1 = rect_mean16(I + node_off(v.w & 0xFFFFu, LW), LW, (v.y >> 6) & 31u, (v.y >> 11) & 31u);
-    const int p2 = rect_mean16(I + node_off(v.w >> 16, LW), LW, (v.y >> 16) & 31u, (v.y >> 21) & 31u);
-    return v.x + ((p1 - p2) <= (int)v.z ? 0u : 1u);
-  };
-  auto fetch = [&](const Walk& k, uint32_t nxt) -> uint4 {
-    const uint32_t r = nxt - k.root;
-    return r < k.ktop_t ? k.tp[r] : A.nodes[nxt];
-  };
-  for (int i0 = tid; i0 < items; i0 += 2 * NT) {
-    Walk P, Q;
-    init(P, i0);
-    init(Q, i0 + NT);
-    for (;;) {
-      P.done = P.done || (P.nd.x & LEAF_BIT);
-      Q.done = Q.done || (Q.nd.x & LEAF_BIT);
-      if (P.done && Q.done) break;
-      if (!P.done) P.nd = fetch(P, child(P));
-      if (!Q.done) Q.nd = fetch(Q, child(Q));
+  auto walk_block = [&](const Blk& B) {
+    const FaceDesc& fd = A.faces[B.f];
+    const int n = B.nx * B.ny, items = GG * B.T, sh = B.px0 & 3;
+    int32_t* out = A.leaf_out + (HP ? fd.hp_off : fd.mp_off);
+    auto init = [&](Walk& w, int item) {
+      w.done = true;
+      w.oidx = -1;
+      w.wbase = 0;
+      w.nd = make_uint4(LEAF_BIT, 0, 0, 0);
+      if (item >= items) return;
+      const int t = item / GG, pl = item - t * GG;
+      const int xi = B.xi0 + pl % G, yi = B.yi0 + pl / G;
+      if (xi >= B.nx || yi >= B.ny) return;
+      const int tree = HP ? t : A.hp_state[B.f].trees[t];
+      w.wbase = (yi - B.yi0) * step * LW + (xi - B.xi0) * step + sh;
+      w.oidx = t * n + yi * B.nx + xi;
+      w.nd = A.nodes[A.roots[tree]];
+      w.done = false;
+    };
+    // both children's records are requested before the split test is evaluated, so the node
+    // fetch overlaps the LDS rectangle reads (children are adjacent: one 32-byte pair)
+    auto advance = [&](Walk& w) {
+      const uint4 v = w.nd;
+      const uint4 c0 = A.nodes[v.x], c1 = A.nodes[v.x + 1];
+      const uint16_t* I = win + (int)(v.y & 63u) * WW * LW + w.wbase;
+      const int p1 = rect_mean16(I + node_off(v.w & 0xFFFFu, LW), LW, (v.y >> 6) & 31u, (v.y >> 11) & 31u);
+      const int p2 = rect_mean16(I + node_off(v.w >> 16, LW), LW, (v.y >> 16) & 31u, (v.y >> 21) & 31u);
+      w.nd = (p1 - p2) <= (int)v.z ? c0 : c1;
+    };
+    if (FFD_TRAV_WALKS == 2) {
+      for (int i0 = tid; i0 < items; i0 += 2 * NW) {
+        Walk P, Q;
+        init(P, i0);
+        init(Q, i0 + NW);
+        for (;;) {
+          P.done = P.done || (P.nd.x & LEAF_BIT);
+          Q.done = Q.done || (Q.nd.x & LEAF_BIT);
+          if (P.done && Q.done) break;
+          if (!P.done) advance(P);
+          if (!Q.done) advance(Q);
+        }
+        if (P.oidx >= 0) out[P.oidx] = (int32_t)(P.nd.x & ~LEAF_BIT);
+        if (Q.oidx >= 0) out[Q.oidx] = (int32_t)(Q.nd.x & ~LEAF_BIT);
+      }
+    } else {
+      for (int i0 = tid; i0 < items; i0 += NW) {
+        Walk P;
+        init(P, i0);
+        while (!P.done && !(P.nd.x & LEAF_BIT)) advance(P);
+        if (P.oidx >= 0) out[P.oidx] = (int32_t)(P.nd.x & ~LEAF_BIT);
+      }
     }
-    if (P.oidx >= 0) out[P.oidx] = (int32_t)(P.nd.x & ~LEAF_BIT);
-    if (Q.oidx >= 0) out[Q.oidx] = (int32_t)(Q.nd.x & ~LEAF_BIT);
+  };
+
+  int lb = start + k;
+  if (lb >= end) return;
+  Blk cur = block(lb);
+  prefetch(cur);
+  for (; lb < end; lb += nk) {
+    __syncthreads();  // the previous block's walks are done with the window
+#if FFD_TRAV_PROBE != 2
+    commit(cur);
+#endif
+    __syncthreads();
+    Blk nxt;
+    nxt.ok = false;
+    if (lb + nk < end) nxt = block(lb + nk);
+#if FFD_TRAV_PROBE != 2
+    prefetch(nxt);
+#endif
+#if FFD_TRAV_PROBE != 1
+    if (tid < NW && cur.ok) walk_block(cur);
+#endif
+    cur = nxt;
   }
 }
 
@@ -818,19 +867,25 @@ void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, const fl
   k_integral<<<grid, 256, 0, s>>>(faces, gray, mag, minmax, chan);
 }
 
-int traverse_lds_bytes(int G, int step, int ktop, int maxT) {
+int traverse_lds_bytes(int G, int step) {
   const int WW = 32 + step * (G - 1);
-  return maxT * ktop * (int)sizeof(uint4) + NCH * WW * trav_row_pitch(WW) * 2;
+  return NCH * WW * trav_row_pitch(WW) * 2;
+}
+
+bool traverse_window_fits(int G, int step, int lds_cap) {
+  const int WW = 32 + step * (G - 1);
+  return traverse_lds_bytes(G, step) <= lds_cap && NCH * WW * (trav_row_pitch(WW) / 4) <= TRAV_NS * TRAV_U;
 }
 
 void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* nodes, const int32_t* roots,
-                     const int32_t* tree_nodes, const HpState* state, int ntrees_hp, int step, int ktop, int maxT,
-                     const uint16_t* chan, int32_t* leaf_out, hipStream_t s) {
+                     const HpState* state, int ntrees_hp, int step, const uint16_t* chan, int32_t* leaf_out,
+                     int n_wg, hipStream_t s) {
   const int total_blocks = n * bpf;
   if (total_blocks <= 0) return;
-  TravArgs A{faces, bpf, nodes, roots, tree_nodes, state, ntrees_hp, step, ktop, maxT, chan, leaf_out};
-  const int lds = traverse_lds_bytes(G, step, ktop, maxT);
-#define FFD_TRAV(HPV, GV) k_traverse<HPV, GV, TRAV_NT><<<total_blocks, TRAV_NT, lds, s>>>(A)
+  TravArgs A{faces, n, bpf, nodes, roots, state, ntrees_hp, step, chan, leaf_out};
+  const int lds = traverse_lds_bytes(G, step);
+  const int grid = std::max(8, n_wg & ~7);
+#define FFD_TRAV(HPV, GV) k_traverse<HPV, GV><<<grid, TRAV_NT, lds, s>>>(A)
   if (hp) {
     if (G == 3) FFD_TRAV(true, 3); else if (G == 5) FFD_TRAV(true, 5); else FFD_TRAV(true, 4);
   } else {
@@ -841,9 +896,9 @@ void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, cons
 
 hipError_t set_traverse_lds_limit(int bytes) {
   hipError_t e = hipSuccess;
-  const void* fns[] = {(const void*)k_traverse<true, 3, TRAV_NT>, (const void*)k_traverse<true, 4, TRAV_NT>,
-                       (const void*)k_traverse<true, 5, TRAV_NT>, (const void*)k_traverse<false, 3, TRAV_NT>,
-                       (const void*)k_traverse<false, 4, TRAV_NT>, (const void*)k_traverse<false, 5, TRAV_NT>};
+  const void* fns[] = {(const void*)k_traverse<true, 3>, (const void*)k_traverse<true, 4>,
+                       (const void*)k_traverse<true, 5>, (const void*)k_traverse<false, 3>,
+                       (const void*)k_traverse<false, 4>, (const void*)k_traverse<false, 5>};
   for (const void* f : fns) {
     hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (r != hipSuccess) e = r;

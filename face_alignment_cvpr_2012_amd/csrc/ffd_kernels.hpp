@@ -9,7 +9,8 @@
 
 namespace ffd {
 
-// Gabor coefficient table layout (see k_gabor): 16 floats per tap / pair (+ centre for W >= 9).
+// Gabor coefficient table layout (see k_gabor): 16 floats per tap / pair (+ centre for W >= 9):
+// [re0, im0, re1, im1, ..., re6, im6, 0, 0].
 constexpr int GABOR_WIDTHS[5] = {7, 9, 13, 19, 25};
 constexpr int gabor_block(int w) { return w == 7 ? 49 * 16 : ((w * w - 1) / 2 + 1) * 16; }
 constexpr int GABOR_OFF0 = 0;
@@ -25,10 +26,12 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_w, int max_h, co
                   const float4* coef, float* mag, uint32_t* minmax, hipStream_t s);
 void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, const float* mag, const uint32_t* minmax,
                      uint16_t* chan, hipStream_t s);
-int traverse_lds_bytes(int G, int step, int ktop, int maxT);
+int traverse_lds_bytes(int G, int step);
+bool traverse_window_fits(int G, int step, int lds_cap);
+// n_wg: persistent workgroups (one per CU; rounded down to a multiple of 8 XCDs)
 void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* nodes, const int32_t* roots,
-                     const int32_t* tree_nodes, const HpState* state, int ntrees_hp, int step, int ktop, int maxT,
-                     const uint16_t* chan, int32_t* leaf_out, hipStream_t s);
+                     const HpState* state, int ntrees_hp, int step, const uint16_t* chan, int32_t* leaf_out,
+                     int n_wg, hipStream_t s);
 hipError_t set_traverse_lds_limit(int bytes);
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
                          const int32_t* patches, int n_patches, const uint16_t* chan, int64_t plane,
