@@ -40,14 +40,44 @@ def gabor_flops_per_pixel(w):
     return core + 7 * 4
 
 
+# profiler stage -> kernel name prefix in rocprofv3 traces (for the PMC traffic lookup)
+STAGE_KERNELS = {
+    "gray_resize": "ffd::k_gray_resize", "gabor_25x25": "void ffd::k_gabor<25>", "gabor_19x19": "void ffd::k_gabor<19>",
+    "gabor_13x13": "void ffd::k_gabor<13>", "gabor_9x9": "void ffd::k_gabor<9>", "gabor_7x7": "void ffd::k_gabor<7>",
+    "integral_channels": "ffd::k_integral", "headpose_traverse": "void ffd::k_traverse<true",
+    "headpose_reduce_select": "ffd::k_hp_pose", "ffd_traverse": "void ffd::k_traverse<false",
+    "votes": "ffd::k_votes", "meanshift": "ffd::k_meanshift",
+}
+
+
+def measured_traffic(stage, faces_per_launch):
+    """HBM bytes per launch of `stage`'s kernel from the newest committed PMC summary
+    (profiles/<round>/traffic.json, written by tools/pmc_traffic.py from tools/profile_round.sh's
+    FETCH_SIZE / WRITE_SIZE passes over this same 4096-face workload), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "traffic.json")))
+    if not files or faces_per_launch != 4096:
+        return None
+    try:
+        kernels = json.load(open(files[-1]))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    pre = STAGE_KERNELS.get(stage)
+    for name, v in kernels.items():
+        if pre and name.startswith(pre) and v.get("traffic_bytes"):
+            return v["traffic_bytes"]
+    return None
+
+
 def stage_work(stage, n_faces, W=125, H=125, n_hp=576, n_mp=1024, trees=20):
-    """Algorithmic work of one launch of `stage` over n_faces: (amount, unit, bound)."""
-    chan_bytes = 38 * (H + 1) * (W + 1) * 4
+    """Algorithmic work of one launch of `stage` over n_faces: (amount, unit, bound).
+    Integral channels are stored as u16 (integral mod 2^16, DESIGN.md §Data layout)."""
+    chan_bytes = 38 * (H + 1) * (W + 1) * 2
     if stage.startswith("gabor_"):
         w = int(stage.split("_")[1].split("x")[0])
         return n_faces * W * H * gabor_flops_per_pixel(w) / 1e12, "TFLOP/s", "mfma"
     if stage == "integral_channels":
-        return n_faces * (35 * W * H * 4 + W * H + chan_bytes) / 1e9, "GB/s", "hbm"
+        return n_faces * (35 * W * H * 4 + W * H + chan_bytes) / 1e9, "GB/s", "hbm"  # read mag+gray, write planes
     if stage == "headpose_traverse":
         return n_faces * (chan_bytes + n_hp * 15 * 4) / 1e9, "GB/s", "hbm"
     if stage == "ffd_traverse":
@@ -119,6 +149,7 @@ def main():
     import torch.distributed as dist
 
     import face_alignment_cvpr_2012_amd as ffd
+    from face_alignment_cvpr_2012_amd.distributed import gather_records
     from face_alignment_cvpr_2012_amd.synthetic import make_crops
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -134,7 +165,6 @@ def main():
     d_crops = torch.from_numpy(crops).to(dev)
     rec = ffd.FACE_RECORD_BYTES
     d_out = torch.zeros(n * rec, dtype=torch.uint8, device=dev)
-    gathered = torch.empty(world * n * rec, dtype=torch.uint8, device=dev) if (world > 1 and rank == 0) else None
     torch.cuda.synchronize()
 
     chunk = args.chunk if 0 < args.chunk < n else 0  # 0: engine default (FFD_CHUNK)
@@ -146,11 +176,8 @@ def main():
         ff.analyze_device(d_crops.data_ptr(), CROP * CROP * 3, CROP, CROP, CROP * 3, n, boxes, box_img,
                           d_out.data_ptr())
         ff.synchronize()
-        if world > 1:  # RCCL gather of the ffd_face records to rank 0
-            if rank == 0:
-                dist.gather(d_out, gather_list=list(gathered.chunk(world)), dst=0)
-            else:
-                dist.gather(d_out, dst=0)
+        if world > 1:  # one RCCL gather of the ffd_face records to rank 0 (faces sharded, no other exchange)
+            gather_records(d_out, world * n, dst=0)
 
     for _ in range(args.warmup):
         step()
@@ -183,6 +210,9 @@ def main():
         faces_per_launch = n * args.steps / launches  # one launch covers one chunk of faces
         amount, unit, bound = stage_work(dom, faces_per_launch)
         achieved = amount / (avg_ms / 1e3)
+        traffic = measured_traffic(dom, faces_per_launch)  # HBM bytes per launch (PMC), or None
+        if traffic is not None:
+            traffic = int(traffic)
         peak = FP32_PEAK_TFLOPS if unit == "TFLOP/s" else HBM_PEAK_GBS
         b_face = CROP * CROP * 3 + 2 * 38 * 126 * 126 * 4 + 100
         out = {
@@ -196,7 +226,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8/u32/f32",
+            "dtype": "u8/u16/i32/f32",
             "data": "synthetic: 4096 C2 150x150 crops per GPU from the 20 bundled LFW faces (seed 2012+rank); "
                     "pretrained reference forests converted to model/ffd_model.bin",
             "config": {"workload": "C2: batch of 4096 pre-cropped 150x150 faces per GPU, pretrained "
@@ -205,8 +235,10 @@ def main():
             "landmark_px_error_vs_cpu": 0.0 if ok else None,
             "parity_spot_check": bool(ok),
             "roofline": {"bound": bound, "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-                         "frac": round(achieved / peak, 4), "traffic": None,
-                         "avg_launch_ms": round(avg_ms, 4), "faces_per_launch": faces_per_launch},
+                         "frac": round(achieved / peak, 4), "traffic": traffic,
+                         "avg_launch_ms": round(avg_ms, 4), "faces_per_launch": faces_per_launch,
+                         "algorithmic_bytes": int(amount * 1e9) if unit == "GB/s" else None,
+                         "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"},
             "path_hbm_roofline": {"b_face": b_face, "achieved_GBs": round(value * b_face / 1e9, 1),
                                   "frac": round(value * b_face / 1e9 / HBM_PEAK_GBS, 4)},
             "stage_ms_per_step": {k: round(v[0] / max(1, args.steps), 3) for k, v in stages.items()},

@@ -1,0 +1,76 @@
+"""Multi-rank path on CPU (gloo, world_size 2): faces sharded in contiguous blocks, results
+gathered once.  Records are produced by the oracle here because there is no GPU
+in the build container; on the GPU box bench.py runs the same helpers over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import face_alignment_cvpr_2012_amd as ffd
+from face_alignment_cvpr_2012_amd.distributed import gather_records, shard_bounds
+
+N_FACES = 5  # ragged over 2 ranks: 3 + 2
+
+
+def test_shard_bounds_cover_exactly():
+    for n in (0, 1, 5, 4096, 4097):
+        for world in (1, 2, 3, 8):
+            spans = [shard_bounds(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert max(hi - lo for lo, hi in spans) == -(-n // world)
+    with pytest.raises(ValueError):
+        shard_bounds(4, 2, 2)
+
+
+def _records(model_path, lo, hi):
+    import oracle
+    from conftest import crops
+    oracle.load_model(model_path)
+    imgs = crops(N_FACES, seed=31)
+    out = bytearray()
+    for k in range(lo, hi):
+        f, _ = oracle.analyze_face(imgs[k], (0, 0, 150, 150), threads=2)
+        r = ffd._Face()
+        r.headpose, r.pose_variance, r.n_trees = f["headpose"], f["pose_variance"], f["n_trees"]
+        r.bbox.width = r.bbox.height = 150
+        for i in range(10):
+            r.points[i][0], r.points[i][1] = int(f["points"][i][0]), int(f["points"][i][1])
+        out += bytes(r)
+    return torch.frombuffer(bytearray(out), dtype=torch.uint8) if out else torch.zeros(0, dtype=torch.uint8)
+
+
+def _worker(rank, world, port, model_path, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = shard_bounds(N_FACES, world, rank)
+        got = gather_records(_records(model_path, lo, hi), N_FACES, dst=0)
+        if rank == 0:
+            np.save(result_path, got.numpy())
+        else:
+            assert got is None
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_gloo_two_ranks_gather_equals_serial(tmp_path, model_path):
+    path = str(tmp_path / "gathered.npy")
+    mp.spawn(_worker, args=(2, _free_port(), model_path, path), nprocs=2, join=True)
+    gathered = np.load(path)
+    serial = _records(model_path, 0, N_FACES).numpy()
+    assert gathered.shape == serial.shape == (N_FACES * ffd.FACE_RECORD_BYTES,)
+    assert np.array_equal(gathered, serial)
+    faces = ffd.faces_from_records(gathered.tobytes())
+    assert len(faces) == N_FACES
