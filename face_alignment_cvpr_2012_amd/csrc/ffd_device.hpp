@@ -3,7 +3,8 @@
 // HBM layout (per face, row pitch PITCH elements, see DESIGN.md §Data layout):
 //   gray   u8  [H][PITCH]                  scaled gray face (FaceForest.cpp:195-204)
 //   mag    f32 [35][H][PITCH]              Gabor magnitudes before min-max normalisation
-//   chan   u32 [38][H+1][PITCH]            integral channels (ImageSample m_feature_channels)
+//   chan   u16 [38][H+1][PITCH]            integral channels mod 2^16 (ImageSample m_feature_channels;
+//                                          every rectangle the trees read is exact, ffd_kernels.hip rect_mean16)
 //   hpleaf i32 [15][n_hp]                  head-pose leaf ordinal per (tree, patch lane-order)
 //   mpleaf i32 [T][n_mp]                   FFD leaf ordinal per (tree slot, patch lane-order)
 //   votes  {i16 x,y; f32 w} [10][T*n_mp]   compacted votes per landmark (MeanShift input)

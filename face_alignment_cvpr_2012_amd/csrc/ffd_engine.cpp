@@ -140,7 +140,7 @@ struct ffd_engine {
   int64_t hp_leaves = 0, mp_leaves = 0;
 
   // device model
-  DevBuf gabor_coef, hp_nodes, hp_roots, hp_sizes, hp_m, mp_nodes, mp_roots, mp_sizes, mp_mask, mp_fg, mp_offs;
+  DevBuf gabor_coef, hp_nodes, hp_roots, hp_sizes, hp_m, mp_nodes, mp_roots, mp_sizes, mp_rec;
 
   std::vector<std::unique_ptr<Workspace>> ws;
   DevBuf images, out, scratch_a, scratch_b, scratch_c;  // host-API staging (ws[0] stream)
@@ -368,9 +368,7 @@ void ffd_engine::load_model(const std::string& path) {
     const auto& var = m.get("mp.leaf_var");
     const auto& pf = m.get("mp.leaf_pf");
     mp_leaves = (int64_t)n.count();
-    std::vector<uint32_t> mask(mp_leaves);
-    std::vector<float> w(mp_leaves);
-    std::vector<int32_t> o(mp_leaves * NPARTS);
+    std::vector<uint32_t> rec(mp_leaves * 16, 0);  // 64-B records {mask, fg bits, off[10], pad} (k_votes)
     const auto& op = desc.mp_option;
     const int np = std::min(op.num_parts, NPARTS);
     for (int64_t L = 0; L < mp_leaves; L++) {
@@ -383,16 +381,15 @@ void ffd_engine::load_model(const std::string& path) {
             n.as<int32_t>()[L] > op.min_samples)
           mk |= 1u << i;
       }
-      mask[L] = mk;
-      w[L] = f;
+      uint32_t* r = &rec[L * 16];
+      r[0] = mk;
+      std::memcpy(&r[1], &f, 4);
       for (int i = 0; i < NPARTS; i++) {
         const int16_t x = off.as<int16_t>()[(L * 10 + i) * 2], y = off.as<int16_t>()[(L * 10 + i) * 2 + 1];
-        o[L * NPARTS + i] = (int32_t)((uint32_t)(uint16_t)x | (uint32_t)(uint16_t)y << 16);
+        r[2 + i] = (uint32_t)(uint16_t)x | (uint32_t)(uint16_t)y << 16;
       }
     }
-    upload(mp_mask, mask, main_stream());
-    upload(mp_fg, w, main_stream());
-    upload(mp_offs, o, main_stream());
+    upload(mp_rec, rec, main_stream());
   }
   HIP_CHECK(hipStreamSynchronize(main_stream()));
 }
@@ -514,9 +511,8 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   });
   const int n_parts = std::min(desc.mp_option.num_parts, NPARTS);
   stage(10, st, [&] {
-    launch_votes(dfd, n, w.mpleaf.as<int32_t>(), mp_mask.as<uint32_t>(), mp_fg.as<float>(), mp_offs.as<int32_t>(),
-                 w.state.as<HpState>(), MAX_TREES, desc.mp_option.step_size, patch / 2, n_parts, w.votes.as<Vote>(),
-                 w.vote_counts.as<int32_t>(), st);
+    launch_votes(dfd, n, w.mpleaf.as<int32_t>(), mp_rec.as<uint4>(), w.state.as<HpState>(), MAX_TREES,
+                 desc.mp_option.step_size, patch / 2, n_parts, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), st);
   });
   stage(11, st, [&] {
     launch_meanshift(dfd, n, w.state.as<HpState>(), MAX_TREES, n_parts, (float)desc.ms_option.kernel_size,

@@ -13,8 +13,9 @@
 //                                ImageSample.cpp:48-63
 //   head-pose reduction + tree   face_utils.cpp:218-241,304-323,      k_hp_pose
 //   selection                    FaceForest.cpp:214-250
-//   vote filter + MeanShift      face_utils.cpp:276-301,              k_votes_meanshift
-//                                MeanShift.hpp:41-135, FaceForest.cpp:255-257
+//   vote filter                  face_utils.cpp:276-301               k_votes
+//   MeanShift + rescale          MeanShift.hpp:41-135,                k_meanshift
+//                                FaceForest.cpp:255-257
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -677,8 +678,7 @@ __global__ __launch_bounds__(256) void k_hp_pose(const FaceDesc* __restrict__ fa
 // the reference's vote order exactly.
 __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ faces, int n_faces,
                                                const int32_t* __restrict__ mp_leaf,
-                                               const uint32_t* __restrict__ mask, const float* __restrict__ fg,
-                                               const int32_t* __restrict__ offs, const HpState* __restrict__ state,
+                                               const uint4* __restrict__ leaf_rec, const HpState* __restrict__ state,
                                                int tslots, int step, int half_patch, int n_parts,
                                                Vote* __restrict__ votes, int32_t* __restrict__ vote_counts) {
   const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -694,29 +694,55 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
   int cnt[NPARTS];
 #pragma unroll
   for (int i = 0; i < NPARTS; i++) cnt[i] = 0;
-  for (int base = 0; base < total; base += 64) {
-    const int k = base + lane;
-    uint32_t mk = 0;
-    int leaf = 0, vx0 = 0, vy0 = 0;
-    if (k < total) {
-      const int pr = k / T, t = k - pr * T;
-      const int xi = pr / ny, yi = pr - xi * ny;
-      leaf = L[(int64_t)t * n + yi * nx + xi];
-      mk = mask[leaf];
-      vx0 = xi * step + half_patch;
-      vy0 = yi * step + half_patch;
-    }
-    const float w = mk ? fg[leaf] : 0.f;
+#ifndef FFD_VOTE_U
+#define FFD_VOTE_U 4
+#endif
+  constexpr int U = FFD_VOTE_U;  // 64-item batches whose loads are in flight together
+  for (int base = 0; base < total; base += 64 * U) {
+    int leaf[U], vx0[U], vy0[U];
 #pragma unroll
-    for (int i = 0; i < NPARTS; i++) {  // mask bits >= n_parts are never set (engine load)
-      const bool vote = (mk >> i) & 1u;
-      const uint64_t bal = __ballot(vote);
-      if (vote) {
-        const int pos = cnt[i] + __popcll(bal & below);
-        const int32_t o = offs[(int64_t)leaf * NPARTS + i];
-        V[i * cap + pos] = Vote{(int16_t)((int)(int16_t)(o & 0xFFFF) + vx0), (int16_t)((int)(int16_t)(o >> 16) + vy0), w};
+    for (int u = 0; u < U; u++) {
+      const int k = base + u * 64 + lane;
+      leaf[u] = -1;
+      vx0[u] = vy0[u] = 0;
+      if (k < total) {
+        const int pr = k / T, t = k - pr * T;
+        const int xi = pr / ny, yi = pr - xi * ny;
+        leaf[u] = L[(int64_t)t * n + yi * nx + xi];
+        vx0[u] = xi * step + half_patch;
+        vy0[u] = yi * step + half_patch;
       }
-      cnt[i] += __popcll(bal);
+    }
+    // packed 64-B leaf records (one sector): {mask, fg, off[0..9], pad} with off = x | y << 16
+    uint4 r0[U], r1[U], r2[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      r0[u] = r1[u] = r2[u] = make_uint4(0, 0, 0, 0);
+      if (leaf[u] >= 0) {
+        const uint4* rec = leaf_rec + (int64_t)leaf[u] * 4;
+        r0[u] = rec[0];
+        r1[u] = rec[1];
+        r2[u] = rec[2];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {  // batches in list order: (patch x-major, tree), then part
+      const uint32_t mk = r0[u].x;
+      const float w = __uint_as_float(r0[u].y);
+      const uint32_t off[NPARTS] = {r0[u].z, r0[u].w, r1[u].x, r1[u].y, r1[u].z,
+                                    r1[u].w, r2[u].x, r2[u].y, r2[u].z, r2[u].w};
+#pragma unroll
+      for (int i = 0; i < NPARTS; i++) {  // mask bits >= n_parts are never set (engine load)
+        const bool vote = (mk >> i) & 1u;
+        const uint64_t bal = __ballot(vote);
+        if (vote) {
+          const int pos = cnt[i] + __popcll(bal & below);
+          const int32_t o = (int32_t)off[i];
+          V[i * cap + pos] = Vote{(int16_t)((int)(int16_t)(o & 0xFFFF) + vx0[u]),
+                                  (int16_t)((int)(int16_t)(o >> 16) + vy0[u]), w};
+        }
+        cnt[i] += __popcll(bal);
+      }
     }
   }
   if (lane < n_parts) {
@@ -735,9 +761,18 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
 //                   with the reference's rounding — into LDS;
 //   serial phase:   lane p (one per face) adds its face's MS_TILE terms in list order,
 // so every running sum equals the reference's sequential float sum bit for bit.
-constexpr int MS_FACES = 64, MS_TILE = 32, MS_LD = MS_FACES + 1;
+#ifndef FFD_MS_FACES
+#define FFD_MS_FACES 32
+#endif
+#ifndef FFD_MS_TILE
+#define FFD_MS_TILE 64
+#endif
+#ifndef FFD_MS_THREADS
+#define FFD_MS_THREADS 256
+#endif
+constexpr int MS_FACES = FFD_MS_FACES, MS_TILE = FFD_MS_TILE, MS_LD = MS_FACES + 1, MS_THREADS = FFD_MS_THREADS;
 
-__global__ __launch_bounds__(256) void k_meanshift(const FaceDesc* __restrict__ faces, int n_faces,
+__global__ __launch_bounds__(MS_THREADS) void k_meanshift(const FaceDesc* __restrict__ faces, int n_faces,
                                                    int tslots, int n_parts, float lamda, int max_iter,
                                                    float stop, const Vote* __restrict__ votes,
                                                    const int32_t* __restrict__ vote_counts,
@@ -782,7 +817,7 @@ __global__ __launch_bounds__(256) void k_meanshift(const FaceDesc* __restrict__ 
     }
     ax = ay = aw = 0;
     for (int k0 = 0; k0 < maxcnt; k0 += MS_TILE) {
-      for (int i = tid; i < MS_TILE * MS_FACES; i += 256) {  // parallel phase
+      for (int i = tid; i < MS_TILE * MS_FACES; i += MS_THREADS) {  // parallel phase
         const int j = i % MS_TILE, p = i / MS_TILE, k = k0 + j;
         float px = 0.f, py = 0.f, w = 0.f;
         if (k < s_cnt[p] && s_live[p]) {
@@ -920,11 +955,10 @@ void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const 
   k_hp_pose<<<(n + 3) / 4, 256, 0, s>>>(faces, n, hp_leaf, hp_m, hp_trees, n_forests, ntrees_per_forest, state, out);
 }
 
-void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint32_t* mask, const float* fg,
-                  const int32_t* offs, const HpState* state, int tslots, int step, int half_patch, int n_parts,
-                  Vote* votes, int32_t* vote_counts, hipStream_t s) {
-  k_votes<<<(n + 3) / 4, 256, 0, s>>>(faces, n, mp_leaf, mask, fg, offs, state, tslots, step, half_patch, n_parts,
-                                      votes, vote_counts);
+void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint4* leaf_rec, const HpState* state,
+                  int tslots, int step, int half_patch, int n_parts, Vote* votes, int32_t* vote_counts, hipStream_t s) {
+  k_votes<<<(n + 3) / 4, 256, 0, s>>>(faces, n, mp_leaf, leaf_rec, state, tslots, step, half_patch, n_parts, votes,
+                                      vote_counts);
 }
 
 void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int tslots, int n_parts, float lamda,
@@ -932,7 +966,7 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
                       FaceOut* out, hipStream_t s) {
   (void)state;
   dim3 grid((n + MS_FACES - 1) / MS_FACES, NPARTS);
-  k_meanshift<<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, max_iter, stop, votes, vote_counts, ms_mean,
+  k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, max_iter, stop, votes, vote_counts, ms_mean,
                                    out);
 }
 

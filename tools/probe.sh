@@ -15,5 +15,5 @@ for extra in "$@"; do
   rc=$?
   cat gpurun_out/probe_tmp.log >> gpurun_out/probe_$TAG.log
   if [ $rc -ne 0 ]; then echo "rc=$rc ($extra)"; exit $rc; fi
-  python3 -c "import json,sys; d=json.loads(open('gpurun_out/probe_tmp.log').read().strip().splitlines()[-1]); s=d['stage_ms_per_step']; print(json.dumps({'extra': sys.argv[1], 'value': d['value'], 'hp': s['headpose_traverse'], 'ffd': s['ffd_traverse'], 'ok': d['parity_spot_check']}))" "$extra" | tee -a "$OUT"
+  python3 -c "import json,sys; d=json.loads(open('gpurun_out/probe_tmp.log').read().strip().splitlines()[-1]); s=d['stage_ms_per_step']; print(json.dumps({'extra': sys.argv[1], 'value': d['value'], 'ok': d['parity_spot_check'], 'stages': s}))" "$extra" | tee -a "$OUT"
 done
