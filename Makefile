@@ -15,12 +15,13 @@ LIB       := $(PKG)/lib/libffd.so
 CONVERT   := $(PKG)/bin/ffd_convert
 ORACLE    := oracle/build/libffd_oracle.so
 MODEL     := model/ffd_model.bin
+EXAMPLE   := examples/build/analyze_face
 
 HIP_OBJS  := $(PKG)/lib/ffd_kernels.o $(PKG)/lib/ffd_engine.o
 HDRS      := include/ffd.h include/ffd_numerics.h include/ffd_model_format.h $(CSRC)/ffd_device.hpp \
              $(CSRC)/ffd_kernels.hpp $(CSRC)/model_io.hpp
 
-all: $(LIB) $(CONVERT) $(ORACLE)
+all: $(LIB) $(CONVERT) $(ORACLE) $(EXAMPLE)
 
 $(PKG)/lib/ffd_kernels.o: $(CSRC)/ffd_kernels.hip $(HDRS)
 	@mkdir -p $(@D)
@@ -49,3 +50,9 @@ clean:
 	rm -rf $(PKG)/lib $(PKG)/bin oracle/build
 
 .PHONY: all model clean
+
+$(EXAMPLE): examples/analyze_face.cpp include/FaceForest.hpp include/ffd.h $(LIB)
+	@mkdir -p $(@D)
+	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(PKG)/lib -lffd -Wl,-rpath,'$$ORIGIN/../../$(PKG)/lib'
+example: $(EXAMPLE)
+.PHONY: example
