@@ -128,6 +128,9 @@ __global__ __launch_bounds__(256) void k_gray_resize(const FaceDesc* __restrict_
 // the restatement's (oracle/ffd_oracle.cpp gabor_mag): 7x7 = OpenCV's direct row-major mul+add;
 // larger = folded pairs S = a+b, D = a-b, fma in row-major pair order, then the centre.
 constexpr int GB_TX = 64, GB_TY = 32, GB_THREADS = 512;
+#ifndef GB_UNROLL
+#define GB_UNROLL 1
+#endif
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <int W> struct GaborCfg;
@@ -183,30 +186,31 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
     c[4] = f2{c2.x, c2.y}; c[5] = f2{c2.z, c2.w}; c[6] = f2{c3.x, c3.y};
   };
 
+  // Kernel rows are an outer loop and the taps of a row an inner loop with per-tap pointer steps
+  // (two address adds per tap against 28 packed FMAs).
   if constexpr (W == 7) {
     // OpenCV Filter2D direct path: s = 0; s += k*p over taps in row-major order
 #pragma unroll 1
-    for (int t = 0; t < 49; t++) {
-      const int dy = t / 7 - 3, dx = t % 7 - 3;
-      const float* pa = ctr + dy * LW + dx;
-      f2 c[7];
-      load_coef(t, c);
+    for (int r = 0; r < 7; r++) {
+      const float* prow = ctr + (r - 3) * LW;
+#pragma unroll GB_UNROLL
+      for (int dxi = 0; dxi < 7; dxi++) {
+        const float* pa = prow + (dxi - 3);
+        f2 c[7];
+        load_coef(r * 7 + dxi, c);
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const float p = pa[k];
-        const f2 pp = f2{p, p};
+        for (int k = 0; k < 4; k++) {
+          const float p = pa[k];
+          const f2 pp = f2{p, p};
 #pragma unroll
-        for (int o = 0; o < 7; o++) acc[k][o] = acc[k][o] + c[o] * pp;
+          for (int o = 0; o < 7; o++) acc[k][o] = acc[k][o] + c[o] * pp;
+        }
       }
     }
   } else {
     // folded pairs t = (dy + R) * W + (dx + R), rows dy = -R .. 0, row 0 only dx < 0
     constexpr int HALF = (W * W - 1) / 2;
-#pragma unroll 1
-    for (int t = 0; t < HALF; t++) {
-      const int dy = t / W - R, dx = t % W - R;
-      const float* pa = ctr + dy * LW + dx;   // a(k) = pa[k]
-      const float* pb = ctr - dy * LW - dx;   // b(k) = pb[k]
+    auto pair = [&](const float* pa, const float* pb, int t) {  // a(k) = pa[k], b(k) = pb[k]
       f2 c[7];
       load_coef(t, c);
 #pragma unroll
@@ -216,7 +220,16 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
 #pragma unroll
         for (int o = 0; o < 7; o++) acc[k][o] = __builtin_elementwise_fma(c[o], sd, acc[k][o]);
       }
+    };
+#pragma unroll 1
+    for (int r = 0; r < R; r++) {  // dy = r - R < 0: full rows
+      const float* rowa = ctr + (r - R) * LW;
+      const float* rowb = ctr - (r - R) * LW;
+#pragma unroll GB_UNROLL
+      for (int dxi = 0; dxi < W; dxi++) pair(rowa + (dxi - R), rowb - (dxi - R), r * W + dxi);
     }
+#pragma unroll GB_UNROLL
+    for (int dxi = 0; dxi < R; dxi++) pair(ctr + (dxi - R), ctr - (dxi - R), R * W + dxi);  // dy = 0
     const float4 c0 = coef[HALF * 4 + 0], c1 = coef[HALF * 4 + 1], c2 = coef[HALF * 4 + 2], c3 = coef[HALF * 4 + 3];
     const float kr[7] = {c0.x, c0.z, c1.x, c1.z, c2.x, c2.z, c3.x};
 #pragma unroll
@@ -312,25 +325,52 @@ __global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ f
     sf = (float)scale;
     hf = (float)shift;
   }
-  uint16_t* out = chan + fd.ch_off + (int64_t)c * fd.plane;  // integral mod 2^16 (see rect_sum16)
-  const int x0 = 2 * lane, x1 = 2 * lane + 1;
-  // row 0 of the integral image is zero
-  for (int x = lane; x <= W; x += 64) out[x] = 0;
+  uint16_t* out = chan + fd.ch_off + (int64_t)c * fd.plane;  // integral mod 2^16 (see rect_mean16)
+  // lane l owns image columns 2l, 2l+1 and writes integral entries 2l, 2l+1 of each row as one
+  // aligned u32 (entry 2l = exclusive prefix, 2l+1 = + column 2l); rows are processed in
+  // batches of RB whose loads are all issued before the first scan.
+  const int x0 = 2 * lane;
+  for (int x = lane; x <= W; x += 64) out[x] = 0;  // row 0 of the integral image
+  constexpr int RB = 8;
   uint32_t c0 = 0, c1 = 0;
-  for (int y = 0; y < H; y++) {
-    c0 += (uint32_t)chan_value(c, g, m, W, H, y, x0, sf, hf);
-    c1 += (uint32_t)chan_value(c, g, m, W, H, y, x1, sf, hf);
-    uint32_t s = c0 + c1, incl = s;
+  for (int y0 = 0; y0 < H; y0 += RB) {
+    uint32_t v0[RB], v1[RB];
+    if (c >= 1 && c <= NGABOR) {
+      float2 mv[RB];
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      uint32_t o = (uint32_t)__shfl_up((int)incl, d);
-      if (lane >= d) incl += o;
+      for (int b = 0; b < RB; b++)
+        mv[b] = (y0 + b < H) ? *reinterpret_cast<const float2*>(&m[(y0 + b) * PITCH + x0]) : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int b = 0; b < RB; b++) {
+        // normalize: v*scale + shift (float, no FMA), convertTo(u8, 255): cvRound, saturate
+        v0[b] = (x0 < W) ? (uint32_t)sat_u8(cv_round((mv[b].x * sf + hf) * 255.f + 0.f)) : 0u;
+        v1[b] = (x0 + 1 < W) ? (uint32_t)sat_u8(cv_round((mv[b].y * sf + hf) * 255.f + 0.f)) : 0u;
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < RB; b++) {
+        const int y = min(y0 + b, H - 1);
+        v0[b] = (uint32_t)chan_value(c, g, m, W, H, y, x0, sf, hf);
+        v1[b] = (uint32_t)chan_value(c, g, m, W, H, y, x0 + 1, sf, hf);
+      }
     }
-    uint32_t excl = incl - s;
-    uint16_t* row = out + (int64_t)(y + 1) * PITCH;
-    if (lane == 0) row[0] = 0;
-    if (x0 + 1 <= W) row[x0 + 1] = (uint16_t)(excl + c0);
-    if (x1 + 1 <= W) row[x1 + 1] = (uint16_t)(excl + c0 + c1);
+#pragma unroll
+    for (int b = 0; b < RB; b++) {
+      if (y0 + b >= H) break;
+      c0 += v0[b];
+      c1 += v1[b];
+      const uint32_t s2 = c0 + c1;
+      uint32_t incl = s2;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+        if (lane >= d) incl += o;
+      }
+      const uint32_t excl = incl - s2;
+      uint32_t* row = reinterpret_cast<uint32_t*>(out + (int64_t)(y0 + b + 1) * PITCH);
+      // entries >= W+1 land in the row's pitch padding (never read by a patch)
+      row[lane] = (excl & 0xFFFFu) | ((excl + c0) << 16);
+    }
   }
 }
 
