@@ -384,7 +384,7 @@ __global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ f
 // estimate plus one integer correction step.
 __device__ __forceinline__ int idiv_small(int R, int area) {
   int q = (int)((float)R * __builtin_amdgcn_rcpf((float)area));
-  const int r = R - q * area;
+  const int r = R - (int)__umul24((unsigned)q, (unsigned)area);  // q, area < 2^24
   q += (r >= area) ? 1 : 0;
   q -= (r < 0) ? 1 : 0;
   return q;
@@ -393,15 +393,18 @@ __device__ __forceinline__ int idiv_small(int R, int area) {
 // I: integral (mod 2^16) at the rectangle's top-left corner; ld: row pitch (elements).
 template <class P>
 __device__ __forceinline__ int rect_mean16(P I, int ld, int w, int h) {
-  const int h1 = h >> 1;
-  const uint32_t a = I[0], b = I[w], c = I[h1 * ld], d = I[h1 * ld + w];
-  const uint32_t e = I[h * ld], f = I[h * ld + w];
+  // all offsets < 2^24: 24-bit multiplies (full rate) instead of v_mul_lo_u32
+  const int h1 = h >> 1, r1 = (int)__umul24((unsigned)h1, (unsigned)ld), r2 = (int)__umul24((unsigned)h, (unsigned)ld);
+  const uint32_t a = I[0], b = I[w], c = I[r1], d = I[r1 + w];
+  const uint32_t e = I[r2], f = I[r2 + w];
   const uint32_t top = (d - c - b + a) & 0xFFFFu, bot = (f - e - d + c) & 0xFFFFu;
-  return idiv_small((int)(top + bot), w * h);
+  return idiv_small((int)(top + bot), (int)__umul24((unsigned)w, (unsigned)h));
 }
 
 // Node fields (ffd_device.hpp): rect offsets are encoded for PITCH; re-derive for a pitch `ld`.
-__device__ __forceinline__ int node_off(uint32_t enc, int ld) { return (int)(enc >> 7) * ld + (int)(enc & 127u); }
+__device__ __forceinline__ int node_off(uint32_t enc, int ld) {
+  return (int)__umul24(enc >> 7, (unsigned)ld) + (int)(enc & 127u);
+}
 
 // Tree<S>::evaluateMT over global u16 planes (ffd_forest_eval_leaves hook).
 __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint32_t node,
@@ -500,8 +503,13 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   auto prefetch = [&](const Blk& B) {
     if (tid < NW || !B.ok) return;
     const FaceDesc& fd = A.faces[B.f];
+    // the resource must be wave-uniform (SGPRs): read it from the first lane explicitly
+    const uint64_t base = (uint64_t)(A.chan + fd.ch_off);
+    const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t bhi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane((int)(NCH * fd.plane * 2));
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(A.chan + fd.ch_off), (short)0, (int)(NCH * fd.plane * 2), BUF_WORD3);
+        (void*)(((uint64_t)bhi << 32) | blo), (short)0, nbytes, BUF_WORD3);
     const int base_b = (B.py0 * PITCH + (B.px0 & ~3)) * 2, plane_b = (int)fd.plane * 2;
     int s = tid - NW;
     asm volatile("" : "+v"(s));  // keep the per-chunk offsets out of loop-invariant hoisting (VGPRs)
@@ -558,7 +566,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     auto advance = [&](Walk& w) {
       const uint4 v = w.nd;
       const uint4 c0 = A.nodes[v.x], c1 = A.nodes[v.x + 1];
-      const uint16_t* I = win + (int)(v.y & 63u) * WW * LW + w.wbase;
+      const uint16_t* I = win + (int)__umul24(v.y & 63u, (unsigned)(WW * LW)) + w.wbase;
       const int p1 = rect_mean16(I + node_off(v.w & 0xFFFFu, LW), LW, (v.y >> 6) & 31u, (v.y >> 11) & 31u);
       const int p2 = rect_mean16(I + node_off(v.w >> 16, LW), LW, (v.y >> 16) & 31u, (v.y >> 21) & 31u);
       w.nd = (p1 - p2) <= (int)v.z ? c0 : c1;
