@@ -1,0 +1,61 @@
+"""The eval_ffd accuracy harness (face_alignment_cvpr_2012_amd/eval.py) pinned against the
+reference's own output/errors.txt and report constants (output/generate_report.m)."""
+import os
+
+import numpy as np
+import pytest
+
+from face_alignment_cvpr_2012_amd import eval as fe
+
+
+@pytest.mark.reference
+def test_report_reproduces_published_numbers(reference_root):
+    text = open(os.path.join(reference_root, "output", "errors.txt")).read()
+    e = fe.parse_errors(text)
+    assert e.shape == (1326, 10)
+    r = fe.report(e)
+    assert round(r["mean_error"], 4) == 0.0781 and round(r["median_error"], 4) == 0.0579
+    assert round(r["accuracy_pct"], 1) == 79.4
+    assert [round(v, 4) for v in r["per_landmark_mean"]] == [
+        0.0948, 0.0575, 0.0843, 0.0861, 0.1057, 0.0764, 0.0540, 0.0819, 0.0699, 0.0702]
+    assert [round(v, 1) for v in r["per_landmark_accuracy_pct"]] == [
+        78.4, 92.4, 71.9, 71.0, 63.8, 77.0, 92.9, 82.0, 81.2, 83.0]
+
+
+@pytest.mark.reference
+def test_errors_txt_format_round_trips(reference_root):
+    lines = open(os.path.join(reference_root, "output", "errors.txt")).read().splitlines(True)[:50]
+    e = fe.parse_errors("".join(lines))
+    assert fe.format_errors(np.float32(e)) == "".join(lines)
+
+
+def test_inter_ocular_distance_and_errors():
+    parts = np.array([[10, 20], [20, 20], [0, 0], [0, 0], [0, 0], [0, 0], [50, 20], [60, 20], [0, 0], [0, 0]])
+    assert fe.inter_ocular_distance(parts) == np.float32(40.0)
+    pred = parts.copy()
+    pred[3] += (3, 4)
+    err = fe.landmark_errors(parts, pred)
+    assert err[3] == np.float32(5.0 / 40.0) and (np.delete(err, 3) == 0).all()
+
+
+def test_oracle_fixture_errors_round_trip(oracle_mod, fixtures):
+    errs = []
+    for img, box, parts in zip(fixtures["images"], fixtures["boxes"], fixtures["parts"]):
+        f, _ = oracle_mod.analyze_face(img, tuple(int(v) for v in box), threads=8)
+        errs.append(fe.landmark_errors(parts, f["points"]))
+    text = fe.format_errors(errs)
+    back = fe.parse_errors(text)
+    assert back.shape == (20, 10) and np.allclose(back, np.array(errs), rtol=1e-5, atol=1e-6)
+    r = fe.report(errs)
+    assert 0.05 < r["mean_error"] < 0.11 and r["accuracy_pct"] > 65.0
+
+
+@pytest.mark.gpu
+def test_engine_eval_cli(tmp_path, capsys):
+    out = tmp_path / "errors.txt"
+    assert fe.main(["--out", str(out)]) == 0
+    e = fe.parse_errors(out.read_text())
+    assert e.shape == (20, 10)
+    r = fe.report(e)
+    assert 0.05 < r["mean_error"] < 0.11 and r["accuracy_pct"] > 65.0
+    assert "mean IOD error" in capsys.readouterr().out
