@@ -91,32 +91,83 @@ def stage_work(stage, n_faces, W=125, H=125, n_hp=576, n_mp=1024, trees=20):
     return n_faces * n_hp * 15 * 4 / 1e9, "GB/s", "hbm"
 
 
-def cpu_baseline(n_budget_s=12.0, max_faces=512):
+def cpu_baseline(wl, n_budget_s=12.0):
     """Oracle (C++ restatement) in reference-shaped mode: faces sequential, per-face thread pools
-    of `cores` threads for the 35 Gabor, 576 head-pose and 1,024 FFD tasks (ThreadPool.hpp:24-64)."""
+    of `cores` threads for the 35 Gabor, 576 head-pose and 1,024 FFD tasks (ThreadPool.hpp:24-64),
+    on a bounded sample (~n_budget_s seconds) of the benchmarked workload's own faces."""
     import oracle
-    from face_alignment_cvpr_2012_amd.synthetic import make_crops
     oracle.load_model(os.path.join(REPO, "model", "ffd_model.bin"))
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
     cores = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)), 16))
-    crops, _ = make_crops(max_faces, seed=4242)
+    face = lambda k: wl.face(k % wl.n)  # noqa: E731
     t0 = time.perf_counter()
-    oracle.analyze_face(crops[0], (0, 0, CROP, CROP), threads=cores)
+    oracle.analyze_face(*face(0), threads=cores)
     one = time.perf_counter() - t0
-    n = int(max(3, min(max_faces - 1, n_budget_s / max(one, 1e-3))))
+    n = int(max(3, min(4 * wl.n, n_budget_s / max(one, 1e-3))))
     t0 = time.perf_counter()
     for k in range(1, n + 1):
-        oracle.analyze_face(crops[k], (0, 0, CROP, CROP), threads=cores)
+        oracle.analyze_face(*face(k), threads=cores)
     dt = time.perf_counter() - t0
+    cpu = ""
+    try:
+        cpu = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     return {"value": round(n / dt, 3), "unit": "faces/s", "cores": cores, "kind": "port",
-            "sample": f"{n} C2 150x150 crops (seed 4242), analyzeFace each, reference-shaped per-face "
-                      f"thread pools, {dt:.1f} s"}
+            "sample": f"first {n} faces of the {wl.name} workload, analyzeFace each, reference-shaped per-face "
+                      f"thread pools of {cores} threads, {dt:.1f} s; host {cpu}, nproc {os.cpu_count()}"}
 
 
-def parity_spot_check(ff, crops, d_out, k=4):
+class Workload:
+    """One GPU's share of a BASELINE.json config: host images, boxes, box -> image map."""
+
+    def __init__(self, name, images, boxes, box_img, scaling, describe, total_faces, n_images=None):
+        self.name, self.images, self.boxes, self.box_img = name, images, boxes, box_img
+        self.scaling, self.describe, self.total_faces = scaling, describe, total_faces
+        # images beyond the distinct ones repeat them cyclically (generation time; same work per image)
+        self.n_images = n_images or len(images)
+
+    @property
+    def n(self):
+        return len(self.boxes)
+
+    def face(self, k):
+        return self.images[self.box_img[k] % len(self.images)], self.boxes[k]
+
+
+def make_workload(name, rank, world, faces, frames):
+    from face_alignment_cvpr_2012_amd.distributed import shard_bounds
+    from face_alignment_cvpr_2012_amd.synthetic import make_crops, make_frames
+    if name == "c2":  # BASELINE configs[1]: 4096 crops per GPU (weak scaling)
+        crops, _ = make_crops(faces, seed=2012 + rank)
+        return Workload("c2", crops, [(0, 0, CROP, CROP)] * faces, np.arange(faces, dtype=np.int32), "weak",
+                        f"C2: batch of {faces} pre-cropped 150x150 faces per GPU, pretrained config_ffd.txt forest "
+                        "(20 trees/face of 5x20, depth<=20), head-pose forest 15 trees, 125x125 faces",
+                        faces * world)
+    if name == "c3":  # configs[2]: 512 1080p frames dealt over the GPUs, 8 detectFace-enlarged boxes each
+        lo, hi = shard_bounds(frames, world, rank)
+        uniq = min(hi - lo, 64)
+        fr, bx, _ = make_frames(uniq, seed=1080 + lo)
+        boxes = [tuple(int(v) for v in bx[k % uniq, j]) for k in range(hi - lo) for j in range(bx.shape[1])]
+        box_img = np.repeat(np.arange(hi - lo), bx.shape[1]).astype(np.int32)
+        return Workload("c3", fr, boxes, box_img, "strong", n_images=hi - lo, describe=
+                        f"C3: {frames} synthetic 1920x1080 frames sharded over the GPUs (64 distinct per GPU, "
+                        "repeated), 8 faces each (paste boxes through the detectFace enlargement: 125 x ~148 faces), "
+                        "pretrained forests", total_faces=frames * 8)
+    if name == "c5":  # configs[4]: 64 faces/frame x 512 frames = 32768 crops over all GPUs (strong scaling)
+        total = 64 * 512
+        lo, hi = shard_bounds(total, world, rank)
+        crops, _ = make_crops(hi - lo, seed=5000 + rank)
+        return Workload("c5", crops, [(0, 0, CROP, CROP)] * (hi - lo), np.arange(hi - lo, dtype=np.int32), "strong",
+                        "C5: 64 faces/frame x 512 frames = 32768 C2-style crops sharded over the GPUs, all 5 "
+                        "pose-conditional FFD forests resident", total)
+    raise ValueError(name)
+
+
+def parity_spot_check(ff, wl, d_out, k=4):
     """Decode the first k output records and compare them with the oracle (outside the timed region)."""
     import torch
 
@@ -126,8 +177,8 @@ def parity_spot_check(ff, crops, d_out, k=4):
     rec = d_out[: k * ffd.FACE_RECORD_BYTES].cpu().numpy().tobytes()
     faces = ffd.faces_from_records(rec)
     ok = True
-    for i in range(k):
-        ref, _ = oracle.analyze_face(crops[i], (0, 0, CROP, CROP), threads=8)
+    for i in range(min(k, wl.n)):
+        ref, _ = oracle.analyze_face(*wl.face(i), threads=8)
         ok &= bool(np.array_equal(faces[i].ffd_cordinates, ref["points"]))
         ok &= np.float32(faces[i].headpose) == np.float32(ref["headpose"])
     del torch
@@ -139,7 +190,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--faces", type=int, default=4096, help="faces per GPU per step")
+    ap.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2",
+                    help="BASELINE.json config: c2 (default, the metric's), c3 1080p frames, c5 crowd")
+    ap.add_argument("--faces", type=int, default=4096, help="c2: faces per GPU per step")
+    ap.add_argument("--frames", type=int, default=512, help="c3: frames per step (whole job)")
     ap.add_argument("--chunk", type=int, default=0, help="faces per pipeline launch (0 = whole batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
@@ -150,7 +204,6 @@ def main():
 
     import face_alignment_cvpr_2012_amd as ffd
     from face_alignment_cvpr_2012_amd.distributed import gather_records
-    from face_alignment_cvpr_2012_amd.synthetic import make_crops
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -160,29 +213,33 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    n = args.faces
-    crops, _ = make_crops(n, seed=2012 + rank)
-    d_crops = torch.from_numpy(crops).to(dev)
+    wl = make_workload(args.workload, rank, world, args.faces, args.frames)
+    n = wl.n
+    n_img, ih, iw = wl.n_images, wl.images.shape[1], wl.images.shape[2]
+    d_images = torch.from_numpy(np.ascontiguousarray(wl.images)).to(dev)
+    if n_img > len(wl.images):
+        reps = -(-n_img // len(wl.images))
+        d_images = d_images.repeat(reps, 1, 1, 1)[:n_img].contiguous()
     rec = ffd.FACE_RECORD_BYTES
-    d_out = torch.zeros(n * rec, dtype=torch.uint8, device=dev)
+    d_out = torch.zeros(max(1, n) * rec, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
 
     chunk = args.chunk if 0 < args.chunk < n else 0  # 0: engine default (FFD_CHUNK)
     ff = ffd.FaceForest(ffd.FaceForestOptions(device=local, max_chunk_faces=chunk))
-    boxes = [(0, 0, CROP, CROP)] * n
-    box_img = np.arange(n, dtype=np.int32)
+    geo = [ff.geometry(b[2], b[3]) for b in wl.boxes[:256]]
+    mean_wh = (float(np.mean([g[0] for g in geo])), float(np.mean([g[1] for g in geo])))
 
     def step():
-        ff.analyze_device(d_crops.data_ptr(), CROP * CROP * 3, CROP, CROP, CROP * 3, n, boxes, box_img,
+        ff.analyze_device(d_images.data_ptr(), iw * ih * 3, iw, ih, iw * 3, n_img, wl.boxes, wl.box_img,
                           d_out.data_ptr())
         ff.synchronize()
         if world > 1:  # one RCCL gather of the ffd_face records to rank 0 (faces sharded, no other exchange)
-            gather_records(d_out, world * n, dst=0)
+            gather_records(d_out[: n * rec], wl.total_faces, dst=0)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    ok = parity_spot_check(ff, crops, d_out) if rank == 0 else True
+    ok = parity_spot_check(ff, wl, d_out) if rank == 0 else True
 
     ff.set_profiling(True)
     if world > 1:
@@ -202,19 +259,24 @@ def main():
         elapsed = float(t.item())
 
     if rank == 0:
-        total_faces = world * n * args.steps
+        total_faces = wl.total_faces * args.steps
         value = total_faces / elapsed
         dom = max((k for k in stages if stages[k][1] > 0), key=lambda k: stages[k][0])
         ms_total, launches = stages[dom]
         avg_ms = ms_total / launches
         faces_per_launch = n * args.steps / launches  # one launch covers one chunk of faces
-        amount, unit, bound = stage_work(dom, faces_per_launch)
+        W, H = mean_wh
+        n_hp = float(np.mean([g[2] for g in geo])) if geo else 0.0
+        n_mp = float(np.mean([g[3] for g in geo])) if geo else 0.0
+        amount, unit, bound = stage_work(dom, faces_per_launch, W=W, H=H, n_hp=n_hp, n_mp=n_mp)
         achieved = amount / (avg_ms / 1e3)
-        traffic = measured_traffic(dom, faces_per_launch)  # HBM bytes per launch (PMC), or None
+        traffic = measured_traffic(dom, faces_per_launch) if wl.name == "c2" else None  # PMC bytes/launch
         if traffic is not None:
             traffic = int(traffic)
         peak = FP32_PEAK_TFLOPS if unit == "TFLOP/s" else HBM_PEAK_GBS
-        b_face = CROP * CROP * 3 + 2 * 38 * 126 * 126 * 4 + 100
+        # B_face = S_in + 2*38*(W+1)*(H+1)*4 + S_out (C2: 4,893,904 B)
+        s_in = iw * ih * 3 * n_img / max(1, n)
+        b_face = int(round(s_in + 2 * 38 * (W + 1) * (H + 1) * 4 + 100))
         out = {
             "metric": "faces/sec (whole node) on pretrained FFD forest; mean landmark px error",
             "value": round(value, 1),
@@ -224,14 +286,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": wl.scaling,
             "vs_baseline": None,
             "dtype": "u8/u16/i32/f32",
-            "data": "synthetic: 4096 C2 150x150 crops per GPU from the 20 bundled LFW faces (seed 2012+rank); "
+            "data": "synthetic (face_alignment_cvpr_2012_amd/synthetic.py) from the 20 bundled LFW faces; "
                     "pretrained reference forests converted to model/ffd_model.bin",
-            "config": {"workload": "C2: batch of 4096 pre-cropped 150x150 faces per GPU, pretrained "
-                                   "config_ffd.txt forest (20 trees/face of 5x20, depth<=20), head-pose forest 15 "
-                                   "trees, 125x125 faces", "faces_per_gpu": n, "parallelism": f"faces sharded x{world}"},
+            "config": {"workload": wl.describe, "faces_per_gpu": n, "mean_face": [round(W, 1), round(H, 1)],
+                       "parallelism": f"faces sharded x{world}"},
             "landmark_px_error_vs_cpu": 0.0 if ok else None,
             "parity_spot_check": bool(ok),
             "roofline": {"bound": bound, "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
@@ -244,7 +305,7 @@ def main():
             "stage_ms_per_step": {k: round(v[0] / max(1, args.steps), 3) for k, v in stages.items()},
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+            out["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget)
         print(json.dumps(out), flush=True)
     ff.close()
     if world > 1:

@@ -4,6 +4,14 @@ C2: crop k = bundled fixture face (k mod 20), annotated bbox jittered by dx, dy 
 scale ~ U[0.95, 1.05], resampled (bilinear, edge-clamped) to 150x150, plus N(0, 2^2) pixel
 noise clipped to [0, 255]; seed 2012.  analyzeFace(crop, Rect(0, 0, 150, 150)) then scales the
 crop to a 125x125 face (576 head-pose + 1,024 FFD patches).
+
+C3: 1920x1080 frames; background = seeded smooth noise (bilinear upsampling of a coarse random
+grid); 8 fixture faces per frame pasted at random non-overlapping positions with face-box sides
+U{100..200} px.  The analysis boxes are the paste boxes put through the reference's detectFace
+enlargement (face_box_from_detection, src/FaceForest.cpp:148-158), so the scaled faces are
+125 x ~148 like Haar boxes.
+
+C5: C2-style crops, 64 per frame x 512 frames = 32,768 faces.
 """
 import os
 
@@ -55,3 +63,78 @@ def make_crops(n, size=150, seed=2012, fixtures=None):
         v += rng.normal(0.0, 2.0, size=v.shape).astype(np.float32)
         out[k] = np.clip(np.rint(v), 0, 255).astype(np.uint8)
     return out, src
+
+
+def _interp_matrix(n, m, cell=64.0):
+    """(n, m) matrix of linear interpolation weights: output i samples coarse coordinate
+    (i + 0.5) / cell (edge clamped), as _bilinear does along one axis."""
+    t = (np.arange(n) + 0.5) / cell
+    i0 = np.clip(np.floor(t).astype(np.int64), 0, m - 1)
+    i1 = np.clip(i0 + 1, 0, m - 1)
+    f = np.clip(t - np.floor(t), 0, 1).astype(np.float32)
+    M = np.zeros((n, m), np.float32)
+    M[np.arange(n), i0] += 1 - f
+    M[np.arange(n), i1] += f
+    return M
+
+
+def face_box_from_detection(det, img_w, img_h):
+    """detectFace's widening of a (Haar) detection, src/FaceForest.cpp:148-158: 5 % of the width
+    on each side, height + 2 x 15 % of the width (below the box), clipped to the image by
+    intersect (src/face_utils.cpp:325-346)."""
+    x, y, w, h = (int(v) for v in det)
+    ox, oy = int(w * 0.05), int(w * 0.15)
+    r = (x - ox, y, w + 2 * ox, h + 2 * oy)
+    ix, iy = max(r[0], 0), max(r[1], 0)
+    iw = min(r[0] + r[2], img_w) - ix
+    ih = min(r[1] + r[3], img_h) - iy
+    if iw <= 0 or ih <= 0:
+        return (0, 0, 0, 0)
+    return (ix, iy, iw, ih)
+
+
+def make_frames(n_frames, faces_per_frame=8, width=1920, height=1080, seed=1080, fixtures=None):
+    """Return (frames uint8 [n, height, width, 3] BGR, boxes int32 [n, faces_per_frame, 4] analysis
+    boxes (detectFace-enlarged), paste boxes int32 [n, faces_per_frame, 4])."""
+    fx = fixtures or load_fixtures()
+    imgs, fboxes = fx["images"], fx["boxes"]
+    rng = np.random.default_rng(seed)
+    frames = np.empty((n_frames, height, width, 3), np.uint8)
+    boxes = np.zeros((n_frames, faces_per_frame, 4), np.int32)
+    paste = np.zeros((n_frames, faces_per_frame, 4), np.int32)
+    gy, gx = (height + 63) // 64 + 1, (width + 63) // 64 + 1
+    for f in range(n_frames):
+        coarse = rng.uniform(40, 200, size=(gy, gx, 3)).astype(np.float32)
+        # bilinear upsampling of the coarse grid as two interpolation matrices (separable)
+        my, mx = _interp_matrix(height, gy), _interp_matrix(width, gx)
+        bg = np.stack([my @ coarse[:, :, c] @ mx.T for c in range(3)], axis=-1)
+        frame = np.clip(np.rint(bg), 0, 255).astype(np.uint8)
+        taken = []
+        for k in range(faces_per_frame):
+            i = int(rng.integers(0, len(imgs)))
+            side = int(rng.integers(100, 201))
+            region = int(round(side * 1.6))  # pasted square around the face box
+            for _ in range(1000):
+                px = int(rng.integers(0, width - region))
+                py = int(rng.integers(0, height - region))
+                if all(px + region <= a or a + b <= px or py + region <= c or c + d <= py for a, c, b, d in taken):
+                    break
+            else:
+                raise RuntimeError("could not place a face")
+            taken.append((px, py, region, region))
+            x, y, w, h = (float(v) for v in fboxes[i])
+            scale = side / w
+            cx, cy = x + w / 2.0, y + h / 2.0
+            t = (np.arange(region) + 0.5) / scale
+            src_x = cx - region / (2 * scale) + t - 0.5
+            src_y = cy - region / (2 * scale) + t - 0.5
+            patch = _bilinear(imgs[i], src_x, src_y)
+            frame[py:py + region, px:px + region] = np.clip(np.rint(patch), 0, 255).astype(np.uint8)
+            # face box inside the paste: the fixture box scaled; detection = that box
+            bx = px + int(round(region / 2.0 - side / 2.0))
+            by = py + int(round(region / 2.0 - h * scale / 2.0))
+            det = (bx, by, side, int(round(h * scale)))
+            paste[f, k] = det
+            boxes[f, k] = face_box_from_detection(det, width, height)
+        frames[f] = frame
+    return frames, boxes, paste
