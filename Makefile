@@ -13,6 +13,7 @@ CXXFLAGS  := -O2 -std=c++17 -fPIC -ffp-contract=off -Wall -Iinclude
 
 LIB       := $(PKG)/lib/libffd.so
 CONVERT   := $(PKG)/bin/ffd_convert
+SYNTH     := $(PKG)/bin/ffd_synth_forest
 ORACLE    := oracle/build/libffd_oracle.so
 MODEL     := model/ffd_model.bin
 EXAMPLE   := examples/build/analyze_face
@@ -21,7 +22,7 @@ HIP_OBJS  := $(PKG)/lib/ffd_kernels.o $(PKG)/lib/ffd_engine.o
 HDRS      := include/ffd.h include/ffd_numerics.h include/ffd_model_format.h $(CSRC)/ffd_device.hpp \
              $(CSRC)/ffd_kernels.hpp $(CSRC)/model_io.hpp
 
-all: $(LIB) $(CONVERT) $(ORACLE) $(EXAMPLE)
+all: $(LIB) $(CONVERT) $(SYNTH) $(ORACLE) $(EXAMPLE)
 
 $(PKG)/lib/ffd_kernels.o: $(CSRC)/ffd_kernels.hip $(HDRS)
 	@mkdir -p $(@D)
@@ -33,6 +34,10 @@ $(PKG)/lib/ffd_engine.o: $(CSRC)/ffd_engine.cpp $(HDRS)
 
 $(LIB): $(HIP_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS)
+
+$(SYNTH): $(CSRC)/ffd_synth_forest.cpp $(CSRC)/model_io.hpp include/ffd_model_format.h
+	@mkdir -p $(@D)
+	$(CXX) $(CXXFLAGS) -o $@ $<
 
 $(CONVERT): $(CSRC)/ffd_convert.cpp $(CSRC)/model_io.hpp include/ffd_model_format.h
 	@mkdir -p $(@D)

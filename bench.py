@@ -96,7 +96,8 @@ def cpu_baseline(wl, n_budget_s=12.0):
     of `cores` threads for the 35 Gabor, 576 head-pose and 1,024 FFD tasks (ThreadPool.hpp:24-64),
     on a bounded sample (~n_budget_s seconds) of the benchmarked workload's own faces."""
     import oracle
-    oracle.load_model(os.path.join(REPO, "model", "ffd_model.bin"))
+    oracle.load_model(wl.model)
+    oracle.set_steps(4, *wl.mp_steps)
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
@@ -124,9 +125,12 @@ def cpu_baseline(wl, n_budget_s=12.0):
 class Workload:
     """One GPU's share of a BASELINE.json config: host images, boxes, box -> image map."""
 
-    def __init__(self, name, images, boxes, box_img, scaling, describe, total_faces, n_images=None):
+    def __init__(self, name, images, boxes, box_img, scaling, describe, total_faces, n_images=None,
+                 model=None, mp_steps=(3, 3)):
         self.name, self.images, self.boxes, self.box_img = name, images, boxes, box_img
         self.scaling, self.describe, self.total_faces = scaling, describe, total_faces
+        self.model = model or os.path.join(REPO, "model", "ffd_model.bin")
+        self.mp_steps = mp_steps  # FFD patch-grid step (x, y)
         # images beyond the distinct ones repeat them cyclically (generation time; same work per image)
         self.n_images = n_images or len(images)
 
@@ -164,7 +168,28 @@ def make_workload(name, rank, world, faces, frames):
         return Workload("c5", crops, [(0, 0, CROP, CROP)] * (hi - lo), np.arange(hi - lo, dtype=np.int32), "strong",
                         "C5: 64 faces/frame x 512 frames = 32768 C2-style crops sharded over the GPUs, all 5 "
                         "pose-conditional FFD forests resident", total)
+    if name == "c4":  # configs[3]: synthetic 20 complete depth-20 trees, 4x patch density, 1 GPU
+        path = synth_forest_path(20)
+        crops, _ = make_crops(faces, seed=4000 + rank)
+        return Workload("c4", crops, [(0, 0, CROP, CROP)] * faces, np.arange(faces, dtype=np.int32), "weak",
+                        f"C4: {faces} C2-style crops per GPU on a synthetic forest of 20 complete depth-20 trees "
+                        "(one forest for all pose bins), FFD grid step (2, 1): 4,418 patches x 20 walks per face",
+                        faces * world, model=path, mp_steps=(2, 1))
     raise ValueError(name)
+
+
+def synth_forest_path(depth):
+    """C4's synthetic forest (face_alignment_cvpr_2012_amd/bin/ffd_synth_forest), generated once
+    per box outside the repository (~3.7 GB at depth 20)."""
+    import subprocess
+    import tempfile
+    path = os.path.join(tempfile.gettempdir(), f"ffd_c4_d{depth}.bin")
+    if not os.path.exists(path):
+        exe = os.path.join(REPO, "face_alignment_cvpr_2012_amd", "bin", "ffd_synth_forest")
+        subprocess.run([exe, os.path.join(REPO, "model", "ffd_model.bin"), path + ".tmp", str(depth), "20", "4"],
+                       check=True, stdout=subprocess.DEVNULL)
+        os.replace(path + ".tmp", path)
+    return path
 
 
 def parity_spot_check(ff, wl, d_out, k=4):
@@ -173,7 +198,8 @@ def parity_spot_check(ff, wl, d_out, k=4):
 
     import face_alignment_cvpr_2012_amd as ffd
     import oracle
-    oracle.load_model(os.path.join(REPO, "model", "ffd_model.bin"))
+    oracle.load_model(wl.model)
+    oracle.set_steps(4, *wl.mp_steps)
     rec = d_out[: k * ffd.FACE_RECORD_BYTES].cpu().numpy().tobytes()
     faces = ffd.faces_from_records(rec)
     ok = True
@@ -190,9 +216,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2",
-                    help="BASELINE.json config: c2 (default, the metric's), c3 1080p frames, c5 crowd")
-    ap.add_argument("--faces", type=int, default=4096, help="c2: faces per GPU per step")
+    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c2",
+                    help="BASELINE.json config: c2 (default, the metric's), c3 1080p frames, c4 deep synthetic "
+                         "forest, c5 crowd")
+    ap.add_argument("--faces", type=int, default=None, help="c2/c4: faces per GPU per step (4096 / 1024)")
     ap.add_argument("--frames", type=int, default=512, help="c3: frames per step (whole job)")
     ap.add_argument("--chunk", type=int, default=0, help="faces per pipeline launch (0 = whole batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -213,7 +240,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    wl = make_workload(args.workload, rank, world, args.faces, args.frames)
+    faces = args.faces or (1024 if args.workload == "c4" else 4096)
+    wl = make_workload(args.workload, rank, world, faces, args.frames)
     n = wl.n
     n_img, ih, iw = wl.n_images, wl.images.shape[1], wl.images.shape[2]
     d_images = torch.from_numpy(np.ascontiguousarray(wl.images)).to(dev)
@@ -225,7 +253,8 @@ def main():
     torch.cuda.synchronize()
 
     chunk = args.chunk if 0 < args.chunk < n else 0  # 0: engine default (FFD_CHUNK)
-    ff = ffd.FaceForest(ffd.FaceForestOptions(device=local, max_chunk_faces=chunk))
+    mp = ffd.MultiPartEstimatorOption(step_size=wl.mp_steps[0], step_size_y=wl.mp_steps[1])
+    ff = ffd.FaceForest(ffd.FaceForestOptions(model_path=wl.model, device=local, max_chunk_faces=chunk, mp_option=mp))
     geo = [ff.geometry(b[2], b[3]) for b in wl.boxes[:256]]
     mean_wh = (float(np.mean([g[0] for g in geo])), float(np.mean([g[1] for g in geo])))
 
@@ -277,6 +306,8 @@ def main():
         # B_face = S_in + 2*38*(W+1)*(H+1)*4 + S_out (C2: 4,893,904 B)
         s_in = iw * ih * 3 * n_img / max(1, n)
         b_face = int(round(s_in + 2 * 38 * (W + 1) * (H + 1) * 4 + 100))
+        if wl.name == "c4":  # + forest gather P*T*(16 B * depth + 48 B)
+            b_face += int(round(n_mp * 20 * (16 * 20 + 48)))
         out = {
             "metric": "faces/sec (whole node) on pretrained FFD forest; mean landmark px error",
             "value": round(value, 1),

@@ -71,7 +71,8 @@ class _HpOpt(ctypes.Structure):
 
 class _MpOpt(ctypes.Structure):
     _fields_ = [("num_parts", ctypes.c_int32), ("step_size", ctypes.c_int32), ("min_samples", ctypes.c_int32),
-                ("min_forground", ctypes.c_float), ("min_pf", ctypes.c_float), ("max_variance", ctypes.c_float)]
+                ("min_forground", ctypes.c_float), ("min_pf", ctypes.c_float), ("max_variance", ctypes.c_float),
+                ("step_size_y", ctypes.c_int32)]
 
 
 class _MsOpt(ctypes.Structure):
@@ -160,6 +161,7 @@ class MultiPartEstimatorOption:         # include/FaceForest.hpp:45-58
     min_forground: float = 0.5
     min_pf: float = 0.25
     max_variance: float = 25.0
+    step_size_y: int = 0                # 0: step_size on both axes (the reference); C4 uses (2, 1)
 
 
 @dataclass
@@ -224,7 +226,8 @@ class FaceForest:
         d.hp_option = _HpOpt(o.hp_option.num_head_pose_labels, o.hp_option.step_size,
                              o.hp_option.min_foreground_probability)
         d.mp_option = _MpOpt(o.mp_option.num_parts, o.mp_option.step_size, o.mp_option.min_samples,
-                             o.mp_option.min_forground, o.mp_option.min_pf, o.mp_option.max_variance)
+                             o.mp_option.min_forground, o.mp_option.min_pf, o.mp_option.max_variance,
+                             o.mp_option.step_size_y)
         d.ms_option = _MsOpt(o.ms_option.kernel_size, o.ms_option.max_iterations, o.ms_option.stopping_criteria)
         h = ctypes.c_void_p()
         st = L.ffd_engine_create(ctypes.byref(d), ctypes.byref(h))

@@ -206,24 +206,26 @@ struct ffd_engine {
     g.nhx = cnt(g.W, desc.hp_option.step_size);
     g.nhy = cnt(g.H, desc.hp_option.step_size);
     g.nmx = cnt(g.W, desc.mp_option.step_size);
-    g.nmy = cnt(g.H, desc.mp_option.step_size);
+    g.nmy = cnt(g.H, mp_step_y());
     return g;
   }
 
   void load_model(const std::string& path);
   void build_gabor();
+  // FFD patch-grid step along y: the reference has one step for both axes (step_size_y == 0)
+  int mp_step_y() const { return desc.mp_option.step_size_y > 0 ? desc.mp_option.step_size_y : desc.mp_option.step_size; }
   // Fit the traversal window into the CU's 160 KB of LDS (and the staging registers), shrinking
   // the patch block if needed, and raise the kernels' dynamic-LDS limit.
   void check_traverse_lds() {
     const int cap = 160 * 1024;
-    auto fit = [&](int& G, int step) {
-      while (!traverse_window_fits(G, step, cap)) {
+    auto fit = [&](int& G, int step, int step_y) {
+      while (!traverse_window_fits(G, step, step_y, cap)) {
         if (G <= 3) throw std::runtime_error("traversal window does not fit in LDS (step size too large)");
         G--;
       }
     };
-    fit(trav_g_hp, desc.hp_option.step_size);
-    fit(trav_g_mp, desc.mp_option.step_size);
+    fit(trav_g_hp, desc.hp_option.step_size, desc.hp_option.step_size);
+    fit(trav_g_mp, desc.mp_option.step_size, mp_step_y());
     HIP_CHECK(set_traverse_lds_limit(cap));
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, device));
@@ -497,7 +499,8 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   });
   stage(7, st, [&] {
     launch_traverse(true, dfd, n, blocks_per_face(fds, true, trav_g_hp), trav_g_hp, hp_nodes.as<uint4>(),
-                    hp_roots.as<int32_t>(), nullptr, hp_trees, desc.hp_option.step_size, w.chan.as<uint16_t>(),
+                    hp_roots.as<int32_t>(), nullptr, hp_trees, desc.hp_option.step_size, desc.hp_option.step_size,
+                    w.chan.as<uint16_t>(),
                     w.hpleaf.as<int32_t>(), trav_wg, st);
   });
   stage(8, st, [&] {
@@ -506,13 +509,13 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   });
   stage(9, st, [&] {
     launch_traverse(false, dfd, n, blocks_per_face(fds, false, trav_g_mp), trav_g_mp, mp_nodes.as<uint4>(),
-                    mp_roots.as<int32_t>(), w.state.as<HpState>(), 0, desc.mp_option.step_size,
+                    mp_roots.as<int32_t>(), w.state.as<HpState>(), 0, desc.mp_option.step_size, mp_step_y(),
                     w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), trav_wg, st);
   });
   const int n_parts = std::min(desc.mp_option.num_parts, NPARTS);
   stage(10, st, [&] {
     launch_votes(dfd, n, w.mpleaf.as<int32_t>(), mp_rec.as<uint4>(), w.state.as<HpState>(), MAX_TREES,
-                 desc.mp_option.step_size, patch / 2, n_parts, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), st);
+                 desc.mp_option.step_size, mp_step_y(), patch / 2, n_parts, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), st);
   });
   stage(11, st, [&] {
     launch_meanshift(dfd, n, w.state.as<HpState>(), MAX_TREES, n_parts, (float)desc.ms_option.kernel_size,
@@ -617,6 +620,7 @@ void ffd_engine_desc_init(ffd_engine_desc* d) {
   d->mp_option.min_forground = 0.5f;
   d->mp_option.min_pf = 0.25f;
   d->mp_option.max_variance = 25.f;
+  d->mp_option.step_size_y = 0;
   d->ms_option.kernel_size = 10;
   d->ms_option.max_iterations = 7;
   d->ms_option.stopping_criteria = 0.05f;
@@ -626,7 +630,8 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   if (!out) return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "out is NULL");
   *out = nullptr;
   if (!d || !d->model_path) return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "desc/model_path is NULL");
-  if (d->hp_option.step_size <= 0 || d->mp_option.step_size <= 0 || d->ms_option.kernel_size == 0)
+  if (d->hp_option.step_size <= 0 || d->mp_option.step_size <= 0 || d->mp_option.step_size_y < 0 ||
+      d->ms_option.kernel_size == 0)
     return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "invalid estimator options");
   std::unique_ptr<ffd_engine> e(new ffd_engine());
   e->desc = *d;

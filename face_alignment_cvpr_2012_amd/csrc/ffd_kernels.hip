@@ -453,7 +453,7 @@ struct TravArgs {
   const int32_t* roots;
   const HpState* hp_state; // FFD pass: selected trees; nullptr for the head-pose pass
   int ntrees_hp;           // head-pose pass: number of trees
-  int step;
+  int step, step_y;        // patch grid steps (x, y)
   const uint16_t* chan;
   int32_t* leaf_out;
 };
@@ -464,8 +464,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   uint16_t* win = reinterpret_cast<uint16_t*>(smem);
   constexpr int NW = TRAV_NW, NS = TRAV_NS, U = TRAV_U, GG = G * G;
   const int tid = threadIdx.x;
-  const int step = A.step, WW = 32 + step * (G - 1), LW = trav_row_pitch(WW), nq = LW >> 2;
-  const int total = NCH * WW * nq;  // 8-byte chunks per window (host guarantees <= NS * U)
+  // window: WW integral columns x WH rows (steps may differ per axis: step_y, C4's (2, 1) grid)
+  const int step = A.step, stepy = A.step_y, WW = 32 + step * (G - 1), WH = 32 + stepy * (G - 1);
+  const int LW = trav_row_pitch(WW), nq = LW >> 2;
+  const int total = NCH * WH * nq;  // 8-byte chunks per window (host guarantees <= NS * U)
   // XCD-contiguous, face-major block range of this workgroup's XCD; workgroups of one XCD stride it
   const int N = A.n_faces * A.bpf, xcd = blockIdx.x & 7, k = blockIdx.x >> 3, nk = gridDim.x >> 3;
   const int q8 = N >> 3, r8 = N & 7;
@@ -487,7 +489,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     B.xi0 = (b % gbx) * G;
     B.yi0 = (b / gbx) * G;
     B.px0 = B.xi0 * step;
-    B.py0 = B.yi0 * step;
+    B.py0 = B.yi0 * stepy;
     B.T = 0;
     if (fd.valid && b < gbx * gby) {
       B.ok = true;
@@ -513,8 +515,8 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     const int base_b = (B.py0 * PITCH + (B.px0 & ~3)) * 2, plane_b = (int)fd.plane * 2;
     int s = tid - NW;
     asm volatile("" : "+v"(s));  // keep the per-chunk offsets out of loop-invariant hoisting (VGPRs)
-    const int dq = NS % nq, dr = (NS / nq) % WW, dc = NS / (nq * WW);
-    int q = s % nq, r = (s / nq) % WW, c = s / (nq * WW);
+    const int dq = NS % nq, dr = (NS / nq) % WH, dc = NS / (nq * WH);
+    int q = s % nq, r = (s / nq) % WH, c = s / (nq * WH);
 #pragma unroll
     for (int u = 0; u < U; u++) {
       st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, base_b + c * plane_b + r * (PITCH * 2) + q * 8, 0, 0);
@@ -522,8 +524,8 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       int cr = q >= nq;
       q -= cr ? nq : 0;
       r += dr + cr;
-      cr = r >= WW;
-      r -= cr ? WW : 0;
+      cr = r >= WH;
+      r -= cr ? WH : 0;
       c += dc + cr;
     }
   };
@@ -556,7 +558,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       const int xi = B.xi0 + pl % G, yi = B.yi0 + pl / G;
       if (xi >= B.nx || yi >= B.ny) return;
       const int tree = HP ? t : A.hp_state[B.f].trees[t];
-      w.wbase = (yi - B.yi0) * step * LW + (xi - B.xi0) * step + sh;
+      w.wbase = (yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh;
       w.oidx = t * n + yi * B.nx + xi;
       w.nd = A.nodes[A.roots[tree]];
       w.done = false;
@@ -566,7 +568,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     auto advance = [&](Walk& w) {
       const uint4 v = w.nd;
       const uint4 c0 = A.nodes[v.x], c1 = A.nodes[v.x + 1];
-      const uint16_t* I = win + (int)__umul24(v.y & 63u, (unsigned)(WW * LW)) + w.wbase;
+      const uint16_t* I = win + (int)__umul24(v.y & 63u, (unsigned)(WH * LW)) + w.wbase;
       const int p1 = rect_mean16(I + node_off(v.w & 0xFFFFu, LW), LW, (v.y >> 6) & 31u, (v.y >> 11) & 31u);
       const int p2 = rect_mean16(I + node_off(v.w >> 16, LW), LW, (v.y >> 16) & 31u, (v.y >> 21) & 31u);
       w.nd = (p1 - p2) <= (int)v.z ? c0 : c1;
@@ -727,7 +729,7 @@ __global__ __launch_bounds__(256) void k_hp_pose(const FaceDesc* __restrict__ fa
 __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ faces, int n_faces,
                                                const int32_t* __restrict__ mp_leaf,
                                                const uint4* __restrict__ leaf_rec, const HpState* __restrict__ state,
-                                               int tslots, int step, int half_patch, int n_parts,
+                                               int tslots, int step, int step_y, int half_patch, int n_parts,
                                                Vote* __restrict__ votes, int32_t* __restrict__ vote_counts) {
   const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -758,7 +760,7 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
         const int xi = pr / ny, yi = pr - xi * ny;
         leaf[u] = L[(int64_t)t * n + yi * nx + xi];
         vx0[u] = xi * step + half_patch;
-        vy0[u] = yi * step + half_patch;
+        vy0[u] = yi * step_y + half_patch;
       }
     }
     // packed 64-B leaf records (one sector): {mask, fg, off[0..9], pad} with off = x | y << 16
@@ -950,23 +952,23 @@ void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, const fl
   k_integral<<<grid, 256, 0, s>>>(faces, gray, mag, minmax, chan);
 }
 
-int traverse_lds_bytes(int G, int step) {
-  const int WW = 32 + step * (G - 1);
-  return NCH * WW * trav_row_pitch(WW) * 2;
+int traverse_lds_bytes(int G, int step, int step_y) {
+  const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1);
+  return NCH * WH * trav_row_pitch(WW) * 2;
 }
 
-bool traverse_window_fits(int G, int step, int lds_cap) {
-  const int WW = 32 + step * (G - 1);
-  return traverse_lds_bytes(G, step) <= lds_cap && NCH * WW * (trav_row_pitch(WW) / 4) <= TRAV_NS * TRAV_U;
+bool traverse_window_fits(int G, int step, int step_y, int lds_cap) {
+  const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1);
+  return traverse_lds_bytes(G, step, step_y) <= lds_cap && NCH * WH * (trav_row_pitch(WW) / 4) <= TRAV_NS * TRAV_U;
 }
 
 void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* nodes, const int32_t* roots,
-                     const HpState* state, int ntrees_hp, int step, const uint16_t* chan, int32_t* leaf_out,
-                     int n_wg, hipStream_t s) {
+                     const HpState* state, int ntrees_hp, int step, int step_y, const uint16_t* chan,
+                     int32_t* leaf_out, int n_wg, hipStream_t s) {
   const int total_blocks = n * bpf;
   if (total_blocks <= 0) return;
-  TravArgs A{faces, n, bpf, nodes, roots, state, ntrees_hp, step, chan, leaf_out};
-  const int lds = traverse_lds_bytes(G, step);
+  TravArgs A{faces, n, bpf, nodes, roots, state, ntrees_hp, step, step_y, chan, leaf_out};
+  const int lds = traverse_lds_bytes(G, step, step_y);
   const int grid = std::max(8, n_wg & ~7);
 #define FFD_TRAV(HPV, GV) k_traverse<HPV, GV><<<grid, TRAV_NT, lds, s>>>(A)
   if (hp) {
@@ -1004,8 +1006,9 @@ void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const 
 }
 
 void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint4* leaf_rec, const HpState* state,
-                  int tslots, int step, int half_patch, int n_parts, Vote* votes, int32_t* vote_counts, hipStream_t s) {
-  k_votes<<<(n + 3) / 4, 256, 0, s>>>(faces, n, mp_leaf, leaf_rec, state, tslots, step, half_patch, n_parts, votes,
+                  int tslots, int step, int step_y, int half_patch, int n_parts, Vote* votes, int32_t* vote_counts,
+                  hipStream_t s) {
+  k_votes<<<(n + 3) / 4, 256, 0, s>>>(faces, n, mp_leaf, leaf_rec, state, tslots, step, step_y, half_patch, n_parts, votes,
                                       vote_counts);
 }
 

@@ -26,12 +26,12 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_w, int max_h, co
                   const float4* coef, float* mag, uint32_t* minmax, hipStream_t s);
 void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, const float* mag, const uint32_t* minmax,
                      uint16_t* chan, hipStream_t s);
-int traverse_lds_bytes(int G, int step);
-bool traverse_window_fits(int G, int step, int lds_cap);
+int traverse_lds_bytes(int G, int step, int step_y);
+bool traverse_window_fits(int G, int step, int step_y, int lds_cap);
 // n_wg: persistent workgroups (one per CU; rounded down to a multiple of 8 XCDs)
 void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* nodes, const int32_t* roots,
-                     const HpState* state, int ntrees_hp, int step, const uint16_t* chan, int32_t* leaf_out,
-                     int n_wg, hipStream_t s);
+                     const HpState* state, int ntrees_hp, int step, int step_y, const uint16_t* chan,
+                     int32_t* leaf_out, int n_wg, hipStream_t s);
 hipError_t set_traverse_lds_limit(int bytes);
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
                          const int32_t* patches, int n_patches, const uint16_t* chan, int64_t plane,
@@ -40,7 +40,8 @@ void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const 
                     int n_forests, int ntrees_per_forest, HpState* state, FaceOut* out, hipStream_t s);
 // leaf_rec: 4 x uint4 (64 B) per FFD leaf = {vote mask, fg, off[10], pad} (off = x | y << 16, int16 each)
 void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint4* leaf_rec, const HpState* state,
-                  int tslots, int step, int half_patch, int n_parts, Vote* votes, int32_t* vote_counts, hipStream_t s);
+                  int tslots, int step, int step_y, int half_patch, int n_parts, Vote* votes, int32_t* vote_counts,
+                  hipStream_t s);
 void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int tslots, int n_parts, float lamda,
                       int max_iter, float stop, const Vote* votes, const int32_t* vote_counts, float* ms_mean,
                       FaceOut* out, hipStream_t s);

@@ -83,6 +83,8 @@ typedef struct {             /* MultiPartEstimatorOption, include/FaceForest.hpp
   float min_forground;               /* 0.5  */
   float min_pf;                      /* 0.25 */
   float max_variance;                /* 25   */
+  int32_t step_size_y;               /* 0: = step_size (the reference's single step); > 0: a
+                                        separate y step (SURVEY.md C4's 4x density grid, (2, 1)) */
 } ffd_multipart_option;
 
 typedef struct {             /* MeanShiftOption, include/MeanShift.hpp:16-25 */

@@ -48,6 +48,7 @@ def lib():
             raise RuntimeError(f"oracle library missing: {LIB_PATH} (run __graft_entry__.build())")
         L = ctypes.CDLL(LIB_PATH)
         L.oracle_load_model.argtypes = [ctypes.c_char_p]
+        L.oracle_set_steps.argtypes = [ctypes.c_int32] * 3
         L.oracle_last_error.restype = ctypes.c_char_p
         L.oracle_analyze_face.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 8 + [
             ctypes.POINTER(OracleFace), ctypes.POINTER(OracleTrace)]
@@ -75,6 +76,12 @@ def load_model(path):
     if lib().oracle_load_model(path.encode()) != 0:
         raise RuntimeError("oracle_load_model: " + lib().oracle_last_error().decode())
     _loaded_model = path
+
+
+def set_steps(hp_step=4, mp_step_x=3, mp_step_y=3):
+    """Patch-grid steps used by analyze_face / geometry (reference defaults 4, 3, 3)."""
+    if lib().oracle_set_steps(hp_step, mp_step_x, mp_step_y) != 0:
+        raise RuntimeError(lib().oracle_last_error().decode())
 
 
 def _p(a):

@@ -485,6 +485,10 @@ inline int to_int_trunc(float v) {  // static_cast<int>(float) on x86-64 (cvttss
 
 struct Geometry { int W, H, patch, nhx, nhy, nmx, nmy; float scale; };
 
+// patch-grid steps: HeadPoseEstimatorOption::step_size 4, MultiPartEstimatorOption::step_size 3
+// (FaceForest.hpp:34-58); the FFD y step may differ only for SURVEY.md's C4 stress grid
+int g_hp_step = 4, g_mp_step_x = 3, g_mp_step_y = 3;
+
 bool geometry(int bw, int bh, Geometry& g) {
   if (bw <= 0 || bh <= 0) return false;
   // FaceForest.cpp:202-204: scale = 125.f/cols; Size(cols*scale, rows*scale) truncates
@@ -493,8 +497,8 @@ bool geometry(int bw, int bh, Geometry& g) {
   g.H = (int)((float)bh * g.scale);
   g.patch = (int)std::round(g_hp.face_size * g_hp.patch_ratio);  // getPatchSize (Constants.hpp:27-30)
   auto cnt = [](int extent, int patch, int step) { int n = 0; for (int x = 0; x < extent - patch; x += step) n++; return n; };
-  g.nhx = cnt(g.W, g.patch, 4); g.nhy = cnt(g.H, g.patch, 4);   // HeadPoseEstimatorOption step 4
-  g.nmx = cnt(g.W, g.patch, 3); g.nmy = cnt(g.H, g.patch, 3);   // MultiPartEstimatorOption step 3
+  g.nhx = cnt(g.W, g.patch, g_hp_step); g.nhy = cnt(g.H, g.patch, g_hp_step);
+  g.nmx = cnt(g.W, g.patch, g_mp_step_x); g.nmy = cnt(g.H, g.patch, g_mp_step_y);
   return g.W > 0 && g.H > 0;
 }
 
@@ -504,6 +508,12 @@ bool geometry(int bw, int bh, Geometry& g) {
 extern "C" {
 
 const char* oracle_last_error(void) { return g_err.c_str(); }
+
+int oracle_set_steps(int32_t hp_step, int32_t mp_step_x, int32_t mp_step_y) {
+  if (hp_step <= 0 || mp_step_x <= 0 || mp_step_y <= 0) { g_err = "bad step"; return -1; }
+  g_hp_step = hp_step; g_mp_step_x = mp_step_x; g_mp_step_y = mp_step_y;
+  return 0;
+}
 
 int oracle_load_model(const char* path) {
   std::lock_guard<std::mutex> lk(g_mu);
@@ -596,8 +606,8 @@ int oracle_analyze_face(const uint8_t* bgr, int32_t iw, int32_t ih, int32_t stri
   // a13: getHeadPoseVotesMT (face_utils.cpp:183-242), grid x outer / y inner, step 4
   const int HT = (int)g_hp.roots.size();
   std::vector<std::pair<int, int>> hp_patches;
-  for (int x = 0; x < W - P; x += 4)
-    for (int y = 0; y < H - P; y += 4) hp_patches.push_back({x, y});
+  for (int x = 0; x < W - P; x += g_hp_step)
+    for (int y = 0; y < H - P; y += g_hp_step) hp_patches.push_back({x, y});
   std::vector<int> hp_leafs(hp_patches.size() * HT);
   run_pool(threads, (int)hp_patches.size(), [&](int i) {
     for (int t = 0; t < HT; t++)
@@ -648,8 +658,8 @@ int oracle_analyze_face(const uint8_t* bgr, int32_t iw, int32_t ih, int32_t stri
   // a16: getFacialFeaturesVotesMT (face_utils.cpp:244-302), step 3
   const int MT = (int)trees.size();
   std::vector<std::pair<int, int>> mp_patches;
-  for (int x = 0; x < W - P; x += 3)
-    for (int y = 0; y < H - P; y += 3) mp_patches.push_back({x, y});
+  for (int x = 0; x < W - P; x += g_mp_step_x)
+    for (int y = 0; y < H - P; y += g_mp_step_y) mp_patches.push_back({x, y});
   std::vector<int> mp_leafs(mp_patches.size() * MT);
   run_pool(threads, (int)mp_patches.size(), [&](int i) {
     for (int t = 0; t < MT; t++)

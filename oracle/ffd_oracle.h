@@ -46,6 +46,8 @@ typedef struct {
 } oracle_trace;
 
 int oracle_load_model(const char* path);
+/* Patch-grid steps (defaults 4 / 3 / 3 = the reference's options; global, not thread-safe). */
+int oracle_set_steps(int32_t hp_step, int32_t mp_step_x, int32_t mp_step_y);
 const char* oracle_last_error(void);
 
 /* analyzeFace (FaceForest.cpp:183-258). threads<=1: serial; >1: reference-shaped
