@@ -123,14 +123,16 @@ __global__ __launch_bounds__(256) void k_gray_resize(const FaceDesc* __restrict_
 //   scale 0 (7x7): 49 taps in row-major order
 //   scale >= 1   : (W*W-1)/2 pairs in row-major order, then the centre [re0..re6, 0]
 // One 512-thread workgroup computes a 64x32 output tile of one face for the 7 orientations of
-// one scale; each thread owns 4 horizontally adjacent pixels and slides a 4-wide window along
-// each kernel row, so one new LDS value per tap feeds 56 FMAs.  The per-pixel operation order is
+// one scale from an LDS copy of the (reflect-101 padded) input tile; each thread owns 4
+// horizontally adjacent pixels, the (re, im) pairs accumulate in packed FMAs whose coefficient
+// operands are wave-uniform scalar loads (SGPR pairs).  The per-pixel operation order is
 // the restatement's (oracle/ffd_oracle.cpp gabor_mag): 7x7 = OpenCV's direct row-major mul+add;
 // larger = folded pairs S = a+b, D = a-b, fma in row-major pair order, then the centre.
 constexpr int GB_TX = 64, GB_TY = 32, GB_THREADS = 512;
 #ifndef GB_UNROLL
 #define GB_UNROLL 1
 #endif
+
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <int W> struct GaborCfg;
@@ -151,16 +153,13 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
   constexpr int LW = ((GB_TX + 2 * R + 3) / 4) * 4 + 1;
   constexpr int LH = GB_TY + 2 * R;
   constexpr int NU = GaborCfg<W>::nu, OFF = GaborCfg<W>::off;
-  constexpr int NTAP = (W == 7) ? 49 : (W * W - 1) / 2 + 1;  // incl. centre
   __shared__ float tile[LH * LW];
-  __shared__ float4 coef[NTAP * 4];
   __shared__ uint32_t red[8][14];
   const FaceDesc fd = faces[blockIdx.y];
   if (!fd.valid) return;
   const int tiles_x = (fd.W + GB_TX - 1) / GB_TX;
   const int tx0 = (blockIdx.x % tiles_x) * GB_TX, ty0 = (blockIdx.x / tiles_x) * GB_TY;
   if (ty0 >= fd.H) return;  // grid is sized for the batch's tallest face
-  for (int i = threadIdx.x; i < NTAP * 4; i += GB_THREADS) coef[i] = coef_g[OFF / 4 + i];
   const uint8_t* g = gray + fd.gray_off;
   for (int i = threadIdx.x; i < LH * (GB_TX + 2 * R); i += GB_THREADS) {
     const int ly = i / (GB_TX + 2 * R), lx = i % (GB_TX + 2 * R);
@@ -180,8 +179,11 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
     for (int o = 0; o < 7; o++) acc[k][o] = f2{0.f, 0.f};
   // centre pixel (ty, 4tx + k) sits at tile (ty + R, 4tx + R + k)
   const float* ctr = &tile[(ty + R) * LW + 4 * tx + R];
+  // wave-uniform coefficients straight from global memory: scalar loads, SGPR-pair operands of
+  // the packed FMAs (no LDS traffic, no VGPRs)
+  const float4* cg = coef_g + OFF / 4;
   auto load_coef = [&](int t, f2* c) {
-    const float4 c0 = coef[t * 4 + 0], c1 = coef[t * 4 + 1], c2 = coef[t * 4 + 2], c3 = coef[t * 4 + 3];
+    const float4 c0 = cg[t * 4 + 0], c1 = cg[t * 4 + 1], c2 = cg[t * 4 + 2], c3 = cg[t * 4 + 3];
     c[0] = f2{c0.x, c0.y}; c[1] = f2{c0.z, c0.w}; c[2] = f2{c1.x, c1.y}; c[3] = f2{c1.z, c1.w};
     c[4] = f2{c2.x, c2.y}; c[5] = f2{c2.z, c2.w}; c[6] = f2{c3.x, c3.y};
   };
@@ -230,7 +232,7 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
     }
 #pragma unroll GB_UNROLL
     for (int dxi = 0; dxi < R; dxi++) pair(ctr + (dxi - R), ctr - (dxi - R), R * W + dxi);  // dy = 0
-    const float4 c0 = coef[HALF * 4 + 0], c1 = coef[HALF * 4 + 1], c2 = coef[HALF * 4 + 2], c3 = coef[HALF * 4 + 3];
+    const float4 c0 = cg[HALF * 4 + 0], c1 = cg[HALF * 4 + 1], c2 = cg[HALF * 4 + 2], c3 = cg[HALF * 4 + 3];
     const float kr[7] = {c0.x, c0.z, c1.x, c1.z, c2.x, c2.z, c3.x};
 #pragma unroll
     for (int k = 0; k < 4; k++) {
