@@ -114,7 +114,7 @@ struct Workspace {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
   bool pending = false;
-  DevBuf faces, gray, mag, minmax, chan, hpleaf, mpleaf, votes, state, ms_mean, vote_counts;
+  DevBuf faces, gray, mag, chan, hpleaf, mpleaf, votes, state, ms_mean, vote_counts;
   std::vector<FaceDesc> h_fds;  // host staging, reused only after `done`
   std::vector<FaceDesc> desc;   // descriptors of the chunk last run here (ffd_get_trace)
   int first = 0, count = 0;
@@ -453,7 +453,6 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   if (n == 0) return;
   const hipStream_t st = w.stream;
   int64_t gray_b = 0, mag_e = 0, ch_e = 0, hp_e = 0, mp_e = 0, vote_e = 0;
-  int max_w = 0, max_h = 0;
   for (auto& f : fds) {
     if (!f.valid) continue;
     f.gray_off = gray_b;
@@ -469,8 +468,6 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
     mp_e += (int64_t)MAX_TREES * f.nmx * f.nmy;
     f.vote_off = vote_e;
     vote_e += (int64_t)NPARTS * MAX_TREES * f.nmx * f.nmy;
-    max_w = std::max(max_w, f.W);
-    max_h = std::max(max_h, f.H);
   }
   w.gray.ensure(gray_b + 256);
   w.mag.ensure((mag_e + 64) * 4);
@@ -478,24 +475,21 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   w.hpleaf.ensure((hp_e + 64) * 4);
   w.mpleaf.ensure((mp_e + 64) * 4);
   w.votes.ensure((vote_e + 64) * sizeof(Vote));
-  w.minmax.ensure((size_t)n * NGABOR * 2 * 4);
   w.state.ensure((size_t)n * sizeof(HpState));
   w.ms_mean.ensure((size_t)n * NPARTS * 2 * 4);
   w.vote_counts.ensure((size_t)n * NPARTS * 4);
   upload(w.faces, fds, st);
-  HIP_CHECK(hipMemsetAsync(w.minmax.p, 0xFF, (size_t)n * NGABOR * 2 * 4, st));
   HIP_CHECK(hipMemsetAsync(d_out, 0, (size_t)n * sizeof(FaceOut), st));
 
   const FaceDesc* dfd = w.faces.as<FaceDesc>();
   stage(0, st, [&] { launch_gray_resize(dfd, n, d_images, w.gray.as<uint8_t>(), st); });
   for (int nu = 4; nu >= 0; nu--)  // largest kernels first
     stage(1 + (4 - nu), st, [&] {
-      launch_gabor(nu, dfd, n, max_w, max_h, w.gray.as<uint8_t>(), gabor_coef.as<float4>(), w.mag.as<float>(),
-                   w.minmax.as<uint32_t>(), st);
+      launch_gabor(nu, dfd, n, w.gray.as<uint8_t>(), gabor_coef.as<float4>(), w.mag.as<float>(),
+                   w.chan.as<uint16_t>(), st);
     });
   stage(6, st, [&] {
-    launch_integral(dfd, n, w.gray.as<uint8_t>(), w.mag.as<float>(), w.minmax.as<uint32_t>(), w.chan.as<uint16_t>(),
-                    st);
+    launch_integral(dfd, n, w.gray.as<uint8_t>(), w.chan.as<uint16_t>(), st);
   });
   stage(7, st, [&] {
     launch_traverse(true, dfd, n, blocks_per_face(fds, true, trav_g_hp), trav_g_hp, hp_nodes.as<uint4>(),
@@ -854,17 +848,14 @@ ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t
     w.gray.ensure((size_t)H * PITCH + 256);
     w.mag.ensure((size_t)NGABOR * H * PITCH * 4 + 256);
     w.chan.ensure((size_t)NCH * f.plane * 2 + 256);
-    w.minmax.ensure(NGABOR * 2 * 4);
     std::vector<FaceDesc> one{f};
     upload(w.faces, one, w.stream);
-    HIP_CHECK(hipMemsetAsync(w.minmax.p, 0xFF, NGABOR * 2 * 4, w.stream));
     const FaceDesc* dfd = w.faces.as<FaceDesc>();
     launch_gray_resize(dfd, 1, e->scratch_a.as<uint8_t>(), w.gray.as<uint8_t>(), w.stream);
     for (int nu = 4; nu >= 0; nu--)
-      launch_gabor(nu, dfd, 1, W, H, w.gray.as<uint8_t>(), e->gabor_coef.as<float4>(), w.mag.as<float>(),
-                   w.minmax.as<uint32_t>(), w.stream);
-    launch_integral(dfd, 1, w.gray.as<uint8_t>(), w.mag.as<float>(), w.minmax.as<uint32_t>(), w.chan.as<uint16_t>(),
-                    w.stream);
+      launch_gabor(nu, dfd, 1, w.gray.as<uint8_t>(), e->gabor_coef.as<float4>(), w.mag.as<float>(),
+                   w.chan.as<uint16_t>(), w.stream);
+    launch_integral(dfd, 1, w.gray.as<uint8_t>(), w.chan.as<uint16_t>(), w.stream);
     HIP_CHECK(hipGetLastError());
     std::vector<uint16_t> v((size_t)NCH * f.plane);
     HIP_CHECK(hipMemcpyAsync(v.data(), w.chan.p, v.size() * 2, hipMemcpyDeviceToHost, w.stream));

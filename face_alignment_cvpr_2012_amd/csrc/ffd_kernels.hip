@@ -117,6 +117,75 @@ __global__ __launch_bounds__(256) void k_gray_resize(const FaceDesc* __restrict_
   }
 }
 
+// ---------------------------------------------------------------- integral --
+// One wave per (face, channel): the wave walks the rows top to bottom; lane l owns image columns
+// 2l, 2l+1, keeps their running column sums, and a 64-lane prefix scan turns them into integral
+// rows; lane l writes integral entries 2l, 2l+1 as one aligned u32 (entry 2l = exclusive prefix,
+// 2l+1 = + column 2l).  Integer-exact, so order does not matter; stored modulo 2^16 (rect_mean16).
+__device__ __forceinline__ int chan_value(int c, const uint8_t* g, int W, int H, int y, int x) {
+  if (x >= W) return 0;
+  if (c == 0) return g[y * PITCH + x];
+  int ym = reflect101(y - 1, H), yp = reflect101(y + 1, H), xm = reflect101(x - 1, W), xp = reflect101(x + 1, W);
+  auto I = [&](int yy, int xx) { return (int)g[yy * PITCH + xx]; };
+  int v;
+  if (c == 36)  // Sobel(0,1): d/dy
+    v = (I(yp, xm) + 2 * I(yp, x) + I(yp, xp)) - (I(ym, xm) + 2 * I(ym, x) + I(ym, xp));
+  else          // Sobel(1,0): d/dx
+    v = (I(ym, xp) + 2 * I(y, xp) + I(yp, xp)) - (I(ym, xm) + 2 * I(y, xm) + I(yp, xm));
+  return sat_u8(v);
+}
+
+// The scan of one channel by one wave.  value(y, b) returns the u8 values of columns 2l, 2l+1 of
+// row y for b = 0..RB-1 batches (all of a batch's loads are issued before its scans).
+template <class RowFn>
+__device__ __forceinline__ void integral_scan(uint16_t* __restrict__ out, int W, int H, int lane, RowFn row_values) {
+  for (int x = lane; x <= W; x += 64) out[x] = 0;  // row 0 of the integral image
+  constexpr int RB = 8;
+  uint32_t c0 = 0, c1 = 0;
+  for (int y0 = 0; y0 < H; y0 += RB) {
+    uint32_t v0[RB], v1[RB];
+    row_values(y0, v0, v1);
+#pragma unroll
+    for (int b = 0; b < RB; b++) {
+      if (y0 + b >= H) break;
+      c0 += v0[b];
+      c1 += v1[b];
+      const uint32_t s2 = c0 + c1;
+      uint32_t incl = s2;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+        if (lane >= d) incl += o;
+      }
+      const uint32_t excl = incl - s2;
+      uint32_t* r = reinterpret_cast<uint32_t*>(out + (int64_t)(y0 + b + 1) * PITCH);
+      // entries >= W+1 land in the row's pitch padding (never read by a patch)
+      r[lane] = (excl & 0xFFFFu) | ((excl + c0) << 16);
+    }
+  }
+}
+
+// gray (channel 0) and the two Sobel channels (36 d/dy, 37 d/dx); the 35 Gabor channels are
+// integrated by k_gabor itself.  One 4-wave workgroup per face (the 4th wave idles).
+__global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ faces,
+                                                  const uint8_t* __restrict__ gray,
+                                                  uint16_t* __restrict__ chan) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const FaceDesc fd = faces[blockIdx.x];
+  if (!fd.valid || wv >= 3) return;
+  const int c = wv == 0 ? 0 : 35 + wv;
+  const int W = fd.W, H = fd.H, x0 = 2 * lane;
+  const uint8_t* g = gray + fd.gray_off;
+  integral_scan(chan + fd.ch_off + (int64_t)c * fd.plane, W, H, lane, [&](int y0, uint32_t* v0, uint32_t* v1) {
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const int y = min(y0 + b, H - 1);
+      v0[b] = (uint32_t)chan_value(c, g, W, H, y, x0);
+      v1[b] = (uint32_t)chan_value(c, g, W, H, y, x0 + 1);
+    }
+  });
+}
+
 // ------------------------------------------------------------------ Gabor --
 // Coefficient table (host-built from createKernel, FeatureChannelFactory.hpp:186-251), 16 floats
 // per tap/pair: [re0..re6, 0, im0..im6, 0]:
@@ -147,7 +216,7 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
                                                       const uint8_t* __restrict__ gray,
                                                       const float4* __restrict__ coef_g,
                                                       float* __restrict__ mag,
-                                                      uint32_t* __restrict__ minmax) {
+                                                      uint16_t* __restrict__ chan) {
   constexpr int R = (W - 1) / 2;
   // row stride (floats) == 1 mod 4: the 4 rows a 32-lane group touches fall on disjoint banks
   constexpr int LW = ((GB_TX + 2 * R + 3) / 4) * 4 + 1;
@@ -155,12 +224,21 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
   constexpr int NU = GaborCfg<W>::nu, OFF = GaborCfg<W>::off;
   __shared__ float tile[LH * LW];
   __shared__ uint32_t red[8][14];
-  const FaceDesc fd = faces[blockIdx.y];
+  __shared__ float s_sf[7], s_hf[7];
+  const FaceDesc fd = faces[blockIdx.x];
   if (!fd.valid) return;
-  const int tiles_x = (fd.W + GB_TX - 1) / GB_TX;
-  const int tx0 = (blockIdx.x % tiles_x) * GB_TX, ty0 = (blockIdx.x / tiles_x) * GB_TY;
-  if (ty0 >= fd.H) return;  // grid is sized for the batch's tallest face
+  const int tiles_x = (fd.W + GB_TX - 1) / GB_TX, tiles = tiles_x * ((fd.H + GB_TY - 1) / GB_TY);
   const uint8_t* g = gray + fd.gray_off;
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  // per-thread min / max of the face's magnitudes (max kept as min(~bits): unsigned order == float
+  // order for m >= +0), over all tiles of the face
+  uint32_t mn[7], mx[7];
+#pragma unroll
+  for (int o = 0; o < 7; o++) mn[o] = mx[o] = 0xFFFFFFFFu;
+#pragma unroll 1
+  for (int tl = 0; tl < tiles; tl++) {
+  const int tx0 = (tl % tiles_x) * GB_TX, ty0 = (tl / tiles_x) * GB_TY;
+  __syncthreads();  // the previous tile's reads of `tile` are done
   for (int i = threadIdx.x; i < LH * (GB_TX + 2 * R); i += GB_THREADS) {
     const int ly = i / (GB_TX + 2 * R), lx = i % (GB_TX + 2 * R);
     const int y = reflect101(ty0 - R + ly, fd.H), x = reflect101(tx0 - R + lx, fd.W);
@@ -168,7 +246,6 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
   }
   __syncthreads();
   // wave w covers threads tx in [8*(w&1), +8) x ty in [8*(w>>1), +8); 4 px per thread
-  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int tx = (wv & 1) * 8 + (ln & 7), ty = (wv >> 1) * 8 + (ln >> 3);
   // acc[k][o] = (re, im): one v_pk_fma_f32 / v_pk_mul+v_pk_add per (pixel, orientation), each
   // half of which is exactly the scalar fmaf / mul+add of the restatement
@@ -242,24 +319,23 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
     }
   }
   const int x0 = tx0 + 4 * tx, y = ty0 + ty;
-  uint32_t mn[7], mx[7];
 #pragma unroll
   for (int o = 0; o < 7; o++) {
     float m4[4];
-    mn[o] = 0xFFFFFFFFu;
-    mx[o] = 0xFFFFFFFFu;  // max kept as min(~bits): one atomicMin serves both
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const float i2 = acc[k][o].y * acc[k][o].y, r2 = acc[k][o].x * acc[k][o].x;
       m4[k] = __builtin_sqrtf(i2 + r2);
       const bool in = (x0 + k) < fd.W && y < fd.H;
-      const uint32_t bits = __float_as_uint(m4[k]);  // m >= +0: unsigned order == float order
+      const uint32_t bits = __float_as_uint(m4[k]);
       if (in) { mn[o] = min(mn[o], bits); mx[o] = min(mx[o], ~bits); }
     }
     if (y < fd.H)  // columns >= W land in the row's pitch padding, never read
       *reinterpret_cast<float4*>(&mag[fd.mag_off + ((int64_t)(NU * 7 + o) * fd.H + y) * PITCH + x0]) =
           make_float4(m4[0], m4[1], m4[2], m4[3]);
   }
+  }  // tiles
+  // face-wide min / max -> cv::normalize(NORM_MINMAX, 0, 1) + convertTo scale / shift (OpenCV 2.4.9)
 #pragma unroll
   for (int o = 0; o < 7; o++) {
 #pragma unroll
@@ -272,107 +348,38 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
 #pragma unroll
     for (int o = 0; o < 7; o++) { red[wv][o] = mn[o]; red[wv][7 + o] = mx[o]; }
   }
+  __syncthreads();  // also: every magnitude store of the workgroup is visible to it
+  if (threadIdx.x < 7) {
+    const int o = threadIdx.x;
+    uint32_t a = red[0][o], b = red[0][7 + o];
+    for (int w = 1; w < GB_THREADS / 64; w++) { a = min(a, red[w][o]); b = min(b, red[w][7 + o]); }
+    const double smin = (double)__uint_as_float(a), smax = (double)__uint_as_float(~b);
+    const double dmin = 0, dmax = 1;
+    const double scale = (dmax - dmin) * (smax - smin > 2.220446049250313e-16 ? 1. / (smax - smin) : 0);
+    const double shift = dmin - smin * scale;
+    s_sf[o] = (float)scale;
+    s_hf[o] = (float)shift;
+  }
   __syncthreads();
-  if (threadIdx.x < 14) {
-    const int k = threadIdx.x;
-    uint32_t v = red[0][k];
-    for (int w = 1; w < GB_THREADS / 64; w++) v = min(v, red[w][k]);
-    uint32_t* slot = minmax + ((int64_t)blockIdx.y * NGABOR + NU * 7 + (k % 7)) * 2;
-    atomicMin(slot + (k < 7 ? 0 : 1), v);
-  }
-}
-
-// ---------------------------------------------------------------- integral --
-// One wave per (face, channel): the wave walks the rows top to bottom; lane l owns
-// columns 2l, 2l+1, keeps their running column sums and a 64-lane prefix scan turns
-// them into integral-image rows.  Integer-exact, so order does not matter.
-__device__ __forceinline__ int chan_value(int c, const uint8_t* g, const float* m, int W, int H, int y, int x,
-                                          float sf, float hf) {
-  if (x >= W) return 0;
-  if (c == 0) return g[y * PITCH + x];
-  if (c <= NGABOR) {
-    float v = m[y * PITCH + x] * sf + hf;  // normalize: v*scale + shift (float, no FMA)
-    return sat_u8(cv_round(v * 255.f + 0.f));
-  }
-  int ym = reflect101(y - 1, H), yp = reflect101(y + 1, H), xm = reflect101(x - 1, W), xp = reflect101(x + 1, W);
-  auto I = [&](int yy, int xx) { return (int)g[yy * PITCH + xx]; };
-  int v;
-  if (c == 36)  // Sobel(0,1): d/dy
-    v = (I(yp, xm) + 2 * I(yp, x) + I(yp, xp)) - (I(ym, xm) + 2 * I(ym, x) + I(ym, xp));
-  else          // Sobel(1,0): d/dx
-    v = (I(ym, xp) + 2 * I(y, xp) + I(yp, xp)) - (I(ym, xm) + 2 * I(y, xm) + I(yp, xm));
-  return sat_u8(v);
-}
-
-__global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ faces,
-                                                  const uint8_t* __restrict__ gray,
-                                                  const float* __restrict__ mag,
-                                                  const uint32_t* __restrict__ minmax,
-                                                  uint16_t* __restrict__ chan) {
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const FaceDesc fd = faces[blockIdx.y];
-  if (!fd.valid || c >= NCH) return;
-  const int W = fd.W, H = fd.H;
-  const uint8_t* g = gray + fd.gray_off;
-  const float* m = mag + fd.mag_off + (c >= 1 && c <= NGABOR ? (int64_t)(c - 1) * H * PITCH : 0);
-  float sf = 0.f, hf = 0.f;
-  if (c >= 1 && c <= NGABOR) {
-    // cv::normalize(NORM_MINMAX, 0, 1) -> convertTo(scale, shift) (OpenCV 2.4.9)
-    const uint32_t* mm = minmax + ((int64_t)blockIdx.y * NGABOR + (c - 1)) * 2;
-    double smin = (double)__uint_as_float(mm[0]), smax = (double)__uint_as_float(~mm[1]);
-    double dmin = 0, dmax = 1;
-    double scale = (dmax - dmin) * (smax - smin > 2.220446049250313e-16 ? 1. / (smax - smin) : 0);
-    double shift = dmin - smin * scale;
-    sf = (float)scale;
-    hf = (float)shift;
-  }
-  uint16_t* out = chan + fd.ch_off + (int64_t)c * fd.plane;  // integral mod 2^16 (see rect_mean16)
-  // lane l owns image columns 2l, 2l+1 and writes integral entries 2l, 2l+1 of each row as one
-  // aligned u32 (entry 2l = exclusive prefix, 2l+1 = + column 2l); rows are processed in
-  // batches of RB whose loads are all issued before the first scan.
-  const int x0 = 2 * lane;
-  for (int x = lane; x <= W; x += 64) out[x] = 0;  // row 0 of the integral image
-  constexpr int RB = 8;
-  uint32_t c0 = 0, c1 = 0;
-  for (int y0 = 0; y0 < H; y0 += RB) {
-    uint32_t v0[RB], v1[RB];
-    if (c >= 1 && c <= NGABOR) {
-      float2 mv[RB];
+  // FeatureChannelFactory.hpp:271-286: quantise (v*scale + shift, *255, cvRound, saturate) and
+  // integrate the 7 channels, one wave each, reading the magnitudes back from L2
+  if (wv < 7) {
+    const int o = wv, lane = ln, x0 = 2 * lane, FW = fd.W, FH = fd.H;
+    const float sf = s_sf[o], hf = s_hf[o];
+    const float* m = mag + fd.mag_off + (int64_t)(NU * 7 + o) * FH * PITCH;
+    integral_scan(chan + fd.ch_off + (int64_t)(1 + NU * 7 + o) * fd.plane, FW, FH, lane,
+                  [&](int y0, uint32_t* v0, uint32_t* v1) {
+                    float2 mv[8];
 #pragma unroll
-      for (int b = 0; b < RB; b++)
-        mv[b] = (y0 + b < H) ? *reinterpret_cast<const float2*>(&m[(y0 + b) * PITCH + x0]) : make_float2(0.f, 0.f);
+                    for (int b = 0; b < 8; b++)
+                      mv[b] = (y0 + b < FH) ? *reinterpret_cast<const float2*>(&m[(y0 + b) * PITCH + x0])
+                                            : make_float2(0.f, 0.f);
 #pragma unroll
-      for (int b = 0; b < RB; b++) {
-        // normalize: v*scale + shift (float, no FMA), convertTo(u8, 255): cvRound, saturate
-        v0[b] = (x0 < W) ? (uint32_t)sat_u8(cv_round((mv[b].x * sf + hf) * 255.f + 0.f)) : 0u;
-        v1[b] = (x0 + 1 < W) ? (uint32_t)sat_u8(cv_round((mv[b].y * sf + hf) * 255.f + 0.f)) : 0u;
-      }
-    } else {
-#pragma unroll
-      for (int b = 0; b < RB; b++) {
-        const int y = min(y0 + b, H - 1);
-        v0[b] = (uint32_t)chan_value(c, g, m, W, H, y, x0, sf, hf);
-        v1[b] = (uint32_t)chan_value(c, g, m, W, H, y, x0 + 1, sf, hf);
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < RB; b++) {
-      if (y0 + b >= H) break;
-      c0 += v0[b];
-      c1 += v1[b];
-      const uint32_t s2 = c0 + c1;
-      uint32_t incl = s2;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
-        if (lane >= d) incl += o;
-      }
-      const uint32_t excl = incl - s2;
-      uint32_t* row = reinterpret_cast<uint32_t*>(out + (int64_t)(y0 + b + 1) * PITCH);
-      // entries >= W+1 land in the row's pitch padding (never read by a patch)
-      row[lane] = (excl & 0xFFFFu) | ((excl + c0) << 16);
-    }
+                    for (int b = 0; b < 8; b++) {
+                      v0[b] = (x0 < FW) ? (uint32_t)sat_u8(cv_round((mv[b].x * sf + hf) * 255.f + 0.f)) : 0u;
+                      v1[b] = (x0 + 1 < FW) ? (uint32_t)sat_u8(cv_round((mv[b].y * sf + hf) * 255.f + 0.f)) : 0u;
+                    }
+                  });
   }
 }
 
@@ -934,24 +941,20 @@ void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uin
   k_gray_resize<<<n, 256, 0, s>>>(faces, images, gray);
 }
 
-void launch_gabor(int nu, const FaceDesc* faces, int n, int max_w, int max_h, const uint8_t* gray,
-                  const float4* coef, float* mag, uint32_t* minmax, hipStream_t s) {
-  const int tiles = ((max_w + GB_TX - 1) / GB_TX) * ((max_h + GB_TY - 1) / GB_TY);
-  if (tiles <= 0 || n <= 0) return;
-  dim3 grid(tiles, n);
+void launch_gabor(int nu, const FaceDesc* faces, int n, const uint8_t* gray, const float4* coef, float* mag,
+                  uint16_t* chan, hipStream_t s) {
+  if (n <= 0) return;
   switch (nu) {
-    case 4: k_gabor<25><<<grid, GB_THREADS, 0, s>>>(faces, gray, coef, mag, minmax); break;
-    case 3: k_gabor<19><<<grid, GB_THREADS, 0, s>>>(faces, gray, coef, mag, minmax); break;
-    case 2: k_gabor<13><<<grid, GB_THREADS, 0, s>>>(faces, gray, coef, mag, minmax); break;
-    case 1: k_gabor<9><<<grid, GB_THREADS, 0, s>>>(faces, gray, coef, mag, minmax); break;
-    default: k_gabor<7><<<grid, GB_THREADS, 0, s>>>(faces, gray, coef, mag, minmax); break;
+    case 4: k_gabor<25><<<n, GB_THREADS, 0, s>>>(faces, gray, coef, mag, chan); break;
+    case 3: k_gabor<19><<<n, GB_THREADS, 0, s>>>(faces, gray, coef, mag, chan); break;
+    case 2: k_gabor<13><<<n, GB_THREADS, 0, s>>>(faces, gray, coef, mag, chan); break;
+    case 1: k_gabor<9><<<n, GB_THREADS, 0, s>>>(faces, gray, coef, mag, chan); break;
+    default: k_gabor<7><<<n, GB_THREADS, 0, s>>>(faces, gray, coef, mag, chan); break;
   }
 }
 
-void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, const float* mag, const uint32_t* minmax,
-                     uint16_t* chan, hipStream_t s) {
-  dim3 grid((NCH + 3) / 4, n);
-  k_integral<<<grid, 256, 0, s>>>(faces, gray, mag, minmax, chan);
+void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t* chan, hipStream_t s) {
+  if (n > 0) k_integral<<<n, 256, 0, s>>>(faces, gray, chan);
 }
 
 int traverse_lds_bytes(int G, int step, int step_y) {

@@ -22,10 +22,12 @@ constexpr int GABOR_COEF_TOTAL = GABOR_OFF4 + gabor_block(25);
 constexpr int GABOR_OFFS[5] = {GABOR_OFF0, GABOR_OFF1, GABOR_OFF2, GABOR_OFF3, GABOR_OFF4};
 
 void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s);
-void launch_gabor(int nu, const FaceDesc* faces, int n, int max_w, int max_h, const uint8_t* gray,
-                  const float4* coef, float* mag, uint32_t* minmax, hipStream_t s);
-void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, const float* mag, const uint32_t* minmax,
-                     uint16_t* chan, hipStream_t s);
+// Gabor scale nu (0..4): magnitudes of the 7 orientations, face-wide min-max normalisation,
+// quantisation and integration of the 7 channels (one workgroup per face)
+void launch_gabor(int nu, const FaceDesc* faces, int n, const uint8_t* gray, const float4* coef, float* mag,
+                  uint16_t* chan, hipStream_t s);
+// integral channels 0 (gray), 36, 37 (Sobel)
+void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t* chan, hipStream_t s);
 int traverse_lds_bytes(int G, int step, int step_y);
 bool traverse_window_fits(int G, int step, int step_y, int lds_cap);
 // n_wg: persistent workgroups (one per CU; rounded down to a multiple of 8 XCDs)
