@@ -141,6 +141,8 @@ struct ffd_engine {
 
   // device model
   DevBuf gabor_coef, hp_nodes, hp_roots, hp_sizes, hp_m, mp_nodes, mp_roots, mp_sizes, mp_rec;
+  bool vote_rec_compact = false;     // 32-B vote records (else 64-B), see load_model
+  int vote_bias_x = 0, vote_bias_y = 0;
 
   std::vector<std::unique_ptr<Workspace>> ws;
   DevBuf images, out, scratch_a, scratch_b, scratch_c;  // host-API staging (ws[0] stream)
@@ -370,9 +372,13 @@ void ffd_engine::load_model(const std::string& path) {
     const auto& var = m.get("mp.leaf_var");
     const auto& pf = m.get("mp.leaf_pf");
     mp_leaves = (int64_t)n.count();
-    std::vector<uint32_t> rec(mp_leaves * 16, 0);  // 64-B records {mask, fg bits, off[10], pad} (k_votes)
+    // per-leaf vote records for k_votes: the filter of face_utils.cpp:276-290 precomputed as a
+    // part mask, fg, and the offsets of the voting parts.  Compact 32-B records (offsets as u8
+    // pairs relative to per-axis biases) when every voting offset fits, else 64-B records.
     const auto& op = desc.mp_option;
     const int np = std::min(op.num_parts, NPARTS);
+    std::vector<uint32_t> mask(mp_leaves);
+    int mnx = 1 << 30, mny = 1 << 30, mxx = -(1 << 30), mxy = -(1 << 30);
     for (int64_t L = 0; L < mp_leaves; L++) {
       uint32_t mk = 0;
       const float f = fg.as<float>()[L];
@@ -380,15 +386,33 @@ void ffd_engine::load_model(const std::string& path) {
         float min_pf = op.min_pf;
         if (i == 0 || i == 7) min_pf *= 1.5;  // outer eye corners
         if (f > op.min_forground && pf.as<float>()[L * 10 + i] > min_pf && var.as<float>()[L * 10 + i] < op.max_variance &&
-            n.as<int32_t>()[L] > op.min_samples)
+            n.as<int32_t>()[L] > op.min_samples) {
           mk |= 1u << i;
+          const int x = off.as<int16_t>()[(L * 10 + i) * 2], y = off.as<int16_t>()[(L * 10 + i) * 2 + 1];
+          mnx = std::min(mnx, x); mxx = std::max(mxx, x);
+          mny = std::min(mny, y); mxy = std::max(mxy, y);
+        }
       }
-      uint32_t* r = &rec[L * 16];
-      r[0] = mk;
-      std::memcpy(&r[1], &f, 4);
+      mask[L] = mk;
+    }
+    vote_rec_compact = mxx - mnx <= 255 && mxy - mny <= 255;
+    vote_bias_x = vote_rec_compact && mnx <= mxx ? mnx : 0;
+    vote_bias_y = vote_rec_compact && mny <= mxy ? mny : 0;
+    const int words = vote_rec_compact ? 8 : 16;
+    std::vector<uint32_t> rec(mp_leaves * words, 0);
+    for (int64_t L = 0; L < mp_leaves; L++) {
+      uint32_t* r = &rec[L * words];
+      r[0] = mask[L];
+      std::memcpy(&r[1], &fg.as<float>()[L], 4);
       for (int i = 0; i < NPARTS; i++) {
-        const int16_t x = off.as<int16_t>()[(L * 10 + i) * 2], y = off.as<int16_t>()[(L * 10 + i) * 2 + 1];
-        r[2 + i] = (uint32_t)(uint16_t)x | (uint32_t)(uint16_t)y << 16;
+        const int x = off.as<int16_t>()[(L * 10 + i) * 2], y = off.as<int16_t>()[(L * 10 + i) * 2 + 1];
+        if (vote_rec_compact) {
+          if (!((mask[L] >> i) & 1u)) continue;  // offsets of non-voting parts are never read
+          const uint32_t u = (uint32_t)(x - vote_bias_x) | (uint32_t)(y - vote_bias_y) << 8;
+          r[2 + i / 2] |= u << (16 * (i & 1));
+        } else {
+          r[2 + i] = (uint32_t)(uint16_t)x | (uint32_t)(uint16_t)y << 16;
+        }
       }
     }
     upload(mp_rec, rec, main_stream());
@@ -508,7 +532,8 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   });
   const int n_parts = std::min(desc.mp_option.num_parts, NPARTS);
   stage(10, st, [&] {
-    launch_votes(dfd, n, w.mpleaf.as<int32_t>(), mp_rec.as<uint4>(), w.state.as<HpState>(), MAX_TREES,
+    launch_votes(dfd, n, w.mpleaf.as<int32_t>(), mp_rec.as<uint4>(), vote_rec_compact, vote_bias_x, vote_bias_y,
+                 w.state.as<HpState>(), MAX_TREES,
                  desc.mp_option.step_size, mp_step_y(), patch / 2, n_parts, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), st);
   });
   stage(11, st, [&] {

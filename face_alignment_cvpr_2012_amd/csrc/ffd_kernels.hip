@@ -737,7 +737,8 @@ __global__ __launch_bounds__(256) void k_hp_pose(const FaceDesc* __restrict__ fa
 // the reference's vote order exactly.
 __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ faces, int n_faces,
                                                const int32_t* __restrict__ mp_leaf,
-                                               const uint4* __restrict__ leaf_rec, const HpState* __restrict__ state,
+                                               const uint4* __restrict__ leaf_rec, int compact, int bias_x,
+                                               int bias_y, const HpState* __restrict__ state,
                                                int tslots, int step, int step_y, int half_patch, int n_parts,
                                                Vote* __restrict__ votes, int32_t* __restrict__ vote_counts) {
   const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -772,24 +773,36 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
         vy0[u] = yi * step_y + half_patch;
       }
     }
-    // packed 64-B leaf records (one sector): {mask, fg, off[0..9], pad} with off = x | y << 16
+    // packed leaf records (see launch_votes): compact 32 B = 2 x uint4, else 64 B = 3 used uint4
     uint4 r0[U], r1[U], r2[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
       r0[u] = r1[u] = r2[u] = make_uint4(0, 0, 0, 0);
       if (leaf[u] >= 0) {
-        const uint4* rec = leaf_rec + (int64_t)leaf[u] * 4;
+        const uint4* rec = leaf_rec + (int64_t)leaf[u] * (compact ? 2 : 4);
         r0[u] = rec[0];
         r1[u] = rec[1];
-        r2[u] = rec[2];
+        if (!compact) r2[u] = rec[2];
       }
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {  // batches in list order: (patch x-major, tree), then part
       const uint32_t mk = r0[u].x;
       const float w = __uint_as_float(r0[u].y);
-      const uint32_t off[NPARTS] = {r0[u].z, r0[u].w, r1[u].x, r1[u].y, r1[u].z,
+      uint32_t off[NPARTS];
+      if (compact) {  // u8 pairs relative to the biases -> the 64-B format's x | y << 16
+        const uint32_t pk[5] = {r0[u].z, r0[u].w, r1[u].x, r1[u].y, r1[u].z};
+#pragma unroll
+        for (int i = 0; i < NPARTS; i++) {
+          const uint32_t v = (pk[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+          off[i] = (uint32_t)(uint16_t)((int)(v & 0xFFu) + bias_x) | (uint32_t)(uint16_t)((int)(v >> 8) + bias_y) << 16;
+        }
+      } else {
+        const uint32_t o[NPARTS] = {r0[u].z, r0[u].w, r1[u].x, r1[u].y, r1[u].z,
                                     r1[u].w, r2[u].x, r2[u].y, r2[u].z, r2[u].w};
+#pragma unroll
+        for (int i = 0; i < NPARTS; i++) off[i] = o[i];
+      }
 #pragma unroll
       for (int i = 0; i < NPARTS; i++) {  // mask bits >= n_parts are never set (engine load)
         const bool vote = (mk >> i) & 1u;
@@ -1010,10 +1023,11 @@ void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const 
   k_hp_pose<<<(n + 3) / 4, 256, 0, s>>>(faces, n, hp_leaf, hp_m, hp_trees, n_forests, ntrees_per_forest, state, out);
 }
 
-void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint4* leaf_rec, const HpState* state,
+void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint4* leaf_rec, bool compact,
+                  int bias_x, int bias_y, const HpState* state,
                   int tslots, int step, int step_y, int half_patch, int n_parts, Vote* votes, int32_t* vote_counts,
                   hipStream_t s) {
-  k_votes<<<(n + 3) / 4, 256, 0, s>>>(faces, n, mp_leaf, leaf_rec, state, tslots, step, step_y, half_patch, n_parts, votes,
+  k_votes<<<(n + 3) / 4, 256, 0, s>>>(faces, n, mp_leaf, leaf_rec, compact ? 1 : 0, bias_x, bias_y, state, tslots, step, step_y, half_patch, n_parts, votes,
                                       vote_counts);
 }
 

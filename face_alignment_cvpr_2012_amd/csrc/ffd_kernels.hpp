@@ -40,8 +40,10 @@ void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t
                          int32_t* leaf_ids, hipStream_t s);
 void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const float* hp_m, int hp_trees,
                     int n_forests, int ntrees_per_forest, HpState* state, FaceOut* out, hipStream_t s);
-// leaf_rec: 4 x uint4 (64 B) per FFD leaf = {vote mask, fg, off[10], pad} (off = x | y << 16, int16 each)
-void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint4* leaf_rec, const HpState* state,
+// leaf_rec per FFD leaf: compact (32 B) = {vote mask, fg, 10 x u16 (x - bias_x) | (y - bias_y) << 8, pad},
+// else 64 B = {vote mask, fg, off[10] = x | y << 16 (int16 each), pad}
+void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint4* leaf_rec, bool compact,
+                  int bias_x, int bias_y, const HpState* state,
                   int tslots, int step, int step_y, int half_patch, int n_parts, Vote* votes, int32_t* vote_counts,
                   hipStream_t s);
 void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int tslots, int n_parts, float lamda,
