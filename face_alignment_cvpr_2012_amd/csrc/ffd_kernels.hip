@@ -839,10 +839,14 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
 #ifndef FFD_MS_TILE
 #define FFD_MS_TILE 64
 #endif
+#ifndef FFD_MS_GRP
+#define FFD_MS_GRP 1
+#endif
 #ifndef FFD_MS_THREADS
 #define FFD_MS_THREADS 256
 #endif
 constexpr int MS_FACES = FFD_MS_FACES, MS_TILE = FFD_MS_TILE, MS_LD = MS_FACES + 1, MS_THREADS = FFD_MS_THREADS;
+constexpr int MS_GRP = FFD_MS_GRP;
 
 __global__ __launch_bounds__(MS_THREADS) void k_meanshift(const FaceDesc* __restrict__ faces, int n_faces,
                                                    int tslots, int n_parts, float lamda, int max_iter,
@@ -889,30 +893,58 @@ __global__ __launch_bounds__(MS_THREADS) void k_meanshift(const FaceDesc* __rest
     }
     ax = ay = aw = 0;
     for (int k0 = 0; k0 < maxcnt; k0 += MS_TILE) {
-      for (int i = tid; i < MS_TILE * MS_FACES; i += MS_THREADS) {  // parallel phase
-        const int j = i % MS_TILE, p = i / MS_TILE, k = k0 + j;
-        float px = 0.f, py = 0.f, w = 0.f;
-        if (k < s_cnt[p] && s_live[p]) {
-          const Vote v = votes[s_vb[p] + k];
-          if (pass < 0) {
-            w = v.w;
-          } else {
-            const float dx = s_mx[p] - (float)v.x, dy = s_my[p] - (float)v.y;
-            float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
-            d = ffd_expf(-d / lamda);
-            w = v.w * d;
-          }
-          px = v.x * w;
-          py = v.y * w;
+      // parallel phase, in groups of MS_GRP items per thread whose vote loads are issued together
+      // (small groups: the kernel's occupancy is what hides the rest of the latency)
+      for (int i0 = tid; i0 < MS_TILE * MS_FACES; i0 += MS_GRP * MS_THREADS) {
+        Vote v[MS_GRP];
+#pragma unroll
+        for (int u = 0; u < MS_GRP; u++) {
+          const int i = i0 + u * MS_THREADS, j = i % MS_TILE, p = i / MS_TILE, k = k0 + j;
+          const bool use = i < MS_TILE * MS_FACES && k < s_cnt[p] && s_live[p];
+          v[u] = use ? votes[s_vb[p] + k] : Vote{0, 0, -1.f};  // w < 0: no vote (real weights are fg > 0.5)
         }
-        tx[j * MS_LD + p] = px;
-        ty[j * MS_LD + p] = py;
-        tw[j * MS_LD + p] = w;
+#pragma unroll
+        for (int u = 0; u < MS_GRP; u++) {
+          const int i = i0 + u * MS_THREADS, j = i % MS_TILE, p = i / MS_TILE;
+          if (i >= MS_TILE * MS_FACES) break;
+          float px = 0.f, py = 0.f, w = 0.f;
+          if (v[u].w >= 0.f) {
+            if (pass < 0) {
+              w = v[u].w;
+            } else {
+              const float dx = s_mx[p] - (float)v[u].x, dy = s_my[p] - (float)v[u].y;
+              float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
+              d = ffd_expf(-d / lamda);
+              w = v[u].w * d;
+            }
+            px = v[u].x * w;
+            py = v[u].y * w;
+          }
+          tx[j * MS_LD + p] = px;
+          ty[j * MS_LD + p] = py;
+          tw[j * MS_LD + p] = w;
+        }
       }
       __syncthreads();
       if (tid < MS_FACES && s_live[tid]) {  // serial phase, in list order
         const int lim = min(MS_TILE, s_cnt[tid] - k0);
-        for (int j = 0; j < lim; j++) {
+        int j = 0;
+        for (; j + 8 <= lim; j += 8) {  // LDS reads of 8 terms ahead of their in-order adds
+          float vx[8], vy[8], vw[8];
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            vx[q] = tx[(j + q) * MS_LD + tid];
+            vy[q] = ty[(j + q) * MS_LD + tid];
+            vw[q] = tw[(j + q) * MS_LD + tid];
+          }
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            ax += vx[q];
+            ay += vy[q];
+            aw += vw[q];
+          }
+        }
+        for (; j < lim; j++) {
           ax += tx[j * MS_LD + tid];
           ay += ty[j * MS_LD + tid];
           aw += tw[j * MS_LD + tid];
