@@ -834,7 +834,7 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
 //   serial phase:   lane p (one per face) adds its face's MS_TILE terms in list order,
 // so every running sum equals the reference's sequential float sum bit for bit.
 #ifndef FFD_MS_FACES
-#define FFD_MS_FACES 32
+#define FFD_MS_FACES 16
 #endif
 #ifndef FFD_MS_TILE
 #define FFD_MS_TILE 64
