@@ -19,7 +19,7 @@ MODEL     := model/ffd_model.bin
 EXAMPLE   := examples/build/analyze_face
 
 HIP_OBJS  := $(PKG)/lib/ffd_kernels.o $(PKG)/lib/ffd_engine.o
-HDRS      := include/ffd.h include/ffd_numerics.h include/ffd_model_format.h $(CSRC)/ffd_device.hpp \
+HDRS      := include/ffd.h include/ffd_numerics.h include/ffd_gabor.h include/ffd_model_format.h $(CSRC)/ffd_device.hpp \
              $(CSRC)/ffd_kernels.hpp $(CSRC)/model_io.hpp
 
 all: $(LIB) $(CONVERT) $(SYNTH) $(ORACLE) $(EXAMPLE)
@@ -43,7 +43,7 @@ $(CONVERT): $(CSRC)/ffd_convert.cpp $(CSRC)/model_io.hpp include/ffd_model_forma
 	@mkdir -p $(@D)
 	$(CXX) $(CXXFLAGS) -o $@ $<
 
-$(ORACLE): oracle/ffd_oracle.cpp oracle/ffd_oracle.h include/ffd_numerics.h include/ffd_model_format.h
+$(ORACLE): oracle/ffd_oracle.cpp oracle/ffd_oracle.h include/ffd_numerics.h include/ffd_gabor.h include/ffd_model_format.h
 	@mkdir -p $(@D)
 	$(CXX) $(CXXFLAGS) -shared -pthread -o $@ $<
 

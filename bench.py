@@ -28,22 +28,27 @@ FP32_PEAK_TFLOPS = 157.3     # MI355X FP32 vector = FP32 matrix peak (no dense M
 CROP = 150
 
 
-def gabor_flops_per_pixel(w):
+def gabor_flops_per_pixel(w, face_w=125):
     """FLOPs the restated Gabor correlation executes per output pixel for the 7 orientations of
-    one scale: 7x7 direct (mul + add per tap, re and im); >= 9x9 folded
-    pairs (S, D adds + 14 FMAs), centre FMAs; + magnitude (2 mul, add, sqrt) per orientation."""
+    one scale.  7x7: OpenCV's direct filter, mul + add per tap for re and im.
+    >= 9x9 (separable definition, include/ffd_gabor.h): V pass per padded column ((W + 2R) / W
+    of the pixels): per folded pair S, D + 9 FMAs, centre 9 FMAs; H pass per tap 25 FMAs
+    (DC, mu 0 and mu 4 one pair each, the other four orientations two pairs each), DC term 7 FMAs.
+    + magnitude (2 mul, add, sqrt) per orientation."""
     if w == 7:
         core = 49 * 7 * 2 * 2
     else:
-        pairs = (w * w - 1) // 2
-        core = pairs * (2 + 7 * 2 * 2) + 7 * 2
+        r = (w - 1) // 2
+        v = (r * (2 + 9 * 2) + 9 * 2) * (face_w + 2 * r) / face_w
+        core = v + w * 25 * 2 + 7 * 2
     return core + 7 * 4
 
 
 # profiler stage -> kernel name prefix in rocprofv3 traces (for the PMC traffic lookup)
 STAGE_KERNELS = {
-    "gray_resize": "ffd::k_gray_resize", "gabor_25x25": "void ffd::k_gabor<25>", "gabor_19x19": "void ffd::k_gabor<19>",
-    "gabor_13x13": "void ffd::k_gabor<13>", "gabor_9x9": "void ffd::k_gabor<9>", "gabor_7x7": "void ffd::k_gabor<7>",
+    "gray_resize": "ffd::k_gray_resize", "gabor_25x25": "void ffd::k_gabor_sep<25>",
+    "gabor_19x19": "void ffd::k_gabor_sep<19>", "gabor_13x13": "void ffd::k_gabor_sep<13>",
+    "gabor_9x9": "void ffd::k_gabor_sep<9>", "gabor_7x7": "ffd::k_gabor7",
     "integral_channels": "ffd::k_integral", "headpose_traverse": "void ffd::k_traverse<true",
     "headpose_reduce_select": "ffd::k_hp_pose", "ffd_traverse": "void ffd::k_traverse<false",
     "votes": "ffd::k_votes", "meanshift": "ffd::k_meanshift",
@@ -75,7 +80,7 @@ def stage_work(stage, n_faces, W=125, H=125, n_hp=576, n_mp=1024, trees=20):
     chan_bytes = 38 * (H + 1) * (W + 1) * 2
     if stage.startswith("gabor_"):
         w = int(stage.split("_")[1].split("x")[0])
-        return n_faces * W * H * gabor_flops_per_pixel(w) / 1e12, "TFLOP/s", "mfma"
+        return n_faces * W * H * gabor_flops_per_pixel(w, W) / 1e12, "TFLOP/s", "valu"
     if stage == "integral_channels":
         return n_faces * (35 * W * H * 4 + W * H + chan_bytes) / 1e9, "GB/s", "hbm"  # read mag+gray, write planes
     if stage == "headpose_traverse":

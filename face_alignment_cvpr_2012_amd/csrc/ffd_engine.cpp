@@ -24,6 +24,7 @@
 #include "../../include/ffd.h"
 #include "ffd_device.hpp"
 #include "ffd_kernels.hpp"
+#include "../../include/ffd_gabor.h"
 #include "model_io.hpp"
 
 #define FFD_VERSION_STR "ffd-mi355x 0.1.0 (gfx950)"
@@ -420,12 +421,15 @@ void ffd_engine::load_model(const std::string& path) {
   HIP_CHECK(hipStreamSynchronize(main_stream()));
 }
 
-// createKernel / initGaborKernels (FeatureChannelFactory.hpp:186-251), packed for k_gabor.
+// Gabor coefficients: scale 0 = createKernel / initGaborKernels (FeatureChannelFactory.hpp:186-251)
+// packed for k_gabor7; scales 1..4 = the separable factors of include/ffd_gabor.h packed for
+// k_gabor_sep (block layout in ffd_kernels.hip).
 void ffd_engine::build_gabor() {
   std::vector<float> coef(GABOR_COEF_TOTAL, 0.f);
   const double CV_PI = 3.1415926535897932384626433832795;
   const double sigma = 1.0 / 2.0 * CV_PI, dF = std::sqrt(2.0);
-  for (int iNu = 0; iNu <= 4; iNu++) {
+  {
+    const int iNu = 0;
     std::vector<std::vector<float>> re(7), im(7);
     int Wk = 0;
     for (int iMu = 0; iMu < 7; iMu++) {
@@ -450,20 +454,41 @@ void ffd_engine::build_gabor() {
           re[iMu][j * Wk + i] = (float)(dTemp1 * dTemp2);
           im[iMu][j * Wk + i] = (float)(dTemp1 * dTemp3);
         }
-      const int n = Wk * Wk;
-      for (int t = 0; t < n; t++)
-        if (re[iMu][t] != re[iMu][n - 1 - t] || im[iMu][t] != -im[iMu][n - 1 - t])
-          throw std::runtime_error("Gabor kernel not point-symmetric on this libm");
     }
-    const int OFF = GABOR_OFFS[iNu];
-    const int ntap = Wk == 7 ? 49 : (Wk * Wk - 1) / 2;  // taps (7x7) or folded pairs
-    for (int t = 0; t < ntap; t++)  // interleaved (re, im) per orientation: one packed operand each
+    for (int t = 0; t < 49; t++)  // interleaved (re, im) per orientation: one packed operand each
       for (int o = 0; o < 7; o++) {
-        coef[OFF + t * 16 + 2 * o] = re[o][t];
-        coef[OFF + t * 16 + 2 * o + 1] = im[o][t];
+        coef[GABOR_OFF0 + t * 16 + 2 * o] = re[o][t];
+        coef[GABOR_OFF0 + t * 16 + 2 * o + 1] = im[o][t];
       }
-    if (Wk != 7)
-      for (int o = 0; o < 7; o++) coef[OFF + ntap * 16 + 2 * o] = re[o][ntap];  // centre tap
+  }
+  for (int nu = 1; nu <= 4; nu++) {
+    ffd_gabor_sep s;
+    ffd_gabor_sep_init(nu, &s);
+    const int R = s.R;
+    if (2 * R + 1 != GABOR_WIDTHS[nu]) throw std::runtime_error("unexpected Gabor kernel width");
+    float* b = coef.data() + GABOR_OFFS[nu];
+    b[0] = s.c;
+    float* v = b + 4;
+    for (int t = 0; t <= R; t++) {
+      v[12 * t] = s.g[t];
+      for (int q = 0; q < 4; q++) {
+        v[12 * t + 2 + 2 * q] = s.vc[q][t];
+        v[12 * t + 3 + 2 * q] = s.vs[q][t];
+      }
+    }
+    float* h = b + 4 + 12 * (R + 1);
+    for (int t = -R; t <= R; t++) {
+      const int at = t < 0 ? -t : t;
+      auto hs = [&](int p) { return t < 0 ? -s.hs[p][at] : s.hs[p][at]; };
+      float* e = h + 20 * (t + R);
+      e[0] = s.hc[0][at]; e[1] = hs(0);
+      e[2] = s.g[at]; e[3] = s.g[at];
+      e[4] = s.hc[1][at]; e[5] = s.hc[1][at]; e[6] = -hs(1); e[7] = hs(1);
+      e[8] = s.hc[2][at]; e[9] = s.hc[2][at]; e[10] = -hs(2); e[11] = hs(2);
+      e[12] = hs(2); e[13] = -hs(2);
+      e[14] = s.hc[3][at]; e[15] = s.hc[3][at]; e[16] = -hs(3); e[17] = hs(3);
+      e[18] = hs(3); e[19] = -hs(3);
+    }
   }
   upload(gabor_coef, coef, main_stream());
   HIP_CHECK(hipStreamSynchronize(main_stream()));
@@ -509,7 +534,7 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   stage(0, st, [&] { launch_gray_resize(dfd, n, d_images, w.gray.as<uint8_t>(), st); });
   for (int nu = 4; nu >= 0; nu--)  // largest kernels first
     stage(1 + (4 - nu), st, [&] {
-      launch_gabor(nu, dfd, n, w.gray.as<uint8_t>(), gabor_coef.as<float4>(), w.mag.as<float>(),
+      launch_gabor(nu, dfd, n, w.gray.as<uint8_t>(), gabor_coef.as<float>(), w.mag.as<float>(),
                    w.chan.as<uint16_t>(), st);
     });
   stage(6, st, [&] {
@@ -878,7 +903,7 @@ ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t
     const FaceDesc* dfd = w.faces.as<FaceDesc>();
     launch_gray_resize(dfd, 1, e->scratch_a.as<uint8_t>(), w.gray.as<uint8_t>(), w.stream);
     for (int nu = 4; nu >= 0; nu--)
-      launch_gabor(nu, dfd, 1, w.gray.as<uint8_t>(), e->gabor_coef.as<float4>(), w.mag.as<float>(),
+      launch_gabor(nu, dfd, 1, w.gray.as<uint8_t>(), e->gabor_coef.as<float>(), w.mag.as<float>(),
                    w.chan.as<uint16_t>(), w.stream);
     launch_integral(dfd, 1, w.gray.as<uint8_t>(), w.chan.as<uint16_t>(), w.stream);
     HIP_CHECK(hipGetLastError());

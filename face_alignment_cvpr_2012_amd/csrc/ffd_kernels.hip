@@ -6,7 +6,7 @@
 //
 // Kernel map (reference -> kernel):
 //   cvtColor + ROI + resize      FaceForest.cpp:195-204              k_gray_resize
-//   Gabor filter2D + magnitude   FeatureChannelFactory.hpp:253-270   k_gabor<W>
+//   Gabor filter2D + magnitude   FeatureChannelFactory.hpp:253-270   k_gabor7, k_gabor_sep<W>
 //   normalize/convertTo/integral FeatureChannelFactory.hpp:271-286,  k_integral (+ gray, Sobel
 //                                46-57, 120-141                       channels fused in)
 //   Forest::evaluateMT           Forest.hpp:80-90, Tree.hpp:173-191,  k_traverse<HP/FFD>
@@ -166,7 +166,7 @@ __device__ __forceinline__ void integral_scan(uint16_t* __restrict__ out, int W,
 }
 
 // gray (channel 0) and the two Sobel channels (36 d/dy, 37 d/dx); the 35 Gabor channels are
-// integrated by k_gabor itself.  One 4-wave workgroup per face (the 4th wave idles).
+// integrated by the Gabor kernels themselves.  One 4-wave workgroup per face (the 4th wave idles).
 __global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ faces,
                                                   const uint8_t* __restrict__ gray,
                                                   uint16_t* __restrict__ chan) {
@@ -187,155 +187,21 @@ __global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ f
 }
 
 // ------------------------------------------------------------------ Gabor --
-// Coefficient table (host-built from createKernel, FeatureChannelFactory.hpp:186-251), 16 floats
-// per tap/pair: [re0..re6, 0, im0..im6, 0]:
-//   scale 0 (7x7): 49 taps in row-major order
-//   scale >= 1   : (W*W-1)/2 pairs in row-major order, then the centre [re0..re6, 0]
-// One 512-thread workgroup computes a 64x32 output tile of one face for the 7 orientations of
-// one scale from an LDS copy of the (reflect-101 padded) input tile; each thread owns 4
-// horizontally adjacent pixels, the (re, im) pairs accumulate in packed FMAs whose coefficient
-// operands are wave-uniform scalar loads (SGPR pairs).  The per-pixel operation order is
-// the restatement's (oracle/ffd_oracle.cpp gabor_mag): 7x7 = OpenCV's direct row-major mul+add;
-// larger = folded pairs S = a+b, D = a-b, fma in row-major pair order, then the centre.
-constexpr int GB_TX = 64, GB_TY = 32, GB_THREADS = 512;
-#ifndef GB_UNROLL
-#define GB_UNROLL 1
-#endif
-
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-template <int W> struct GaborCfg;
-template <> struct GaborCfg<7>  { static constexpr int nu = 0, off = GABOR_OFF0; };
-template <> struct GaborCfg<9>  { static constexpr int nu = 1, off = GABOR_OFF1; };
-template <> struct GaborCfg<13> { static constexpr int nu = 2, off = GABOR_OFF2; };
-template <> struct GaborCfg<19> { static constexpr int nu = 3, off = GABOR_OFF3; };
-template <> struct GaborCfg<25> { static constexpr int nu = 4, off = GABOR_OFF4; };
-
-template <int W>
-__global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict__ faces,
-                                                      const uint8_t* __restrict__ gray,
-                                                      const float4* __restrict__ coef_g,
-                                                      float* __restrict__ mag,
-                                                      uint16_t* __restrict__ chan) {
-  constexpr int R = (W - 1) / 2;
-  // row stride (floats) == 1 mod 4: the 4 rows a 32-lane group touches fall on disjoint banks
-  constexpr int LW = ((GB_TX + 2 * R + 3) / 4) * 4 + 1;
-  constexpr int LH = GB_TY + 2 * R;
-  constexpr int NU = GaborCfg<W>::nu, OFF = GaborCfg<W>::off;
-  __shared__ float tile[LH * LW];
-  __shared__ uint32_t red[8][14];
+// Face-wide min / max of one scale's 7 magnitude planes -> cv::normalize(NORM_MINMAX, 0, 1) +
+// convertTo(CV_8U, 255) (FeatureChannelFactory.hpp:271-286): quantise (v*scale + shift, *255,
+// cvRound, saturate) and integrate the 7 channels, one wave per channel, reading the magnitudes
+// back from L2.  mn / mx: this thread's minima of the magnitudes' bits and of their complements
+// (unsigned order == float order for m >= +0).  Every magnitude store of the workgroup precedes
+// the first barrier here.
+template <int NWV>
+__device__ __forceinline__ void gabor_normalise_integrate(const FaceDesc& fd, int nu, uint32_t (&mn)[7],
+                                                          uint32_t (&mx)[7], const float* __restrict__ mag,
+                                                          uint16_t* __restrict__ chan) {
+  __shared__ uint32_t red[NWV][14];
   __shared__ float s_sf[7], s_hf[7];
-  const FaceDesc fd = faces[blockIdx.x];
-  if (!fd.valid) return;
-  const int tiles_x = (fd.W + GB_TX - 1) / GB_TX, tiles = tiles_x * ((fd.H + GB_TY - 1) / GB_TY);
-  const uint8_t* g = gray + fd.gray_off;
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  // per-thread min / max of the face's magnitudes (max kept as min(~bits): unsigned order == float
-  // order for m >= +0), over all tiles of the face
-  uint32_t mn[7], mx[7];
-#pragma unroll
-  for (int o = 0; o < 7; o++) mn[o] = mx[o] = 0xFFFFFFFFu;
-#pragma unroll 1
-  for (int tl = 0; tl < tiles; tl++) {
-  const int tx0 = (tl % tiles_x) * GB_TX, ty0 = (tl / tiles_x) * GB_TY;
-  __syncthreads();  // the previous tile's reads of `tile` are done
-  for (int i = threadIdx.x; i < LH * (GB_TX + 2 * R); i += GB_THREADS) {
-    const int ly = i / (GB_TX + 2 * R), lx = i % (GB_TX + 2 * R);
-    const int y = reflect101(ty0 - R + ly, fd.H), x = reflect101(tx0 - R + lx, fd.W);
-    tile[ly * LW + lx] = (float)g[y * PITCH + x];
-  }
-  __syncthreads();
-  // wave w covers threads tx in [8*(w&1), +8) x ty in [8*(w>>1), +8); 4 px per thread
-  const int tx = (wv & 1) * 8 + (ln & 7), ty = (wv >> 1) * 8 + (ln >> 3);
-  // acc[k][o] = (re, im): one v_pk_fma_f32 / v_pk_mul+v_pk_add per (pixel, orientation), each
-  // half of which is exactly the scalar fmaf / mul+add of the restatement
-  f2 acc[4][7];
-#pragma unroll
-  for (int k = 0; k < 4; k++)
-#pragma unroll
-    for (int o = 0; o < 7; o++) acc[k][o] = f2{0.f, 0.f};
-  // centre pixel (ty, 4tx + k) sits at tile (ty + R, 4tx + R + k)
-  const float* ctr = &tile[(ty + R) * LW + 4 * tx + R];
-  // wave-uniform coefficients straight from global memory: scalar loads, SGPR-pair operands of
-  // the packed FMAs (no LDS traffic, no VGPRs)
-  const float4* cg = coef_g + OFF / 4;
-  auto load_coef = [&](int t, f2* c) {
-    const float4 c0 = cg[t * 4 + 0], c1 = cg[t * 4 + 1], c2 = cg[t * 4 + 2], c3 = cg[t * 4 + 3];
-    c[0] = f2{c0.x, c0.y}; c[1] = f2{c0.z, c0.w}; c[2] = f2{c1.x, c1.y}; c[3] = f2{c1.z, c1.w};
-    c[4] = f2{c2.x, c2.y}; c[5] = f2{c2.z, c2.w}; c[6] = f2{c3.x, c3.y};
-  };
-
-  // Kernel rows are an outer loop and the taps of a row an inner loop with per-tap pointer steps
-  // (two address adds per tap against 28 packed FMAs).
-  if constexpr (W == 7) {
-    // OpenCV Filter2D direct path: s = 0; s += k*p over taps in row-major order
-#pragma unroll 1
-    for (int r = 0; r < 7; r++) {
-      const float* prow = ctr + (r - 3) * LW;
-#pragma unroll GB_UNROLL
-      for (int dxi = 0; dxi < 7; dxi++) {
-        const float* pa = prow + (dxi - 3);
-        f2 c[7];
-        load_coef(r * 7 + dxi, c);
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const float p = pa[k];
-          const f2 pp = f2{p, p};
-#pragma unroll
-          for (int o = 0; o < 7; o++) acc[k][o] = acc[k][o] + c[o] * pp;
-        }
-      }
-    }
-  } else {
-    // folded pairs t = (dy + R) * W + (dx + R), rows dy = -R .. 0, row 0 only dx < 0
-    constexpr int HALF = (W * W - 1) / 2;
-    auto pair = [&](const float* pa, const float* pb, int t) {  // a(k) = pa[k], b(k) = pb[k]
-      f2 c[7];
-      load_coef(t, c);
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const float av = pa[k], bv = pb[k];
-        const f2 sd = f2{av, av} + f2{bv, -bv};  // (S, D) = (a + b, a - b)
-#pragma unroll
-        for (int o = 0; o < 7; o++) acc[k][o] = __builtin_elementwise_fma(c[o], sd, acc[k][o]);
-      }
-    };
-#pragma unroll 1
-    for (int r = 0; r < R; r++) {  // dy = r - R < 0: full rows
-      const float* rowa = ctr + (r - R) * LW;
-      const float* rowb = ctr - (r - R) * LW;
-#pragma unroll GB_UNROLL
-      for (int dxi = 0; dxi < W; dxi++) pair(rowa + (dxi - R), rowb - (dxi - R), r * W + dxi);
-    }
-#pragma unroll GB_UNROLL
-    for (int dxi = 0; dxi < R; dxi++) pair(ctr + (dxi - R), ctr - (dxi - R), R * W + dxi);  // dy = 0
-    const float4 c0 = cg[HALF * 4 + 0], c1 = cg[HALF * 4 + 1], c2 = cg[HALF * 4 + 2], c3 = cg[HALF * 4 + 3];
-    const float kr[7] = {c0.x, c0.z, c1.x, c1.z, c2.x, c2.z, c3.x};
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const float p0 = ctr[k];
-#pragma unroll
-      for (int o = 0; o < 7; o++) acc[k][o].x = fmaf(kr[o], p0, acc[k][o].x);
-    }
-  }
-  const int x0 = tx0 + 4 * tx, y = ty0 + ty;
-#pragma unroll
-  for (int o = 0; o < 7; o++) {
-    float m4[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const float i2 = acc[k][o].y * acc[k][o].y, r2 = acc[k][o].x * acc[k][o].x;
-      m4[k] = __builtin_sqrtf(i2 + r2);
-      const bool in = (x0 + k) < fd.W && y < fd.H;
-      const uint32_t bits = __float_as_uint(m4[k]);
-      if (in) { mn[o] = min(mn[o], bits); mx[o] = min(mx[o], ~bits); }
-    }
-    if (y < fd.H)  // columns >= W land in the row's pitch padding, never read
-      *reinterpret_cast<float4*>(&mag[fd.mag_off + ((int64_t)(NU * 7 + o) * fd.H + y) * PITCH + x0]) =
-          make_float4(m4[0], m4[1], m4[2], m4[3]);
-  }
-  }  // tiles
-  // face-wide min / max -> cv::normalize(NORM_MINMAX, 0, 1) + convertTo scale / shift (OpenCV 2.4.9)
 #pragma unroll
   for (int o = 0; o < 7; o++) {
 #pragma unroll
@@ -348,11 +214,11 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
 #pragma unroll
     for (int o = 0; o < 7; o++) { red[wv][o] = mn[o]; red[wv][7 + o] = mx[o]; }
   }
-  __syncthreads();  // also: every magnitude store of the workgroup is visible to it
+  __syncthreads();
   if (threadIdx.x < 7) {
     const int o = threadIdx.x;
     uint32_t a = red[0][o], b = red[0][7 + o];
-    for (int w = 1; w < GB_THREADS / 64; w++) { a = min(a, red[w][o]); b = min(b, red[w][7 + o]); }
+    for (int w = 1; w < NWV; w++) { a = min(a, red[w][o]); b = min(b, red[w][7 + o]); }
     const double smin = (double)__uint_as_float(a), smax = (double)__uint_as_float(~b);
     const double dmin = 0, dmax = 1;
     const double scale = (dmax - dmin) * (smax - smin > 2.220446049250313e-16 ? 1. / (smax - smin) : 0);
@@ -361,13 +227,11 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
     s_hf[o] = (float)shift;
   }
   __syncthreads();
-  // FeatureChannelFactory.hpp:271-286: quantise (v*scale + shift, *255, cvRound, saturate) and
-  // integrate the 7 channels, one wave each, reading the magnitudes back from L2
-  if (wv < 7) {
-    const int o = wv, lane = ln, x0 = 2 * lane, FW = fd.W, FH = fd.H;
+  for (int o = wv; o < 7; o += NWV) {
+    const int lane = ln, x0 = 2 * lane, FW = fd.W, FH = fd.H;
     const float sf = s_sf[o], hf = s_hf[o];
-    const float* m = mag + fd.mag_off + (int64_t)(NU * 7 + o) * FH * PITCH;
-    integral_scan(chan + fd.ch_off + (int64_t)(1 + NU * 7 + o) * fd.plane, FW, FH, lane,
+    const float* m = mag + fd.mag_off + (int64_t)(nu * 7 + o) * FH * PITCH;
+    integral_scan(chan + fd.ch_off + (int64_t)(1 + nu * 7 + o) * fd.plane, FW, FH, lane,
                   [&](int y0, uint32_t* v0, uint32_t* v1) {
                     float2 mv[8];
 #pragma unroll
@@ -381,6 +245,301 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor(const FaceDesc* __restrict
                     }
                   });
   }
+}
+
+__device__ __forceinline__ void minmax_update(uint32_t& mn, uint32_t& mx, float m, bool in) {
+  const uint32_t bits = __float_as_uint(m);
+  if (in) { mn = min(mn, bits); mx = min(mx, ~bits); }
+}
+
+// 7x7 (scale 0): OpenCV 2.4.9's direct Filter2D (49 taps < dft_filter_size 50), restated bit-exactly.
+// Coefficients (host-built from createKernel, FeatureChannelFactory.hpp:186-251), 16 floats per tap
+// in row-major order: [re0, im0, re1, im1, ..., re6, im6, 0, 0].
+// One 512-thread workgroup computes 64x32 output tiles of one face for the 7 orientations from an
+// LDS copy of the (reflect-101 padded) input tile; each thread owns 4 horizontally adjacent pixels,
+// the (re, im) pairs accumulate as packed mul + add (s = 0; s += k*p, no FMA) whose coefficient
+// operands are wave-uniform scalar loads (SGPR pairs).
+constexpr int GB_TX = 64, GB_TY = 32, GB_THREADS = 512;
+
+__global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restrict__ faces,
+                                                       const uint8_t* __restrict__ gray,
+                                                       const float4* __restrict__ coef_g,
+                                                       float* __restrict__ mag,
+                                                       uint16_t* __restrict__ chan) {
+  constexpr int R = 3;
+  // row stride (floats) == 1 mod 4: the 4 rows a 32-lane group touches fall on disjoint banks
+  constexpr int LW = ((GB_TX + 2 * R + 3) / 4) * 4 + 1;
+  constexpr int LH = GB_TY + 2 * R;
+  __shared__ float tile[LH * LW];
+  const FaceDesc fd = faces[blockIdx.x];
+  if (!fd.valid) return;
+  const int tiles_x = (fd.W + GB_TX - 1) / GB_TX, tiles = tiles_x * ((fd.H + GB_TY - 1) / GB_TY);
+  const uint8_t* g = gray + fd.gray_off;
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  uint32_t mn[7], mx[7];
+#pragma unroll
+  for (int o = 0; o < 7; o++) mn[o] = mx[o] = 0xFFFFFFFFu;
+#pragma unroll 1
+  for (int tl = 0; tl < tiles; tl++) {
+    const int tx0 = (tl % tiles_x) * GB_TX, ty0 = (tl / tiles_x) * GB_TY;
+    __syncthreads();  // the previous tile's reads of `tile` are done
+    for (int i = threadIdx.x; i < LH * (GB_TX + 2 * R); i += GB_THREADS) {
+      const int ly = i / (GB_TX + 2 * R), lx = i % (GB_TX + 2 * R);
+      const int y = reflect101(ty0 - R + ly, fd.H), x = reflect101(tx0 - R + lx, fd.W);
+      tile[ly * LW + lx] = (float)g[y * PITCH + x];
+    }
+    __syncthreads();
+    // wave w covers threads tx in [8*(w&1), +8) x ty in [8*(w>>1), +8); 4 px per thread
+    const int tx = (wv & 1) * 8 + (ln & 7), ty = (wv >> 1) * 8 + (ln >> 3);
+    // acc[k][o] = (re, im): one v_pk_mul + v_pk_add per (pixel, orientation), each half of
+    // which is exactly the scalar mul + add of the restatement
+    f2 acc[4][7];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int o = 0; o < 7; o++) acc[k][o] = f2{0.f, 0.f};
+    // centre pixel (ty, 4tx + k) sits at tile (ty + R, 4tx + R + k)
+    const float* ctr = &tile[(ty + R) * LW + 4 * tx + R];
+#pragma unroll 1
+    for (int r = 0; r < 7; r++) {
+      const float* prow = ctr + (r - 3) * LW;
+#pragma unroll 1
+      for (int dxi = 0; dxi < 7; dxi++) {
+        const float* pa = prow + (dxi - 3);
+        const int t = r * 7 + dxi;
+        const float4 c0 = coef_g[t * 4 + 0], c1 = coef_g[t * 4 + 1], c2 = coef_g[t * 4 + 2], c3 = coef_g[t * 4 + 3];
+        const f2 c[7] = {f2{c0.x, c0.y}, f2{c0.z, c0.w}, f2{c1.x, c1.y}, f2{c1.z, c1.w},
+                         f2{c2.x, c2.y}, f2{c2.z, c2.w}, f2{c3.x, c3.y}};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const float p = pa[k];
+          const f2 pp = f2{p, p};
+#pragma unroll
+          for (int o = 0; o < 7; o++) acc[k][o] = acc[k][o] + c[o] * pp;
+        }
+      }
+    }
+    const int x0 = tx0 + 4 * tx, y = ty0 + ty;
+#pragma unroll
+    for (int o = 0; o < 7; o++) {
+      float m4[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const float i2 = acc[k][o].y * acc[k][o].y, r2 = acc[k][o].x * acc[k][o].x;
+        m4[k] = __builtin_sqrtf(i2 + r2);
+        minmax_update(mn[o], mx[o], m4[k], (x0 + k) < fd.W && y < fd.H);
+      }
+      if (y < fd.H)  // columns >= W land in the row's pitch padding, never read
+        *reinterpret_cast<float4*>(&mag[fd.mag_off + ((int64_t)o * fd.H + y) * PITCH + x0]) =
+            make_float4(m4[0], m4[1], m4[2], m4[3]);
+    }
+  }
+  gabor_normalise_integrate<GB_THREADS / 64>(fd, 0, mn, mx, mag, chan);
+}
+
+// Scales 1..4 (9x9 .. 25x25): the separable definition of include/ffd_gabor.h, in the operation
+// order of oracle/ffd_oracle.cpp gabor_sep_mag.  One 256-thread workgroup per face walks bands of
+// GS_BY output rows:
+//   stage   the band's gray rows [y0-R, y0+BY+R) x padded columns [-R, W+R) (reflect-101) as floats;
+//   V pass  per (row, padded column): Vg and (Vc_q, Vs_q), q = 1..4 (folded taps, packed FMAs);
+//   H pass  per (row, 4 adjacent columns): the 7 orientations' (re, im) as packed FMAs over the
+//           V planes (taps -R..R), the DC term, magnitudes to HBM, running min / max.
+// V planes sit in LDS "quad-split": padded column cc at (cc & 3) * QS + (cc >> 2), so the 32 lanes
+// of an H-pass row reading column 4*cq + u hit 32 consecutive words (conflict-free ds_read_b64).
+// Coefficient block (floats, host-built by ffd_engine build_gabor from ffd_gabor_sep):
+//   [0]                 c
+//   V_OFF + 12 t        t = 0..R: g, 0, (vc_q, vs_q) q = 1..4, 0, 0
+//   H_OFF + 20 (t + R)  t = -R..R: (hc0, hs0), (g, g), mu1 (hc1, hc1, -hs1, hs1), mu2 (hc2, hc2, -hs2, hs2),
+//                       mu6 (hs2, -hs2), mu3 (hc3, hc3, -hs3, hs3), mu5 (hs3, -hs3)    [hs_p(t) odd in t]
+constexpr int GS_THREADS = 256, GS_BY = 8;
+
+template <int R> struct GSep {
+  static constexpr int GP = (PITCH + 2 * R + 3) / 4 * 4;  // gray band row pitch (floats)
+  static constexpr int BR = GS_BY + 2 * R;                // gray band rows
+  static constexpr int QS = 32 + ((3 + 2 * R) >> 2);      // quad-split slots per phase
+  static constexpr int VP = 4 * QS;                       // V row pitch (elements) >= W + 2R
+  static constexpr int SC = GP;                           // staging / V-pass column range
+  static constexpr int V_OFF = 4, H_OFF = 4 + 12 * (R + 1);
+};
+
+template <int W>
+__global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __restrict__ faces,
+                                                          const uint8_t* __restrict__ gray,
+                                                          const float* __restrict__ coef,
+                                                          float* __restrict__ mag,
+                                                          uint16_t* __restrict__ chan) {
+  constexpr int R = (W - 1) / 2;
+  using C = GSep<R>;
+  constexpr int NU = W == 9 ? 1 : W == 13 ? 2 : W == 19 ? 3 : 4;
+  __shared__ float gt[C::BR * C::GP];
+  __shared__ float vg[GS_BY * C::VP];
+  __shared__ f2 vq[4][GS_BY * C::VP];
+  const FaceDesc fd = faces[blockIdx.x];
+  if (!fd.valid) return;
+  const int FW = fd.W, FH = fd.H, NPC = FW + 2 * R;
+  const uint8_t* g = gray + fd.gray_off;
+  const float* cv = coef + C::V_OFF;
+  const float* chh = coef + C::H_OFF;
+  const float cdc = coef[0];
+  const int tid = threadIdx.x;
+  uint32_t mn[7], mx[7];
+#pragma unroll
+  for (int o = 0; o < 7; o++) mn[o] = mx[o] = 0xFFFFFFFFu;
+
+  auto stage = [&](int y0) {  // (row, column quad) items, float4 LDS stores
+    constexpr int NQ = C::GP / 4;
+    for (int i = tid; i < C::BR * NQ; i += GS_THREADS) {
+      const int r = i / NQ, j = i - r * NQ;
+      const uint8_t* row = g + reflect101(y0 - R + r, FH) * PITCH;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        int x = 4 * j + e - R;
+        x = x < 0 ? -x : x;
+        x = x >= FW ? 2 * FW - 2 - x : x;
+        x = min(max(x, 0), FW - 1);  // columns past W + R (never used) stay in the row
+        v[e] = (float)row[x];
+      }
+      *reinterpret_cast<float4*>(&gt[r * C::GP + 4 * j]) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  };
+
+  stage(0);
+#pragma unroll 1
+  for (int y0 = 0; y0 < FH; y0 += GS_BY) {
+    __syncthreads();  // the band's gray rows are staged; the previous H pass is done with vg / vq
+    // ---- V pass
+#pragma unroll 1
+    for (int i = tid; i < GS_BY * C::SC; i += GS_THREADS) {
+      const int r = i / C::SC, cc = i - r * C::SC;
+      if (cc >= NPC) continue;
+      const float* col = &gt[(r + R) * C::GP + cc];
+      float vgv = 0.f;
+      f2 vqv[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) vqv[q] = f2{0.f, 0.f};
+#pragma unroll
+      for (int t = R; t >= 1; t--) {
+        const float a = col[t * C::GP], b = col[-t * C::GP];
+        const f2 sd = f2{a, a} + f2{b, -b};  // (S, D) = (a + b, a - b), exact
+        const float* c = cv + 12 * t;
+        vgv = fmaf(c[0], sd.x, vgv);
+#pragma unroll
+        for (int q = 0; q < 4; q++) vqv[q] = __builtin_elementwise_fma(f2{c[2 + 2 * q], c[3 + 2 * q]}, sd, vqv[q]);
+      }
+      const float p0 = col[0];
+      vgv = fmaf(cv[0], p0, vgv);
+#pragma unroll
+      for (int q = 0; q < 4; q++) vqv[q] = __builtin_elementwise_fma(f2{cv[2 + 2 * q], cv[3 + 2 * q]}, f2{p0, p0}, vqv[q]);
+      const int qi = r * C::VP + (cc & 3) * C::QS + (cc >> 2);
+      vg[qi] = vgv;
+#pragma unroll
+      for (int q = 0; q < 4; q++) vq[q][qi] = vqv[q];
+    }
+    __syncthreads();  // V planes ready; the gray band is free
+    if (y0 + GS_BY < FH) stage(y0 + GS_BY);
+    // ---- H pass: thread = (row hr, column quad cq), outputs x = 4 cq + k
+    const int hr = tid >> 5, cq = tid & 31, y = y0 + hr, x0 = 4 * cq;
+    f2 acc[4][7];
+    float dc[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      dc[k] = 0.f;
+#pragma unroll
+      for (int o = 0; o < 7; o++) acc[k][o] = f2{0.f, 0.f};
+    }
+    const int rb = hr * C::VP + cq;
+    // V value at padded column x0 + u + R: quad-split slot (u + R) & 3, offset (u + R) >> 2
+#define GS_IDX(u) (rb + (((u) + R) & 3) * C::QS + (((u) + R) >> 2))
+    // Vg: DC term and mu 0
+#pragma unroll
+    for (int u = -R; u <= R + 3; u++) {
+      const float v = vg[GS_IDX(u)];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int t = u - k;
+        if (t < -R || t > R) continue;
+        const float* h = chh + 20 * (t + R);
+        dc[k] = fmaf(h[2], v, dc[k]);
+        acc[k][0] = __builtin_elementwise_fma(f2{h[0], h[1]}, f2{v, v}, acc[k][0]);
+      }
+    }
+    // q = 4: mu 4
+#pragma unroll
+    for (int u = -R; u <= R + 3; u++) {
+      const f2 v = vq[3][GS_IDX(u)];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int t = u - k;
+        if (t < -R || t > R) continue;
+        const float* h = chh + 20 * (t + R);
+        acc[k][4] = __builtin_elementwise_fma(f2{h[2], h[3]}, v, acc[k][4]);
+      }
+    }
+    // q = 1: mu 1
+#pragma unroll
+    for (int u = -R; u <= R + 3; u++) {
+      const f2 v = vq[0][GS_IDX(u)], vs = f2{v.y, v.x};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int t = u - k;
+        if (t < -R || t > R) continue;
+        const float* h = chh + 20 * (t + R);
+        acc[k][1] = __builtin_elementwise_fma(f2{h[4], h[5]}, v, acc[k][1]);
+        acc[k][1] = __builtin_elementwise_fma(f2{h[6], h[7]}, vs, acc[k][1]);
+      }
+    }
+    // q = 2: mu 2, mu 6
+#pragma unroll
+    for (int u = -R; u <= R + 3; u++) {
+      const f2 v = vq[1][GS_IDX(u)], vs = f2{v.y, v.x};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int t = u - k;
+        if (t < -R || t > R) continue;
+        const float* h = chh + 20 * (t + R);
+        const f2 hc = f2{h[8], h[9]};
+        acc[k][2] = __builtin_elementwise_fma(hc, v, acc[k][2]);
+        acc[k][2] = __builtin_elementwise_fma(f2{h[10], h[11]}, vs, acc[k][2]);
+        acc[k][6] = __builtin_elementwise_fma(hc, v, acc[k][6]);
+        acc[k][6] = __builtin_elementwise_fma(f2{h[12], h[13]}, vs, acc[k][6]);
+      }
+    }
+    // q = 3: mu 3, mu 5
+#pragma unroll
+    for (int u = -R; u <= R + 3; u++) {
+      const f2 v = vq[2][GS_IDX(u)], vs = f2{v.y, v.x};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int t = u - k;
+        if (t < -R || t > R) continue;
+        const float* h = chh + 20 * (t + R);
+        const f2 hc = f2{h[14], h[15]};
+        acc[k][3] = __builtin_elementwise_fma(hc, v, acc[k][3]);
+        acc[k][3] = __builtin_elementwise_fma(f2{h[16], h[17]}, vs, acc[k][3]);
+        acc[k][5] = __builtin_elementwise_fma(hc, v, acc[k][5]);
+        acc[k][5] = __builtin_elementwise_fma(f2{h[18], h[19]}, vs, acc[k][5]);
+      }
+    }
+#undef GS_IDX
+    if (y < FH) {
+#pragma unroll
+      for (int o = 0; o < 7; o++) {
+        float m4[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const float re = fmaf(-cdc, dc[k], acc[k][o].x), im = acc[k][o].y;
+          const float i2 = im * im, r2 = re * re;
+          m4[k] = __builtin_sqrtf(i2 + r2);
+          minmax_update(mn[o], mx[o], m4[k], x0 + k < FW);
+        }
+        // columns >= W land in the row's pitch padding, never read
+        *reinterpret_cast<float4*>(&mag[fd.mag_off + ((int64_t)(NU * 7 + o) * FH + y) * PITCH + x0]) =
+            make_float4(m4[0], m4[1], m4[2], m4[3]);
+      }
+    }
+  }
+  gabor_normalise_integrate<GS_THREADS / 64>(fd, NU, mn, mx, mag, chan);
 }
 
 // --------------------------------------------------------------- traversal --
@@ -986,15 +1145,16 @@ void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uin
   k_gray_resize<<<n, 256, 0, s>>>(faces, images, gray);
 }
 
-void launch_gabor(int nu, const FaceDesc* faces, int n, const uint8_t* gray, const float4* coef, float* mag,
+void launch_gabor(int nu, const FaceDesc* faces, int n, const uint8_t* gray, const float* coef, float* mag,
                   uint16_t* chan, hipStream_t s) {
   if (n <= 0) return;
+  const float* c = coef + GABOR_OFFS[nu];
   switch (nu) {
-    case 4: k_gabor<25><<<n, GB_THREADS, 0, s>>>(faces, gray, coef, mag, chan); break;
-    case 3: k_gabor<19><<<n, GB_THREADS, 0, s>>>(faces, gray, coef, mag, chan); break;
-    case 2: k_gabor<13><<<n, GB_THREADS, 0, s>>>(faces, gray, coef, mag, chan); break;
-    case 1: k_gabor<9><<<n, GB_THREADS, 0, s>>>(faces, gray, coef, mag, chan); break;
-    default: k_gabor<7><<<n, GB_THREADS, 0, s>>>(faces, gray, coef, mag, chan); break;
+    case 4: k_gabor_sep<25><<<n, GS_THREADS, 0, s>>>(faces, gray, c, mag, chan); break;
+    case 3: k_gabor_sep<19><<<n, GS_THREADS, 0, s>>>(faces, gray, c, mag, chan); break;
+    case 2: k_gabor_sep<13><<<n, GS_THREADS, 0, s>>>(faces, gray, c, mag, chan); break;
+    case 1: k_gabor_sep<9><<<n, GS_THREADS, 0, s>>>(faces, gray, c, mag, chan); break;
+    default: k_gabor7<<<n, GB_THREADS, 0, s>>>(faces, gray, reinterpret_cast<const float4*>(c), mag, chan); break;
   }
 }
 

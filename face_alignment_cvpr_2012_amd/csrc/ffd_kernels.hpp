@@ -9,22 +9,23 @@
 
 namespace ffd {
 
-// Gabor coefficient table layout (see k_gabor): 16 floats per tap / pair (+ centre for W >= 9):
-// [re0, im0, re1, im1, ..., re6, im6, 0, 0].
+// Gabor coefficient table (floats): scale 0 (7x7, k_gabor7) = 49 taps x 16 floats
+// [re0, im0, ..., re6, im6, 0, 0]; scales 1..4 = the separable factor blocks of k_gabor_sep
+// (layout in ffd_kernels.hip), each 16-B aligned.
 constexpr int GABOR_WIDTHS[5] = {7, 9, 13, 19, 25};
-constexpr int gabor_block(int w) { return w == 7 ? 49 * 16 : ((w * w - 1) / 2 + 1) * 16; }
+constexpr int gabor_sep_block(int R) { return (4 + 12 * (R + 1) + 20 * (2 * R + 1) + 3) / 4 * 4; }
 constexpr int GABOR_OFF0 = 0;
-constexpr int GABOR_OFF1 = GABOR_OFF0 + gabor_block(7);
-constexpr int GABOR_OFF2 = GABOR_OFF1 + gabor_block(9);
-constexpr int GABOR_OFF3 = GABOR_OFF2 + gabor_block(13);
-constexpr int GABOR_OFF4 = GABOR_OFF3 + gabor_block(19);
-constexpr int GABOR_COEF_TOTAL = GABOR_OFF4 + gabor_block(25);
+constexpr int GABOR_OFF1 = GABOR_OFF0 + 49 * 16;
+constexpr int GABOR_OFF2 = GABOR_OFF1 + gabor_sep_block(4);
+constexpr int GABOR_OFF3 = GABOR_OFF2 + gabor_sep_block(6);
+constexpr int GABOR_OFF4 = GABOR_OFF3 + gabor_sep_block(9);
+constexpr int GABOR_COEF_TOTAL = GABOR_OFF4 + gabor_sep_block(12);
 constexpr int GABOR_OFFS[5] = {GABOR_OFF0, GABOR_OFF1, GABOR_OFF2, GABOR_OFF3, GABOR_OFF4};
 
 void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s);
 // Gabor scale nu (0..4): magnitudes of the 7 orientations, face-wide min-max normalisation,
 // quantisation and integration of the 7 channels (one workgroup per face)
-void launch_gabor(int nu, const FaceDesc* faces, int n, const uint8_t* gray, const float4* coef, float* mag,
+void launch_gabor(int nu, const FaceDesc* faces, int n, const uint8_t* gray, const float* coef, float* mag,
                   uint16_t* chan, hipStream_t s);
 // integral channels 0 (gray), 36, 37 (Sobel)
 void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t* chan, hipStream_t s);

@@ -30,6 +30,7 @@
 //   include/FaceForest.hpp:34-58, include/Constants.hpp:24-30,65-68  options/constants
 //   include/ThreadPool.hpp:24-64         per-call pools (CPU-baseline shape)
 #include "ffd_oracle.h"
+#include "ffd_gabor.h"
 
 #include <algorithm>
 #include <atomic>
@@ -354,17 +355,92 @@ void init_gabor() {
     }
 }
 
+// Separable factors of scales nu = 1..4 (include/ffd_gabor.h).
+const ffd_gabor_sep& gabor_sep(int nu) {
+  static ffd_gabor_sep tab[5];
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (int v = 1; v <= 4; v++) ffd_gabor_sep_init(v, &tab[v]);
+  });
+  return tab[nu];
+}
+
+// >= 9x9 kernels (DEFINED, see include/ffd_gabor.h): the exact separable factorisation.
+//  V pass (down each column, reflect-101 rows), for t = R..1 then the centre:
+//    S = p(y+t) + p(y-t), D = p(y+t) - p(y-t) (exact);  Vg = fma(g_t, S, Vg);
+//    Vc = fma(vc_qt, S, Vc);  Vs = fma(vs_qt, D, Vs);  centre: the same fmas with p(y) (vs_q0 = 0).
+//  H pass (along each row, reflect-101 columns), taps t = -R..R in order, hs(-t) = -hs(t):
+//    Dc = fma(g_|t|, Vg, Dc);
+//    mu 0 (b = 0):  re = fma(hc_0t, Vg, re);  im = fma(hs_0t, Vg, im)
+//    mu 4 (a = 0):  re = fma(g_|t|, Vc, re); im = fma(g_|t|, Vs, im)
+//    other mu, hsv = sgn * hs_pt:  re = fma(hc_pt, Vc, re); im = fma(hc_pt, Vs, im);
+//                                  re = fma(-hsv, Vs, re);  im = fma(hsv, Vc, im)
+//  then re = fma(-c, Dc, re)   (the reference kernel's DC term -c g(x) g(y)).
+void gabor_sep_mag(const uint8_t* img, int w, int h, int index, float* mag) {
+  const int nu = index / 7, mu = index % 7;
+  const ffd_gabor_sep& s = gabor_sep(nu);
+  const int R = s.R, p = FFD_GABOR_P[mu], q = FFD_GABOR_Q[mu];
+  const float sgn = (float)FFD_GABOR_SGN[mu];
+  std::vector<float> Vg((size_t)w * h), Vc((size_t)w * h), Vs((size_t)w * h);
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      auto P = [&](int yy) { return (float)img[reflect101(yy, h) * w + x]; };
+      float g = 0.f, c = 0.f, sv = 0.f;
+      const float* vc = q > 0 ? s.vc[q - 1] : s.g;
+      const float* vs = q > 0 ? s.vs[q - 1] : s.g;
+      for (int t = R; t >= 1; t--) {
+        const float a = P(y + t), b = P(y - t), S = a + b, D = a - b;
+        g = std::fmaf(s.g[t], S, g);
+        c = std::fmaf(vc[t], S, c);
+        sv = std::fmaf(vs[t], D, sv);
+      }
+      const float p0 = P(y);
+      g = std::fmaf(s.g[0], p0, g);
+      c = std::fmaf(vc[0], p0, c);
+      sv = std::fmaf(vs[0], p0, sv);
+      Vg[(size_t)y * w + x] = g;
+      Vc[(size_t)y * w + x] = c;   // q = 0: unused
+      Vs[(size_t)y * w + x] = sv;  // q = 0: unused
+    }
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      float re = 0.f, im = 0.f, dc = 0.f;
+      for (int t = -R; t <= R; t++) {
+        const size_t i = (size_t)y * w + reflect101(x + t, w);
+        const int at = t < 0 ? -t : t;
+        const float gv = Vg[i];
+        dc = std::fmaf(s.g[at], gv, dc);
+        if (mu == 0) {
+          const float hs = t < 0 ? -s.hs[0][at] : s.hs[0][at];
+          re = std::fmaf(s.hc[0][at], gv, re);
+          im = std::fmaf(hs, gv, im);
+        } else if (mu == 4) {
+          re = std::fmaf(s.g[at], Vc[i], re);
+          im = std::fmaf(s.g[at], Vs[i], im);
+        } else {
+          const float hc = s.hc[p][at], hsv = sgn * (t < 0 ? -s.hs[p][at] : s.hs[p][at]);
+          re = std::fmaf(hc, Vc[i], re);
+          im = std::fmaf(hc, Vs[i], im);
+          re = std::fmaf(-hsv, Vs[i], re);
+          im = std::fmaf(hsv, Vc[i], im);
+        }
+      }
+      re = std::fmaf(-s.c, dc, re);
+      const float r2 = re * re, i2 = im * im;
+      mag[(size_t)y * w + x] = std::sqrt(i2 + r2);
+    }
+}
+
 // One Gabor magnitude plane (gaborTransform, FeatureChannelFactory.hpp:253-286).
 //  * 7x7 kernels (49 taps < OpenCV's dft_filter_size 50): OpenCV's direct
 //    Filter2D, row-major taps, s = 0; s += k*p (no FMA) — bit-exact restatement.
 //  * >= 9x9 kernels: OpenCV 2.4.9 switches to a DFT (crossCorr) whose rounding
-//    cannot be reproduced; the restatement DEFINES the correlation as the
-//    point-symmetric folded sum: for the first (W*W-1)/2 taps t in row-major
-//    order, S = p(+t)+p(-t), D = p(+t)-p(-t) (exact), re = fma(kre_t, S, re),
-//    im = fma(kim_t, D, im); then re = fma(kre_centre, p(0), re).
+//    cannot be reproduced; the restatement DEFINES the correlation by the exact
+//    separable factorisation of the kernel, gabor_sep_mag above.
 void gabor_mag(const uint8_t* img, int w, int h, int index, float* mag) {
   const GaborKernel& g = g_gabor[index];
-  int W = g.width, R = (W - 1) / 2, n = W * W, half = (n - 1) / 2;
+  if (g.width != 7) return gabor_sep_mag(img, w, h, index, mag);
+  const int W = 7, R = 3;
   std::vector<int> rx(w + 2 * R), ry(h + 2 * R);
   for (int i = 0; i < w + 2 * R; i++) rx[i] = reflect101(i - R, w);
   for (int i = 0; i < h + 2 * R; i++) ry[i] = reflect101(i - R, h);
@@ -372,22 +448,12 @@ void gabor_mag(const uint8_t* img, int w, int h, int index, float* mag) {
   for (int py = 0; py < h; py++)
     for (int px = 0; px < w; px++) {
       float re = 0.f, im = 0.f;
-      if (W == 7) {
-        for (int r = 0; r < W; r++)
-          for (int c = 0; c < W; c++) {
-            float p = P(py + r - R, px + c - R);
-            re = re + g.re[r * W + c] * p;
-            im = im + g.im[r * W + c] * p;
-          }
-      } else {
-        for (int t = 0; t < half; t++) {
-          int dy = t / W - R, dx = t % W - R;
-          float a = P(py + dy, px + dx), b = P(py - dy, px - dx);
-          re = std::fmaf(g.re[t], a + b, re);
-          im = std::fmaf(g.im[t], a - b, im);
+      for (int r = 0; r < W; r++)
+        for (int c = 0; c < W; c++) {
+          float p = P(py + r - R, px + c - R);
+          re = re + g.re[r * W + c] * p;
+          im = im + g.im[r * W + c] * p;
         }
-        re = std::fmaf(g.re[half], P(py, px), re);
-      }
       // pow(r,2), pow(i,2), add(i,r), pow(.,0.5) == sqrt
       float r2 = re * re, i2 = im * im;
       mag[py * w + px] = std::sqrt(i2 + r2);
