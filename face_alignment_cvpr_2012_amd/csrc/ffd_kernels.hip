@@ -605,6 +605,9 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 #ifndef FFD_TRAV_WALKS
 #define FFD_TRAV_WALKS 1
 #endif
+#ifndef FFD_TRAV_PAIR
+#define FFD_TRAV_PAIR 1  // 1: request both children before the split test; 0: only the chosen one after it
+#endif
 constexpr int TRAV_NT = 1024, TRAV_NW = FFD_TRAV_NW, TRAV_NS = TRAV_NT - TRAV_NW;
 constexpr int TRAV_U = (20480 + TRAV_NS - 1) / TRAV_NS;  // 8-byte window chunks held in registers per staging thread
 
@@ -671,7 +674,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   // the face's integral image are never referenced by a patch)
   v2u st[U];
   auto prefetch = [&](const Blk& B) {
-    if (tid < NW || !B.ok) return;
+    if (!B.ok) return;
     const FaceDesc& fd = A.faces[B.f];
     // the resource must be wave-uniform (SGPRs): read it from the first lane explicitly
     const uint64_t base = (uint64_t)(A.chan + fd.ch_off);
@@ -698,7 +701,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     }
   };
   auto commit = [&](const Blk& B) {
-    if (tid < NW || !B.ok) return;
+    if (!B.ok) return;
     v2u* dst = reinterpret_cast<v2u*>(win);
     const int s = tid - NW;
 #pragma unroll
@@ -735,26 +738,52 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     // fetch overlaps the LDS rectangle reads (children are adjacent: one 32-byte pair)
     auto advance = [&](Walk& w) {
       const uint4 v = w.nd;
+#if FFD_TRAV_PAIR
       const uint4 c0 = A.nodes[v.x], c1 = A.nodes[v.x + 1];
+#endif
       const uint16_t* I = win + (int)__umul24(v.y & 63u, (unsigned)(WH * LW)) + w.wbase;
       const int p1 = rect_mean16(I + node_off(v.w & 0xFFFFu, LW), LW, (v.y >> 6) & 31u, (v.y >> 11) & 31u);
       const int p2 = rect_mean16(I + node_off(v.w >> 16, LW), LW, (v.y >> 16) & 31u, (v.y >> 21) & 31u);
+#if FFD_TRAV_PAIR
       w.nd = (p1 - p2) <= (int)v.z ? c0 : c1;
+#else
+      w.nd = A.nodes[v.x + ((p1 - p2) <= (int)v.z ? 0u : 1u)];
+#endif
     };
     if (FFD_TRAV_WALKS == 2) {
+      // Two walks per lane advanced in ONE basic block (no per-walk branches), so the compiler
+      // interleaves their rectangle reads, ALU chains and node fetches.  A finished walk (its node
+      // is a leaf) is parked: it tests a dummy split (channel 0, 1x1 rectangles at its patch
+      // corner), fetches nodes[0..1] (L1 hits) and keeps its leaf.  Nodes are held as plain
+      // 4-vectors so the selects stay in registers.
+      typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+      const v4u* nodes = reinterpret_cast<const v4u*>(A.nodes);
+      const v4u park = v4u{0u, (1u << 6) | (1u << 11) | (1u << 16) | (1u << 21), 0u, 0u};
+      auto goes_left = [&](v4u v, int wbase) {
+        const uint16_t* I = win + (int)__umul24(v.y & 63u, (unsigned)(WH * LW)) + wbase;
+        const int p1 = rect_mean16(I + node_off(v.w & 0xFFFFu, LW), LW, (v.y >> 6) & 31u, (v.y >> 11) & 31u);
+        const int p2 = rect_mean16(I + node_off(v.w >> 16, LW), LW, (v.y >> 16) & 31u, (v.y >> 21) & 31u);
+        return (p1 - p2) <= (int)v.z;
+      };
       for (int i0 = tid; i0 < items; i0 += 2 * NW) {
         Walk P, Q;
         init(P, i0);
         init(Q, i0 + NW);
+        v4u ndp = v4u{P.nd.x, P.nd.y, P.nd.z, P.nd.w}, ndq = v4u{Q.nd.x, Q.nd.y, Q.nd.z, Q.nd.w};
+        const int wbp = P.wbase, wbq = Q.wbase;
         for (;;) {
-          P.done = P.done || (P.nd.x & LEAF_BIT);
-          Q.done = Q.done || (Q.nd.x & LEAF_BIT);
-          if (P.done && Q.done) break;
-          if (!P.done) advance(P);
-          if (!Q.done) advance(Q);
+          const bool pa = !(ndp.x & LEAF_BIT), qa = !(ndq.x & LEAF_BIT);
+          if (!pa && !qa) break;
+          const v4u vp = pa ? ndp : park, vq = qa ? ndq : park;
+          const v4u p0 = nodes[vp.x], p1 = nodes[vp.x + 1];
+          const v4u q0 = nodes[vq.x], q1 = nodes[vq.x + 1];
+          const bool lp = goes_left(vp, wbp), lq = goes_left(vq, wbq);
+          const v4u np = lp ? p0 : p1, nq = lq ? q0 : q1;
+          ndp = pa ? np : ndp;
+          ndq = qa ? nq : ndq;
         }
-        if (P.oidx >= 0) out[P.oidx] = (int32_t)(P.nd.x & ~LEAF_BIT);
-        if (Q.oidx >= 0) out[Q.oidx] = (int32_t)(Q.nd.x & ~LEAF_BIT);
+        if (P.oidx >= 0) out[P.oidx] = (int32_t)(ndp.x & ~LEAF_BIT);
+        if (Q.oidx >= 0) out[Q.oidx] = (int32_t)(ndq.x & ~LEAF_BIT);
       }
     } else {
       for (int i0 = tid; i0 < items; i0 += NW) {
@@ -766,26 +795,39 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     }
   };
 
+  // Stager waves and walker waves run separate loops with the same barrier sequence per block
+  // (waves are wholly one role), so the staging registers are live only in the stager loop and
+  // the walkers get the rest of the register file.
   int lb = start + k;
   if (lb >= end) return;
-  Blk cur = block(lb);
-  prefetch(cur);
-  for (; lb < end; lb += nk) {
-    __syncthreads();  // the previous block's walks are done with the window
+  if (tid >= NW) {
+    Blk cur = block(lb);
 #if FFD_TRAV_PROBE != 2
-    commit(cur);
+    prefetch(cur);
 #endif
-    __syncthreads();
-    Blk nxt;
-    nxt.ok = false;
-    if (lb + nk < end) nxt = block(lb + nk);
+    for (; lb < end; lb += nk) {
+      __syncthreads();  // the previous block's walks are done with the window
 #if FFD_TRAV_PROBE != 2
-    prefetch(nxt);
+      commit(cur);
 #endif
+      __syncthreads();  // the window holds block lb
+      Blk nxt;
+      nxt.ok = false;
+      if (lb + nk < end) nxt = block(lb + nk);
+#if FFD_TRAV_PROBE != 2
+      prefetch(nxt);
+#endif
+      cur = nxt;
+    }
+  } else {
+    for (; lb < end; lb += nk) {
+      __syncthreads();
+      __syncthreads();
 #if FFD_TRAV_PROBE != 1
-    if (tid < NW && cur.ok) walk_block(cur);
+      const Blk cur = block(lb);
+      if (cur.ok) walk_block(cur);
 #endif
-    cur = nxt;
+    }
   }
 }
 
