@@ -34,6 +34,13 @@ constexpr uint32_t LEAF_BIT = 0x80000000u;
 //   w: off1 | off2<<16, off = ry*PITCH + rx (patch-relative integral-image offsets)
 // Source fields: ThresholdSplit<SimplePatchFeature> (ThresholdSplit.hpp:51-67,
 // ImageSample.hpp:462-464) and TreeNode::left/right (TreeNode.hpp:138-141).
+//
+// Walk nodes (k_traverse, re-encoded per forest for its LDS window of WH rows x LW columns):
+//   x: as above (child index / LEAF_BIT | ordinal)
+//   y: rect1: byte offset of its top-left integral corner in the window, channel plane included
+//      (18 bits) | 2*w << 18 (6 bits) | h << 24
+//   z: rect2, same layout
+//   w: threshold (10-bit two's complement) | w1*h1 << 10 (9 bits) | w2*h2 << 19 (9 bits)
 
 struct FaceDesc {
   int64_t img_off;        // byte offset of the source image

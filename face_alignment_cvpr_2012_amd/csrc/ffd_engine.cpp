@@ -142,6 +142,8 @@ struct ffd_engine {
 
   // device model
   DevBuf gabor_coef, hp_nodes, hp_roots, hp_sizes, hp_m, mp_nodes, mp_roots, mp_sizes, mp_rec;
+  DevBuf hp_wnodes, mp_wnodes;       // walk-node encodings for k_traverse (ffd_device.hpp)
+  std::vector<uint4> hp_nodes_h, mp_nodes_h;  // host copies until the walk nodes are built
   bool vote_rec_compact = false;     // 32-B vote records (else 64-B), see load_model
   int vote_bias_x = 0, vote_bias_y = 0;
 
@@ -229,6 +231,16 @@ struct ffd_engine {
     };
     fit(trav_g_hp, desc.hp_option.step_size, desc.hp_option.step_size);
     fit(trav_g_mp, desc.mp_option.step_size, mp_step_y());
+    auto walk_nodes = [&](std::vector<uint4>& h, DevBuf& d, int G, int step, int step_y) {
+      std::vector<uint4> wn(h.size());
+      if (!encode_walk_nodes(h.data(), h.size(), G, step, step_y, wn.data()))
+        throw std::runtime_error("forest does not fit the traversal's walk-node encoding");
+      upload(d, wn, main_stream());
+      HIP_CHECK(hipStreamSynchronize(main_stream()));
+      std::vector<uint4>().swap(h);
+    };
+    walk_nodes(hp_nodes_h, hp_wnodes, trav_g_hp, desc.hp_option.step_size, desc.hp_option.step_size);
+    walk_nodes(mp_nodes_h, mp_wnodes, trav_g_mp, desc.mp_option.step_size, mp_step_y());
     HIP_CHECK(set_traverse_lds_limit(cap));
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, device));
@@ -335,11 +347,13 @@ void ffd_engine::load_model(const std::string& path) {
   flatten_forest(m, "hp", nodes, roots, sizes);
   hp_trees = (int)roots.size();
   upload(hp_nodes, nodes, main_stream());
+  hp_nodes_h = nodes;
   upload(hp_roots, roots, main_stream());
   upload(hp_sizes, sizes, main_stream());
   flatten_forest(m, "mp", nodes, roots, sizes);
   if ((int)roots.size() != n_forests * ntrees_per_forest) throw std::runtime_error("FFD tree count mismatch");
   upload(mp_nodes, nodes, main_stream());
+  mp_nodes_h = nodes;
   upload(mp_roots, roots, main_stream());
   upload(mp_sizes, sizes, main_stream());
   HIP_CHECK(hipStreamSynchronize(main_stream()));  // host vectors are reused below
@@ -502,13 +516,17 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   if (n == 0) return;
   const hipStream_t st = w.stream;
   int64_t gray_b = 0, mag_e = 0, ch_e = 0, hp_e = 0, mp_e = 0, vote_e = 0;
+  // one channel plane stride for the whole batch (the traversal's window staging assumes it)
+  int64_t plane = PITCH;
+  for (const auto& f : fds)
+    if (f.valid) plane = std::max(plane, (int64_t)(f.H + 1) * PITCH);
   for (auto& f : fds) {
     if (!f.valid) continue;
     f.gray_off = gray_b;
     gray_b += align_up((int64_t)f.H * PITCH, 256);
     f.mag_off = mag_e;
     mag_e += (int64_t)NGABOR * f.H * PITCH;
-    f.plane = (int64_t)(f.H + 1) * PITCH;
+    f.plane = plane;
     f.ch_off = ch_e;
     ch_e += NCH * f.plane;
     f.hp_off = hp_e;
@@ -541,9 +559,9 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
     launch_integral(dfd, n, w.gray.as<uint8_t>(), w.chan.as<uint16_t>(), st);
   });
   stage(7, st, [&] {
-    launch_traverse(true, dfd, n, blocks_per_face(fds, true, trav_g_hp), trav_g_hp, hp_nodes.as<uint4>(),
+    launch_traverse(true, dfd, n, blocks_per_face(fds, true, trav_g_hp), trav_g_hp, hp_wnodes.as<uint4>(),
                     hp_roots.as<int32_t>(), nullptr, hp_trees, desc.hp_option.step_size, desc.hp_option.step_size,
-                    w.chan.as<uint16_t>(),
+                    plane, w.chan.as<uint16_t>(),
                     w.hpleaf.as<int32_t>(), trav_wg, st);
   });
   stage(8, st, [&] {
@@ -551,9 +569,9 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
                    w.state.as<HpState>(), d_out, st);
   });
   stage(9, st, [&] {
-    launch_traverse(false, dfd, n, blocks_per_face(fds, false, trav_g_mp), trav_g_mp, mp_nodes.as<uint4>(),
+    launch_traverse(false, dfd, n, blocks_per_face(fds, false, trav_g_mp), trav_g_mp, mp_wnodes.as<uint4>(),
                     mp_roots.as<int32_t>(), w.state.as<HpState>(), 0, desc.mp_option.step_size, mp_step_y(),
-                    w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), trav_wg, st);
+                    plane, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), trav_wg, st);
   });
   const int n_parts = std::min(desc.mp_option.num_parts, NPARTS);
   stage(10, st, [&] {

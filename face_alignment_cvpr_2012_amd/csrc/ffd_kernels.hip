@@ -574,6 +574,22 @@ __device__ __forceinline__ int node_off(uint32_t enc, int ld) {
   return (int)__umul24(enc >> 7, (unsigned)ld) + (int)(enc & 127u);
 }
 
+// Walk-node rectangle (k_traverse; encoding in ffd_device.hpp "walk nodes"): e = byte offset of
+// the rectangle's top-left integral corner in the window (channel plane included) | 2w << 18 |
+// h << 24.  ImageSample::evalTest's (int)(R / (float)area) as fma(R, rcp(area), 0.00075) truncated:
+// equal to the integer quotient for every R in [0, 255 area], area in [1, 484], with rcp off by up
+// to 2 ulp (tests/test_numerics.py checks all pairs).
+__device__ __forceinline__ int rect_mean_walk(const unsigned char* __restrict__ base, uint32_t e, uint32_t area, int ld2) {
+  const unsigned char* p = base + (e & 0x3FFFFu);
+  const int wb = (int)((e >> 18) & 63u);
+  const int r1 = (int)__umul24(e >> 25, (unsigned)ld2), r2 = (int)__umul24(e >> 24, (unsigned)ld2);
+  const uint32_t a = *reinterpret_cast<const uint16_t*>(p), b = *reinterpret_cast<const uint16_t*>(p + wb);
+  const uint32_t c = *reinterpret_cast<const uint16_t*>(p + r1), d = *reinterpret_cast<const uint16_t*>(p + r1 + wb);
+  const uint32_t f0 = *reinterpret_cast<const uint16_t*>(p + r2), f1 = *reinterpret_cast<const uint16_t*>(p + r2 + wb);
+  const uint32_t top = (d - c - b + a) & 0xFFFFu, bot = (f1 - f0 - d + c) & 0xFFFFu;
+  return (int)__builtin_fmaf((float)(top + bot), __builtin_amdgcn_rcpf((float)area), 0.00075f);
+}
+
 // Tree<S>::evaluateMT over global u16 planes (ffd_forest_eval_leaves hook).
 __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint32_t node,
                                            const uint16_t* __restrict__ chan, int64_t plane) {
@@ -602,11 +618,8 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 #ifndef FFD_TRAV_NW
 #define FFD_TRAV_NW 384
 #endif
-#ifndef FFD_TRAV_WALKS
-#define FFD_TRAV_WALKS 1
-#endif
-#ifndef FFD_TRAV_PAIR
-#define FFD_TRAV_PAIR 1  // 1: request both children before the split test; 0: only the chosen one after it
+#ifndef FFD_TRAV_K
+#define FFD_TRAV_K 1  // walks per walker lane (> 1: interleaved, each fetching only its taken child)
 #endif
 constexpr int TRAV_NT = 1024, TRAV_NW = FFD_TRAV_NW, TRAV_NS = TRAV_NT - TRAV_NW;
 constexpr int TRAV_U = (20480 + TRAV_NS - 1) / TRAV_NS;  // 8-byte window chunks held in registers per staging thread
@@ -625,6 +638,7 @@ struct TravArgs {
   const HpState* hp_state; // FFD pass: selected trees; nullptr for the head-pose pass
   int ntrees_hp;           // head-pose pass: number of trees
   int step, step_y;        // patch grid steps (x, y)
+  int plane;               // channel plane stride (elements), the same for every face of the batch
   const uint16_t* chan;
   int32_t* leaf_out;
 };
@@ -672,43 +686,6 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   // staging registers: window chunks (c, r, q) of the next block, NS chunks apart
   // (buffer loads: 32-bit offsets, and reads past the face's planes return 0; window rows below
   // the face's integral image are never referenced by a patch)
-  v2u st[U];
-  auto prefetch = [&](const Blk& B) {
-    if (!B.ok) return;
-    const FaceDesc& fd = A.faces[B.f];
-    // the resource must be wave-uniform (SGPRs): read it from the first lane explicitly
-    const uint64_t base = (uint64_t)(A.chan + fd.ch_off);
-    const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)base);
-    const uint32_t bhi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-    const int nbytes = __builtin_amdgcn_readfirstlane((int)(NCH * fd.plane * 2));
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(((uint64_t)bhi << 32) | blo), (short)0, nbytes, BUF_WORD3);
-    const int base_b = (B.py0 * PITCH + (B.px0 & ~3)) * 2, plane_b = (int)fd.plane * 2;
-    int s = tid - NW;
-    asm volatile("" : "+v"(s));  // keep the per-chunk offsets out of loop-invariant hoisting (VGPRs)
-    const int dq = NS % nq, dr = (NS / nq) % WH, dc = NS / (nq * WH);
-    int q = s % nq, r = (s / nq) % WH, c = s / (nq * WH);
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, base_b + c * plane_b + r * (PITCH * 2) + q * 8, 0, 0);
-      q += dq;
-      int cr = q >= nq;
-      q -= cr ? nq : 0;
-      r += dr + cr;
-      cr = r >= WH;
-      r -= cr ? WH : 0;
-      c += dc + cr;
-    }
-  };
-  auto commit = [&](const Blk& B) {
-    if (!B.ok) return;
-    v2u* dst = reinterpret_cast<v2u*>(win);
-    const int s = tid - NW;
-#pragma unroll
-    for (int u = 0; u < U; u++)
-      if (u * NS + s < total) dst[u * NS + s] = st[u];
-  };
-
   struct Walk {
     uint4 nd;
     int wbase;  // window offset of the patch's top-left corner
@@ -738,61 +715,62 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     // fetch overlaps the LDS rectangle reads (children are adjacent: one 32-byte pair)
     auto advance = [&](Walk& w) {
       const uint4 v = w.nd;
-#if FFD_TRAV_PAIR
       const uint4 c0 = A.nodes[v.x], c1 = A.nodes[v.x + 1];
-#endif
-      const uint16_t* I = win + (int)__umul24(v.y & 63u, (unsigned)(WH * LW)) + w.wbase;
-      const int p1 = rect_mean16(I + node_off(v.w & 0xFFFFu, LW), LW, (v.y >> 6) & 31u, (v.y >> 11) & 31u);
-      const int p2 = rect_mean16(I + node_off(v.w >> 16, LW), LW, (v.y >> 16) & 31u, (v.y >> 21) & 31u);
-#if FFD_TRAV_PAIR
-      w.nd = (p1 - p2) <= (int)v.z ? c0 : c1;
-#else
-      w.nd = A.nodes[v.x + ((p1 - p2) <= (int)v.z ? 0u : 1u)];
-#endif
+      const unsigned char* base = reinterpret_cast<const unsigned char*>(win) + 2 * w.wbase;
+      const int p1 = rect_mean_walk(base, v.y, (v.w >> 10) & 511u, 2 * LW);
+      const int p2 = rect_mean_walk(base, v.z, v.w >> 19, 2 * LW);
+      w.nd = (p1 - p2) <= ((int)(v.w << 22) >> 22) ? c0 : c1;  // 10-bit signed threshold
     };
-    if (FFD_TRAV_WALKS == 2) {
-      // Two walks per lane advanced in ONE basic block (no per-walk branches), so the compiler
-      // interleaves their rectangle reads, ALU chains and node fetches.  A finished walk (its node
-      // is a leaf) is parked: it tests a dummy split (channel 0, 1x1 rectangles at its patch
-      // corner), fetches nodes[0..1] (L1 hits) and keeps its leaf.  Nodes are held as plain
-      // 4-vectors so the selects stay in registers.
-      typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-      const v4u* nodes = reinterpret_cast<const v4u*>(A.nodes);
-      const v4u park = v4u{0u, (1u << 6) | (1u << 11) | (1u << 16) | (1u << 21), 0u, 0u};
-      auto goes_left = [&](v4u v, int wbase) {
-        const uint16_t* I = win + (int)__umul24(v.y & 63u, (unsigned)(WH * LW)) + wbase;
-        const int p1 = rect_mean16(I + node_off(v.w & 0xFFFFu, LW), LW, (v.y >> 6) & 31u, (v.y >> 11) & 31u);
-        const int p2 = rect_mean16(I + node_off(v.w >> 16, LW), LW, (v.y >> 16) & 31u, (v.y >> 21) & 31u);
-        return (p1 - p2) <= (int)v.z;
-      };
-      for (int i0 = tid; i0 < items; i0 += 2 * NW) {
-        Walk P, Q;
-        init(P, i0);
-        init(Q, i0 + NW);
-        v4u ndp = v4u{P.nd.x, P.nd.y, P.nd.z, P.nd.w}, ndq = v4u{Q.nd.x, Q.nd.y, Q.nd.z, Q.nd.w};
-        const int wbp = P.wbase, wbq = Q.wbase;
-        for (;;) {
-          const bool pa = !(ndp.x & LEAF_BIT), qa = !(ndq.x & LEAF_BIT);
-          if (!pa && !qa) break;
-          const v4u vp = pa ? ndp : park, vq = qa ? ndq : park;
-          const v4u p0 = nodes[vp.x], p1 = nodes[vp.x + 1];
-          const v4u q0 = nodes[vq.x], q1 = nodes[vq.x + 1];
-          const bool lp = goes_left(vp, wbp), lq = goes_left(vq, wbq);
-          const v4u np = lp ? p0 : p1, nq = lq ? q0 : q1;
-          ndp = pa ? np : ndp;
-          ndq = qa ? nq : ndq;
-        }
-        if (P.oidx >= 0) out[P.oidx] = (int32_t)(ndp.x & ~LEAF_BIT);
-        if (Q.oidx >= 0) out[Q.oidx] = (int32_t)(ndq.x & ~LEAF_BIT);
-      }
-    } else {
-      for (int i0 = tid; i0 < items; i0 += NW) {
+#if FFD_TRAV_K > 1
+    // K walks per lane advanced in one basic block (no per-walk branches, so their LDS reads, ALU
+    // chains and node fetches interleave); each walk fetches only the child it takes.  A finished
+    // walk keeps its leaf and re-reads a parked record (nodes[0]: L1-resident).
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u* nodes = reinterpret_cast<const v4u*>(A.nodes);
+    for (int i0 = tid; i0 < items; i0 += FFD_TRAV_K * NW) {
+      v4u nd[FFD_TRAV_K];
+      int wb[FFD_TRAV_K], oi[FFD_TRAV_K];
+#pragma unroll
+      for (int j = 0; j < FFD_TRAV_K; j++) {
         Walk P;
-        init(P, i0);
-        while (!P.done && !(P.nd.x & LEAF_BIT)) advance(P);
-        if (P.oidx >= 0) out[P.oidx] = (int32_t)(P.nd.x & ~LEAF_BIT);
+        init(P, i0 + j * NW);
+        nd[j] = v4u{P.nd.x, P.nd.y, P.nd.z, P.nd.w};
+        wb[j] = 2 * P.wbase;
+        oi[j] = P.oidx;
       }
+      for (;;) {
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < FFD_TRAV_K; j++) any = any || !(nd[j].x & LEAF_BIT);
+        if (!any) break;
+        uint32_t nxt[FFD_TRAV_K];
+#pragma unroll
+        for (int j = 0; j < FFD_TRAV_K; j++) {
+          const v4u v = nd[j];
+          const bool act = !(v.x & LEAF_BIT);
+          const unsigned char* base = reinterpret_cast<const unsigned char*>(win) + wb[j];
+          const int p1 = rect_mean_walk(base, act ? v.y : 0u, act ? (v.w >> 10) & 511u : 1u, 2 * LW);
+          const int p2 = rect_mean_walk(base, act ? v.z : 0u, act ? v.w >> 19 : 1u, 2 * LW);
+          nxt[j] = act ? v.x + ((p1 - p2) <= ((int)(v.w << 22) >> 22) ? 0u : 1u) : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < FFD_TRAV_K; j++) {
+          const v4u c = nodes[nxt[j]];
+          nd[j] = (nd[j].x & LEAF_BIT) ? nd[j] : c;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < FFD_TRAV_K; j++)
+        if (oi[j] >= 0) out[oi[j]] = (int32_t)(nd[j].x & ~LEAF_BIT);
     }
+#else
+    for (int i0 = tid; i0 < items; i0 += NW) {
+      Walk P;
+      init(P, i0);
+      while (!P.done && !(P.nd.x & LEAF_BIT)) advance(P);
+      if (P.oidx >= 0) out[P.oidx] = (int32_t)(P.nd.x & ~LEAF_BIT);
+    }
+#endif
   };
 
   // Stager waves and walker waves run separate loops with the same barrier sequence per block
@@ -801,6 +779,53 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   int lb = start + k;
   if (lb >= end) return;
   if (tid >= NW) {
+    // Staging: chunk i = (channel c, window row r, 4-column group q), i = (c * WH + r) * nq + q, goes
+    // to LDS chunk i; staging thread s owns chunks s + u * NS.  Their face-relative source byte
+    // offsets c * plane + r * PITCH * 2 + q * 8 are computed once (every face of a batch has the
+    // same plane stride, TravArgs::plane), so a block costs one load per chunk.
+    v2u st[U];
+    int voff[U];
+    auto stage_offsets = [&](int plane_b) {
+      const int s = tid - NW;
+      const int dq = NS % nq, dr = (NS / nq) % WH, dc = NS / (nq * WH);
+      int q = s % nq, r = (s / nq) % WH, c = s / (nq * WH);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        voff[u] = min(c, NCH) * plane_b + r * (PITCH * 2) + q * 8;
+        q += dq;
+        int cr = q >= nq;
+        q -= cr ? nq : 0;
+        r += dr + cr;
+        cr = r >= WH;
+        r -= cr ? WH : 0;
+        c += dc + cr;
+      }
+    };
+    auto prefetch = [&](const Blk& B) {
+      if (!B.ok) return;
+      const FaceDesc& fd = A.faces[B.f];
+      // the resource and the block offset must be wave-uniform (SGPRs): read them from the first lane
+      const uint64_t base = (uint64_t)(A.chan + fd.ch_off);
+      const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+      const uint32_t bhi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+      const int nbytes = __builtin_amdgcn_readfirstlane((int)(NCH * fd.plane * 2));
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(((uint64_t)bhi << 32) | blo), (short)0, nbytes, BUF_WORD3);
+      const int base_b = __builtin_amdgcn_readfirstlane((B.py0 * PITCH + (B.px0 & ~3)) * 2);
+      // (reads past the face's planes return 0; chunks past the window are loaded but never committed)
+#pragma unroll
+      for (int u = 0; u < U; u++) st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff[u], base_b, 0);
+    };
+    auto commit = [&](const Blk& B) {
+      if (!B.ok) return;
+      v2u* dst = reinterpret_cast<v2u*>(win);
+      const int s = tid - NW;
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (u * NS + s < total) dst[u * NS + s] = st[u];
+    };
+
+    stage_offsets(A.plane * 2);
     Blk cur = block(lb);
 #if FFD_TRAV_PROBE != 2
     prefetch(cur);
@@ -1204,6 +1229,29 @@ void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t
   if (n > 0) k_integral<<<n, 256, 0, s>>>(faces, gray, chan);
 }
 
+bool encode_walk_nodes(const uint4* nodes, size_t n, int G, int step, int step_y, uint4* out) {
+  const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1), LW = trav_row_pitch(WW);
+  for (size_t i = 0; i < n; i++) {
+    const uint4 v = nodes[i];
+    if (v.x & LEAF_BIT) {
+      out[i] = make_uint4(v.x, 0u, 0u, 0u);
+      continue;
+    }
+    const uint32_t ch = v.y & 63u, w1 = (v.y >> 6) & 31u, h1 = (v.y >> 11) & 31u, w2 = (v.y >> 16) & 31u,
+                   h2 = (v.y >> 21) & 31u;
+    const uint32_t e1 = v.w & 0xFFFFu, e2 = v.w >> 16;
+    const uint32_t o1 = 2 * (ch * WH * LW + (e1 / PITCH) * LW + e1 % PITCH);
+    const uint32_t o2 = 2 * (ch * WH * LW + (e2 / PITCH) * LW + e2 % PITCH);
+    const int thr = (int)v.z;
+    if (o1 >= (1u << 18) || o2 >= (1u << 18) || h1 > 31 || h2 > 31 || w1 * h1 > 511 || w2 * h2 > 511 ||
+        thr < -512 || thr > 511)
+      return false;
+    out[i] = make_uint4(v.x, o1 | (2 * w1) << 18 | h1 << 24, o2 | (2 * w2) << 18 | h2 << 24,
+                        ((uint32_t)thr & 0x3FFu) | (w1 * h1) << 10 | (w2 * h2) << 19);
+  }
+  return true;
+}
+
 int traverse_lds_bytes(int G, int step, int step_y) {
   const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1);
   return NCH * WH * trav_row_pitch(WW) * 2;
@@ -1215,11 +1263,11 @@ bool traverse_window_fits(int G, int step, int step_y, int lds_cap) {
 }
 
 void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* nodes, const int32_t* roots,
-                     const HpState* state, int ntrees_hp, int step, int step_y, const uint16_t* chan,
+                     const HpState* state, int ntrees_hp, int step, int step_y, int64_t plane, const uint16_t* chan,
                      int32_t* leaf_out, int n_wg, hipStream_t s) {
   const int total_blocks = n * bpf;
   if (total_blocks <= 0) return;
-  TravArgs A{faces, n, bpf, nodes, roots, state, ntrees_hp, step, step_y, chan, leaf_out};
+  TravArgs A{faces, n, bpf, nodes, roots, state, ntrees_hp, step, step_y, (int)plane, chan, leaf_out};
   const int lds = traverse_lds_bytes(G, step, step_y);
   const int grid = std::max(8, n_wg & ~7);
 #define FFD_TRAV(HPV, GV) k_traverse<HPV, GV><<<grid, TRAV_NT, lds, s>>>(A)

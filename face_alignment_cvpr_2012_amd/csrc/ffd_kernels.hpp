@@ -29,11 +29,14 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, const uint8_t* gray, con
                   uint16_t* chan, hipStream_t s);
 // integral channels 0 (gray), 36, 37 (Sobel)
 void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t* chan, hipStream_t s);
+// Re-encode 16-byte nodes as k_traverse's walk nodes for a G x G patch block window (ffd_device.hpp);
+// false if a field does not fit the encoding.
+bool encode_walk_nodes(const uint4* nodes, size_t n, int G, int step, int step_y, uint4* out);
 int traverse_lds_bytes(int G, int step, int step_y);
 bool traverse_window_fits(int G, int step, int step_y, int lds_cap);
-// n_wg: persistent workgroups (one per CU; rounded down to a multiple of 8 XCDs)
+// plane: the channel plane stride shared by every face of the batch; n_wg: persistent workgroups (one per CU; rounded down to a multiple of 8 XCDs)
 void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* nodes, const int32_t* roots,
-                     const HpState* state, int ntrees_hp, int step, int step_y, const uint16_t* chan,
+                     const HpState* state, int ntrees_hp, int step, int step_y, int64_t plane, const uint16_t* chan,
                      int32_t* leaf_out, int n_wg, hipStream_t s);
 hipError_t set_traverse_lds_limit(int bytes);
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,

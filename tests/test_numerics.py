@@ -16,6 +16,27 @@ def test_float_division_truncation_equals_integer_division():
         assert np.array_equal(q, R // a), a
 
 
+def test_rcp_fma_division_equals_integer_division():
+    """The traversal kernel (ffd_kernels.hip rect_mean_walk) computes the quotient as
+    (int)fma((float)R, rcp(area), 0.00075) with the hardware reciprocal; equal to R // area for
+    every R in [0, 255*area], area in [1, 484], for any reciprocal within 2 ulp of 1/area.
+    fma is emulated exactly: R * r + eps needs <= 48 significant bits, so float64 holds it exactly
+    and one rounding to float32 is the fused result."""
+    eps = np.float64(np.float32(0.00075))
+    for a in range(1, 485):
+        R = np.arange(0, 255 * a + 1, dtype=np.float64)
+        r0 = np.float32(1.0) / np.float32(a)
+        rs = [r0]
+        for d in (np.float32(np.inf), np.float32(0.0)):
+            r = r0
+            for _ in range(2):
+                r = np.nextafter(r, d)
+                rs.append(r)
+        for r in rs:
+            q = (R * np.float64(r) + eps).astype(np.float32).astype(np.int64)
+            assert np.array_equal(q, np.arange(0, 255 * a + 1) // a), (a, r)
+
+
 def test_ffd_exp_matches_libm(oracle_mod):
     """ffd_exp (include/ffd_numerics.h) is within 2 ulp of libm exp over the argument ranges the
     path uses (areaUnderCurve: -0.5 t^2 <= 0; MeanShift: -d/10 in [-30, 0])."""
