@@ -625,7 +625,7 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 #define FFD_TRAV_PROBE 0  // timing probes (tools/probe.sh): 1 = stage only, 2 = walk only
 #endif
 #ifndef FFD_TRAV_NW
-#define FFD_TRAV_NW 384
+#define FFD_TRAV_NW 320
 #endif
 #ifndef FFD_TRAV_XLDS
 #define FFD_TRAV_XLDS 0
