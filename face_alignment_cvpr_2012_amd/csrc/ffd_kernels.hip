@@ -651,6 +651,11 @@ constexpr int TRAV_U = (20480 + TRAV_NS - 1) / TRAV_NS;  // 8-byte window chunks
 // LDS row pitch (u16) of a traversal window WW columns wide staged from a 4-element aligned column.
 __host__ __device__ __forceinline__ int trav_row_pitch(int WW) { return (WW + 3 + 3) & ~3; }
 
+// Window bytes (16-byte aligned); the block's root node records (uint4 [MAX_TREES]) follow it.
+__host__ __device__ __forceinline__ int trav_window_bytes(int WW, int WH) {
+  return (NCH * WH * trav_row_pitch(WW) * 2 + 15) & ~15;
+}
+
 constexpr int BUF_WORD3 = 0x00020000;  // raw buffer resource word 3 (gfx950: 32-bit data format)
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
@@ -677,6 +682,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   const int step = A.step, stepy = A.step_y, WW = 32 + step * (G - 1), WH = 32 + stepy * (G - 1);
   const int LW = trav_row_pitch(WW), nq = LW >> 2;
   const int total = NCH * WH * nq;  // 8-byte chunks per window (host guarantees <= NS * U)
+  uint4* root_rec = reinterpret_cast<uint4*>(smem + trav_window_bytes(WW, WH));  // [t]: tree t's root
   // XCD-contiguous, face-major block range of this workgroup's XCD; workgroups of one XCD stride it
   const int N = A.n_faces * A.bpf, xcd = blockIdx.x & 7, k = blockIdx.x >> 3, nk = gridDim.x >> 3;
   const int q8 = N >> 3, r8 = N & 7;
@@ -729,10 +735,9 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       const int t = item / GG, pl = item - t * GG;
       const int xi = B.xi0 + pl % G, yi = B.yi0 + pl / G;
       if (xi >= B.nx || yi >= B.ny) return;
-      const int tree = HP ? t : A.hp_state[B.f].trees[t];
       w.wbase = (yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh;
       w.oidx = t * n + yi * B.nx + xi;
-      w.nd = A.nodes[A.roots[tree]];
+      w.nd = root_rec[t];
       w.done = false;
     };
     // both children's records are requested before the split test is evaluated, so the node
@@ -820,6 +825,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     // same plane stride, TravArgs::plane), so a block costs one load per chunk.
     v2u st[U];
     int voff[U];
+    uint4 root_nd = make_uint4(LEAF_BIT, 0u, 0u, 0u);
     auto stage_offsets = [&](int plane_b) {
       const int s = tid - NW;
       const int dq = NS % nq, dr = (NS / nq) % WH, dc = NS / (nq * WH);
@@ -848,6 +854,12 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
           (void*)(((uint64_t)bhi << 32) | blo), (short)0, nbytes, BUF_WORD3);
       const int base_b = __builtin_amdgcn_readfirstlane((B.py0 * PITCH + (B.px0 & ~3)) * 2);
       // (reads past the face's planes return 0; chunks past the window are loaded but never committed)
+      // the block's root records (tree t of the block: lane t of the first staging wave)
+      const int j = tid - NW;
+      if (j < B.T) {
+        const int tree = HP ? j : A.hp_state[B.f].trees[j];
+        root_nd = A.nodes[A.roots[tree]];
+      }
 #pragma unroll
       for (int u = 0; u < U; u++) {
 #if FFD_TRAV_SLEEP
@@ -860,6 +872,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       if (!B.ok) return;
       v2u* dst = reinterpret_cast<v2u*>(win);
       const int s = tid - NW;
+      if (s < B.T) root_rec[s] = root_nd;
 #pragma unroll
       for (int u = 0; u < U; u++)
         if (u * NS + s < total) dst[u * NS + s] = st[u];
@@ -1294,7 +1307,7 @@ bool encode_walk_nodes(const uint4* nodes, size_t n, int G, int step, int step_y
 
 int traverse_lds_bytes(int G, int step, int step_y) {
   const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1);
-  return NCH * WH * trav_row_pitch(WW) * 2;
+  return trav_window_bytes(WW, WH) + MAX_TREES * 16;  // window + the block's root records
 }
 
 bool traverse_window_fits(int G, int step, int step_y, int lds_cap) {
