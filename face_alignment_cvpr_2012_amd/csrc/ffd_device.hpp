@@ -5,13 +5,12 @@
 //   mag    f32 [35][H][PITCH]              Gabor magnitudes before min-max normalisation
 //   chan   u16 [38][H+1][PITCH]            integral channels mod 2^16 (ImageSample m_feature_channels;
 //                                          every rectangle the trees read is exact, ffd_kernels.hip rect_mean16)
-//   hpleaf i32 [15][n_hp]                  head-pose leaf ordinal per (tree, patch lane-order)
-//   mpleaf i32 [T][n_mp]                   FFD leaf ordinal per (tree slot, patch lane-order)
+//   hpleaf i32 [n_hp][15]                  head-pose leaf ordinal per (patch, tree), reference order
+//   mpleaf i32 [n_mp][T]                   FFD leaf ordinal per (patch, tree slot), reference order
 //   votes  {i16 x,y; f32 w} [10][T*n_mp]   compacted votes per landmark (MeanShift input)
-// "lane order" enumerates the patch grid y-major (q = yi*nx + xi) so that the 64 lanes
-// of a traversal wave read horizontally adjacent patches; the reference order is
-// x-major (i = xi*ny + yi, face_utils.cpp:200-207) and every consumer that depends on
-// order (head-pose sums, vote lists) walks the reference order.
+// The reference order is x-major over the patch grid (i = xi*ny + yi, face_utils.cpp:200-207),
+// tree-minor; the traversal writes its leaves there, so the order-dependent consumers (head-pose
+// sums, vote lists) read them contiguously.
 #pragma once
 
 #include <stdint.h>

@@ -872,7 +872,7 @@ ffd_status ffd_get_trace(ffd_engine* e, int32_t index, ffd_trace* tr) {
       for (int xi = 0; xi < f.nhx; xi++)
         for (int yi = 0; yi < f.nhy; yi++)
           for (int t = 0; t < e->hp_trees; t++)
-            tr->hp_leaves[(xi * f.nhy + yi) * e->hp_trees + t] = v[(size_t)t * nh + yi * f.nhx + xi];
+            tr->hp_leaves[(xi * f.nhy + yi) * e->hp_trees + t] = v[(size_t)(xi * f.nhy + yi) * e->hp_trees + t];
     }
     if (tr->mp_leaves) {
       const int nm = f.nmx * f.nmy, T = hs.n_trees;
@@ -880,7 +880,7 @@ ffd_status ffd_get_trace(ffd_engine* e, int32_t index, ffd_trace* tr) {
       HIP_CHECK(hipMemcpy(v.data(), w.mpleaf.as<int32_t>() + f.mp_off, (size_t)T * nm * 4, hipMemcpyDeviceToHost));
       for (int xi = 0; xi < f.nmx; xi++)
         for (int yi = 0; yi < f.nmy; yi++)
-          for (int t = 0; t < T; t++) tr->mp_leaves[(xi * f.nmy + yi) * T + t] = v[(size_t)t * nm + yi * f.nmx + xi];
+          for (int t = 0; t < T; t++) tr->mp_leaves[(xi * f.nmy + yi) * T + t] = v[(size_t)(xi * f.nmy + yi) * T + t];
     }
     if (tr->trees)
       for (int t = 0; t < MAX_TREES; t++) tr->trees[t] = t < hs.n_trees ? hs.trees[t] : -1;

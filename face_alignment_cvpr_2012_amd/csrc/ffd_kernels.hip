@@ -724,7 +724,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   };
   auto walk_block = [&](const Blk& B) {
     const FaceDesc& fd = A.faces[B.f];
-    const int n = B.nx * B.ny, items = GG * B.T, sh = B.px0 & 3;
+    const int items = GG * B.T, sh = B.px0 & 3;
     int32_t* out = A.leaf_out + (HP ? fd.hp_off : fd.mp_off);
     auto init = [&](Walk& w, int item) {
       w.done = true;
@@ -736,7 +736,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       const int xi = B.xi0 + pl % G, yi = B.yi0 + pl / G;
       if (xi >= B.nx || yi >= B.ny) return;
       w.wbase = (yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh;
-      w.oidx = t * n + yi * B.nx + xi;
+      w.oidx = (xi * B.ny + yi) * B.T + t;  // reference order: patch x-major, tree-minor
       w.nd = root_rec[t];
       w.done = false;
     };
@@ -955,9 +955,7 @@ __global__ __launch_bounds__(256) void k_hp_pose(const FaceDesc* __restrict__ fa
     const int k = base + lane;
     float m = 0.f, mm = 0.f, one = 0.f;
     if (k < total) {
-      const int pr = k / T, t = k - pr * T;
-      const int xi = pr / ny, yi = pr - xi * ny;
-      const float v = hp_m[L[(int64_t)t * n + yi * nx + xi]];
+      const float v = hp_m[L[k]];  // leaves are stored in the reference order
       if (v >= 0.f) { m = v; mm = v * v; one = 1.f; }
     }
     const int lim = min(64, total - base);
@@ -1045,9 +1043,8 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
       leaf[u] = -1;
       vx0[u] = vy0[u] = 0;
       if (k < total) {
-        const int pr = k / T, t = k - pr * T;
-        const int xi = pr / ny, yi = pr - xi * ny;
-        leaf[u] = L[(int64_t)t * n + yi * nx + xi];
+        const int pr = idiv_small(k, T), xi = idiv_small(pr, ny), yi = pr - xi * ny;
+        leaf[u] = L[k];  // leaves are stored in the reference order
         vx0[u] = xi * step + half_patch;
         vy0[u] = yi * step_y + half_patch;
       }
