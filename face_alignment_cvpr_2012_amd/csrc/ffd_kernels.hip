@@ -135,12 +135,24 @@ __device__ __forceinline__ int chan_value(int c, const uint8_t* g, int W, int H,
   return sat_u8(v);
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave with DPP: row_shr 1, 2, 4, 8 within each row of
+// 16 lanes, then row_bcast:15 (rows 1, 3 add lane 15 of the row before) and row_bcast:31 (rows 2, 3
+// add lane 31).  Integer adds: the order does not matter.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false); // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false); // row_bcast:31
+  return v;
+}
+
 // The scan of one channel by one wave.  value(y, b) returns the u8 values of columns 2l, 2l+1 of
 // row y for b = 0..RB-1 batches (all of a batch's loads are issued before its scans).
-template <class RowFn>
+template <int RB = 8, class RowFn>
 __device__ __forceinline__ void integral_scan(uint16_t* __restrict__ out, int W, int H, int lane, RowFn row_values) {
   for (int x = lane; x <= W; x += 64) out[x] = 0;  // row 0 of the integral image
-  constexpr int RB = 8;
   uint32_t c0 = 0, c1 = 0;
   for (int y0 = 0; y0 < H; y0 += RB) {
     uint32_t v0[RB], v1[RB];
@@ -151,13 +163,7 @@ __device__ __forceinline__ void integral_scan(uint16_t* __restrict__ out, int W,
       c0 += v0[b];
       c1 += v1[b];
       const uint32_t s2 = c0 + c1;
-      uint32_t incl = s2;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
-        if (lane >= d) incl += o;
-      }
-      const uint32_t excl = incl - s2;
+      const uint32_t excl = wave_incl_scan(s2) - s2;
       uint32_t* r = reinterpret_cast<uint32_t*>(out + (int64_t)(y0 + b + 1) * PITCH);
       // entries >= W+1 land in the row's pitch padding (never read by a patch)
       r[lane] = (excl & 0xFFFFu) | ((excl + c0) << 16);
@@ -231,15 +237,16 @@ __device__ __forceinline__ void gabor_normalise_integrate(const FaceDesc& fd, in
     const int lane = ln, x0 = 2 * lane, FW = fd.W, FH = fd.H;
     const float sf = s_sf[o], hf = s_hf[o];
     const float* m = mag + fd.mag_off + (int64_t)(nu * 7 + o) * FH * PITCH;
-    integral_scan(chan + fd.ch_off + (int64_t)(1 + nu * 7 + o) * fd.plane, FW, FH, lane,
+    constexpr int RB = 16;
+    integral_scan<RB>(chan + fd.ch_off + (int64_t)(1 + nu * 7 + o) * fd.plane, FW, FH, lane,
                   [&](int y0, uint32_t* v0, uint32_t* v1) {
-                    float2 mv[8];
+                    float2 mv[RB];
 #pragma unroll
-                    for (int b = 0; b < 8; b++)
+                    for (int b = 0; b < RB; b++)
                       mv[b] = (y0 + b < FH) ? *reinterpret_cast<const float2*>(&m[(y0 + b) * PITCH + x0])
                                             : make_float2(0.f, 0.f);
 #pragma unroll
-                    for (int b = 0; b < 8; b++) {
+                    for (int b = 0; b < RB; b++) {
                       v0[b] = (x0 < FW) ? (uint32_t)sat_u8(cv_round((mv[b].x * sf + hf) * 255.f + 0.f)) : 0u;
                       v1[b] = (x0 + 1 < FW) ? (uint32_t)sat_u8(cv_round((mv[b].y * sf + hf) * 255.f + 0.f)) : 0u;
                     }
@@ -413,7 +420,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
     __syncthreads();  // the band's gray rows are staged; the previous H pass is done with vg / vq
     // ---- V pass
 #pragma unroll 1
-    for (int i = tid; i < GS_BY * C::SC; i += GS_THREADS) {
+    for (int i = tid; i < (FFD_GABOR_PROBE == 3 ? 0 : GS_BY * C::SC); i += GS_THREADS) {
       const int r = i / C::SC, cc = i - r * C::SC;
       if (cc >= NPC) continue;
       const float* col = &gt[(r + R) * C::GP + cc];
@@ -544,7 +551,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
       }
     }
   }
-#if FFD_GABOR_PROBE == 1  // timing probe: magnitudes are neither stored nor normalised / integrated
+#if FFD_GABOR_PROBE == 1 || FFD_GABOR_PROBE == 2  // timing probes: no normalisation / integration
   if (mn[0] == 0x12345u && mx[1] == 0x6789u) mag[0] = 0.f;
   return;
 #endif
