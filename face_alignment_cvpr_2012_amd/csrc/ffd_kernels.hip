@@ -653,10 +653,16 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 #define FFD_TRAV_K 1  // walks per walker lane (> 1: interleaved, each fetching only its taken child)
 #endif
 constexpr int TRAV_NT = 1024, TRAV_NW = FFD_TRAV_NW, TRAV_NS = TRAV_NT - TRAV_NW;
-constexpr int TRAV_U = (20480 + TRAV_NS - 1) / TRAV_NS;  // 8-byte window chunks held in registers per staging thread
+// Window chunks held in registers per staging thread: 16-byte chunks when the window row pitch is
+// a multiple of 8 columns, else 8-byte chunks (the pitch also sets the LDS bank pattern of the
+// rectangle reads, so it is not padded up).
+template <int CB> struct TravStage;
+template <> struct TravStage<8> { static constexpr int U = (20480 + TRAV_NS - 1) / TRAV_NS; typedef uint32_t T __attribute__((ext_vector_type(2))); };
+template <> struct TravStage<16> { static constexpr int U = (11000 + TRAV_NS - 1) / TRAV_NS; typedef uint32_t T __attribute__((ext_vector_type(4))); };
 
 // LDS row pitch (u16) of a traversal window WW columns wide staged from a 4-element aligned column.
 __host__ __device__ __forceinline__ int trav_row_pitch(int WW) { return (WW + 3 + 3) & ~3; }
+__host__ __device__ __forceinline__ int trav_chunk_bytes(int WW) { return trav_row_pitch(WW) % 8 == 0 ? 16 : 8; }
 
 // Window bytes (16-byte aligned); the block's root node records (uint4 [MAX_TREES]) follow it.
 __host__ __device__ __forceinline__ int trav_window_bytes(int WW, int WH) {
@@ -664,7 +670,6 @@ __host__ __device__ __forceinline__ int trav_window_bytes(int WW, int WH) {
 }
 
 constexpr int BUF_WORD3 = 0x00020000;  // raw buffer resource word 3 (gfx950: 32-bit data format)
-typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
 struct TravArgs {
   const FaceDesc* faces;
@@ -679,16 +684,17 @@ struct TravArgs {
   int32_t* leaf_out;
 };
 
-template <bool HP, int G>
+template <bool HP, int G, int CB>
 __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* win = reinterpret_cast<uint16_t*>(smem);
-  constexpr int NW = TRAV_NW, NS = TRAV_NS, U = TRAV_U, GG = G * G;
+  constexpr int NW = TRAV_NW, NS = TRAV_NS, U = TravStage<CB>::U, GG = G * G;
+  typedef typename TravStage<CB>::T chunk_t;
   const int tid = threadIdx.x;
   // window: WW integral columns x WH rows (steps may differ per axis: step_y, C4's (2, 1) grid)
   const int step = A.step, stepy = A.step_y, WW = 32 + step * (G - 1), WH = 32 + stepy * (G - 1);
-  const int LW = trav_row_pitch(WW), nq = LW >> 2;
-  const int total = NCH * WH * nq;  // 8-byte chunks per window (host guarantees <= NS * U)
+  const int LW = trav_row_pitch(WW), nq = LW * 2 / CB;
+  const int total = NCH * WH * nq;  // chunks per window (host guarantees <= NS * U)
   uint4* root_rec = reinterpret_cast<uint4*>(smem + trav_window_bytes(WW, WH));  // [t]: tree t's root
   // XCD-contiguous, face-major block range of this workgroup's XCD; workgroups of one XCD stride it
   const int N = A.n_faces * A.bpf, xcd = blockIdx.x & 7, k = blockIdx.x >> 3, nk = gridDim.x >> 3;
@@ -826,11 +832,11 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   int lb = start + k;
   if (lb >= end) return;
   if (tid >= NW) {
-    // Staging: chunk i = (channel c, window row r, 4-column group q), i = (c * WH + r) * nq + q, goes
+    // Staging: chunk i = (channel c, window row r, 8-column group q), i = (c * WH + r) * nq + q, goes
     // to LDS chunk i; staging thread s owns chunks s + u * NS.  Their face-relative source byte
     // offsets c * plane + r * PITCH * 2 + q * 8 are computed once (every face of a batch has the
     // same plane stride, TravArgs::plane), so a block costs one load per chunk.
-    v2u st[U];
+    chunk_t st[U];
     int voff[U];
     uint4 root_nd = make_uint4(LEAF_BIT, 0u, 0u, 0u);
     auto stage_offsets = [&](int plane_b) {
@@ -839,7 +845,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       int q = s % nq, r = (s / nq) % WH, c = s / (nq * WH);
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        voff[u] = min(c, NCH) * plane_b + r * (PITCH * 2) + q * 8;
+        voff[u] = min(c, NCH) * plane_b + r * (PITCH * 2) + q * CB;
         q += dq;
         int cr = q >= nq;
         q -= cr ? nq : 0;
@@ -872,12 +878,13 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
 #if FFD_TRAV_SLEEP
         if (u % FFD_TRAV_SLEEP_GROUP == 0 && u > 0) __builtin_amdgcn_s_sleep(FFD_TRAV_SLEEP);
 #endif
-        st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff[u], base_b, 0);
+        if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff[u], base_b, 0);
+        else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff[u], base_b, 0);
       }
     };
     auto commit = [&](const Blk& B) {
       if (!B.ok) return;
-      v2u* dst = reinterpret_cast<v2u*>(win);
+      chunk_t* dst = reinterpret_cast<chunk_t*>(win);
       const int s = tid - NW;
       if (s < B.T) root_rec[s] = root_nd;
 #pragma unroll
@@ -1316,7 +1323,9 @@ int traverse_lds_bytes(int G, int step, int step_y) {
 
 bool traverse_window_fits(int G, int step, int step_y, int lds_cap) {
   const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1);
-  return traverse_lds_bytes(G, step, step_y) <= lds_cap && NCH * WH * (trav_row_pitch(WW) / 4) <= TRAV_NS * TRAV_U;
+  const int cb = trav_chunk_bytes(WW);
+  return traverse_lds_bytes(G, step, step_y) <= lds_cap &&
+         NCH * WH * (trav_row_pitch(WW) * 2 / cb) <= TRAV_NS * (cb == 16 ? TravStage<16>::U : TravStage<8>::U);
 }
 
 void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* nodes, const int32_t* roots,
@@ -1327,7 +1336,11 @@ void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, cons
   TravArgs A{faces, n, bpf, nodes, roots, state, ntrees_hp, step, step_y, (int)plane, chan, leaf_out};
   const int lds = traverse_lds_bytes(G, step, step_y);
   const int grid = std::max(8, n_wg & ~7);
-#define FFD_TRAV(HPV, GV) k_traverse<HPV, GV><<<grid, TRAV_NT, lds, s>>>(A)
+#define FFD_TRAV(HPV, GV)                                                                              \
+  do {                                                                                                 \
+    if (trav_chunk_bytes(32 + step * (GV - 1)) == 16) k_traverse<HPV, GV, 16><<<grid, TRAV_NT, lds, s>>>(A); \
+    else k_traverse<HPV, GV, 8><<<grid, TRAV_NT, lds, s>>>(A);                                          \
+  } while (0)
   if (hp) {
     if (G == 3) FFD_TRAV(true, 3); else if (G == 5) FFD_TRAV(true, 5); else FFD_TRAV(true, 4);
   } else {
@@ -1338,9 +1351,12 @@ void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, cons
 
 hipError_t set_traverse_lds_limit(int bytes) {
   hipError_t e = hipSuccess;
-  const void* fns[] = {(const void*)k_traverse<true, 3>, (const void*)k_traverse<true, 4>,
-                       (const void*)k_traverse<true, 5>, (const void*)k_traverse<false, 3>,
-                       (const void*)k_traverse<false, 4>, (const void*)k_traverse<false, 5>};
+  const void* fns[] = {(const void*)k_traverse<true, 3, 8>,  (const void*)k_traverse<true, 4, 8>,
+                       (const void*)k_traverse<true, 5, 8>,  (const void*)k_traverse<false, 3, 8>,
+                       (const void*)k_traverse<false, 4, 8>, (const void*)k_traverse<false, 5, 8>,
+                       (const void*)k_traverse<true, 3, 16>,  (const void*)k_traverse<true, 4, 16>,
+                       (const void*)k_traverse<true, 5, 16>,  (const void*)k_traverse<false, 3, 16>,
+                       (const void*)k_traverse<false, 4, 16>, (const void*)k_traverse<false, 5, 16>};
   for (const void* f : fns) {
     hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (r != hipSuccess) e = r;
