@@ -8,10 +8,10 @@
  * glibc's and the GPU's (ocml) exponentials are both faithful (<1 ulp) but not
  * bitwise identical, and the head-pose tree selection takes floor(area*20)
  * (FaceForest.cpp:243), so a 1-ulp difference could flip a tree choice.  The
- * restatement therefore DEFINES exp as the deterministic routine below
- * (Cody-Waite reduction + degree-13 Taylor/Horner, no FMA contraction), used
- * by both sides.  Its accuracy against libm is checked in
- * tests/test_numerics.py (|err| <= 2 ulp).
+ * restatement therefore DEFINES exp as the deterministic routines below
+ * (Cody-Waite reduction + Taylor polynomial in explicit fma Horner steps),
+ * used by both sides.  Their accuracy against libm is checked in
+ * tests/test_numerics.py (exp: |err| <= 2 ulp; expf: <= 1 ulp of the float).
  *
  * Everything here is IEEE binary64/binary32 arithmetic with round-to-nearest
  * and no contraction; both the oracle (g++ -ffp-contract=off) and the kernels
@@ -36,36 +36,70 @@
 #define FFD_LDEXP(x, k) ldexp((x), (k))
 #endif
 
-/* exp(x) in binary64. */
-FFD_HD double ffd_exp(double x) {
-  if (x != x) return x;                               /* NaN */
-  if (x > 709.782712893384) return HUGE_VAL;           /* overflow */
-  if (x < -745.1332191019412) return 0.0;              /* underflow */
+#ifdef __cplusplus
+#define FFD_FMA(a, b, c) std::fma((a), (b), (c))
+#else
+#define FFD_FMA(a, b, c) fma((a), (b), (c))
+#endif
+
+/* Cody-Waite reduction x = k ln2 + r, |r| <= ln2/2 (shared by both routines). */
+FFD_HD double ffd_exp_reduce(double x, int* k) {
   const double log2e = 1.4426950408889634074;
   const double ln2_hi = 6.93147180369123816490e-01;   /* 0x3FE62E42FEE00000 */
   const double ln2_lo = 1.90821492927058770002e-10;   /* 0x3DEA39EF35793C76 */
   double kd = FFD_RINT(x * log2e);
-  int k = (int)kd;
+  *k = (int)kd;
   double hi = x - kd * ln2_hi; /* exact: kd*ln2_hi has <= 43 significant bits */
-  double r = hi - kd * ln2_lo;
-  double p = 1.0 / 6227020800.0;           /* 1/13! */
-  p = p * r + 1.0 / 479001600.0;           /* 1/12! */
-  p = p * r + 1.0 / 39916800.0;            /* 1/11! */
-  p = p * r + 1.0 / 3628800.0;             /* 1/10! */
-  p = p * r + 1.0 / 362880.0;              /* 1/9!  */
-  p = p * r + 1.0 / 40320.0;               /* 1/8!  */
-  p = p * r + 1.0 / 5040.0;                /* 1/7!  */
-  p = p * r + 1.0 / 720.0;                 /* 1/6!  */
-  p = p * r + 1.0 / 120.0;                 /* 1/5!  */
-  p = p * r + 1.0 / 24.0;                  /* 1/4!  */
-  p = p * r + 1.0 / 6.0;                   /* 1/3!  */
-  p = p * r + 0.5;                         /* 1/2!  */
-  p = p * r + 1.0;
-  p = p * r + 1.0;
+  return hi - kd * ln2_lo;
+}
+
+/* exp(x) in binary64: degree-13 Taylor polynomial of the reduced argument, fma Horner steps. */
+FFD_HD double ffd_exp(double x) {
+  if (x != x) return x;                               /* NaN */
+  if (x > 709.782712893384) return HUGE_VAL;           /* overflow */
+  if (x < -745.1332191019412) return 0.0;              /* underflow */
+  int k;
+  const double r = ffd_exp_reduce(x, &k);
+  double p = 1.0 / 6227020800.0;                      /* 1/13! */
+  p = FFD_FMA(p, r, 1.0 / 479001600.0);               /* 1/12! */
+  p = FFD_FMA(p, r, 1.0 / 39916800.0);                /* 1/11! */
+  p = FFD_FMA(p, r, 1.0 / 3628800.0);                 /* 1/10! */
+  p = FFD_FMA(p, r, 1.0 / 362880.0);                  /* 1/9!  */
+  p = FFD_FMA(p, r, 1.0 / 40320.0);                   /* 1/8!  */
+  p = FFD_FMA(p, r, 1.0 / 5040.0);                    /* 1/7!  */
+  p = FFD_FMA(p, r, 1.0 / 720.0);                     /* 1/6!  */
+  p = FFD_FMA(p, r, 1.0 / 120.0);                     /* 1/5!  */
+  p = FFD_FMA(p, r, 1.0 / 24.0);                      /* 1/4!  */
+  p = FFD_FMA(p, r, 1.0 / 6.0);                       /* 1/3!  */
+  p = FFD_FMA(p, r, 0.5);                             /* 1/2!  */
+  p = FFD_FMA(p, r, 1.0);
+  p = FFD_FMA(p, r, 1.0);
   return FFD_LDEXP(p, k);
 }
 
-/* expf(x) in binary32, defined as the binary32 rounding of ffd_exp. */
-FFD_HD float ffd_expf(float x) { return (float)ffd_exp((double)x); }
+/* expf(x) in binary32 (MeanShift weights, MeanShift.hpp:106-135): the binary32 rounding of a
+ * degree-11 Taylor evaluation in binary64 (truncation error < 1e-14 relative, so the result is
+ * the correctly rounded expf except within 1e-14 of a rounding boundary). */
+FFD_HD float ffd_expf(float xf) {
+  const double x = (double)xf;
+  if (x != x) return xf;                               /* NaN */
+  if (x > 88.8) return HUGE_VALF;                      /* overflow */
+  if (x < -104.0) return 0.0f;                         /* underflow (below the smallest subnormal) */
+  int k;
+  const double r = ffd_exp_reduce(x, &k);
+  double p = 1.0 / 39916800.0;                         /* 1/11! */
+  p = FFD_FMA(p, r, 1.0 / 3628800.0);
+  p = FFD_FMA(p, r, 1.0 / 362880.0);
+  p = FFD_FMA(p, r, 1.0 / 40320.0);
+  p = FFD_FMA(p, r, 1.0 / 5040.0);
+  p = FFD_FMA(p, r, 1.0 / 720.0);
+  p = FFD_FMA(p, r, 1.0 / 120.0);
+  p = FFD_FMA(p, r, 1.0 / 24.0);
+  p = FFD_FMA(p, r, 1.0 / 6.0);
+  p = FFD_FMA(p, r, 0.5);
+  p = FFD_FMA(p, r, 1.0);
+  p = FFD_FMA(p, r, 1.0);
+  return (float)FFD_LDEXP(p, k);
+}
 
 #endif /* FFD_NUMERICS_H */

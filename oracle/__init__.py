@@ -62,6 +62,8 @@ def lib():
         L.oracle_area_under_curve.restype = ctypes.c_double
         L.oracle_exp.argtypes = [ctypes.c_double]
         L.oracle_exp.restype = ctypes.c_double
+        L.oracle_expf.argtypes = [ctypes.c_float]
+        L.oracle_expf.restype = ctypes.c_float
         _lib = L
     return _lib
 
@@ -178,3 +180,7 @@ def area_under_curve(x1, x2, mean, std):
 
 def exp(x):
     return lib().oracle_exp(x)
+
+
+def expf(x):
+    return lib().oracle_expf(x)

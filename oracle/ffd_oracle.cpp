@@ -641,6 +641,7 @@ double oracle_area_under_curve(float x1, float x2, double mean, double std_) {
 }
 
 double oracle_exp(double x) { return ffd_exp(x); }
+float oracle_expf(float x) { return ffd_expf(x); }
 
 int oracle_analyze_face(const uint8_t* bgr, int32_t iw, int32_t ih, int32_t stride, int32_t bx, int32_t by,
                         int32_t bw, int32_t bh, int32_t threads, oracle_face* out, oracle_trace* tr) {

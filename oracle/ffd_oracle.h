@@ -69,6 +69,7 @@ int oracle_gabor_kernel(int32_t index, float* real, float* imag, int32_t* width)
 int oracle_gabor_mag(const uint8_t* face, int32_t w, int32_t h, int32_t index, float* mag);
 double oracle_area_under_curve(float x1, float x2, double mean, double std_);
 double oracle_exp(double x);
+float oracle_expf(float x);
 
 #ifdef __cplusplus
 }

@@ -57,6 +57,20 @@ def test_ffd_exp_matches_libm(oracle_mod):
     assert oracle_mod.exp(-1e6) == 0.0 and oracle_mod.exp(1e6) == math.inf
 
 
+def test_ffd_expf_within_one_ulp_of_correctly_rounded(oracle_mod):
+    """ffd_expf (MeanShift weights) is within 1 ulp of the correctly rounded binary32 exp over the
+    MeanShift argument range -d/10, d in [0, 400], and a few wider points."""
+    rng = np.random.default_rng(1)
+    xs = np.concatenate([rng.uniform(-40, 0, 20000), rng.uniform(-103, 88, 2000), [0.0, -1e-7, -87.0]])
+    for x in xs.astype(np.float32):
+        got = np.float32(oracle_mod.expf(float(x)))
+        ref = np.float32(math.exp(float(x)))  # float64 exp, then one rounding to float32
+        if ref == 0 or got == 0:
+            assert abs(float(got) - float(ref)) <= 2 * 1.4e-45
+            continue
+        assert abs(float(got) - float(ref)) <= float(np.spacing(ref)), (x, got, ref)
+
+
 def test_sqrt_2pi_literal():
     assert 2.5066282746310002 == math.sqrt(2 * math.pi)
 
