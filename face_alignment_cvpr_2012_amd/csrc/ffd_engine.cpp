@@ -494,14 +494,13 @@ void ffd_engine::build_gabor() {
     for (int t = -R; t <= R; t++) {
       const int at = t < 0 ? -t : t;
       auto hs = [&](int p) { return t < 0 ? -s.hs[p][at] : s.hs[p][at]; };
-      float* e = h + 20 * (t + R);
+      float* e = h + 16 * (t + R);
       e[0] = s.hc[0][at]; e[1] = hs(0);
       e[2] = s.g[at]; e[3] = s.g[at];
-      e[4] = s.hc[1][at]; e[5] = s.hc[1][at]; e[6] = -hs(1); e[7] = hs(1);
-      e[8] = s.hc[2][at]; e[9] = s.hc[2][at]; e[10] = -hs(2); e[11] = hs(2);
-      e[12] = hs(2); e[13] = -hs(2);
-      e[14] = s.hc[3][at]; e[15] = s.hc[3][at]; e[16] = -hs(3); e[17] = hs(3);
-      e[18] = hs(3); e[19] = -hs(3);
+      for (int p = 1; p <= 3; p++) {
+        e[4 * p] = e[4 * p + 1] = s.hc[p][at];
+        e[4 * p + 2] = e[4 * p + 3] = hs(p);
+      }
     }
   }
   upload(gabor_coef, coef, main_stream());

@@ -202,11 +202,8 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // (unsigned order == float order for m >= +0).  Every magnitude store of the workgroup precedes
 // the first barrier here.
 template <int NWV>
-__device__ __forceinline__ void gabor_normalise_integrate(const FaceDesc& fd, int nu, uint32_t (&mn)[7],
-                                                          uint32_t (&mx)[7], const float* __restrict__ mag,
-                                                          uint16_t* __restrict__ chan) {
+__device__ __forceinline__ void gabor_minmax_scale(uint32_t (&mn)[7], uint32_t (&mx)[7], float* s_sf, float* s_hf) {
   __shared__ uint32_t red[NWV][14];
-  __shared__ float s_sf[7], s_hf[7];
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
 #pragma unroll
   for (int o = 0; o < 7; o++) {
@@ -233,6 +230,20 @@ __device__ __forceinline__ void gabor_normalise_integrate(const FaceDesc& fd, in
     s_hf[o] = (float)shift;
   }
   __syncthreads();
+}
+
+// convertTo(CV_8U, 255) of a normalised magnitude (FeatureChannelFactory.hpp:276)
+__device__ __forceinline__ uint32_t gabor_quantise(float m, float sf, float hf) {
+  return (uint32_t)sat_u8(cv_round((m * sf + hf) * 255.f + 0.f));
+}
+
+template <int NWV>
+__device__ __forceinline__ void gabor_normalise_integrate(const FaceDesc& fd, int nu, uint32_t (&mn)[7],
+                                                          uint32_t (&mx)[7], const float* __restrict__ mag,
+                                                          uint16_t* __restrict__ chan) {
+  __shared__ float s_sf[7], s_hf[7];
+  gabor_minmax_scale<NWV>(mn, mx, s_sf, s_hf);
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   for (int o = wv; o < 7; o += NWV) {
     const int lane = ln, x0 = 2 * lane, FW = fd.W, FH = fd.H;
     const float sf = s_sf[o], hf = s_hf[o];
@@ -247,8 +258,8 @@ __device__ __forceinline__ void gabor_normalise_integrate(const FaceDesc& fd, in
                                             : make_float2(0.f, 0.f);
 #pragma unroll
                     for (int b = 0; b < RB; b++) {
-                      v0[b] = (x0 < FW) ? (uint32_t)sat_u8(cv_round((mv[b].x * sf + hf) * 255.f + 0.f)) : 0u;
-                      v1[b] = (x0 + 1 < FW) ? (uint32_t)sat_u8(cv_round((mv[b].y * sf + hf) * 255.f + 0.f)) : 0u;
+                      v0[b] = (x0 < FW) ? gabor_quantise(mv[b].x, sf, hf) : 0u;
+                      v1[b] = (x0 + 1 < FW) ? gabor_quantise(mv[b].y, sf, hf) : 0u;
                     }
                   });
   }
@@ -356,12 +367,13 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restric
 // Coefficient block (floats, host-built by ffd_engine build_gabor from ffd_gabor_sep):
 //   [0]                 c
 //   V_OFF + 12 t        t = 0..R: g, 0, (vc_q, vs_q) q = 1..4, 0, 0
-//   H_OFF + 20 (t + R)  t = -R..R: (hc0, hs0), (g, g), mu1 (hc1, hc1, -hs1, hs1), mu2 (hc2, hc2, -hs2, hs2),
-//                       mu6 (hs2, -hs2), mu3 (hc3, hc3, -hs3, hs3), mu5 (hs3, -hs3)    [hs_p(t) odd in t]
+//   H_OFF + 16 (t + R)  t = -R..R: (hc0, hs0), (g, g), then for p = 1..3 (hc_p, hc_p, hs_p, hs_p)
+//                       [hs_p(t) odd in t]
 constexpr int GS_THREADS = 256, GS_BY = 8;
 #ifndef FFD_GABOR_PROBE
 #define FFD_GABOR_PROBE 0
 #endif
+
 
 template <int R> struct GSep {
   static constexpr int GP = (PITCH + 2 * R + 3) / 4 * 4;  // gray band row pitch (floats)
@@ -450,13 +462,14 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
     if (y0 + GS_BY < FH) stage(y0 + GS_BY);
     // ---- H pass: thread = (row hr, column quad cq), outputs x = 4 cq + k
     const int hr = tid >> 5, cq = tid & 31, y = y0 + hr, x0 = 4 * cq;
-    f2 acc[4][7];
+    f2 acc0[4], acc4[4], ac[3][4], be[3][4];  // mu 0, mu 4; per horizontal set p = 1..3: (A, C), (B, E)
     float dc[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       dc[k] = 0.f;
+      acc0[k] = acc4[k] = f2{0.f, 0.f};
 #pragma unroll
-      for (int o = 0; o < 7; o++) acc[k][o] = f2{0.f, 0.f};
+      for (int p = 0; p < 3; p++) ac[p][k] = be[p][k] = f2{0.f, 0.f};
     }
     const int rb = hr * C::VP + cq;
     // V value at padded column x0 + u + R: quad-split slot (u + R) & 3, offset (u + R) >> 2
@@ -469,9 +482,9 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
       for (int k = 0; k < 4; k++) {
         const int t = u - k;
         if (t < -R || t > R) continue;
-        const float* h = chh + 20 * (t + R);
+        const float* h = chh + 16 * (t + R);
         dc[k] = fmaf(h[2], v, dc[k]);
-        acc[k][0] = __builtin_elementwise_fma(f2{h[0], h[1]}, f2{v, v}, acc[k][0]);
+        acc0[k] = __builtin_elementwise_fma(f2{h[0], h[1]}, f2{v, v}, acc0[k]);
       }
     }
     // q = 4: mu 4
@@ -482,54 +495,36 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
       for (int k = 0; k < 4; k++) {
         const int t = u - k;
         if (t < -R || t > R) continue;
-        const float* h = chh + 20 * (t + R);
-        acc[k][4] = __builtin_elementwise_fma(f2{h[2], h[3]}, v, acc[k][4]);
+        const float* h = chh + 16 * (t + R);
+        acc4[k] = __builtin_elementwise_fma(f2{h[2], h[3]}, v, acc4[k]);
       }
     }
-    // q = 1: mu 1
+    // q = p = 1, 2, 3: the four sums shared by mu and its mirror (mu 2 / 6, mu 3 / 5)
 #pragma unroll
-    for (int u = -R; u <= R + 3; u++) {
-      const f2 v = vq[0][GS_IDX(u)], vs = f2{v.y, v.x};
+    for (int p = 0; p < 3; p++) {
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int t = u - k;
-        if (t < -R || t > R) continue;
-        const float* h = chh + 20 * (t + R);
-        acc[k][1] = __builtin_elementwise_fma(f2{h[4], h[5]}, v, acc[k][1]);
-        acc[k][1] = __builtin_elementwise_fma(f2{h[6], h[7]}, vs, acc[k][1]);
+      for (int u = -R; u <= R + 3; u++) {
+        const f2 v = vq[p][GS_IDX(u)], vs = f2{v.y, v.x};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int t = u - k;
+          if (t < -R || t > R) continue;
+          const float* h = chh + 16 * (t + R) + 4 * (p + 1);
+          ac[p][k] = __builtin_elementwise_fma(f2{h[0], h[1]}, v, ac[p][k]);
+          be[p][k] = __builtin_elementwise_fma(f2{h[2], h[3]}, vs, be[p][k]);
+        }
       }
     }
-    // q = 2: mu 2, mu 6
+    f2 acc[4][7];
 #pragma unroll
-    for (int u = -R; u <= R + 3; u++) {
-      const f2 v = vq[1][GS_IDX(u)], vs = f2{v.y, v.x};
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int t = u - k;
-        if (t < -R || t > R) continue;
-        const float* h = chh + 20 * (t + R);
-        const f2 hc = f2{h[8], h[9]};
-        acc[k][2] = __builtin_elementwise_fma(hc, v, acc[k][2]);
-        acc[k][2] = __builtin_elementwise_fma(f2{h[10], h[11]}, vs, acc[k][2]);
-        acc[k][6] = __builtin_elementwise_fma(hc, v, acc[k][6]);
-        acc[k][6] = __builtin_elementwise_fma(f2{h[12], h[13]}, vs, acc[k][6]);
-      }
-    }
-    // q = 3: mu 3, mu 5
-#pragma unroll
-    for (int u = -R; u <= R + 3; u++) {
-      const f2 v = vq[2][GS_IDX(u)], vs = f2{v.y, v.x};
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int t = u - k;
-        if (t < -R || t > R) continue;
-        const float* h = chh + 20 * (t + R);
-        const f2 hc = f2{h[14], h[15]};
-        acc[k][3] = __builtin_elementwise_fma(hc, v, acc[k][3]);
-        acc[k][3] = __builtin_elementwise_fma(f2{h[16], h[17]}, vs, acc[k][3]);
-        acc[k][5] = __builtin_elementwise_fma(hc, v, acc[k][5]);
-        acc[k][5] = __builtin_elementwise_fma(f2{h[18], h[19]}, vs, acc[k][5]);
-      }
+    for (int k = 0; k < 4; k++) {
+      acc[k][0] = acc0[k];
+      acc[k][4] = acc4[k];
+      acc[k][1] = f2{ac[0][k].x - be[0][k].x, ac[0][k].y + be[0][k].y};
+      acc[k][2] = f2{ac[1][k].x - be[1][k].x, ac[1][k].y + be[1][k].y};
+      acc[k][6] = f2{ac[1][k].x + be[1][k].x, ac[1][k].y - be[1][k].y};
+      acc[k][3] = f2{ac[2][k].x - be[2][k].x, ac[2][k].y + be[2][k].y};
+      acc[k][5] = f2{ac[2][k].x + be[2][k].x, ac[2][k].y - be[2][k].y};
     }
 #undef GS_IDX
     if (y < FH) {

@@ -13,7 +13,7 @@ namespace ffd {
 // [re0, im0, ..., re6, im6, 0, 0]; scales 1..4 = the separable factor blocks of k_gabor_sep
 // (layout in ffd_kernels.hip), each 16-B aligned.
 constexpr int GABOR_WIDTHS[5] = {7, 9, 13, 19, 25};
-constexpr int gabor_sep_block(int R) { return (4 + 12 * (R + 1) + 20 * (2 * R + 1) + 3) / 4 * 4; }
+constexpr int gabor_sep_block(int R) { return (4 + 12 * (R + 1) + 16 * (2 * R + 1) + 3) / 4 * 4; }
 constexpr int GABOR_OFF0 = 0;
 constexpr int GABOR_OFF1 = GABOR_OFF0 + 49 * 16;
 constexpr int GABOR_OFF2 = GABOR_OFF1 + gabor_sep_block(4);

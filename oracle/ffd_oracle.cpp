@@ -373,8 +373,9 @@ const ffd_gabor_sep& gabor_sep(int nu) {
 //    Dc = fma(g_|t|, Vg, Dc);
 //    mu 0 (b = 0):  re = fma(hc_0t, Vg, re);  im = fma(hs_0t, Vg, im)
 //    mu 4 (a = 0):  re = fma(g_|t|, Vc, re); im = fma(g_|t|, Vs, im)
-//    other mu, hsv = sgn * hs_pt:  re = fma(hc_pt, Vc, re); im = fma(hc_pt, Vs, im);
-//                                  re = fma(-hsv, Vs, re);  im = fma(hsv, Vc, im)
+//    other mu (horizontal set p): four chains A = fma(hc_pt, Vc, A), C = fma(hc_pt, Vs, C),
+//      B = fma(hs_pt, Vs, B), E = fma(hs_pt, Vc, E); then with the sign of a (mu 5, 6: -1)
+//      re = A - sgn*B, im = C + sgn*E  (mu and its mirror share the four sums)
 //  then re = fma(-c, Dc, re)   (the reference kernel's DC term -c g(x) g(y)).
 void gabor_sep_mag(const uint8_t* img, int w, int h, int index, float* mag) {
   const int nu = index / 7, mu = index % 7;
@@ -404,7 +405,7 @@ void gabor_sep_mag(const uint8_t* img, int w, int h, int index, float* mag) {
     }
   for (int y = 0; y < h; y++)
     for (int x = 0; x < w; x++) {
-      float re = 0.f, im = 0.f, dc = 0.f;
+      float re = 0.f, im = 0.f, dc = 0.f, A = 0.f, B = 0.f, C = 0.f, E = 0.f;
       for (int t = -R; t <= R; t++) {
         const size_t i = (size_t)y * w + reflect101(x + t, w);
         const int at = t < 0 ? -t : t;
@@ -418,12 +419,16 @@ void gabor_sep_mag(const uint8_t* img, int w, int h, int index, float* mag) {
           re = std::fmaf(s.g[at], Vc[i], re);
           im = std::fmaf(s.g[at], Vs[i], im);
         } else {
-          const float hc = s.hc[p][at], hsv = sgn * (t < 0 ? -s.hs[p][at] : s.hs[p][at]);
-          re = std::fmaf(hc, Vc[i], re);
-          im = std::fmaf(hc, Vs[i], im);
-          re = std::fmaf(-hsv, Vs[i], re);
-          im = std::fmaf(hsv, Vc[i], im);
+          const float hc = s.hc[p][at], hs = t < 0 ? -s.hs[p][at] : s.hs[p][at];
+          A = std::fmaf(hc, Vc[i], A);
+          C = std::fmaf(hc, Vs[i], C);
+          B = std::fmaf(hs, Vs[i], B);
+          E = std::fmaf(hs, Vc[i], E);
         }
+      }
+      if (mu != 0 && mu != 4) {
+        re = sgn > 0 ? A - B : A + B;
+        im = sgn > 0 ? C + E : C - E;
       }
       re = std::fmaf(-s.c, dc, re);
       const float r2 = re * re, i2 = im * im;
