@@ -114,12 +114,18 @@ struct Geometry {
 struct Workspace {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
+  // channel-stage fork: the five Gabor kernels and k_integral are independent, so they are spread
+  // over `stream` and these streams (joined back before the head-pose traversal)
+  std::vector<hipStream_t> fork;
+  std::vector<hipEvent_t> fork_ev;  // [0]: gray ready; [1 + i]: fork stream i done
   bool pending = false;
   DevBuf faces, gray, mag, chan, hpleaf, mpleaf, votes, state, ms_mean, vote_counts;
   std::vector<FaceDesc> h_fds;  // host staging, reused only after `done`
   std::vector<FaceDesc> desc;   // descriptors of the chunk last run here (ffd_get_trace)
   int first = 0, count = 0;
   ~Workspace() {
+    for (auto e : fork_ev) (void)hipEventDestroy(e);
+    for (auto f : fork) (void)hipStreamDestroy(f);
     if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -131,6 +137,7 @@ struct ffd_engine {
   ffd_engine_desc desc{};
   int max_chunk = 4096;
   int n_streams = 1;
+  int channel_streams = 1;  // streams the channel stage is spread over (FFD_CHANNEL_STREAMS; 2-4 measured no gain)
   // traversal tuning: patch block edge G (a workgroup walks all trees of a G x G block of patches
   // over an LDS copy of the block's integral window) and the persistent workgroups (one per CU).
   // Overridable with FFD_TRAV_G_{HP,FFD} / FFD_TRAV_WG / FFD_CHUNK / FFD_STREAMS.
@@ -176,7 +183,10 @@ struct ffd_engine {
     pending.push_back(p);
   }
   void sync_all() {
-    for (auto& w : ws) HIP_CHECK(hipStreamSynchronize(w->stream));
+    for (auto& w : ws) {
+      for (auto f : w->fork) HIP_CHECK(hipStreamSynchronize(f));
+      HIP_CHECK(hipStreamSynchronize(w->stream));
+    }
   }
   void resolve() {
     if (pending.empty()) return;
@@ -549,14 +559,28 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
 
   const FaceDesc* dfd = w.faces.as<FaceDesc>();
   stage(0, st, [&] { launch_gray_resize(dfd, n, d_images, w.gray.as<uint8_t>(), st); });
-  for (int nu = 4; nu >= 0; nu--)  // largest kernels first
-    stage(1 + (4 - nu), st, [&] {
+  // channel stage: Gabor scales 4..0 and the gray / Sobel integrals, dealt over the fork streams
+  const int nfork = (int)w.fork.size();
+  if (nfork > 0) {
+    HIP_CHECK(hipEventRecord(w.fork_ev[0], st));
+    for (auto f : w.fork) HIP_CHECK(hipStreamWaitEvent(f, w.fork_ev[0], 0));
+  }
+  auto cs = [&](int i) { return i % (nfork + 1) == 0 ? st : w.fork[i % (nfork + 1) - 1]; };
+  for (int nu = 4; nu >= 0; nu--) {  // largest kernels first
+    const hipStream_t s2 = cs(4 - nu);
+    stage(1 + (4 - nu), s2, [&] {
       launch_gabor(nu, dfd, n, w.gray.as<uint8_t>(), gabor_coef.as<float>(), w.mag.as<float>(),
-                   w.chan.as<uint16_t>(), st);
+                   w.chan.as<uint16_t>(), s2);
     });
-  stage(6, st, [&] {
-    launch_integral(dfd, n, w.gray.as<uint8_t>(), w.chan.as<uint16_t>(), st);
-  });
+  }
+  {
+    const hipStream_t s2 = cs(5);
+    stage(6, s2, [&] { launch_integral(dfd, n, w.gray.as<uint8_t>(), w.chan.as<uint16_t>(), s2); });
+  }
+  for (int i = 0; i < nfork; i++) {
+    HIP_CHECK(hipEventRecord(w.fork_ev[1 + i], w.fork[i]));
+    HIP_CHECK(hipStreamWaitEvent(st, w.fork_ev[1 + i], 0));
+  }
   stage(7, st, [&] {
     launch_traverse(true, dfd, n, blocks_per_face(fds, true, trav_g_hp), trav_g_hp, hp_wnodes.as<uint4>(),
                     hp_roots.as<int32_t>(), nullptr, hp_trees, desc.hp_option.step_size, desc.hp_option.step_size,
@@ -700,6 +724,7 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   if (const char* v = std::getenv("FFD_TRAV_G_HP")) e->trav_g_hp = std::max(3, std::min(5, std::atoi(v)));
   if (const char* v = std::getenv("FFD_TRAV_G_FFD")) e->trav_g_mp = std::max(3, std::min(5, std::atoi(v)));
   if (const char* v = std::getenv("FFD_TRAV_WG")) e->trav_wg = std::max(8, std::atoi(v));
+  if (const char* v = std::getenv("FFD_CHANNEL_STREAMS")) e->channel_streams = std::max(1, std::min(4, std::atoi(v)));
   if (const char* v = std::getenv("FFD_CHUNK")) e->max_chunk = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("FFD_STREAMS")) e->n_streams = std::max(1, std::min(8, std::atoi(v)));
   if (d->max_chunk_faces > 0) e->max_chunk = d->max_chunk_faces;
@@ -713,6 +738,16 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
       auto w = std::make_unique<Workspace>();
       HIP_CHECK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
       HIP_CHECK(hipEventCreateWithFlags(&w->done, hipEventDisableTiming));
+      for (int j = 1; j < e->channel_streams; j++) {
+        hipStream_t f;
+        HIP_CHECK(hipStreamCreateWithFlags(&f, hipStreamNonBlocking));
+        w->fork.push_back(f);
+      }
+      for (int j = 0; j < e->channel_streams; j++) {
+        hipEvent_t ev;
+        HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        w->fork_ev.push_back(ev);
+      }
       e->ws.push_back(std::move(w));
     }
     e->load_model(d->model_path);
