@@ -252,6 +252,7 @@ struct ffd_engine {
     walk_nodes(hp_nodes_h, hp_wnodes, trav_g_hp, desc.hp_option.step_size, desc.hp_option.step_size);
     walk_nodes(mp_nodes_h, mp_wnodes, trav_g_mp, desc.mp_option.step_size, mp_step_y());
     HIP_CHECK(set_traverse_lds_limit(cap));
+    HIP_CHECK(set_gabor_lds_limit(96 * 1024));  // padded u8 face of up to MAX_FACE_H rows
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, device));
     if (!std::getenv("FFD_TRAV_WG")) trav_wg = std::max(8, prop.multiProcessorCount);
@@ -527,8 +528,12 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   int64_t gray_b = 0, mag_e = 0, ch_e = 0, hp_e = 0, mp_e = 0, vote_e = 0;
   // one channel plane stride for the whole batch (the traversal's window staging assumes it)
   int64_t plane = PITCH;
+  int max_h = 1;
   for (const auto& f : fds)
-    if (f.valid) plane = std::max(plane, (int64_t)(f.H + 1) * PITCH);
+    if (f.valid) {
+      plane = std::max(plane, (int64_t)(f.H + 1) * PITCH);
+      max_h = std::max(max_h, f.H);
+    }
   for (auto& f : fds) {
     if (!f.valid) continue;
     f.gray_off = gray_b;
@@ -569,7 +574,7 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   for (int nu = 4; nu >= 0; nu--) {  // largest kernels first
     const hipStream_t s2 = cs(4 - nu);
     stage(1 + (4 - nu), s2, [&] {
-      launch_gabor(nu, dfd, n, w.gray.as<uint8_t>(), gabor_coef.as<float>(), w.mag.as<float>(),
+      launch_gabor(nu, dfd, n, max_h, w.gray.as<uint8_t>(), gabor_coef.as<float>(), w.mag.as<float>(),
                    w.chan.as<uint16_t>(), s2);
     });
   }
@@ -955,7 +960,7 @@ ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t
     const FaceDesc* dfd = w.faces.as<FaceDesc>();
     launch_gray_resize(dfd, 1, e->scratch_a.as<uint8_t>(), w.gray.as<uint8_t>(), w.stream);
     for (int nu = 4; nu >= 0; nu--)
-      launch_gabor(nu, dfd, 1, w.gray.as<uint8_t>(), e->gabor_coef.as<float>(), w.mag.as<float>(),
+      launch_gabor(nu, dfd, 1, H, w.gray.as<uint8_t>(), e->gabor_coef.as<float>(), w.mag.as<float>(),
                    w.chan.as<uint16_t>(), w.stream);
     launch_integral(dfd, 1, w.gray.as<uint8_t>(), w.chan.as<uint16_t>(), w.stream);
     HIP_CHECK(hipGetLastError());

@@ -376,8 +376,7 @@ constexpr int GS_THREADS = 256, GS_BY = 8;
 
 
 template <int R> struct GSep {
-  static constexpr int GP = (PITCH + 2 * R + 3) / 4 * 4;  // gray band row pitch (floats)
-  static constexpr int BR = GS_BY + 2 * R;                // gray band rows
+  static constexpr int GP = (PITCH + 2 * R + 3) / 4 * 4;  // padded gray row pitch (bytes)
   static constexpr int QS = 32 + ((3 + 2 * R) >> 2);      // quad-split slots per phase
   static constexpr int VP = 4 * QS;                       // V row pitch (elements) >= W + 2R
   static constexpr int SC = GP;                           // staging / V-pass column range
@@ -393,7 +392,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
   constexpr int R = (W - 1) / 2;
   using C = GSep<R>;
   constexpr int NU = W == 9 ? 1 : W == 13 ? 2 : W == 19 ? 3 : 4;
-  __shared__ float gt[C::BR * C::GP];
+  extern __shared__ __attribute__((aligned(16))) uint8_t gface[];  // (H + 2R) x GP reflect-101 padded face
   __shared__ float vg[GS_BY * C::VP];
   __shared__ f2 vq[4][GS_BY * C::VP];
   const FaceDesc fd = faces[blockIdx.x];
@@ -408,48 +407,47 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
 #pragma unroll
   for (int o = 0; o < 7; o++) mn[o] = mx[o] = 0xFFFFFFFFu;
 
-  auto stage = [&](int y0) {  // (row, column quad) items, float4 LDS stores
+  {  // the whole reflect-101 padded face, once: (row, 4-column group) items, u32 LDS stores
     constexpr int NQ = C::GP / 4;
-    for (int i = tid; i < C::BR * NQ; i += GS_THREADS) {
+    for (int i = tid; i < (FH + 2 * R) * NQ; i += GS_THREADS) {
       const int r = i / NQ, j = i - r * NQ;
-      const uint8_t* row = g + reflect101(y0 - R + r, FH) * PITCH;
-      float v[4];
+      const uint8_t* row = g + reflect101(r - R, FH) * PITCH;
+      uint32_t v = 0;
 #pragma unroll
       for (int e = 0; e < 4; e++) {
         int x = 4 * j + e - R;
         x = x < 0 ? -x : x;
         x = x >= FW ? 2 * FW - 2 - x : x;
         x = min(max(x, 0), FW - 1);  // columns past W + R (never used) stay in the row
-        v[e] = (float)row[x];
+        v |= (uint32_t)row[x] << (8 * e);
       }
-      *reinterpret_cast<float4*>(&gt[r * C::GP + 4 * j]) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<uint32_t*>(&gface[r * C::GP + 4 * j]) = v;
     }
-  };
+  }
 
-  stage(0);
 #pragma unroll 1
   for (int y0 = 0; y0 < FH; y0 += GS_BY) {
-    __syncthreads();  // the band's gray rows are staged; the previous H pass is done with vg / vq
+    __syncthreads();  // the face is staged; the previous H pass is done with vg / vq
     // ---- V pass
 #pragma unroll 1
     for (int i = tid; i < (FFD_GABOR_PROBE == 3 ? 0 : GS_BY * C::SC); i += GS_THREADS) {
       const int r = i / C::SC, cc = i - r * C::SC;
       if (cc >= NPC) continue;
-      const float* col = &gt[(r + R) * C::GP + cc];
+      const uint8_t* col = &gface[(y0 + r + R) * C::GP + cc];
       float vgv = 0.f;
       f2 vqv[4];
 #pragma unroll
       for (int q = 0; q < 4; q++) vqv[q] = f2{0.f, 0.f};
 #pragma unroll
       for (int t = R; t >= 1; t--) {
-        const float a = col[t * C::GP], b = col[-t * C::GP];
+        const float a = (float)col[t * C::GP], b = (float)col[-t * C::GP];
         const f2 sd = f2{a, a} + f2{b, -b};  // (S, D) = (a + b, a - b), exact
         const float* c = cv + 12 * t;
         vgv = fmaf(c[0], sd.x, vgv);
 #pragma unroll
         for (int q = 0; q < 4; q++) vqv[q] = __builtin_elementwise_fma(f2{c[2 + 2 * q], c[3 + 2 * q]}, sd, vqv[q]);
       }
-      const float p0 = col[0];
+      const float p0 = (float)col[0];
       vgv = fmaf(cv[0], p0, vgv);
 #pragma unroll
       for (int q = 0; q < 4; q++) vqv[q] = __builtin_elementwise_fma(f2{cv[2 + 2 * q], cv[3 + 2 * q]}, f2{p0, p0}, vqv[q]);
@@ -458,8 +456,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
 #pragma unroll
       for (int q = 0; q < 4; q++) vq[q][qi] = vqv[q];
     }
-    __syncthreads();  // V planes ready; the gray band is free
-    if (y0 + GS_BY < FH) stage(y0 + GS_BY);
+    __syncthreads();  // V planes ready
     // ---- H pass: thread = (row hr, column quad cq), outputs x = 4 cq + k
     const int hr = tid >> 5, cq = tid & 31, y = y0 + hr, x0 = 4 * cq;
     f2 acc0[4], acc4[4], ac[3][4], be[3][4];  // mu 0, mu 4; per horizontal set p = 1..3: (A, C), (B, E)
@@ -1271,15 +1268,18 @@ void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uin
   k_gray_resize<<<n, 256, 0, s>>>(faces, images, gray);
 }
 
-void launch_gabor(int nu, const FaceDesc* faces, int n, const uint8_t* gray, const float* coef, float* mag,
+// dynamic LDS of k_gabor_sep: the padded u8 face of the tallest face of the batch
+static int gabor_face_lds(int R, int max_h) { return (max_h + 2 * R) * ((PITCH + 2 * R + 3) / 4 * 4); }
+
+void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t* gray, const float* coef, float* mag,
                   uint16_t* chan, hipStream_t s) {
   if (n <= 0) return;
   const float* c = coef + GABOR_OFFS[nu];
   switch (nu) {
-    case 4: k_gabor_sep<25><<<n, GS_THREADS, 0, s>>>(faces, gray, c, mag, chan); break;
-    case 3: k_gabor_sep<19><<<n, GS_THREADS, 0, s>>>(faces, gray, c, mag, chan); break;
-    case 2: k_gabor_sep<13><<<n, GS_THREADS, 0, s>>>(faces, gray, c, mag, chan); break;
-    case 1: k_gabor_sep<9><<<n, GS_THREADS, 0, s>>>(faces, gray, c, mag, chan); break;
+    case 4: k_gabor_sep<25><<<n, GS_THREADS, gabor_face_lds(12, max_h), s>>>(faces, gray, c, mag, chan); break;
+    case 3: k_gabor_sep<19><<<n, GS_THREADS, gabor_face_lds(9, max_h), s>>>(faces, gray, c, mag, chan); break;
+    case 2: k_gabor_sep<13><<<n, GS_THREADS, gabor_face_lds(6, max_h), s>>>(faces, gray, c, mag, chan); break;
+    case 1: k_gabor_sep<9><<<n, GS_THREADS, gabor_face_lds(4, max_h), s>>>(faces, gray, c, mag, chan); break;
     default: k_gabor7<<<n, GB_THREADS, 0, s>>>(faces, gray, reinterpret_cast<const float4*>(c), mag, chan); break;
   }
 }
@@ -1342,6 +1342,17 @@ void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, cons
     if (G == 3) FFD_TRAV(false, 3); else if (G == 5) FFD_TRAV(false, 5); else FFD_TRAV(false, 4);
   }
 #undef FFD_TRAV
+}
+
+hipError_t set_gabor_lds_limit(int bytes) {
+  hipError_t e = hipSuccess;
+  const void* fns[] = {(const void*)k_gabor_sep<9>, (const void*)k_gabor_sep<13>, (const void*)k_gabor_sep<19>,
+                       (const void*)k_gabor_sep<25>};
+  for (const void* f : fns) {
+    hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (r != hipSuccess) e = r;
+  }
+  return e;
 }
 
 hipError_t set_traverse_lds_limit(int bytes) {

@@ -25,8 +25,10 @@ constexpr int GABOR_OFFS[5] = {GABOR_OFF0, GABOR_OFF1, GABOR_OFF2, GABOR_OFF3, G
 void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s);
 // Gabor scale nu (0..4): magnitudes of the 7 orientations, face-wide min-max normalisation,
 // quantisation and integration of the 7 channels (one workgroup per face)
-void launch_gabor(int nu, const FaceDesc* faces, int n, const uint8_t* gray, const float* coef, float* mag,
+// max_h: the tallest scaled face of the batch (sizes the padded-face LDS copy)
+void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t* gray, const float* coef, float* mag,
                   uint16_t* chan, hipStream_t s);
+hipError_t set_gabor_lds_limit(int bytes);
 // integral channels 0 (gray), 36, 37 (Sobel)
 void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t* chan, hipStream_t s);
 // Re-encode 16-byte nodes as k_traverse's walk nodes for a G x G patch block window (ffd_device.hpp);
