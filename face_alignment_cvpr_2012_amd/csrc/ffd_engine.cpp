@@ -131,6 +131,11 @@ struct Workspace {
   }
 };
 
+namespace {
+void layout_pair_blocks(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots, std::vector<uint4>& out,
+                        std::vector<int32_t>& out_roots);
+}  // namespace
+
 struct ffd_engine {
   std::string err;
   int device = 0;
@@ -150,7 +155,10 @@ struct ffd_engine {
   // device model
   DevBuf gabor_coef, hp_nodes, hp_roots, hp_sizes, hp_m, mp_nodes, mp_roots, mp_sizes, mp_rec;
   DevBuf hp_wnodes, mp_wnodes;       // walk-node encodings for k_traverse (ffd_device.hpp)
+  DevBuf hp_wroots, mp_wroots;       // tree roots in the walk-node arrays
   std::vector<uint4> hp_nodes_h, mp_nodes_h;  // host copies until the walk nodes are built
+  std::vector<int32_t> hp_roots_h, mp_roots_h;
+  bool pair_blocks = true;           // walk-node layout (FFD_NODE_LAYOUT=bfs for plain breadth-first)
   bool vote_rec_compact = false;     // 32-B vote records (else 64-B), see load_model
   int vote_bias_x = 0, vote_bias_y = 0;
 
@@ -241,16 +249,27 @@ struct ffd_engine {
     };
     fit(trav_g_hp, desc.hp_option.step_size, desc.hp_option.step_size);
     fit(trav_g_mp, desc.mp_option.step_size, mp_step_y());
-    auto walk_nodes = [&](std::vector<uint4>& h, DevBuf& d, int G, int step, int step_y) {
+    auto walk_nodes = [&](std::vector<uint4>& h, std::vector<int32_t>& roots, DevBuf& d, DevBuf& droots, int G,
+                          int step, int step_y) {
       std::vector<uint4> wn(h.size());
       if (!encode_walk_nodes(h.data(), h.size(), G, step, step_y, wn.data()))
         throw std::runtime_error("forest does not fit the traversal's walk-node encoding");
+      if (pair_blocks) {
+        std::vector<uint4> pb;
+        std::vector<int32_t> pr;
+        layout_pair_blocks(wn, roots, pb, pr);
+        wn.swap(pb);
+        roots.swap(pr);
+      }
       upload(d, wn, main_stream());
+      upload(droots, roots, main_stream());
       HIP_CHECK(hipStreamSynchronize(main_stream()));
       std::vector<uint4>().swap(h);
+      std::vector<int32_t>().swap(roots);
     };
-    walk_nodes(hp_nodes_h, hp_wnodes, trav_g_hp, desc.hp_option.step_size, desc.hp_option.step_size);
-    walk_nodes(mp_nodes_h, mp_wnodes, trav_g_mp, desc.mp_option.step_size, mp_step_y());
+    walk_nodes(hp_nodes_h, hp_roots_h, hp_wnodes, hp_wroots, trav_g_hp, desc.hp_option.step_size,
+               desc.hp_option.step_size);
+    walk_nodes(mp_nodes_h, mp_roots_h, mp_wnodes, mp_wroots, trav_g_mp, desc.mp_option.step_size, mp_step_y());
     HIP_CHECK(set_traverse_lds_limit(cap));
     HIP_CHECK(set_gabor_lds_limit(96 * 1024));  // padded u8 face of up to MAX_FACE_H rows
     hipDeviceProp_t prop;
@@ -331,6 +350,65 @@ void flatten_forest(const ModelFile& m, const std::string& p, std::vector<uint4>
   if ((int64_t)nodes.size() != (int64_t)nl.count()) throw std::runtime_error("node count mismatch");
 }
 
+// Re-lay breadth-first walk nodes (children adjacent) into 128-byte "pair blocks" so that every
+// second level of a walk is a hit in the cache line the previous level brought in:
+//   root block:    [root, -, children of root, children of slot 2, children of slot 3]
+//   general block: [pair P, children of P.0, children of P.1, -, -]
+// Children of the block's last level start new blocks.  Leaves keep their ordinals; the padding
+// slots are never referenced.  Speed only: every walk visits the same nodes in the same order.
+void layout_pair_blocks(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots, std::vector<uint4>& out,
+                        std::vector<int32_t>& out_roots) {
+  const uint4 pad = make_uint4(LEAF_BIT, 0u, 0u, 0u);
+  out.clear();
+  out_roots.clear();
+  auto internal = [&](uint32_t i) { return !(bfs[i].x & LEAF_BIT); };
+  for (int32_t root : roots) {
+    // (bfs index of a pair's first node, slot of the out node whose child pointer it fills)
+    std::vector<std::pair<uint32_t, int64_t>> queue;
+    auto place = [&](uint32_t src, int64_t dst) {  // copy a node; its child pointer is patched later
+      out[dst] = bfs[src];
+    };
+    const int64_t rb = (int64_t)out.size();
+    out.resize(rb + 8, pad);
+    out_roots.push_back((int32_t)rb);
+    place((uint32_t)root, rb);
+    size_t qi = 0;
+    if (internal((uint32_t)root)) {
+      const uint32_t c = bfs[(uint32_t)root].x;
+      out[rb].x = (uint32_t)(rb + 2);
+      place(c, rb + 2);
+      place(c + 1, rb + 3);
+      for (int j = 0; j < 2; j++) {
+        if (!internal(c + j)) continue;
+        const uint32_t gc = bfs[c + j].x;
+        out[rb + 2 + j].x = (uint32_t)(rb + 4 + 2 * j);
+        place(gc, rb + 4 + 2 * j);
+        place(gc + 1, rb + 5 + 2 * j);
+        for (int k = 0; k < 2; k++)
+          if (internal(gc + k)) queue.push_back({bfs[gc + k].x, rb + 4 + 2 * j + k});
+      }
+    }
+    for (; qi < queue.size(); qi++) {
+      const uint32_t p = queue[qi].first;
+      const int64_t b = (int64_t)out.size();
+      out.resize(b + 8, pad);
+      out[queue[qi].second].x = (uint32_t)b;
+      place(p, b);
+      place(p + 1, b + 1);
+      for (int j = 0; j < 2; j++) {
+        if (!internal(p + j)) continue;
+        const uint32_t c = bfs[p + j].x;
+        out[b + j].x = (uint32_t)(b + 2 + 2 * j);
+        place(c, b + 2 + 2 * j);
+        place(c + 1, b + 3 + 2 * j);
+        for (int k = 0; k < 2; k++)
+          if (internal(c + k)) queue.push_back({bfs[c + k].x, b + 2 + 2 * j + k});
+      }
+    }
+  }
+  if (out.size() >= (size_t)LEAF_BIT) throw std::runtime_error("walk-node array too large");
+}
+
 }  // namespace
 
 void ffd_engine::load_model(const std::string& path) {
@@ -360,12 +438,14 @@ void ffd_engine::load_model(const std::string& path) {
   upload(hp_nodes, nodes, main_stream());
   hp_nodes_h = nodes;
   upload(hp_roots, roots, main_stream());
+  hp_roots_h = roots;
   upload(hp_sizes, sizes, main_stream());
   flatten_forest(m, "mp", nodes, roots, sizes);
   if ((int)roots.size() != n_forests * ntrees_per_forest) throw std::runtime_error("FFD tree count mismatch");
   upload(mp_nodes, nodes, main_stream());
   mp_nodes_h = nodes;
   upload(mp_roots, roots, main_stream());
+  mp_roots_h = roots;
   upload(mp_sizes, sizes, main_stream());
   HIP_CHECK(hipStreamSynchronize(main_stream()));  // host vectors are reused below
 
@@ -588,7 +668,7 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   }
   stage(7, st, [&] {
     launch_traverse(true, dfd, n, blocks_per_face(fds, true, trav_g_hp), trav_g_hp, hp_wnodes.as<uint4>(),
-                    hp_roots.as<int32_t>(), nullptr, hp_trees, desc.hp_option.step_size, desc.hp_option.step_size,
+                    hp_wroots.as<int32_t>(), nullptr, hp_trees, desc.hp_option.step_size, desc.hp_option.step_size,
                     plane, w.chan.as<uint16_t>(),
                     w.hpleaf.as<int32_t>(), trav_wg, st);
   });
@@ -598,7 +678,7 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   });
   stage(9, st, [&] {
     launch_traverse(false, dfd, n, blocks_per_face(fds, false, trav_g_mp), trav_g_mp, mp_wnodes.as<uint4>(),
-                    mp_roots.as<int32_t>(), w.state.as<HpState>(), 0, desc.mp_option.step_size, mp_step_y(),
+                    mp_wroots.as<int32_t>(), w.state.as<HpState>(), 0, desc.mp_option.step_size, mp_step_y(),
                     plane, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), trav_wg, st);
   });
   const int n_parts = std::min(desc.mp_option.num_parts, NPARTS);
@@ -729,6 +809,7 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   if (const char* v = std::getenv("FFD_TRAV_G_HP")) e->trav_g_hp = std::max(3, std::min(5, std::atoi(v)));
   if (const char* v = std::getenv("FFD_TRAV_G_FFD")) e->trav_g_mp = std::max(3, std::min(5, std::atoi(v)));
   if (const char* v = std::getenv("FFD_TRAV_WG")) e->trav_wg = std::max(8, std::atoi(v));
+  if (const char* v = std::getenv("FFD_NODE_LAYOUT")) e->pair_blocks = std::string(v) != "bfs";
   if (const char* v = std::getenv("FFD_CHANNEL_STREAMS")) e->channel_streams = std::max(1, std::min(4, std::atoi(v)));
   if (const char* v = std::getenv("FFD_CHUNK")) e->max_chunk = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("FFD_STREAMS")) e->n_streams = std::max(1, std::min(8, std::atoi(v)));
