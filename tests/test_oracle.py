@@ -91,15 +91,17 @@ def test_threaded_equals_serial(oracle_mod):
 
 def test_accuracy_band_on_bundled_faces(oracle_mod, fixtures):
     """eval_ffd's metric (eval_ffd.cpp:33-46,102-108) on the 20 annotated faces the reference ships.
-    Sanity band around the reference's published result on LFW (mean 0.078, 79.4% < 0.1 IOD)."""
+    Pinned to the restatement's measured result (mean 0.0747, 78.5 % < 0.1 IOD; the reference's
+    published LFW-test figures are 0.078 / 79.4 %, output/errors.txt).  Per-face parity with the
+    reference's own output is pinned in tests/test_reference_pins.py."""
     errs = []
     for img, box, parts in zip(fixtures["images"], fixtures["boxes"], fixtures["parts"]):
         f, _ = oracle_mod.analyze_face(img, tuple(int(v) for v in box), threads=8)
         iod = np.linalg.norm((parts[0] + parts[1]) / 2.0 - (parts[6] + parts[7]) / 2.0)
         errs.append(np.linalg.norm(parts - f["points"], axis=1) / iod)
     errs = np.array(errs)
-    assert 0.05 < errs.mean() < 0.11, errs.mean()
-    assert (errs < 0.1).mean() > 0.65
+    assert abs(errs.mean() - 0.07472) < 5e-5, errs.mean()
+    assert (errs < 0.1).sum() == 157, (errs < 0.1).sum()  # 157 of 200 landmarks = 78.5 %
 
 
 def test_rejects_box_outside_image(oracle_mod, fixtures):
