@@ -8,13 +8,18 @@ head-pose forest, tree selection, FFD forest, votes, MeanShift.  Inputs are resi
 the timed region starts; outputs stay in HBM (for N > 1 they are gathered to rank 0 with an
 RCCL gather over xGMI inside the step).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
-Rank 0 prints ONE JSON line.
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5]
+N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) WORLD_SIZE must equal N;
+run directly, bench.py starts the N ranks itself (torch.distributed.run as a child process, before
+anything touches the GPU) and exits with its status.  Rank 0 prints ONE JSON line.
+--dry-run: the launcher and the record gather without a GPU (gloo, synthetic records; tests).
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -55,22 +60,41 @@ STAGE_KERNELS = {
 }
 
 
-def measured_traffic(stage, faces_per_launch):
-    """HBM bytes per launch of `stage`'s kernel from the newest committed PMC summary
-    (profiles/<round>/traffic.json, written by tools/pmc_traffic.py from tools/profile_round.sh's
-    FETCH_SIZE / WRITE_SIZE passes over this same 4096-face workload), or None."""
+SOURCE_FILES = ("face_alignment_cvpr_2012_amd/csrc/ffd_kernels.hip", "face_alignment_cvpr_2012_amd/csrc/ffd_engine.cpp",
+                "face_alignment_cvpr_2012_amd/csrc/ffd_device.hpp", "face_alignment_cvpr_2012_amd/csrc/ffd_kernels.hpp",
+                "include/ffd_numerics.h", "include/ffd_gabor.h")
+
+
+def source_digest():
+    """sha256 (16 hex) of the kernel and engine sources: ties a PMC summary to the code it measured
+    (the GPU box gets no .git, so the commit id is not available there)."""
+    h = hashlib.sha256()
+    for f in SOURCE_FILES:
+        with open(os.path.join(REPO, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def measured_traffic(stage, faces_per_launch, workload="c2"):
+    """HBM bytes per launch of `stage`'s kernel from the committed PMC summary of THIS source tree
+    (profiles/<round>/traffic.json with a matching source_digest, written by tools/pmc_traffic.py
+    from tools/profile_round.sh's FETCH_SIZE / WRITE_SIZE passes over the same workload), or None
+    (no summary was collected for the code being measured)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "traffic.json")))
-    if not files or faces_per_launch != 4096:
-        return None
-    try:
-        kernels = json.load(open(files[-1]))["kernels"]
-    except (OSError, ValueError, KeyError):
-        return None
-    pre = STAGE_KERNELS.get(stage)
-    for name, v in kernels.items():
-        if pre and name.startswith(pre) and v.get("traffic_bytes"):
-            return v["traffic_bytes"]
+    digest = source_digest()
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "traffic.json")), reverse=True):
+        try:
+            doc = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if doc.get("source_digest") != digest or doc.get("workload", "c2") != workload:
+            continue
+        if doc.get("faces_per_launch", 4096) != faces_per_launch:
+            continue
+        pre = STAGE_KERNELS.get(stage)
+        for name, v in doc.get("kernels", {}).items():
+            if pre and name.startswith(pre) and v.get("traffic_bytes"):
+                return v["traffic_bytes"]
     return None
 
 
@@ -96,18 +120,29 @@ def stage_work(stage, n_faces, W=125, H=125, n_hp=576, n_mp=1024, trees=20):
     return n_faces * n_hp * 15 * 4 / 1e9, "GB/s", "hbm"
 
 
-def cpu_baseline(wl, n_budget_s=12.0):
-    """Oracle (C++ restatement) in reference-shaped mode: faces sequential, per-face thread pools
-    of `cores` threads for the 35 Gabor, 576 head-pose and 1,024 FFD tasks (ThreadPool.hpp:24-64),
-    on a bounded sample (~n_budget_s seconds) of the benchmarked workload's own faces."""
-    import oracle
-    oracle.load_model(wl.model)
-    oracle.set_steps(4, *wl.mp_steps)
+def host_cores():
+    """Host threads this process may use: its CPU affinity, capped by OMP_NUM_THREADS (the GPU box
+    sets it to the box's CPU share, 16 per GPU; nproc there shows the whole machine)."""
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    cores = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail)), 16))
+    return max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
+
+
+def cpu_baseline(wl, n_budget_s=12.0):
+    """Oracle (C++ restatement) timed on the host cores, on bounded samples (~n_budget_s seconds
+    each) of the benchmarked workload's own faces:
+      value          reference-shaped: faces sequential, per-face thread pools of `cores` threads
+                     for the 35 Gabor, the head-pose and the FFD patch tasks (ThreadPool.hpp:24-64,
+                     the reference's hardware_concurrency() pools sized to the cores available);
+      faces_parallel labelled alternative: `cores` faces at once, one thread each."""
+    import concurrent.futures as cf
+
+    import oracle
+    oracle.load_model(wl.model)
+    oracle.set_steps(4, *wl.mp_steps)
+    cores = host_cores()
     face = lambda k: wl.face(k % wl.n)  # noqa: E731
     t0 = time.perf_counter()
     oracle.analyze_face(*face(0), threads=cores)
@@ -117,6 +152,12 @@ def cpu_baseline(wl, n_budget_s=12.0):
     for k in range(1, n + 1):
         oracle.analyze_face(*face(k), threads=cores)
     dt = time.perf_counter() - t0
+    # faces-parallel: ctypes releases the GIL, so `cores` Python threads run `cores` faces at once
+    n_par = int(max(cores, min(4 * wl.n, n_budget_s * cores / max(one * cores, 1e-3))))
+    with cf.ThreadPoolExecutor(cores) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(lambda k: oracle.analyze_face(*face(k), threads=1), range(1, n_par + 1)))
+        dt_par = time.perf_counter() - t0
     cpu = ""
     try:
         cpu = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
@@ -124,7 +165,10 @@ def cpu_baseline(wl, n_budget_s=12.0):
         pass
     return {"value": round(n / dt, 3), "unit": "faces/s", "cores": cores, "kind": "port",
             "sample": f"first {n} faces of the {wl.name} workload, analyzeFace each, reference-shaped per-face "
-                      f"thread pools of {cores} threads, {dt:.1f} s; host {cpu}, nproc {os.cpu_count()}"}
+                      f"thread pools of {cores} threads, {dt:.1f} s; host {cpu}, nproc {os.cpu_count()}, "
+                      f"affinity/OMP_NUM_THREADS share {cores}",
+            "faces_parallel": {"value": round(n_par / dt_par, 3), "unit": "faces/s", "cores": cores,
+                               "sample": f"{n_par} faces, {cores} at once (one thread each), {dt_par:.1f} s"}}
 
 
 class Workload:
@@ -132,7 +176,8 @@ class Workload:
 
     def __init__(self, name, images, boxes, box_img, scaling, describe, total_faces, n_images=None,
                  model=None, mp_steps=(3, 3)):
-        self.name, self.images, self.boxes, self.box_img = name, images, boxes, box_img
+        self.name, self.images, self.box_img = name, images, box_img
+        self.boxes = np.ascontiguousarray(np.asarray(boxes, np.int32).reshape(-1, 4))  # packed once
         self.scaling, self.describe, self.total_faces = scaling, describe, total_faces
         self.model = model or os.path.join(REPO, "model", "ffd_model.bin")
         self.mp_steps = mp_steps  # FFD patch-grid step (x, y)
@@ -144,7 +189,7 @@ class Workload:
         return len(self.boxes)
 
     def face(self, k):
-        return self.images[self.box_img[k] % len(self.images)], self.boxes[k]
+        return self.images[self.box_img[k] % len(self.images)], tuple(int(v) for v in self.boxes[k])
 
 
 def make_workload(name, rank, world, faces, frames):
@@ -216,6 +261,41 @@ def parity_spot_check(ff, wl, d_out, k=4):
     return ok
 
 
+def launch_ranks(n):
+    """Start n ranks of this script under torch.distributed.run as a child process (nothing in this
+    process has touched the GPU) and return the child's exit status."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def dry_run(args, world, rank):
+    """The N-rank path without a GPU: gloo process group, each rank's contiguous shard of synthetic
+    records (headpose = global face index), one gather to rank 0 (distributed.gather_records)."""
+    import torch
+    import torch.distributed as dist
+
+    import face_alignment_cvpr_2012_amd as ffd
+    from face_alignment_cvpr_2012_amd.distributed import gather_records, shard_bounds
+    dist.init_process_group("gloo")
+    total = args.faces or 61
+    lo, hi = shard_bounds(total, world, rank)
+    recs = np.zeros((hi - lo, ffd.FACE_RECORD_BYTES), np.uint8)
+    recs[:, :4] = np.arange(lo, hi, dtype=np.float32).view(np.uint8).reshape(-1, 4)
+    ranks = [None] * world
+    dist.all_gather_object(ranks, (rank, os.getpid()))
+    got = gather_records(torch.from_numpy(recs.reshape(-1)), total, dst=0)
+    if rank == 0:
+        faces = ffd.faces_from_records(got.numpy().tobytes())
+        ok = [f.headpose for f in faces] == [float(i) for i in range(total)]
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": sorted(r for r, _ in ranks),
+                          "pids": len({p for _, p in ranks}), "faces": total, "gather_ok": ok}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -229,7 +309,19 @@ def main():
     ap.add_argument("--chunk", type=int, default=0, help="faces per pipeline launch (0 = whole batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
+    ap.add_argument("--dry-run", action="store_true", help="launcher + gather only, gloo, no GPU")
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # one process per GPU, started before any GPU call
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (one rank per GPU)")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
 
     import torch
     import torch.distributed as dist
@@ -237,9 +329,6 @@ def main():
     import face_alignment_cvpr_2012_amd as ffd
     from face_alignment_cvpr_2012_amd.distributed import gather_records
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

@@ -122,7 +122,7 @@ def lib():
     L.ffd_analyze_faces.argtypes = [ctypes.c_void_p, P(_Image), ctypes.c_int32, P(_Rect), ctypes.c_void_p,
                                     ctypes.c_int32, P(_Face)]
     L.ffd_analyze_faces_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
-                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P(_Rect),
+                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
     L.ffd_synchronize.argtypes = [ctypes.c_void_p]
     L.ffd_stream.argtypes = [ctypes.c_void_p]
@@ -201,6 +201,13 @@ def faces_from_records(buf):
     """Decode a bytes/uint8 buffer of ffd_face records (e.g. copied back from the device)."""
     arr = (_Face * (len(buf) // FACE_RECORD_BYTES)).from_buffer_copy(bytes(buf))
     return [_face_from_record(r) for r in arr]
+
+
+def _packed_rects(boxes):
+    """(n, 4) C-contiguous int32 view/copy of `boxes` (ffd_rect array layout)."""
+    a = boxes if isinstance(boxes, np.ndarray) else np.asarray(boxes)
+    a = np.ascontiguousarray(a, np.int32).reshape(-1, 4)
+    return a
 
 
 def _check(status, handle=None):
@@ -287,13 +294,15 @@ class FaceForest:
         return [_face_from_record(r) for r in out]
 
     def analyze_device(self, d_images, image_bytes, width, height, stride, n_img, boxes, box_img, d_out):
-        """Enqueue a batch whose images (and output records) live in device memory."""
-        n = len(boxes)
-        crect = (_Rect * n)(*[_Rect(*[int(v) for v in b]) for b in boxes])
+        """Enqueue a batch whose images (and output records) live in device memory.  boxes: (n, 4)
+        int32 array (x, y, w, h; ffd_rect layout, passed without copying when already packed) or a
+        sequence of 4-tuples; box_img: (n,) int32 image index per box, or None."""
+        rects = _packed_rects(boxes)
         cmap = np.ascontiguousarray(box_img, np.int32) if box_img is not None else None
-        _check(lib().ffd_analyze_faces_device(self._h, d_images, image_bytes, width, height, stride, n_img, crect,
-                                              cmap.ctypes.data if cmap is not None else None, n, d_out), self._h)
-        self._keep = cmap
+        _check(lib().ffd_analyze_faces_device(self._h, d_images, image_bytes, width, height, stride, n_img,
+                                              rects.ctypes.data, cmap.ctypes.data if cmap is not None else None,
+                                              rects.shape[0], d_out), self._h)
+        self._keep = (rects, cmap)
 
     def synchronize(self):
         _check(lib().ffd_synchronize(self._h), self._h)

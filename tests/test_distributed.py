@@ -74,3 +74,29 @@ def test_gloo_two_ranks_gather_equals_serial(tmp_path, model_path):
     assert np.array_equal(gathered, serial)
     faces = ffd.faces_from_records(gathered.tobytes())
     assert len(faces) == N_FACES
+
+
+def test_bench_gpus_2_starts_two_ranks():
+    """bench.py --gpus N with no launcher environment starts N ranks itself (torch.distributed.run,
+    before any GPU call) and every rank sees WORLD_SIZE == N; --dry-run swaps the GPU work for
+    synthetic records so the launcher and the gather run here on gloo."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run", "--faces", "5"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["ranks"] == [0, 1] and line["pids"] == 2 and line["gather_ok"]
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr

@@ -5,7 +5,9 @@ Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half
 wide coalesced reads, so it is doubled; WRITE_SIZE is taken as is.  Infinity-Cache hits are
 counted by these counters, so the figure is L2-miss traffic (an upper bound on HBM bytes).
 
-usage: python tools/pmc_traffic.py gpurun_out/round_TAG [out.json]
+usage: python tools/pmc_traffic.py gpurun_out/round_TAG [out.json] [workload] [faces_per_launch]
+The summary records bench.source_digest() of the tree it was run from: bench.py quotes `traffic`
+only from a summary whose digest matches the code being benchmarked.
 """
 import csv
 import glob
@@ -39,7 +41,13 @@ def main():
         wb = sum(w) / len(w) if w else None
         out[k] = {"fetch_bytes": fb, "write_bytes": wb, "launches": max(len(f), len(w)),
                   "traffic_bytes": (fb or 0.0) + (wb or 0.0)}
-    text = json.dumps({"source": root, "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KiB -> bytes",
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from bench import source_digest
+    workload = sys.argv[3] if len(sys.argv) > 3 else "c2"
+    per_launch = int(sys.argv[4]) if len(sys.argv) > 4 else 4096
+    text = json.dumps({"source": root, "source_digest": source_digest(), "workload": workload,
+                       "faces_per_launch": per_launch,
+                       "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KiB -> bytes",
                        "kernels": out}, indent=1)
     if len(sys.argv) > 2:
         open(sys.argv[2], "w").write(text + "\n")
