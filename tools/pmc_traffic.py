@@ -45,7 +45,9 @@ def main():
     from bench import source_digest
     workload = sys.argv[3] if len(sys.argv) > 3 else "c2"
     per_launch = int(sys.argv[4]) if len(sys.argv) > 4 else 4096
-    text = json.dumps({"source": root, "source_digest": source_digest(), "workload": workload,
+    dg = os.path.join(root, "source_digest.txt")  # written on the GPU box by profile_round.sh
+    digest = open(dg).read().strip() if os.path.exists(dg) else source_digest()
+    text = json.dumps({"source": root, "source_digest": digest, "workload": workload,
                        "faces_per_launch": per_launch,
                        "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KiB -> bytes",
                        "kernels": out}, indent=1)

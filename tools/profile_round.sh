@@ -9,6 +9,7 @@ R=$PWD
 TAG=${1:-r1}
 OUT=$R/gpurun_out/round_$TAG
 mkdir -p "$OUT"
+python3 -c "import bench; print(bench.source_digest())" > "$OUT/source_digest.txt"  # the code measured here
 BARGS=${BENCH_ARGS:---steps 5 --warmup 2}
 timeout -k 10 ${BENCH_TIMEOUT:-600} python bench.py $BARGS > "$OUT/bench.log" 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 "$OUT/bench.log"; [ $rc -eq 0 ] || exit $rc
