@@ -18,9 +18,9 @@ ORACLE    := oracle/build/libffd_oracle.so
 MODEL     := model/ffd_model.bin
 EXAMPLE   := examples/build/analyze_face
 
-HIP_OBJS  := $(PKG)/lib/ffd_kernels.o $(PKG)/lib/ffd_engine.o
+HIP_OBJS  := $(PKG)/lib/ffd_kernels.o $(PKG)/lib/ffd_engine.o $(PKG)/lib/ffd_group.o
 HDRS      := include/ffd.h include/ffd_numerics.h include/ffd_gabor.h include/ffd_model_format.h $(CSRC)/ffd_device.hpp \
-             $(CSRC)/ffd_kernels.hpp $(CSRC)/model_io.hpp
+             $(CSRC)/ffd_kernels.hpp $(CSRC)/model_io.hpp $(CSRC)/ffd_engine_impl.hpp
 
 all: $(LIB) $(CONVERT) $(SYNTH) $(ORACLE) $(EXAMPLE)
 
@@ -32,8 +32,14 @@ $(PKG)/lib/ffd_engine.o: $(CSRC)/ffd_engine.cpp $(HDRS)
 	@mkdir -p $(@D)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(PKG)/lib/ffd_group.o: $(CSRC)/ffd_group.cpp $(HDRS)
+	@mkdir -p $(@D)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# RCCL (multi-device gather, ffd_group.cpp): the system librccl.so.1; in a process where PyTorch
+# already loaded its bundled librccl.so.1 (same soname) the loader reuses that one
 $(LIB): $(HIP_OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS) -L/opt/rocm/lib -lrccl
 
 $(SYNTH): $(CSRC)/ffd_synth_forest.cpp $(CSRC)/model_io.hpp include/ffd_model_format.h
 	@mkdir -p $(@D)

@@ -327,7 +327,6 @@ def main():
     import torch.distributed as dist
 
     import face_alignment_cvpr_2012_amd as ffd
-    from face_alignment_cvpr_2012_amd.distributed import gather_records
 
     if world > 1:
         torch.cuda.set_device(local)
@@ -343,21 +342,32 @@ def main():
         reps = -(-n_img // len(wl.images))
         d_images = d_images.repeat(reps, 1, 1, 1)[:n_img].contiguous()
     rec = ffd.FACE_RECORD_BYTES
-    d_out = torch.zeros(max(1, n) * rec, dtype=torch.uint8, device=dev)
+    per = -(-wl.total_faces // world)  # records per rank in the gather (shards padded to ceil(N / world))
+    d_out = torch.zeros(max(1, per) * rec, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
 
     chunk = args.chunk if 0 < args.chunk < n else 0  # 0: engine default (FFD_CHUNK)
     mp = ffd.MultiPartEstimatorOption(step_size=wl.mp_steps[0], step_size_y=wl.mp_steps[1])
     ff = ffd.FaceForest(ffd.FaceForestOptions(model_path=wl.model, device=local, max_chunk_faces=chunk, mp_option=mp))
-    geo = [ff.geometry(b[2], b[3]) for b in wl.boxes[:256]]
+    geo = [ff.geometry(int(b[2]), int(b[3])) for b in wl.boxes[:256]]
     mean_wh = (float(np.mean([g[0] for g in geo])), float(np.mean([g[1] for g in geo])))
+    d_root = None
+    if world > 1:
+        # the engines join one RCCL communicator inside libffd.so (ffd_engine_join); the 128-byte id
+        # travels over the launcher's process group
+        cid = torch.tensor(list(ffd.comm_id() if rank == 0 else bytes(ffd.COMM_ID_BYTES)), dtype=torch.uint8,
+                           device=dev)
+        dist.broadcast(cid, 0)
+        ff.join(bytes(cid.cpu().tolist()), world, rank)
+        if rank == 0:
+            d_root = torch.zeros(world * per * rec, dtype=torch.uint8, device=dev)
 
     def step():
         ff.analyze_device(d_images.data_ptr(), iw * ih * 3, iw, ih, iw * 3, n_img, wl.boxes, wl.box_img,
                           d_out.data_ptr())
+        if world > 1:  # ONE RCCL gather of the ffd_face records to rank 0 (faces sharded, no other exchange)
+            ff.gather(d_out.data_ptr(), per, d_root.data_ptr() if d_root is not None else None, 0)
         ff.synchronize()
-        if world > 1:  # one RCCL gather of the ffd_face records to rank 0 (faces sharded, no other exchange)
-            gather_records(d_out[: n * rec], wl.total_faces, dst=0)
 
     for _ in range(args.warmup):
         step()

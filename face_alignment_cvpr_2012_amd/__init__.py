@@ -18,7 +18,8 @@ import numpy as np
 
 __all__ = [
     "FaceForestOptions", "HeadPoseEstimatorOption", "MultiPartEstimatorOption", "MeanShiftOption",
-    "Face", "FaceForest", "Forest", "FFDError", "default_model_path", "library_path",
+    "Face", "FaceForest", "FaceForestGroup", "Forest", "FFDError", "default_model_path", "library_path",
+    "comm_id", "status_string",
     "FOREST_HEADPOSE", "FOREST_FFD", "LANDMARK_NAMES",
 ]
 
@@ -97,8 +98,12 @@ EXPORTED_SYMBOLS = (
     "ffd_engine_desc_init", "ffd_engine_create", "ffd_engine_destroy", "ffd_last_error", "ffd_face_geometry",
     "ffd_analyze_faces", "ffd_analyze_faces_device", "ffd_synchronize", "ffd_stream", "ffd_extract_channels",
     "ffd_forest_eval_leaves", "ffd_get_trace", "ffd_version", "ffd_set_profiling", "ffd_get_stage_times",
-    "ffd_stage_name",
+    "ffd_stage_name", "ffd_status_string", "ffd_estimate_headpose", "ffd_estimate_facial_features",
+    "ffd_group_create", "ffd_group_destroy", "ffd_group_last_error", "ffd_group_size", "ffd_group_engine",
+    "ffd_group_analyze_faces", "ffd_comm_id", "ffd_engine_join", "ffd_gather_faces",
 )
+COMM_ID_BYTES = 128
+STATUS_OK, STATUS_INVALID_ARGUMENT, STATUS_UNSUPPORTED = 0, 1, 7
 NUM_STAGES = 12
 
 
@@ -137,9 +142,29 @@ def lib():
     L.ffd_get_stage_times.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
     L.ffd_stage_name.argtypes = [ctypes.c_int32]
     L.ffd_stage_name.restype = ctypes.c_char_p
+    L.ffd_status_string.argtypes = [ctypes.c_int32]
+    L.ffd_status_string.restype = ctypes.c_char_p
+    L.ffd_estimate_headpose.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                        P(_Rect), P(ctypes.c_float), P(ctypes.c_float)]
+    L.ffd_estimate_facial_features.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                               P(_Rect), ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+    L.ffd_group_create.argtypes = [P(_Desc), ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_void_p)]
+    L.ffd_group_destroy.argtypes = [ctypes.c_void_p]
+    L.ffd_group_last_error.argtypes = [ctypes.c_void_p]
+    L.ffd_group_last_error.restype = ctypes.c_char_p
+    L.ffd_group_size.argtypes = [ctypes.c_void_p]
+    L.ffd_group_engine.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    L.ffd_group_engine.restype = ctypes.c_void_p
+    L.ffd_group_analyze_faces.argtypes = [ctypes.c_void_p, P(_Image), ctypes.c_int32, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_int32, P(_Face)]
+    L.ffd_comm_id.argtypes = [ctypes.c_void_p]
+    L.ffd_engine_join.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+    L.ffd_gather_faces.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
     for name in ("ffd_engine_create", "ffd_face_geometry", "ffd_analyze_faces", "ffd_analyze_faces_device",
                  "ffd_synchronize", "ffd_extract_channels", "ffd_forest_eval_leaves", "ffd_get_trace",
-                 "ffd_set_profiling", "ffd_get_stage_times"):
+                 "ffd_set_profiling", "ffd_get_stage_times", "ffd_estimate_headpose",
+                 "ffd_estimate_facial_features", "ffd_group_create", "ffd_group_analyze_faces", "ffd_comm_id",
+                 "ffd_engine_join", "ffd_gather_faces", "ffd_group_size"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -216,6 +241,36 @@ def _check(status, handle=None):
         raise FFDError(status, msg)
 
 
+def _make_desc(o):
+    """ffd_engine_desc from FaceForestOptions (returns the desc and the bytes its path points to)."""
+    d = _Desc()
+    lib().ffd_engine_desc_init(ctypes.byref(d))
+    path = os.fspath(o.model_path).encode()
+    d.model_path = path
+    d.device = o.device
+    d.max_chunk_faces = o.max_chunk_faces
+    d.hp_option = _HpOpt(o.hp_option.num_head_pose_labels, o.hp_option.step_size, o.hp_option.min_foreground_probability)
+    d.mp_option = _MpOpt(o.mp_option.num_parts, o.mp_option.step_size, o.mp_option.min_samples,
+                         o.mp_option.min_forground, o.mp_option.min_pf, o.mp_option.max_variance,
+                         o.mp_option.step_size_y)
+    d.ms_option = _MsOpt(o.ms_option.kernel_size, o.ms_option.max_iterations, o.ms_option.stopping_criteria)
+    return d, path
+
+
+def status_string(status):
+    return lib().ffd_status_string(int(status)).decode()
+
+
+def _image_array(images):
+    imgs = [np.ascontiguousarray(im, dtype=np.uint8) for im in images]
+    cim = (_Image * len(imgs))()
+    for i, im in enumerate(imgs):
+        if im.ndim != 3 or im.shape[2] != 3:
+            raise ValueError("images must be HxWx3 BGR uint8")
+        cim[i] = _Image(im.ctypes.data, im.shape[1], im.shape[0], im.strides[0])
+    return imgs, cim
+
+
 # --------------------------------------------------------------- FaceForest --
 class FaceForest:
     """FaceForest (include/FaceForest.hpp:81-157) on one MI355X device."""
@@ -223,19 +278,7 @@ class FaceForest:
     def __init__(self, options=None):
         self.options = options or FaceForestOptions()
         L = lib()
-        d = _Desc()
-        L.ffd_engine_desc_init(ctypes.byref(d))
-        o = self.options
-        self._model_path_bytes = os.fspath(o.model_path).encode()
-        d.model_path = self._model_path_bytes
-        d.device = o.device
-        d.max_chunk_faces = o.max_chunk_faces
-        d.hp_option = _HpOpt(o.hp_option.num_head_pose_labels, o.hp_option.step_size,
-                             o.hp_option.min_foreground_probability)
-        d.mp_option = _MpOpt(o.mp_option.num_parts, o.mp_option.step_size, o.mp_option.min_samples,
-                             o.mp_option.min_forground, o.mp_option.min_pf, o.mp_option.max_variance,
-                             o.mp_option.step_size_y)
-        d.ms_option = _MsOpt(o.ms_option.kernel_size, o.ms_option.max_iterations, o.ms_option.stopping_criteria)
+        d, self._model_path_bytes = _make_desc(self.options)
         h = ctypes.c_void_p()
         st = L.ffd_engine_create(ctypes.byref(d), ctypes.byref(h))
         if st != 0:
@@ -275,15 +318,10 @@ class FaceForest:
 
     # ---- batched API --------------------------------------------------------
     def analyzeFaces(self, images, boxes, box_img=None):
-        imgs = [np.ascontiguousarray(im, dtype=np.uint8) for im in images]
         n = len(boxes)
         if n == 0:
             return []
-        cim = (_Image * len(imgs))()
-        for i, im in enumerate(imgs):
-            if im.ndim != 3 or im.shape[2] != 3:
-                raise ValueError("images must be HxWx3 BGR uint8")
-            cim[i] = _Image(im.ctypes.data, im.shape[1], im.shape[0], im.strides[0])
+        imgs, cim = _image_array(images)
         crect = (_Rect * n)(*[_Rect(*[int(v) for v in b]) for b in boxes])
         cmap = None
         if box_img is not None:
@@ -333,6 +371,40 @@ class FaceForest:
         _check(lib().ffd_extract_channels(self._h, g.ctypes.data, w, h, out.ctypes.data), self._h)
         return out
 
+    def estimateHeadPose(self, channels, face_bbox=None):
+        """FaceForest::estimateHeadPose (src/FaceForest.cpp:60-72) on an image sample's 38 integral
+        channels (extract_channels layout); face_bbox = the patch region (default: whole sample).
+        Returns (headpose, variance)."""
+        ch = np.ascontiguousarray(channels, np.uint32)
+        _, h1, w1 = ch.shape
+        r = _Rect(*[int(v) for v in (face_bbox or (0, 0, w1 - 1, h1 - 1))])
+        hp, var = ctypes.c_float(), ctypes.c_float()
+        _check(lib().ffd_estimate_headpose(self._h, ch.ctypes.data, w1 - 1, h1 - 1, ctypes.byref(r), ctypes.byref(hp),
+                                           ctypes.byref(var)), self._h)
+        return hp.value, var.value
+
+    def estimateFacialFeatures(self, channels, face_bbox, tree_ids):
+        """FaceForest::estimateFacialFeatures (src/FaceForest.cpp:74-95): the FFD forest made of the
+        global tree ids (forest * 20 + tree), default MeanShiftOption; 10 x 2 int landmarks in sample
+        coordinates."""
+        ch = np.ascontiguousarray(channels, np.uint32)
+        _, h1, w1 = ch.shape
+        r = _Rect(*[int(v) for v in (face_bbox or (0, 0, w1 - 1, h1 - 1))])
+        t = np.ascontiguousarray(tree_ids, np.int32)
+        pts = np.zeros((10, 2), np.int32)
+        _check(lib().ffd_estimate_facial_features(self._h, ch.ctypes.data, w1 - 1, h1 - 1, ctypes.byref(r),
+                                                  t.ctypes.data, t.size, pts.ctypes.data), self._h)
+        return pts
+
+    def join(self, comm_id, n_ranks, rank):
+        """Join the RCCL communicator `comm_id` (bytes from comm_id() on one rank) as `rank`."""
+        buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(bytes(comm_id))
+        _check(lib().ffd_engine_join(self._h, buf, n_ranks, rank), self._h)
+
+    def gather(self, d_local, n_per_rank, d_root, root=0):
+        """Enqueue the RCCL gather of n_per_rank ffd_face records per rank into d_root on `root`."""
+        _check(lib().ffd_gather_faces(self._h, d_local, n_per_rank, d_root, root), self._h)
+
     def trace(self, index, box_w, box_h):
         """Per-stage intermediates of face `index` of the last batch."""
         fw, fh, nhp, nmp = self.geometry(box_w, box_h)
@@ -346,6 +418,64 @@ class FaceForest:
         bufs["trees"] = bufs["trees"][:nt]
         bufs["mp_leaves"] = bufs["mp_leaves"][: nmp * nt].reshape(nmp, nt)
         return bufs
+
+
+def comm_id():
+    """ncclGetUniqueId through libffd (FFD_COMM_ID_BYTES bytes, to be shared with the other ranks)."""
+    buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
+    st = lib().ffd_comm_id(buf)
+    if st != 0:
+        raise FFDError(st, lib().ffd_group_last_error(None).decode(errors="replace"))
+    return bytes(buf)
+
+
+class FaceForestGroup:
+    """One process driving several devices (ffd_group_*): faces sharded in contiguous blocks,
+    one engine (model copy) per device, one RCCL gather of the records."""
+
+    def __init__(self, devices, options=None):
+        self.options = options or FaceForestOptions()
+        d, self._path = _make_desc(self.options)
+        devs = (ctypes.c_int32 * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        st = lib().ffd_group_create(ctypes.byref(d), devs, len(devices), ctypes.byref(h))
+        if st != 0:
+            raise FFDError(st, lib().ffd_group_last_error(None).decode(errors="replace"))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ffd_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def size(self):
+        return lib().ffd_group_size(self._h)
+
+    def analyzeFaces(self, images, boxes, box_img=None):
+        n = len(boxes)
+        if n == 0:
+            return []
+        imgs, cim = _image_array(images)
+        rects = _packed_rects(boxes)
+        cmap = np.ascontiguousarray(box_img, np.int32) if box_img is not None else None
+        out = (_Face * n)()
+        st = lib().ffd_group_analyze_faces(self._h, cim, len(imgs), rects.ctypes.data,
+                                           cmap.ctypes.data if cmap is not None else None, n, out)
+        if st != 0:
+            raise FFDError(st, lib().ffd_group_last_error(self._h).decode(errors="replace"))
+        return [_face_from_record(r) for r in out]
 
 
 class Forest:

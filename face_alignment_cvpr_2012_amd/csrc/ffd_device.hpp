@@ -23,7 +23,7 @@ constexpr int NGABOR = 35;
 constexpr int NPARTS = 10;
 constexpr int NHP_LABELS = 5;
 constexpr int MAX_TREES = 32;     // FFD_MAX_TREES
-constexpr int MAX_FACE_H = 320;   // scaled face height limit (aspect <= 2.56)
+constexpr int MAX_FACE_H = 600;   // scaled face height limit (box aspect h/w <= 4.8); taller -> FFD_ERR_UNSUPPORTED
 constexpr uint32_t LEAF_BIT = 0x80000000u;
 
 // Flattened tree node (16 B), breadth-first per tree, children adjacent:
@@ -58,7 +58,11 @@ struct FaceDesc {
   int64_t hp_off;         // element offset into the head-pose leaf buffer
   int64_t mp_off;         // element offset into the FFD leaf buffer
   int64_t vote_off;       // element offset into the vote buffer
-  int32_t valid;          // 0: box rejected, face skipped
+  int32_t valid;          // 0: box rejected, face skipped (its record gets status `reject`)
+  int32_t nochan;         // 1: the channel stage skips this face (channels preloaded, or never read:
+                          //    no head-pose patch fits, the reference then averages 0/0)
+  int32_t reject;         // ffd_status of a rejected face
+  int32_t vox, voy;       // patch-grid origin in the image sample (estimateFacialFeatures' face_bbox)
   int32_t pad_;
 };
 

@@ -26,47 +26,14 @@
 #include "ffd_kernels.hpp"
 #include "../../include/ffd_gabor.h"
 #include "model_io.hpp"
+#include "ffd_engine_impl.hpp"
 
 #define FFD_VERSION_STR "ffd-mi355x 0.1.0 (gfx950)"
 
 namespace {
 
 using namespace ffd;
-
-struct HipError : std::runtime_error {
-  using std::runtime_error::runtime_error;
-};
-
-#define HIP_CHECK(expr)                                                                        \
-  do {                                                                                         \
-    hipError_t e_ = (expr);                                                                    \
-    if (e_ != hipSuccess)                                                                      \
-      throw HipError(std::string(#expr) + ": " + hipGetErrorString(e_) + " (" __FILE__ ":" +  \
-                     std::to_string(__LINE__) + ")");                                         \
-  } while (0)
-
-// Device buffer that grows on demand (never shrinks).
-struct DevBuf {
-  void* p = nullptr;
-  size_t n = 0;
-  ~DevBuf() { if (p) (void)hipFree(p); }
-  void* ensure(size_t bytes) {
-    if (bytes <= n) return p;
-    if (p) { (void)hipFree(p); p = nullptr; n = 0; }
-    size_t want = std::max<size_t>(bytes, 256);
-    HIP_CHECK(hipMalloc(&p, want));
-    n = want;
-    return p;
-  }
-  template <class T> T* as() const { return static_cast<T*>(p); }
-};
-
-template <class T> void upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
-  b.ensure(v.size() * sizeof(T));
-  if (!v.empty()) HIP_CHECK(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
-}
-
-int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+using namespace ffd_host;
 
 // Device integrals are kept modulo 2^16; the u8 plane is the exact mod-2^16 second difference,
 // from which the full 32-bit integral ([NCH][H+1][W+1], the reference's layout) is rebuilt.
@@ -100,185 +67,7 @@ int blocks_per_face(const std::vector<FaceDesc>& fds, bool hp, int G) {
   return m;
 }
 
-struct Geometry {
-  int W = 0, H = 0, nhx = 0, nhy = 0, nmx = 0, nmy = 0;
-  float scale = 0;
-};
-
 }  // namespace
-
-// Per-stream workspace: a chunk of faces runs its whole pipeline on one stream; consecutive
-// chunks alternate streams so one chunk's memory-bound traversal overlaps the next chunk's
-// VALU-bound Gabor stage, and a chunk's channel planes stay in the Infinity Cache between the
-// kernel that writes them and the traversals that read them.
-struct Workspace {
-  hipStream_t stream = nullptr;
-  hipEvent_t done = nullptr;
-  // channel-stage fork: the five Gabor kernels and k_integral are independent, so they are spread
-  // over `stream` and these streams (joined back before the head-pose traversal)
-  std::vector<hipStream_t> fork;
-  std::vector<hipEvent_t> fork_ev;  // [0]: gray ready; [1 + i]: fork stream i done
-  bool pending = false;
-  DevBuf faces, gray, mag, chan, hpleaf, mpleaf, votes, state, ms_mean, vote_counts;
-  std::vector<FaceDesc> h_fds;  // host staging, reused only after `done`
-  std::vector<FaceDesc> desc;   // descriptors of the chunk last run here (ffd_get_trace)
-  int first = 0, count = 0;
-  ~Workspace() {
-    for (auto e : fork_ev) (void)hipEventDestroy(e);
-    for (auto f : fork) (void)hipStreamDestroy(f);
-    if (done) (void)hipEventDestroy(done);
-    if (stream) (void)hipStreamDestroy(stream);
-  }
-};
-
-namespace {
-void layout_pair_blocks(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots, std::vector<uint4>& out,
-                        std::vector<int32_t>& out_roots);
-}  // namespace
-
-struct ffd_engine {
-  std::string err;
-  int device = 0;
-  ffd_engine_desc desc{};
-  int max_chunk = 4096;
-  int n_streams = 1;
-  int channel_streams = 1;  // streams the channel stage is spread over (FFD_CHANNEL_STREAMS; 2-4 measured no gain)
-  // traversal tuning: patch block edge G (a workgroup walks all trees of a G x G block of patches
-  // over an LDS copy of the block's integral window) and the persistent workgroups (one per CU).
-  // Overridable with FFD_TRAV_G_{HP,FFD} / FFD_TRAV_WG / FFD_CHUNK / FFD_STREAMS.
-  int trav_g_hp = 4, trav_g_mp = 4, trav_wg = 256;
-
-  // model parameters
-  int face_size = 125, patch = 31, hp_trees = 0, n_forests = 0, ntrees_per_forest = 0;
-  int64_t hp_leaves = 0, mp_leaves = 0;
-
-  // device model
-  DevBuf gabor_coef, hp_nodes, hp_roots, hp_sizes, hp_m, mp_nodes, mp_roots, mp_sizes, mp_rec;
-  DevBuf hp_wnodes, mp_wnodes;       // walk-node encodings for k_traverse (ffd_device.hpp)
-  DevBuf hp_wroots, mp_wroots;       // tree roots in the walk-node arrays
-  std::vector<uint4> hp_nodes_h, mp_nodes_h;  // host copies until the walk nodes are built
-  std::vector<int32_t> hp_roots_h, mp_roots_h;
-  bool pair_blocks = true;           // walk-node layout (FFD_NODE_LAYOUT=bfs for plain breadth-first)
-  bool vote_rec_compact = false;     // 32-B vote records (else 64-B), see load_model
-  int vote_bias_x = 0, vote_bias_y = 0;
-
-  std::vector<std::unique_ptr<Workspace>> ws;
-  DevBuf images, out, scratch_a, scratch_b, scratch_c;  // host-API staging (ws[0] stream)
-  int last_ws = -1;
-
-  hipStream_t main_stream() const { return ws[0]->stream; }
-
-  // stage profiler (hipEvents around each launch, on the launching stream)
-  struct Pending { int stage; hipEvent_t a, b; };
-  bool profiling = false;
-  std::vector<hipEvent_t> event_pool;
-  std::vector<Pending> pending;
-  double stage_ms[FFD_NUM_STAGES] = {0};
-  int64_t stage_n[FFD_NUM_STAGES] = {0};
-
-  hipEvent_t get_event() {
-    if (!event_pool.empty()) { hipEvent_t e = event_pool.back(); event_pool.pop_back(); return e; }
-    hipEvent_t e;
-    HIP_CHECK(hipEventCreate(&e));
-    return e;
-  }
-  template <class F> void stage(int id, hipStream_t s, F&& fn) {
-    if (!profiling) { fn(); return; }
-    Pending p{id, get_event(), get_event()};
-    HIP_CHECK(hipEventRecord(p.a, s));
-    fn();
-    HIP_CHECK(hipEventRecord(p.b, s));
-    pending.push_back(p);
-  }
-  void sync_all() {
-    for (auto& w : ws) {
-      for (auto f : w->fork) HIP_CHECK(hipStreamSynchronize(f));
-      HIP_CHECK(hipStreamSynchronize(w->stream));
-    }
-  }
-  void resolve() {
-    if (pending.empty()) return;
-    sync_all();
-    for (auto& p : pending) {
-      float ms = 0;
-      HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
-      stage_ms[p.stage] += ms;
-      stage_n[p.stage] += 1;
-      event_pool.push_back(p.a);
-      event_pool.push_back(p.b);
-    }
-    pending.clear();
-  }
-
-  ~ffd_engine() {
-    for (auto& p : pending) { event_pool.push_back(p.a); event_pool.push_back(p.b); }
-    for (auto e : event_pool) (void)hipEventDestroy(e);
-  }
-
-  Geometry geometry(int bw, int bh) const {
-    Geometry g;
-    if (bw <= 0 || bh <= 0) return g;
-    g.scale = (float)face_size / (float)bw;  // FaceForest.cpp:202
-    g.W = (int)((float)bw * g.scale);        // cv::Size(cols*scale, rows*scale) truncation
-    g.H = (int)((float)bh * g.scale);
-    auto cnt = [&](int extent, int step) {
-      int n = 0;
-      for (int x = 0; x < extent - patch; x += step) n++;
-      return n;
-    };
-    g.nhx = cnt(g.W, desc.hp_option.step_size);
-    g.nhy = cnt(g.H, desc.hp_option.step_size);
-    g.nmx = cnt(g.W, desc.mp_option.step_size);
-    g.nmy = cnt(g.H, mp_step_y());
-    return g;
-  }
-
-  void load_model(const std::string& path);
-  void build_gabor();
-  // FFD patch-grid step along y: the reference has one step for both axes (step_size_y == 0)
-  int mp_step_y() const { return desc.mp_option.step_size_y > 0 ? desc.mp_option.step_size_y : desc.mp_option.step_size; }
-  // Fit the traversal window into the CU's 160 KB of LDS (and the staging registers), shrinking
-  // the patch block if needed, and raise the kernels' dynamic-LDS limit.
-  void check_traverse_lds() {
-    const int cap = 160 * 1024;
-    auto fit = [&](int& G, int step, int step_y) {
-      while (!traverse_window_fits(G, step, step_y, cap)) {
-        if (G <= 3) throw std::runtime_error("traversal window does not fit in LDS (step size too large)");
-        G--;
-      }
-    };
-    fit(trav_g_hp, desc.hp_option.step_size, desc.hp_option.step_size);
-    fit(trav_g_mp, desc.mp_option.step_size, mp_step_y());
-    auto walk_nodes = [&](std::vector<uint4>& h, std::vector<int32_t>& roots, DevBuf& d, DevBuf& droots, int G,
-                          int step, int step_y) {
-      std::vector<uint4> wn(h.size());
-      if (!encode_walk_nodes(h.data(), h.size(), G, step, step_y, wn.data()))
-        throw std::runtime_error("forest does not fit the traversal's walk-node encoding");
-      if (pair_blocks) {
-        std::vector<uint4> pb;
-        std::vector<int32_t> pr;
-        layout_pair_blocks(wn, roots, pb, pr);
-        wn.swap(pb);
-        roots.swap(pr);
-      }
-      upload(d, wn, main_stream());
-      upload(droots, roots, main_stream());
-      HIP_CHECK(hipStreamSynchronize(main_stream()));
-      std::vector<uint4>().swap(h);
-      std::vector<int32_t>().swap(roots);
-    };
-    walk_nodes(hp_nodes_h, hp_roots_h, hp_wnodes, hp_wroots, trav_g_hp, desc.hp_option.step_size,
-               desc.hp_option.step_size);
-    walk_nodes(mp_nodes_h, mp_roots_h, mp_wnodes, mp_wroots, trav_g_mp, desc.mp_option.step_size, mp_step_y());
-    HIP_CHECK(set_traverse_lds_limit(cap));
-    HIP_CHECK(set_gabor_lds_limit(96 * 1024));  // padded u8 face of up to MAX_FACE_H rows
-    hipDeviceProp_t prop;
-    HIP_CHECK(hipGetDeviceProperties(&prop, device));
-    if (!std::getenv("FFD_TRAV_WG")) trav_wg = std::max(8, prop.multiProcessorCount);
-  }
-  void run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out);
-  void analyze(const uint8_t* d_images, const std::vector<FaceDesc>& all, FaceOut* d_out);
-};
 
 namespace {
 
@@ -332,8 +121,11 @@ void flatten_forest(const ModelFile& m, const std::string& p, std::vector<uint4>
         const int16_t* s = sp + (b + v) * FFD_SPLIT_FIELDS;
         const int ch = s[0], x1 = s[1], y1 = s[2], w1 = s[3], h1 = s[4], x2 = s[5], y2 = s[6], w2 = s[7], h2 = s[8];
         if (ch < 0 || ch >= NCH) throw std::runtime_error("split channel out of range");
+        // sides <= 22 (SimplePatchFeature::generate, ImageSample.hpp:42-72): the u16 integrals sum a
+        // rectangle as two halves of <= 22 x 11 pixels (exact mod 2^16) and the evalTest quotient
+        // fma(R, rcp(area), 0.00075) is proven exact for areas <= 484 (tests/test_numerics.py)
         for (int q : {w1, h1, w2, h2})
-          if (q < 1 || q > 31) throw std::runtime_error("split rectangle size out of range");
+          if (q < 1 || q > 22) throw std::runtime_error("split rectangle side outside [1, 22] (unsupported model)");
         for (int q : {x1, y1, x2, y2})
           if (q < 0 || q > 31) throw std::runtime_error("split rectangle offset out of range");
         if (x1 + w1 > 31 || y1 + h1 > 31 || x2 + w2 > 31 || y2 + h2 > 31)
@@ -356,8 +148,10 @@ void flatten_forest(const ModelFile& m, const std::string& p, std::vector<uint4>
 //   general block: [pair P, children of P.0, children of P.1, -, -]
 // Children of the block's last level start new blocks.  Leaves keep their ordinals; the padding
 // slots are never referenced.  Speed only: every walk visits the same nodes in the same order.
-void layout_pair_blocks(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots, std::vector<uint4>& out,
-                        std::vector<int32_t>& out_roots) {
+}  // namespace
+
+void ffd_host::layout_pair_blocks(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots,
+                                  std::vector<uint4>& out, std::vector<int32_t>& out_roots) {
   const uint4 pad = make_uint4(LEAF_BIT, 0u, 0u, 0u);
   out.clear();
   out_roots.clear();
@@ -408,8 +202,6 @@ void layout_pair_blocks(const std::vector<uint4>& bfs, const std::vector<int32_t
   }
   if (out.size() >= (size_t)LEAF_BIT) throw std::runtime_error("walk-node array too large");
 }
-
-}  // namespace
 
 void ffd_engine::load_model(const std::string& path) {
   ModelFile m;
@@ -717,26 +509,38 @@ void ffd_engine::analyze(const uint8_t* d_images, const std::vector<FaceDesc>& a
     if (ws[i]->pending) HIP_CHECK(hipStreamWaitEvent(main_stream(), ws[i]->done, 0));
 }
 
-namespace {
-
-ffd_status fail(ffd_engine* e, ffd_status s, const std::string& msg) {
+ffd_status ffd_host::fail(ffd_engine* e, ffd_status s, const std::string& msg) {
   if (e) e->err = msg;
   else g_create_err = msg;
   return s;
 }
 
-// Fill the per-face descriptor (geometry + resize parameters) for a box on an image.
-bool make_desc(const ffd_engine* e, int64_t img_off, int iw, int ih, int stride, const ffd_rect& b, FaceDesc& f) {
+namespace {
+
+// Fill the per-face descriptor (geometry + resize parameters) for a box on an image.  Returns the
+// face's status: FFD_OK, FFD_ERR_INVALID_ARGUMENT (box outside the image or an empty scaled face:
+// the reference's cv::Mat ROI / resize assertions throw) or FFD_ERR_UNSUPPORTED (scaled face taller
+// than MAX_FACE_H).  A face on which no head-pose patch fits runs like the reference: 0/0 head pose
+// (NaN), trees 0..19 of forest 0, no votes, landmarks (0, 0); its channels are never read, so the
+// channel stage skips it.
+ffd_status make_desc(const ffd_engine* e, int64_t img_off, int iw, int ih, int stride, const ffd_rect& b, FaceDesc& f) {
   std::memset(&f, 0, sizeof(f));
   f.img_off = img_off;
   f.img_w = iw; f.img_h = ih; f.img_stride = stride;
   f.bx = b.x; f.by = b.y; f.bw = b.width; f.bh = b.height;
-  if (b.x < 0 || b.y < 0 || b.width <= 0 || b.height <= 0 || b.x + b.width > iw || b.y + b.height > ih) return false;
+  f.reject = FFD_ERR_INVALID_ARGUMENT;
+  if (b.x < 0 || b.y < 0 || b.width <= 0 || b.height <= 0 || (int64_t)b.x + b.width > iw ||
+      (int64_t)b.y + b.height > ih)
+    return FFD_ERR_INVALID_ARGUMENT;
   Geometry g = e->geometry(b.width, b.height);
-  if (g.W < 2 || g.H < 2 || g.W > PITCH - 3 || g.H > MAX_FACE_H) return false;
+  if (g.W < 1 || g.H < 1 || g.W > PITCH - 3) return FFD_ERR_INVALID_ARGUMENT;
+  if (g.H > MAX_FACE_H) {
+    f.reject = FFD_ERR_UNSUPPORTED;
+    return FFD_ERR_UNSUPPORTED;
+  }
   f.W = g.W; f.H = g.H; f.scale = g.scale;
   f.nhx = g.nhx; f.nhy = g.nhy; f.nmx = g.nmx; f.nmy = g.nmy;
-  if (f.nhx * f.nhy == 0) return false;  // no head-pose patches: the reference divides 0/0
+  f.nochan = (f.nhx * f.nhy == 0 || g.W < 2 || g.H < 2) ? 1 : 0;
   if (g.W == b.width && g.H == b.height) {
     f.mode = 0;
   } else {
@@ -752,7 +556,8 @@ bool make_desc(const ffd_engine* e, int64_t img_off, int iw, int ih, int stride,
   while (xv < g.W - 4) xv += 4;
   f.xv = xv;
   f.valid = 1;
-  return true;
+  f.reject = FFD_OK;
+  return FFD_OK;
 }
 
 template <class F> ffd_status guarded(ffd_engine* e, F&& fn) {
@@ -771,9 +576,58 @@ template <class F> ffd_status guarded(ffd_engine* e, F&& fn) {
 
 }  // namespace
 
+// Host images in, results in device memory (d_out, n_faces FaceOut), everything enqueued on the
+// engine's streams; main_stream() is ordered after the batch on return.  Throws HipError.
+ffd_status ffd_host::analyze_host(ffd_engine* e, const ffd_image* imgs, int32_t n_img, const ffd_rect* boxes,
+                                  const int32_t* box_img, int32_t n_faces, void* d_out) {
+  if (n_faces < 0 || (n_faces > 0 && (!imgs || !boxes || !d_out)) || n_img < 0)
+    return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (!box_img && n_img != n_faces) return fail(e, FFD_ERR_INVALID_ARGUMENT, "box_img NULL requires n_img == n_faces");
+  if (n_faces == 0) return FFD_OK;
+  // pack the images into one device buffer
+  std::vector<int64_t> img_off(n_img);
+  int64_t total = 0;
+  for (int i = 0; i < n_img; i++) {
+    if (!imgs[i].bgr || imgs[i].width <= 0 || imgs[i].height <= 0 || imgs[i].stride < 3 * imgs[i].width)
+      return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad image " + std::to_string(i));
+    img_off[i] = total;
+    total += align_up((int64_t)imgs[i].stride * imgs[i].height, 256);
+  }
+  std::vector<FaceDesc> fds(n_faces);
+  for (int i = 0; i < n_faces; i++) {
+    int k = box_img ? box_img[i] : i;
+    if (k < 0 || k >= n_img) return fail(e, FFD_ERR_INVALID_ARGUMENT, "box_img out of range");
+    make_desc(e, img_off[k], imgs[k].width, imgs[k].height, imgs[k].stride, boxes[i], fds[i]);
+  }
+  e->sync_all();  // the staging buffer may still be read by the previous batch
+  e->images.ensure(total);
+  for (int i = 0; i < n_img; i++)
+    HIP_CHECK(hipMemcpyAsync(e->images.as<uint8_t>() + img_off[i], imgs[i].bgr, (size_t)imgs[i].stride * imgs[i].height,
+                             hipMemcpyHostToDevice, e->main_stream()));
+  // the other streams must see the uploaded images
+  HIP_CHECK(hipEventRecord(e->ws[0]->done, e->main_stream()));
+  for (size_t i = 1; i < e->ws.size(); i++) HIP_CHECK(hipStreamWaitEvent(e->ws[i]->stream, e->ws[0]->done, 0));
+  e->analyze(e->images.as<uint8_t>(), fds, static_cast<FaceOut*>(d_out));
+  return FFD_OK;
+}
+
 extern "C" {
 
 const char* ffd_version(void) { return FFD_VERSION_STR; }
+
+const char* ffd_status_string(int32_t s) {
+  switch (s) {
+    case FFD_OK: return "ok";
+    case FFD_ERR_INVALID_ARGUMENT: return "invalid argument (face box outside the image or empty scaled face)";
+    case FFD_ERR_MODEL: return "model file invalid or unsupported";
+    case FFD_ERR_DEVICE: return "HIP device error or no HIP device";
+    case FFD_ERR_OUT_OF_MEMORY: return "out of memory";
+    case FFD_ERR_NOT_INITIALIZED: return "not initialised";
+    case FFD_ERR_INTERNAL: return "internal error";
+    case FFD_ERR_UNSUPPORTED: return "unsupported face geometry (scaled face taller than 600 rows)";
+    default: return "unknown status";
+  }
+}
 
 void ffd_engine_desc_init(ffd_engine_desc* d) {
   if (!d) return;
@@ -851,6 +705,7 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
 void ffd_engine_destroy(ffd_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
+  release_comm(e);
   for (auto& w : e->ws) (void)hipStreamSynchronize(w->stream);
   delete e;
 }
@@ -908,40 +763,14 @@ ffd_status ffd_face_geometry(const ffd_engine* e, int32_t bw, int32_t bh, int32_
 ffd_status ffd_analyze_faces(ffd_engine* e, const ffd_image* imgs, int32_t n_img, const ffd_rect* boxes,
                              const int32_t* box_img, int32_t n_faces, ffd_face* out) {
   return guarded(e, [&]() -> ffd_status {
-    if (n_faces < 0 || (n_faces > 0 && (!imgs || !boxes || !out)) || n_img < 0)
-      return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
-    if (!box_img && n_img != n_faces) return fail(e, FFD_ERR_INVALID_ARGUMENT, "box_img NULL requires n_img == n_faces");
-    if (n_faces == 0) return FFD_OK;
-    // pack the images into one device buffer
-    std::vector<int64_t> img_off(n_img);
-    int64_t total = 0;
-    for (int i = 0; i < n_img; i++) {
-      if (!imgs[i].bgr || imgs[i].width <= 0 || imgs[i].height <= 0 || imgs[i].stride < 3 * imgs[i].width)
-        return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad image " + std::to_string(i));
-      img_off[i] = total;
-      total += align_up((int64_t)imgs[i].stride * imgs[i].height, 256);
-    }
-    e->images.ensure(total);
-    for (int i = 0; i < n_img; i++)
-      HIP_CHECK(hipMemcpyAsync(e->images.as<uint8_t>() + img_off[i], imgs[i].bgr, (size_t)imgs[i].stride * imgs[i].height,
-                               hipMemcpyHostToDevice, e->main_stream()));
-    // the other streams must see the uploaded images
-    HIP_CHECK(hipEventRecord(e->ws[0]->done, e->main_stream()));
-    for (size_t i = 1; i < e->ws.size(); i++) HIP_CHECK(hipStreamWaitEvent(e->ws[i]->stream, e->ws[0]->done, 0));
-    std::vector<FaceDesc> fds(n_faces);
-    for (int i = 0; i < n_faces; i++) {
-      int k = box_img ? box_img[i] : i;
-      if (k < 0 || k >= n_img) return fail(e, FFD_ERR_INVALID_ARGUMENT, "box_img out of range");
-      make_desc(e, img_off[k], imgs[k].width, imgs[k].height, imgs[k].stride, boxes[i], fds[i]);
-    }
-    e->out.ensure((size_t)n_faces * sizeof(FaceOut));
-    e->analyze(e->images.as<uint8_t>(), fds, e->out.as<FaceOut>());
+    if (n_faces > 0 && !out) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (n_faces > 0) e->out.ensure((size_t)n_faces * sizeof(FaceOut));
+    const ffd_status st = analyze_host(e, imgs, n_img, boxes, box_img, n_faces, e->out.p);
+    if (st != FFD_OK || n_faces == 0) return st;
     static_assert(sizeof(FaceOut) == sizeof(ffd_face), "FaceOut must mirror ffd_face");
     HIP_CHECK(hipMemcpyAsync(out, e->out.p, (size_t)n_faces * sizeof(ffd_face), hipMemcpyDeviceToHost,
                              e->main_stream()));
     HIP_CHECK(hipStreamSynchronize(e->main_stream()));
-    for (int i = 0; i < n_faces; i++)
-      if (out[i].status != FFD_OK) out[i].status = FFD_ERR_INVALID_ARGUMENT;
     return FFD_OK;
   });
 }
@@ -974,6 +803,8 @@ ffd_status ffd_get_trace(ffd_engine* e, int32_t index, ffd_trace* tr) {
     if (k < 0 || k >= w.count) return fail(e, FFD_ERR_INVALID_ARGUMENT, "index not in the last chunk");
     const FaceDesc& f = w.desc[k];
     if (!f.valid) return fail(e, FFD_ERR_INVALID_ARGUMENT, "face was rejected");
+    if (f.nochan && (tr->face || tr->channels))
+      return fail(e, FFD_ERR_INVALID_ARGUMENT, "no head-pose patch fits this face: its channels were not computed");
     e->sync_all();
     const int W = f.W, H = f.H;
     if (tr->face)
@@ -1052,6 +883,144 @@ ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t
     w.count = 0;  // workspace no longer holds a batch
     w.pending = false;
     if (e->last_ws == 0) e->last_ws = -1;
+    return FFD_OK;
+  });
+}
+
+}  // extern "C"
+
+namespace {
+
+// One image sample (38 integral planes, the reference's [c][H+1][W+1] layout) restricted to the
+// region `r` as a one-face chunk on workspace 0: the region's integrals are the second differences
+// of the sample's at the region origin (mod 2^16, exact for every rectangle a split reads), the
+// patch grid covers the region (face_utils.cpp:197-207,255-265: x from bbox.x while
+// x < bbox.x + bbox.width - patch) and votes keep sample coordinates (vox, voy).  The channel stage
+// is skipped (nochan); the caller launches the forest stages.
+FaceDesc stage_sample(ffd_engine* e, Workspace& w, const uint32_t* ch, int W, int H, const ffd_rect& r) {
+  FaceDesc f;
+  std::memset(&f, 0, sizeof(f));
+  const int rw = r.width, rh = r.height;
+  const int P = e->patch;
+  auto cnt = [&](int extent, int step) {
+    int n = 0;
+    for (int x = 0; x < extent - P; x += step) n++;
+    return n;
+  };
+  f.W = rw; f.H = rh; f.bw = rw; f.bh = rh; f.scale = 1.f;
+  f.nhx = cnt(rw, e->desc.hp_option.step_size);
+  f.nhy = cnt(rh, e->desc.hp_option.step_size);
+  f.nmx = cnt(rw, e->desc.mp_option.step_size);
+  f.nmy = cnt(rh, e->mp_step_y());
+  f.vox = r.x; f.voy = r.y;
+  f.valid = 1; f.nochan = 1;
+  f.plane = (int64_t)(rh + 1) * PITCH;
+  f.hp_off = f.mp_off = f.vote_off = f.ch_off = 0;
+  std::vector<uint16_t> J((size_t)NCH * f.plane, 0);
+  const size_t ow = (size_t)W + 1, oplane = ((size_t)H + 1) * ow;
+  for (int c = 0; c < NCH; c++) {
+    const uint32_t* I = ch + c * oplane;
+    for (int y = 0; y <= rh; y++)
+      for (int x = 0; x <= rw; x++)
+        J[(size_t)c * f.plane + (size_t)y * PITCH + x] =
+            (uint16_t)(I[(r.y + y) * ow + r.x + x] - I[r.y * ow + r.x + x] - I[(r.y + y) * ow + r.x] + I[r.y * ow + r.x]);
+  }
+  w.chan.ensure(J.size() * 2 + 512);  // slack: traversal windows read past a row
+  HIP_CHECK(hipMemcpyAsync(w.chan.p, J.data(), J.size() * 2, hipMemcpyHostToDevice, w.stream));
+  w.hpleaf.ensure(((size_t)e->hp_trees * f.nhx * f.nhy + 64) * 4);
+  w.mpleaf.ensure(((size_t)MAX_TREES * f.nmx * f.nmy + 64) * 4);
+  w.votes.ensure(((size_t)NPARTS * MAX_TREES * f.nmx * f.nmy + 64) * sizeof(Vote));
+  w.state.ensure(sizeof(HpState));
+  w.ms_mean.ensure(NPARTS * 2 * 4);
+  w.vote_counts.ensure(NPARTS * 4);
+  std::vector<FaceDesc> one{f};
+  upload(w.faces, one, w.stream);
+  HIP_CHECK(hipStreamSynchronize(w.stream));  // J is released on return
+  w.count = 0;  // the workspace no longer holds a batch for ffd_get_trace
+  w.pending = false;
+  if (e->last_ws == 0) e->last_ws = -1;
+  return f;
+}
+
+bool region_ok(int W, int H, const ffd_rect* r) {
+  return r && r->x >= 0 && r->y >= 0 && r->width > 0 && r->height > 0 && (int64_t)r->x + r->width <= W &&
+         (int64_t)r->y + r->height <= H && r->width <= PITCH - 3 && r->height <= MAX_FACE_H;
+}
+
+}  // namespace
+
+extern "C" {
+
+ffd_status ffd_estimate_headpose(ffd_engine* e, const uint32_t* channels, int32_t W, int32_t H,
+                                 const ffd_rect* region, float* headpose, float* variance) {
+  return guarded(e, [&]() -> ffd_status {
+    if (!channels || W < 1 || H < 1) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    const ffd_rect full{0, 0, W, H};
+    if (!region) region = &full;
+    if (!region_ok(W, H, region)) return fail(e, FFD_ERR_INVALID_ARGUMENT, "face_bbox outside the image sample");
+    e->sync_all();
+    Workspace& w = *e->ws[0];
+    const FaceDesc f = stage_sample(e, w, channels, W, H, *region);
+    const FaceDesc* dfd = w.faces.as<FaceDesc>();
+    std::vector<FaceDesc> fv{f};
+    e->out.ensure(sizeof(FaceOut));
+    launch_traverse(true, dfd, 1, blocks_per_face(fv, true, e->trav_g_hp), e->trav_g_hp, e->hp_wnodes.as<uint4>(),
+                    e->hp_wroots.as<int32_t>(), nullptr, e->hp_trees, e->desc.hp_option.step_size,
+                    e->desc.hp_option.step_size, f.plane, w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), e->trav_wg,
+                    w.stream);
+    launch_hp_pose(dfd, 1, w.hpleaf.as<int32_t>(), e->hp_m.as<float>(), e->hp_trees, e->n_forests,
+                   e->ntrees_per_forest, w.state.as<HpState>(), e->out.as<FaceOut>(), w.stream);
+    HIP_CHECK(hipGetLastError());
+    HpState hs;
+    HIP_CHECK(hipMemcpyAsync(&hs, w.state.p, sizeof(hs), hipMemcpyDeviceToHost, w.stream));
+    HIP_CHECK(hipStreamSynchronize(w.stream));
+    if (headpose) *headpose = hs.headpose;
+    if (variance) *variance = hs.variance;
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_estimate_facial_features(ffd_engine* e, const uint32_t* channels, int32_t W, int32_t H,
+                                        const ffd_rect* region, const int32_t* tree_ids, int32_t n_trees,
+                                        int32_t* points) {
+  return guarded(e, [&]() -> ffd_status {
+    if (!channels || !points || W < 1 || H < 1 || n_trees < 1 || n_trees > MAX_TREES || !tree_ids)
+      return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    const ffd_rect full{0, 0, W, H};
+    if (!region) region = &full;
+    if (!region_ok(W, H, region)) return fail(e, FFD_ERR_INVALID_ARGUMENT, "face_bbox outside the image sample");
+    const int ntot = e->n_forests * e->ntrees_per_forest;
+    for (int t = 0; t < n_trees; t++)
+      if (tree_ids[t] < 0 || tree_ids[t] >= ntot) return fail(e, FFD_ERR_INVALID_ARGUMENT, "tree id out of range");
+    e->sync_all();
+    Workspace& w = *e->ws[0];
+    const FaceDesc f = stage_sample(e, w, channels, W, H, *region);
+    const FaceDesc* dfd = w.faces.as<FaceDesc>();
+    std::vector<FaceDesc> fv{f};
+    HpState hs;
+    std::memset(&hs, 0, sizeof(hs));
+    hs.n_trees = n_trees;
+    for (int t = 0; t < n_trees; t++) hs.trees[t] = tree_ids[t];
+    HIP_CHECK(hipMemcpyAsync(w.state.p, &hs, sizeof(hs), hipMemcpyHostToDevice, w.stream));
+    e->out.ensure(sizeof(FaceOut));
+    const int n_parts = std::min(e->desc.mp_option.num_parts, NPARTS);
+    launch_traverse(false, dfd, 1, blocks_per_face(fv, false, e->trav_g_mp), e->trav_g_mp, e->mp_wnodes.as<uint4>(),
+                    e->mp_wroots.as<int32_t>(), w.state.as<HpState>(), 0, e->desc.mp_option.step_size, e->mp_step_y(),
+                    f.plane, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), e->trav_wg, w.stream);
+    launch_votes(dfd, 1, w.mpleaf.as<int32_t>(), e->mp_rec.as<uint4>(), e->vote_rec_compact, e->vote_bias_x,
+                 e->vote_bias_y, w.state.as<HpState>(), MAX_TREES, e->desc.mp_option.step_size, e->mp_step_y(),
+                 e->patch / 2, n_parts, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), w.stream);
+    // FaceForest::estimateFacialFeatures shifts with a default MeanShiftOption (FaceForest.cpp:89-92)
+    launch_meanshift(dfd, 1, w.state.as<HpState>(), MAX_TREES, n_parts, 10.f, 7, 0.05f, w.votes.as<Vote>(),
+                     w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(), e->out.as<FaceOut>(), w.stream);
+    HIP_CHECK(hipGetLastError());
+    FaceOut o;
+    HIP_CHECK(hipMemcpyAsync(&o, e->out.p, sizeof(o), hipMemcpyDeviceToHost, w.stream));
+    HIP_CHECK(hipStreamSynchronize(w.stream));
+    for (int i = 0; i < n_parts; i++) {  // scale 1: cvRound of the MeanShift mode, sample coordinates
+      points[2 * i] = o.points[i][0];
+      points[2 * i + 1] = o.points[i][1];
+    }
     return FFD_OK;
   });
 }

@@ -1,0 +1,252 @@
+// ffd_engine_impl.hpp — host-side engine state shared by the translation units of libffd.so
+// (ffd_engine.cpp: model, pipeline and the single-device C ABI; ffd_group.cpp: multi-device and
+// RCCL).  Not installed: the public interface is include/ffd.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/ffd.h"
+#include "ffd_device.hpp"
+#include "ffd_kernels.hpp"
+
+namespace ffd_host {
+
+using namespace ffd;
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIP_CHECK(expr)                                                                        \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      throw HipError(std::string(#expr) + ": " + hipGetErrorString(e_) + " (" __FILE__ ":" +  \
+                     std::to_string(__LINE__) + ")");                                         \
+  } while (0)
+
+// Device buffer that grows on demand (never shrinks).
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  void* ensure(size_t bytes) {
+    if (bytes <= n) return p;
+    if (p) { (void)hipFree(p); p = nullptr; n = 0; }
+    size_t want = std::max<size_t>(bytes, 256);
+    HIP_CHECK(hipMalloc(&p, want));
+    n = want;
+    return p;
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+template <class T> void upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
+  b.ensure(v.size() * sizeof(T));
+  if (!v.empty()) HIP_CHECK(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+}
+
+inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+struct Geometry {
+  int W = 0, H = 0, nhx = 0, nhy = 0, nmx = 0, nmy = 0;
+  float scale = 0;
+};
+
+}  // namespace ffd_host
+
+using namespace ffd;  // internal header: the engine's TUs work in ffd's vocabulary
+using ffd_host::DevBuf;
+using ffd_host::Geometry;
+using ffd_host::HipError;
+using ffd_host::upload;
+
+// Per-stream workspace: a chunk of faces runs its whole pipeline on one stream; consecutive
+// chunks alternate streams so one chunk's memory-bound traversal overlaps the next chunk's
+// VALU-bound Gabor stage, and a chunk's channel planes stay in the Infinity Cache between the
+// kernel that writes them and the traversals that read them.
+struct Workspace {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  // channel-stage fork: the five Gabor kernels and k_integral are independent, so they are spread
+  // over `stream` and these streams (joined back before the head-pose traversal)
+  std::vector<hipStream_t> fork;
+  std::vector<hipEvent_t> fork_ev;  // [0]: gray ready; [1 + i]: fork stream i done
+  bool pending = false;
+  DevBuf faces, gray, mag, chan, hpleaf, mpleaf, votes, state, ms_mean, vote_counts;
+  std::vector<FaceDesc> h_fds;  // host staging, reused only after `done`
+  std::vector<FaceDesc> desc;   // descriptors of the chunk last run here (ffd_get_trace)
+  int first = 0, count = 0;
+  ~Workspace() {
+    for (auto e : fork_ev) (void)hipEventDestroy(e);
+    for (auto f : fork) (void)hipStreamDestroy(f);
+    if (done) (void)hipEventDestroy(done);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace ffd_host {
+void layout_pair_blocks(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots, std::vector<uint4>& out,
+                        std::vector<int32_t>& out_roots);
+}  // namespace ffd_host
+
+struct ffd_engine {
+  std::string err;
+  int device = 0;
+  ffd_engine_desc desc{};
+  int max_chunk = 4096;
+  int n_streams = 1;
+  int channel_streams = 1;  // streams the channel stage is spread over (FFD_CHANNEL_STREAMS; 2-4 measured no gain)
+  // traversal tuning: patch block edge G (a workgroup walks all trees of a G x G block of patches
+  // over an LDS copy of the block's integral window) and the persistent workgroups (one per CU).
+  // Overridable with FFD_TRAV_G_{HP,FFD} / FFD_TRAV_WG / FFD_CHUNK / FFD_STREAMS.
+  int trav_g_hp = 4, trav_g_mp = 4, trav_wg = 256;
+
+  // model parameters
+  int face_size = 125, patch = 31, hp_trees = 0, n_forests = 0, ntrees_per_forest = 0;
+  int64_t hp_leaves = 0, mp_leaves = 0;
+
+  // device model
+  DevBuf gabor_coef, hp_nodes, hp_roots, hp_sizes, hp_m, mp_nodes, mp_roots, mp_sizes, mp_rec;
+  DevBuf hp_wnodes, mp_wnodes;       // walk-node encodings for k_traverse (ffd_device.hpp)
+  DevBuf hp_wroots, mp_wroots;       // tree roots in the walk-node arrays
+  std::vector<uint4> hp_nodes_h, mp_nodes_h;  // host copies until the walk nodes are built
+  std::vector<int32_t> hp_roots_h, mp_roots_h;
+  bool pair_blocks = true;           // walk-node layout (FFD_NODE_LAYOUT=bfs for plain breadth-first)
+  bool vote_rec_compact = false;     // 32-B vote records (else 64-B), see load_model
+  int vote_bias_x = 0, vote_bias_y = 0;
+
+  std::vector<std::unique_ptr<Workspace>> ws;
+  DevBuf images, out, scratch_a, scratch_b, scratch_c;  // host-API staging (ws[0] stream)
+  int last_ws = -1;
+
+  hipStream_t main_stream() const { return ws[0]->stream; }
+
+  // stage profiler (hipEvents around each launch, on the launching stream)
+  struct Pending { int stage; hipEvent_t a, b; };
+  bool profiling = false;
+  std::vector<hipEvent_t> event_pool;
+  std::vector<Pending> pending;
+  double stage_ms[FFD_NUM_STAGES] = {0};
+  int64_t stage_n[FFD_NUM_STAGES] = {0};
+
+  hipEvent_t get_event() {
+    if (!event_pool.empty()) { hipEvent_t e = event_pool.back(); event_pool.pop_back(); return e; }
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    return e;
+  }
+  template <class F> void stage(int id, hipStream_t s, F&& fn) {
+    if (!profiling) { fn(); return; }
+    Pending p{id, get_event(), get_event()};
+    HIP_CHECK(hipEventRecord(p.a, s));
+    fn();
+    HIP_CHECK(hipEventRecord(p.b, s));
+    pending.push_back(p);
+  }
+  void sync_all() {
+    for (auto& w : ws) {
+      for (auto f : w->fork) HIP_CHECK(hipStreamSynchronize(f));
+      HIP_CHECK(hipStreamSynchronize(w->stream));
+    }
+  }
+  void resolve() {
+    if (pending.empty()) return;
+    sync_all();
+    for (auto& p : pending) {
+      float ms = 0;
+      HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
+      stage_ms[p.stage] += ms;
+      stage_n[p.stage] += 1;
+      event_pool.push_back(p.a);
+      event_pool.push_back(p.b);
+    }
+    pending.clear();
+  }
+
+  ~ffd_engine() {
+    for (auto& p : pending) { event_pool.push_back(p.a); event_pool.push_back(p.b); }
+    for (auto e : event_pool) (void)hipEventDestroy(e);
+  }
+
+  Geometry geometry(int bw, int bh) const {
+    Geometry g;
+    if (bw <= 0 || bh <= 0) return g;
+    g.scale = (float)face_size / (float)bw;  // FaceForest.cpp:202
+    g.W = (int)((float)bw * g.scale);        // cv::Size(cols*scale, rows*scale) truncation
+    g.H = (int)((float)bh * g.scale);
+    auto cnt = [&](int extent, int step) {
+      int n = 0;
+      for (int x = 0; x < extent - patch; x += step) n++;
+      return n;
+    };
+    g.nhx = cnt(g.W, desc.hp_option.step_size);
+    g.nhy = cnt(g.H, desc.hp_option.step_size);
+    g.nmx = cnt(g.W, desc.mp_option.step_size);
+    g.nmy = cnt(g.H, mp_step_y());
+    return g;
+  }
+
+  void load_model(const std::string& path);
+  void build_gabor();
+  // FFD patch-grid step along y: the reference has one step for both axes (step_size_y == 0)
+  int mp_step_y() const { return desc.mp_option.step_size_y > 0 ? desc.mp_option.step_size_y : desc.mp_option.step_size; }
+  // Fit the traversal window into the CU's 160 KB of LDS (and the staging registers), shrinking
+  // the patch block if needed, and raise the kernels' dynamic-LDS limit.
+  void check_traverse_lds() {
+    const int cap = 160 * 1024;
+    auto fit = [&](int& G, int step, int step_y) {
+      while (!traverse_window_fits(G, step, step_y, cap)) {
+        if (G <= 3) throw std::runtime_error("traversal window does not fit in LDS (step size too large)");
+        G--;
+      }
+    };
+    fit(trav_g_hp, desc.hp_option.step_size, desc.hp_option.step_size);
+    fit(trav_g_mp, desc.mp_option.step_size, mp_step_y());
+    auto walk_nodes = [&](std::vector<uint4>& h, std::vector<int32_t>& roots, DevBuf& d, DevBuf& droots, int G,
+                          int step, int step_y) {
+      std::vector<uint4> wn(h.size());
+      if (!encode_walk_nodes(h.data(), h.size(), G, step, step_y, wn.data()))
+        throw std::runtime_error("forest does not fit the traversal's walk-node encoding");
+      if (pair_blocks) {
+        std::vector<uint4> pb;
+        std::vector<int32_t> pr;
+        ffd_host::layout_pair_blocks(wn, roots, pb, pr);
+        wn.swap(pb);
+        roots.swap(pr);
+      }
+      upload(d, wn, main_stream());
+      upload(droots, roots, main_stream());
+      HIP_CHECK(hipStreamSynchronize(main_stream()));
+      std::vector<uint4>().swap(h);
+      std::vector<int32_t>().swap(roots);
+    };
+    walk_nodes(hp_nodes_h, hp_roots_h, hp_wnodes, hp_wroots, trav_g_hp, desc.hp_option.step_size,
+               desc.hp_option.step_size);
+    walk_nodes(mp_nodes_h, mp_roots_h, mp_wnodes, mp_wroots, trav_g_mp, desc.mp_option.step_size, mp_step_y());
+    HIP_CHECK(set_traverse_lds_limit(cap));
+    HIP_CHECK(set_gabor_lds_limit(96 * 1024));  // padded u8 face of up to MAX_FACE_H rows
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    if (!std::getenv("FFD_TRAV_WG")) trav_wg = std::max(8, prop.multiProcessorCount);
+  }
+  void run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out);
+  void analyze(const uint8_t* d_images, const std::vector<FaceDesc>& all, FaceOut* d_out);
+};
+
+namespace ffd_host {
+// status + message helpers shared by the C entry points
+ffd_status fail(ffd_engine* e, ffd_status s, const std::string& msg);
+// analyzeFace over host images: upload, descriptors, pipeline; results left in d_out (device)
+ffd_status analyze_host(ffd_engine* e, const ffd_image* imgs, int32_t n_img, const ffd_rect* boxes,
+                        const int32_t* box_img, int32_t n_faces, void* d_out);
+// the engine's per-rank RCCL communicator, if it joined one (ffd_group.cpp)
+void release_comm(const ffd_engine* e);
+}  // namespace ffd_host

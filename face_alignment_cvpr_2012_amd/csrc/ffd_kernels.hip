@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) void k_gray_resize(const FaceDesc* __restrict_
                                                      const uint8_t* __restrict__ images,
                                                      uint8_t* __restrict__ gray) {
   const FaceDesc fd = faces[blockIdx.x];
-  if (!fd.valid) return;
+  if (!fd.valid || fd.nochan) return;
   const uint8_t* img = images + fd.img_off;
   uint8_t* out = gray + fd.gray_off;
   auto G = [&](int y, int x) -> int {
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ f
                                                   uint16_t* __restrict__ chan) {
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const FaceDesc fd = faces[blockIdx.x];
-  if (!fd.valid || wv >= 3) return;
+  if (!fd.valid || fd.nochan || wv >= 3) return;
   const int c = wv == 0 ? 0 : 35 + wv;
   const int W = fd.W, H = fd.H, x0 = 2 * lane;
   const uint8_t* g = gray + fd.gray_off;
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restric
   constexpr int LH = GB_TY + 2 * R;
   __shared__ float tile[LH * LW];
   const FaceDesc fd = faces[blockIdx.x];
-  if (!fd.valid) return;
+  if (!fd.valid || fd.nochan) return;
   const int tiles_x = (fd.W + GB_TX - 1) / GB_TX, tiles = tiles_x * ((fd.H + GB_TY - 1) / GB_TY);
   const uint8_t* g = gray + fd.gray_off;
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
@@ -396,7 +396,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
   __shared__ float vg[GS_BY * C::VP];
   __shared__ f2 vq[4][GS_BY * C::VP];
   const FaceDesc fd = faces[blockIdx.x];
-  if (!fd.valid) return;
+  if (!fd.valid || fd.nochan) return;
   const int FW = fd.W, FH = fd.H, NPC = FW + 2 * R;
   const uint8_t* g = gray + fd.gray_off;
   const float* cv = coef + C::V_OFF;
@@ -407,9 +407,11 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
 #pragma unroll
   for (int o = 0; o < 7; o++) mn[o] = mx[o] = 0xFFFFFFFFu;
 
-  {  // the whole reflect-101 padded face, once: (row, 4-column group) items, u32 LDS stores
+  {  // the whole reflect-101 padded face, once: (row, 4-column group) items, u32 LDS stores; rows up
+     // to the last band's end (ceil(FH / GS_BY) * GS_BY + 2R: every row the V pass reads is staged)
     constexpr int NQ = C::GP / 4;
-    for (int i = tid; i < (FH + 2 * R) * NQ; i += GS_THREADS) {
+    const int rows = (FH + GS_BY - 1) / GS_BY * GS_BY + 2 * R;
+    for (int i = tid; i < rows * NQ; i += GS_THREADS) {
       const int r = i / NQ, j = i - r * NQ;
       const uint8_t* row = g + reflect101(r - R, FH) * PITCH;
       uint32_t v = 0;
@@ -705,13 +707,13 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     const FaceDesc& fd = A.faces[B.f];
     B.nx = HP ? fd.nhx : fd.nmx;
     B.ny = HP ? fd.nhy : fd.nmy;
-    const int gbx = (B.nx + G - 1) / G, gby = (B.ny + G - 1) / G;
+    const int gbx = max(1, (B.nx + G - 1) / G), gby = (B.ny + G - 1) / G;
     B.xi0 = (b % gbx) * G;
     B.yi0 = (b / gbx) * G;
     B.px0 = B.xi0 * step;
     B.py0 = B.yi0 * stepy;
     B.T = 0;
-    if (fd.valid && b < gbx * gby) {
+    if (fd.valid && B.nx > 0 && b < gbx * gby) {
       B.ok = true;
       B.T = HP ? A.ntrees_hp : A.hp_state[B.f].n_trees;
     }
@@ -951,7 +953,7 @@ __global__ __launch_bounds__(256) void k_hp_pose(const FaceDesc* __restrict__ fa
   FaceOut& o = out[f];
   if (lane == 0) { o.bbox[0] = fd.bx; o.bbox[1] = fd.by; o.bbox[2] = fd.bw; o.bbox[3] = fd.bh; }
   if (!fd.valid) {
-    if (lane == 0) { o.status = 1; o.n_trees = 0; state[f].n_trees = 0; }
+    if (lane == 0) { o.status = fd.reject; o.n_trees = 0; state[f].n_trees = 0; }
     return;
   }
   const int nx = fd.nhx, ny = fd.nhy, n = nx * ny, T = hp_trees, total = n * T;
@@ -1051,8 +1053,8 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
       if (k < total) {
         const int pr = idiv_small(k, T), xi = idiv_small(pr, ny), yi = pr - xi * ny;
         leaf[u] = L[k];  // leaves are stored in the reference order
-        vx0[u] = xi * step + half_patch;
-        vy0[u] = yi * step_y + half_patch;
+        vx0[u] = fd.vox + xi * step + half_patch;  // patch.x + 15 (face_utils.cpp:257-293)
+        vy0[u] = fd.voy + yi * step_y + half_patch;
       }
     }
     // packed leaf records (see launch_votes): compact 32 B = 2 x uint4, else 64 B = 3 used uint4
@@ -1268,8 +1270,11 @@ void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uin
   k_gray_resize<<<n, 256, 0, s>>>(faces, images, gray);
 }
 
-// dynamic LDS of k_gabor_sep: the padded u8 face of the tallest face of the batch
-static int gabor_face_lds(int R, int max_h) { return (max_h + 2 * R) * ((PITCH + 2 * R + 3) / 4 * 4); }
+// dynamic LDS of k_gabor_sep: the padded u8 face of the tallest face of the batch, its rows rounded up
+// to whole GS_BY-row bands (the V pass of the last band reads up to row ceil(FH / GS_BY) * GS_BY + 2R - 1)
+int gabor_face_lds(int R, int max_h) {
+  return ((max_h + GS_BY - 1) / GS_BY * GS_BY + 2 * R) * ((PITCH + 2 * R + 3) / 4 * 4);
+}
 
 void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t* gray, const float* coef, float* mag,
                   uint16_t* chan, hipStream_t s) {

@@ -46,8 +46,12 @@ typedef enum {
   FFD_ERR_DEVICE = 3,
   FFD_ERR_OUT_OF_MEMORY = 4,
   FFD_ERR_NOT_INITIALIZED = 5,
-  FFD_ERR_INTERNAL = 6
+  FFD_ERR_INTERNAL = 6,
+  FFD_ERR_UNSUPPORTED = 7    /* per face: scaled face taller than the engine supports (box h/w > 4.8) */
 } ffd_status;
+
+/* Human-readable meaning of a status code (call or per-face). */
+const char* ffd_status_string(int32_t status);
 
 typedef struct ffd_engine ffd_engine;
 
@@ -67,7 +71,10 @@ typedef struct {                                                       /* struct
   ffd_rect bbox;             /* Face::bbox = input box              FaceForest.cpp:192 */
   int32_t points[FFD_NUM_LANDMARKS][2]; /* Face::ffd_cordinates (bbox-relative) */
   int32_t n_trees;           /* FFD trees selected for this face (20 except edge cases) */
-  int32_t status;            /* FFD_OK, or FFD_ERR_INVALID_ARGUMENT for a rejected box */
+  int32_t status;            /* FFD_OK; FFD_ERR_INVALID_ARGUMENT: box outside the image or empty scaled
+                                face (the reference's CV_Assert); FFD_ERR_UNSUPPORTED: face too tall.
+                                A face with no head-pose patch is FFD_OK with the reference's result:
+                                NaN headpose / variance, landmarks (0, 0) */
 } ffd_face;
 
 typedef struct {             /* HeadPoseEstimatorOption, include/FaceForest.hpp:34-43 */
@@ -151,6 +158,21 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* engine, int32_t forest_kind, const
                                   int32_t n_patches, const int32_t* tree_ids, int32_t n_trees,
                                   int32_t* leaf_ids);
 
+/* FaceForest::estimateHeadPose (src/FaceForest.cpp:60-72 -> getHeadPoseVotesMT,
+ * src/face_utils.cpp:183-242) on an image sample given as 38 integral planes (layout of
+ * ffd_extract_channels), patches over `region` (the reference's face_bbox; NULL = the whole
+ * sample).  headpose / variance as Face::headpose and getHeadPoseVotesMT's variance. */
+ffd_status ffd_estimate_headpose(ffd_engine* engine, const uint32_t* channels, int32_t face_w, int32_t face_h,
+                                 const ffd_rect* region, float* headpose, float* variance);
+
+/* FaceForest::estimateFacialFeatures (src/FaceForest.cpp:74-95): the FFD forest made of the given
+ * global tree ids (forest*20 + tree, at most FFD_MAX_TREES), votes over the patches of `region`
+ * (getFacialFeaturesVotesMT, src/face_utils.cpp:244-302) and MeanShift::shift with a default
+ * MeanShiftOption; points[2*i], points[2*i+1] = landmark i in sample coordinates (cvRound). */
+ffd_status ffd_estimate_facial_features(ffd_engine* engine, const uint32_t* channels, int32_t face_w,
+                                        int32_t face_h, const ffd_rect* region, const int32_t* tree_ids,
+                                        int32_t n_trees, int32_t* points);
+
 /* Intermediates of face `index` of the most recent ffd_analyze_faces[_device] batch.
  * Any pointer may be NULL; sizes as documented per field (from ffd_face_geometry). */
 typedef struct {
@@ -173,6 +195,33 @@ ffd_status ffd_get_trace(ffd_engine* engine, int32_t index, ffd_trace* trace);
 ffd_status ffd_set_profiling(ffd_engine* engine, int32_t enable);
 ffd_status ffd_get_stage_times(ffd_engine* engine, double* total_ms, int64_t* launches, int32_t n_stages);
 const char* ffd_stage_name(int32_t stage);
+
+/* ---- multi-device ----------------------------------------------------------
+ * Faces are independent (the reference loops them, src/FaceForest.cpp:175-180): each device keeps
+ * its own copy of the model, owns a contiguous block of ceil(N / G) faces and runs the whole path on
+ * it; the ffd_face records are gathered to one device with ONE RCCL gather over xGMI. */
+
+/* One process, G devices: an engine per device (desc->device is ignored) + ncclCommInitAll. */
+typedef struct ffd_group ffd_group;
+ffd_status ffd_group_create(const ffd_engine_desc* desc, const int32_t* devices, int32_t n_devices, ffd_group** out);
+void ffd_group_destroy(ffd_group* group);
+const char* ffd_group_last_error(const ffd_group* group);  /* group == NULL: the last failed create */
+int32_t ffd_group_size(const ffd_group* group);
+ffd_engine* ffd_group_engine(ffd_group* group, int32_t index);  /* owned by the group */
+/* analyzeFace over n_faces boxes sharded over the devices; same arguments and results as
+ * ffd_analyze_faces (out: host array, face order preserved). */
+ffd_status ffd_group_analyze_faces(ffd_group* group, const ffd_image* imgs, int32_t n_img, const ffd_rect* boxes,
+                                   const int32_t* box_img, int32_t n_faces, ffd_face* out);
+
+/* One process per device: one rank creates the id (ncclGetUniqueId) and shares it with the others
+ * (MPI / torch.distributed broadcast, a file ...); every rank joins with its engine
+ * (ncclCommInitRank on the engine's device); ffd_gather_faces then gathers n_per_rank ffd_face
+ * records from every rank's device buffer d_local into d_root (n_ranks * n_per_rank records, rank
+ * order) on rank `root`, enqueued on the engine's stream (after its pending batch). */
+#define FFD_COMM_ID_BYTES 128
+ffd_status ffd_comm_id(uint8_t* id /* FFD_COMM_ID_BYTES */);
+ffd_status ffd_engine_join(ffd_engine* engine, const uint8_t* id, int32_t n_ranks, int32_t rank);
+ffd_status ffd_gather_faces(ffd_engine* engine, const void* d_local, int32_t n_per_rank, void* d_root, int32_t root);
 
 /* Library version string. */
 const char* ffd_version(void);

@@ -64,6 +64,10 @@ def lib():
         L.oracle_exp.restype = ctypes.c_double
         L.oracle_expf.argtypes = [ctypes.c_float]
         L.oracle_expf.restype = ctypes.c_float
+        L.oracle_estimate_headpose.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 6 + [
+            ctypes.POINTER(ctypes.c_float)] * 2
+        L.oracle_estimate_facial_features.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 6 + [
+            ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -184,3 +188,27 @@ def exp(x):
 
 def expf(x):
     return lib().oracle_expf(x)
+
+
+def estimate_headpose(channels, region=None):
+    """FaceForest::estimateHeadPose on 38 integral planes (38 x (H+1) x (W+1)); region (x, y, w, h)."""
+    ch = np.ascontiguousarray(channels, np.uint32)
+    h, w = ch.shape[1] - 1, ch.shape[2] - 1
+    rx, ry, rw, rh = region or (0, 0, w, h)
+    hp, var = ctypes.c_float(), ctypes.c_float()
+    if lib().oracle_estimate_headpose(ch.ctypes.data, w, h, rx, ry, rw, rh, ctypes.byref(hp), ctypes.byref(var)) != 0:
+        raise RuntimeError(lib().oracle_last_error().decode())
+    return hp.value, var.value
+
+
+def estimate_facial_features(channels, region, tree_ids):
+    """FaceForest::estimateFacialFeatures: 10 x 2 int landmarks in sample coordinates."""
+    ch = np.ascontiguousarray(channels, np.uint32)
+    h, w = ch.shape[1] - 1, ch.shape[2] - 1
+    rx, ry, rw, rh = region or (0, 0, w, h)
+    t = np.ascontiguousarray(tree_ids, np.int32)
+    pts = np.zeros((10, 2), np.int32)
+    if lib().oracle_estimate_facial_features(ch.ctypes.data, w, h, rx, ry, rw, rh, t.ctypes.data, t.size,
+                                             pts.ctypes.data) != 0:
+        raise RuntimeError(lib().oracle_last_error().decode())
+    return pts

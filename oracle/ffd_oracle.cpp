@@ -575,6 +575,100 @@ bool geometry(int bw, int bh, Geometry& g) {
 
 }  // namespace
 
+// getHeadPoseVotesMT (face_utils.cpp:183-242): patches over the region (x from rx while
+// x < rx + rw - patch, step 4, x outer / y inner), every tree per patch, leaf filter fg > 0.5,
+// sequential float sums in that order; FaceForest::estimateHeadPose (FaceForest.cpp:60-72).
+void estimate_headpose(const uint32_t* ch, int W, int H, int rx, int ry, int rw, int rh, int threads, float* out_mean,
+                       float* out_var, std::vector<int>& hp_leafs) {
+  const int P = (int)std::round(g_hp.face_size * g_hp.patch_ratio);
+  const int HT = (int)g_hp.roots.size();
+  std::vector<std::pair<int, int>> hp_patches;
+  for (int x = rx; x < rx + rw - P; x += g_hp_step)
+    for (int y = ry; y < ry + rh - P; y += g_hp_step) hp_patches.push_back({x, y});
+  hp_leafs.assign(hp_patches.size() * HT, 0);
+  run_pool(threads, (int)hp_patches.size(), [&](int i) {
+    for (int t = 0; t < HT; t++)
+      hp_leafs[i * HT + t] = walk(g_hp, g_hp.roots[t], ch, W, H, hp_patches[i].first, hp_patches[i].second);
+  });
+  float n = 0, sum = 0, sum_sq = 0;
+  for (size_t i = 0; i < hp_leafs.size(); ++i) {
+    int L = hp_leafs[i];
+    if (g_hp.hp_fg[L] > 0.5f) {  // HeadPoseEstimatorOption::min_foreground_probability
+      float m = 0;
+      for (int j = 0; j < FFD_NUM_HP_LABELS; j++) m += g_hp.hp_labels[L * 5 + j] * j;
+      m /= (g_hp.hp_n[L] * g_hp.hp_fg[L]);
+      sum += m;
+      sum_sq += m * m;
+      n++;
+    }
+  }
+  float mean = sum / n;
+  float var = (sum_sq / n) - (mean * mean);
+  mean -= 2;
+  var *= 0.05f;  // NORM_HEADPOSE_VARIANCE_FACTOR (Constants.hpp:67)
+  *out_mean = mean;
+  *out_var = var;
+}
+
+// getFacialFeaturesVotesMT (face_utils.cpp:244-302) over the region with the given trees, then
+// MeanShift::shift per part (MeanShift.hpp:41-135; kernel 10, 7 iterations, 0.05) as
+// FaceForest::estimateFacialFeatures (FaceForest.cpp:74-95): pts = cvRound of the modes, in sample
+// coordinates.
+void estimate_facial_features(const uint32_t* ch, int W, int H, int rx, int ry, int rw, int rh,
+                              const std::vector<int>& trees, int threads, int pts[][2], float* ms_mean,
+                              int* vote_counts, std::vector<int>& mp_leafs) {
+  const int P = (int)std::round(g_hp.face_size * g_hp.patch_ratio);
+  const int MT = (int)trees.size();
+  std::vector<std::pair<int, int>> mp_patches;
+  for (int x = rx; x < rx + rw - P; x += g_mp_step_x)
+    for (int y = ry; y < ry + rh - P; y += g_mp_step_y) mp_patches.push_back({x, y});
+  mp_leafs.assign(mp_patches.size() * MT, 0);
+  run_pool(threads, (int)mp_patches.size(), [&](int i) {
+    for (int t = 0; t < MT; t++)
+      mp_leafs[i * MT + t] = walk(g_mp, g_mp.roots[trees[t]], ch, W, H, mp_patches[i].first, mp_patches[i].second);
+  });
+  struct Vote { int x, y; float w; };
+  std::vector<std::vector<Vote>> votes(FFD_NUM_PARTS);
+  for (size_t k = 0; k < mp_leafs.size(); k++) {
+    int L = mp_leafs[k];
+    int ox = mp_patches[k / MT].first + P / 2, oy = mp_patches[k / MT].second + P / 2;
+    for (int i = 0; i < FFD_NUM_PARTS; i++) {
+      float min_pf = 0.25f;             // MultiPartEstimatorOption::min_pf
+      if (i == 0 || i == 7) min_pf *= 1.5;
+      if (g_mp.mp_fg[L] > 0.5f && g_mp.mp_pf[L * 10 + i] > min_pf && g_mp.mp_var[L * 10 + i] < 25.f &&
+          g_mp.mp_n[L] > 2)
+        votes[i].push_back({g_mp.mp_off[(L * 10 + i) * 2] + ox, g_mp.mp_off[(L * 10 + i) * 2 + 1] + oy, g_mp.mp_fg[L]});
+    }
+  }
+  for (int i = 0; i < FFD_NUM_PARTS; i++) {
+    const auto& V = votes[i];
+    vote_counts[i] = (int)V.size();
+    float mx = 0, my = 0, sw = 0;
+    for (const auto& v : V) { float w = v.w; mx += v.x * w; my += v.y * w; sw += w; }
+    if (sw > 0) { mx /= sw; my /= sw; }
+    bool conv = false;
+    const float lamda = 10.f, stop = 0.05f;
+    for (int it = 0; it < 7 && !conv; it++) {
+      float sx = 0, sy = 0, s = 0;
+      for (const auto& v : V) {
+        float dx = mx - (float)v.x, dy = my - (float)v.y;
+        float d = (float)std::sqrt((double)dx * dx + (double)dy * dy);
+        d = ffd_expf(-d / lamda);
+        float w = v.w * d;
+        sx += v.x * w; sy += v.y * w; s += w;
+      }
+      if (s > 0) { sx /= s; sy /= s; }
+      float ddx = sx - mx, ddy = sy - my;
+      if (std::sqrt((double)ddx * ddx + (double)ddy * ddy) < stop) conv = true;
+      mx = sx; my = sy;
+    }
+    ms_mean[2 * i] = mx;
+    ms_mean[2 * i + 1] = my;
+    pts[i][0] = cv_round(mx);
+    pts[i][1] = cv_round(my);
+  }
+}
+
 // ------------------------------------------------------------------- C API --
 extern "C" {
 
@@ -657,7 +751,7 @@ int oracle_analyze_face(const uint8_t* bgr, int32_t iw, int32_t ih, int32_t stri
   }
   Geometry g;
   if (!geometry(bw, bh, g)) { g_err = "degenerate box"; return -2; }
-  const int W = g.W, H = g.H, P = g.patch;
+  const int W = g.W, H = g.H;
   std::memset(out, 0, sizeof(*out));
   out->face_w = W; out->face_h = H;
 
@@ -675,33 +769,11 @@ int oracle_analyze_face(const uint8_t* bgr, int32_t iw, int32_t ih, int32_t stri
   catch (const std::exception& e) { g_err = e.what(); return -1; }
   if (tr && tr->channels) std::memcpy(tr->channels, ch.data(), ch.size() * 4);
 
-  // a13: getHeadPoseVotesMT (face_utils.cpp:183-242), grid x outer / y inner, step 4
-  const int HT = (int)g_hp.roots.size();
-  std::vector<std::pair<int, int>> hp_patches;
-  for (int x = 0; x < W - P; x += g_hp_step)
-    for (int y = 0; y < H - P; y += g_hp_step) hp_patches.push_back({x, y});
-  std::vector<int> hp_leafs(hp_patches.size() * HT);
-  run_pool(threads, (int)hp_patches.size(), [&](int i) {
-    for (int t = 0; t < HT; t++)
-      hp_leafs[i * HT + t] = walk(g_hp, g_hp.roots[t], ch.data(), W, H, hp_patches[i].first, hp_patches[i].second);
-  });
+  // a13/a14: estimateHeadPose over the whole scaled face (FaceForest.cpp:211)
+  float mean = 0, var = 0;
+  std::vector<int> hp_leafs;
+  estimate_headpose(ch.data(), W, H, 0, 0, W, H, threads, &mean, &var, hp_leafs);
   if (tr && tr->hp_leaves) std::memcpy(tr->hp_leaves, hp_leafs.data(), hp_leafs.size() * 4);
-  float n = 0, sum = 0, sum_sq = 0;
-  for (size_t i = 0; i < hp_leafs.size(); ++i) {
-    int L = hp_leafs[i];
-    if (g_hp.hp_fg[L] > 0.5f) {  // HeadPoseEstimatorOption::min_foreground_probability
-      float m = 0;
-      for (int j = 0; j < FFD_NUM_HP_LABELS; j++) m += g_hp.hp_labels[L * 5 + j] * j;
-      m /= (g_hp.hp_n[L] * g_hp.hp_fg[L]);
-      sum += m;
-      sum_sq += m * m;
-      n++;
-    }
-  }
-  float mean = sum / n;
-  float var = (sum_sq / n) - (mean * mean);
-  mean -= 2;
-  var *= 0.05f;  // NORM_HEADPOSE_VARIANCE_FACTOR (Constants.hpp:67)
   out->headpose = mean;
   out->pose_variance = var;
 
@@ -727,60 +799,48 @@ int oracle_analyze_face(const uint8_t* bgr, int32_t iw, int32_t ih, int32_t stri
   out->n_trees = (int)trees.size();
   if (tr && tr->trees) std::memcpy(tr->trees, trees.data(), trees.size() * 4);
 
-  // a16: getFacialFeaturesVotesMT (face_utils.cpp:244-302), step 3
-  const int MT = (int)trees.size();
-  std::vector<std::pair<int, int>> mp_patches;
-  for (int x = 0; x < W - P; x += g_mp_step_x)
-    for (int y = 0; y < H - P; y += g_mp_step_y) mp_patches.push_back({x, y});
-  std::vector<int> mp_leafs(mp_patches.size() * MT);
-  run_pool(threads, (int)mp_patches.size(), [&](int i) {
-    for (int t = 0; t < MT; t++)
-      mp_leafs[i * MT + t] = walk(g_mp, g_mp.roots[trees[t]], ch.data(), W, H, mp_patches[i].first, mp_patches[i].second);
-  });
+  // a16-a18: estimateFacialFeatures over the whole scaled face (FaceForest.cpp:253), then the
+  // rescale of FaceForest.cpp:255-257
+  std::vector<int> mp_leafs;
+  int pts[FFD_NUM_PARTS][2];
+  float msm[2 * FFD_NUM_PARTS];
+  int vc[FFD_NUM_PARTS];
+  estimate_facial_features(ch.data(), W, H, 0, 0, W, H, trees, threads, pts, msm, vc, mp_leafs);
   if (tr && tr->mp_leaves) std::memcpy(tr->mp_leaves, mp_leafs.data(), mp_leafs.size() * 4);
-  struct Vote { int x, y; float w; };
-  std::vector<std::vector<Vote>> votes(FFD_NUM_PARTS);
-  for (size_t k = 0; k < mp_leafs.size(); k++) {
-    int L = mp_leafs[k];
-    int ox = mp_patches[k / MT].first + P / 2, oy = mp_patches[k / MT].second + P / 2;
-    for (int i = 0; i < FFD_NUM_PARTS; i++) {
-      float min_pf = 0.25f;             // MultiPartEstimatorOption::min_pf
-      if (i == 0 || i == 7) min_pf *= 1.5;
-      if (g_mp.mp_fg[L] > 0.5f && g_mp.mp_pf[L * 10 + i] > min_pf && g_mp.mp_var[L * 10 + i] < 25.f &&
-          g_mp.mp_n[L] > 2)
-        votes[i].push_back({g_mp.mp_off[(L * 10 + i) * 2] + ox, g_mp.mp_off[(L * 10 + i) * 2 + 1] + oy, g_mp.mp_fg[L]});
-    }
-  }
-  // a18: MeanShift::shift per part (MeanShift.hpp:41-135), kernel 10, 7 iterations, 0.05
+  if (tr && tr->vote_counts) std::memcpy(tr->vote_counts, vc, sizeof(vc));
+  if (tr && tr->ms_mean) std::memcpy(tr->ms_mean, msm, sizeof(msm));
   float inv_scale = 1.0f / g.scale;
   for (int i = 0; i < FFD_NUM_PARTS; i++) {
-    const auto& V = votes[i];
-    if (tr && tr->vote_counts) tr->vote_counts[i] = (int)V.size();
-    float mx = 0, my = 0, sw = 0;
-    for (const auto& v : V) { float w = v.w; mx += v.x * w; my += v.y * w; sw += w; }
-    if (sw > 0) { mx /= sw; my /= sw; }
-    bool conv = false;
-    const float lamda = 10.f, stop = 0.05f;
-    for (int it = 0; it < 7 && !conv; it++) {
-      float sx = 0, sy = 0, s = 0;
-      for (const auto& v : V) {
-        float dx = mx - (float)v.x, dy = my - (float)v.y;
-        float d = (float)std::sqrt((double)dx * dx + (double)dy * dy);
-        d = ffd_expf(-d / lamda);
-        float w = v.w * d;
-        sx += v.x * w; sy += v.y * w; s += w;
-      }
-      if (s > 0) { sx /= s; sy /= s; }
-      float ddx = sx - mx, ddy = sy - my;
-      if (std::sqrt((double)ddx * ddx + (double)ddy * ddy) < stop) conv = true;
-      mx = sx; my = sy;
-    }
-    if (tr && tr->ms_mean) { tr->ms_mean[2 * i] = mx; tr->ms_mean[2 * i + 1] = my; }
-    int px = cv_round(mx), py = cv_round(my);
     // FaceForest.cpp:255-257: Point_<int> *= 1.0f/scale -> cvRound(x * inv)
-    out->points[i][0] = cv_round((float)px * inv_scale);
-    out->points[i][1] = cv_round((float)py * inv_scale);
+    out->points[i][0] = cv_round((float)pts[i][0] * inv_scale);
+    out->points[i][1] = cv_round((float)pts[i][1] * inv_scale);
   }
+  return 0;
+}
+
+static bool region_ok(int W, int H, int rx, int ry, int rw, int rh) {
+  return rx >= 0 && ry >= 0 && rw > 0 && rh > 0 && rx + rw <= W && ry + rh <= H;
+}
+
+int oracle_estimate_headpose(const uint32_t* channels, int32_t W, int32_t H, int32_t rx, int32_t ry, int32_t rw,
+                             int32_t rh, float* headpose, float* variance) {
+  if (!g_loaded) { g_err = "model not loaded"; return -1; }
+  if (!region_ok(W, H, rx, ry, rw, rh)) { g_err = "face_bbox outside the image sample"; return -2; }
+  std::vector<int> leafs;
+  estimate_headpose(channels, W, H, rx, ry, rw, rh, 1, headpose, variance, leafs);
+  return 0;
+}
+
+int oracle_estimate_facial_features(const uint32_t* channels, int32_t W, int32_t H, int32_t rx, int32_t ry,
+                                    int32_t rw, int32_t rh, const int32_t* tree_ids, int32_t n_trees,
+                                    int32_t* points) {
+  if (!g_loaded) { g_err = "model not loaded"; return -1; }
+  if (!region_ok(W, H, rx, ry, rw, rh)) { g_err = "face_bbox outside the image sample"; return -2; }
+  std::vector<int> trees(tree_ids, tree_ids + n_trees), leafs;
+  int pts[FFD_NUM_PARTS][2], vc[FFD_NUM_PARTS];
+  float msm[2 * FFD_NUM_PARTS];
+  estimate_facial_features(channels, W, H, rx, ry, rw, rh, trees, 1, pts, msm, vc, leafs);
+  for (int i = 0; i < FFD_NUM_PARTS; i++) { points[2 * i] = pts[i][0]; points[2 * i + 1] = pts[i][1]; }
   return 0;
 }
 

@@ -56,6 +56,15 @@ int oracle_analyze_face(const uint8_t* bgr, int32_t w, int32_t h, int32_t stride
                         int32_t bx, int32_t by, int32_t bw, int32_t bh, int32_t threads,
                         oracle_face* out, oracle_trace* trace);
 
+/* FaceForest::estimateHeadPose / estimateFacialFeatures (FaceForest.cpp:60-95) on an image
+ * sample's 38 integral planes ([c][H+1][W+1]) with patches over the region (rx, ry, rw, rh);
+ * points: 10 x (x, y) cvRound'ed MeanShift modes in sample coordinates. */
+int oracle_estimate_headpose(const uint32_t* channels, int32_t W, int32_t H, int32_t rx, int32_t ry, int32_t rw,
+                             int32_t rh, float* headpose, float* variance);
+int oracle_estimate_facial_features(const uint32_t* channels, int32_t W, int32_t H, int32_t rx, int32_t ry,
+                                    int32_t rw, int32_t rh, const int32_t* tree_ids, int32_t n_trees,
+                                    int32_t* points);
+
 /* Geometry of the scaled face for a bbox of bw x bh. */
 int oracle_face_geometry(int32_t bw, int32_t bh, int32_t* face_w, int32_t* face_h,
                          int32_t* n_hp_patches, int32_t* n_mp_patches);
