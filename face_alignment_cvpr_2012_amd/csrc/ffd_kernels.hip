@@ -643,6 +643,12 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 #ifndef FFD_TRAV_SLEEP_GROUP
 #define FFD_TRAV_SLEEP_GROUP 8
 #endif
+#ifndef FFD_TRAV_ONELOAD
+#define FFD_TRAV_ONELOAD 0  // timing probe: one 16-B node load per visit (c1 := c0; results invalid)
+#endif
+#ifndef FFD_TRAV_SAMETREE
+#define FFD_TRAV_SAMETREE 0  // timing probe: every walk of a block uses the block's first tree
+#endif
 #ifndef FFD_TRAV_K
 #define FFD_TRAV_K 1  // walks per walker lane (> 1: interleaved, each fetching only its taken child)
 #endif
@@ -744,7 +750,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       if (xi >= B.nx || yi >= B.ny) return;
       w.wbase = (yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh;
       w.oidx = (xi * B.ny + yi) * B.T + t;  // reference order: patch x-major, tree-minor
-      w.nd = root_rec[t];
+      w.nd = root_rec[FFD_TRAV_SAMETREE ? 0 : t];
       w.done = false;
     };
     // both children's records are requested before the split test is evaluated, so the node
@@ -752,7 +758,11 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     uint32_t probe_acc = 0;  // FFD_TRAV_X* perturbation probes (timing only; never changes results)
     auto advance = [&](Walk& w) {
       const uint4 v = w.nd;
+#if FFD_TRAV_ONELOAD
+      const uint4 c0 = A.nodes[v.x], c1 = c0;
+#else
       const uint4 c0 = A.nodes[v.x], c1 = A.nodes[v.x + 1];
+#endif
       const unsigned char* base = reinterpret_cast<const unsigned char*>(win) + 2 * w.wbase;
       const int p1 = rect_mean_walk(base, v.y, (v.w >> 10) & 511u, 2 * LW);
       const int p2 = rect_mean_walk(base, v.z, v.w >> 19, 2 * LW);
