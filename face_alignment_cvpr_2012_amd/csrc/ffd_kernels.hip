@@ -634,6 +634,9 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 #ifndef FFD_TRAV_XMEM
 #define FFD_TRAV_XMEM 0
 #endif
+#ifndef FFD_TRAV_XMEM2
+#define FFD_TRAV_XMEM2 0
+#endif
 #ifndef FFD_TRAV_XVALU
 #define FFD_TRAV_XVALU 0
 #endif
@@ -771,6 +774,9 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
 #endif
 #if FFD_TRAV_XMEM
       probe_acc += A.nodes[v.x ^ 64u].y;
+#endif
+#if FFD_TRAV_XMEM2  // one more 16-B load from the same 64-B sector as the children
+      { const uint4 q = A.nodes[v.x ^ 2u]; probe_acc += q.x ^ q.y ^ q.z ^ q.w; }
 #endif
 #if FFD_TRAV_XVALU
 #pragma unroll
