@@ -34,12 +34,16 @@ constexpr uint32_t LEAF_BIT = 0x80000000u;
 // Source fields: ThresholdSplit<SimplePatchFeature> (ThresholdSplit.hpp:51-67,
 // ImageSample.hpp:462-464) and TreeNode::left/right (TreeNode.hpp:138-141).
 //
-// Walk nodes (k_traverse, re-encoded per forest for its LDS window of WH rows x LW columns):
-//   x: as above (child index / LEAF_BIT | ordinal)
-//   y: rect1: byte offset of its top-left integral corner in the window, channel plane included
-//      (18 bits) | 2*w << 18 (6 bits) | h << 24
-//   z: rect2, same layout
-//   w: threshold (10-bit two's complement) | w1*h1 << 10 (9 bits) | w2*h2 << 19 (9 bits)
+// Pair records (k_traverse): 16 bytes = the two children (c0, c1) of one internal node, each as
+// a 56-bit test, plus a 16-bit offset.  Words: x = lo(c0), y = lo(c1), z = hi(c0) | off1[7:0] << 24,
+// w = hi(c1) | off1[15:8] << 24, where for a split node
+//   lo = x1 | y1 << 5 | x2 << 10 | y2 << 15 | ch << 20 | thr[5:0] << 26
+//   hi = (w1-1) | (h1-1) << 5 | (w2-1) << 10 | (h2-1) << 15 | thr[9:6] << 20
+// (rectangles patch-relative, sides 1..22, threshold 10-bit two's complement), and for a leaf
+// ch = 63 with the leaf ordinal = lo[19:0] | hi << 20.  Depth-first layout per tree: the pair of
+// c0's children is the next record, c1's children are off1 records ahead (off1 = 0: the 32-bit
+// offset is far[pair]).  Each tree starts with a root pair (root, unused leaf).
+// Source fields: ThresholdSplit<SimplePatchFeature> (ThresholdSplit.hpp:51-67, ImageSample.hpp:83-90).
 
 struct FaceDesc {
   int64_t img_off;        // byte offset of the source image

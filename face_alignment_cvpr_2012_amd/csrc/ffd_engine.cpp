@@ -142,65 +142,85 @@ void flatten_forest(const ModelFile& m, const std::string& p, std::vector<uint4>
   if ((int64_t)nodes.size() != (int64_t)nl.count()) throw std::runtime_error("node count mismatch");
 }
 
-// Re-lay breadth-first walk nodes (children adjacent) into 128-byte "pair blocks" so that every
-// second level of a walk is a hit in the cache line the previous level brought in:
-//   root block:    [root, -, children of root, children of slot 2, children of slot 3]
-//   general block: [pair P, children of P.0, children of P.1, -, -]
-// Children of the block's last level start new blocks.  Leaves keep their ordinals; the padding
-// slots are never referenced.  Speed only: every walk visits the same nodes in the same order.
 }  // namespace
 
-void ffd_host::layout_pair_blocks(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots,
-                                  std::vector<uint4>& out, std::vector<int32_t>& out_roots) {
-  const uint4 pad = make_uint4(LEAF_BIT, 0u, 0u, 0u);
+// One node's 56-bit test (ffd_device.hpp "pair records"): lo 32 bits, hi 24 bits.
+static void encode_test(const uint4& n, uint32_t& lo, uint32_t& hi) {
+  if (n.x & LEAF_BIT) {
+    const uint64_t ord = n.x & ~LEAF_BIT;
+    lo = (uint32_t)(ord & 0xFFFFFu) | 63u << 20;
+    hi = (uint32_t)(ord >> 20) & 0xFFFFFFu;
+    return;
+  }
+  const uint32_t ch = n.y & 63u, w1 = (n.y >> 6) & 31u, h1 = (n.y >> 11) & 31u, w2 = (n.y >> 16) & 31u,
+                 h2 = (n.y >> 21) & 31u;
+  const uint32_t e1 = n.w & 0xFFFFu, e2 = n.w >> 16;
+  const uint32_t x1 = e1 % PITCH, y1 = e1 / PITCH, x2 = e2 % PITCH, y2 = e2 / PITCH;
+  const int thr = (int)n.z;
+  if (ch >= 63 || x1 > 31 || y1 > 31 || x2 > 31 || y2 > 31 || w1 < 1 || w1 > 22 || h1 < 1 || h1 > 22 || w2 < 1 ||
+      w2 > 22 || h2 < 1 || h2 > 22 || thr < -512 || thr > 511)
+    throw std::runtime_error("split outside the pair-record encoding");
+  const uint32_t t = (uint32_t)thr & 0x3FFu;
+  lo = x1 | y1 << 5 | x2 << 10 | y2 << 15 | ch << 20 | (t & 63u) << 26;
+  hi = (w1 - 1) | (h1 - 1) << 5 | (w2 - 1) << 10 | (h2 - 1) << 15 | (t >> 6) << 20;
+}
+
+// Depth-first pair layout: a pair (a, b) is followed by the pair of a's children and a's whole
+// subtree, then b's children pair at offset off1 (16 bits; 0 = look up far[pair]).  Each tree starts
+// with a root pair (root, unused leaf).  Leaves keep their model ordinals; speed-neutral for parity:
+// every walk visits the same nodes in the same order as Tree<S>::evaluateMT.
+void ffd_host::build_pair_records(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots,
+                                  std::vector<uint4>& out, std::vector<int32_t>& roots_out,
+                                  std::vector<uint32_t>& far) {
   out.clear();
-  out_roots.clear();
+  roots_out.clear();
+  far.clear();
   auto internal = [&](uint32_t i) { return !(bfs[i].x & LEAF_BIT); };
+  const uint4 unused_leaf = make_uint4(LEAF_BIT, 0u, 0u, 0u);
+  // iterative DFS: a frame places pair (a, b); phase 0 = a's children, 1 = b's children, 2 = done
+  struct Frame { uint4 a, b; size_t idx; int phase; };
   for (int32_t root : roots) {
-    // (bfs index of a pair's first node, slot of the out node whose child pointer it fills)
-    std::vector<std::pair<uint32_t, int64_t>> queue;
-    auto place = [&](uint32_t src, int64_t dst) {  // copy a node; its child pointer is patched later
-      out[dst] = bfs[src];
-    };
-    const int64_t rb = (int64_t)out.size();
-    out.resize(rb + 8, pad);
-    out_roots.push_back((int32_t)rb);
-    place((uint32_t)root, rb);
-    size_t qi = 0;
-    if (internal((uint32_t)root)) {
-      const uint32_t c = bfs[(uint32_t)root].x;
-      out[rb].x = (uint32_t)(rb + 2);
-      place(c, rb + 2);
-      place(c + 1, rb + 3);
-      for (int j = 0; j < 2; j++) {
-        if (!internal(c + j)) continue;
-        const uint32_t gc = bfs[c + j].x;
-        out[rb + 2 + j].x = (uint32_t)(rb + 4 + 2 * j);
-        place(gc, rb + 4 + 2 * j);
-        place(gc + 1, rb + 5 + 2 * j);
-        for (int k = 0; k < 2; k++)
-          if (internal(gc + k)) queue.push_back({bfs[gc + k].x, rb + 4 + 2 * j + k});
+    std::vector<Frame> st;
+    roots_out.push_back((int32_t)out.size());
+    st.push_back({bfs[(uint32_t)root], unused_leaf, out.size(), 0});
+    out.push_back(make_uint4(0, 0, 0, 0));
+    far.push_back(0);
+    while (!st.empty()) {
+      Frame& f = st.back();
+      if (f.phase == 0) {
+        f.phase = 1;
+        if (!(f.a.x & LEAF_BIT)) {
+          const uint32_t c = f.a.x;
+          st.push_back({bfs[c], bfs[c + 1], out.size(), 0});
+          out.push_back(make_uint4(0, 0, 0, 0));
+          far.push_back(0);
+        }
+        continue;
       }
-    }
-    for (; qi < queue.size(); qi++) {
-      const uint32_t p = queue[qi].first;
-      const int64_t b = (int64_t)out.size();
-      out.resize(b + 8, pad);
-      out[queue[qi].second].x = (uint32_t)b;
-      place(p, b);
-      place(p + 1, b + 1);
-      for (int j = 0; j < 2; j++) {
-        if (!internal(p + j)) continue;
-        const uint32_t c = bfs[p + j].x;
-        out[b + j].x = (uint32_t)(b + 2 + 2 * j);
-        place(c, b + 2 + 2 * j);
-        place(c + 1, b + 3 + 2 * j);
-        for (int k = 0; k < 2; k++)
-          if (internal(c + k)) queue.push_back({bfs[c + k].x, b + 2 + 2 * j + k});
+      if (f.phase == 1) {
+        f.phase = 2;
+        const uint64_t off1 = out.size() - f.idx;  // where b's children pair goes
+        uint32_t lo0, hi0, lo1, hi1;
+        encode_test(f.a, lo0, hi0);
+        encode_test(f.b, lo1, hi1);
+        uint32_t o16 = off1 <= 0xFFFFu ? (uint32_t)off1 : 0u;
+        if (o16 == 0 && !(f.b.x & LEAF_BIT)) far[f.idx] = (uint32_t)off1;
+        if (off1 > 0xFFFFFFFFull) throw std::runtime_error("pair array too large");
+        out[f.idx] = make_uint4(lo0, lo1, hi0 | (o16 & 0xFFu) << 24, hi1 | (o16 >> 8) << 24);
+        if (!(f.b.x & LEAF_BIT)) {
+          const uint32_t c = f.b.x;
+          const size_t at = out.size();
+          out.push_back(make_uint4(0, 0, 0, 0));
+          far.push_back(0);
+          st.push_back({bfs[c], bfs[c + 1], at, 0});
+        }
+        continue;
       }
+      st.pop_back();
     }
   }
-  if (out.size() >= (size_t)LEAF_BIT) throw std::runtime_error("walk-node array too large");
+  (void)internal;
+  if (out.size() >= 0x80000000ull) throw std::runtime_error("pair array too large");
 }
 
 void ffd_engine::load_model(const std::string& path) {
@@ -459,8 +479,8 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
     HIP_CHECK(hipStreamWaitEvent(st, w.fork_ev[1 + i], 0));
   }
   stage(7, st, [&] {
-    launch_traverse(true, dfd, n, blocks_per_face(fds, true, trav_g_hp), trav_g_hp, hp_wnodes.as<uint4>(),
-                    hp_wroots.as<int32_t>(), nullptr, hp_trees, desc.hp_option.step_size, desc.hp_option.step_size,
+    launch_traverse(true, dfd, n, blocks_per_face(fds, true, trav_g_hp), trav_g_hp, hp_pairs.as<uint4>(),
+                    hp_proots.as<int32_t>(), hp_far.as<uint32_t>(), nullptr, hp_trees, desc.hp_option.step_size, desc.hp_option.step_size,
                     plane, w.chan.as<uint16_t>(),
                     w.hpleaf.as<int32_t>(), trav_wg, st);
   });
@@ -469,8 +489,8 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
                    w.state.as<HpState>(), d_out, st);
   });
   stage(9, st, [&] {
-    launch_traverse(false, dfd, n, blocks_per_face(fds, false, trav_g_mp), trav_g_mp, mp_wnodes.as<uint4>(),
-                    mp_wroots.as<int32_t>(), w.state.as<HpState>(), 0, desc.mp_option.step_size, mp_step_y(),
+    launch_traverse(false, dfd, n, blocks_per_face(fds, false, trav_g_mp), trav_g_mp, mp_pairs.as<uint4>(),
+                    mp_proots.as<int32_t>(), mp_far.as<uint32_t>(), w.state.as<HpState>(), 0, desc.mp_option.step_size, mp_step_y(),
                     plane, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), trav_wg, st);
   });
   const int n_parts = std::min(desc.mp_option.num_parts, NPARTS);
@@ -663,7 +683,6 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   if (const char* v = std::getenv("FFD_TRAV_G_HP")) e->trav_g_hp = std::max(3, std::min(5, std::atoi(v)));
   if (const char* v = std::getenv("FFD_TRAV_G_FFD")) e->trav_g_mp = std::max(3, std::min(5, std::atoi(v)));
   if (const char* v = std::getenv("FFD_TRAV_WG")) e->trav_wg = std::max(8, std::atoi(v));
-  if (const char* v = std::getenv("FFD_NODE_LAYOUT")) e->pair_blocks = std::string(v) != "bfs";
   if (const char* v = std::getenv("FFD_CHANNEL_STREAMS")) e->channel_streams = std::max(1, std::min(4, std::atoi(v)));
   if (const char* v = std::getenv("FFD_CHUNK")) e->max_chunk = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("FFD_STREAMS")) e->n_streams = std::max(1, std::min(8, std::atoi(v)));
@@ -964,8 +983,8 @@ ffd_status ffd_estimate_headpose(ffd_engine* e, const uint32_t* channels, int32_
     const FaceDesc* dfd = w.faces.as<FaceDesc>();
     std::vector<FaceDesc> fv{f};
     e->out.ensure(sizeof(FaceOut));
-    launch_traverse(true, dfd, 1, blocks_per_face(fv, true, e->trav_g_hp), e->trav_g_hp, e->hp_wnodes.as<uint4>(),
-                    e->hp_wroots.as<int32_t>(), nullptr, e->hp_trees, e->desc.hp_option.step_size,
+    launch_traverse(true, dfd, 1, blocks_per_face(fv, true, e->trav_g_hp), e->trav_g_hp, e->hp_pairs.as<uint4>(),
+                    e->hp_proots.as<int32_t>(), e->hp_far.as<uint32_t>(), nullptr, e->hp_trees, e->desc.hp_option.step_size,
                     e->desc.hp_option.step_size, f.plane, w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), e->trav_wg,
                     w.stream);
     launch_hp_pose(dfd, 1, w.hpleaf.as<int32_t>(), e->hp_m.as<float>(), e->hp_trees, e->n_forests,
@@ -1004,8 +1023,8 @@ ffd_status ffd_estimate_facial_features(ffd_engine* e, const uint32_t* channels,
     HIP_CHECK(hipMemcpyAsync(w.state.p, &hs, sizeof(hs), hipMemcpyHostToDevice, w.stream));
     e->out.ensure(sizeof(FaceOut));
     const int n_parts = std::min(e->desc.mp_option.num_parts, NPARTS);
-    launch_traverse(false, dfd, 1, blocks_per_face(fv, false, e->trav_g_mp), e->trav_g_mp, e->mp_wnodes.as<uint4>(),
-                    e->mp_wroots.as<int32_t>(), w.state.as<HpState>(), 0, e->desc.mp_option.step_size, e->mp_step_y(),
+    launch_traverse(false, dfd, 1, blocks_per_face(fv, false, e->trav_g_mp), e->trav_g_mp, e->mp_pairs.as<uint4>(),
+                    e->mp_proots.as<int32_t>(), e->mp_far.as<uint32_t>(), w.state.as<HpState>(), 0, e->desc.mp_option.step_size, e->mp_step_y(),
                     f.plane, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), e->trav_wg, w.stream);
     launch_votes(dfd, 1, w.mpleaf.as<int32_t>(), e->mp_rec.as<uint4>(), e->vote_rec_compact, e->vote_bias_x,
                  e->vote_bias_y, w.state.as<HpState>(), MAX_TREES, e->desc.mp_option.step_size, e->mp_step_y(),

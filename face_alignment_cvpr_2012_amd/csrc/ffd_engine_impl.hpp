@@ -93,8 +93,10 @@ struct Workspace {
 };
 
 namespace ffd_host {
-void layout_pair_blocks(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots, std::vector<uint4>& out,
-                        std::vector<int32_t>& out_roots);
+// Re-encode breadth-first 16-byte nodes (children adjacent) as k_traverse's 16-byte pair records
+// in depth-first order (ffd_device.hpp "pair records"); roots_out[t] = tree t's root pair.
+void build_pair_records(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots, std::vector<uint4>& out,
+                        std::vector<int32_t>& roots_out, std::vector<uint32_t>& far);
 }  // namespace ffd_host
 
 struct ffd_engine {
@@ -115,11 +117,11 @@ struct ffd_engine {
 
   // device model
   DevBuf gabor_coef, hp_nodes, hp_roots, hp_sizes, hp_m, mp_nodes, mp_roots, mp_sizes, mp_rec;
-  DevBuf hp_wnodes, mp_wnodes;       // walk-node encodings for k_traverse (ffd_device.hpp)
-  DevBuf hp_wroots, mp_wroots;       // tree roots in the walk-node arrays
+  DevBuf hp_pairs, mp_pairs;         // pair records for k_traverse (ffd_device.hpp "pair records")
+  DevBuf hp_proots, mp_proots;       // per tree: index of its root pair
+  DevBuf hp_far, mp_far;             // per pair: far offset of child 1's children (when > 65535)
   std::vector<uint4> hp_nodes_h, mp_nodes_h;  // host copies until the walk nodes are built
   std::vector<int32_t> hp_roots_h, mp_roots_h;
-  bool pair_blocks = true;           // walk-node layout (FFD_NODE_LAYOUT=bfs for plain breadth-first)
   bool vote_rec_compact = false;     // 32-B vote records (else 64-B), see load_model
   int vote_bias_x = 0, vote_bias_y = 0;
 
@@ -210,27 +212,20 @@ struct ffd_engine {
     };
     fit(trav_g_hp, desc.hp_option.step_size, desc.hp_option.step_size);
     fit(trav_g_mp, desc.mp_option.step_size, mp_step_y());
-    auto walk_nodes = [&](std::vector<uint4>& h, std::vector<int32_t>& roots, DevBuf& d, DevBuf& droots, int G,
-                          int step, int step_y) {
-      std::vector<uint4> wn(h.size());
-      if (!encode_walk_nodes(h.data(), h.size(), G, step, step_y, wn.data()))
-        throw std::runtime_error("forest does not fit the traversal's walk-node encoding");
-      if (pair_blocks) {
-        std::vector<uint4> pb;
-        std::vector<int32_t> pr;
-        ffd_host::layout_pair_blocks(wn, roots, pb, pr);
-        wn.swap(pb);
-        roots.swap(pr);
-      }
-      upload(d, wn, main_stream());
-      upload(droots, roots, main_stream());
+    auto pairs = [&](std::vector<uint4>& h, std::vector<int32_t>& roots, DevBuf& d, DevBuf& droots, DevBuf& dfar) {
+      std::vector<uint4> pr;
+      std::vector<int32_t> rp;
+      std::vector<uint32_t> far;
+      ffd_host::build_pair_records(h, roots, pr, rp, far);
+      upload(d, pr, main_stream());
+      upload(droots, rp, main_stream());
+      upload(dfar, far, main_stream());
       HIP_CHECK(hipStreamSynchronize(main_stream()));
       std::vector<uint4>().swap(h);
       std::vector<int32_t>().swap(roots);
     };
-    walk_nodes(hp_nodes_h, hp_roots_h, hp_wnodes, hp_wroots, trav_g_hp, desc.hp_option.step_size,
-               desc.hp_option.step_size);
-    walk_nodes(mp_nodes_h, mp_roots_h, mp_wnodes, mp_wroots, trav_g_mp, desc.mp_option.step_size, mp_step_y());
+    pairs(hp_nodes_h, hp_roots_h, hp_pairs, hp_proots, hp_far);
+    pairs(mp_nodes_h, mp_roots_h, mp_pairs, mp_proots, mp_far);
     HIP_CHECK(set_traverse_lds_limit(cap));
     HIP_CHECK(set_gabor_lds_limit(96 * 1024));  // padded u8 face of up to MAX_FACE_H rows
     hipDeviceProp_t prop;

@@ -584,20 +584,19 @@ __device__ __forceinline__ int node_off(uint32_t enc, int ld) {
   return (int)__umul24(enc >> 7, (unsigned)ld) + (int)(enc & 127u);
 }
 
-// Walk-node rectangle (k_traverse; encoding in ffd_device.hpp "walk nodes"): e = byte offset of
-// the rectangle's top-left integral corner in the window (channel plane included) | 2w << 18 |
-// h << 24.  ImageSample::evalTest's (int)(R / (float)area) as fma(R, rcp(area), 0.00075) truncated:
-// equal to the integer quotient for every R in [0, 255 area], area in [1, 484], with rcp off by up
-// to 2 ulp (tests/test_numerics.py checks all pairs).
-__device__ __forceinline__ int rect_mean_walk(const unsigned char* __restrict__ base, uint32_t e, uint32_t area, int ld2) {
-  const unsigned char* p = base + (e & 0x3FFFFu);
-  const int wb = (int)((e >> 18) & 63u);
-  const int r1 = (int)__umul24(e >> 25, (unsigned)ld2), r2 = (int)__umul24(e >> 24, (unsigned)ld2);
+// ImageSample::evalTest's rectangle mean over the LDS window (k_traverse): p = byte address of the
+// rectangle's top-left integral corner, ld2 = window row pitch in bytes.  The sum is taken as two
+// halves split at h >> 1 rows, each exact modulo 2^16 (rect_mean16), and the quotient
+// (int)(R / (float)(w*h)) as fma(R, rcp(area), 0.00075) truncated: equal to the integer quotient
+// for every R in [0, 255 area], area in [1, 484], with rcp off by up to 2 ulp (tests/test_numerics.py).
+__device__ __forceinline__ int rect_mean_lds(const unsigned char* __restrict__ p, uint32_t w, uint32_t h, int ld2) {
+  const int wb = (int)(2u * w);
+  const int r1 = (int)__umul24(h >> 1, (unsigned)ld2), r2 = (int)__umul24(h, (unsigned)ld2);
   const uint32_t a = *reinterpret_cast<const uint16_t*>(p), b = *reinterpret_cast<const uint16_t*>(p + wb);
   const uint32_t c = *reinterpret_cast<const uint16_t*>(p + r1), d = *reinterpret_cast<const uint16_t*>(p + r1 + wb);
   const uint32_t f0 = *reinterpret_cast<const uint16_t*>(p + r2), f1 = *reinterpret_cast<const uint16_t*>(p + r2 + wb);
   const uint32_t top = (d - c - b + a) & 0xFFFFu, bot = (f1 - f0 - d + c) & 0xFFFFu;
-  return (int)__builtin_fmaf((float)(top + bot), __builtin_amdgcn_rcpf((float)area), 0.00075f);
+  return (int)__builtin_fmaf((float)(top + bot), __builtin_amdgcn_rcpf((float)__umul24(w, h)), 0.00075f);
 }
 
 // Tree<S>::evaluateMT over global u16 planes (ffd_forest_eval_leaves hook).
@@ -616,44 +615,22 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 
 // Traversal of all (patch, tree) pairs of a batch.  Work unit = a G x G block of one face's patch
 // grid with ALL the face's trees: the block's 38-channel u16 integral window (WW = 32 + step*(G-1)
-// rows and columns) sits in LDS, so every rectangle read is an LDS read and only node records come
-// from L2.  The window fills the CU's LDS, so the kernel is persistent (one workgroup per CU) and
-// software-pipelined: waves [NW/64, NT/64) load the NEXT block's window into registers while waves
-// [0, NW/64) walk the current block; the registers are committed to LDS between blocks.  Blocks
-// are dealt XCD-contiguously and face-major, so the 32 workgroups of an XCD share one or two faces'
-// planes in that XCD's L2.
+// columns, WH = 32 + step_y*(G-1) rows) sits in LDS, so every rectangle read is an LDS read and only
+// pair records come from L2.  The window fills the CU's LDS, so the kernel is persistent (one
+// workgroup per CU) and software-pipelined: waves [NW/64, NT/64) load the NEXT block's window into
+// registers while waves [0, NW/64) walk the current block; the registers are committed to LDS
+// between blocks.  Blocks are dealt XCD-contiguously and face-major, so the 32 workgroups of an XCD
+// share one or two faces' planes in that XCD's L2.
+//
+// A walk holds the 16-byte pair record of the node it stands on (both siblings' 56-bit tests,
+// ffd_device.hpp "pair records"): the node's children pair is requested before its test is
+// evaluated (one 16-byte load per visit; the CU's vector-memory return path is the traversal's
+// bottleneck, profiles/r2a), and the test picks the child.
 #ifndef FFD_TRAV_PROBE
 #define FFD_TRAV_PROBE 0  // timing probes (tools/probe.sh): 1 = stage only, 2 = walk only
 #endif
 #ifndef FFD_TRAV_NW
 #define FFD_TRAV_NW 320
-#endif
-#ifndef FFD_TRAV_XLDS
-#define FFD_TRAV_XLDS 0
-#endif
-#ifndef FFD_TRAV_XMEM
-#define FFD_TRAV_XMEM 0
-#endif
-#ifndef FFD_TRAV_XMEM2
-#define FFD_TRAV_XMEM2 0
-#endif
-#ifndef FFD_TRAV_XVALU
-#define FFD_TRAV_XVALU 0
-#endif
-#ifndef FFD_TRAV_SLEEP
-#define FFD_TRAV_SLEEP 0  // staging throttle probe: s_sleep between load groups
-#endif
-#ifndef FFD_TRAV_SLEEP_GROUP
-#define FFD_TRAV_SLEEP_GROUP 8
-#endif
-#ifndef FFD_TRAV_ONELOAD
-#define FFD_TRAV_ONELOAD 0  // timing probe: one 16-B node load per visit (c1 := c0; results invalid)
-#endif
-#ifndef FFD_TRAV_SAMETREE
-#define FFD_TRAV_SAMETREE 0  // timing probe: every walk of a block uses the block's first tree
-#endif
-#ifndef FFD_TRAV_K
-#define FFD_TRAV_K 1  // walks per walker lane (> 1: interleaved, each fetching only its taken child)
 #endif
 constexpr int TRAV_NT = 1024, TRAV_NW = FFD_TRAV_NW, TRAV_NS = TRAV_NT - TRAV_NW;
 // Window chunks held in registers per staging thread: 16-byte chunks when the window row pitch is
@@ -667,7 +644,8 @@ template <> struct TravStage<16> { static constexpr int U = (11000 + TRAV_NS - 1
 __host__ __device__ __forceinline__ int trav_row_pitch(int WW) { return (WW + 3 + 3) & ~3; }
 __host__ __device__ __forceinline__ int trav_chunk_bytes(int WW) { return trav_row_pitch(WW) % 8 == 0 ? 16 : 8; }
 
-// Window bytes (16-byte aligned); the block's root node records (uint4 [MAX_TREES]) follow it.
+// Window bytes (16-byte aligned); the block's root pair records (uint4 [MAX_TREES]) and their
+// indices (u32 [MAX_TREES]) follow it.
 __host__ __device__ __forceinline__ int trav_window_bytes(int WW, int WH) {
   return (NCH * WH * trav_row_pitch(WW) * 2 + 15) & ~15;
 }
@@ -677,8 +655,9 @@ constexpr int BUF_WORD3 = 0x00020000;  // raw buffer resource word 3 (gfx950: 32
 struct TravArgs {
   const FaceDesc* faces;
   int n_faces, bpf;        // blocks per face: ceil(nx/G) * ceil(ny/G) (max over the batch)
-  const uint4* nodes;
-  const int32_t* roots;
+  const uint4* pairs;      // pair records
+  const int32_t* roots;    // per tree: its root pair
+  const uint32_t* far;     // per pair: offset of child 1's children pair when it exceeds 16 bits
   const HpState* hp_state; // FFD pass: selected trees; nullptr for the head-pose pass
   int ntrees_hp;           // head-pose pass: number of trees
   int step, step_y;        // patch grid steps (x, y)
@@ -698,7 +677,8 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   const int step = A.step, stepy = A.step_y, WW = 32 + step * (G - 1), WH = 32 + stepy * (G - 1);
   const int LW = trav_row_pitch(WW), nq = LW * 2 / CB;
   const int total = NCH * WH * nq;  // chunks per window (host guarantees <= NS * U)
-  uint4* root_rec = reinterpret_cast<uint4*>(smem + trav_window_bytes(WW, WH));  // [t]: tree t's root
+  uint4* root_rec = reinterpret_cast<uint4*>(smem + trav_window_bytes(WW, WH));  // [t]: tree t's root pair
+  uint32_t* root_idx = reinterpret_cast<uint32_t*>(root_rec + MAX_TREES);
   // XCD-contiguous, face-major block range of this workgroup's XCD; workgroups of one XCD stride it
   const int N = A.n_faces * A.bpf, xcd = blockIdx.x & 7, k = blockIdx.x >> 3, nk = gridDim.x >> 3;
   const int q8 = N >> 3, r8 = N & 7;
@@ -729,111 +709,41 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     return B;
   };
 
-  // staging registers: window chunks (c, r, q) of the next block, NS chunks apart
-  // (buffer loads: 32-bit offsets, and reads past the face's planes return 0; window rows below
-  // the face's integral image are never referenced by a patch)
-  struct Walk {
-    uint4 nd;
-    int wbase;  // window offset of the patch's top-left corner
-    int oidx;   // output index
-    bool done;
-  };
   auto walk_block = [&](const Blk& B) {
     const FaceDesc& fd = A.faces[B.f];
     const int items = GG * B.T, sh = B.px0 & 3;
     int32_t* out = A.leaf_out + (HP ? fd.hp_off : fd.mp_off);
-    auto init = [&](Walk& w, int item) {
-      w.done = true;
-      w.oidx = -1;
-      w.wbase = 0;
-      w.nd = make_uint4(LEAF_BIT, 0, 0, 0);
-      if (item >= items) return;
+    const int ld2 = 2 * LW, chs2 = 2 * WH * LW;  // window row / channel-plane strides (bytes)
+    for (int item = tid; item < items; item += NW) {
       const int t = item / GG, pl = item - t * GG;
       const int xi = B.xi0 + pl % G, yi = B.yi0 + pl / G;
-      if (xi >= B.nx || yi >= B.ny) return;
-      w.wbase = (yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh;
-      w.oidx = (xi * B.ny + yi) * B.T + t;  // reference order: patch x-major, tree-minor
-      w.nd = root_rec[FFD_TRAV_SAMETREE ? 0 : t];
-      w.done = false;
-    };
-    // both children's records are requested before the split test is evaluated, so the node
-    // fetch overlaps the LDS rectangle reads (children are adjacent: one 32-byte pair)
-    uint32_t probe_acc = 0;  // FFD_TRAV_X* perturbation probes (timing only; never changes results)
-    auto advance = [&](Walk& w) {
-      const uint4 v = w.nd;
-#if FFD_TRAV_ONELOAD
-      const uint4 c0 = A.nodes[v.x], c1 = c0;
-#else
-      const uint4 c0 = A.nodes[v.x], c1 = A.nodes[v.x + 1];
-#endif
-      const unsigned char* base = reinterpret_cast<const unsigned char*>(win) + 2 * w.wbase;
-      const int p1 = rect_mean_walk(base, v.y, (v.w >> 10) & 511u, 2 * LW);
-      const int p2 = rect_mean_walk(base, v.z, v.w >> 19, 2 * LW);
-#if FFD_TRAV_XLDS
-      probe_acc += (uint32_t)rect_mean_walk(base + 2, v.y, (v.w >> 10) & 511u, 2 * LW);
-#endif
-#if FFD_TRAV_XMEM
-      probe_acc += A.nodes[v.x ^ 64u].y;
-#endif
-#if FFD_TRAV_XMEM2  // one more 16-B load from the same 64-B sector as the children
-      { const uint4 q = A.nodes[v.x ^ 2u]; probe_acc += q.x ^ q.y ^ q.z ^ q.w; }
-#endif
-#if FFD_TRAV_XVALU
-#pragma unroll
-      for (int i = 0; i < 16; i++) probe_acc = probe_acc * 0x9E3779B1u + (uint32_t)p1;
-#endif
-      w.nd = (p1 - p2) <= ((int)(v.w << 22) >> 22) ? c0 : c1;  // 10-bit signed threshold
-    };
-#if FFD_TRAV_K > 1
-    // K walks per lane advanced in one basic block (no per-walk branches, so their LDS reads, ALU
-    // chains and node fetches interleave); each walk fetches only the child it takes.  A finished
-    // walk keeps its leaf and re-reads a parked record (nodes[0]: L1-resident).
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    const v4u* nodes = reinterpret_cast<const v4u*>(A.nodes);
-    for (int i0 = tid; i0 < items; i0 += FFD_TRAV_K * NW) {
-      v4u nd[FFD_TRAV_K];
-      int wb[FFD_TRAV_K], oi[FFD_TRAV_K];
-#pragma unroll
-      for (int j = 0; j < FFD_TRAV_K; j++) {
-        Walk P;
-        init(P, i0 + j * NW);
-        nd[j] = v4u{P.nd.x, P.nd.y, P.nd.z, P.nd.w};
-        wb[j] = 2 * P.wbase;
-        oi[j] = P.oidx;
+      if (xi >= B.nx || yi >= B.ny) continue;
+      // byte address of the patch's top-left integral corner in channel 0's window plane
+      const unsigned char* base = reinterpret_cast<const unsigned char*>(win) +
+                                  2 * ((yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh);
+      uint32_t P = root_idx[t], s = 0;
+      uint4 R = root_rec[t];
+      uint32_t lo = R.x, hi = R.z & 0xFFFFFFu;
+      while (((lo >> 20) & 63u) != 63u) {
+        // children pair of the current node: right after its pair (child 0), or off1 away (child 1)
+        const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
+        uint32_t Q = P + (s ? off1 : 1u);
+        if (s && off1 == 0u) Q = P + A.far[P];
+        const uint4 N = A.pairs[Q];
+        const unsigned char* cb = base + __umul24((lo >> 20) & 63u, (unsigned)chs2);
+        const int p1 = rect_mean_lds(cb + 2 * (int)__umul24((lo >> 5) & 31u, (unsigned)LW) + 2 * (int)(lo & 31u),
+                                     (hi & 31u) + 1u, ((hi >> 5) & 31u) + 1u, ld2);
+        const int p2 = rect_mean_lds(cb + 2 * (int)__umul24((lo >> 15) & 31u, (unsigned)LW) + 2 * (int)((lo >> 10) & 31u),
+                                     ((hi >> 10) & 31u) + 1u, ((hi >> 15) & 31u) + 1u, ld2);
+        const int thr = (int)(((lo >> 26) | (hi >> 20) << 6) << 22) >> 22;  // 10-bit two's complement
+        s = (p1 - p2) <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
+        P = Q;
+        R = N;
+        lo = s ? R.y : R.x;
+        hi = (s ? R.w : R.z) & 0xFFFFFFu;
       }
-      for (;;) {
-        bool any = false;
-#pragma unroll
-        for (int j = 0; j < FFD_TRAV_K; j++) any = any || !(nd[j].x & LEAF_BIT);
-        if (!any) break;
-        uint32_t nxt[FFD_TRAV_K];
-#pragma unroll
-        for (int j = 0; j < FFD_TRAV_K; j++) {
-          const v4u v = nd[j];
-          const bool act = !(v.x & LEAF_BIT);
-          const unsigned char* base = reinterpret_cast<const unsigned char*>(win) + wb[j];
-          const int p1 = rect_mean_walk(base, act ? v.y : 0u, act ? (v.w >> 10) & 511u : 1u, 2 * LW);
-          const int p2 = rect_mean_walk(base, act ? v.z : 0u, act ? v.w >> 19 : 1u, 2 * LW);
-          nxt[j] = act ? v.x + ((p1 - p2) <= ((int)(v.w << 22) >> 22) ? 0u : 1u) : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < FFD_TRAV_K; j++) {
-          const v4u c = nodes[nxt[j]];
-          nd[j] = (nd[j].x & LEAF_BIT) ? nd[j] : c;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < FFD_TRAV_K; j++)
-        if (oi[j] >= 0) out[oi[j]] = (int32_t)(nd[j].x & ~LEAF_BIT);
+      out[(xi * B.ny + yi) * B.T + t] = (int32_t)((lo & 0xFFFFFu) | hi << 20);  // reference order
     }
-#else
-    for (int i0 = tid; i0 < items; i0 += NW) {
-      Walk P;
-      init(P, i0);
-      while (!P.done && !(P.nd.x & LEAF_BIT)) advance(P);
-      if (P.oidx >= 0) out[P.oidx] = (int32_t)(P.nd.x & ~LEAF_BIT) + (probe_acc == 0x7FFFFFFFu ? 1 : 0);
-    }
-#endif
   };
 
   // Stager waves and walker waves run separate loops with the same barrier sequence per block
@@ -848,7 +758,8 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     // same plane stride, TravArgs::plane), so a block costs one load per chunk.
     chunk_t st[U];
     int voff[U];
-    uint4 root_nd = make_uint4(LEAF_BIT, 0u, 0u, 0u);
+    uint4 root_nd = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t root_p = 0;
     auto stage_offsets = [&](int plane_b) {
       const int s = tid - NW;
       const int dq = NS % nq, dr = (NS / nq) % WH, dc = NS / (nq * WH);
@@ -877,17 +788,15 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
           (void*)(((uint64_t)bhi << 32) | blo), (short)0, nbytes, BUF_WORD3);
       const int base_b = __builtin_amdgcn_readfirstlane((B.py0 * PITCH + (B.px0 & ~3)) * 2);
       // (reads past the face's planes return 0; chunks past the window are loaded but never committed)
-      // the block's root records (tree t of the block: lane t of the first staging wave)
+      // the block's root pair records (tree t of the block: lane t of the first staging wave)
       const int j = tid - NW;
       if (j < B.T) {
         const int tree = HP ? j : A.hp_state[B.f].trees[j];
-        root_nd = A.nodes[A.roots[tree]];
+        root_p = (uint32_t)A.roots[tree];
+        root_nd = A.pairs[root_p];
       }
 #pragma unroll
       for (int u = 0; u < U; u++) {
-#if FFD_TRAV_SLEEP
-        if (u % FFD_TRAV_SLEEP_GROUP == 0 && u > 0) __builtin_amdgcn_s_sleep(FFD_TRAV_SLEEP);
-#endif
         if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff[u], base_b, 0);
         else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff[u], base_b, 0);
       }
@@ -896,7 +805,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       if (!B.ok) return;
       chunk_t* dst = reinterpret_cast<chunk_t*>(win);
       const int s = tid - NW;
-      if (s < B.T) root_rec[s] = root_nd;
+      if (s < B.T) {
+        root_rec[s] = root_nd;
+        root_idx[s] = root_p;
+      }
 #pragma unroll
       for (int u = 0; u < U; u++)
         if (u * NS + s < total) dst[u * NS + s] = st[u];
@@ -1309,32 +1221,9 @@ void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t
   if (n > 0) k_integral<<<n, 256, 0, s>>>(faces, gray, chan);
 }
 
-bool encode_walk_nodes(const uint4* nodes, size_t n, int G, int step, int step_y, uint4* out) {
-  const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1), LW = trav_row_pitch(WW);
-  for (size_t i = 0; i < n; i++) {
-    const uint4 v = nodes[i];
-    if (v.x & LEAF_BIT) {
-      out[i] = make_uint4(v.x, 0u, 0u, 0u);
-      continue;
-    }
-    const uint32_t ch = v.y & 63u, w1 = (v.y >> 6) & 31u, h1 = (v.y >> 11) & 31u, w2 = (v.y >> 16) & 31u,
-                   h2 = (v.y >> 21) & 31u;
-    const uint32_t e1 = v.w & 0xFFFFu, e2 = v.w >> 16;
-    const uint32_t o1 = 2 * (ch * WH * LW + (e1 / PITCH) * LW + e1 % PITCH);
-    const uint32_t o2 = 2 * (ch * WH * LW + (e2 / PITCH) * LW + e2 % PITCH);
-    const int thr = (int)v.z;
-    if (o1 >= (1u << 18) || o2 >= (1u << 18) || h1 > 31 || h2 > 31 || w1 * h1 > 511 || w2 * h2 > 511 ||
-        thr < -512 || thr > 511)
-      return false;
-    out[i] = make_uint4(v.x, o1 | (2 * w1) << 18 | h1 << 24, o2 | (2 * w2) << 18 | h2 << 24,
-                        ((uint32_t)thr & 0x3FFu) | (w1 * h1) << 10 | (w2 * h2) << 19);
-  }
-  return true;
-}
-
 int traverse_lds_bytes(int G, int step, int step_y) {
   const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1);
-  return trav_window_bytes(WW, WH) + MAX_TREES * 16;  // window + the block's root records
+  return trav_window_bytes(WW, WH) + MAX_TREES * 20;  // window + the block's root pairs + their indices
 }
 
 bool traverse_window_fits(int G, int step, int step_y, int lds_cap) {
@@ -1344,12 +1233,12 @@ bool traverse_window_fits(int G, int step, int step_y, int lds_cap) {
          NCH * WH * (trav_row_pitch(WW) * 2 / cb) <= TRAV_NS * (cb == 16 ? TravStage<16>::U : TravStage<8>::U);
 }
 
-void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* nodes, const int32_t* roots,
-                     const HpState* state, int ntrees_hp, int step, int step_y, int64_t plane, const uint16_t* chan,
-                     int32_t* leaf_out, int n_wg, hipStream_t s) {
+void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* pairs, const int32_t* roots,
+                     const uint32_t* far, const HpState* state, int ntrees_hp, int step, int step_y, int64_t plane,
+                     const uint16_t* chan, int32_t* leaf_out, int n_wg, hipStream_t s) {
   const int total_blocks = n * bpf;
   if (total_blocks <= 0) return;
-  TravArgs A{faces, n, bpf, nodes, roots, state, ntrees_hp, step, step_y, (int)plane, chan, leaf_out};
+  TravArgs A{faces, n, bpf, pairs, roots, far, state, ntrees_hp, step, step_y, (int)plane, chan, leaf_out};
   const int lds = traverse_lds_bytes(G, step, step_y);
   const int grid = std::max(8, n_wg & ~7);
 #define FFD_TRAV(HPV, GV)                                                                              \

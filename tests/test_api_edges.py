@@ -7,7 +7,7 @@
   face (125 x 375); and the per-face statuses of the boxes it rejects;
 * the multi-device entry points on the one device a box has (ffd_group_*, ffd_engine_join +
   ffd_gather_faces through RCCL);
-* the engine's non-default layouts (FFD_NODE_LAYOUT=bfs, FFD_CHANNEL_STREAMS=2), read at
+* the engine's non-default configurations (3 x 3 patch blocks, FFD_CHANNEL_STREAMS=2, two streams), read at
   ffd_engine_create."""
 import os
 
@@ -99,7 +99,7 @@ def test_rccl_join_and_gather_single_rank(engine):
     assert torch.equal(local, root)
 
 
-@pytest.mark.parametrize("env", [{"FFD_NODE_LAYOUT": "bfs"}, {"FFD_CHANNEL_STREAMS": "2"},
+@pytest.mark.parametrize("env", [{"FFD_TRAV_G_FFD": "3", "FFD_TRAV_G_HP": "3"}, {"FFD_CHANNEL_STREAMS": "2"},
                                  {"FFD_STREAMS": "2", "FFD_CHUNK": "5"}])
 def test_engine_variants_bit_exact(model_path, oracle_mod, env):
     old = {k: os.environ.get(k) for k in env}
