@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "../../include/ffd_numerics.h"
 #include "ffd_device.hpp"
@@ -795,11 +796,13 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         root_p = (uint32_t)A.roots[tree];
         root_nd = A.pairs[root_p];
       }
+#if FFD_TRAV_PROBE != 2
 #pragma unroll
       for (int u = 0; u < U; u++) {
         if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff[u], base_b, 0);
         else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff[u], base_b, 0);
       }
+#endif
     };
     auto commit = [&](const Blk& B) {
       if (!B.ok) return;
@@ -809,28 +812,24 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         root_rec[s] = root_nd;
         root_idx[s] = root_p;
       }
+#if FFD_TRAV_PROBE != 2  // the walk-only probe keeps the root pairs (walks need valid records)
 #pragma unroll
       for (int u = 0; u < U; u++)
         if (u * NS + s < total) dst[u * NS + s] = st[u];
+#endif
     };
 
     stage_offsets(A.plane * 2);
     Blk cur = block(lb);
-#if FFD_TRAV_PROBE != 2
     prefetch(cur);
-#endif
     for (; lb < end; lb += nk) {
       __syncthreads();  // the previous block's walks are done with the window
-#if FFD_TRAV_PROBE != 2
       commit(cur);
-#endif
       __syncthreads();  // the window holds block lb
       Blk nxt;
       nxt.ok = false;
       if (lb + nk < end) nxt = block(lb + nk);
-#if FFD_TRAV_PROBE != 2
       prefetch(nxt);
-#endif
       cur = nxt;
     }
   } else {
@@ -1193,6 +1192,129 @@ __global__ __launch_bounds__(MS_THREADS) void k_meanshift(const FaceDesc* __rest
   }
 }
 
+// MeanShift, chain-parallel form (default; FFD_MS_KERNEL=1 selects k_meanshift above).  A "chain"
+// is one (face, landmark) vote list; a 256-thread workgroup runs 64 chains (64 faces, one landmark)
+// through MeanShift::shift (MeanShift.hpp:41-135) in tiles of MS2_T votes per chain:
+//   terms   all 256 threads compute the per-vote terms (x*w, y*w, w) of the next tile (the votes
+//           were loaded into registers one tile ahead), into a double-buffered LDS tile;
+//   sums    lane c of wave 0 adds chain c's MS2_T terms in list order (one ds_read_b128 each),
+// so every running sum is the reference's sequential float sum bit for bit, every lane of wave 0
+// carries a chain during the serial part, and one barrier per tile orders the two buffers.
+constexpr int MS2_CH = 64, MS2_T = 32, MS2_THREADS = 256, MS2_U = MS2_CH * MS2_T / MS2_THREADS;
+
+__global__ __launch_bounds__(MS2_THREADS) void k_meanshift2(const FaceDesc* __restrict__ faces, int n_faces,
+                                                            int tslots, int n_parts, float lamda, int max_iter,
+                                                            float stop, const Vote* __restrict__ votes,
+                                                            const int32_t* __restrict__ vote_counts,
+                                                            float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
+  __shared__ float4 term[2][MS2_T][MS2_CH];  // [buffer][vote j][chain c] = (x*w, y*w, w, 0)
+  __shared__ float s_mx[MS2_CH], s_my[MS2_CH];
+  __shared__ int s_cnt[MS2_CH], s_live[MS2_CH];
+  __shared__ int64_t s_vb[MS2_CH];
+  __shared__ int s_maxcnt;
+  const int part = blockIdx.y, f0 = blockIdx.x * MS2_CH, tid = threadIdx.x;
+  if (tid < MS2_CH) {
+    const int f = f0 + tid;
+    int cnt = 0, live = 0;
+    int64_t vb = 0;
+    if (f < n_faces && faces[f].valid) {
+      const FaceDesc& fd = faces[f];
+      cnt = part < n_parts ? vote_counts[(int64_t)f * NPARTS + part] : 0;
+      vb = fd.vote_off + (int64_t)part * tslots * fd.nmx * fd.nmy;
+      live = 1;
+    }
+    s_cnt[tid] = cnt;
+    s_vb[tid] = vb;
+    s_live[tid] = live;
+    s_mx[tid] = 0.f;
+    s_my[tid] = 0.f;
+  }
+  // this thread's items: chain c = (tid >> 5) + 8u, vote j = tid & 31 of each tile
+  const int j = tid & (MS2_T - 1), cb = tid >> 5;
+  float ax = 0, ay = 0, aw = 0;  // lane c < 64 of wave 0: chain c's running sums
+  for (int pass = -1; pass < max_iter; pass++) {
+    if (tid == 0) s_maxcnt = 0;
+    __syncthreads();  // s_mx / s_my / s_live of the previous pass are final
+    if (tid < MS2_CH && s_live[tid]) atomicMax(&s_maxcnt, s_cnt[tid]);
+    __syncthreads();
+    const int maxcnt = s_maxcnt;
+    if (pass >= 0 && maxcnt == 0) {  // no live chain with votes left: every chain has converged
+      bool any = false;
+      for (int c = 0; c < MS2_CH; c++) any |= s_live[c] != 0;
+      if (!any) break;
+    }
+    ax = ay = aw = 0;
+    Vote v[MS2_U];
+    auto load_tile = [&](int k0) {
+#pragma unroll
+      for (int u = 0; u < MS2_U; u++) {
+        const int c = cb + 8 * u, k = k0 + j;
+        v[u] = (s_live[c] && k < s_cnt[c]) ? votes[s_vb[c] + k] : Vote{0, 0, -1.f};
+      }
+    };
+    load_tile(0);
+    int buf = 0;
+    for (int k0 = 0; k0 < maxcnt; k0 += MS2_T, buf ^= 1) {
+#pragma unroll
+      for (int u = 0; u < MS2_U; u++) {
+        const int c = cb + 8 * u;
+        float px = 0.f, py = 0.f, w = 0.f;
+        if (v[u].w >= 0.f) {  // real weights are fg > 0.5
+          if (pass < 0) {
+            w = v[u].w;
+          } else {
+            const float dx = s_mx[c] - (float)v[u].x, dy = s_my[c] - (float)v[u].y;
+            float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
+            d = ffd_expf(-d / lamda);
+            w = v[u].w * d;
+          }
+          px = v[u].x * w;
+          py = v[u].y * w;
+        }
+        term[buf][j][c] = make_float4(px, py, w, 0.f);
+      }
+      if (k0 + MS2_T < maxcnt) load_tile(k0 + MS2_T);  // in flight during the serial part
+      __syncthreads();  // tile k0's terms are in term[buf]; term[buf ^ 1] was consumed last tile
+      if (tid < MS2_CH && s_live[tid]) {
+        const int lim = min(MS2_T, s_cnt[tid] - k0);
+        for (int q = 0; q < lim; q++) {
+          const float4 t = term[buf][q][tid];
+          ax += t.x;
+          ay += t.y;
+          aw += t.z;
+        }
+      }
+    }
+    __syncthreads();  // every chain's sums are complete before the means change
+    if (tid < MS2_CH && s_live[tid]) {
+      if (aw > 0) { ax /= aw; ay /= aw; }
+      if (pass < 0) {
+        s_mx[tid] = ax;
+        s_my[tid] = ay;
+      } else {
+        const float ddx = ax - s_mx[tid], ddy = ay - s_my[tid];
+        if (__builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) s_live[tid] = 0;  // converged
+        s_mx[tid] = ax;
+        s_my[tid] = ay;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < MS2_CH) {
+    const int f = f0 + tid;
+    if (f < n_faces && faces[f].valid) {
+      const float mx = s_mx[tid], my = s_my[tid];
+      if (part < n_parts) {
+        ms_mean[((int64_t)f * NPARTS + part) * 2] = mx;
+        ms_mean[((int64_t)f * NPARTS + part) * 2 + 1] = my;
+      }
+      const float inv = 1.0f / faces[f].scale;  // FaceForest.cpp:255-257
+      out[f].points[part][0] = part < n_parts ? cv_round((float)cv_round(mx) * inv) : 0;
+      out[f].points[part][1] = part < n_parts ? cv_round((float)cv_round(my) * inv) : 0;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ launch --
 void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s) {
   k_gray_resize<<<n, 256, 0, s>>>(faces, images, gray);
@@ -1306,9 +1428,19 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
                       int max_iter, float stop, const Vote* votes, const int32_t* vote_counts, float* ms_mean,
                       FaceOut* out, hipStream_t s) {
   (void)state;
-  dim3 grid((n + MS_FACES - 1) / MS_FACES, NPARTS);
-  k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, max_iter, stop, votes, vote_counts, ms_mean,
-                                   out);
+  static const int which = [] {
+    const char* v = std::getenv("FFD_MS_KERNEL");
+    return v ? std::atoi(v) : 2;
+  }();
+  if (which == 1) {
+    dim3 grid((n + MS_FACES - 1) / MS_FACES, NPARTS);
+    k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, max_iter, stop, votes, vote_counts,
+                                            ms_mean, out);
+  } else {
+    dim3 grid((n + MS2_CH - 1) / MS2_CH, NPARTS);
+    k_meanshift2<<<grid, MS2_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, max_iter, stop, votes, vote_counts,
+                                              ms_mean, out);
+  }
 }
 
 }  // namespace ffd
