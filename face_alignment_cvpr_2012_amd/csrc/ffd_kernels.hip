@@ -642,7 +642,12 @@ template <> struct TravStage<8> { static constexpr int U = (20480 + TRAV_NS - 1)
 template <> struct TravStage<16> { static constexpr int U = (11000 + TRAV_NS - 1) / TRAV_NS; typedef uint32_t T __attribute__((ext_vector_type(4))); };
 
 // LDS row pitch (u16) of a traversal window WW columns wide staged from a 4-element aligned column.
-__host__ __device__ __forceinline__ int trav_row_pitch(int WW) { return (WW + 3 + 3) & ~3; }
+#ifndef FFD_TRAV_PITCH8
+#define FFD_TRAV_PITCH8 0  // 1: window pitch a multiple of 8 columns (16-byte staging chunks)
+#endif
+__host__ __device__ __forceinline__ int trav_row_pitch(int WW) {
+  return FFD_TRAV_PITCH8 ? (WW + 3 + 7) & ~7 : (WW + 3 + 3) & ~3;
+}
 __host__ __device__ __forceinline__ int trav_chunk_bytes(int WW) { return trav_row_pitch(WW) % 8 == 0 ? 16 : 8; }
 
 // Window bytes (16-byte aligned); the block's root pair records (uint4 [MAX_TREES]) and their
