@@ -539,7 +539,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
           minmax_update(mn[o], mx[o], m4[k], x0 + k < FW);
         }
         // columns >= W land in the row's pitch padding, never read
-#if FFD_GABOR_PROBE != 1
+#if FFD_GABOR_PROBE != 1 && FFD_GABOR_PROBE != 4  // 4: epilogue reads whatever the buffer holds
         *reinterpret_cast<float4*>(&mag[fd.mag_off + ((int64_t)(NU * 7 + o) * FH + y) * PITCH + x0]) =
             make_float4(m4[0], m4[1], m4[2], m4[3]);
 #endif
