@@ -244,25 +244,45 @@ __device__ __forceinline__ void gabor_normalise_integrate(const FaceDesc& fd, in
                                                           uint16_t* __restrict__ chan) {
   __shared__ float s_sf[7], s_hf[7];
   gabor_minmax_scale<NWV>(mn, mx, s_sf, s_hf);
-  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int x0 = 2 * lane, FW = fd.W, FH = fd.H;
+  // Software-pipelined read-back: the magnitudes of rows [y0 + RB, y0 + 2RB) are in flight while rows
+  // [y0, y0 + RB) are quantised and scanned (two register buffers), so the L2 / Infinity-Cache
+  // latency of the read-back is paid once per plane instead of once per batch.
+  constexpr int RB = 16;
+  typedef float2 rowbuf[RB];
   for (int o = wv; o < 7; o += NWV) {
-    const int lane = ln, x0 = 2 * lane, FW = fd.W, FH = fd.H;
     const float sf = s_sf[o], hf = s_hf[o];
-    const float* m = mag + fd.mag_off + (int64_t)(nu * 7 + o) * FH * PITCH;
-    constexpr int RB = 16;
-    integral_scan<RB>(chan + fd.ch_off + (int64_t)(1 + nu * 7 + o) * fd.plane, FW, FH, lane,
-                  [&](int y0, uint32_t* v0, uint32_t* v1) {
-                    float2 mv[RB];
+    const float* m = mag + fd.mag_off + (int64_t)(nu * 7 + o) * FH * PITCH + x0;
+    uint16_t* out = chan + fd.ch_off + (int64_t)(1 + nu * 7 + o) * fd.plane;
+    for (int x = lane; x <= FW; x += 64) out[x] = 0;  // row 0 of the integral image
+    uint32_t c0 = 0, c1 = 0;
+    auto load = [&](int y0, rowbuf& mv) {
 #pragma unroll
-                    for (int b = 0; b < RB; b++)
-                      mv[b] = (y0 + b < FH) ? *reinterpret_cast<const float2*>(&m[(y0 + b) * PITCH + x0])
-                                            : make_float2(0.f, 0.f);
+      for (int b = 0; b < RB; b++)
+        mv[b] = (y0 + b < FH) ? *reinterpret_cast<const float2*>(&m[(y0 + b) * PITCH]) : make_float2(0.f, 0.f);
+    };
+    auto scan = [&](int y0, const rowbuf& mv) {
 #pragma unroll
-                    for (int b = 0; b < RB; b++) {
-                      v0[b] = (x0 < FW) ? gabor_quantise(mv[b].x, sf, hf) : 0u;
-                      v1[b] = (x0 + 1 < FW) ? gabor_quantise(mv[b].y, sf, hf) : 0u;
-                    }
-                  });
+      for (int b = 0; b < RB; b++) {
+        if (y0 + b >= FH) break;
+        c0 += (x0 < FW) ? gabor_quantise(mv[b].x, sf, hf) : 0u;
+        c1 += (x0 + 1 < FW) ? gabor_quantise(mv[b].y, sf, hf) : 0u;
+        const uint32_t s2 = c0 + c1;
+        const uint32_t excl = wave_incl_scan(s2) - s2;
+        // entries >= W+1 land in the row's pitch padding (never read by a patch)
+        reinterpret_cast<uint32_t*>(out + (int64_t)(y0 + b + 1) * PITCH)[lane] = (excl & 0xFFFFu) | ((excl + c0) << 16);
+      }
+    };
+    rowbuf A, B;
+    load(0, A);
+    for (int y0 = 0; y0 < FH; y0 += 2 * RB) {
+      if (y0 + RB < FH) load(y0 + RB, B);
+      scan(y0, A);
+      if (y0 + RB >= FH) break;
+      if (y0 + 2 * RB < FH) load(y0 + 2 * RB, A);
+      scan(y0 + RB, B);
+    }
   }
 }
 
@@ -1205,7 +1225,10 @@ __global__ __launch_bounds__(MS_THREADS) void k_meanshift(const FaceDesc* __rest
 //   sums    lane c of wave 0 adds chain c's MS2_T terms in list order (one ds_read_b128 each),
 // so every running sum is the reference's sequential float sum bit for bit, every lane of wave 0
 // carries a chain during the serial part, and one barrier per tile orders the two buffers.
-constexpr int MS2_CH = 64, MS2_T = 32, MS2_THREADS = 256, MS2_U = MS2_CH * MS2_T / MS2_THREADS;
+#ifndef FFD_MS2_CH
+#define FFD_MS2_CH 32
+#endif
+constexpr int MS2_CH = FFD_MS2_CH, MS2_T = 32, MS2_THREADS = 256, MS2_U = MS2_CH * MS2_T / MS2_THREADS;
 
 __global__ __launch_bounds__(MS2_THREADS) void k_meanshift2(const FaceDesc* __restrict__ faces, int n_faces,
                                                             int tslots, int n_parts, float lamda, int max_iter,
@@ -1234,8 +1257,9 @@ __global__ __launch_bounds__(MS2_THREADS) void k_meanshift2(const FaceDesc* __re
     s_mx[tid] = 0.f;
     s_my[tid] = 0.f;
   }
-  // this thread's items: chain c = (tid >> 5) + 8u, vote j = tid & 31 of each tile
-  const int j = tid & (MS2_T - 1), cb = tid >> 5;
+  // this thread's items: vote j = tid % T of chains c = tid / T + u * (256 / T) of each tile
+  constexpr int CSTEP = MS2_THREADS / MS2_T;
+  const int j = tid % MS2_T, cb = tid / MS2_T;
   float ax = 0, ay = 0, aw = 0;  // lane c < 64 of wave 0: chain c's running sums
   for (int pass = -1; pass < max_iter; pass++) {
     if (tid == 0) s_maxcnt = 0;
@@ -1253,7 +1277,7 @@ __global__ __launch_bounds__(MS2_THREADS) void k_meanshift2(const FaceDesc* __re
     auto load_tile = [&](int k0) {
 #pragma unroll
       for (int u = 0; u < MS2_U; u++) {
-        const int c = cb + 8 * u, k = k0 + j;
+        const int c = cb + CSTEP * u, k = k0 + j;
         v[u] = (s_live[c] && k < s_cnt[c]) ? votes[s_vb[c] + k] : Vote{0, 0, -1.f};
       }
     };
@@ -1262,7 +1286,7 @@ __global__ __launch_bounds__(MS2_THREADS) void k_meanshift2(const FaceDesc* __re
     for (int k0 = 0; k0 < maxcnt; k0 += MS2_T, buf ^= 1) {
 #pragma unroll
       for (int u = 0; u < MS2_U; u++) {
-        const int c = cb + 8 * u;
+        const int c = cb + CSTEP * u;
         float px = 0.f, py = 0.f, w = 0.f;
         if (v[u].w >= 0.f) {  // real weights are fg > 0.5
           if (pass < 0) {
@@ -1276,14 +1300,26 @@ __global__ __launch_bounds__(MS2_THREADS) void k_meanshift2(const FaceDesc* __re
           px = v[u].x * w;
           py = v[u].y * w;
         }
-        term[buf][j][c] = make_float4(px, py, w, 0.f);
+        term[buf][j][(c + j) & (MS2_CH - 1)] = make_float4(px, py, w, 0.f);  // skewed: conflict-free
       }
       if (k0 + MS2_T < maxcnt) load_tile(k0 + MS2_T);  // in flight during the serial part
       __syncthreads();  // tile k0's terms are in term[buf]; term[buf ^ 1] was consumed last tile
       if (tid < MS2_CH && s_live[tid]) {
         const int lim = min(MS2_T, s_cnt[tid] - k0);
-        for (int q = 0; q < lim; q++) {
-          const float4 t = term[buf][q][tid];
+        int q = 0;
+        for (; q + 8 <= lim; q += 8) {  // LDS reads 8 ahead of their in-order adds
+          float4 t[8];
+#pragma unroll
+          for (int e = 0; e < 8; e++) t[e] = term[buf][q + e][(tid + q + e) & (MS2_CH - 1)];
+#pragma unroll
+          for (int e = 0; e < 8; e++) {
+            ax += t[e].x;
+            ay += t[e].y;
+            aw += t[e].z;
+          }
+        }
+        for (; q < lim; q++) {
+          const float4 t = term[buf][q][(tid + q) & (MS2_CH - 1)];
           ax += t.x;
           ay += t.y;
           aw += t.z;
