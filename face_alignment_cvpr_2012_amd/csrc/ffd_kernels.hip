@@ -1217,7 +1217,8 @@ __global__ __launch_bounds__(MS_THREADS) void k_meanshift(const FaceDesc* __rest
   }
 }
 
-// MeanShift, chain-parallel form (default; FFD_MS_KERNEL=1 selects k_meanshift above).  A "chain"
+// MeanShift, chain-parallel form (FFD_MS_KERNEL=2; measured 3.3 ms vs 3.0 ms for k_meanshift at C2,
+// profiles/r2 notes, so k_meanshift stays the default).  A "chain"
 // is one (face, landmark) vote list; a 256-thread workgroup runs 64 chains (64 faces, one landmark)
 // through MeanShift::shift (MeanShift.hpp:41-135) in tiles of MS2_T votes per chain:
 //   terms   all 256 threads compute the per-vote terms (x*w, y*w, w) of the next tile (the votes
@@ -1471,7 +1472,7 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
   (void)state;
   static const int which = [] {
     const char* v = std::getenv("FFD_MS_KERNEL");
-    return v ? std::atoi(v) : 2;
+    return v ? std::atoi(v) : 1;
   }();
   if (which == 1) {
     dim3 grid((n + MS_FACES - 1) / MS_FACES, NPARTS);
