@@ -133,3 +133,29 @@ def test_c4_deep_synthetic_forest_bit_exact(tmp_path, fixtures):
         oracle.set_steps(4, 3, 3)
         from conftest import MODEL
         oracle.load_model(MODEL)
+
+
+@pytest.mark.gpu
+def test_c4_depth20_forest_bit_exact(tmp_path, fixtures):
+    """C4 as BASELINE.json states it: 20 complete trees of depth 20 (42 M nodes, 21 M leaves) for
+    every pose bin, at 4x patch density: leaf ordinals and landmarks against the oracle on one face.
+    The depth-20 trees also exercise the traversal's far child offsets (subtrees > 65535 pairs)."""
+    import face_alignment_cvpr_2012_amd as ffd
+    import oracle
+    path = _synth_forest(tmp_path, 20)
+    opts = ffd.FaceForestOptions(model_path=path, mp_option=ffd.MultiPartEstimatorOption(step_size=2, step_size_y=1))
+    img, b = fixtures["images"][4], tuple(int(v) for v in fixtures["boxes"][4])
+    with ffd.FaceForest(opts) as ff:
+        face = ff.analyzeFace(img, b)
+        tr = ff.trace(0, b[2], b[3])
+    oracle.load_model(path)
+    oracle.set_steps(4, 2, 1)
+    try:
+        ref, rt = oracle.analyze_face(img, b, threads=16, trace=True)
+        assert face.n_trees == 20 and tr["mp_leaves"].shape == rt["mp_leaves"].shape
+        np.testing.assert_array_equal(tr["mp_leaves"], rt["mp_leaves"])
+        assert np.array_equal(face.ffd_cordinates, ref["points"])
+    finally:
+        oracle.set_steps(4, 3, 3)
+        from conftest import MODEL
+        oracle.load_model(MODEL)
