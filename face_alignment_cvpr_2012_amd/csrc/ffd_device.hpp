@@ -45,6 +45,11 @@ constexpr uint32_t LEAF_BIT = 0x80000000u;
 // offset is far[pair]).  Each tree starts with a root pair (root, unused leaf).
 // Source fields: ThresholdSplit<SimplePatchFeature> (ThresholdSplit.hpp:51-67, ImageSample.hpp:83-90).
 
+// Tree tops (k_traverse): per tree, TOP_CAP pair records of its top levels in heap order: entry 0
+// = the root pair, entry 1 = the root's children pair, entry 2h + s (h >= 1) = the children pair of
+// node s of entry h; entries under leaves are zero (never read).  Plus each entry's pair index.
+constexpr int TOP_CAP = 64;  // levels 0..6
+
 struct FaceDesc {
   int64_t img_off;        // byte offset of the source image
   int32_t img_w, img_h, img_stride;

@@ -223,6 +223,36 @@ void ffd_host::build_pair_records(const std::vector<uint4>& bfs, const std::vect
   if (out.size() >= 0x80000000ull) throw std::runtime_error("pair array too large");
 }
 
+void ffd_host::build_tree_tops(const std::vector<uint4>& pairs, const std::vector<int32_t>& proots,
+                               const std::vector<uint32_t>& far, std::vector<uint4>& tops,
+                               std::vector<uint32_t>& top_idx) {
+  tops.assign(proots.size() * TOP_CAP, make_uint4(0, 0, 0, 0));
+  top_idx.assign(proots.size() * TOP_CAP, 0u);
+  auto leaf = [](uint32_t lo) { return ((lo >> 20) & 63u) == 63u; };
+  for (size_t t = 0; t < proots.size(); t++) {
+    uint4* rec = &tops[t * TOP_CAP];
+    uint32_t* idx = &top_idx[t * TOP_CAP];
+    idx[0] = (uint32_t)proots[t];
+    rec[0] = pairs[idx[0]];
+    std::vector<bool> live(TOP_CAP, false);
+    live[0] = true;
+    for (int h = 0; h < TOP_CAP; h++) {
+      if (!live[h]) continue;
+      const uint4 R = rec[h];
+      for (uint32_t s = 0; s < (h ? 2u : 1u); s++) {  // the root pair's second slot is an unused leaf
+        if (leaf(s ? R.y : R.x)) continue;
+        const int h2 = h ? 2 * h + (int)s : 1;
+        if (h2 >= TOP_CAP) continue;
+        const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
+        const uint32_t q = idx[h] + (s ? (off1 ? off1 : far[idx[h]]) : 1u);
+        rec[h2] = pairs[q];
+        idx[h2] = q;
+        live[h2] = true;
+      }
+    }
+  }
+}
+
 void ffd_engine::load_model(const std::string& path) {
   ModelFile m;
   m.load(path);
@@ -480,9 +510,9 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   }
   stage(7, st, [&] {
     launch_traverse(true, dfd, n, blocks_per_face(fds, true, trav_g_hp), trav_g_hp, hp_pairs.as<uint4>(),
-                    hp_proots.as<int32_t>(), hp_far.as<uint32_t>(), nullptr, hp_trees, desc.hp_option.step_size, desc.hp_option.step_size,
-                    plane, w.chan.as<uint16_t>(),
-                    w.hpleaf.as<int32_t>(), trav_wg, st);
+                    hp_tops.as<uint4>(), hp_topi.as<uint32_t>(), trav_top_max, hp_far.as<uint32_t>(), nullptr,
+                    hp_trees, desc.hp_option.step_size, desc.hp_option.step_size, plane, w.chan.as<uint16_t>(),
+                    w.hpleaf.as<int32_t>(), trav_wg, TRAV_LDS_CAP, st);
   });
   stage(8, st, [&] {
     launch_hp_pose(dfd, n, w.hpleaf.as<int32_t>(), hp_m.as<float>(), hp_trees, n_forests, ntrees_per_forest,
@@ -490,8 +520,9 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   });
   stage(9, st, [&] {
     launch_traverse(false, dfd, n, blocks_per_face(fds, false, trav_g_mp), trav_g_mp, mp_pairs.as<uint4>(),
-                    mp_proots.as<int32_t>(), mp_far.as<uint32_t>(), w.state.as<HpState>(), 0, desc.mp_option.step_size, mp_step_y(),
-                    plane, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), trav_wg, st);
+                    mp_tops.as<uint4>(), mp_topi.as<uint32_t>(), trav_top_max, mp_far.as<uint32_t>(),
+                    w.state.as<HpState>(), 0, desc.mp_option.step_size, mp_step_y(), plane, w.chan.as<uint16_t>(),
+                    w.mpleaf.as<int32_t>(), trav_wg, TRAV_LDS_CAP, st);
   });
   const int n_parts = std::min(desc.mp_option.num_parts, NPARTS);
   stage(10, st, [&] {
@@ -683,6 +714,7 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   if (const char* v = std::getenv("FFD_TRAV_G_HP")) e->trav_g_hp = std::max(3, std::min(5, std::atoi(v)));
   if (const char* v = std::getenv("FFD_TRAV_G_FFD")) e->trav_g_mp = std::max(3, std::min(5, std::atoi(v)));
   if (const char* v = std::getenv("FFD_TRAV_WG")) e->trav_wg = std::max(8, std::atoi(v));
+  if (const char* v = std::getenv("FFD_TRAV_TOPMAX")) e->trav_top_max = std::max(1, std::min(TOP_CAP, std::atoi(v)));
   if (const char* v = std::getenv("FFD_CHANNEL_STREAMS")) e->channel_streams = std::max(1, std::min(4, std::atoi(v)));
   if (const char* v = std::getenv("FFD_CHUNK")) e->max_chunk = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("FFD_STREAMS")) e->n_streams = std::max(1, std::min(8, std::atoi(v)));
@@ -984,9 +1016,9 @@ ffd_status ffd_estimate_headpose(ffd_engine* e, const uint32_t* channels, int32_
     std::vector<FaceDesc> fv{f};
     e->out.ensure(sizeof(FaceOut));
     launch_traverse(true, dfd, 1, blocks_per_face(fv, true, e->trav_g_hp), e->trav_g_hp, e->hp_pairs.as<uint4>(),
-                    e->hp_proots.as<int32_t>(), e->hp_far.as<uint32_t>(), nullptr, e->hp_trees, e->desc.hp_option.step_size,
-                    e->desc.hp_option.step_size, f.plane, w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), e->trav_wg,
-                    w.stream);
+                    e->hp_tops.as<uint4>(), e->hp_topi.as<uint32_t>(), e->trav_top_max, e->hp_far.as<uint32_t>(),
+                    nullptr, e->hp_trees, e->desc.hp_option.step_size, e->desc.hp_option.step_size, f.plane,
+                    w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), e->trav_wg, TRAV_LDS_CAP, w.stream);
     launch_hp_pose(dfd, 1, w.hpleaf.as<int32_t>(), e->hp_m.as<float>(), e->hp_trees, e->n_forests,
                    e->ntrees_per_forest, w.state.as<HpState>(), e->out.as<FaceOut>(), w.stream);
     HIP_CHECK(hipGetLastError());
@@ -1024,8 +1056,9 @@ ffd_status ffd_estimate_facial_features(ffd_engine* e, const uint32_t* channels,
     e->out.ensure(sizeof(FaceOut));
     const int n_parts = std::min(e->desc.mp_option.num_parts, NPARTS);
     launch_traverse(false, dfd, 1, blocks_per_face(fv, false, e->trav_g_mp), e->trav_g_mp, e->mp_pairs.as<uint4>(),
-                    e->mp_proots.as<int32_t>(), e->mp_far.as<uint32_t>(), w.state.as<HpState>(), 0, e->desc.mp_option.step_size, e->mp_step_y(),
-                    f.plane, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), e->trav_wg, w.stream);
+                    e->mp_tops.as<uint4>(), e->mp_topi.as<uint32_t>(), e->trav_top_max, e->mp_far.as<uint32_t>(),
+                    w.state.as<HpState>(), 0, e->desc.mp_option.step_size, e->mp_step_y(), f.plane,
+                    w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), e->trav_wg, TRAV_LDS_CAP, w.stream);
     launch_votes(dfd, 1, w.mpleaf.as<int32_t>(), e->mp_rec.as<uint4>(), e->vote_rec_compact, e->vote_bias_x,
                  e->vote_bias_y, w.state.as<HpState>(), MAX_TREES, e->desc.mp_option.step_size, e->mp_step_y(),
                  e->patch / 2, n_parts, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), w.stream);

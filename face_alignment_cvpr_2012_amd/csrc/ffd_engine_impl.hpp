@@ -97,6 +97,9 @@ namespace ffd_host {
 // in depth-first order (ffd_device.hpp "pair records"); roots_out[t] = tree t's root pair.
 void build_pair_records(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots, std::vector<uint4>& out,
                         std::vector<int32_t>& roots_out, std::vector<uint32_t>& far);
+// Heap-ordered tree tops (ffd_device.hpp "tree tops") of every tree: TOP_CAP records + pair indices.
+void build_tree_tops(const std::vector<uint4>& pairs, const std::vector<int32_t>& proots,
+                     const std::vector<uint32_t>& far, std::vector<uint4>& tops, std::vector<uint32_t>& top_idx);
 }  // namespace ffd_host
 
 struct ffd_engine {
@@ -120,6 +123,8 @@ struct ffd_engine {
   DevBuf hp_pairs, mp_pairs;         // pair records for k_traverse (ffd_device.hpp "pair records")
   DevBuf hp_proots, mp_proots;       // per tree: index of its root pair
   DevBuf hp_far, mp_far;             // per pair: far offset of child 1's children (when > 65535)
+  DevBuf hp_tops, mp_tops, hp_topi, mp_topi;  // per tree: heap-ordered top pair records + their indices
+  int trav_top_max = TOP_CAP;        // tree-top entries staged per tree at most (FFD_TRAV_TOPMAX)
   std::vector<uint4> hp_nodes_h, mp_nodes_h;  // host copies until the walk nodes are built
   std::vector<int32_t> hp_roots_h, mp_roots_h;
   bool vote_rec_compact = false;     // 32-B vote records (else 64-B), see load_model
@@ -203,7 +208,7 @@ struct ffd_engine {
   // Fit the traversal window into the CU's 160 KB of LDS (and the staging registers), shrinking
   // the patch block if needed, and raise the kernels' dynamic-LDS limit.
   void check_traverse_lds() {
-    const int cap = 160 * 1024;
+    const int cap = TRAV_LDS_CAP;
     auto fit = [&](int& G, int step, int step_y) {
       while (!traverse_window_fits(G, step, step_y, cap)) {
         if (G <= 3) throw std::runtime_error("traversal window does not fit in LDS (step size too large)");
@@ -212,20 +217,24 @@ struct ffd_engine {
     };
     fit(trav_g_hp, desc.hp_option.step_size, desc.hp_option.step_size);
     fit(trav_g_mp, desc.mp_option.step_size, mp_step_y());
-    auto pairs = [&](std::vector<uint4>& h, std::vector<int32_t>& roots, DevBuf& d, DevBuf& droots, DevBuf& dfar) {
-      std::vector<uint4> pr;
+    auto pairs = [&](std::vector<uint4>& h, std::vector<int32_t>& roots, DevBuf& d, DevBuf& droots, DevBuf& dfar,
+                     DevBuf& dtops, DevBuf& dtopi) {
+      std::vector<uint4> pr, tops;
       std::vector<int32_t> rp;
-      std::vector<uint32_t> far;
+      std::vector<uint32_t> far, topi;
       ffd_host::build_pair_records(h, roots, pr, rp, far);
+      ffd_host::build_tree_tops(pr, rp, far, tops, topi);
       upload(d, pr, main_stream());
       upload(droots, rp, main_stream());
       upload(dfar, far, main_stream());
+      upload(dtops, tops, main_stream());
+      upload(dtopi, topi, main_stream());
       HIP_CHECK(hipStreamSynchronize(main_stream()));
       std::vector<uint4>().swap(h);
       std::vector<int32_t>().swap(roots);
     };
-    pairs(hp_nodes_h, hp_roots_h, hp_pairs, hp_proots, hp_far);
-    pairs(mp_nodes_h, mp_roots_h, mp_pairs, mp_proots, mp_far);
+    pairs(hp_nodes_h, hp_roots_h, hp_pairs, hp_proots, hp_far, hp_tops, hp_topi);
+    pairs(mp_nodes_h, mp_roots_h, mp_pairs, mp_proots, mp_far, mp_tops, mp_topi);
     HIP_CHECK(set_traverse_lds_limit(cap));
     HIP_CHECK(set_gabor_lds_limit(96 * 1024));  // padded u8 face of up to MAX_FACE_H rows
     hipDeviceProp_t prop;

@@ -670,10 +670,20 @@ __host__ __device__ __forceinline__ int trav_row_pitch(int WW) {
 }
 __host__ __device__ __forceinline__ int trav_chunk_bytes(int WW) { return trav_row_pitch(WW) % 8 == 0 ? 16 : 8; }
 
-// Window bytes (16-byte aligned); the block's root pair records (uint4 [MAX_TREES]) and their
-// indices (u32 [MAX_TREES]) follow it.
+// Window bytes (16-byte aligned); the block's tree tops follow it (trav_top_n).
 __host__ __device__ __forceinline__ int trav_window_bytes(int WW, int WH) {
   return (NCH * WH * trav_row_pitch(WW) * 2 + 15) & ~15;
+}
+
+// Tree tops in LDS: for each of the block's T trees the first TOPN entries of its heap-ordered top
+// table (TOP_CAP entries per tree in HBM, ffd_device.hpp "tree tops"): a 16-byte pair record and its
+// global pair index each (20 B).  TOPN = the largest power of two <= top_max whose T tables fit in
+// the LDS left over by the window (FFD 4x4 window, 20 trees: 64 entries = levels 0..6).
+constexpr int TRAV_TOP_ENTRIES = 1400;  // tree-top entries a block stages at most (2 per staging thread)
+__host__ __device__ __forceinline__ int trav_top_n(int T, int free_bytes, int top_max) {
+  int n = TOP_CAP;
+  while (n > 1 && (n > top_max || T * n * 20 > free_bytes || T * n > TRAV_TOP_ENTRIES)) n >>= 1;
+  return n;
 }
 
 constexpr int BUF_WORD3 = 0x00020000;  // raw buffer resource word 3 (gfx950: 32-bit data format)
@@ -682,7 +692,9 @@ struct TravArgs {
   const FaceDesc* faces;
   int n_faces, bpf;        // blocks per face: ceil(nx/G) * ceil(ny/G) (max over the batch)
   const uint4* pairs;      // pair records
-  const int32_t* roots;    // per tree: its root pair
+  const uint4* tops;       // per tree: TOP_CAP heap-ordered pair records (levels 0..6)
+  const uint32_t* top_idx; // ... and their global pair indices
+  int top_free, top_max;   // LDS bytes after the window; cap on the entries staged per tree
   const uint32_t* far;     // per pair: offset of child 1's children pair when it exceeds 16 bits
   const HpState* hp_state; // FFD pass: selected trees; nullptr for the head-pose pass
   int ntrees_hp;           // head-pose pass: number of trees
@@ -703,8 +715,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   const int step = A.step, stepy = A.step_y, WW = 32 + step * (G - 1), WH = 32 + stepy * (G - 1);
   const int LW = trav_row_pitch(WW), nq = LW * 2 / CB;
   const int total = NCH * WH * nq;  // chunks per window (host guarantees <= NS * U)
-  uint4* root_rec = reinterpret_cast<uint4*>(smem + trav_window_bytes(WW, WH));  // [t]: tree t's root pair
-  uint32_t* root_idx = reinterpret_cast<uint32_t*>(root_rec + MAX_TREES);
+  uint4* top_rec = reinterpret_cast<uint4*>(smem + trav_window_bytes(WW, WH));  // [t][TOPN] heap-ordered pairs
   // XCD-contiguous, face-major block range of this workgroup's XCD; workgroups of one XCD stride it
   const int N = A.n_faces * A.bpf, xcd = blockIdx.x & 7, k = blockIdx.x >> 3, nk = gridDim.x >> 3;
   const int q8 = N >> 3, r8 = N & 7;
@@ -740,6 +751,8 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     const int items = GG * B.T, sh = B.px0 & 3;
     int32_t* out = A.leaf_out + (HP ? fd.hp_off : fd.mp_off);
     const int ld2 = 2 * LW, chs2 = 2 * WH * LW;  // window row / channel-plane strides (bytes)
+    const int topn = trav_top_n(B.T, A.top_free, A.top_max);
+    const uint32_t* top_i = reinterpret_cast<const uint32_t*>(top_rec + B.T * topn);
     for (int item = tid; item < items; item += NW) {
       const int t = item / GG, pl = item - t * GG;
       const int xi = B.xi0 + pl % G, yi = B.yi0 + pl / G;
@@ -747,22 +760,40 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       // byte address of the patch's top-left integral corner in channel 0's window plane
       const unsigned char* base = reinterpret_cast<const unsigned char*>(win) +
                                   2 * ((yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh);
-      uint32_t P = root_idx[t], s = 0;
-      uint4 R = root_rec[t];
-      uint32_t lo = R.x, hi = R.z & 0xFFFFFFu;
-      while (((lo >> 20) & 63u) != 63u) {
-        // children pair of the current node: right after its pair (child 0), or off1 away (child 1)
-        const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
-        uint32_t Q = P + (s ? off1 : 1u);
-        if (s && off1 == 0u) Q = P + A.far[P];
-        const uint4 N = A.pairs[Q];
+      auto test = [&](uint32_t lo, uint32_t hi) {
         const unsigned char* cb = base + __umul24((lo >> 20) & 63u, (unsigned)chs2);
         const int p1 = rect_mean_lds(cb + 2 * (int)__umul24((lo >> 5) & 31u, (unsigned)LW) + 2 * (int)(lo & 31u),
                                      (hi & 31u) + 1u, ((hi >> 5) & 31u) + 1u, ld2);
         const int p2 = rect_mean_lds(cb + 2 * (int)__umul24((lo >> 15) & 31u, (unsigned)LW) + 2 * (int)((lo >> 10) & 31u),
                                      ((hi >> 10) & 31u) + 1u, ((hi >> 15) & 31u) + 1u, ld2);
         const int thr = (int)(((lo >> 26) | (hi >> 20) << 6) << 22) >> 22;  // 10-bit two's complement
-        s = (p1 - p2) <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
+        return (p1 - p2) <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
+      };
+      // levels 0..log2(topn): heap-ordered pair records in LDS (the children pair of node (h, s) is
+      // entry 2h + s, of the root (h = 0) entry 1)
+      const uint4* trec = top_rec + t * topn;
+      uint32_t h = 0, s = 0;
+      uint4 R = trec[0];
+      uint32_t lo = R.x, hi = R.z & 0xFFFFFFu;
+      while (((lo >> 20) & 63u) != 63u) {
+        const uint32_t h2 = h ? 2u * h + s : 1u;
+        if (h2 >= (uint32_t)topn) break;
+        const uint4 N = trec[h2];
+        s = test(lo, hi);
+        h = h2;
+        R = N;
+        lo = s ? R.y : R.x;
+        hi = (s ? R.w : R.z) & 0xFFFFFFu;
+      }
+      uint32_t P = top_i[t * topn + h];
+      // deeper levels: pair records from HBM (L2), the children pair requested before the test
+      while (((lo >> 20) & 63u) != 63u) {
+        // children pair of the current node: right after its pair (child 0), or off1 away (child 1)
+        const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
+        uint32_t Q = P + (s ? off1 : 1u);
+        if (s && off1 == 0u) Q = P + A.far[P];
+        const uint4 N = A.pairs[Q];
+        s = test(lo, hi);
         P = Q;
         R = N;
         lo = s ? R.y : R.x;
@@ -784,8 +815,14 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     // same plane stride, TravArgs::plane), so a block costs one load per chunk.
     chunk_t st[U];
     int voff[U];
-    uint4 root_nd = make_uint4(0u, 0u, 0u, 0u);
-    uint32_t root_p = 0;
+    // tree tops of the next block (entry e = j + u * NS of its T x TOPN tables), reloaded only when
+    // the face (and so the tree set) changes
+    constexpr int TU = (TRAV_TOP_ENTRIES + NS - 1) / NS;
+    typedef uint32_t rec_t __attribute__((ext_vector_type(4)));  // (a uint4 array lands in scratch)
+    rec_t top_nd[TU];
+    uint32_t top_p[TU];
+    int top_face = -1;  // face whose tops the LDS holds after the next commit
+    bool top_new = false;
     auto stage_offsets = [&](int plane_b) {
       const int s = tid - NW;
       const int dq = NS % nq, dr = (NS / nq) % WH, dc = NS / (nq * WH);
@@ -814,12 +851,20 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
           (void*)(((uint64_t)bhi << 32) | blo), (short)0, nbytes, BUF_WORD3);
       const int base_b = __builtin_amdgcn_readfirstlane((B.py0 * PITCH + (B.px0 & ~3)) * 2);
       // (reads past the face's planes return 0; chunks past the window are loaded but never committed)
-      // the block's root pair records (tree t of the block: lane t of the first staging wave)
-      const int j = tid - NW;
-      if (j < B.T) {
-        const int tree = HP ? j : A.hp_state[B.f].trees[j];
-        root_p = (uint32_t)A.roots[tree];
-        root_nd = A.pairs[root_p];
+      top_new = B.f != top_face;
+      if (top_new) {
+        top_face = B.f;
+        const int topn = trav_top_n(B.T, A.top_free, A.top_max), lg = __builtin_ctz(topn);
+#pragma unroll
+        for (int u = 0; u < TU; u++) {
+          const int e = tid - NW + u * NS;
+          if (e < B.T * topn) {
+            const int j = e >> lg, tree = HP ? j : A.hp_state[B.f].trees[j];
+            const int g = tree * TOP_CAP + (e & (topn - 1));
+            top_nd[u] = reinterpret_cast<const rec_t*>(A.tops)[g];
+            top_p[u] = A.top_idx[g];
+          }
+        }
       }
 #if FFD_TRAV_PROBE != 2
 #pragma unroll
@@ -833,11 +878,18 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       if (!B.ok) return;
       chunk_t* dst = reinterpret_cast<chunk_t*>(win);
       const int s = tid - NW;
-      if (s < B.T) {
-        root_rec[s] = root_nd;
-        root_idx[s] = root_p;
+      if (top_new) {
+        const int n = B.T * trav_top_n(B.T, A.top_free, A.top_max);
+        uint32_t* top_i = reinterpret_cast<uint32_t*>(top_rec + n);
+#pragma unroll
+        for (int u = 0; u < TU; u++) {
+          if (s + u * NS < n) {
+            reinterpret_cast<rec_t*>(top_rec)[s + u * NS] = top_nd[u];
+            top_i[s + u * NS] = top_p[u];
+          }
+        }
       }
-#if FFD_TRAV_PROBE != 2  // the walk-only probe keeps the root pairs (walks need valid records)
+#if FFD_TRAV_PROBE != 2  // the walk-only probe keeps the tree tops (walks need valid records)
 #pragma unroll
       for (int u = 0; u < U; u++)
         if (u * NS + s < total) dst[u * NS + s] = st[u];
@@ -1387,7 +1439,7 @@ void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t
 
 int traverse_lds_bytes(int G, int step, int step_y) {
   const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1);
-  return trav_window_bytes(WW, WH) + MAX_TREES * 20;  // window + the block's root pairs + their indices
+  return trav_window_bytes(WW, WH) + MAX_TREES * 20;  // window + at least the block's root pairs
 }
 
 bool traverse_window_fits(int G, int step, int step_y, int lds_cap) {
@@ -1397,13 +1449,16 @@ bool traverse_window_fits(int G, int step, int step_y, int lds_cap) {
          NCH * WH * (trav_row_pitch(WW) * 2 / cb) <= TRAV_NS * (cb == 16 ? TravStage<16>::U : TravStage<8>::U);
 }
 
-void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* pairs, const int32_t* roots,
-                     const uint32_t* far, const HpState* state, int ntrees_hp, int step, int step_y, int64_t plane,
-                     const uint16_t* chan, int32_t* leaf_out, int n_wg, hipStream_t s) {
+void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* pairs, const uint4* tops,
+                     const uint32_t* top_idx, int top_max, const uint32_t* far, const HpState* state, int ntrees_hp,
+                     int step, int step_y, int64_t plane, const uint16_t* chan, int32_t* leaf_out, int n_wg,
+                     int lds_cap, hipStream_t s) {
   const int total_blocks = n * bpf;
   if (total_blocks <= 0) return;
-  TravArgs A{faces, n, bpf, pairs, roots, far, state, ntrees_hp, step, step_y, (int)plane, chan, leaf_out};
-  const int lds = traverse_lds_bytes(G, step, step_y);
+  // the window, then as many tree-top entries as the rest of the CU's LDS holds
+  const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1), lds = lds_cap;
+  TravArgs A{faces, n, bpf, pairs, tops, top_idx, lds - trav_window_bytes(WW, WH), top_max, far, state, ntrees_hp,
+             step, step_y, (int)plane, chan, leaf_out};
   const int grid = std::max(8, n_wg & ~7);
 #define FFD_TRAV(HPV, GV)                                                                              \
   do {                                                                                                 \

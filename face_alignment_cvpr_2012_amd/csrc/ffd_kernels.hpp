@@ -31,13 +31,17 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t
 hipError_t set_gabor_lds_limit(int bytes);
 // integral channels 0 (gray), 36, 37 (Sobel)
 void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t* chan, hipStream_t s);
+constexpr int TRAV_LDS_CAP = 160 * 1024;  // one traversal workgroup per CU: all of its LDS
 int traverse_lds_bytes(int G, int step, int step_y);
 bool traverse_window_fits(int G, int step, int step_y, int lds_cap);
 // plane: the channel plane stride shared by every face of the batch; n_wg: persistent workgroups (one per CU; rounded down to a multiple of 8 XCDs)
-// pairs / roots / far: the forest's pair records (ffd_device.hpp), root pair per tree, far offsets
-void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* pairs, const int32_t* roots,
-                     const uint32_t* far, const HpState* state, int ntrees_hp, int step, int step_y, int64_t plane,
-                     const uint16_t* chan, int32_t* leaf_out, int n_wg, hipStream_t s);
+// pairs / far: the forest's pair records (ffd_device.hpp) and far offsets; tops / top_idx: per tree
+// TOP_CAP heap-ordered pair records of its top levels and their pair indices (at most top_max
+// entries per tree are staged into LDS); lds_cap: dynamic LDS of a workgroup (window + tops)
+void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* pairs, const uint4* tops,
+                     const uint32_t* top_idx, int top_max, const uint32_t* far, const HpState* state, int ntrees_hp,
+                     int step, int step_y, int64_t plane, const uint16_t* chan, int32_t* leaf_out, int n_wg,
+                     int lds_cap, hipStream_t s);
 hipError_t set_traverse_lds_limit(int bytes);
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
                          const int32_t* patches, int n_patches, const uint16_t* chan, int64_t plane,
