@@ -19,7 +19,7 @@ MODEL     := model/ffd_model.bin
 EXAMPLE   := examples/build/analyze_face
 EXAMPLE2  := examples/build/estimate
 
-HIP_OBJS  := $(PKG)/lib/ffd_kernels.o $(PKG)/lib/ffd_engine.o $(PKG)/lib/ffd_group.o
+HIP_OBJS  := $(PKG)/lib/ffd_kernels.o $(PKG)/lib/ffd_engine.o $(PKG)/lib/ffd_group.o $(PKG)/lib/ffd_archive.o
 HDRS      := include/ffd.h include/ffd_numerics.h include/ffd_gabor.h include/ffd_model_format.h $(CSRC)/ffd_device.hpp \
              $(CSRC)/ffd_kernels.hpp $(CSRC)/model_io.hpp $(CSRC)/ffd_engine_impl.hpp
 
@@ -32,6 +32,11 @@ $(PKG)/lib/ffd_kernels.o: $(CSRC)/ffd_kernels.hip $(HDRS)
 $(PKG)/lib/ffd_engine.o: $(CSRC)/ffd_engine.cpp $(HDRS)
 	@mkdir -p $(@D)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# host-only (the archive writer): plain g++
+$(PKG)/lib/ffd_archive.o: $(CSRC)/ffd_archive.cpp include/ffd.h include/ffd_model_format.h $(CSRC)/model_io.hpp
+	@mkdir -p $(@D)
+	$(CXX) $(CXXFLAGS) -Iinclude -c $< -o $@
 
 $(PKG)/lib/ffd_group.o: $(CSRC)/ffd_group.cpp $(HDRS)
 	@mkdir -p $(@D)

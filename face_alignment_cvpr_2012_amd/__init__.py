@@ -101,6 +101,8 @@ EXPORTED_SYMBOLS = (
     "ffd_stage_name", "ffd_status_string", "ffd_estimate_headpose", "ffd_estimate_facial_features",
     "ffd_group_create", "ffd_group_destroy", "ffd_group_last_error", "ffd_group_size", "ffd_group_engine",
     "ffd_group_analyze_faces", "ffd_comm_id", "ffd_engine_join", "ffd_gather_faces",
+    "ffd_model_open", "ffd_model_close", "ffd_model_last_error", "ffd_model_num_trees", "ffd_model_tree_save_path",
+    "ffd_model_tree_archive", "ffd_model_save_tree",
 )
 COMM_ID_BYTES = 128
 STATUS_OK, STATUS_INVALID_ARGUMENT, STATUS_UNSUPPORTED = 0, 1, 7
@@ -160,7 +162,17 @@ def lib():
     L.ffd_comm_id.argtypes = [ctypes.c_void_p]
     L.ffd_engine_join.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
     L.ffd_gather_faces.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
-    for name in ("ffd_engine_create", "ffd_face_geometry", "ffd_analyze_faces", "ffd_analyze_faces_device",
+    L.ffd_model_open.argtypes = [ctypes.c_char_p, P(ctypes.c_void_p)]
+    L.ffd_model_close.argtypes = [ctypes.c_void_p]
+    L.ffd_model_last_error.restype = ctypes.c_char_p
+    L.ffd_model_num_trees.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    L.ffd_model_num_trees.restype = ctypes.c_int32
+    L.ffd_model_tree_save_path.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
+                                           ctypes.c_int32]
+    L.ffd_model_tree_archive.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                         ctypes.c_int64, P(ctypes.c_int64)]
+    L.ffd_model_save_tree.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p]
+    for name in ("ffd_model_open", "ffd_model_tree_save_path", "ffd_model_tree_archive", "ffd_model_save_tree","ffd_engine_create", "ffd_face_geometry", "ffd_analyze_faces", "ffd_analyze_faces_device",
                  "ffd_synchronize", "ffd_extract_channels", "ffd_forest_eval_leaves", "ffd_get_trace",
                  "ffd_set_profiling", "ffd_get_stage_times", "ffd_estimate_headpose",
                  "ffd_estimate_facial_features", "ffd_group_create", "ffd_group_analyze_faces", "ffd_comm_id",

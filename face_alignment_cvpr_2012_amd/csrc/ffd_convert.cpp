@@ -153,6 +153,15 @@ struct ForestOut {
   std::vector<int32_t> hp_labels;
   std::vector<int16_t> mp_offset;
   std::vector<float> mp_var, mp_pf;
+  // the fields only the archive writer needs (ffd_archive.cpp, Tree<S>::save Tree.hpp:239-256)
+  std::vector<double> node_info;                 // ThresholdSplit::info (0 for leaves)
+  std::vector<int64_t> tree_counts;              // per tree: m_num_nodes, i_node
+  std::vector<int32_t> tree_param;               // per tree: the archived ForestParam ints (7)
+  std::vector<float> tree_ratio;                 // per tree: ForestParam::patch_size_ratio
+  std::vector<int32_t> tree_features;            // concatenated ForestParam::features
+  std::vector<int64_t> tree_features_off{0};
+  std::vector<uint8_t> tree_strings;             // per tree: tree_path, image_path, m_save_path
+  std::vector<int64_t> tree_strings_off{0};
 };
 
 struct TreeParseState {
@@ -172,6 +181,7 @@ void parse_node(Tokens& tk, Kind kind, TreeParseState& st, ForestOut& out, int d
   long has_split = tk.i();
   if (d != depth) throw std::runtime_error("archive grammar: depth mismatch");
   int16_t split[FFD_SPLIT_FIELDS] = {0};
+  double info = 0.0;
   if (is_leaf) {
     if (st.first_leaf) { tk.expect(0, "leaf class tracking"); tk.expect(0, "leaf class version"); st.first_leaf = false; }
     out.node_leaf.push_back((int32_t)out.leaf_n.size());
@@ -216,7 +226,7 @@ void parse_node(Tokens& tk, Kind kind, TreeParseState& st, ForestOut& out, int d
     split[0] = (int16_t)tk.i();  // feature_channel
     if (st.first_split) { tk.expect(0, "Rect tracking"); tk.expect(0, "Rect version"); st.first_split = false; }
     for (int j = 0; j < 8; j++) split[1 + j] = (int16_t)tk.i();  // rect1, rect2 (x y w h)
-    (void)tk.d();                                                 // info (unused at test time)
+    info = tk.d();                                                // info (unused at test time; kept for the writer)
     long thr = tk.i();
     if (thr < -32768 || thr > 32767) throw std::runtime_error("threshold out of int16");
     split[9] = (int16_t)thr;
@@ -224,6 +234,7 @@ void parse_node(Tokens& tk, Kind kind, TreeParseState& st, ForestOut& out, int d
   if (is_leaf && has_split) throw std::runtime_error("node is both leaf and split");
   if (!is_leaf && !has_split) throw std::runtime_error("internal node without split");
   for (int j = 0; j < FFD_SPLIT_FIELDS; j++) out.node_split.push_back(is_leaf ? 0 : split[j]);
+  out.node_info.push_back(info);
   if (!is_leaf) {
     tk.expect(3, "TreeNode pointer class id");
     parse_node(tk, kind, st, out, depth + 1);
@@ -243,14 +254,21 @@ void parse_tree(const std::string& path, Kind kind, ForestOut& out) {
   // ForestParam (Constants.hpp:44-59)
   tk.expect(0, "ForestParam tracking");
   tk.expect(0, "ForestParam version");
-  for (int j = 0; j < 7; j++) (void)tk.i();
-  (void)tk.f();
-  (void)tk.str();
-  (void)tk.str();
+  for (int j = 0; j < 7; j++) out.tree_param.push_back((int32_t)tk.i());
+  out.tree_ratio.push_back(tk.f());
+  auto put_str = [&](const std::string& v) {
+    out.tree_strings.insert(out.tree_strings.end(), v.begin(), v.end());
+    out.tree_strings_off.push_back((int64_t)out.tree_strings.size());
+  };
+  put_str(tk.str());  // tree_path
+  put_str(tk.str());  // image_path
   long nf = tk.i();
   tk.expect(0, "features item_version");
-  for (long j = 0; j < nf; j++) (void)tk.i();
-  (void)tk.str();  // m_save_path
+  for (long j = 0; j < nf; j++) out.tree_features.push_back((int32_t)tk.i());
+  out.tree_features_off.push_back((int64_t)out.tree_features.size());
+  put_str(tk.str());  // m_save_path
+  out.tree_counts.push_back(num_nodes);
+  out.tree_counts.push_back(i_node);
   // root pointer: class id 3, tracking 1, version 0
   tk.expect(3, "root class id");
   tk.expect(1, "TreeNode tracking");
@@ -304,6 +322,14 @@ void put_forest(ffd::ModelFile& m, const std::string& p, Kind kind, const Forest
     m.put<float>(p + ".leaf_var", "f32", {L, FFD_NUM_PARTS}, o.mp_var);
     m.put<float>(p + ".leaf_pf", "f32", {L, FFD_NUM_PARTS}, o.mp_pf);
   }
+  m.put<double>(p + ".node_info", "f64", {N}, o.node_info);
+  m.put<int64_t>(p + ".tree_counts", "i64", {T, 2}, o.tree_counts);
+  m.put<int32_t>(p + ".tree_param", "i32", {T, 7}, o.tree_param);
+  m.put<float>(p + ".tree_ratio", "f32", {T}, o.tree_ratio);
+  m.put<int32_t>(p + ".tree_features", "i32", {(uint64_t)o.tree_features.size()}, o.tree_features);
+  m.put<int64_t>(p + ".tree_features_off", "i64", {T + 1}, o.tree_features_off);
+  m.put<uint8_t>(p + ".tree_strings", "u8", {(uint64_t)o.tree_strings.size()}, o.tree_strings);
+  m.put<int64_t>(p + ".tree_strings_off", "i64", {3 * T + 1}, o.tree_strings_off);
 }
 
 }  // namespace

@@ -223,6 +223,25 @@ ffd_status ffd_comm_id(uint8_t* id /* FFD_COMM_ID_BYTES */);
 ffd_status ffd_engine_join(ffd_engine* engine, const uint8_t* id, int32_t n_ranks, int32_t rank);
 ffd_status ffd_gather_faces(ffd_engine* engine, const void* d_local, int32_t n_per_rank, void* d_root, int32_t root);
 
+/* ---- Boost text-archive writer ------------------------------------------
+ * Replaces Tree<S>::save (include/Tree.hpp:239-256: boost::archive::text_oarchive << *this) and the
+ * serializers it runs (Tree.hpp:336-343, Constants.hpp:44-59, TreeNode.hpp:150-164,
+ * ThresholdSplit.hpp:60-67, ImageSample.hpp:83-90, MPSample.hpp:149-158, HeadPoseSample.hpp:154-161):
+ * re-emits a tree of an FFDMODEL container as the reference's archive bytes (the converted
+ * pretrained trees byte-for-byte equal to the shipped files).  Host only; no device needed.
+ * Tree index t of FFD_FOREST_FFD is forest-major (forest t / ntrees, tree t % ntrees). */
+typedef struct ffd_model ffd_model;
+ffd_status ffd_model_open(const char* path, ffd_model** out);
+void ffd_model_close(ffd_model* model);
+const char* ffd_model_last_error(void);  /* this thread's last ffd_model_* failure */
+int32_t ffd_model_num_trees(const ffd_model* model, int32_t forest_kind);
+/* the tree's archived m_save_path (Tree.hpp:254: where Tree<S>::save writes) */
+ffd_status ffd_model_tree_save_path(const ffd_model* model, int32_t forest_kind, int32_t tree, char* buf, int32_t cap);
+/* the archive bytes into buf (buf == NULL: only *size); not NUL-terminated */
+ffd_status ffd_model_tree_archive(const ffd_model* model, int32_t forest_kind, int32_t tree, char* buf, int64_t cap,
+                                  int64_t* size);
+ffd_status ffd_model_save_tree(const ffd_model* model, int32_t forest_kind, int32_t tree, const char* path);
+
 /* Library version string. */
 const char* ffd_version(void);
 

@@ -39,6 +39,17 @@
  *   mp.leaf_var        f32[L,10] MPLeaf::mp_parts_variance
  *   mp.leaf_pf         f32[L,10] MPLeaf::mp_prob_foreground
  *
+ * Archive-only fields (not used by the engine; the Boost text-archive writer
+ * ffd_model_save_tree re-emits the reference's files from them, Tree.hpp:239-256):
+ *   <p>.node_info         f64[N]   ThresholdSplit::info (0 for leaves)
+ *   <p>.tree_counts       i64[T,2] Tree::m_num_nodes, Tree::i_node
+ *   <p>.tree_param        i32[T,7] the ForestParam each archive holds (its ints)
+ *   <p>.tree_ratio        f32[T]   ... and its patch_size_ratio
+ *   <p>.tree_features     i32[k]   ... and its features, per tree at
+ *   <p>.tree_features_off i64[T+1]
+ *   <p>.tree_strings      u8[b]    tree_path, image_path, m_save_path of tree t are
+ *   <p>.tree_strings_off  i64[3T+1] bytes [off[3t+j], off[3t+j+1]), j = 0, 1, 2
+ *
  * Pre-order means: a node's left subtree follows it immediately, then its
  * right subtree (TreeNode::serialize, TreeNode.hpp:150-164).
  */
