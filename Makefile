@@ -19,9 +19,10 @@ MODEL     := model/ffd_model.bin
 EXAMPLE   := examples/build/analyze_face
 EXAMPLE2  := examples/build/estimate
 
-HIP_OBJS  := $(PKG)/lib/ffd_kernels.o $(PKG)/lib/ffd_engine.o $(PKG)/lib/ffd_group.o $(PKG)/lib/ffd_archive.o
+HIP_OBJS  := $(PKG)/lib/ffd_kernels.o $(PKG)/lib/ffd_engine.o $(PKG)/lib/ffd_group.o $(PKG)/lib/ffd_archive.o \
+             $(PKG)/lib/ffd_haar.o $(PKG)/lib/ffd_detect.o
 HDRS      := include/ffd.h include/ffd_numerics.h include/ffd_gabor.h include/ffd_model_format.h $(CSRC)/ffd_device.hpp \
-             $(CSRC)/ffd_kernels.hpp $(CSRC)/model_io.hpp $(CSRC)/ffd_engine_impl.hpp
+             $(CSRC)/ffd_kernels.hpp $(CSRC)/model_io.hpp $(CSRC)/ffd_engine_impl.hpp $(CSRC)/ffd_haar.hpp
 
 all: $(LIB) $(CONVERT) $(SYNTH) $(ORACLE) $(EXAMPLE) $(EXAMPLE2)
 
@@ -37,6 +38,14 @@ $(PKG)/lib/ffd_engine.o: $(CSRC)/ffd_engine.cpp $(HDRS)
 $(PKG)/lib/ffd_archive.o: $(CSRC)/ffd_archive.cpp include/ffd.h include/ffd_model_format.h $(CSRC)/model_io.hpp
 	@mkdir -p $(@D)
 	$(CXX) $(CXXFLAGS) -Iinclude -c $< -o $@
+
+$(PKG)/lib/ffd_haar.o: $(CSRC)/ffd_haar.hip $(CSRC)/ffd_haar.hpp
+	@mkdir -p $(@D)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(PKG)/lib/ffd_detect.o: $(CSRC)/ffd_detect.cpp $(HDRS)
+	@mkdir -p $(@D)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(PKG)/lib/ffd_group.o: $(CSRC)/ffd_group.cpp $(HDRS)
 	@mkdir -p $(@D)

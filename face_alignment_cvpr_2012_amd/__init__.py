@@ -86,6 +86,11 @@ class _Desc(ctypes.Structure):
                 ("hp_option", _HpOpt), ("mp_option", _MpOpt), ("ms_option", _MsOpt)]
 
 
+class _DetOpt(ctypes.Structure):
+    _fields_ = [("min_feature_size", ctypes.c_int32), ("min_neighbors", ctypes.c_int32),
+                ("search_scale_factor", ctypes.c_float), ("widen", ctypes.c_int32)]
+
+
 class _Trace(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in
                 ("face", "channels", "hp_leaves", "mp_leaves", "trees", "pose_freq", "vote_counts", "ms_mean")]
@@ -101,7 +106,8 @@ EXPORTED_SYMBOLS = (
     "ffd_stage_name", "ffd_status_string", "ffd_estimate_headpose", "ffd_estimate_facial_features",
     "ffd_group_create", "ffd_group_destroy", "ffd_group_last_error", "ffd_group_size", "ffd_group_engine",
     "ffd_group_analyze_faces", "ffd_comm_id", "ffd_engine_join", "ffd_gather_faces",
-    "ffd_model_open", "ffd_model_close", "ffd_model_last_error", "ffd_model_num_trees", "ffd_model_tree_save_path",
+    "ffd_detect_options_init", "ffd_detect_faces", "ffd_detect_faces_device", "ffd_analyze_images",
+    "ffd_detect_candidates", "ffd_model_open", "ffd_model_close", "ffd_model_last_error", "ffd_model_num_trees", "ffd_model_tree_save_path",
     "ffd_model_tree_archive", "ffd_model_save_tree",
 )
 COMM_ID_BYTES = 128
@@ -162,6 +168,16 @@ def lib():
     L.ffd_comm_id.argtypes = [ctypes.c_void_p]
     L.ffd_engine_join.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
     L.ffd_gather_faces.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
+    L.ffd_detect_options_init.argtypes = [P(_DetOpt)]
+    L.ffd_detect_faces.argtypes = [ctypes.c_void_p, P(_Image), ctypes.c_int32, P(_DetOpt), ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int32)]
+    L.ffd_detect_faces_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P(_DetOpt), ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int32)]
+    L.ffd_analyze_images.argtypes = [ctypes.c_void_p, P(_Image), ctypes.c_int32, P(_DetOpt), ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int32)]
+    L.ffd_detect_candidates.argtypes = [ctypes.c_void_p, P(_Image), P(_DetOpt), ctypes.c_void_p, ctypes.c_int32,
+                                        P(ctypes.c_int32)]
     L.ffd_model_open.argtypes = [ctypes.c_char_p, P(ctypes.c_void_p)]
     L.ffd_model_close.argtypes = [ctypes.c_void_p]
     L.ffd_model_last_error.restype = ctypes.c_char_p
@@ -172,7 +188,8 @@ def lib():
     L.ffd_model_tree_archive.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                          ctypes.c_int64, P(ctypes.c_int64)]
     L.ffd_model_save_tree.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p]
-    for name in ("ffd_model_open", "ffd_model_tree_save_path", "ffd_model_tree_archive", "ffd_model_save_tree","ffd_engine_create", "ffd_face_geometry", "ffd_analyze_faces", "ffd_analyze_faces_device",
+    for name in ("ffd_detect_faces", "ffd_detect_faces_device", "ffd_analyze_images", "ffd_detect_candidates",
+                 "ffd_model_open", "ffd_model_tree_save_path", "ffd_model_tree_archive", "ffd_model_save_tree","ffd_engine_create", "ffd_face_geometry", "ffd_analyze_faces", "ffd_analyze_faces_device",
                  "ffd_synchronize", "ffd_extract_channels", "ffd_forest_eval_leaves", "ffd_get_trace",
                  "ffd_set_profiling", "ffd_get_stage_times", "ffd_estimate_headpose",
                  "ffd_estimate_facial_features", "ffd_group_create", "ffd_group_analyze_faces", "ffd_comm_id",
@@ -209,6 +226,19 @@ class MeanShiftOption:                  # include/MeanShift.hpp:16-25
 
 
 @dataclass
+class FaceDetectionOption:              # include/FaceForest.hpp:21-32
+    min_feature_size: int = 30
+    min_neighbors: int = 1
+    search_scale_factor: float = 1.3
+    widen: bool = True                  # detectFace's 5 % / 15 % enlargement (FaceForest.cpp:148-158)
+
+
+def _det_opt(o):
+    o = o or FaceDetectionOption()
+    return _DetOpt(int(o.min_feature_size), int(o.min_neighbors), float(o.search_scale_factor), int(bool(o.widen)))
+
+
+@dataclass
 class FaceForestOptions:                # include/FaceForest.hpp:60-68
     model_path: str = field(default_factory=default_model_path)
     device: int = 0
@@ -216,6 +246,7 @@ class FaceForestOptions:                # include/FaceForest.hpp:60-68
     hp_option: HeadPoseEstimatorOption = field(default_factory=HeadPoseEstimatorOption)
     mp_option: MultiPartEstimatorOption = field(default_factory=MultiPartEstimatorOption)
     ms_option: MeanShiftOption = field(default_factory=MeanShiftOption)
+    fd_option: FaceDetectionOption = field(default_factory=FaceDetectionOption)
 
 
 @dataclass
@@ -323,10 +354,68 @@ class FaceForest:
         """FaceForest::analyzeFace(img, bbox, face) (src/FaceForest.cpp:183-258)."""
         return self.analyzeFaces([img], [face_bbox])[0]
 
-    def analyzeImage(self, img, faces_bboxes):
-        """FaceForest::analyzeImage (src/FaceForest.cpp:161-181) with the face boxes supplied by
-        the caller's detector (the Haar cascade stays outside this engine)."""
-        return self.analyzeFaces([img], list(faces_bboxes), [0] * len(faces_bboxes))
+    def analyzeImage(self, img, faces_bboxes=None):
+        """FaceForest::analyzeImage (src/FaceForest.cpp:161-181): the GPU Haar detector
+        (detectFace) then analyzeFace on every box.  With faces_bboxes given, those boxes are analysed
+        instead (a caller-side detector)."""
+        if faces_bboxes is not None:
+            return self.analyzeFaces([img], list(faces_bboxes), [0] * len(faces_bboxes))
+        return self.analyzeImages([img])[0]
+
+    def detectFace(self, img, fd_option=None):
+        """FaceForest::detectFace (src/FaceForest.cpp:136-159) on the GPU: boxes as (n, 4) int32."""
+        return self.detectFaces([img], fd_option)[0]
+
+    def detectFaces(self, images, fd_option=None):
+        """detectFace over a batch of frames (one GPU pass); a list of (n_k, 4) arrays."""
+        imgs, cim = _image_array(images)
+        opt = _det_opt(fd_option or self.options.fd_option)
+        cap = 64 * max(1, len(imgs))
+        for _ in range(2):
+            boxes = np.zeros((cap, 4), np.int32)
+            owner = np.zeros(cap, np.int32)
+            n = ctypes.c_int32()
+            _check(lib().ffd_detect_faces(self._h, cim, len(imgs), ctypes.byref(opt), boxes.ctypes.data,
+                                          owner.ctypes.data, cap, ctypes.byref(n)), self._h)
+            if n.value <= cap:
+                break
+            cap = n.value
+        return [boxes[: n.value][owner[: n.value] == k] for k in range(len(imgs))]
+
+    def analyzeImages(self, images, fd_option=None):
+        """analyzeImage over a batch of frames: detection and all faces as GPU batches; a list of
+        Face lists, one per frame."""
+        imgs, cim = _image_array(images)
+        opt = _det_opt(fd_option or self.options.fd_option)
+        cap = 64 * max(1, len(imgs))
+        for _ in range(2):
+            out = (_Face * cap)()
+            owner = np.zeros(cap, np.int32)
+            n = ctypes.c_int32()
+            _check(lib().ffd_analyze_images(self._h, cim, len(imgs), ctypes.byref(opt), out, owner.ctypes.data, cap,
+                                            ctypes.byref(n)), self._h)
+            if n.value <= cap:
+                break
+            cap = n.value
+        res = [[] for _ in imgs]
+        for i in range(n.value):
+            res[owner[i]].append(_face_from_record(out[i]))
+        return res
+
+    def detect_candidates(self, img, fd_option=None):
+        """Test hook: detectMultiScale's ungrouped candidates of one frame in scan order, (n, 4)."""
+        imgs, cim = _image_array([img])
+        opt = _det_opt(fd_option or self.options.fd_option)
+        cap = 4096
+        for _ in range(2):
+            raw = np.zeros((cap, 4), np.int32)
+            n = ctypes.c_int32()
+            _check(lib().ffd_detect_candidates(self._h, cim, ctypes.byref(opt), raw.ctypes.data, cap,
+                                               ctypes.byref(n)), self._h)
+            if n.value <= cap:
+                break
+            cap = n.value
+        return raw[: n.value].copy()
 
     # ---- batched API --------------------------------------------------------
     def analyzeFaces(self, images, boxes, box_img=None):

@@ -332,6 +332,138 @@ void put_forest(ffd::ModelFile& m, const std::string& p, Kind kind, const Forest
   m.put<int64_t>(p + ".tree_strings_off", "i64", {3 * T + 1}, o.tree_strings_off);
 }
 
+// ---- Haar cascade --------------------------------------------------------
+// data/haarcascade_frontalface_alt.xml is in OpenCV's "opencv-cascade-classifier" format (stageType
+// BOOST, featureType HAAR), which OpenCV 2.4.9's CascadeClassifier::load reads with
+// CascadeClassifier::Data::read + HaarEvaluator::read (objdetect/cascadedetect.cpp); numbers are
+// parsed as double (FileNode) and stored as float.  Only stump cascades (one internal node per weak
+// classifier, the detector FaceForest.cpp:146 loads) without tilted features are accepted.
+struct Cascade {
+  int win_w = 0, win_h = 0;
+  std::vector<int32_t> stage_first, stage_ntrees, weak_feature, feature_rect;
+  std::vector<float> stage_threshold, weak_threshold, weak_leaves, feature_weight;
+};
+
+std::string tag_text(const std::string& s, size_t& pos, const std::string& tag, size_t limit) {
+  const std::string open = "<" + tag + ">", close = "</" + tag + ">";
+  size_t a = s.find(open, pos);
+  if (a == std::string::npos || a >= limit) throw std::runtime_error("cascade: missing <" + tag + ">");
+  a += open.size();
+  size_t b = s.find(close, a);
+  if (b == std::string::npos) throw std::runtime_error("cascade: unterminated <" + tag + ">");
+  pos = b + close.size();
+  return s.substr(a, b - a);
+}
+
+std::vector<double> numbers(const std::string& t) {
+  std::vector<double> v;
+  const char* p = t.c_str();
+  char* e = nullptr;
+  for (;;) {
+    while (*p && isspace((unsigned char)*p)) p++;
+    if (!*p) break;
+    double d = std::strtod(p, &e);
+    if (e == p) throw std::runtime_error("cascade: bad number in '" + t + "'");
+    v.push_back(d);
+    p = e;
+  }
+  return v;
+}
+
+bool parse_cascade(const std::string& path, Cascade& c) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f.is_open()) return false;
+  std::stringstream ss;
+  ss << f.rdbuf();
+  const std::string s = ss.str();
+  size_t pos = 0;
+  if (tag_text(s, pos, "stageType", s.size()).find("BOOST") == std::string::npos ||
+      tag_text(s, pos, "featureType", s.size()).find("HAAR") == std::string::npos)
+    throw std::runtime_error("cascade: only BOOST / HAAR cascades are supported");
+  c.win_h = (int)numbers(tag_text(s, pos, "height", s.size())).at(0);
+  c.win_w = (int)numbers(tag_text(s, pos, "width", s.size())).at(0);
+  size_t st = s.find("<stages>", pos), st_end = s.find("</stages>", pos);
+  size_t ft = s.find("<features>", pos), ft_end = s.find("</features>", pos);
+  if (st == std::string::npos || st_end == std::string::npos || ft == std::string::npos || ft_end == std::string::npos)
+    throw std::runtime_error("cascade: missing <stages> or <features>");
+  // stages: <maxWeakCount> <stageThreshold> <weakClassifiers> (<internalNodes> <leafValues>)*
+  pos = st;
+  for (;;) {
+    size_t nxt = s.find("<maxWeakCount>", pos);
+    if (nxt == std::string::npos || nxt > st_end) break;
+    pos = nxt;
+    (void)tag_text(s, pos, "maxWeakCount", st_end);
+    c.stage_threshold.push_back((float)numbers(tag_text(s, pos, "stageThreshold", st_end)).at(0));
+    size_t wc_end = s.find("</weakClassifiers>", pos);
+    if (wc_end == std::string::npos || wc_end > st_end) throw std::runtime_error("cascade: bad <weakClassifiers>");
+    c.stage_first.push_back((int32_t)c.weak_feature.size());
+    int n = 0;
+    for (;;) {
+      size_t in = s.find("<internalNodes>", pos);
+      if (in == std::string::npos || in > wc_end) break;
+      pos = in;
+      std::vector<double> nd = numbers(tag_text(s, pos, "internalNodes", wc_end));
+      std::vector<double> lv = numbers(tag_text(s, pos, "leafValues", wc_end));
+      if (nd.size() != 4 || lv.size() != 2)
+        throw std::runtime_error("cascade: only stump classifiers (one internal node, two leaves) are supported");
+      c.weak_feature.push_back((int32_t)nd[2]);
+      c.weak_threshold.push_back((float)nd[3]);
+      c.weak_leaves.push_back((float)lv[0]);
+      c.weak_leaves.push_back((float)lv[1]);
+      n++;
+    }
+    c.stage_ntrees.push_back(n);
+    pos = wc_end;
+  }
+  // features: <_> <rects> (<_> x y w h weight </_>){2,3} </rects> [<tilted>t</tilted>] </_>
+  pos = ft;
+  for (;;) {
+    size_t r = s.find("<rects>", pos);
+    if (r == std::string::npos || r > ft_end) break;
+    size_t r_end = s.find("</rects>", r);
+    int k = 0;
+    int32_t rect[12] = {0};
+    float w[3] = {0.f, 0.f, 0.f};
+    pos = r + 7;
+    for (;;) {
+      size_t a = s.find("<_>", pos);
+      if (a == std::string::npos || a > r_end) break;
+      size_t b = s.find("</_>", a);
+      std::vector<double> v = numbers(s.substr(a + 3, b - a - 3));
+      if (v.size() != 5 || k >= 3) throw std::runtime_error("cascade: bad feature rectangle");
+      for (int j = 0; j < 4; j++) rect[4 * k + j] = (int32_t)v[j];
+      w[k] = (float)v[4];
+      k++;
+      pos = b + 4;
+    }
+    if (k < 2) throw std::runtime_error("cascade: feature with fewer than 2 rectangles");
+    pos = r_end + 8;
+    size_t tl = s.find("<tilted>", pos), next_r = s.find("<rects>", pos);
+    if (tl != std::string::npos && tl < ft_end && (next_r == std::string::npos || tl < next_r) &&
+        numbers(tag_text(s, tl, "tilted", ft_end)).at(0) != 0)
+      throw std::runtime_error("cascade: tilted features are not supported");
+    c.feature_rect.insert(c.feature_rect.end(), rect, rect + 12);
+    c.feature_weight.insert(c.feature_weight.end(), w, w + 3);
+  }
+  const int nf = (int)c.feature_weight.size() / 3;
+  for (int32_t fi : c.weak_feature)
+    if (fi < 0 || fi >= nf) throw std::runtime_error("cascade: feature index out of range");
+  return true;
+}
+
+void put_cascade(ffd::ModelFile& m, const Cascade& c) {
+  const uint64_t S = c.stage_threshold.size(), C = c.weak_feature.size(), F = c.feature_weight.size() / 3;
+  m.put<int32_t>("haar.window", "i32", {2}, {c.win_w, c.win_h});
+  m.put<int32_t>("haar.stage_first", "i32", {S}, c.stage_first);
+  m.put<int32_t>("haar.stage_ntrees", "i32", {S}, c.stage_ntrees);
+  m.put<float>("haar.stage_threshold", "f32", {S}, c.stage_threshold);
+  m.put<int32_t>("haar.weak_feature", "i32", {C}, c.weak_feature);
+  m.put<float>("haar.weak_threshold", "f32", {C}, c.weak_threshold);
+  m.put<float>("haar.weak_leaves", "f32", {C, 2}, c.weak_leaves);
+  m.put<int32_t>("haar.feature_rect", "i32", {F, 3, 4}, c.feature_rect);
+  m.put<float>("haar.feature_weight", "f32", {F, 3}, c.feature_weight);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -365,12 +497,18 @@ int main(int argc, char** argv) {
       }
     put_params(m, "mp", mp, (int)dirs.size());
     put_forest(m, "mp", MP, mpo);
+    Cascade cas;  // FaceDetectionOption::path_face_cascade as demo.cpp:186 / eval_ffd.cpp:143 set it
+    const bool have_cascade = parse_cascade(root + "/data/haarcascade_frontalface_alt.xml", cas);
+    if (have_cascade) put_cascade(m, cas);
     std::string tmp = outp + ".tmp";
     m.save(tmp);
     if (std::rename(tmp.c_str(), outp.c_str()) != 0) throw std::runtime_error("rename failed");
     std::printf("ffd_convert: hp %zu trees %zu nodes %zu leaves; mp %zu forests %zu trees %zu nodes %zu leaves -> %s\n",
                 hpo.tree_node_off.size() - 1, hpo.node_leaf.size(), hpo.leaf_n.size(), dirs.size(),
                 mpo.tree_node_off.size() - 1, mpo.node_leaf.size(), mpo.leaf_n.size(), outp.c_str());
+    if (have_cascade)
+      std::printf("ffd_convert: haar cascade %dx%d, %zu stages, %zu weak classifiers, %zu features\n", cas.win_w,
+                  cas.win_h, cas.stage_threshold.size(), cas.weak_feature.size(), cas.feature_weight.size() / 3);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "ffd_convert: ERROR: %s\n", e.what());
     return 1;

@@ -1,0 +1,390 @@
+// ffd_detect.cpp — host side of the Haar face detector and the frame-level
+// entry points built on it:
+//   ffd_detect_faces[_device]  FaceForest::detectFace      /root/reference/src/FaceForest.cpp:136-159
+//   ffd_analyze_images         FaceForest::analyzeImage    /root/reference/src/FaceForest.cpp:161-181
+//   ffd_detect_candidates      (test hook) detectMultiScale's ungrouped candidates of one frame
+// The pyramid geometry (which scales detectMultiScale scans, their sizes and resize modes) is built
+// here with the restatement's double arithmetic (oracle/ffd_oracle.cpp haar_scan); all pixel work runs
+// in the ffd_haar.hip kernels on the engine's main stream.
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ffd_engine_impl.hpp"
+#include "model_io.hpp"
+
+using namespace ffd_host;
+
+// Load the cascade arrays written by ffd_convert (haar.*) into device records.
+void ffd_engine::load_cascade(const ffd::ModelFile& m) {
+  have_haar = m.has("haar.window");
+  if (!have_haar) return;
+  const int32_t* win = m.get("haar.window").as<int32_t>();
+  haar_ww = win[0];
+  haar_wh = win[1];
+  if (haar_ww < 3 || haar_wh < 3 || haar_ww > 255 || haar_wh > 255) throw std::runtime_error("cascade window size");
+  const auto& sf = m.get("haar.stage_first");
+  const auto& sn = m.get("haar.stage_ntrees");
+  const auto& st = m.get("haar.stage_threshold");
+  haar_stages = (int)sf.count();
+  std::vector<HaarStage> stages(haar_stages);
+  for (int s = 0; s < haar_stages; s++) {
+    stages[s].first = sf.as<int32_t>()[s];
+    stages[s].ntrees = sn.as<int32_t>()[s];
+    stages[s].thr = st.as<float>()[s] - 1e-5f;  // CascadeClassifier::Data::read THRESHOLD_EPS
+    stages[s].pad = 0;
+  }
+  const auto& wf = m.get("haar.weak_feature");
+  const auto& wt = m.get("haar.weak_threshold");
+  const auto& wl = m.get("haar.weak_leaves");
+  const auto& fr = m.get("haar.feature_rect");
+  const auto& fw = m.get("haar.feature_weight");
+  const int64_t nw = (int64_t)wf.count(), nf = (int64_t)fw.count() / 3;
+  std::vector<HaarWeak> weak(nw);
+  for (int64_t i = 0; i < nw; i++) {
+    const int f = wf.as<int32_t>()[i];
+    if (f < 0 || f >= nf) throw std::runtime_error("cascade feature index out of range");
+    const int32_t* r = fr.as<int32_t>() + f * 12;
+    auto pack = [&](int k) {
+      for (int j = 0; j < 4; j++)
+        if (r[4 * k + j] < 0 || r[4 * k + j] > 255) throw std::runtime_error("cascade rectangle out of range");
+      if (r[4 * k] + r[4 * k + 2] > haar_ww || r[4 * k + 1] + r[4 * k + 3] > haar_wh)
+        throw std::runtime_error("cascade rectangle outside the window");
+      return (uint32_t)r[4 * k] | (uint32_t)r[4 * k + 1] << 8 | (uint32_t)r[4 * k + 2] << 16 | (uint32_t)r[4 * k + 3] << 24;
+    };
+    HaarWeak& w = weak[i];
+    std::memset(&w, 0, sizeof(w));
+    w.r0 = pack(0);
+    w.r1 = pack(1);
+    w.w0 = fw.as<float>()[f * 3];
+    w.w1 = fw.as<float>()[f * 3 + 1];
+    w.w2 = fw.as<float>()[f * 3 + 2];
+    w.r2 = w.w2 != 0.0f ? pack(2) : 0u;
+    w.thr = wt.as<float>()[i];
+    w.leaf0 = wl.as<float>()[2 * i];
+    w.leaf1 = wl.as<float>()[2 * i + 1];
+  }
+  for (const auto& s : stages)
+    if (s.first < 0 || s.ntrees < 0 || s.first + s.ntrees > nw) throw std::runtime_error("cascade stage range");
+  upload(haar_weak, weak, main_stream());
+  upload(haar_stage, stages, main_stream());
+}
+
+namespace {
+
+struct FrameIn {
+  int64_t img_off;
+  int w, h, stride;
+};
+
+void default_options(ffd_detect_options* o) {
+  o->min_feature_size = 30;     // FaceDetectionOption (include/FaceForest.hpp:21-32)
+  o->min_neighbors = 1;
+  o->search_scale_factor = 1.3f;
+  o->widen = 1;
+}
+
+// detectMultiScale's pyramid (oracle haar_scan) for every frame -> levels; returns false if a frame
+// is smaller than the cascade window at every scale (no levels)
+void build_levels(const ffd_engine* e, const std::vector<FrameIn>& in, const ffd_detect_options& o,
+                  std::vector<HaarFrame>& frames, std::vector<HaarLevel>& levels, int64_t sizes[4]) {
+  frames.clear();
+  levels.clear();
+  int64_t gray = 0, scaled = 0, sums = 0, res = 0;
+  const double sf = (double)o.search_scale_factor;
+  for (size_t k = 0; k < in.size(); k++) {
+    HaarFrame f;
+    std::memset(&f, 0, sizeof(f));
+    f.img_off = in[k].img_off;
+    f.gray_off = gray;
+    f.w = in[k].w;
+    f.h = in[k].h;
+    f.stride = in[k].stride;
+    f.level0 = (int)levels.size();
+    gray += align_up((int64_t)f.w * f.h, 256);
+    int rows = 0;
+    for (double factor = 1;; factor *= sf) {
+      const int winW = (int)std::nearbyint(e->haar_ww * factor), winH = (int)std::nearbyint(e->haar_wh * factor);
+      const int sW = (int)std::nearbyint(f.w / factor), sH = (int)std::nearbyint(f.h / factor);
+      const int pW = sW - e->haar_ww, pH = sH - e->haar_wh;
+      if (pW <= 0 || pH <= 0) break;
+      if (winW > f.w || winH > f.h) break;  // maxObjectSize = image size
+      if (winW < o.min_feature_size || winH < o.min_feature_size) continue;
+      HaarLevel L;
+      std::memset(&L, 0, sizeof(L));
+      L.gray_off = f.gray_off;
+      L.img_off = scaled;
+      L.sum_off = sums;
+      L.res_off = res;
+      L.factor = factor;
+      L.src_w = f.w;
+      L.src_h = f.h;
+      L.sw = sW;
+      L.sh = sH;
+      L.ystep = factor > 2. ? 1 : 2;
+      L.nx = (pW + L.ystep - 1) / L.ystep;
+      L.ny = (pH + L.ystep - 1) / L.ystep;
+      L.win_w = winW;
+      L.win_h = winH;
+      if (sW == f.w && sH == f.h) {
+        L.mode = 0;
+      } else {  // resize()'s INTER_LINEAR -> INTER_AREA 2x switch (oracle cv_resize)
+        L.scale_x = 1. / ((double)sW / f.w);
+        L.scale_y = 1. / ((double)sH / f.h);
+        const int ix = (int)std::nearbyint(L.scale_x), iy = (int)std::nearbyint(L.scale_y);
+        const bool area_fast = std::fabs(L.scale_x - ix) < DBL_EPSILON && std::fabs(L.scale_y - iy) < DBL_EPSILON;
+        L.mode = (area_fast && ix == 2 && iy == 2) ? 2 : 1;
+      }
+      int xv = 0;
+      while (xv <= sW - 16) xv += 16;
+      while (xv < sW - 4) xv += 4;
+      L.xv = xv;
+      L.row0 = rows;
+      L.frame = (int)k;
+      rows += L.ny;
+      scaled += align_up((int64_t)sW * sH, 256);
+      sums += align_up((int64_t)(sW + 1) * (sH + 1), 64);
+      res += align_up((int64_t)L.nx * L.ny, 256);
+      levels.push_back(L);
+    }
+    f.level1 = (int)levels.size();
+    f.rows = rows;
+    frames.push_back(f);
+  }
+  sizes[0] = gray;
+  sizes[1] = scaled;
+  sizes[2] = sums;
+  sizes[3] = res;
+}
+
+// Run the detector over frames already in device memory (e->main_stream()); boxes per frame out.
+ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vector<FrameIn>& in,
+                        const ffd_detect_options& o, std::vector<std::vector<ffd_rect>>& out,
+                        std::vector<std::vector<ffd_rect>>* raw) {
+  if (!e->have_haar) return fail(e, FFD_ERR_MODEL, "the model has no Haar cascade (convert it with ffd_convert)");
+  if (!(o.search_scale_factor > 1.f) || o.min_feature_size < 0)
+    return fail(e, FFD_ERR_INVALID_ARGUMENT, "search_scale_factor must be > 1 and min_feature_size >= 0");
+  out.assign(in.size(), {});
+  if (raw) raw->assign(in.size(), {});
+  if (in.empty()) return FFD_OK;
+  std::vector<HaarFrame> frames;
+  std::vector<HaarLevel> levels;
+  int64_t sz[4];
+  build_levels(e, in, o, frames, levels, sz);
+  hipStream_t s = e->main_stream();
+  const int nF = (int)frames.size(), nL = (int)levels.size();
+  const int cap = HAAR_MAX_CAND;
+  upload(e->det_frames, frames, s);
+  e->det_gray.ensure(sz[0]);
+  e->det_ncand.ensure((size_t)nF * 4);
+  e->det_nboxes.ensure((size_t)nF * 4);
+  e->det_cand.ensure((size_t)nF * cap * 16);
+  e->det_clsrect.ensure((size_t)nF * cap * 16);
+  e->det_clssum.ensure((size_t)nF * cap * 20);
+  e->det_boxes.ensure((size_t)nF * cap * 16);
+  if (nL > 0) {
+    upload(e->det_levels, levels, s);
+    e->det_scaled.ensure(sz[1]);
+    e->det_sum.ensure(sz[2] * 4);
+    e->det_sq.ensure(sz[2] * 8);
+    e->det_res.ensure(sz[3]);
+  }
+  int max_px = 0, max_lpx = 0, max_rows = 0, max_cols = 0, max_tiles = 0;
+  for (const auto& f : frames) max_px = std::max(max_px, f.w * f.h);
+  for (const auto& L : levels) {
+    max_lpx = std::max(max_lpx, L.sw * L.sh);
+    max_rows = std::max(max_rows, L.sh);
+    max_cols = std::max(max_cols, L.sw);
+    max_tiles = std::max(max_tiles, ((L.nx + 63) / 64) * ((L.ny + 3) / 4));
+  }
+  if (nL > 0) {
+    launch_haar_gray(e->det_frames.as<HaarFrame>(), nF, max_px, d_images, e->det_gray.as<uint8_t>(), s);
+    launch_haar_pyramid(e->det_levels.as<HaarLevel>(), nL, max_lpx, max_rows, max_cols, e->det_gray.as<uint8_t>(),
+                        e->det_scaled.as<uint8_t>(), e->det_sum.as<int32_t>(), e->det_sq.as<uint64_t>(), s);
+    launch_haar_cascade(e->det_levels.as<HaarLevel>(), nL, max_tiles, e->det_sum.as<int32_t>(),
+                        e->det_sq.as<uint64_t>(), e->haar_weak.as<HaarWeak>(), e->haar_stage.as<HaarStage>(),
+                        e->haar_stages, e->haar_ww, e->haar_wh, e->det_res.as<int8_t>(), s);
+  }
+  launch_haar_group(e->det_frames.as<HaarFrame>(), nF, nL > 0 ? e->det_levels.as<HaarLevel>() : nullptr,
+                    nL > 0 ? e->det_res.as<int8_t>() : nullptr, cap, e->det_cand.as<int4>(), e->det_ncand.as<int32_t>(),
+                    o.min_neighbors, o.widen, e->det_clsrect.as<int4>(), e->det_clssum.as<int>(),
+                    e->det_boxes.as<int4>(), e->det_nboxes.as<int32_t>(), s);
+  std::vector<int32_t> ncand(nF), nbox(nF);
+  HIP_CHECK(hipMemcpyAsync(ncand.data(), e->det_ncand.p, nF * 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(nbox.data(), e->det_nboxes.p, nF * 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  for (int k = 0; k < nF; k++)
+    if (ncand[k] > cap)
+      return fail(e, FFD_ERR_UNSUPPORTED, "frame " + std::to_string(k) + ": " + std::to_string(ncand[k]) +
+                                              " raw detections exceed the grouping capacity " + std::to_string(cap));
+  std::vector<int4> tmp;
+  for (int k = 0; k < nF; k++) {
+    tmp.resize(nbox[k]);
+    if (nbox[k] > 0)
+      HIP_CHECK(hipMemcpyAsync(tmp.data(), e->det_boxes.as<int4>() + (int64_t)k * cap, nbox[k] * sizeof(int4),
+                               hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    for (const int4& b : tmp) out[k].push_back(ffd_rect{b.x, b.y, b.z, b.w});
+    if (raw) {
+      tmp.resize(ncand[k]);
+      if (ncand[k] > 0)
+        HIP_CHECK(hipMemcpyAsync(tmp.data(), e->det_cand.as<int4>() + (int64_t)k * cap, ncand[k] * sizeof(int4),
+                                 hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      for (const int4& b : tmp) (*raw)[k].push_back(ffd_rect{b.x, b.y, b.z, b.w});
+    }
+  }
+  return FFD_OK;
+}
+
+// upload host frames into the engine's image staging buffer
+ffd_status upload_frames(ffd_engine* e, const ffd_image* imgs, int32_t n_img, std::vector<FrameIn>& in) {
+  if (n_img < 0 || (n_img > 0 && !imgs)) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad image list");
+  in.resize(n_img);
+  int64_t total = 0;
+  for (int i = 0; i < n_img; i++) {
+    if (!imgs[i].bgr || imgs[i].width <= 0 || imgs[i].height <= 0 || imgs[i].stride < 3 * imgs[i].width)
+      return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad image " + std::to_string(i));
+    in[i] = FrameIn{total, imgs[i].width, imgs[i].height, imgs[i].stride};
+    total += align_up((int64_t)imgs[i].stride * imgs[i].height, 256);
+  }
+  e->sync_all();  // the staging buffer may still be read by the previous batch
+  e->images.ensure(std::max<int64_t>(total, 256));
+  for (int i = 0; i < n_img; i++)
+    HIP_CHECK(hipMemcpyAsync(e->images.as<uint8_t>() + in[i].img_off, imgs[i].bgr,
+                             (size_t)imgs[i].stride * imgs[i].height, hipMemcpyHostToDevice, e->main_stream()));
+  return FFD_OK;
+}
+
+ffd_status copy_boxes(ffd_engine* e, const std::vector<std::vector<ffd_rect>>& det, ffd_rect* boxes, int32_t* box_img,
+                      int32_t max_boxes, int32_t* n_boxes) {
+  int32_t n = 0;
+  for (size_t k = 0; k < det.size(); k++)
+    for (const auto& b : det[k]) {
+      if (n < max_boxes) {
+        if (boxes) boxes[n] = b;
+        if (box_img) box_img[n] = (int32_t)k;
+      }
+      n++;
+    }
+  *n_boxes = n;
+  (void)e;
+  return FFD_OK;
+}
+
+template <class F> ffd_status guarded_d(ffd_engine* e, F&& fn) {
+  if (!e) return FFD_ERR_INVALID_ARGUMENT;
+  try {
+    HIP_CHECK(hipSetDevice(e->device));
+    return fn();
+  } catch (const HipError& x) {
+    return fail(e, FFD_ERR_DEVICE, x.what());
+  } catch (const std::bad_alloc&) {
+    return fail(e, FFD_ERR_OUT_OF_MEMORY, "host allocation failed");
+  } catch (const std::exception& x) {
+    return fail(e, FFD_ERR_INTERNAL, x.what());
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+void ffd_detect_options_init(ffd_detect_options* o) {
+  if (o) default_options(o);
+}
+
+ffd_status ffd_detect_faces(ffd_engine* e, const ffd_image* imgs, int32_t n_img, const ffd_detect_options* opt,
+                            ffd_rect* boxes, int32_t* box_img, int32_t max_boxes, int32_t* n_boxes) {
+  return guarded_d(e, [&]() -> ffd_status {
+    if (!n_boxes || max_boxes < 0 || (max_boxes > 0 && !boxes)) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    ffd_detect_options o;
+    default_options(&o);
+    if (opt) o = *opt;
+    std::vector<FrameIn> in;
+    ffd_status st = upload_frames(e, imgs, n_img, in);
+    if (st != FFD_OK) return st;
+    std::vector<std::vector<ffd_rect>> det;
+    st = detect_batch(e, e->images.as<uint8_t>(), in, o, det, nullptr);
+    if (st != FFD_OK) return st;
+    return copy_boxes(e, det, boxes, box_img, max_boxes, n_boxes);
+  });
+}
+
+ffd_status ffd_detect_faces_device(ffd_engine* e, const void* d_images, int64_t image_bytes, int32_t width,
+                                   int32_t height, int32_t stride, int32_t n_img, const ffd_detect_options* opt,
+                                   ffd_rect* boxes, int32_t* box_img, int32_t max_boxes, int32_t* n_boxes) {
+  return guarded_d(e, [&]() -> ffd_status {
+    if (!n_boxes || max_boxes < 0 || (max_boxes > 0 && !boxes) || n_img < 0 || (n_img > 0 && !d_images) ||
+        width <= 0 || height <= 0 || stride < 3 * width || image_bytes < (int64_t)stride * height)
+      return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    ffd_detect_options o;
+    default_options(&o);
+    if (opt) o = *opt;
+    std::vector<FrameIn> in(n_img);
+    for (int i = 0; i < n_img; i++) in[i] = FrameIn{(int64_t)i * image_bytes, width, height, stride};
+    std::vector<std::vector<ffd_rect>> det;
+    ffd_status st = detect_batch(e, static_cast<const uint8_t*>(d_images), in, o, det, nullptr);
+    if (st != FFD_OK) return st;
+    return copy_boxes(e, det, boxes, box_img, max_boxes, n_boxes);
+  });
+}
+
+ffd_status ffd_detect_candidates(ffd_engine* e, const ffd_image* img, const ffd_detect_options* opt, ffd_rect* raw,
+                                 int32_t cap, int32_t* n_raw) {
+  return guarded_d(e, [&]() -> ffd_status {
+    if (!img || !n_raw || cap < 0 || (cap > 0 && !raw)) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    ffd_detect_options o;
+    default_options(&o);
+    if (opt) o = *opt;
+    std::vector<FrameIn> in;
+    ffd_status st = upload_frames(e, img, 1, in);
+    if (st != FFD_OK) return st;
+    std::vector<std::vector<ffd_rect>> det, rw;
+    st = detect_batch(e, e->images.as<uint8_t>(), in, o, det, &rw);
+    if (st != FFD_OK) return st;
+    *n_raw = (int32_t)rw[0].size();
+    for (int i = 0; i < (int)rw[0].size() && i < cap; i++) raw[i] = rw[0][i];
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_analyze_images(ffd_engine* e, const ffd_image* imgs, int32_t n_img, const ffd_detect_options* opt,
+                              ffd_face* faces, int32_t* face_img, int32_t max_faces, int32_t* n_faces) {
+  return guarded_d(e, [&]() -> ffd_status {
+    if (!n_faces || max_faces < 0 || (max_faces > 0 && !faces)) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    ffd_detect_options o;
+    default_options(&o);
+    if (opt) o = *opt;
+    std::vector<FrameIn> in;
+    ffd_status st = upload_frames(e, imgs, n_img, in);
+    if (st != FFD_OK) return st;
+    std::vector<std::vector<ffd_rect>> det;
+    st = detect_batch(e, e->images.as<uint8_t>(), in, o, det, nullptr);
+    if (st != FFD_OK) return st;
+    // analyzeImage: analyzeFace on every detected box (FaceForest.cpp:174-180), as one GPU batch
+    std::vector<FaceDesc> fds;
+    std::vector<int32_t> owner;
+    for (size_t k = 0; k < det.size(); k++)
+      for (const auto& b : det[k]) {
+        FaceDesc f;
+        make_desc(e, in[k].img_off, in[k].w, in[k].h, in[k].stride, b, f);
+        fds.push_back(f);
+        owner.push_back((int32_t)k);
+      }
+    *n_faces = (int32_t)fds.size();
+    if (fds.empty()) return FFD_OK;
+    e->out.ensure(fds.size() * sizeof(FaceOut));
+    e->analyze(e->images.as<uint8_t>(), fds, e->out.as<FaceOut>());
+    const int32_t n = std::min<int32_t>((int32_t)fds.size(), max_faces);
+    if (n > 0)
+      HIP_CHECK(hipMemcpyAsync(faces, e->out.p, (size_t)n * sizeof(ffd_face), hipMemcpyDeviceToHost, e->main_stream()));
+    HIP_CHECK(hipStreamSynchronize(e->main_stream()));
+    for (int32_t i = 0; face_img && i < n; i++) face_img[i] = owner[i];
+    return FFD_OK;
+  });
+}
+
+}  // extern "C"

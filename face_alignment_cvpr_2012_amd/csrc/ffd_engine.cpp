@@ -365,6 +365,7 @@ void ffd_engine::load_model(const std::string& path) {
     }
     upload(mp_rec, rec, main_stream());
   }
+  load_cascade(m);
   HIP_CHECK(hipStreamSynchronize(main_stream()));
 }
 
@@ -566,15 +567,14 @@ ffd_status ffd_host::fail(ffd_engine* e, ffd_status s, const std::string& msg) {
   return s;
 }
 
-namespace {
-
 // Fill the per-face descriptor (geometry + resize parameters) for a box on an image.  Returns the
 // face's status: FFD_OK, FFD_ERR_INVALID_ARGUMENT (box outside the image or an empty scaled face:
 // the reference's cv::Mat ROI / resize assertions throw) or FFD_ERR_UNSUPPORTED (scaled face taller
 // than MAX_FACE_H).  A face on which no head-pose patch fits runs like the reference: 0/0 head pose
 // (NaN), trees 0..19 of forest 0, no votes, landmarks (0, 0); its channels are never read, so the
 // channel stage skips it.
-ffd_status make_desc(const ffd_engine* e, int64_t img_off, int iw, int ih, int stride, const ffd_rect& b, FaceDesc& f) {
+ffd_status ffd_host::make_desc(const ffd_engine* e, int64_t img_off, int iw, int ih, int stride, const ffd_rect& b,
+                               FaceDesc& f) {
   std::memset(&f, 0, sizeof(f));
   f.img_off = img_off;
   f.img_w = iw; f.img_h = ih; f.img_stride = stride;
@@ -610,6 +610,8 @@ ffd_status make_desc(const ffd_engine* e, int64_t img_off, int iw, int ih, int s
   f.reject = FFD_OK;
   return FFD_OK;
 }
+
+namespace {
 
 template <class F> ffd_status guarded(ffd_engine* e, F&& fn) {
   if (!e) return FFD_ERR_INVALID_ARGUMENT;

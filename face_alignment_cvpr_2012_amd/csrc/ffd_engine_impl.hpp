@@ -14,7 +14,12 @@
 
 #include "../../include/ffd.h"
 #include "ffd_device.hpp"
+#include "ffd_haar.hpp"
 #include "ffd_kernels.hpp"
+
+namespace ffd {
+class ModelFile;  // model_io.hpp
+}
 
 namespace ffd_host {
 
@@ -130,6 +135,13 @@ struct ffd_engine {
   bool vote_rec_compact = false;     // 32-B vote records (else 64-B), see load_model
   int vote_bias_x = 0, vote_bias_y = 0;
 
+  // Haar face detector (ffd_detect.cpp): the model's cascade, when it has one
+  bool have_haar = false;
+  int haar_ww = 0, haar_wh = 0, haar_stages = 0;
+  DevBuf haar_weak, haar_stage;
+  DevBuf det_frames, det_levels, det_gray, det_scaled, det_sum, det_sq, det_res, det_cand, det_ncand, det_clsrect,
+      det_clssum, det_boxes, det_nboxes;
+
   std::vector<std::unique_ptr<Workspace>> ws;
   DevBuf images, out, scratch_a, scratch_b, scratch_c;  // host-API staging (ws[0] stream)
   int last_ws = -1;
@@ -202,6 +214,7 @@ struct ffd_engine {
   }
 
   void load_model(const std::string& path);
+  void load_cascade(const ffd::ModelFile& m);  // ffd_detect.cpp
   void build_gabor();
   // FFD patch-grid step along y: the reference has one step for both axes (step_size_y == 0)
   int mp_step_y() const { return desc.mp_option.step_size_y > 0 ? desc.mp_option.step_size_y : desc.mp_option.step_size; }
@@ -251,6 +264,8 @@ ffd_status fail(ffd_engine* e, ffd_status s, const std::string& msg);
 // analyzeFace over host images: upload, descriptors, pipeline; results left in d_out (device)
 ffd_status analyze_host(ffd_engine* e, const ffd_image* imgs, int32_t n_img, const ffd_rect* boxes,
                         const int32_t* box_img, int32_t n_faces, void* d_out);
+// per-face descriptor of a box on an image (ffd_engine.cpp); returns the face's status
+ffd_status make_desc(const ffd_engine* e, int64_t img_off, int iw, int ih, int stride, const ffd_rect& b, FaceDesc& f);
 // the engine's per-rank RCCL communicator, if it joined one (ffd_group.cpp)
 void release_comm(const ffd_engine* e);
 }  // namespace ffd_host

@@ -1,0 +1,462 @@
+// ffd_haar.hip — gfx950 Haar face detector: FaceForest::detectFace (src/FaceForest.cpp:136-159),
+// i.e. OpenCV 2.4.9 CascadeClassifier::detectMultiScale(frame, boxes, 1.3, 1, 0, Size(30, 30)) on the
+// new-format stump cascade data/haarcascade_frontalface_alt.xml, then detectFace's widening.
+// Bit-exact with the CPU restatement oracle/ffd_oracle.cpp (haar_scan / haar_group / widen_box),
+// which states the OpenCV semantics followed (parity with OpenCV itself unpinned: no OpenCV here).
+//
+// A batch of frames runs as one pass of six launches over a host-built level table (one level per
+// (frame, pyramid scale) that detectMultiScale scans):
+//   k_haar_gray      cvtColor(BGR2GRAY) of each frame, once per frame
+//   k_haar_resize    the pyramid level: resize(INTER_LINEAR) to cvRound(cols / f) x cvRound(rows / f)
+//   k_haar_rows      per level row: u32 prefix sums of v and v^2 (a wave per row, DPP scans)
+//   k_haar_cols      per level column: the running column sums -> integral sum (i32) / sqsum (u64)
+//   k_haar_cascade   a thread per scan position (x, y on the yStep grid): predictOrderedStump over the
+//                    22 stages, weak classifiers read as wave-uniform scalar loads; result per position
+//   k_haar_collect   a workgroup per frame: each thread walks one scan row applying the invoker's
+//                    skip rule (a stage-0 reject skips the next x) and emits the candidates in scan
+//                    order (block prefix sums)
+//   k_haar_group     a workgroup per frame: groupRectangles (connected components of SimilarRects by
+//                    min-label propagation = cv::partition's classes, numbered by smallest member),
+//                    averages, the small-inside-large filter, detectFace's widening + intersect
+// Integer-exact integrals (sum < 2^31, sqsum < 2^53 as u64), fp32 / fp64 evaluated in the
+// restatement's operation order (-ffp-contract=off), so every position's result is identical.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "ffd_haar.hpp"
+
+namespace ffd {
+
+namespace {
+
+__device__ __forceinline__ int hsat_u8(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+__device__ __forceinline__ int hsat_s16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+__device__ __forceinline__ int hround(float v) {  // cvRound(float)
+  if (!(v >= -2147483648.0f && v < 2147483648.0f)) return (int)0x80000000;
+  return (int)__builtin_rintf(v);
+}
+__device__ __forceinline__ int hround_d(double v) {  // cvRound(double)
+  if (!(v >= -2147483648.0 && v < 2147483648.0)) return (int)0x80000000;
+  return (int)__builtin_rint(v);
+}
+
+// inclusive prefix sum over a wave (DPP row shifts + row broadcasts); integer adds
+__device__ __forceinline__ uint32_t wave_scan_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+  return v;
+}
+
+// ---------------------------------------------------------------------------- gray ----
+__global__ __launch_bounds__(256) void k_haar_gray(const HaarFrame* __restrict__ frames,
+                                                   const uint8_t* __restrict__ images, uint8_t* __restrict__ gray) {
+  const HaarFrame f = frames[blockIdx.y];
+  const uint8_t* img = images + f.img_off;
+  uint8_t* g = gray + f.gray_off;
+  const int n = f.w * f.h;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int y = i / f.w, x = i - y * f.w;
+    const uint8_t* p = img + (int64_t)y * f.stride + 3 * x;
+    g[i] = (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14);
+  }
+}
+
+// ------------------------------------------------------------------------ resize ----
+// resize(INTER_LINEAR) 8U as oracle cv_resize (OpenCV 2.4.9 fixed point: 11-bit horizontal
+// coefficients, SSE2 vertical pass on columns [0, xv), scalar tail); mode 0 copy, 2 area 2x.
+__global__ __launch_bounds__(256) void k_haar_resize(const HaarLevel* __restrict__ levels,
+                                                     const uint8_t* __restrict__ gray, uint8_t* __restrict__ scaled) {
+  const HaarLevel L = levels[blockIdx.y];
+  const uint8_t* src = gray + L.gray_off;
+  uint8_t* dst = scaled + L.img_off;
+  const int sw = L.src_w, sh = L.src_h, n = L.sw * L.sh;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int dy = i / L.sw, dx = i - dy * L.sw;
+    int v;
+    if (L.mode == 0) {
+      v = src[(int64_t)dy * sw + dx];
+    } else if (L.mode == 2) {
+      const uint8_t* s0 = src + (int64_t)(2 * dy) * sw + 2 * dx;
+      v = (s0[0] + s0[1] + s0[sw] + s0[sw + 1] + 2) >> 2;
+    } else {
+      float fx = (float)((dx + 0.5) * L.scale_x - 0.5);
+      int sx = (int)floorf(fx);
+      fx -= sx;
+      if (sx < 0) fx = 0, sx = 0;
+      bool right = false;
+      if (sx + 1 >= sw) {
+        right = true;
+        if (sx >= sw - 1) fx = 0, sx = sw - 1;
+      }
+      const int a0 = hsat_s16(hround((1.f - fx) * 2048.f)), a1 = hsat_s16(hround(fx * 2048.f));
+      float fy = (float)((dy + 0.5) * L.scale_y - 0.5);
+      const int sy = (int)floorf(fy);
+      fy -= sy;
+      const int b0 = hsat_s16(hround((1.f - fy) * 2048.f)), b1 = hsat_s16(hround(fy * 2048.f));
+      const int y0 = min(max(sy, 0), sh - 1), y1 = min(max(sy + 1, 0), sh - 1);
+      const uint8_t* r0p = src + (int64_t)y0 * sw;
+      const uint8_t* r1p = src + (int64_t)y1 * sw;
+      int r0, r1;
+      if (right) {
+        r0 = r0p[sx] * 2048;
+        r1 = r1p[sx] * 2048;
+      } else {
+        r0 = r0p[sx] * a0 + r0p[sx + 1] * a1;
+        r1 = r1p[sx] * a0 + r1p[sx + 1] * a1;
+      }
+      if (dx < L.xv) {
+        const int s0 = max(-32768, min(32767, r0 >> 4)), s1 = max(-32768, min(32767, r1 >> 4));
+        int m = max(-32768, min(32767, ((s0 * b0) >> 16) + ((s1 * b1) >> 16)));
+        m = max(-32768, min(32767, m + 2)) >> 2;
+        v = hsat_u8(m);
+      } else {
+        v = hsat_u8((b0 * r0 + b1 * r1 + (1 << 21)) >> 22);
+      }
+    }
+    dst[i] = (uint8_t)v;
+  }
+}
+
+// ---------------------------------------------------------------------- integrals ----
+// Pass 1: one wave per (level, row y): prefix sums of v and v*v along the row (both < 2^32 for rows
+// up to 2^16 pixels) into sum[y + 1][x + 1] / sq[y + 1][x + 1]; column 0 and row 0 are zeroed here.
+__global__ __launch_bounds__(256) void k_haar_rows(const HaarLevel* __restrict__ levels,
+                                                   const uint8_t* __restrict__ scaled, int32_t* __restrict__ sum,
+                                                   uint64_t* __restrict__ sq) {
+  const HaarLevel L = levels[blockIdx.y];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int P = L.sw + 1;
+  int32_t* S = sum + L.sum_off;
+  uint64_t* Q = sq + L.sum_off;
+  for (int y = blockIdx.x * 4 + wv; y <= L.sh; y += gridDim.x * 4) {
+    if (y == 0) {
+      for (int x = lane; x < P; x += 64) { S[x] = 0; Q[x] = 0; }
+      continue;
+    }
+    const uint8_t* row = scaled + L.img_off + (int64_t)(y - 1) * L.sw;
+    int32_t* so = S + (int64_t)y * P;
+    uint64_t* qo = Q + (int64_t)y * P;
+    if (lane == 0) { so[0] = 0; qo[0] = 0; }
+    uint32_t cs = 0, cq = 0;
+    for (int x0 = 0; x0 < L.sw; x0 += 64) {
+      const int x = x0 + lane;
+      const uint32_t v = x < L.sw ? row[x] : 0u;
+      const uint32_t ps = wave_scan_u32(v), pq = wave_scan_u32(v * v);
+      if (x < L.sw) { so[x + 1] = (int32_t)(cs + ps); qo[x + 1] = (uint64_t)(cq + pq); }
+      cs += (uint32_t)__builtin_amdgcn_readlane((int)ps, 63);
+      cq += (uint32_t)__builtin_amdgcn_readlane((int)pq, 63);
+    }
+  }
+}
+
+// Pass 2: one thread per (level, column x >= 1): running sums down the rows, 8 rows' loads in flight.
+__global__ __launch_bounds__(256) void k_haar_cols(const HaarLevel* __restrict__ levels, int32_t* __restrict__ sum,
+                                                   uint64_t* __restrict__ sq) {
+  const HaarLevel L = levels[blockIdx.y];
+  const int x = 1 + blockIdx.x * 256 + threadIdx.x;
+  if (x > L.sw) return;
+  const int P = L.sw + 1;
+  int32_t* S = sum + L.sum_off + x;
+  uint64_t* Q = sq + L.sum_off + x;
+  int32_t as = 0;
+  uint64_t aq = 0;
+  for (int y0 = 1; y0 <= L.sh; y0 += 8) {
+    int32_t vs[8];
+    uint64_t vq[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      if (y0 + k <= L.sh) { vs[k] = S[(int64_t)(y0 + k) * P]; vq[k] = Q[(int64_t)(y0 + k) * P]; }
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      if (y0 + k <= L.sh) {
+        as += vs[k];
+        aq += vq[k];
+        S[(int64_t)(y0 + k) * P] = as;
+        Q[(int64_t)(y0 + k) * P] = aq;
+      }
+  }
+}
+
+// ------------------------------------------------------------------------ cascade ----
+// One thread per scan position of a level: 64 x 4 positions per workgroup (x fastest, so a wave's
+// corner reads are one row of the integral).  Result: 1 (face) or -stage (stage 0 -> 0), as int8.
+__global__ __launch_bounds__(256) void k_haar_cascade(const HaarLevel* __restrict__ levels,
+                                                      const int32_t* __restrict__ sum, const uint64_t* __restrict__ sq,
+                                                      const HaarWeak* __restrict__ weak,
+                                                      const HaarStage* __restrict__ stages, int n_stages, int ww,
+                                                      int wh, int8_t* __restrict__ result) {
+  const HaarLevel L = levels[blockIdx.y];
+  const int tiles_x = (L.nx + 63) >> 6;
+  const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
+  const int ix = tx * 64 + (threadIdx.x & 63), iy = ty * 4 + (threadIdx.x >> 6);
+  if (iy >= L.ny) return;
+  if (ix >= L.nx) return;
+  const int x = ix * L.ystep, y = iy * L.ystep;
+  const int P = L.sw + 1;
+  const int32_t* S = sum + L.sum_off + (int64_t)y * P + x;
+  const uint64_t* Q = sq + L.sum_off + (int64_t)y * P + x;
+  // setWindow: normrect (1, 1, ww - 2, wh - 2)
+  const int a = P + 1, b = a + (ww - 2), c = (wh - 1) * P + 1, d = c + (ww - 2);
+  const int valsum = S[a] - S[b] - S[c] + S[d];
+  const double valsq = (double)(int64_t)(Q[a] - Q[b] - Q[c] + Q[d]);
+  double nf = (double)((ww - 2) * (wh - 2)) * valsq - (double)valsum * (double)valsum;
+  nf = nf > 0. ? __builtin_sqrt(nf) : 1.;
+  const double vnf = 1. / nf;
+  int res = 1;
+  for (int s = 0; s < n_stages; s++) {
+    const HaarStage st = stages[s];
+    double acc = 0.0;
+    for (int i = st.first; i < st.first + st.ntrees; i++) {
+      const HaarWeak w = weak[i];
+      auto rs = [&](uint32_t r) {
+        const int rx = r & 255u, ry = (r >> 8) & 255u, rw = (r >> 16) & 255u, rh = r >> 24;
+        const int p0 = ry * P + rx, p2 = p0 + rh * P;
+        return S[p0] - S[p0 + rw] - S[p2] + S[p2 + rw];
+      };
+      float ret = w.w0 * (float)rs(w.r0) + w.w1 * (float)rs(w.r1);
+      if (w.w2 != 0.0f) ret += w.w2 * (float)rs(w.r2);
+      const float value = (float)((double)ret * vnf);
+      acc += (double)(value < w.thr ? w.leaf0 : w.leaf1);
+    }
+    if (acc < (double)st.thr) { res = -s; break; }
+  }
+  result[L.res_off + (int64_t)iy * L.nx + ix] = (int8_t)res;
+}
+
+// ------------------------------------------------------------------------ collect ----
+constexpr int HC_THREADS = 1024;
+
+__device__ __forceinline__ int block_excl_scan(int v, int* sh, int& total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int incl = (int)wave_scan_u32((uint32_t)v);
+  if (lane == 63) sh[wv] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int w = 0; w < HC_THREADS / 64; w++) { int t = sh[w]; sh[w] = acc; acc += t; }
+    sh[HC_THREADS / 64] = acc;
+  }
+  __syncthreads();
+  const int r = sh[wv] + incl - v;
+  total = sh[HC_THREADS / 64];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(HC_THREADS) void k_haar_collect(const HaarFrame* __restrict__ frames,
+                                                              const HaarLevel* __restrict__ levels,
+                                                              const int8_t* __restrict__ result, int cap,
+                                                              int4* __restrict__ cand, int32_t* __restrict__ n_cand) {
+  __shared__ int sh[HC_THREADS / 64 + 1];
+  const HaarFrame f = frames[blockIdx.x];
+  int base = 0;
+  for (int r0 = 0; r0 < f.rows; r0 += HC_THREADS) {
+    const int r = r0 + threadIdx.x;
+    int lv = -1, iy = 0;
+    if (r < f.rows) {
+      lv = f.level0;
+      while (lv + 1 < f.level1 && levels[lv + 1].row0 <= r) lv++;
+      iy = r - levels[lv].row0;
+    }
+    // invoker scan of one row: x steps by yStep, a stage-0 reject (result 0) skips the next x
+    auto walk = [&](bool emit, int at) {
+      int n = 0;
+      if (lv < 0) return 0;
+      const HaarLevel& L = levels[lv];
+      const int8_t* row = result + L.res_off + (int64_t)iy * L.nx;
+      for (int ix = 0; ix < L.nx;) {
+        const int v = row[ix];
+        if (v > 0) {
+          if (emit && at + n < cap) {
+            const int x = ix * L.ystep, y = iy * L.ystep;
+            cand[(int64_t)blockIdx.x * cap + at + n] =
+                make_int4(hround_d(x * L.factor), hround_d(y * L.factor), L.win_w, L.win_h);
+          }
+          n++;
+        }
+        ix += v == 0 ? 2 : 1;
+      }
+      return n;
+    };
+    const int cnt = walk(false, 0);
+    int tot;
+    const int off = block_excl_scan(cnt, sh, tot);
+    walk(true, base + off);
+    base += tot;
+  }
+  if (threadIdx.x == 0) n_cand[blockIdx.x] = base;
+}
+
+// -------------------------------------------------------------------------- group ----
+__device__ __forceinline__ bool similar_rects(int4 a, int4 b, double eps) {  // cv::SimilarRects
+  const double delta = eps * (double)(min(a.z, b.z) + min(a.w, b.w)) * 0.5;
+  return (double)abs(a.x - b.x) <= delta && (double)abs(a.y - b.y) <= delta &&
+         (double)abs(a.x + a.z - b.x - b.z) <= delta && (double)abs(a.y + a.w - b.y - b.w) <= delta;
+}
+
+__device__ __forceinline__ int ld_agent(const int* p) {  // coherent read of a value other waves wrote atomically
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(HC_THREADS) void k_haar_group(const HaarFrame* __restrict__ frames, int cap,
+                                                            const int4* __restrict__ cand,
+                                                            const int32_t* __restrict__ n_cand, int min_neighbors,
+                                                            int widen, int4* __restrict__ cls_rect,
+                                                            int* __restrict__ cls_sum, int4* __restrict__ boxes,
+                                                            int32_t* __restrict__ n_boxes) {
+  __shared__ int label[HAAR_MAX_CAND];
+  __shared__ int sh[HC_THREADS / 64 + 1];
+  __shared__ int changed;
+  const HaarFrame f = frames[blockIdx.x];
+  const int N = min(n_cand[blockIdx.x], cap);
+  const int4* R = cand + (int64_t)blockIdx.x * cap;
+  int4* out = boxes + (int64_t)blockIdx.x * cap;
+  const double eps = 0.2;  // detectMultiScale GROUP_EPS
+  if (min_neighbors <= 0) {  // groupRectangles returns the list unchanged
+    for (int i = threadIdx.x; i < N; i += HC_THREADS) out[i] = R[i];
+    if (threadIdx.x == 0) n_boxes[blockIdx.x] = N;
+    return;
+  }
+  // connected components of SimilarRects: every label converges to its component's smallest index
+  for (int i = threadIdx.x; i < N; i += HC_THREADS) label[i] = i;
+  for (;;) {
+    if (threadIdx.x == 0) changed = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < N; i += HC_THREADS) {
+      const int4 ri = R[i];
+      int m = label[i];
+      for (int j = 0; j < N; j++)
+        if (j != i && label[j] < m && similar_rects(ri, R[j], eps)) m = label[j];
+      if (m < label[i]) { label[i] = m; changed = 1; }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < N; i += HC_THREADS) {  // pointer jumping (labels only decrease)
+      int l = label[i];
+      while (label[l] != l) l = label[l];
+      label[i] = l;
+    }
+    __syncthreads();
+    if (!changed) break;
+    __syncthreads();
+  }
+  // class ids in order of their smallest member (cv::partition's numbering)
+  int* csum = cls_sum + (int64_t)blockIdx.x * cap * 5;  // per class: x, y, w, h sums, count
+  int ncls = 0;
+  for (int i0 = 0; i0 < N; i0 += HC_THREADS) {
+    const int i = i0 + threadIdx.x;
+    const int is_root = (i < N && label[i] == i) ? 1 : 0;
+    int tot;
+    const int id = block_excl_scan(is_root, sh, tot) + ncls;
+    if (is_root) {
+      label[i] = -1 - id;  // roots now hold ~class id (members still point at the root index)
+      for (int k = 0; k < 5; k++) __hip_atomic_store(&csum[id * 5 + k], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    ncls += tot;
+  }
+  __threadfence();
+  __syncthreads();
+  for (int i = threadIdx.x; i < N; i += HC_THREADS) {
+    const int l = label[i];
+    const int id = l < 0 ? -1 - l : -1 - label[l];
+    const int4 r = R[i];
+    atomicAdd(&csum[id * 5 + 0], r.x);
+    atomicAdd(&csum[id * 5 + 1], r.y);
+    atomicAdd(&csum[id * 5 + 2], r.z);
+    atomicAdd(&csum[id * 5 + 3], r.w);
+    atomicAdd(&csum[id * 5 + 4], 1);
+  }
+  __threadfence();
+  __syncthreads();
+  int4* crect = cls_rect + (int64_t)blockIdx.x * cap;
+  for (int c = threadIdx.x; c < ncls; c += HC_THREADS) {
+    const float s = 1.f / (float)ld_agent(&csum[c * 5 + 4]);
+    int* cr = reinterpret_cast<int*>(&crect[c]);
+    for (int k = 0; k < 4; k++)
+      __hip_atomic_store(&cr[k], hround((float)ld_agent(&csum[c * 5 + k]) * s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __threadfence();
+  __syncthreads();
+  auto class_rect = [&](int c) {
+    const int* cr = reinterpret_cast<const int*>(&crect[c]);
+    return make_int4(ld_agent(&cr[0]), ld_agent(&cr[1]), ld_agent(&cr[2]), ld_agent(&cr[3]));
+  };
+  // small-inside-large filter, output in class order
+  int nout = 0;
+  for (int c0 = 0; c0 < ncls; c0 += HC_THREADS) {
+    const int c = c0 + threadIdx.x;
+    int keep = 0;
+    int4 r1 = make_int4(0, 0, 0, 0);
+    if (c < ncls) {
+      r1 = class_rect(c);
+      const int n1 = ld_agent(&csum[c * 5 + 4]);
+      if (n1 > min_neighbors) {
+        keep = 1;
+        for (int j = 0; j < ncls; j++) {
+          const int n2 = ld_agent(&csum[j * 5 + 4]);
+          if (j == c || n2 <= min_neighbors) continue;
+          const int4 r2 = class_rect(j);
+          const int dx = hround_d(r2.z * eps), dy = hround_d(r2.w * eps);
+          if (r1.x >= r2.x - dx && r1.y >= r2.y - dy && r1.x + r1.z <= r2.x + r2.z + dx &&
+              r1.y + r1.w <= r2.y + r2.w + dy && (n2 > max(3, n1) || n1 < 3)) {
+            keep = 0;
+            break;
+          }
+        }
+      }
+    }
+    int tot;
+    const int at = block_excl_scan(keep, sh, tot) + nout;
+    if (keep) {
+      if (widen) {  // detectFace (FaceForest.cpp:148-158) + intersect (face_utils.cpp:328-346)
+        const int ox = (int)(r1.z * 0.05), oy = (int)(r1.z * 0.15);
+        const int x1 = r1.x - ox, y1 = r1.y, w1 = r1.z + ox * 2, h1 = r1.w + oy * 2;
+        int4 r;
+        r.x = x1 < 0 ? 0 : x1;
+        r.y = y1 < 0 ? 0 : y1;
+        r.z = (x1 + w1 < f.w ? x1 + w1 : f.w) - r.x;
+        r.w = (y1 + h1 < f.h ? y1 + h1 : f.h) - r.y;
+        if (r.z <= 0 || r.w <= 0) r = make_int4(0, 0, 0, 0);
+        r1 = r;
+      }
+      out[at] = r1;
+    }
+    nout += tot;
+  }
+  if (threadIdx.x == 0) n_boxes[blockIdx.x] = nout;
+}
+
+}  // namespace
+
+void launch_haar_gray(const HaarFrame* frames, int n_frames, int max_pixels, const uint8_t* images, uint8_t* gray,
+                      hipStream_t s) {
+  const int blocks = std::min(1024, (max_pixels + 255) / 256);
+  k_haar_gray<<<dim3(blocks, n_frames), 256, 0, s>>>(frames, images, gray);
+}
+
+void launch_haar_pyramid(const HaarLevel* levels, int n_levels, int max_pixels, int max_rows, int max_cols,
+                         const uint8_t* gray, uint8_t* scaled, int32_t* sum, uint64_t* sq, hipStream_t s) {
+  k_haar_resize<<<dim3(std::min(512, (max_pixels + 255) / 256), n_levels), 256, 0, s>>>(levels, gray, scaled);
+  k_haar_rows<<<dim3(std::min(256, (max_rows + 1 + 3) / 4), n_levels), 256, 0, s>>>(levels, scaled, sum, sq);
+  k_haar_cols<<<dim3((max_cols + 255) / 256, n_levels), 256, 0, s>>>(levels, sum, sq);
+}
+
+void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint64_t* sq,
+                         const HaarWeak* weak, const HaarStage* stages, int n_stages, int ww, int wh, int8_t* result,
+                         hipStream_t s) {
+  k_haar_cascade<<<dim3(max_tiles, n_levels), 256, 0, s>>>(levels, sum, sq, weak, stages, n_stages, ww, wh, result);
+}
+
+void launch_haar_group(const HaarFrame* frames, int n_frames, const HaarLevel* levels, const int8_t* result, int cap,
+                       int4* cand, int32_t* n_cand, int min_neighbors, int widen, int4* cls_rect, int* cls_sum,
+                       int4* boxes, int32_t* n_boxes, hipStream_t s) {
+  k_haar_collect<<<n_frames, HC_THREADS, 0, s>>>(frames, levels, result, cap, cand, n_cand);
+  k_haar_group<<<n_frames, HC_THREADS, 0, s>>>(frames, cap, cand, n_cand, min_neighbors, widen, cls_rect, cls_sum,
+                                              boxes, n_boxes);
+}
+
+}  // namespace ffd

@@ -1,0 +1,67 @@
+// ffd_haar.hpp — data layout and launchers of the Haar face detector (ffd_haar.hip), shared by the
+// kernels and the host orchestration (ffd_detect.cpp).  SURVEY.md §8(f) #1: FaceForest::detectFace,
+// /root/reference/src/FaceForest.cpp:136-159.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+namespace ffd {
+
+constexpr int HAAR_MAX_CAND = 8192;  // raw candidates per frame the grouping kernel holds (LDS labels)
+
+// One frame of a detection batch.
+struct HaarFrame {
+  int64_t img_off;   // BGR bytes in the image buffer
+  int64_t gray_off;  // its gray copy (pitch w)
+  int32_t w, h, stride;
+  int32_t level0, level1;  // its pyramid levels [level0, level1)
+  int32_t rows;            // scan rows over all its levels
+};
+
+// One pyramid level (frame, scale factor) that detectMultiScale scans.
+struct HaarLevel {
+  int64_t gray_off;  // source gray frame (pitch src_w)
+  int64_t img_off;   // scaled image (pitch sw)
+  int64_t sum_off;   // integral sum / sqsum ((sh + 1) x (sw + 1))
+  int64_t res_off;   // per-position results (ny x nx, int8)
+  double factor, scale_x, scale_y;
+  int32_t src_w, src_h, sw, sh;
+  int32_t ystep, nx, ny, win_w, win_h;
+  int32_t mode, xv;  // resize: 0 copy, 1 bilinear, 2 area 2x; SSE2 column bound
+  int32_t row0;      // first scan row of this level within its frame
+  int32_t frame;
+};
+
+// One stump weak classifier with its Haar feature (HaarEvaluator::Feature + DTreeNode + 2 leaves).
+struct HaarWeak {
+  uint32_t r0, r1, r2;  // rect x | y << 8 | w << 16 | h << 24
+  float w0, w1, w2;     // rect weights (w2 == 0: two-rectangle feature)
+  float thr, leaf0, leaf1;
+  uint32_t pad[3];
+};
+static_assert(sizeof(HaarWeak) == 48, "HaarWeak is 48 bytes");
+
+struct HaarStage {
+  int32_t first, ntrees;
+  float thr;  // (float)stageThreshold - 1e-5f (CascadeClassifier::Data::read THRESHOLD_EPS)
+  int32_t pad;
+};
+
+void launch_haar_gray(const HaarFrame* frames, int n_frames, int max_pixels, const uint8_t* images, uint8_t* gray,
+                      hipStream_t s);
+void launch_haar_pyramid(const HaarLevel* levels, int n_levels, int max_pixels, int max_rows, int max_cols,
+                         const uint8_t* gray, uint8_t* scaled, int32_t* sum, uint64_t* sq, hipStream_t s);
+// max_tiles: the largest level's ceil(nx / 64) * ceil(ny / 4)
+void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint64_t* sq,
+                         const HaarWeak* weak, const HaarStage* stages, int n_stages, int ww, int wh, int8_t* result,
+                         hipStream_t s);
+// candidates (cap per frame) in scan order, then grouped + widened boxes (cap per frame);
+// cls_rect: cap int4 per frame, cls_sum: 5 cap ints per frame (scratch)
+void launch_haar_group(const HaarFrame* frames, int n_frames, const HaarLevel* levels, const int8_t* result, int cap,
+                       int4* cand, int32_t* n_cand, int min_neighbors, int widen, int4* cls_rect, int* cls_sum,
+                       int4* boxes, int32_t* n_boxes, hipStream_t s);
+
+}  // namespace ffd

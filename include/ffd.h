@@ -223,6 +223,36 @@ ffd_status ffd_comm_id(uint8_t* id /* FFD_COMM_ID_BYTES */);
 ffd_status ffd_engine_join(ffd_engine* engine, const uint8_t* id, int32_t n_ranks, int32_t rank);
 ffd_status ffd_gather_faces(ffd_engine* engine, const void* d_local, int32_t n_per_rank, void* d_root, int32_t root);
 
+/* ---- Haar face detector and the frame-level API ---------------------------
+ * ffd_detect_faces      FaceForest::detectFace   src/FaceForest.cpp:136-159: the model's Haar cascade
+ *                       (ffd_convert reads data/haarcascade_frontalface_alt.xml) run as OpenCV 2.4.9's
+ *                       CascadeClassifier::detectMultiScale(frame, boxes, search_scale_factor,
+ *                       min_neighbors, 0, Size(min_feature_size, min_feature_size)), then the 5 % / 15 %
+ *                       widening clipped to the frame; on the GPU, every frame of the batch at once.
+ * ffd_analyze_images    FaceForest::analyzeImage src/FaceForest.cpp:161-181: detect, then analyzeFace on
+ *                       every box (all boxes of all frames as one batch); faces in frame order, then
+ *                       detection order; face_img[i] = the frame of face i.
+ * Boxes beyond max_boxes / max_faces are counted in *n_boxes / *n_faces but not written.
+ * Parity: bit-exact with the CPU restatement (oracle/); with OpenCV itself unpinned (no OpenCV here). */
+typedef struct {
+  int32_t min_feature_size;    /* FaceDetectionOption (include/FaceForest.hpp:21-32): 30 */
+  int32_t min_neighbors;       /* 1 (0: the raw, ungrouped detections) */
+  float search_scale_factor;   /* 1.3f */
+  int32_t widen;               /* 1: detectFace's enlargement + clip; 0: detectMultiScale's boxes */
+} ffd_detect_options;
+void ffd_detect_options_init(ffd_detect_options* opt);
+ffd_status ffd_detect_faces(ffd_engine* engine, const ffd_image* imgs, int32_t n_img, const ffd_detect_options* opt,
+                            ffd_rect* boxes, int32_t* box_img, int32_t max_boxes, int32_t* n_boxes);
+/* frames already in HBM: n_img frames of one size, image_bytes apart */
+ffd_status ffd_detect_faces_device(ffd_engine* engine, const void* d_images, int64_t image_bytes, int32_t width,
+                                   int32_t height, int32_t stride, int32_t n_img, const ffd_detect_options* opt,
+                                   ffd_rect* boxes, int32_t* box_img, int32_t max_boxes, int32_t* n_boxes);
+ffd_status ffd_analyze_images(ffd_engine* engine, const ffd_image* imgs, int32_t n_img, const ffd_detect_options* opt,
+                              ffd_face* faces, int32_t* face_img, int32_t max_faces, int32_t* n_faces);
+/* test hook: detectMultiScale's ungrouped candidates of one frame, in scan order */
+ffd_status ffd_detect_candidates(ffd_engine* engine, const ffd_image* img, const ffd_detect_options* opt,
+                                 ffd_rect* raw, int32_t cap, int32_t* n_raw);
+
 /* ---- Boost text-archive writer ------------------------------------------
  * Replaces Tree<S>::save (include/Tree.hpp:239-256: boost::archive::text_oarchive << *this) and the
  * serializers it runs (Tree.hpp:336-343, Constants.hpp:44-59, TreeNode.hpp:150-164,

@@ -68,6 +68,9 @@ def lib():
             ctypes.POINTER(ctypes.c_float)] * 2
         L.oracle_estimate_facial_features.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 6 + [
             ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+        L.oracle_detect_faces.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 5 + [ctypes.c_float, ctypes.c_int32,
+            ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), ctypes.c_void_p, ctypes.c_int32,
+            ctypes.POINTER(ctypes.c_int32)]
         _lib = L
     return _lib
 
@@ -142,6 +145,27 @@ def bgr2gray(img):
     out = np.zeros((h, w), np.uint8)
     lib().oracle_bgr2gray(img.ctypes.data, w, h, img.strides[0], out.ctypes.data)
     return out
+
+
+def detect_faces(img, min_size=30, min_neighbors=1, scale_factor=1.3, widen=True, raw=False):
+    """FaceForest::detectFace (src/FaceForest.cpp:136-159) restated: (boxes [n, 4] x, y, w, h) and,
+    with raw=True, also the ungrouped candidates in scan order.  Parity with OpenCV unpinned."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape[:2]
+    cap = 4096
+    for _ in range(3):
+        boxes = np.zeros((cap, 4), np.int32)
+        rawv = np.zeros((cap * 8, 4), np.int32)
+        n, nr = ctypes.c_int32(), ctypes.c_int32()
+        if lib().oracle_detect_faces(img.ctypes.data, w, h, img.strides[0], min_size, min_neighbors,
+                                     scale_factor, int(widen), boxes.ctypes.data, cap, ctypes.byref(n),
+                                     rawv.ctypes.data, cap * 8, ctypes.byref(nr)) != 0:
+            raise RuntimeError(lib().oracle_last_error().decode())
+        if n.value <= cap and nr.value <= cap * 8:
+            break
+        cap = max(n.value, nr.value // 8 + 1)
+    out = boxes[: n.value].copy()
+    return (out, rawv[: nr.value].copy()) if raw else out
 
 
 def resize(src, dw, dh):

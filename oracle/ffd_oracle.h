@@ -69,6 +69,14 @@ int oracle_estimate_facial_features(const uint32_t* channels, int32_t W, int32_t
 int oracle_face_geometry(int32_t bw, int32_t bh, int32_t* face_w, int32_t* face_h,
                          int32_t* n_hp_patches, int32_t* n_mp_patches);
 
+/* FaceForest::detectFace (src/FaceForest.cpp:136-159): the Haar cascade of the loaded model over a BGR
+ * frame (cvtColor, detectMultiScale(scale_factor, min_neighbors, flags 0, Size(min_size, min_size)))
+ * -> boxes[cap][4] (x, y, w, h), widened and clipped like detectFace when `widen`; raw: the ungrouped
+ * candidates in scan order (optional).  Parity with OpenCV unpinned (see ffd_oracle.cpp). */
+int oracle_detect_faces(const uint8_t* bgr, int32_t w, int32_t h, int32_t stride, int32_t min_size,
+                        int32_t min_neighbors, float scale_factor, int32_t widen, int32_t* boxes, int32_t cap,
+                        int32_t* n_boxes, int32_t* raw, int32_t raw_cap, int32_t* n_raw);
+
 /* Stage hooks for known-answer tests. */
 int oracle_bgr2gray(const uint8_t* bgr, int32_t w, int32_t h, int32_t stride, uint8_t* gray);
 int oracle_resize(const uint8_t* src, int32_t sw, int32_t sh, int32_t sstride, int32_t dw,
