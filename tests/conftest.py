@@ -40,6 +40,9 @@ def oracle_mod(model_path):
 @pytest.fixture(scope="session")
 def engine(model_path):
     import face_alignment_cvpr_2012_amd as ffd
+    import torch
+    if torch.cuda.is_available():  # PyTorch's HIP runtime first: tests hand torch buffers to the engine
+        torch.cuda.init()
     ff = ffd.FaceForest(ffd.FaceForestOptions(model_path=model_path))
     yield ff
     ff.close()
