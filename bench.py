@@ -306,6 +306,9 @@ def main():
                          "forest, c5 crowd")
     ap.add_argument("--faces", type=int, default=None, help="c2/c4: faces per GPU per step (4096 / 1024)")
     ap.add_argument("--frames", type=int, default=512, help="c3: frames per step (whole job)")
+    ap.add_argument("--detect", action="store_true",
+                    help="c3: boxes from the GPU Haar detector (FaceForest::detectFace) inside the timed step "
+                         "instead of the known paste boxes")
     ap.add_argument("--chunk", type=int, default=0, help="faces per pipeline launch (0 = whole batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
@@ -362,8 +365,28 @@ def main():
         if rank == 0:
             d_root = torch.zeros(world * per * rec, dtype=torch.uint8, device=dev)
 
+    if args.detect:
+        if wl.name != "c3":
+            raise SystemExit("--detect applies to the c3 (1080p frames) workload")
+        # analyzeImage (FaceForest.cpp:161-181): the frames' faces are whatever the detector finds
+        det_boxes, det_img = ff.detect_device(d_images.data_ptr(), iw * ih * 3, iw, ih, iw * 3, n_img)
+        n_det = torch.tensor([len(det_boxes)], dtype=torch.int64, device=dev)
+        if world > 1:
+            dist.all_reduce(n_det)
+        wl.total_faces = int(n_det.item())
+        wl.boxes, wl.box_img = det_boxes, det_img
+        wl.describe += "; boxes from the GPU Haar detector inside the step (detectFace on every frame)"
+        n = wl.n
+        per = -(-wl.total_faces // world)
+        d_out = torch.zeros(max(1, per) * rec, dtype=torch.uint8, device=dev)
+        if world > 1 and rank == 0:
+            d_root = torch.zeros(world * per * rec, dtype=torch.uint8, device=dev)
+
     def step():
-        ff.analyze_device(d_images.data_ptr(), iw * ih * 3, iw, ih, iw * 3, n_img, wl.boxes, wl.box_img,
+        boxes, box_img = wl.boxes, wl.box_img
+        if args.detect:
+            boxes, box_img = ff.detect_device(d_images.data_ptr(), iw * ih * 3, iw, ih, iw * 3, n_img, cap=len(wl.boxes))
+        ff.analyze_device(d_images.data_ptr(), iw * ih * 3, iw, ih, iw * 3, n_img, boxes, box_img,
                           d_out.data_ptr())
         if world > 1:  # ONE RCCL gather of the ffd_face records to rank 0 (faces sharded, no other exchange)
             ff.gather(d_out.data_ptr(), per, d_root.data_ptr() if d_root is not None else None, 0)
@@ -386,6 +409,13 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     stages = ff.stage_times()
+    detect_ms = None
+    if args.detect:  # the detector alone, same frames (its share of the step)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            ff.detect_device(d_images.data_ptr(), iw * ih * 3, iw, ih, iw * 3, n_img, cap=len(wl.boxes))
+        detect_ms = (time.perf_counter() - t1) / args.steps * 1e3
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -439,6 +469,10 @@ def main():
                                   "frac": round(value * b_face / 1e9 / HBM_PEAK_GBS, 4)},
             "stage_ms_per_step": {k: round(v[0] / max(1, args.steps), 3) for k, v in stages.items()},
         }
+        if detect_ms is not None:
+            out["detect"] = {"frames_per_step": wl.n_images * world, "faces_found": wl.total_faces,
+                             "detect_ms_per_step": round(detect_ms, 3),
+                             "frames_per_s": round(wl.n_images * world / (detect_ms / 1e3), 1)}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_budget)
         print(json.dumps(out), flush=True)

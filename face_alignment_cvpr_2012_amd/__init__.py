@@ -402,6 +402,23 @@ class FaceForest:
             res[owner[i]].append(_face_from_record(out[i]))
         return res
 
+    def detect_device(self, d_images, image_bytes, width, height, stride, n_img, fd_option=None, cap=None):
+        """detectFace over n_img frames already in device memory (one size, image_bytes apart):
+        (boxes (n, 4) int32, frame index per box (n,) int32), frames in order."""
+        opt = _det_opt(fd_option or self.options.fd_option)
+        cap = cap or 64 * max(1, n_img)
+        for _ in range(2):
+            boxes = np.zeros((cap, 4), np.int32)
+            owner = np.zeros(cap, np.int32)
+            n = ctypes.c_int32()
+            _check(lib().ffd_detect_faces_device(self._h, d_images, image_bytes, width, height, stride, n_img,
+                                                 ctypes.byref(opt), boxes.ctypes.data, owner.ctypes.data, cap,
+                                                 ctypes.byref(n)), self._h)
+            if n.value <= cap:
+                break
+            cap = n.value
+        return boxes[: n.value], owner[: n.value]
+
     def detect_candidates(self, img, fd_option=None):
         """Test hook: detectMultiScale's ungrouped candidates of one frame in scan order, (n, 4)."""
         imgs, cim = _image_array([img])

@@ -8,6 +8,7 @@
 // in the ffd_haar.hip kernels on the engine's main stream.
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -160,80 +161,98 @@ void build_levels(const ffd_engine* e, const std::vector<FrameIn>& in, const ffd
 }
 
 // Run the detector over frames already in device memory (e->main_stream()); boxes per frame out.
-ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vector<FrameIn>& in,
+// Frames go through in groups (FFD_DETECT_GROUP frames, default 64) so the pyramid / integral /
+// survivor buffers stay bounded whatever the batch.
+ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vector<FrameIn>& all_in,
                         const ffd_detect_options& o, std::vector<std::vector<ffd_rect>>& out,
                         std::vector<std::vector<ffd_rect>>* raw) {
   if (!e->have_haar) return fail(e, FFD_ERR_MODEL, "the model has no Haar cascade (convert it with ffd_convert)");
   if (!(o.search_scale_factor > 1.f) || o.min_feature_size < 0)
     return fail(e, FFD_ERR_INVALID_ARGUMENT, "search_scale_factor must be > 1 and min_feature_size >= 0");
-  out.assign(in.size(), {});
-  if (raw) raw->assign(in.size(), {});
-  if (in.empty()) return FFD_OK;
-  std::vector<HaarFrame> frames;
-  std::vector<HaarLevel> levels;
-  int64_t sz[4];
-  build_levels(e, in, o, frames, levels, sz);
+  for (const auto& f : all_in)
+    if (f.w > 32767 || f.h > 32767) return fail(e, FFD_ERR_UNSUPPORTED, "frames wider or taller than 32767 pixels");
+  out.assign(all_in.size(), {});
+  if (raw) raw->assign(all_in.size(), {});
+  int group = 64;
+  if (const char* v = std::getenv("FFD_DETECT_GROUP")) group = std::max(1, std::atoi(v));
   hipStream_t s = e->main_stream();
-  const int nF = (int)frames.size(), nL = (int)levels.size();
   const int cap = HAAR_MAX_CAND;
-  upload(e->det_frames, frames, s);
-  e->det_gray.ensure(sz[0]);
-  e->det_ncand.ensure((size_t)nF * 4);
-  e->det_nboxes.ensure((size_t)nF * 4);
-  e->det_cand.ensure((size_t)nF * cap * 16);
-  e->det_clsrect.ensure((size_t)nF * cap * 16);
-  e->det_clssum.ensure((size_t)nF * cap * 20);
-  e->det_boxes.ensure((size_t)nF * cap * 16);
-  if (nL > 0) {
-    upload(e->det_levels, levels, s);
-    e->det_scaled.ensure(sz[1]);
-    e->det_sum.ensure(sz[2] * 4);
-    e->det_sq.ensure(sz[2] * 8);
-    e->det_res.ensure(sz[3]);
-  }
-  int max_px = 0, max_lpx = 0, max_rows = 0, max_cols = 0, max_tiles = 0;
-  for (const auto& f : frames) max_px = std::max(max_px, f.w * f.h);
-  for (const auto& L : levels) {
-    max_lpx = std::max(max_lpx, L.sw * L.sh);
-    max_rows = std::max(max_rows, L.sh);
-    max_cols = std::max(max_cols, L.sw);
-    max_tiles = std::max(max_tiles, ((L.nx + 63) / 64) * ((L.ny + 3) / 4));
-  }
-  if (nL > 0) {
-    launch_haar_gray(e->det_frames.as<HaarFrame>(), nF, max_px, d_images, e->det_gray.as<uint8_t>(), s);
-    launch_haar_pyramid(e->det_levels.as<HaarLevel>(), nL, max_lpx, max_rows, max_cols, e->det_gray.as<uint8_t>(),
-                        e->det_scaled.as<uint8_t>(), e->det_sum.as<int32_t>(), e->det_sq.as<uint64_t>(), s);
-    launch_haar_cascade(e->det_levels.as<HaarLevel>(), nL, max_tiles, e->det_sum.as<int32_t>(),
-                        e->det_sq.as<uint64_t>(), e->haar_weak.as<HaarWeak>(), e->haar_stage.as<HaarStage>(),
-                        e->haar_stages, e->haar_ww, e->haar_wh, e->det_res.as<int8_t>(), s);
-  }
-  launch_haar_group(e->det_frames.as<HaarFrame>(), nF, nL > 0 ? e->det_levels.as<HaarLevel>() : nullptr,
-                    nL > 0 ? e->det_res.as<int8_t>() : nullptr, cap, e->det_cand.as<int4>(), e->det_ncand.as<int32_t>(),
-                    o.min_neighbors, o.widen, e->det_clsrect.as<int4>(), e->det_clssum.as<int>(),
-                    e->det_boxes.as<int4>(), e->det_nboxes.as<int32_t>(), s);
-  std::vector<int32_t> ncand(nF), nbox(nF);
-  HIP_CHECK(hipMemcpyAsync(ncand.data(), e->det_ncand.p, nF * 4, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipMemcpyAsync(nbox.data(), e->det_nboxes.p, nF * 4, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-  for (int k = 0; k < nF; k++)
-    if (ncand[k] > cap)
-      return fail(e, FFD_ERR_UNSUPPORTED, "frame " + std::to_string(k) + ": " + std::to_string(ncand[k]) +
-                                              " raw detections exceed the grouping capacity " + std::to_string(cap));
-  std::vector<int4> tmp;
-  for (int k = 0; k < nF; k++) {
-    tmp.resize(nbox[k]);
-    if (nbox[k] > 0)
-      HIP_CHECK(hipMemcpyAsync(tmp.data(), e->det_boxes.as<int4>() + (int64_t)k * cap, nbox[k] * sizeof(int4),
-                               hipMemcpyDeviceToHost, s));
+  for (size_t g0 = 0; g0 < all_in.size(); g0 += group) {
+    const std::vector<FrameIn> in(all_in.begin() + g0, all_in.begin() + std::min(all_in.size(), g0 + group));
+    std::vector<HaarFrame> frames;
+    std::vector<HaarLevel> levels;
+    int64_t sz[4];
+    build_levels(e, in, o, frames, levels, sz);
+    const int nF = (int)frames.size(), nL = (int)levels.size();
+    upload(e->det_frames, frames, s);
+    e->det_gray.ensure(sz[0]);
+    e->det_ncand.ensure((size_t)nF * 8);
+    e->det_cand.ensure((size_t)nF * cap * 16);
+    e->det_clsrect.ensure((size_t)nF * cap * 16);
+    e->det_clssum.ensure((size_t)nF * cap * 20);
+    e->det_boxes.ensure((size_t)nF * cap * 16);
+    e->det_packed.ensure((size_t)nF * cap * 20);
+    int max_px = 0, max_lpx = 0, max_rows = 0, max_cols = 0, max_tiles = 0, max_ystep = 1;
+    for (const auto& f : frames) max_px = std::max(max_px, f.w * f.h);
+    for (const auto& L : levels) {
+      max_lpx = std::max(max_lpx, L.sw * L.sh);
+      max_rows = std::max(max_rows, L.sh);
+      max_cols = std::max(max_cols, L.sw);
+      max_tiles = std::max(max_tiles, ((L.nx + HAAR_TILE_X - 1) / HAAR_TILE_X) * ((L.ny + HAAR_TILE_Y - 1) / HAAR_TILE_Y));
+      max_ystep = std::max(max_ystep, L.ystep);
+    }
+    int32_t* n_cand = e->det_ncand.as<int32_t>();
+    int32_t* n_boxes = n_cand + nF;
+    if (nL > 0) {
+      upload(e->det_levels, levels, s);
+      e->det_scaled.ensure(sz[1]);
+      e->det_sum.ensure(sz[2] * 4);
+      e->det_sq.ensure(sz[2] * 8);
+      e->det_res.ensure(sz[3]);
+      launch_haar_gray(e->det_frames.as<HaarFrame>(), nF, max_px, d_images, e->det_gray.as<uint8_t>(), s);
+      launch_haar_pyramid(e->det_levels.as<HaarLevel>(), nL, max_lpx, max_rows, max_cols, e->det_gray.as<uint8_t>(),
+                          e->det_scaled.as<uint8_t>(), e->det_sum.as<int32_t>(), e->det_sq.as<uint64_t>(), s);
+      const int lds = haar_cascade_lds(max_ystep, e->haar_ww, e->haar_wh);
+      if (lds > 64 * 1024) return fail(e, FFD_ERR_UNSUPPORTED, "cascade window too large for the LDS tile");
+      launch_haar_cascade(e->det_levels.as<HaarLevel>(), nL, max_tiles, e->det_sum.as<int32_t>(),
+                          e->det_sq.as<uint64_t>(), e->haar_weak.as<HaarWeak>(), e->haar_stage.as<HaarStage>(),
+                          e->haar_stages, e->haar_ww, e->haar_wh, e->det_res.as<int8_t>(), lds, s);
+    }
+    launch_haar_group(e->det_frames.as<HaarFrame>(), nF, nL > 0 ? e->det_levels.as<HaarLevel>() : nullptr,
+                      nL > 0 ? e->det_res.as<int8_t>() : nullptr, cap, e->det_cand.as<int4>(), n_cand,
+                      o.min_neighbors, o.widen, e->det_clsrect.as<int4>(), e->det_clssum.as<int>(),
+                      e->det_boxes.as<int4>(), n_boxes, s);
+    int4* packed = e->det_packed.as<int4>();
+    int32_t* owner = reinterpret_cast<int32_t*>(packed + (size_t)nF * cap);
+    launch_haar_pack(nF, cap, e->det_boxes.as<int4>(), n_boxes, packed, owner, s);
+    std::vector<int32_t> counts(2 * nF);
+    HIP_CHECK(hipMemcpyAsync(counts.data(), n_cand, 2 * nF * 4, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    for (const int4& b : tmp) out[k].push_back(ffd_rect{b.x, b.y, b.z, b.w});
-    if (raw) {
-      tmp.resize(ncand[k]);
-      if (ncand[k] > 0)
-        HIP_CHECK(hipMemcpyAsync(tmp.data(), e->det_cand.as<int4>() + (int64_t)k * cap, ncand[k] * sizeof(int4),
-                                 hipMemcpyDeviceToHost, s));
+    int64_t total = 0;
+    for (int k = 0; k < nF; k++) {
+      if (counts[k] > cap)
+        return fail(e, FFD_ERR_UNSUPPORTED, "frame " + std::to_string(g0 + k) + ": " + std::to_string(counts[k]) +
+                                                " raw detections exceed the grouping capacity " + std::to_string(cap));
+      total += counts[nF + k];
+    }
+    std::vector<int4> pb(total);
+    std::vector<int32_t> po(total);
+    if (total > 0) {
+      HIP_CHECK(hipMemcpyAsync(pb.data(), packed, total * sizeof(int4), hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipMemcpyAsync(po.data(), owner, total * sizeof(int32_t), hipMemcpyDeviceToHost, s));
       HIP_CHECK(hipStreamSynchronize(s));
-      for (const int4& b : tmp) (*raw)[k].push_back(ffd_rect{b.x, b.y, b.z, b.w});
+    }
+    for (int64_t i = 0; i < total; i++) out[g0 + po[i]].push_back(ffd_rect{pb[i].x, pb[i].y, pb[i].z, pb[i].w});
+    if (raw) {
+      for (int k = 0; k < nF; k++) {
+        std::vector<int4> tmp(counts[k]);
+        if (counts[k] > 0) {
+          HIP_CHECK(hipMemcpyAsync(tmp.data(), e->det_cand.as<int4>() + (int64_t)k * cap, counts[k] * sizeof(int4),
+                                   hipMemcpyDeviceToHost, s));
+          HIP_CHECK(hipStreamSynchronize(s));
+        }
+        for (const int4& b : tmp) (*raw)[g0 + k].push_back(ffd_rect{b.x, b.y, b.z, b.w});
+      }
     }
   }
   return FFD_OK;

@@ -140,7 +140,8 @@ struct ffd_engine {
   int haar_ww = 0, haar_wh = 0, haar_stages = 0;
   DevBuf haar_weak, haar_stage;
   DevBuf det_frames, det_levels, det_gray, det_scaled, det_sum, det_sq, det_res, det_cand, det_ncand, det_clsrect,
-      det_clssum, det_boxes, det_nboxes;
+      det_clssum, det_boxes, det_packed;
+  int n_cu = 256;  // compute units of the device (survivor-pass grids)
 
   std::vector<std::unique_ptr<Workspace>> ws;
   DevBuf images, out, scratch_a, scratch_b, scratch_c;  // host-API staging (ws[0] stream)
@@ -253,6 +254,7 @@ struct ffd_engine {
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, device));
     if (!std::getenv("FFD_TRAV_WG")) trav_wg = std::max(8, prop.multiProcessorCount);
+    n_cu = std::max(1, prop.multiProcessorCount);
   }
   void run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out);
   void analyze(const uint8_t* d_images, const std::vector<FaceDesc>& all, FaceOut* d_out);

@@ -183,49 +183,118 @@ __global__ __launch_bounds__(256) void k_haar_cols(const HaarLevel* __restrict__
 }
 
 // ------------------------------------------------------------------------ cascade ----
-// One thread per scan position of a level: 64 x 4 positions per workgroup (x fastest, so a wave's
-// corner reads are one row of the integral).  Result: 1 (face) or -stage (stage 0 -> 0), as int8.
-__global__ __launch_bounds__(256) void k_haar_cascade(const HaarLevel* __restrict__ levels,
-                                                      const int32_t* __restrict__ sum, const uint64_t* __restrict__ sq,
-                                                      const HaarWeak* __restrict__ weak,
-                                                      const HaarStage* __restrict__ stages, int n_stages, int ww,
-                                                      int wh, int8_t* __restrict__ result) {
+// predictOrderedStump for a tile of 64 x 8 scan positions per workgroup.  The tile's integral
+// window (sum, i32) is staged once in LDS, so every rectangle corner is an LDS read; the squared
+// integral is read from HBM only for the 4 normrect corners.  The tile's positions then run the
+// stages in passes ([0,1), [1,2), [2,4), [4,7), [7,n)): between passes the survivors are compacted
+// into an LDS list, so the waves of later passes are dense (without it almost every wave keeps some
+// lane alive through the early stages and runs ~100 weak classifiers for lanes that need ~10).
+// Each stage's sum restarts at 0, so splitting at stage boundaries is exact.
+// Result per position: 1 (face) or -stage (stage 0 -> 0), as int8.
+constexpr int HT_X = 64, HT_Y = 8, HT_THREADS = 256, HT_POS = HT_X * HT_Y;
+
+__host__ __device__ constexpr int haar_win_cols(int ystep, int ww) { return HT_X * ystep + ww; }
+__host__ __device__ constexpr int haar_win_rows(int ystep, int wh) { return HT_Y * ystep + wh; }
+
+__global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __restrict__ levels,
+                                                             const int32_t* __restrict__ sum,
+                                                             const uint64_t* __restrict__ sq,
+                                                             const HaarWeak* __restrict__ weak,
+                                                             const HaarStage* __restrict__ stages, int n_stages,
+                                                             int ww, int wh, int8_t* __restrict__ result) {
+  extern __shared__ __attribute__((aligned(16))) int32_t win[];
+  __shared__ double vnf[HT_POS];
+  __shared__ uint16_t list[2][HT_POS];
+  __shared__ int n_list[2];
   const HaarLevel L = levels[blockIdx.y];
-  const int tiles_x = (L.nx + 63) >> 6;
+  const int tiles_x = (L.nx + HT_X - 1) / HT_X;
   const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
-  const int ix = tx * 64 + (threadIdx.x & 63), iy = ty * 4 + (threadIdx.x >> 6);
-  if (iy >= L.ny) return;
-  if (ix >= L.nx) return;
-  const int x = ix * L.ystep, y = iy * L.ystep;
-  const int P = L.sw + 1;
-  const int32_t* S = sum + L.sum_off + (int64_t)y * P + x;
-  const uint64_t* Q = sq + L.sum_off + (int64_t)y * P + x;
-  // setWindow: normrect (1, 1, ww - 2, wh - 2)
-  const int a = P + 1, b = a + (ww - 2), c = (wh - 1) * P + 1, d = c + (ww - 2);
-  const int valsum = S[a] - S[b] - S[c] + S[d];
-  const double valsq = (double)(int64_t)(Q[a] - Q[b] - Q[c] + Q[d]);
-  double nf = (double)((ww - 2) * (wh - 2)) * valsq - (double)valsum * (double)valsum;
-  nf = nf > 0. ? __builtin_sqrt(nf) : 1.;
-  const double vnf = 1. / nf;
-  int res = 1;
-  for (int s = 0; s < n_stages; s++) {
-    const HaarStage st = stages[s];
-    double acc = 0.0;
-    for (int i = st.first; i < st.first + st.ntrees; i++) {
-      const HaarWeak w = weak[i];
-      auto rs = [&](uint32_t r) {
-        const int rx = r & 255u, ry = (r >> 8) & 255u, rw = (r >> 16) & 255u, rh = r >> 24;
-        const int p0 = ry * P + rx, p2 = p0 + rh * P;
-        return S[p0] - S[p0 + rw] - S[p2] + S[p2 + rw];
-      };
-      float ret = w.w0 * (float)rs(w.r0) + w.w1 * (float)rs(w.r1);
-      if (w.w2 != 0.0f) ret += w.w2 * (float)rs(w.r2);
-      const float value = (float)((double)ret * vnf);
-      acc += (double)(value < w.thr ? w.leaf0 : w.leaf1);
-    }
-    if (acc < (double)st.thr) { res = -s; break; }
+  if (ty * HT_Y >= L.ny) return;
+  const int ys = L.ystep, P = L.sw + 1;
+  const int WC = haar_win_cols(ys, ww), WR = haar_win_rows(ys, wh);
+  const int x0 = tx * HT_X * ys, y0 = ty * HT_Y * ys;
+  const int32_t* S = sum + L.sum_off;
+  const uint64_t* Q = sq + L.sum_off;
+  for (int i = threadIdx.x; i < WC * WR; i += HT_THREADS) {
+    const int r = i / WC, c = i - r * WC;
+    const int gy = y0 + r, gx = x0 + c;
+    win[i] = (gy <= L.sh && gx < P) ? S[(int64_t)gy * P + gx] : 0;
   }
-  result[L.res_off + (int64_t)iy * L.nx + ix] = (int8_t)res;
+  if (threadIdx.x == 0) { n_list[0] = 0; n_list[1] = 0; }
+  __syncthreads();
+  // setWindow for every position of the tile: normrect (1, 1, ww - 2, wh - 2)
+  const int na = WC + 1, nb = na + (ww - 2), nc = (wh - 1) * WC + 1, nd = nc + (ww - 2);
+  const int qa = P + 1, qb = qa + (ww - 2), qc = (wh - 1) * P + 1, qd = qc + (ww - 2);
+  for (int p = threadIdx.x; p < HT_POS; p += HT_THREADS) {
+    const int lx = p & (HT_X - 1), ly = p / HT_X;
+    const int ix = tx * HT_X + lx, iy = ty * HT_Y + ly;
+    if (ix >= L.nx || iy >= L.ny) continue;
+    const int o = ly * ys * WC + lx * ys;
+    const int valsum = win[o + na] - win[o + nb] - win[o + nc] + win[o + nd];
+    const uint64_t* q = Q + (int64_t)(y0 + ly * ys) * P + x0 + lx * ys;
+    const double valsq = (double)(int64_t)(q[qa] - q[qb] - q[qc] + q[qd]);
+    double nf = (double)((ww - 2) * (wh - 2)) * valsq - (double)valsum * (double)valsum;
+    nf = nf > 0. ? __builtin_sqrt(nf) : 1.;
+    vnf[p] = 1. / nf;
+    list[0][atomicAdd(&n_list[0], 1)] = (uint16_t)p;  // order within a pass does not matter
+  }
+  __syncthreads();
+  const int bounds[6] = {0, 1, 2, 4, 7, n_stages};
+  int cur = 0;
+  for (int pass = 0; pass < 5; pass++) {
+    const int s0 = min(bounds[pass], n_stages), s1 = pass == 4 ? n_stages : min(bounds[pass + 1], n_stages);
+    if (s0 >= s1) continue;
+    const int n = n_list[cur];
+    if (threadIdx.x == 0) n_list[cur ^ 1] = 0;
+    __syncthreads();
+    for (int k = threadIdx.x; k < n; k += HT_THREADS) {
+      const int p = list[cur][k];
+      const int lx = p & (HT_X - 1), ly = p / HT_X;
+      const int32_t* w0 = win + ly * ys * WC + lx * ys;
+      const double f = vnf[p];
+      int s = s0;
+      for (; s < s1; s++) {
+        const HaarStage st = stages[s];
+        double acc = 0.0;
+        // 4 weak classifiers per step: their records (wave-uniform scalar loads) and all 36 window
+        // reads are issued together; the sum still accumulates in classifier order
+        auto value_of = [&](const HaarWeak& c) {
+          auto rs = [&](uint32_t r) {
+            const int rx = r & 255u, ry = (r >> 8) & 255u, rw = (r >> 16) & 255u, rh = r >> 24;
+            const int p0 = ry * WC + rx, p2 = p0 + rh * WC;
+            return w0[p0] - w0[p0 + rw] - w0[p2] + w0[p2 + rw];
+          };
+          float ret = c.w0 * (float)rs(c.r0) + c.w1 * (float)rs(c.r1);
+          // two-rectangle features carry w2 = 0 and an empty rect 2: + (+0) leaves ret unchanged
+          // (up to the sign of a zero, which no comparison below distinguishes)
+          ret += c.w2 * (float)rs(c.r2);
+          return (float)((double)ret * f);
+        };
+        int i = st.first;
+        const int e = st.first + st.ntrees;
+        for (; i + 4 <= e; i += 4) {
+          const HaarWeak c0 = weak[i], c1 = weak[i + 1], c2 = weak[i + 2], c3 = weak[i + 3];
+          const float v0 = value_of(c0), v1 = value_of(c1), v2 = value_of(c2), v3 = value_of(c3);
+          acc += (double)(v0 < c0.thr ? c0.leaf0 : c0.leaf1);
+          acc += (double)(v1 < c1.thr ? c1.leaf0 : c1.leaf1);
+          acc += (double)(v2 < c2.thr ? c2.leaf0 : c2.leaf1);
+          acc += (double)(v3 < c3.thr ? c3.leaf0 : c3.leaf1);
+        }
+        for (; i < e; i++) {
+          const HaarWeak c = weak[i];
+          const float v = value_of(c);
+          acc += (double)(v < c.thr ? c.leaf0 : c.leaf1);
+        }
+        if (acc < (double)st.thr) break;
+      }
+      const int ix = tx * HT_X + lx, iy = ty * HT_Y + ly;
+      if (s < s1) result[L.res_off + (int64_t)iy * L.nx + ix] = (int8_t)(-s);
+      else if (s1 == n_stages) result[L.res_off + (int64_t)iy * L.nx + ix] = 1;
+      else list[cur ^ 1][atomicAdd(&n_list[cur ^ 1], 1)] = (uint16_t)p;
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
 }
 
 // ------------------------------------------------------------------------ collect ----
@@ -269,17 +338,28 @@ __global__ __launch_bounds__(HC_THREADS) void k_haar_collect(const HaarFrame* __
       if (lv < 0) return 0;
       const HaarLevel& L = levels[lv];
       const int8_t* row = result + L.res_off + (int64_t)iy * L.nx;
-      for (int ix = 0; ix < L.nx;) {
-        const int v = row[ix];
-        if (v > 0) {
-          if (emit && at + n < cap) {
-            const int x = ix * L.ystep, y = iy * L.ystep;
-            cand[(int64_t)blockIdx.x * cap + at + n] =
-                make_int4(hround_d(x * L.factor), hround_d(y * L.factor), L.win_w, L.win_h);
+      // 16 results per batch of independent loads, so the skip chain runs in registers instead of
+      // one dependent load per step
+      int ix = 0;
+      for (int c0 = 0; c0 < L.nx; c0 += 16) {
+        int8_t v16[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) v16[k] = c0 + k < L.nx ? row[c0 + k] : (int8_t)-1;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+          if (ix != c0 + k) continue;
+          const int v = v16[k];
+          if (c0 + k >= L.nx) break;
+          if (v > 0) {
+            if (emit && at + n < cap) {
+              const int x = ix * L.ystep, y = iy * L.ystep;
+              cand[(int64_t)blockIdx.x * cap + at + n] =
+                  make_int4(hround_d(x * L.factor), hround_d(y * L.factor), L.win_w, L.win_h);
+            }
+            n++;
           }
-          n++;
+          ix += v == 0 ? 2 : 1;
         }
-        ix += v == 0 ? 2 : 1;
       }
       return n;
     };
@@ -430,7 +510,31 @@ __global__ __launch_bounds__(HC_THREADS) void k_haar_group(const HaarFrame* __re
   if (threadIdx.x == 0) n_boxes[blockIdx.x] = nout;
 }
 
+// every frame's boxes packed contiguously in frame order (one workgroup)
+__global__ __launch_bounds__(HC_THREADS) void k_haar_pack(int n_frames, int cap, const int4* __restrict__ boxes,
+                                                           const int32_t* __restrict__ n_boxes,
+                                                           int4* __restrict__ packed, int32_t* __restrict__ owner) {
+  __shared__ int sh[HC_THREADS / 64 + 1];
+  int base = 0;
+  for (int f0 = 0; f0 < n_frames; f0 += HC_THREADS) {
+    const int f = f0 + threadIdx.x;
+    const int n = f < n_frames ? n_boxes[f] : 0;
+    int tot;
+    const int at = base + block_excl_scan(n, sh, tot);
+    for (int i = 0; i < n; i++) {
+      packed[at + i] = boxes[(int64_t)f * cap + i];
+      owner[at + i] = f;
+    }
+    base += tot;
+  }
+}
+
 }  // namespace
+
+void launch_haar_pack(int n_frames, int cap, const int4* boxes, const int32_t* n_boxes, int4* packed, int32_t* owner,
+                      hipStream_t s) {
+  k_haar_pack<<<1, HC_THREADS, 0, s>>>(n_frames, cap, boxes, n_boxes, packed, owner);
+}
 
 void launch_haar_gray(const HaarFrame* frames, int n_frames, int max_pixels, const uint8_t* images, uint8_t* gray,
                       hipStream_t s) {
@@ -445,10 +549,15 @@ void launch_haar_pyramid(const HaarLevel* levels, int n_levels, int max_pixels, 
   k_haar_cols<<<dim3((max_cols + 255) / 256, n_levels), 256, 0, s>>>(levels, sum, sq);
 }
 
+int haar_cascade_lds(int max_ystep, int ww, int wh) {
+  return haar_win_cols(max_ystep, ww) * haar_win_rows(max_ystep, wh) * 4;
+}
+
 void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint64_t* sq,
                          const HaarWeak* weak, const HaarStage* stages, int n_stages, int ww, int wh, int8_t* result,
-                         hipStream_t s) {
-  k_haar_cascade<<<dim3(max_tiles, n_levels), 256, 0, s>>>(levels, sum, sq, weak, stages, n_stages, ww, wh, result);
+                         int lds_bytes, hipStream_t s) {
+  k_haar_cascade<<<dim3(max_tiles, n_levels), HT_THREADS, lds_bytes, s>>>(levels, sum, sq, weak, stages, n_stages, ww,
+                                                                           wh, result);
 }
 
 void launch_haar_group(const HaarFrame* frames, int n_frames, const HaarLevel* levels, const int8_t* result, int cap,

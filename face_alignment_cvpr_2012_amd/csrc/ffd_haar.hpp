@@ -54,10 +54,16 @@ void launch_haar_gray(const HaarFrame* frames, int n_frames, int max_pixels, con
                       hipStream_t s);
 void launch_haar_pyramid(const HaarLevel* levels, int n_levels, int max_pixels, int max_rows, int max_cols,
                          const uint8_t* gray, uint8_t* scaled, int32_t* sum, uint64_t* sq, hipStream_t s);
-// max_tiles: the largest level's ceil(nx / 64) * ceil(ny / 4)
+// a workgroup per 64 x 8 scan positions: max_tiles = the largest level's ceil(nx / 64) * ceil(ny / 8);
+// lds_bytes = haar_cascade_lds(largest ystep of the batch, ww, wh) (dynamic LDS: the integral window)
+constexpr int HAAR_TILE_X = 64, HAAR_TILE_Y = 8;
+int haar_cascade_lds(int max_ystep, int ww, int wh);
 void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint64_t* sq,
                          const HaarWeak* weak, const HaarStage* stages, int n_stages, int ww, int wh, int8_t* result,
-                         hipStream_t s);
+                         int lds_bytes, hipStream_t s);
+// pack every frame's boxes (cap apart) contiguously: packed[i], owner[i]; totals[0] = box count
+void launch_haar_pack(int n_frames, int cap, const int4* boxes, const int32_t* n_boxes, int4* packed, int32_t* owner,
+                      hipStream_t s);
 // candidates (cap per frame) in scan order, then grouped + widened boxes (cap per frame);
 // cls_rect: cap int4 per frame, cls_sum: 5 cap ints per frame (scratch)
 void launch_haar_group(const HaarFrame* frames, int n_frames, const HaarLevel* levels, const int8_t* result, int cap,
