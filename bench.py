@@ -261,6 +261,60 @@ def parity_spot_check(ff, wl, d_out, k=4):
     return ok
 
 
+def host_inclusive(ff, wl, iw, ih, steps, chunks=4):
+    """SURVEY.md §8(d)'s timing rule for the host API: batch in pinned host memory -> H2D -> the
+    path -> D2H of the records, in `chunks` chunks whose H2D (own stream) overlaps the previous
+    chunk's compute (engine stream).  C2-shaped workloads only (one image per face)."""
+    import torch
+    n, rec = wl.n, 112
+    h_img = torch.from_numpy(np.ascontiguousarray(wl.images[:n])).pin_memory()
+    d_img = torch.empty(h_img.shape, dtype=torch.uint8, device="cuda")
+    d_out = torch.empty(n * rec, dtype=torch.uint8, device="cuda")
+    h_out = torch.empty(n * rec, dtype=torch.uint8).pin_memory()
+    eng = torch.cuda.ExternalStream(ff.stream())
+    copy = torch.cuda.Stream()
+    bounds = [n * c // chunks for c in range(chunks + 1)]
+    per_img = iw * ih * 3
+
+    def run():
+        for c in range(chunks):
+            a, b = bounds[c], bounds[c + 1]
+            if a == b:
+                continue
+            with torch.cuda.stream(copy):
+                d_img[a:b].copy_(h_img[a:b], non_blocking=True)
+                ev = copy.record_event()
+            eng.wait_event(ev)
+            ff.analyze_device(d_img[a].data_ptr(), per_img, iw, ih, iw * 3, b - a, wl.boxes[a:b],
+                              np.arange(b - a, dtype=np.int32), d_out[a * rec].data_ptr())
+            with torch.cuda.stream(eng):
+                h_out[a * rec:b * rec].copy_(d_out[a * rec:b * rec], non_blocking=True)
+        ff.synchronize()
+        torch.cuda.synchronize()
+
+    run()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": round(n / dt, 1), "unit": "faces/s", "ms_per_step": round(dt * 1e3, 3), "chunks": chunks,
+            "h2d_bytes": int(n * per_img), "note": "pinned host batch in, host records out; chunked H2D on its own "
+                                                   "stream overlapping the previous chunk's compute"}
+
+
+def single_face_latency(ff, wl, reps=50):
+    """The reference's call pattern (eval_ffd.cpp:89): one analyzeFace per call, host image in,
+    host record out, through ffd_analyze_faces (the C ABI the C++ shim calls)."""
+    img, box = wl.face(0)
+    ff.analyzeFace(img, box)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ff.analyzeFace(img, box)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    return {"median_ms": round(float(np.median(ts)), 3), "min_ms": round(float(np.min(ts)), 3), "calls": reps}
+
+
 def launch_ranks(n):
     """Start n ranks of this script under torch.distributed.run as a child process (nothing in this
     process has touched the GPU) and return the child's exit status."""
@@ -311,6 +365,7 @@ def main():
                          "instead of the known paste boxes")
     ap.add_argument("--chunk", type=int, default=0, help="faces per pipeline launch (0 = whole batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-paths", action="store_true", help="skip the host-inclusive and latency lines")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
     ap.add_argument("--dry-run", action="store_true", help="launcher + gather only, gloo, no GPU")
     args = ap.parse_args()
@@ -409,6 +464,11 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     stages = ff.stage_times()
+    ff.set_profiling(False)
+    host_incl = latency = None
+    if world == 1 and wl.name == "c2" and not args.no_host_paths:
+        host_incl = host_inclusive(ff, wl, iw, ih, max(1, min(args.steps, 3)))
+        latency = single_face_latency(ff, wl)
     detect_ms = None
     if args.detect:  # the detector alone, same frames (its share of the step)
         torch.cuda.synchronize()
@@ -469,6 +529,9 @@ def main():
                                   "frac": round(value * b_face / 1e9 / HBM_PEAK_GBS, 4)},
             "stage_ms_per_step": {k: round(v[0] / max(1, args.steps), 3) for k, v in stages.items()},
         }
+        if host_incl is not None:
+            out["host_inclusive"] = host_incl
+            out["analyze_face_latency"] = latency
         if detect_ms is not None:
             out["detect"] = {"frames_per_step": wl.n_images * world, "faces_found": wl.total_faces,
                              "detect_ms_per_step": round(detect_ms, 3),

@@ -5,8 +5,10 @@
 //   HeadPoseEstimatorOption, MultiPartEstimatorOption, FaceDetectionOption, FaceForestOptions,
 //   Face { headpose, bbox, ffd_cordinates }, FaceForest(FaceForestOptions),
 //   FaceForest::analyzeFace(img, bbox, Face&)      (FaceForest.cpp:183-258)
-//   FaceForest::analyzeImage(img, boxes, faces)    (FaceForest.cpp:161-181 without detectFace:
-//                                                   the Haar detector stays on the caller's side)
+//   FaceForest::analyzeImage(img, faces)           (FaceForest.cpp:161-181: the GPU Haar detector, then
+//                                                   analyzeFace on every box, one GPU batch)
+//   FaceForest::detectFace(img, boxes)             (FaceForest.cpp:136-159, the model's cascade)
+//   FaceForest::analyzeImage(img, boxes, faces)    (the same with the caller's own boxes)
 //   FaceForest::estimateHeadPose / estimateFacialFeatures (static, FaceForest.hpp:97-115,
 //                                                   FaceForest.cpp:60-95) over an ImageSample
 //   ImageSample(img, features, useIntegral)         (ImageSample.cpp:11-20, channels on the GPU)
@@ -66,11 +68,11 @@ inline const uint8_t* mat_data(const Mat& m) { return m.data; }
 inline int mat_step(const Mat& m) { return (int)m.step; }
 #endif
 
-struct FaceDetectionOption {  // kept for source compatibility; detection is the caller's
+struct FaceDetectionOption {  // include/FaceForest.hpp:21-32 (the cascade comes from the converted model)
   int min_feature_size = 30;
   int min_neighbors = 1;
   float search_scale_factor = 1.3f;
-  std::string path_face_cascade;
+  std::string path_face_cascade;  // unused: ffd_convert puts data/haarcascade_frontalface_alt.xml in the model
 };
 
 struct HeadPoseEstimatorOption {
@@ -205,10 +207,13 @@ class FaceForest {
       engine_ = nullptr;
     }
     if (engine_) detail::current_engine() = engine_;
+    fd_option_ = option.fd_option;
   }
   FaceForest(const FaceForest&) = delete;
   FaceForest& operator=(const FaceForest&) = delete;
-  FaceForest(FaceForest&& o) noexcept : engine_(o.engine_), err_(std::move(o.err_)) { o.engine_ = nullptr; }
+  FaceForest(FaceForest&& o) noexcept : engine_(o.engine_), err_(std::move(o.err_)), fd_option_(o.fd_option_) {
+    o.engine_ = nullptr;
+  }
   virtual ~FaceForest() {
     if (engine_ && detail::current_engine() == engine_) detail::current_engine() = nullptr;
     ffd_engine_destroy(engine_);
@@ -222,6 +227,49 @@ class FaceForest {
     std::vector<Face> faces;
     analyzeImage(img, std::vector<Rect>{face_bbox}, faces);
     face = faces.at(0);
+  }
+
+  // FaceForest::detectFace (FaceForest.cpp:136-159) with this object's fd_option, on the GPU.
+  void detectFace(const Mat img, std::vector<Rect>& faces_bboxes) {
+    if (!engine_) throw std::runtime_error("FaceForest not initialised: " + err_);
+    ffd_image im{mat_data(img), img.cols, img.rows, mat_step(img)};
+    const ffd_detect_options o = detect_options();
+    std::vector<ffd_rect> r(64);
+    int32_t n = 0;
+    for (int pass = 0; pass < 2; pass++) {
+      const ffd_status st = ffd_detect_faces(engine_, &im, 1, &o, r.data(), nullptr, (int32_t)r.size(), &n);
+      if (st != FFD_OK) throw std::runtime_error(ffd_last_error(engine_));
+      if (n <= (int32_t)r.size()) break;
+      r.resize(n);
+    }
+    faces_bboxes.clear();
+    for (int32_t i = 0; i < n; i++) faces_bboxes.emplace_back(r[i].x, r[i].y, r[i].width, r[i].height);
+  }
+
+  // FaceForest::analyzeImage (FaceForest.cpp:161-181): detectFace, then analyzeFace on every box (one
+  // GPU batch).  Appends to `faces` like the reference; faces with no usable analysis are skipped
+  // only if the reference would throw for them (never for detector boxes, which lie in the image).
+  void analyzeImage(const Mat img, std::vector<Face>& faces) {
+    if (!engine_) throw std::runtime_error("FaceForest not initialised: " + err_);
+    ffd_image im{mat_data(img), img.cols, img.rows, mat_step(img)};
+    const ffd_detect_options o = detect_options();
+    std::vector<ffd_face> out(64);
+    int32_t n = 0;
+    for (int pass = 0; pass < 2; pass++) {
+      const ffd_status st = ffd_analyze_images(engine_, &im, 1, &o, out.data(), nullptr, (int32_t)out.size(), &n);
+      if (st != FFD_OK) throw std::runtime_error(ffd_last_error(engine_));
+      if (n <= (int32_t)out.size()) break;
+      out.resize(n);
+    }
+    for (int32_t i = 0; i < n; i++) {
+      if (out[i].status != FFD_OK)
+        throw std::invalid_argument("face " + std::to_string(i) + ": " + ffd_status_string(out[i].status));
+      Face f;
+      f.headpose = out[i].headpose;
+      f.bbox = Rect(out[i].bbox.x, out[i].bbox.y, out[i].bbox.width, out[i].bbox.height);
+      for (int k = 0; k < FFD_NUM_LANDMARKS; k++) f.ffd_cordinates.emplace_back(out[i].points[k][0], out[i].points[k][1]);
+      faces.push_back(f);
+    }
   }
 
   // FaceForest::analyzeImage (FaceForest.cpp:161-181) with the face boxes supplied by the caller;
@@ -288,8 +336,17 @@ class FaceForest {
   ffd_engine* engine() const { return engine_; }
 
  private:
+  ffd_detect_options detect_options() const {
+    ffd_detect_options o;
+    ffd_detect_options_init(&o);
+    o.min_feature_size = fd_option_.min_feature_size;
+    o.min_neighbors = fd_option_.min_neighbors;
+    o.search_scale_factor = fd_option_.search_scale_factor;
+    return o;
+  }
   ffd_engine* engine_ = nullptr;
   std::string err_;
+  FaceDetectionOption fd_option_;
 };
 
 }  // namespace ffd

@@ -65,3 +65,21 @@ def test_shim_estimators_and_forest(model_path, fixtures, engine, oracle_mod, tm
     import face_alignment_cvpr_2012_amd as ffd
     want = ffd.Forest(engine, ffd.FOREST_HEADPOSE).evaluate(ch, [region[:2]], list(range(15)))[0]
     assert np.array_equal(leaves, want)
+
+
+@pytest.mark.gpu
+def test_shim_analyze_image_detects(model_path, fixtures, engine, tmp_path):
+    """analyzeImage(img, faces) from C++: the GPU Haar detector then analyzeFace, equal to the Python API."""
+    img = fixtures["images"][9]
+    path = tmp_path / "img.bgr"
+    np.ascontiguousarray(img).tofile(path)
+    h, w = img.shape[:2]
+    r = subprocess.run([EXE, model_path, str(path), str(w), str(h)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [ln.split() for ln in r.stdout.strip().splitlines()]
+    faces = engine.analyzeImage(img)
+    assert len(lines) == len(faces) == 1
+    for ln, f in zip(lines, faces):
+        assert tuple(int(v) for v in ln[:4]) == f.bbox
+        assert np.float32(float(ln[4])) == np.float32(f.headpose)
+        assert np.array_equal(np.array(ln[5:], np.int32).reshape(10, 2), f.ffd_cordinates)
