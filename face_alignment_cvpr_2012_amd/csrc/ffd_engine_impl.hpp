@@ -117,7 +117,7 @@ struct ffd_engine {
   // traversal tuning: patch block edge G (a workgroup walks all trees of a G x G block of patches
   // over an LDS copy of the block's integral window) and the persistent workgroups (one per CU).
   // Overridable with FFD_TRAV_G_{HP,FFD} / FFD_TRAV_WG / FFD_CHUNK / FFD_STREAMS.
-  int trav_g_hp = 4, trav_g_mp = 4, trav_wg = 256;
+  int trav_g_hp = 4, trav_g_mp = 5, trav_wg = 256;
 
   // model parameters
   int face_size = 125, patch = 31, hp_trees = 0, n_forests = 0, ntrees_per_forest = 0;

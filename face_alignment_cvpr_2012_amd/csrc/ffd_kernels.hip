@@ -650,16 +650,18 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 #ifndef FFD_TRAV_PROBE
 #define FFD_TRAV_PROBE 0  // timing probes (tools/probe.sh): 1 = stage only, 2 = walk only
 #endif
-#ifndef FFD_TRAV_NW
-#define FFD_TRAV_NW 320
-#endif
-constexpr int TRAV_NT = 1024, TRAV_NW = FFD_TRAV_NW, TRAV_NS = TRAV_NT - TRAV_NW;
+// Walker threads per workgroup by patch-block edge G: a block's G*G*T walks run in one round (T = 20
+// FFD trees: 4x4 -> 320, 5x5 -> 500 of 512), the other threads stage the next window.  A block costs
+// about its longest walk chain, so the walks a window holds per block set the throughput: FFD 5x5
+// blocks with 512 walkers took the FFD pass from 10.4 to 8.6 ms at C2 (profiles/r2c).
+constexpr int TRAV_NT = 1024;
+__host__ __device__ constexpr int trav_nw(int G) { return G >= 5 ? 512 : 320; }
 // Window chunks held in registers per staging thread: 16-byte chunks when the window row pitch is
 // a multiple of 8 columns, else 8-byte chunks (the pitch also sets the LDS bank pattern of the
 // rectangle reads, so it is not padded up).
-template <int CB> struct TravStage;
-template <> struct TravStage<8> { static constexpr int U = (20480 + TRAV_NS - 1) / TRAV_NS; typedef uint32_t T __attribute__((ext_vector_type(2))); };
-template <> struct TravStage<16> { static constexpr int U = (11000 + TRAV_NS - 1) / TRAV_NS; typedef uint32_t T __attribute__((ext_vector_type(4))); };
+template <int CB, int NS> struct TravStage;
+template <int NS> struct TravStage<8, NS> { static constexpr int U = (20480 + NS - 1) / NS; typedef uint32_t T __attribute__((ext_vector_type(2))); };
+template <int NS> struct TravStage<16, NS> { static constexpr int U = (11000 + NS - 1) / NS; typedef uint32_t T __attribute__((ext_vector_type(4))); };
 
 // LDS row pitch (u16) of a traversal window WW columns wide staged from a 4-element aligned column.
 #ifndef FFD_TRAV_PITCH8
@@ -708,8 +710,8 @@ template <bool HP, int G, int CB>
 __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* win = reinterpret_cast<uint16_t*>(smem);
-  constexpr int NW = TRAV_NW, NS = TRAV_NS, U = TravStage<CB>::U, GG = G * G;
-  typedef typename TravStage<CB>::T chunk_t;
+  constexpr int NW = trav_nw(G), NS = TRAV_NT - NW, U = TravStage<CB, NS>::U, GG = G * G;
+  typedef typename TravStage<CB, NS>::T chunk_t;
   const int tid = threadIdx.x;
   // window: WW integral columns x WH rows (steps may differ per axis: step_y, C4's (2, 1) grid)
   const int step = A.step, stepy = A.step_y, WW = 32 + step * (G - 1), WH = 32 + stepy * (G - 1);
@@ -1446,7 +1448,9 @@ bool traverse_window_fits(int G, int step, int step_y, int lds_cap) {
   const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1);
   const int cb = trav_chunk_bytes(WW);
   return traverse_lds_bytes(G, step, step_y) <= lds_cap &&
-         NCH * WH * (trav_row_pitch(WW) * 2 / cb) <= TRAV_NS * (cb == 16 ? TravStage<16>::U : TravStage<8>::U);
+         NCH * WH * (trav_row_pitch(WW) * 2 / cb) <=
+             ((G >= 5) ? (TRAV_NT - trav_nw(5)) * (cb == 16 ? TravStage<16, TRAV_NT - trav_nw(5)>::U : TravStage<8, TRAV_NT - trav_nw(5)>::U)
+                       : (TRAV_NT - trav_nw(4)) * (cb == 16 ? TravStage<16, TRAV_NT - trav_nw(4)>::U : TravStage<8, TRAV_NT - trav_nw(4)>::U));
 }
 
 void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* pairs, const uint4* tops,
