@@ -56,13 +56,13 @@ void widen_integrals(const uint16_t* J, int64_t plane, int W, int H, uint32_t* o
   }
 }
 
-// Traversal workgroups per face: one per G x G block of the face's patch grid (max over the chunk).
-int blocks_per_face(const std::vector<FaceDesc>& fds, bool hp, int G) {
+// Traversal workgroups per face: one per gx x gy block of the face's patch grid (max over the chunk).
+int blocks_per_face(const std::vector<FaceDesc>& fds, bool hp, TravShape g) {
   int m = 0;
   for (const auto& f : fds)
     if (f.valid) {
       const int nx = hp ? f.nhx : f.nmx, ny = hp ? f.nhy : f.nmy;
-      m = std::max(m, ((nx + G - 1) / G) * ((ny + G - 1) / G));
+      m = std::max(m, ((nx + g.gx - 1) / g.gx) * ((ny + g.gy - 1) / g.gy));
     }
   return m;
 }
@@ -713,8 +713,13 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   std::unique_ptr<ffd_engine> e(new ffd_engine());
   e->desc = *d;
   e->device = d->device;
-  if (const char* v = std::getenv("FFD_TRAV_G_HP")) e->trav_g_hp = std::max(3, std::min(5, std::atoi(v)));
-  if (const char* v = std::getenv("FFD_TRAV_G_FFD")) e->trav_g_mp = std::max(3, std::min(5, std::atoi(v)));
+  auto shape = [](const char* v, TravShape& g) {  // "G" or "GXxGY"
+    int x = 0, y = 0;
+    if (std::sscanf(v, "%dx%d", &x, &y) == 2) g = TravShape{x, y};
+    else if (std::sscanf(v, "%d", &x) == 1) g = TravShape{x, x};
+  };
+  if (const char* v = std::getenv("FFD_TRAV_G_HP")) shape(v, e->trav_g_hp);
+  if (const char* v = std::getenv("FFD_TRAV_G_FFD")) shape(v, e->trav_g_mp);
   if (const char* v = std::getenv("FFD_TRAV_WG")) e->trav_wg = std::max(8, std::atoi(v));
   if (const char* v = std::getenv("FFD_TRAV_TOPMAX")) e->trav_top_max = std::max(1, std::min(TOP_CAP, std::atoi(v)));
   if (const char* v = std::getenv("FFD_CHANNEL_STREAMS")) e->channel_streams = std::max(1, std::min(4, std::atoi(v)));

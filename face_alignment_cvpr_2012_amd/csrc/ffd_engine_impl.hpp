@@ -117,7 +117,8 @@ struct ffd_engine {
   // traversal tuning: patch block edge G (a workgroup walks all trees of a G x G block of patches
   // over an LDS copy of the block's integral window) and the persistent workgroups (one per CU).
   // Overridable with FFD_TRAV_G_{HP,FFD} / FFD_TRAV_WG / FFD_CHUNK / FFD_STREAMS.
-  int trav_g_hp = 4, trav_g_mp = 5, trav_wg = 256;
+  TravShape trav_g_hp{5, 4}, trav_g_mp{5, 5};
+  int trav_wg = 256;
 
   // model parameters
   int face_size = 125, patch = 31, hp_trees = 0, n_forests = 0, ntrees_per_forest = 0;
@@ -223,14 +224,18 @@ struct ffd_engine {
   // the patch block if needed, and raise the kernels' dynamic-LDS limit.
   void check_traverse_lds() {
     const int cap = TRAV_LDS_CAP;
-    auto fit = [&](int& G, int step, int step_y) {
-      while (!traverse_window_fits(G, step, step_y, cap)) {
-        if (G <= 3) throw std::runtime_error("traversal window does not fit in LDS (step size too large)");
-        G--;
-      }
+    // the preferred shape, else the shapes below it (instantiated in ffd_kernels.hip) that fit
+    auto fit = [&](TravShape& g, bool hp, int step, int step_y) {
+      const TravShape cands[] = {g, {5, 5}, {5, 4}, {4, 4}, {3, 3}};
+      for (const TravShape& c : cands)
+        if (c.gx * c.gy <= g.gx * g.gy && traverse_shape_supported(c, hp) && traverse_window_fits(c, hp, step, step_y, cap)) {
+          g = c;
+          return;
+        }
+      throw std::runtime_error("traversal window does not fit in LDS (step size too large)");
     };
-    fit(trav_g_hp, desc.hp_option.step_size, desc.hp_option.step_size);
-    fit(trav_g_mp, desc.mp_option.step_size, mp_step_y());
+    fit(trav_g_hp, true, desc.hp_option.step_size, desc.hp_option.step_size);
+    fit(trav_g_mp, false, desc.mp_option.step_size, mp_step_y());
     auto pairs = [&](std::vector<uint4>& h, std::vector<int32_t>& roots, DevBuf& d, DevBuf& droots, DevBuf& dfar,
                      DevBuf& dtops, DevBuf& dtopi) {
       std::vector<uint4> pr, tops;

@@ -655,7 +655,7 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 // about its longest walk chain, so the walks a window holds per block set the throughput: FFD 5x5
 // blocks with 512 walkers took the FFD pass from 10.4 to 8.6 ms at C2 (profiles/r2c).
 constexpr int TRAV_NT = 1024;
-__host__ __device__ constexpr int trav_nw(int G) { return G >= 5 ? 512 : 320; }
+__host__ __device__ constexpr int trav_nw(int GX, int GY, bool HP) { return GX * GY * (HP ? 15 : 20) <= 320 ? 320 : 512; }
 // Window chunks held in registers per staging thread: 16-byte chunks when the window row pitch is
 // a multiple of 8 columns, else 8-byte chunks (the pitch also sets the LDS bank pattern of the
 // rectangle reads, so it is not padded up).
@@ -663,18 +663,21 @@ template <int CB, int NS> struct TravStage;
 template <int NS> struct TravStage<8, NS> { static constexpr int U = (20480 + NS - 1) / NS; typedef uint32_t T __attribute__((ext_vector_type(2))); };
 template <int NS> struct TravStage<16, NS> { static constexpr int U = (11000 + NS - 1) / NS; typedef uint32_t T __attribute__((ext_vector_type(4))); };
 
-// LDS row pitch (u16) of a traversal window WW columns wide staged from a 4-element aligned column.
+// LDS row pitch (u16) of a traversal window WW columns wide staged from a 4-element aligned column:
+// a block starting at patch x px0 is staged from column px0 & ~3, so a step that is not a multiple of
+// 4 needs up to 3 columns of slack.
 #ifndef FFD_TRAV_PITCH8
 #define FFD_TRAV_PITCH8 0  // 1: window pitch a multiple of 8 columns (16-byte staging chunks)
 #endif
-__host__ __device__ __forceinline__ int trav_row_pitch(int WW) {
-  return FFD_TRAV_PITCH8 ? (WW + 3 + 7) & ~7 : (WW + 3 + 3) & ~3;
+__host__ __device__ __forceinline__ int trav_row_pitch(int WW, int step) {
+  const int pad = (step & 3) ? 3 : 0;
+  return FFD_TRAV_PITCH8 ? (WW + pad + 7) & ~7 : (WW + pad + 3) & ~3;
 }
-__host__ __device__ __forceinline__ int trav_chunk_bytes(int WW) { return trav_row_pitch(WW) % 8 == 0 ? 16 : 8; }
+__host__ __device__ __forceinline__ int trav_chunk_bytes(int WW, int step) { return trav_row_pitch(WW, step) % 8 == 0 ? 16 : 8; }
 
 // Window bytes (16-byte aligned); the block's tree tops follow it (trav_top_n).
-__host__ __device__ __forceinline__ int trav_window_bytes(int WW, int WH) {
-  return (NCH * WH * trav_row_pitch(WW) * 2 + 15) & ~15;
+__host__ __device__ __forceinline__ int trav_window_bytes(int WW, int WH, int step) {
+  return (NCH * WH * trav_row_pitch(WW, step) * 2 + 15) & ~15;
 }
 
 // Tree tops in LDS: for each of the block's T trees the first TOPN entries of its heap-ordered top
@@ -706,18 +709,18 @@ struct TravArgs {
   int32_t* leaf_out;
 };
 
-template <bool HP, int G, int CB>
+template <bool HP, int GX, int GY, int CB>
 __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* win = reinterpret_cast<uint16_t*>(smem);
-  constexpr int NW = trav_nw(G), NS = TRAV_NT - NW, U = TravStage<CB, NS>::U, GG = G * G;
+  constexpr int NW = trav_nw(GX, GY, HP), NS = TRAV_NT - NW, U = TravStage<CB, NS>::U, GG = GX * GY;
   typedef typename TravStage<CB, NS>::T chunk_t;
   const int tid = threadIdx.x;
   // window: WW integral columns x WH rows (steps may differ per axis: step_y, C4's (2, 1) grid)
-  const int step = A.step, stepy = A.step_y, WW = 32 + step * (G - 1), WH = 32 + stepy * (G - 1);
-  const int LW = trav_row_pitch(WW), nq = LW * 2 / CB;
+  const int step = A.step, stepy = A.step_y, WW = 32 + step * (GX - 1), WH = 32 + stepy * (GY - 1);
+  const int LW = trav_row_pitch(WW, step), nq = LW * 2 / CB;
   const int total = NCH * WH * nq;  // chunks per window (host guarantees <= NS * U)
-  uint4* top_rec = reinterpret_cast<uint4*>(smem + trav_window_bytes(WW, WH));  // [t][TOPN] heap-ordered pairs
+  uint4* top_rec = reinterpret_cast<uint4*>(smem + trav_window_bytes(WW, WH, step));  // [t][TOPN] heap-ordered pairs
   // XCD-contiguous, face-major block range of this workgroup's XCD; workgroups of one XCD stride it
   const int N = A.n_faces * A.bpf, xcd = blockIdx.x & 7, k = blockIdx.x >> 3, nk = gridDim.x >> 3;
   const int q8 = N >> 3, r8 = N & 7;
@@ -735,9 +738,9 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     const FaceDesc& fd = A.faces[B.f];
     B.nx = HP ? fd.nhx : fd.nmx;
     B.ny = HP ? fd.nhy : fd.nmy;
-    const int gbx = max(1, (B.nx + G - 1) / G), gby = (B.ny + G - 1) / G;
-    B.xi0 = (b % gbx) * G;
-    B.yi0 = (b / gbx) * G;
+    const int gbx = max(1, (B.nx + GX - 1) / GX), gby = (B.ny + GY - 1) / GY;
+    B.xi0 = (b % gbx) * GX;
+    B.yi0 = (b / gbx) * GY;
     B.px0 = B.xi0 * step;
     B.py0 = B.yi0 * stepy;
     B.T = 0;
@@ -757,7 +760,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     const uint32_t* top_i = reinterpret_cast<const uint32_t*>(top_rec + B.T * topn);
     for (int item = tid; item < items; item += NW) {
       const int t = item / GG, pl = item - t * GG;
-      const int xi = B.xi0 + pl % G, yi = B.yi0 + pl / G;
+      const int xi = B.xi0 + pl % GX, yi = B.yi0 + pl / GX;
       if (xi >= B.nx || yi >= B.ny) continue;
       // byte address of the patch's top-left integral corner in channel 0's window plane
       const unsigned char* base = reinterpret_cast<const unsigned char*>(win) +
@@ -1439,42 +1442,51 @@ void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t
   if (n > 0) k_integral<<<n, 256, 0, s>>>(faces, gray, chan);
 }
 
-int traverse_lds_bytes(int G, int step, int step_y) {
-  const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1);
-  return trav_window_bytes(WW, WH) + MAX_TREES * 20;  // window + at least the block's root pairs
+int traverse_lds_bytes(TravShape g, int step, int step_y) {
+  const int WW = 32 + step * (g.gx - 1), WH = 32 + step_y * (g.gy - 1);
+  return trav_window_bytes(WW, WH, step) + MAX_TREES * 20;  // window + at least the block's root pairs
 }
 
-bool traverse_window_fits(int G, int step, int step_y, int lds_cap) {
-  const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1);
-  const int cb = trav_chunk_bytes(WW);
-  return traverse_lds_bytes(G, step, step_y) <= lds_cap &&
-         NCH * WH * (trav_row_pitch(WW) * 2 / cb) <=
-             ((G >= 5) ? (TRAV_NT - trav_nw(5)) * (cb == 16 ? TravStage<16, TRAV_NT - trav_nw(5)>::U : TravStage<8, TRAV_NT - trav_nw(5)>::U)
-                       : (TRAV_NT - trav_nw(4)) * (cb == 16 ? TravStage<16, TRAV_NT - trav_nw(4)>::U : TravStage<8, TRAV_NT - trav_nw(4)>::U));
+bool traverse_window_fits(TravShape g, bool hp, int step, int step_y, int lds_cap) {
+  const int WW = 32 + step * (g.gx - 1), WH = 32 + step_y * (g.gy - 1);
+  const int cb = trav_chunk_bytes(WW, step);
+  const int ns = TRAV_NT - trav_nw(g.gx, g.gy, hp);
+  const int u = ns == TRAV_NT - 512 ? (cb == 16 ? TravStage<16, TRAV_NT - 512>::U : TravStage<8, TRAV_NT - 512>::U)
+                                    : (cb == 16 ? TravStage<16, TRAV_NT - 320>::U : TravStage<8, TRAV_NT - 320>::U);
+  return traverse_lds_bytes(g, step, step_y) <= lds_cap && NCH * WH * (trav_row_pitch(WW, step) * 2 / cb) <= ns * u;
 }
 
-void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* pairs, const uint4* tops,
+// The block shapes instantiated (x x y patches): head pose 4x4, 5x4, 3x3; FFD 5x5, 4x4, 3x3.
+#define FFD_TRAV_SHAPES(X)                                                                              \
+  X(true, 4, 4) X(true, 5, 4) X(true, 3, 3) X(false, 5, 5) X(false, 4, 4) X(false, 3, 3)
+
+bool traverse_shape_supported(TravShape g, bool hp) {
+#define FFD_TRAV_SUP(HPV, GXV, GYV) if (hp == HPV && g.gx == GXV && g.gy == GYV) return true;
+  FFD_TRAV_SHAPES(FFD_TRAV_SUP)
+#undef FFD_TRAV_SUP
+  return false;
+}
+
+void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, TravShape g, const uint4* pairs, const uint4* tops,
                      const uint32_t* top_idx, int top_max, const uint32_t* far, const HpState* state, int ntrees_hp,
                      int step, int step_y, int64_t plane, const uint16_t* chan, int32_t* leaf_out, int n_wg,
                      int lds_cap, hipStream_t s) {
   const int total_blocks = n * bpf;
   if (total_blocks <= 0) return;
   // the window, then as many tree-top entries as the rest of the CU's LDS holds
-  const int WW = 32 + step * (G - 1), WH = 32 + step_y * (G - 1), lds = lds_cap;
-  TravArgs A{faces, n, bpf, pairs, tops, top_idx, lds - trav_window_bytes(WW, WH), top_max, far, state, ntrees_hp,
-             step, step_y, (int)plane, chan, leaf_out};
+  const int WW = 32 + step * (g.gx - 1), WH = 32 + step_y * (g.gy - 1), lds = lds_cap;
+  TravArgs A{faces, n, bpf, pairs, tops, top_idx, lds - trav_window_bytes(WW, WH, step), top_max, far, state,
+             ntrees_hp, step, step_y, (int)plane, chan, leaf_out};
   const int grid = std::max(8, n_wg & ~7);
-#define FFD_TRAV(HPV, GV)                                                                              \
-  do {                                                                                                 \
-    if (trav_chunk_bytes(32 + step * (GV - 1)) == 16) k_traverse<HPV, GV, 16><<<grid, TRAV_NT, lds, s>>>(A); \
-    else k_traverse<HPV, GV, 8><<<grid, TRAV_NT, lds, s>>>(A);                                          \
-  } while (0)
-  if (hp) {
-    if (G == 3) FFD_TRAV(true, 3); else if (G == 5) FFD_TRAV(true, 5); else FFD_TRAV(true, 4);
-  } else {
-    if (G == 3) FFD_TRAV(false, 3); else if (G == 5) FFD_TRAV(false, 5); else FFD_TRAV(false, 4);
+  const bool c16 = trav_chunk_bytes(WW, step) == 16;
+#define FFD_TRAV_LAUNCH(HPV, GXV, GYV)                                                    \
+  if (hp == HPV && g.gx == GXV && g.gy == GYV) {                                          \
+    if (c16) k_traverse<HPV, GXV, GYV, 16><<<grid, TRAV_NT, lds, s>>>(A);                 \
+    else k_traverse<HPV, GXV, GYV, 8><<<grid, TRAV_NT, lds, s>>>(A);                      \
+    return;                                                                               \
   }
-#undef FFD_TRAV
+  FFD_TRAV_SHAPES(FFD_TRAV_LAUNCH)
+#undef FFD_TRAV_LAUNCH
 }
 
 hipError_t set_gabor_lds_limit(int bytes) {
@@ -1490,16 +1502,13 @@ hipError_t set_gabor_lds_limit(int bytes) {
 
 hipError_t set_traverse_lds_limit(int bytes) {
   hipError_t e = hipSuccess;
-  const void* fns[] = {(const void*)k_traverse<true, 3, 8>,  (const void*)k_traverse<true, 4, 8>,
-                       (const void*)k_traverse<true, 5, 8>,  (const void*)k_traverse<false, 3, 8>,
-                       (const void*)k_traverse<false, 4, 8>, (const void*)k_traverse<false, 5, 8>,
-                       (const void*)k_traverse<true, 3, 16>,  (const void*)k_traverse<true, 4, 16>,
-                       (const void*)k_traverse<true, 5, 16>,  (const void*)k_traverse<false, 3, 16>,
-                       (const void*)k_traverse<false, 4, 16>, (const void*)k_traverse<false, 5, 16>};
-  for (const void* f : fns) {
-    hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    if (r != hipSuccess) e = r;
+#define FFD_TRAV_ATTR(HPV, GXV, GYV)                                                                     \
+  for (const void* f : {(const void*)k_traverse<HPV, GXV, GYV, 8>, (const void*)k_traverse<HPV, GXV, GYV, 16>}) { \
+    hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);            \
+    if (r != hipSuccess) e = r;                                                                          \
   }
+  FFD_TRAV_SHAPES(FFD_TRAV_ATTR)
+#undef FFD_TRAV_ATTR
   return e;
 }
 

@@ -32,13 +32,18 @@ hipError_t set_gabor_lds_limit(int bytes);
 // integral channels 0 (gray), 36, 37 (Sobel)
 void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t* chan, hipStream_t s);
 constexpr int TRAV_LDS_CAP = 160 * 1024;  // one traversal workgroup per CU: all of its LDS
-int traverse_lds_bytes(int G, int step, int step_y);
-bool traverse_window_fits(int G, int step, int step_y, int lds_cap);
+// patch block of a traversal workgroup: gx x gy patches of one face's grid
+struct TravShape {
+  int gx, gy;
+};
+int traverse_lds_bytes(TravShape g, int step, int step_y);
+bool traverse_window_fits(TravShape g, bool hp, int step, int step_y, int lds_cap);
+bool traverse_shape_supported(TravShape g, bool hp);  // an instantiated k_traverse shape
 // plane: the channel plane stride shared by every face of the batch; n_wg: persistent workgroups (one per CU; rounded down to a multiple of 8 XCDs)
 // pairs / far: the forest's pair records (ffd_device.hpp) and far offsets; tops / top_idx: per tree
 // TOP_CAP heap-ordered pair records of its top levels and their pair indices (at most top_max
 // entries per tree are staged into LDS); lds_cap: dynamic LDS of a workgroup (window + tops)
-void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, int G, const uint4* pairs, const uint4* tops,
+void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, TravShape g, const uint4* pairs, const uint4* tops,
                      const uint32_t* top_idx, int top_max, const uint32_t* far, const HpState* state, int ntrees_hp,
                      int step, int step_y, int64_t plane, const uint16_t* chan, int32_t* leaf_out, int n_wg,
                      int lds_cap, hipStream_t s);
