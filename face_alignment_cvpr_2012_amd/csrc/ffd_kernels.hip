@@ -449,7 +449,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
   }
 
 #pragma unroll 1
-  for (int y0 = 0; y0 < FH; y0 += GS_BY) {
+  for (int y0 = 0; y0 < (FFD_GABOR_PROBE == 5 ? 0 : FH); y0 += GS_BY) {  // probe 5: epilogue only
     __syncthreads();  // the face is staged; the previous H pass is done with vg / vq
     // ---- V pass
 #pragma unroll 1
