@@ -941,74 +941,88 @@ __global__ void k_eval_patches(const uint4* __restrict__ nodes, const int32_t* _
 
 // -------------------------------------------------- head pose + tree choice --
 // getHeadPoseVotesMT reduction (face_utils.cpp:218-241) + areaUnderCurve (face_utils.cpp:304-323)
-// + tree selection (FaceForest.cpp:214-250).  One wave per face: the 64 lanes gather the leaf
-// values of 64 consecutive (patch, tree) pairs in the reference order (patch-major x-outer,
-// tree-minor) and compute m and m*m per element (element-wise, same rounding as the serial
-// loop); the running sums are then advanced IN ORDER with one add per element (readlane), so
-// they equal the reference's sequential float sums bit for bit.  Filtered-out leaves add +0,
-// which leaves a non-negative float sum unchanged.
-__device__ __forceinline__ float lane_f(float v, int lane) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
-}
+// + tree selection (FaceForest.cpp:214-250).  One LANE per face: the three running float sums
+// (count, sum m, sum m*m) are sequential by definition (the reference adds in leaf order: patch-major
+// x-outer, tree-minor), so each lane walks its own face's leaf list in that order; a wave advances
+// 64 faces' chains at once.  The leaf ids arrive 4 per 16-byte load and the leaf values are gathered
+// one batch ahead of the adds (double-buffered), so the chain waits on arithmetic, not memory.
+// Filtered-out leaves add +0, which leaves a non-negative float sum unchanged.
+constexpr int HPB = 64;  // leaves per batch
 
-__global__ __launch_bounds__(256) void k_hp_pose(const FaceDesc* __restrict__ faces, int n_faces,
-                                                 const int32_t* __restrict__ hp_leaf, const float* __restrict__ hp_m,
-                                                 int hp_trees, int n_forests, int ntrees_per_forest,
-                                                 HpState* __restrict__ state, FaceOut* __restrict__ out) {
-  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+__global__ __launch_bounds__(64) void k_hp_pose(const FaceDesc* __restrict__ faces, int n_faces,
+                                                const int32_t* __restrict__ hp_leaf, const float* __restrict__ hp_m,
+                                                int hp_trees, int n_forests, int ntrees_per_forest,
+                                                HpState* __restrict__ state, FaceOut* __restrict__ out) {
+  const int f = blockIdx.x * 64 + threadIdx.x;
   if (f >= n_faces) return;
   const FaceDesc& fd = faces[f];
   FaceOut& o = out[f];
-  if (lane == 0) { o.bbox[0] = fd.bx; o.bbox[1] = fd.by; o.bbox[2] = fd.bw; o.bbox[3] = fd.bh; }
+  o.bbox[0] = fd.bx; o.bbox[1] = fd.by; o.bbox[2] = fd.bw; o.bbox[3] = fd.bh;
   if (!fd.valid) {
-    if (lane == 0) { o.status = fd.reject; o.n_trees = 0; state[f].n_trees = 0; }
+    o.status = fd.reject; o.n_trees = 0; state[f].n_trees = 0;
     return;
   }
-  const int nx = fd.nhx, ny = fd.nhy, n = nx * ny, T = hp_trees, total = n * T;
+  const int total = fd.nhx * fd.nhy * hp_trees;
   const int32_t* L = hp_leaf + fd.hp_off;
-  float cnt = 0, sum = 0, sum_sq = 0;
-  for (int base = 0; base < total; base += 64) {
-    const int k = base + lane;
-    float m = 0.f, mm = 0.f, one = 0.f;
-    if (k < total) {
-      const float v = hp_m[L[k]];  // leaves are stored in the reference order
-      if (v >= 0.f) { m = v; mm = v * v; one = 1.f; }
+  float sum = 0, sum_sq = 0;
+  int count = 0;  // leaves that pass: the reference's float count of +1s is exact below 2^24
+  // three-stage pipeline over batches of HPB leaves: ids of batch b + 2 and values of batch b + 1
+  // are in flight while batch b is added
+  int ids[HPB];
+  float va[HPB], vb[HPB];
+  auto load_ids = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < HPB; i++) ids[i] = k0 + i < total ? L[k0 + i] : -1;
+  };
+  auto gather = [&](float (&v)[HPB]) {  // -1: filtered leaf or past the end
+#pragma unroll
+    for (int i = 0; i < HPB; i++) v[i] = ids[i] >= 0 ? hp_m[ids[i]] : -1.f;
+  };
+  auto add = [&](const float (&v)[HPB]) {
+#pragma unroll
+    for (int i = 0; i < HPB; i++) {
+      const bool in = v[i] >= 0.f;
+      const float m = in ? v[i] : 0.f;
+      sum += m;
+      sum_sq += in ? m * m : 0.f;
+      count += in ? 1 : 0;
     }
-    const int lim = min(64, total - base);
-    for (int j = 0; j < lim; j++) {
-      sum += lane_f(m, j);
-      sum_sq += lane_f(mm, j);
-      cnt += lane_f(one, j);
-    }
+  };
+  load_ids(0);
+  gather(va);
+  load_ids(HPB);
+  for (int k0 = 0; k0 < total; k0 += 2 * HPB) {
+    gather(vb);
+    load_ids(k0 + 2 * HPB);
+    add(va);
+    if (k0 + HPB >= total) break;
+    gather(va);
+    load_ids(k0 + 3 * HPB);
+    add(vb);
   }
+  const float cnt = (float)count;
   float mean = sum / cnt;
   float var = (sum_sq / cnt) - (mean * mean);
   mean -= 2;
   var *= 0.05f;  // NORM_HEADPOSE_VARIANCE_FACTOR
-  // areaUnderCurve per pose bin: lane j < n_forests integrates bin j
-  const float poseT[6] = {-2.5f, -0.35f, -0.20f, 0.20f, 0.35f, 2.5f};
-  float area = 0.f;
-  if (lane < n_forests) {
-    const double dmean = (double)mean, dstd = __builtin_sqrt((double)var);
-    double acc = 0, step = 0.01, tt;
-    for (double x = poseT[lane]; x < (double)poseT[lane + 1]; x += step) {
-      tt = (x - dmean) / dstd;
-      acc += ffd_exp(-0.5 * (tt * tt)) * step;
-    }
-    area = (float)(acc * 1.0 / (dstd * 2.5066282746310002));
-  }
-  if (lane != 0) return;
   o.status = 0;
   o.headpose = mean;
   o.pose_variance = var;
   HpState& s = state[f];
   s.headpose = mean;
   s.variance = var;
+  // areaUnderCurve per pose bin (fp64 left Riemann sums), dominant = first strict maximum
+  const float poseT[6] = {-2.5f, -0.35f, -0.20f, 0.20f, 0.35f, 2.5f};
+  const double dmean = (double)mean, dstd = __builtin_sqrt((double)var);
   float max_area = 0;
   int dominant = 0;
   for (int j = 0; j < n_forests; j++) {
-    const float a = lane_f(area, j);
+    double acc = 0, step = 0.01, tt;
+    for (double x = poseT[j]; x < (double)poseT[j + 1]; x += step) {
+      tt = (x - dmean) / dstd;
+      acc += ffd_exp(-0.5 * (tt * tt)) * step;
+    }
+    const float a = (float)(acc * 1.0 / (dstd * 2.5066282746310002));
     s.pose_freq[j] = a;
     if (max_area < a) { max_area = a; dominant = j; }
   }
@@ -1524,7 +1538,7 @@ void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t
 
 void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const float* hp_m, int hp_trees,
                     int n_forests, int ntrees_per_forest, HpState* state, FaceOut* out, hipStream_t s) {
-  k_hp_pose<<<(n + 3) / 4, 256, 0, s>>>(faces, n, hp_leaf, hp_m, hp_trees, n_forests, ntrees_per_forest, state, out);
+  k_hp_pose<<<(n + 63) / 64, 64, 0, s>>>(faces, n, hp_leaf, hp_m, hp_trees, n_forests, ntrees_per_forest, state, out);
 }
 
 void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint4* leaf_rec, bool compact,
