@@ -1134,29 +1134,43 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
 }
 
 // -------------------------------------------------------------- MeanShift ----
-// MeanShift::shift (MeanShift.hpp:41-135) for one landmark of 64 faces per workgroup, then the
+// MeanShift::shift (MeanShift.hpp:41-135) for one landmark of MS_FACES faces per workgroup, then the
 // rescale of FaceForest.cpp:255-257.  Each pass walks the vote lists in tiles of MS_TILE votes:
 //   parallel phase: all 256 threads compute the per-vote terms (x*w, y*w, w) — element-wise ops
 //                   with the reference's rounding — into LDS;
 //   serial phase:   lane p (one per face) adds its face's MS_TILE terms in list order,
 // so every running sum equals the reference's sequential float sum bit for bit.
 #ifndef FFD_MS_FACES
-#define FFD_MS_FACES 16
+#define FFD_MS_FACES 20  // 4096 faces x 10 landmarks = 2048 workgroups = one round of 8 per CU
 #endif
 #ifndef FFD_MS_TILE
 #define FFD_MS_TILE 64
-#endif
-#ifndef FFD_MS_GRP
-#define FFD_MS_GRP 1
 #endif
 #ifndef FFD_MS_THREADS
 #define FFD_MS_THREADS 256
 #endif
 constexpr int MS_FACES = FFD_MS_FACES, MS_TILE = FFD_MS_TILE, MS_LD = MS_FACES + 1, MS_THREADS = FFD_MS_THREADS;
-constexpr int MS_GRP = FFD_MS_GRP;
+static_assert(MS_TILE == 64 && MS_THREADS == 256, "k_meanshift maps a face's tile onto one of 4 waves");
+constexpr int MS_FPW = (MS_FACES + 3) / 4;  // faces per wave
+#ifndef FFD_MS_RA
+#define FFD_MS_RA 4
+#endif
+constexpr int MS_RA = FFD_MS_RA;  // serial phase: LDS reads in flight ahead of the adds
 
-__global__ __launch_bounds__(MS_THREADS) void k_meanshift(const FaceDesc* __restrict__ faces, int n_faces,
-                                                   int tslots, int n_parts, float lamda, int max_iter,
+// MeanShift::getWeightedMean's weight of one vote (MeanShift.hpp:122-124): d = cv::norm(mean - pos)
+// (double sqrt, rounded to float), w = weight * expf(-d / lamda).  lam_y > 0: RN(1 / lamda) for the
+// exact ffd_div_rcp quotient (lamda == 10 only, checked for every float in tests/test_numerics.py);
+// the argument of the exponential is <= 0, where ffd_expf_nonpos == ffd_expf.
+__device__ __forceinline__ float ms_weight(float mx, float my, float x, float y, float w, float lamda, float lam_y) {
+  const float dx = mx - x, dy = my - y;
+  const float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
+  const float q = lam_y > 0.f ? ffd_div_rcp(-d, lamda, lam_y) : -d / lamda;
+  return w * ffd_expf_nonpos(q);
+}
+
+// 8 waves per SIMD (<= 64 VGPRs): 8 workgroups per CU, so C2's 2048 workgroups run as one round
+__global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_meanshift(const FaceDesc* __restrict__ faces, int n_faces,
+                                                   int tslots, int n_parts, float lamda, float lam_y, int max_iter,
                                                    float stop, const Vote* __restrict__ votes,
                                                    const int32_t* __restrict__ vote_counts,
                                                    float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
@@ -1199,53 +1213,48 @@ __global__ __launch_bounds__(MS_THREADS) void k_meanshift(const FaceDesc* __rest
       if (s_nlive == 0) break;
     }
     ax = ay = aw = 0;
-    for (int k0 = 0; k0 < maxcnt; k0 += MS_TILE) {
-      // parallel phase, in groups of MS_GRP items per thread whose vote loads are issued together
-      // (small groups: the kernel's occupancy is what hides the rest of the latency)
-      for (int i0 = tid; i0 < MS_TILE * MS_FACES; i0 += MS_GRP * MS_THREADS) {
-        Vote v[MS_GRP];
+    // wave w owns faces w + 4 i (i < MS_FPW): a face's MS_TILE = 64 votes of a tile are one wave's lanes,
+    // so its count, list base and mean are wave-uniform.  The votes of tile k0 are loaded into
+    // registers during tile k0 - 64's serial phase (the first tile's here).
+    const int wv = tid >> 6, j = tid & 63;
+    Vote vv[MS_FPW];
+    auto load_tile = [&](int k0) {
 #pragma unroll
-        for (int u = 0; u < MS_GRP; u++) {
-          const int i = i0 + u * MS_THREADS, j = i % MS_TILE, p = i / MS_TILE, k = k0 + j;
-          const bool use = i < MS_TILE * MS_FACES && k < s_cnt[p] && s_live[p];
-          v[u] = use ? votes[s_vb[p] + k] : Vote{0, 0, -1.f};  // w < 0: no vote (real weights are fg > 0.5)
-        }
-#pragma unroll
-        for (int u = 0; u < MS_GRP; u++) {
-          const int i = i0 + u * MS_THREADS, j = i % MS_TILE, p = i / MS_TILE;
-          if (i >= MS_TILE * MS_FACES) break;
-          float px = 0.f, py = 0.f, w = 0.f;
-          if (v[u].w >= 0.f) {
-            if (pass < 0) {
-              w = v[u].w;
-            } else {
-              const float dx = s_mx[p] - (float)v[u].x, dy = s_my[p] - (float)v[u].y;
-              float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
-              d = ffd_expf(-d / lamda);
-              w = v[u].w * d;
-            }
-            px = v[u].x * w;
-            py = v[u].y * w;
-          }
-          tx[j * MS_LD + p] = px;
-          ty[j * MS_LD + p] = py;
-          tw[j * MS_LD + p] = w;
-        }
+      for (int i = 0; i < MS_FPW; i++) {
+        const int p = wv + 4 * i, k = k0 + j;
+        if (p < MS_FACES && s_live[p] && k < s_cnt[p]) vv[i] = votes[s_vb[p] + k];
       }
+    };
+    load_tile(0);
+    for (int k0 = 0; k0 < maxcnt; k0 += MS_TILE) {
+      // parallel phase; faces that converged or whose list ended skip the tile (the serial phase
+      // reads none of it)
+#pragma unroll
+      for (int i = 0; i < MS_FPW; i++) {
+        const int p = wv + 4 * i;
+        if (p >= MS_FACES || !s_live[p] || k0 + j >= s_cnt[p]) continue;
+        const Vote v = vv[i];
+        const float fx = (float)v.x, fy = (float)v.y;
+        const float w = pass < 0 ? v.w : ms_weight(s_mx[p], s_my[p], fx, fy, v.w, lamda, lam_y);
+        tx[j * MS_LD + p] = fx * w;
+        ty[j * MS_LD + p] = fy * w;
+        tw[j * MS_LD + p] = w;
+      }
+      if (k0 + MS_TILE < maxcnt) load_tile(k0 + MS_TILE);  // in flight during the serial phase
       __syncthreads();
       if (tid < MS_FACES && s_live[tid]) {  // serial phase, in list order
         const int lim = min(MS_TILE, s_cnt[tid] - k0);
         int j = 0;
-        for (; j + 8 <= lim; j += 8) {  // LDS reads of 8 terms ahead of their in-order adds
-          float vx[8], vy[8], vw[8];
+        for (; j + MS_RA <= lim; j += MS_RA) {  // LDS reads of MS_RA terms ahead of their in-order adds
+          float vx[MS_RA], vy[MS_RA], vw[MS_RA];
 #pragma unroll
-          for (int q = 0; q < 8; q++) {
+          for (int q = 0; q < MS_RA; q++) {
             vx[q] = tx[(j + q) * MS_LD + tid];
             vy[q] = ty[(j + q) * MS_LD + tid];
             vw[q] = tw[(j + q) * MS_LD + tid];
           }
 #pragma unroll
-          for (int q = 0; q < 8; q++) {
+          for (int q = 0; q < MS_RA; q++) {
             ax += vx[q];
             ay += vy[q];
             aw += vw[q];
@@ -1367,7 +1376,7 @@ __global__ __launch_bounds__(MS2_THREADS) void k_meanshift2(const FaceDesc* __re
             const float dx = s_mx[c] - (float)v[u].x, dy = s_my[c] - (float)v[u].y;
             float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
             d = ffd_expf(-d / lamda);
-            w = v[u].w * d;
+            w = v[u].w * d;  // (the default kernel uses ms_weight's exact fast path)
           }
           px = v[u].x * w;
           py = v[u].y * w;
@@ -1559,8 +1568,9 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
   }();
   if (which == 1) {
     dim3 grid((n + MS_FACES - 1) / MS_FACES, NPARTS);
-    k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, max_iter, stop, votes, vote_counts,
-                                            ms_mean, out);
+    const float lam_y = lamda == 10.f ? 1.f / 10.f : 0.f;  // the verified fast quotient (ffd_div_rcp)
+    k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes,
+                                            vote_counts, ms_mean, out);
   } else {
     dim3 grid((n + MS2_CH - 1) / MS2_CH, NPARTS);
     k_meanshift2<<<grid, MS2_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, max_iter, stop, votes, vote_counts,

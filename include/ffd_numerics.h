@@ -102,4 +102,48 @@ FFD_HD float ffd_expf(float xf) {
   return (float)FFD_LDEXP(p, k);
 }
 
+/* ffd_expf for arguments x <= 0 (MeanShift's -d/lamda, d >= 0 finite): the same operations without
+ * the NaN / overflow branches, which no such argument reaches, and with the underflow test as a
+ * select (no divergent branch on the GPU).  Equal to ffd_expf(x) for every x <= 0, -0 and -inf
+ * included (tests/test_numerics.py). */
+FFD_HD float ffd_expf_nonpos(float xf) {
+  const int under = xf < -104.0f;
+  const double x = (double)(under ? -104.0f : xf);
+  int k;
+  const double r = ffd_exp_reduce(x, &k);
+  double p = 1.0 / 39916800.0;                         /* 1/11! */
+  p = FFD_FMA(p, r, 1.0 / 3628800.0);
+  p = FFD_FMA(p, r, 1.0 / 362880.0);
+  p = FFD_FMA(p, r, 1.0 / 40320.0);
+  p = FFD_FMA(p, r, 1.0 / 5040.0);
+  p = FFD_FMA(p, r, 1.0 / 720.0);
+  p = FFD_FMA(p, r, 1.0 / 120.0);
+  p = FFD_FMA(p, r, 1.0 / 24.0);
+  p = FFD_FMA(p, r, 1.0 / 6.0);
+  p = FFD_FMA(p, r, 0.5);
+  p = FFD_FMA(p, r, 1.0);
+  p = FFD_FMA(p, r, 1.0);
+  const float e = (float)FFD_LDEXP(p, k);
+  return under ? 0.0f : e;
+}
+
+/* a / b for a divisor b whose reciprocal y = RN(1/b) is given: q = RN(a y), r = a - b q (exact with
+ * an fma), RN(q + r y) (Markstein's correction).  It is the correctly rounded quotient whenever the
+ * premises of Markstein's theorem hold (not for subnormal quotients: |a| <= 2^-100 divides
+ * directly); tests/test_numerics.py checks it against IEEE division for
+ * every finite binary32 a at b = 10 (MeanShiftOption::kernel_size's default, MeanShift.hpp:20), the
+ * only divisor the kernels use it for. */
+FFD_HD float ffd_div_rcp(float a, float b, float y) {
+  if (!(a > 0x1p-100f || a < -0x1p-100f)) return a / b;  /* tiny |a| (subnormal quotients): IEEE division */
+#ifdef __cplusplus
+  const float q = a * y;
+  const float r = std::fma(-q, b, a);
+  return std::fma(r, y, q);
+#else
+  const float q = a * y;
+  const float r = fmaf(-q, b, a);
+  return fmaf(r, y, q);
+#endif
+}
+
 #endif /* FFD_NUMERICS_H */

@@ -88,3 +88,27 @@ def test_area_under_curve_partition(oracle_mod):
 def test_gabor_flop_model(w):
     import bench
     assert bench.gabor_flops_per_pixel(w) > 0
+
+
+def _run_numerics_check(which):
+    """Build and run tests/numerics/check_numerics.c (exhaustive, multi-threaded C; see its header)."""
+    import os
+    import subprocess
+    import tempfile
+    here = os.path.dirname(os.path.abspath(__file__))
+    src = os.path.join(here, "numerics", "check_numerics.c")
+    exe = os.path.join(tempfile.mkdtemp(prefix="ffd_num_"), "check_numerics")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", exe, src, "-lm", "-lpthread"], check=True)
+    out = subprocess.run([exe, which], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stdout
+
+
+def test_markstein_division_by_ten_is_ieee_division():
+    """ffd_div_rcp(a, 10, RN(1/10)) == a / 10 for every finite binary32 a (the MeanShift weight's
+    -d/lamda at the default kernel_size, MeanShift.hpp:20,123; k_meanshift's fast quotient)."""
+    _run_numerics_check("div")
+
+
+def test_expf_nonpos_equals_expf():
+    """ffd_expf_nonpos == ffd_expf bitwise for every binary32 x in [-110, 0] (and -inf, -1e30)."""
+    _run_numerics_check("exp")
