@@ -941,101 +941,175 @@ __global__ void k_eval_patches(const uint4* __restrict__ nodes, const int32_t* _
 
 // -------------------------------------------------- head pose + tree choice --
 // getHeadPoseVotesMT reduction (face_utils.cpp:218-241) + areaUnderCurve (face_utils.cpp:304-323)
-// + tree selection (FaceForest.cpp:214-250).  One LANE per face: the three running float sums
-// (count, sum m, sum m*m) are sequential by definition (the reference adds in leaf order: patch-major
-// x-outer, tree-minor), so each lane walks its own face's leaf list in that order; a wave advances
-// 64 faces' chains at once.  The leaf ids arrive 4 per 16-byte load and the leaf values are gathered
-// one batch ahead of the adds (double-buffered), so the chain waits on arithmetic, not memory.
-// Filtered-out leaves add +0, which leaves a non-negative float sum unchanged.
-constexpr int HPB = 64;  // leaves per batch
+// + tree selection (FaceForest.cpp:214-250).  A 256-thread workgroup per HP_FACES faces.  The
+// running float sums (sum m, sum m*m) are sequential by definition (the reference adds in leaf order:
+// patch-major x-outer, tree-minor), so lane p < HP_FACES of wave 0 adds face p's leaves in that order; the
+// leaf values arrive through LDS in tiles of 64 leaves per face, gathered by all four waves (wave w:
+// faces w, w + 4, ...; leaf values three tiles ahead, their ids four, so the serial adds wait on
+// neither).  Filtered-out leaves add +0, which leaves a non-negative float sum unchanged; the count
+// of passing leaves (exact integer) comes from one ballot per face and tile.  Then the five pose-bin
+// integrals (fp64 left Riemann sums) run on five lanes per face and lane p selects the trees.
+constexpr int HP_T = 64;
 
-__global__ __launch_bounds__(64) void k_hp_pose(const FaceDesc* __restrict__ faces, int n_faces,
-                                                const int32_t* __restrict__ hp_leaf, const float* __restrict__ hp_m,
-                                                int hp_trees, int n_forests, int ntrees_per_forest,
-                                                HpState* __restrict__ state, FaceOut* __restrict__ out) {
-  const int f = blockIdx.x * 64 + threadIdx.x;
-  if (f >= n_faces) return;
-  const FaceDesc& fd = faces[f];
-  FaceOut& o = out[f];
-  o.bbox[0] = fd.bx; o.bbox[1] = fd.by; o.bbox[2] = fd.bw; o.bbox[3] = fd.bh;
-  if (!fd.valid) {
-    o.status = fd.reject; o.n_trees = 0; state[f].n_trees = 0;
-    return;
+template <int HP_FACES>
+__global__ __launch_bounds__(256) void k_hp_pose(const FaceDesc* __restrict__ faces, int n_faces,
+                                                 const int32_t* __restrict__ hp_leaf, const float* __restrict__ hp_m,
+                                                 int hp_trees, int n_forests, int ntrees_per_forest,
+                                                 HpState* __restrict__ state, FaceOut* __restrict__ out) {
+  constexpr int HP_LD = HP_FACES + 1, HP_FPW = HP_FACES / 4;
+  static_assert(HP_FACES % 4 == 0 && HP_FACES * 8 <= 256, "faces per workgroup");
+  __shared__ float tm[HP_T * HP_LD], tq[HP_T * HP_LD];  // [leaf][face]: m (0 if filtered), m * m (0)
+  __shared__ int s_total[HP_FACES], s_tcnt[HP_FACES], s_valid[HP_FACES];
+  __shared__ int64_t s_off[HP_FACES];
+  __shared__ int s_max;
+  __shared__ float s_mean[HP_FACES], s_var[HP_FACES], s_area[HP_FACES][8];
+  const int f0 = blockIdx.x * HP_FACES, tid = threadIdx.x, wv = tid >> 6, j = tid & 63;
+  if (tid == 0) s_max = 0;
+  __syncthreads();
+  if (tid < HP_FACES) {
+    const int f = f0 + tid;
+    int total = 0, valid = 0;
+    int64_t off = 0;
+    if (f < n_faces) {
+      const FaceDesc& fd = faces[f];
+      FaceOut& o = out[f];
+      o.bbox[0] = fd.bx; o.bbox[1] = fd.by; o.bbox[2] = fd.bw; o.bbox[3] = fd.bh;
+      if (fd.valid) {  // (no head-pose patch: total 0, the reference's 0 / 0 pose)
+        total = fd.nhx * fd.nhy * hp_trees;
+        off = fd.hp_off;
+        valid = 1;
+      } else {
+        o.status = fd.reject; o.n_trees = 0; state[f].n_trees = 0;
+      }
+    }
+    s_total[tid] = total;
+    s_off[tid] = off;
+    s_valid[tid] = valid;
+    atomicMax(&s_max, total);
   }
-  const int total = fd.nhx * fd.nhy * hp_trees;
-  const int32_t* L = hp_leaf + fd.hp_off;
-  float sum = 0, sum_sq = 0;
-  int count = 0;  // leaves that pass: the reference's float count of +1s is exact below 2^24
-  // three-stage pipeline over batches of HPB leaves: ids of batch b + 2 and values of batch b + 1
-  // are in flight while batch b is added
-  int ids[HPB];
-  float va[HPB], vb[HPB];
+  __syncthreads();
+  const int maxt = s_max;
+  // values HP_PF tiles ahead of the adds (a shift register), their ids one tile further ahead
+  constexpr int HP_PF = 3;
+  int ids[HP_FPW];
+  float vals[HP_PF][HP_FPW];
   auto load_ids = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < HPB; i++) ids[i] = k0 + i < total ? L[k0 + i] : -1;
-  };
-  auto gather = [&](float (&v)[HPB]) {  // -1: filtered leaf or past the end
-#pragma unroll
-    for (int i = 0; i < HPB; i++) v[i] = ids[i] >= 0 ? hp_m[ids[i]] : -1.f;
-  };
-  auto add = [&](const float (&v)[HPB]) {
-#pragma unroll
-    for (int i = 0; i < HPB; i++) {
-      const bool in = v[i] >= 0.f;
-      const float m = in ? v[i] : 0.f;
-      sum += m;
-      sum_sq += in ? m * m : 0.f;
-      count += in ? 1 : 0;
+    for (int i = 0; i < HP_FPW; i++) {
+      const int p = wv + 4 * i, k = k0 + j;
+      ids[i] = k < s_total[p] ? hp_leaf[s_off[p] + k] : -1;
     }
   };
-  load_ids(0);
-  gather(va);
-  load_ids(HPB);
-  for (int k0 = 0; k0 < total; k0 += 2 * HPB) {
-    gather(vb);
-    load_ids(k0 + 2 * HPB);
-    add(va);
-    if (k0 + HPB >= total) break;
-    gather(va);
-    load_ids(k0 + 3 * HPB);
-    add(vb);
+  auto gather = [&](float (&v)[HP_FPW]) {  // -1: filtered leaf or past the end
+#pragma unroll
+    for (int i = 0; i < HP_FPW; i++) v[i] = ids[i] >= 0 ? hp_m[ids[i]] : -1.f;
+  };
+  float sum = 0.f, sum_sq = 0.f;
+  int count = 0;
+#pragma unroll
+  for (int d = 0; d < HP_PF; d++) {
+    load_ids(d * HP_T);
+    gather(vals[d]);
   }
-  const float cnt = (float)count;
-  float mean = sum / cnt;
-  float var = (sum_sq / cnt) - (mean * mean);
-  mean -= 2;
-  var *= 0.05f;  // NORM_HEADPOSE_VARIANCE_FACTOR
-  o.status = 0;
-  o.headpose = mean;
-  o.pose_variance = var;
-  HpState& s = state[f];
-  s.headpose = mean;
-  s.variance = var;
-  // areaUnderCurve per pose bin (fp64 left Riemann sums), dominant = first strict maximum
-  const float poseT[6] = {-2.5f, -0.35f, -0.20f, 0.20f, 0.35f, 2.5f};
-  const double dmean = (double)mean, dstd = __builtin_sqrt((double)var);
-  float max_area = 0;
-  int dominant = 0;
-  for (int j = 0; j < n_forests; j++) {
-    double acc = 0, step = 0.01, tt;
-    for (double x = poseT[j]; x < (double)poseT[j + 1]; x += step) {
-      tt = (x - dmean) / dstd;
-      acc += ffd_exp(-0.5 * (tt * tt)) * step;
+  load_ids(HP_PF * HP_T);
+  for (int k0 = 0; k0 < maxt; k0 += HP_T) {
+    // terms of tile k0 and this tile's passing-leaf counts
+#pragma unroll
+    for (int i = 0; i < HP_FPW; i++) {
+      const int p = wv + 4 * i;
+      const bool in = vals[0][i] >= 0.f;
+      const float m = in ? vals[0][i] : 0.f;
+      tm[j * HP_LD + p] = m;
+      tq[j * HP_LD + p] = in ? m * m : 0.f;
+      const int c = __popcll(__ballot(in));
+      if (j == 0) s_tcnt[p] = c;
     }
-    const float a = (float)(acc * 1.0 / (dstd * 2.5066282746310002));
-    s.pose_freq[j] = a;
-    if (max_area < a) { max_area = a; dominant = j; }
+#pragma unroll
+    for (int d = 0; d + 1 < HP_PF; d++)
+#pragma unroll
+      for (int i = 0; i < HP_FPW; i++) vals[d][i] = vals[d + 1][i];
+    if (k0 + HP_PF * HP_T < maxt) {
+      gather(vals[HP_PF - 1]);                      // values of tile k0 + HP_PF * 64
+      load_ids(k0 + (HP_PF + 1) * HP_T);            // ids one tile further
+    }
+    __syncthreads();
+    if (tid < HP_FACES) {  // serial phase, in leaf order
+      const int lim = min(HP_T, s_total[tid] - k0);
+      count += s_tcnt[tid];
+      int q = 0;
+      for (; q + 8 <= lim; q += 8) {  // LDS reads 8 ahead of their in-order adds
+        float vm[8], vq[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          vm[e] = tm[(q + e) * HP_LD + tid];
+          vq[e] = tq[(q + e) * HP_LD + tid];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          sum += vm[e];
+          sum_sq += vq[e];
+        }
+      }
+      for (; q < lim; q++) {
+        sum += tm[q * HP_LD + tid];
+        sum_sq += tq[q * HP_LD + tid];
+      }
+    }
+    __syncthreads();
   }
-  int nt_total = 0;
-  for (int i = 0; i < n_forests; i++) {
-    const float v = floorf(s.pose_freq[i] * (float)ntrees_per_forest);
-    int k = (v > -2147483649.0f && v < 2147483648.0f) ? (int)v : (int)0x80000000;
-    k = min(k, ntrees_per_forest);
-    for (int j = 0; j < k && nt_total < MAX_TREES; j++) s.trees[nt_total++] = i * ntrees_per_forest + j;
+  if (tid < HP_FACES && s_valid[tid]) {
+    const float cnt = (float)count;  // the reference's float count of +1s is exact below 2^24
+    float mean = sum / cnt;
+    float var = (sum_sq / cnt) - (mean * mean);
+    mean -= 2;
+    var *= 0.05f;  // NORM_HEADPOSE_VARIANCE_FACTOR
+    s_mean[tid] = mean;
+    s_var[tid] = var;
   }
-  for (int i = nt_total; i < ntrees_per_forest; i++) s.trees[nt_total++] = dominant * ntrees_per_forest + i;
-  s.n_trees = nt_total;
-  o.n_trees = nt_total;
+  __syncthreads();
+  // areaUnderCurve per pose bin: lane (face p, bin j) = tid / 8, tid % 8 (fp64 left Riemann sums)
+  if (tid < HP_FACES * 8) {
+    const int p = tid >> 3, bin = tid & 7;
+    if (s_valid[p] && bin < n_forests && bin < 5) {
+      const float poseT[6] = {-2.5f, -0.35f, -0.20f, 0.20f, 0.35f, 2.5f};
+      const double dmean = (double)s_mean[p], dstd = __builtin_sqrt((double)s_var[p]);
+      double acc = 0, step = 0.01, tt;
+      for (double x = poseT[bin]; x < (double)poseT[bin + 1]; x += step) {
+        tt = (x - dmean) / dstd;
+        acc += ffd_exp(-0.5 * (tt * tt)) * step;
+      }
+      s_area[p][bin] = (float)(acc * 1.0 / (dstd * 2.5066282746310002));
+    }
+  }
+  __syncthreads();
+  if (tid < HP_FACES && s_valid[tid]) {
+    const int f = f0 + tid;
+    const float mean = s_mean[tid], var = s_var[tid];
+    FaceOut& o = out[f];
+    o.status = 0;
+    o.headpose = mean;
+    o.pose_variance = var;
+    HpState& s = state[f];
+    s.headpose = mean;
+    s.variance = var;
+    float max_area = 0;
+    int dominant = 0;  // first strict maximum
+    for (int jj = 0; jj < n_forests; jj++) {
+      const float a = s_area[tid][jj];
+      s.pose_freq[jj] = a;
+      if (max_area < a) { max_area = a; dominant = jj; }
+    }
+    int nt_total = 0;
+    for (int i = 0; i < n_forests; i++) {
+      const float v = floorf(s.pose_freq[i] * (float)ntrees_per_forest);
+      int k = (v > -2147483649.0f && v < 2147483648.0f) ? (int)v : (int)0x80000000;
+      k = min(k, ntrees_per_forest);
+      for (int jj = 0; jj < k && nt_total < MAX_TREES; jj++) s.trees[nt_total++] = i * ntrees_per_forest + jj;
+    }
+    for (int i = nt_total; i < ntrees_per_forest; i++) s.trees[nt_total++] = dominant * ntrees_per_forest + i;
+    s.n_trees = nt_total;
+    o.n_trees = nt_total;
+  }
 }
 
 // ------------------------------------------------------------ vote lists ----
@@ -1547,7 +1621,17 @@ void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t
 
 void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const float* hp_m, int hp_trees,
                     int n_forests, int ntrees_per_forest, HpState* state, FaceOut* out, hipStream_t s) {
-  k_hp_pose<<<(n + 63) / 64, 64, 0, s>>>(faces, n, hp_leaf, hp_m, hp_trees, n_forests, ntrees_per_forest, state, out);
+  static const int nf = [] {  // faces per workgroup (FFD_HP_FACES: 4, 8 or 16; C2: 0.261 / 0.256 / 0.281 ms)
+    const char* v = std::getenv("FFD_HP_FACES");
+    const int k = v ? std::atoi(v) : 8;
+    return k == 4 || k == 16 ? k : 8;
+  }();
+  if (nf == 16)
+    k_hp_pose<16><<<(n + 15) / 16, 256, 0, s>>>(faces, n, hp_leaf, hp_m, hp_trees, n_forests, ntrees_per_forest, state, out);
+  else if (nf == 8)
+    k_hp_pose<8><<<(n + 7) / 8, 256, 0, s>>>(faces, n, hp_leaf, hp_m, hp_trees, n_forests, ntrees_per_forest, state, out);
+  else
+    k_hp_pose<4><<<(n + 3) / 4, 256, 0, s>>>(faces, n, hp_leaf, hp_m, hp_trees, n_forests, ntrees_per_forest, state, out);
 }
 
 void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const uint4* leaf_rec, bool compact,
