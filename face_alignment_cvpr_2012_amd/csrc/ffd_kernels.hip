@@ -1117,9 +1117,10 @@ __global__ __launch_bounds__(256) void k_hp_pose(const FaceDesc* __restrict__ fa
 // FFD leaves in reference order (patch-major x-outer, tree-minor), 64 at a time; for each
 // landmark a ballot + popcount gives every voting lane its slot, so the compacted list keeps
 // the reference's vote order exactly.
+template <bool compact>
 __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ faces, int n_faces,
                                                const int32_t* __restrict__ mp_leaf,
-                                               const uint4* __restrict__ leaf_rec, int compact, int bias_x,
+                                               const uint4* __restrict__ leaf_rec, int bias_x,
                                                int bias_y, const HpState* __restrict__ state,
                                                int tslots, int step, int step_y, int half_patch, int n_parts,
                                                Vote* __restrict__ votes, int32_t* __restrict__ vote_counts) {
@@ -1137,50 +1138,69 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
 #pragma unroll
   for (int i = 0; i < NPARTS; i++) cnt[i] = 0;
 #ifndef FFD_VOTE_U
-#define FFD_VOTE_U 4
+#define FFD_VOTE_U 2
 #endif
   constexpr int U = FFD_VOTE_U;  // 64-item batches whose loads are in flight together
-  for (int base = 0; base < total; base += 64 * U) {
+  // software pipeline over groups of U batches: the leaf ids of group g + 2 and the leaf records of
+  // group g + 1 are in flight while group g is filtered
+  struct Grp {
     int leaf[U], vx0[U], vy0[U];
+    uint4 r0[U], r1[U], r2[compact ? 1 : U];
+  };
+  auto load_ids = [&](int base, Grp& G) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int k = base + u * 64 + lane;
-      leaf[u] = -1;
-      vx0[u] = vy0[u] = 0;
+      G.leaf[u] = -1;
+      G.vx0[u] = G.vy0[u] = 0;
       if (k < total) {
         const int pr = idiv_small(k, T), xi = idiv_small(pr, ny), yi = pr - xi * ny;
-        leaf[u] = L[k];  // leaves are stored in the reference order
-        vx0[u] = fd.vox + xi * step + half_patch;  // patch.x + 15 (face_utils.cpp:257-293)
-        vy0[u] = fd.voy + yi * step_y + half_patch;
+        G.leaf[u] = L[k];  // leaves are stored in the reference order
+        G.vx0[u] = fd.vox + xi * step + half_patch;  // patch.x + 15 (face_utils.cpp:257-293)
+        G.vy0[u] = fd.voy + yi * step_y + half_patch;
       }
     }
-    // packed leaf records (see launch_votes): compact 32 B = 2 x uint4, else 64 B = 3 used uint4
-    uint4 r0[U], r1[U], r2[U];
+  };
+  // packed leaf records (see launch_votes): compact 32 B = 2 x uint4, else 64 B = 3 used uint4
+  auto load_recs = [&](Grp& G) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      r0[u] = r1[u] = r2[u] = make_uint4(0, 0, 0, 0);
-      if (leaf[u] >= 0) {
-        const uint4* rec = leaf_rec + (int64_t)leaf[u] * (compact ? 2 : 4);
-        r0[u] = rec[0];
-        r1[u] = rec[1];
-        if (!compact) r2[u] = rec[2];
+      G.r0[u] = G.r1[u] = make_uint4(0, 0, 0, 0);
+      if constexpr (!compact) G.r2[u] = make_uint4(0, 0, 0, 0);
+      if (G.leaf[u] >= 0) {
+        const uint4* rec = leaf_rec + (int64_t)G.leaf[u] * (compact ? 2 : 4);
+        G.r0[u] = rec[0];
+        G.r1[u] = rec[1];
+        if constexpr (!compact) G.r2[u] = rec[2];
       }
+    }
+  };
+  Grp cur, nxt;
+  load_ids(0, cur);
+  load_recs(cur);
+  load_ids(64 * U, nxt);
+  for (int base = 0; base < total; base += 64 * U) {
+    Grp nn;
+    const bool more = base + 64 * U < total;
+    if (more) {
+      load_recs(nxt);
+      load_ids(base + 2 * 64 * U, nn);
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {  // batches in list order: (patch x-major, tree), then part
-      const uint32_t mk = r0[u].x;
-      const float w = __uint_as_float(r0[u].y);
+      const uint32_t mk = cur.r0[u].x;
+      const float w = __uint_as_float(cur.r0[u].y);
       uint32_t off[NPARTS];
-      if (compact) {  // u8 pairs relative to the biases -> the 64-B format's x | y << 16
-        const uint32_t pk[5] = {r0[u].z, r0[u].w, r1[u].x, r1[u].y, r1[u].z};
+      if constexpr (compact) {  // u8 pairs relative to the biases -> the 64-B format's x | y << 16
+        const uint32_t pk[5] = {cur.r0[u].z, cur.r0[u].w, cur.r1[u].x, cur.r1[u].y, cur.r1[u].z};
 #pragma unroll
         for (int i = 0; i < NPARTS; i++) {
           const uint32_t v = (pk[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
           off[i] = (uint32_t)(uint16_t)((int)(v & 0xFFu) + bias_x) | (uint32_t)(uint16_t)((int)(v >> 8) + bias_y) << 16;
         }
       } else {
-        const uint32_t o[NPARTS] = {r0[u].z, r0[u].w, r1[u].x, r1[u].y, r1[u].z,
-                                    r1[u].w, r2[u].x, r2[u].y, r2[u].z, r2[u].w};
+        const uint32_t o[NPARTS] = {cur.r0[u].z, cur.r0[u].w, cur.r1[u].x, cur.r1[u].y, cur.r1[u].z,
+                                    cur.r1[u].w, cur.r2[u].x, cur.r2[u].y, cur.r2[u].z, cur.r2[u].w};  // (!compact)
 #pragma unroll
         for (int i = 0; i < NPARTS; i++) off[i] = o[i];
       }
@@ -1191,12 +1211,15 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
         if (vote) {
           const int pos = cnt[i] + __popcll(bal & below);
           const int32_t o = (int32_t)off[i];
-          V[i * cap + pos] = Vote{(int16_t)((int)(int16_t)(o & 0xFFFF) + vx0[u]),
-                                  (int16_t)((int)(int16_t)(o >> 16) + vy0[u]), w};
+          V[i * cap + pos] = Vote{(int16_t)((int)(int16_t)(o & 0xFFFF) + cur.vx0[u]),
+                                  (int16_t)((int)(int16_t)(o >> 16) + cur.vy0[u]), w};
         }
         cnt[i] += __popcll(bal);
       }
     }
+    if (!more) break;
+    cur = nxt;
+    nxt = nn;
   }
   if (lane < n_parts) {
     int c = 0;
@@ -1638,8 +1661,12 @@ void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const ui
                   int bias_x, int bias_y, const HpState* state,
                   int tslots, int step, int step_y, int half_patch, int n_parts, Vote* votes, int32_t* vote_counts,
                   hipStream_t s) {
-  k_votes<<<(n + 3) / 4, 256, 0, s>>>(faces, n, mp_leaf, leaf_rec, compact ? 1 : 0, bias_x, bias_y, state, tslots, step, step_y, half_patch, n_parts, votes,
-                                      vote_counts);
+  if (compact)
+    k_votes<true><<<(n + 3) / 4, 256, 0, s>>>(faces, n, mp_leaf, leaf_rec, bias_x, bias_y, state, tslots, step, step_y,
+                                              half_patch, n_parts, votes, vote_counts);
+  else
+    k_votes<false><<<(n + 3) / 4, 256, 0, s>>>(faces, n, mp_leaf, leaf_rec, bias_x, bias_y, state, tslots, step, step_y,
+                                               half_patch, n_parts, votes, vote_counts);
 }
 
 void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int tslots, int n_parts, float lamda,
