@@ -51,9 +51,9 @@ def gabor_flops_per_pixel(w, face_w=125):
 
 # profiler stage -> kernel name prefix in rocprofv3 traces (for the PMC traffic lookup)
 STAGE_KERNELS = {
-    "gray_resize": "ffd::k_gray_resize", "gabor_25x25": "void ffd::k_gabor_sep<25>",
-    "gabor_19x19": "void ffd::k_gabor_sep<19>", "gabor_13x13": "void ffd::k_gabor_sep<13>",
-    "gabor_9x9": "void ffd::k_gabor_sep<9>", "gabor_7x7": "ffd::k_gabor7",
+    "gray_resize": "ffd::k_gray_resize", "gabor_25x25": "void ffd::k_gabor_sep<25, false>",
+    "gabor_19x19": "void ffd::k_gabor_sep<19, false>", "gabor_13x13": "void ffd::k_gabor_sep<13, false>",
+    "gabor_9x9": "void ffd::k_gabor_sep<9, false>", "gabor_7x7": "void ffd::k_gabor7<false>",
     "integral_channels": "ffd::k_integral", "headpose_traverse": "void ffd::k_traverse<true",
     "headpose_reduce_select": "ffd::k_hp_pose", "ffd_traverse": "void ffd::k_traverse<false",
     "votes": "ffd::k_votes", "meanshift": "ffd::k_meanshift",

@@ -102,7 +102,7 @@ _lib = None
 EXPORTED_SYMBOLS = (
     "ffd_engine_desc_init", "ffd_engine_create", "ffd_engine_destroy", "ffd_last_error", "ffd_face_geometry",
     "ffd_analyze_faces", "ffd_analyze_faces_device", "ffd_synchronize", "ffd_stream", "ffd_extract_channels",
-    "ffd_forest_eval_leaves", "ffd_get_trace", "ffd_version", "ffd_set_profiling", "ffd_get_stage_times",
+    "ffd_forest_eval_leaves", "ffd_get_trace", "ffd_version", "ffd_set_profiling", "ffd_get_stage_times", "ffd_check_mag_sqrt",
     "ffd_stage_name", "ffd_status_string", "ffd_estimate_headpose", "ffd_estimate_facial_features",
     "ffd_group_create", "ffd_group_destroy", "ffd_group_last_error", "ffd_group_size", "ffd_group_engine",
     "ffd_group_analyze_faces", "ffd_comm_id", "ffd_engine_join", "ffd_gather_faces",
@@ -150,6 +150,7 @@ def lib():
     L.ffd_get_stage_times.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
     L.ffd_stage_name.argtypes = [ctypes.c_int32]
     L.ffd_stage_name.restype = ctypes.c_char_p
+    L.ffd_check_mag_sqrt.argtypes = [ctypes.c_void_p, P(ctypes.c_uint64), P(ctypes.c_uint64)]
     L.ffd_status_string.argtypes = [ctypes.c_int32]
     L.ffd_status_string.restype = ctypes.c_char_p
     L.ffd_estimate_headpose.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
@@ -465,6 +466,12 @@ class FaceForest:
 
     def stream(self):
         return lib().ffd_stream(self._h)
+
+    def check_mag_sqrt(self):
+        """ffd_check_mag_sqrt: (floats checked, mismatches) of the Gabor magnitude sqrt vs sqrtf."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().ffd_check_mag_sqrt(self._h, ctypes.byref(a), ctypes.byref(b)), self._h)
+        return a.value, b.value
 
     def set_profiling(self, enable=True):
         _check(lib().ffd_set_profiling(self._h, 1 if enable else 0), self._h)

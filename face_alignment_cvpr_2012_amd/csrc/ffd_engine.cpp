@@ -482,6 +482,7 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   w.state.ensure((size_t)n * sizeof(HpState));
   w.ms_mean.ensure((size_t)n * NPARTS * 2 * 4);
   w.vote_counts.ensure((size_t)n * NPARTS * 4);
+  w.gabor_redo.ensure((size_t)n * 5 * 4);  // 5 scales
   upload(w.faces, fds, st);
   HIP_CHECK(hipMemsetAsync(d_out, 0, (size_t)n * sizeof(FaceOut), st));
 
@@ -498,7 +499,7 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
     const hipStream_t s2 = cs(4 - nu);
     stage(1 + (4 - nu), s2, [&] {
       launch_gabor(nu, dfd, n, max_h, w.gray.as<uint8_t>(), gabor_coef.as<float>(), w.mag.as<float>(),
-                   w.chan.as<uint16_t>(), s2);
+                   w.chan.as<uint16_t>(), w.gabor_redo.as<int>(), gabor_exact, s2);
     });
   }
   {
@@ -722,6 +723,7 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   if (const char* v = std::getenv("FFD_TRAV_G_FFD")) shape(v, e->trav_g_mp);
   if (const char* v = std::getenv("FFD_TRAV_WG")) e->trav_wg = std::max(8, std::atoi(v));
   if (const char* v = std::getenv("FFD_TRAV_TOPMAX")) e->trav_top_max = std::max(1, std::min(TOP_CAP, std::atoi(v)));
+  if (const char* v = std::getenv("FFD_GABOR_EXACT")) e->gabor_exact = std::atoi(v) != 0;
   if (const char* v = std::getenv("FFD_CHANNEL_STREAMS")) e->channel_streams = std::max(1, std::min(4, std::atoi(v)));
   if (const char* v = std::getenv("FFD_CHUNK")) e->max_chunk = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("FFD_STREAMS")) e->n_streams = std::max(1, std::min(8, std::atoi(v)));
@@ -776,6 +778,30 @@ ffd_status ffd_synchronize(ffd_engine* e) {
   return guarded(e, [&] {
     e->sync_all();
     e->resolve();
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_check_mag_sqrt(ffd_engine* e, uint64_t* checked, uint64_t* mismatches) {
+  return guarded(e, [&] {
+    e->resolve();
+    constexpr int kBlocks = 8192;
+    const hipStream_t st = e->main_stream();
+    e->scratch_c.ensure((size_t)kBlocks * 4 * 4);
+    std::vector<uint32_t> bad((size_t)kBlocks * 4);
+    uint64_t n_bad = 0, n_chk = 0;
+    // mag_sqrt's exact domain: +0 and every finite s >= 2^-96 (bits 0x0F800000 .. 0x7F7FFFFF)
+    const uint32_t ranges[2][2] = {{0u, 1u}, {0x0F800000u, 0x7F800000u - 0x0F800000u}};
+    for (const auto& r : ranges) {
+      launch_check_mag_sqrt(r[0], r[1], e->scratch_c.as<uint32_t>(), kBlocks, st);
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipMemcpyAsync(bad.data(), e->scratch_c.p, bad.size() * 4, hipMemcpyDeviceToHost, st));
+      HIP_CHECK(hipStreamSynchronize(st));
+      for (uint32_t b : bad) n_bad += b;
+      n_chk += r[1];
+    }
+    if (checked) *checked = n_chk;
+    if (mismatches) *mismatches = n_bad;
     return FFD_OK;
   });
 }
@@ -925,13 +951,14 @@ ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t
     w.gray.ensure((size_t)H * PITCH + 256);
     w.mag.ensure((size_t)NGABOR * H * PITCH * 4 + 256);
     w.chan.ensure((size_t)NCH * f.plane * 2 + 256);
+    w.gabor_redo.ensure(5 * 4);
     std::vector<FaceDesc> one{f};
     upload(w.faces, one, w.stream);
     const FaceDesc* dfd = w.faces.as<FaceDesc>();
     launch_gray_resize(dfd, 1, e->scratch_a.as<uint8_t>(), w.gray.as<uint8_t>(), w.stream);
     for (int nu = 4; nu >= 0; nu--)
       launch_gabor(nu, dfd, 1, H, w.gray.as<uint8_t>(), e->gabor_coef.as<float>(), w.mag.as<float>(),
-                   w.chan.as<uint16_t>(), w.stream);
+                   w.chan.as<uint16_t>(), w.gabor_redo.as<int>(), e->gabor_exact, w.stream);
     launch_integral(dfd, 1, w.gray.as<uint8_t>(), w.chan.as<uint16_t>(), w.stream);
     HIP_CHECK(hipGetLastError());
     std::vector<uint16_t> v((size_t)NCH * f.plane);

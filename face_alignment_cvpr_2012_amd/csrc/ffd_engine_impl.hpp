@@ -86,6 +86,7 @@ struct Workspace {
   std::vector<hipEvent_t> fork_ev;  // [0]: gray ready; [1 + i]: fork stream i done
   bool pending = false;
   DevBuf faces, gray, mag, chan, hpleaf, mpleaf, votes, state, ms_mean, vote_counts;
+  DevBuf gabor_redo;  // per scale and face: the fast Gabor instance flags faces for the exact one
   std::vector<FaceDesc> h_fds;  // host staging, reused only after `done`
   std::vector<FaceDesc> desc;   // descriptors of the chunk last run here (ffd_get_trace)
   int first = 0, count = 0;
@@ -113,6 +114,7 @@ struct ffd_engine {
   ffd_engine_desc desc{};
   int max_chunk = 4096;
   int n_streams = 1;
+  int gabor_exact = 0;      // FFD_GABOR_EXACT=1: every face through the exact (sqrtf) Gabor instance (tests)
   int channel_streams = 1;  // streams the channel stage is spread over (FFD_CHANNEL_STREAMS; 2-4 measured no gain)
   // traversal tuning: patch block edge G (a workgroup walks all trees of a G x G block of patches
   // over an LDS copy of the block's integral window) and the persistent workgroups (one per CU).

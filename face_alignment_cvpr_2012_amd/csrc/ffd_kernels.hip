@@ -199,8 +199,8 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // Face-wide min / max of one scale's 7 magnitude planes -> cv::normalize(NORM_MINMAX, 0, 1) +
 // convertTo(CV_8U, 255) (FeatureChannelFactory.hpp:271-286): quantise (v*scale + shift, *255,
 // cvRound, saturate) and integrate the 7 channels, one wave per channel, reading the magnitudes
-// back from L2.  mn / mx: this thread's minima of the magnitudes' bits and of their complements
-// (unsigned order == float order for m >= +0).  Every magnitude store of the workgroup precedes
+// back from L2.  mn / mx: this thread's minimum and maximum of the magnitudes' bits (unsigned
+// order == float order for m >= +0).  Every magnitude store of the workgroup precedes
 // the first barrier here.
 template <int NWV>
 __device__ __forceinline__ void gabor_minmax_scale(uint32_t (&mn)[7], uint32_t (&mx)[7], float* s_sf, float* s_hf) {
@@ -211,7 +211,7 @@ __device__ __forceinline__ void gabor_minmax_scale(uint32_t (&mn)[7], uint32_t (
 #pragma unroll
     for (int sh = 32; sh >= 1; sh >>= 1) {
       mn[o] = min(mn[o], (uint32_t)__shfl_xor((int)mn[o], sh));
-      mx[o] = min(mx[o], (uint32_t)__shfl_xor((int)mx[o], sh));
+      mx[o] = max(mx[o], (uint32_t)__shfl_xor((int)mx[o], sh));
     }
   }
   if (ln == 0) {
@@ -222,8 +222,8 @@ __device__ __forceinline__ void gabor_minmax_scale(uint32_t (&mn)[7], uint32_t (
   if (threadIdx.x < 7) {
     const int o = threadIdx.x;
     uint32_t a = red[0][o], b = red[0][7 + o];
-    for (int w = 1; w < NWV; w++) { a = min(a, red[w][o]); b = min(b, red[w][7 + o]); }
-    const double smin = (double)__uint_as_float(a), smax = (double)__uint_as_float(~b);
+    for (int w = 1; w < NWV; w++) { a = min(a, red[w][o]); b = max(b, red[w][7 + o]); }
+    const double smin = (double)__uint_as_float(a), smax = (double)__uint_as_float(b);
     const double dmin = 0, dmax = 1;
     const double scale = (dmax - dmin) * (smax - smin > 2.220446049250313e-16 ? 1. / (smax - smin) : 0);
     const double shift = dmin - smin * scale;
@@ -233,9 +233,41 @@ __device__ __forceinline__ void gabor_minmax_scale(uint32_t (&mn)[7], uint32_t (
   __syncthreads();
 }
 
-// convertTo(CV_8U, 255) of a normalised magnitude (FeatureChannelFactory.hpp:276)
+// convertTo(CV_8U, 255) of a normalised magnitude (FeatureChannelFactory.hpp:276):
+// saturate(cvRound(v * 255 + 0)).  "+ 0" only turns -0 into +0, which cvRound maps to 0 either way,
+// and v * 255 lies in [-1, 256] for every magnitude of the plane (m in [min, max]), where cvRound's
+// out-of-range test never fires: both are left out (the values are the same for every input).
 __device__ __forceinline__ uint32_t gabor_quantise(float m, float sf, float hf) {
-  return (uint32_t)sat_u8(cv_round((m * sf + hf) * 255.f + 0.f));
+  return (uint32_t)sat_u8((int)__builtin_rintf((m * sf + hf) * 255.f));
+}
+
+// Correctly rounded sqrt of a magnitude's squared norm s (finite, >= +0), branch-free: the compiler's
+// expansion of sqrtf (v_sqrt_f32, then the two residual tests with its neighbours) without its
+// subnormal scaling and its class test.  Both are identities for s = +0 (the rm residual is NaN, the rp
+// residual +0) and for s >= 2^-96 (no scaling applies), so mag_sqrt(s) == sqrtf(s) there.  For
+// 0 < s < 2^-96 (both |re| and |im| below 2^-48: not met by real faces) it may differ: the Gabor
+// kernels flag such a face (mag_tiny) and their EXACT instance recomputes it with sqrtf.
+__device__ __forceinline__ float mag_sqrt(float s) {
+  const float r = __builtin_amdgcn_sqrtf(s);
+  const float rm = __uint_as_float(__float_as_uint(r) - 1u), rp = __uint_as_float(__float_as_uint(r) + 1u);
+  const float r1 = __builtin_fmaf(-rm, r, s) <= 0.f ? rm : r;
+  return __builtin_fmaf(-rp, r, s) > 0.f ? rp : r1;
+}
+// running minimum of bits(s) - 1: below 0x0F7FFFFF iff some 0 < s < 2^-96 was seen
+__device__ __forceinline__ void mag_tiny_update(uint32_t& t, float s) { t = min(t, __float_as_uint(s) - 1u); }
+template <bool EXACT, bool FAST>
+__device__ __forceinline__ float mag_of(float s, uint32_t& tiny) {
+  if (EXACT || !FAST) return __builtin_sqrtf(s);
+  mag_tiny_update(tiny, s);
+  return mag_sqrt(s);
+}
+// fast instance: record whether the face needs the exact instance (one workgroup-wide vote, after
+// the compute phase); every valid face's flag is written, so the array needs no clearing
+template <bool EXACT>
+__device__ __forceinline__ void mag_flag(uint32_t tiny, int* __restrict__ redo, int force) {
+  if (EXACT) return;
+  const int any = __syncthreads_or(tiny < 0x0F7FFFFFu || force ? 1 : 0);
+  if (threadIdx.x == 0) redo[blockIdx.x] = any;
 }
 
 template <int NWV>
@@ -286,9 +318,21 @@ __device__ __forceinline__ void gabor_normalise_integrate(const FaceDesc& fd, in
   }
 }
 
+// running min / max of a plane's magnitudes as their bits (unsigned order == float order for m >= +0).
+// MASK: pixels outside the face (in == false) enter as the neutral elements (all ones / zero), four
+// ALU operations with no select; else a predicated update.  Which form a kernel uses is decided per
+// Gabor scale by measurement (the register allocator's SGPR spills differ, k_gabor_sep below).
+template <bool MASK>
 __device__ __forceinline__ void minmax_update(uint32_t& mn, uint32_t& mx, float m, bool in) {
   const uint32_t bits = __float_as_uint(m);
-  if (in) { mn = min(mn, bits); mx = min(mx, ~bits); }
+  if (MASK) {
+    const uint32_t im = in ? 0xFFFFFFFFu : 0u;
+    mn = min(mn, bits | ~im);
+    mx = max(mx, bits & im);
+  } else if (in) {
+    mn = min(mn, bits);
+    mx = max(mx, bits);
+  }
 }
 
 // 7x7 (scale 0): OpenCV 2.4.9's direct Filter2D (49 taps < dft_filter_size 50), restated bit-exactly.
@@ -300,11 +344,12 @@ __device__ __forceinline__ void minmax_update(uint32_t& mn, uint32_t& mx, float 
 // operands are wave-uniform scalar loads (SGPR pairs).
 constexpr int GB_TX = 64, GB_TY = 32, GB_THREADS = 512;
 
+template <bool EXACT>
 __global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restrict__ faces,
                                                        const uint8_t* __restrict__ gray,
                                                        const float4* __restrict__ coef_g,
                                                        float* __restrict__ mag,
-                                                       uint16_t* __restrict__ chan) {
+                                                       uint16_t* __restrict__ chan, int* __restrict__ redo, int force) {
   constexpr int R = 3;
   // row stride (floats) == 1 mod 4: the 4 rows a 32-lane group touches fall on disjoint banks
   constexpr int LW = ((GB_TX + 2 * R + 3) / 4) * 4 + 1;
@@ -312,12 +357,14 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restric
   __shared__ float tile[LH * LW];
   const FaceDesc fd = faces[blockIdx.x];
   if (!fd.valid || fd.nochan) return;
+  if (EXACT && !redo[blockIdx.x]) return;  // the fast instance's mag_sqrt was exact for this face
+  uint32_t tiny = 0xFFFFFFFFu;
   const int tiles_x = (fd.W + GB_TX - 1) / GB_TX, tiles = tiles_x * ((fd.H + GB_TY - 1) / GB_TY);
   const uint8_t* g = gray + fd.gray_off;
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   uint32_t mn[7], mx[7];
 #pragma unroll
-  for (int o = 0; o < 7; o++) mn[o] = mx[o] = 0xFFFFFFFFu;
+  for (int o = 0; o < 7; o++) { mn[o] = 0xFFFFFFFFu; mx[o] = 0u; }
 #pragma unroll 1
   for (int tl = 0; tl < tiles; tl++) {
     const int tx0 = (tl % tiles_x) * GB_TX, ty0 = (tl / tiles_x) * GB_TY;
@@ -365,14 +412,15 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restric
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const float i2 = acc[k][o].y * acc[k][o].y, r2 = acc[k][o].x * acc[k][o].x;
-        m4[k] = __builtin_sqrtf(i2 + r2);
-        minmax_update(mn[o], mx[o], m4[k], (x0 + k) < fd.W && y < fd.H);
+        m4[k] = mag_of<EXACT, true>(i2 + r2, tiny);
+        minmax_update<true>(mn[o], mx[o], m4[k], (x0 + k) < fd.W && y < fd.H);
       }
       if (y < fd.H)  // columns >= W land in the row's pitch padding, never read
         *reinterpret_cast<float4*>(&mag[fd.mag_off + ((int64_t)o * fd.H + y) * PITCH + x0]) =
             make_float4(m4[0], m4[1], m4[2], m4[3]);
     }
   }
+  mag_flag<EXACT>(tiny, redo, force);
   gabor_normalise_integrate<GB_THREADS / 64>(fd, 0, mn, mx, mag, chan);
 }
 
@@ -404,20 +452,26 @@ template <int R> struct GSep {
   static constexpr int V_OFF = 4, H_OFF = 4 + 12 * (R + 1);
 };
 
-template <int W>
+template <int W, bool EXACT>
 __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __restrict__ faces,
                                                           const uint8_t* __restrict__ gray,
                                                           const float* __restrict__ coef,
                                                           float* __restrict__ mag,
-                                                          uint16_t* __restrict__ chan) {
+                                                          uint16_t* __restrict__ chan, int* __restrict__ redo, int force) {
   constexpr int R = (W - 1) / 2;
   using C = GSep<R>;
   constexpr int NU = W == 9 ? 1 : W == 13 ? 2 : W == 19 ? 3 : 4;
+  // magnitude sqrt / min-max forms per scale (r2e, C2, ms): 25x25 sqrtf + masked min-max 1.88 (both
+  // compiler forms 1.93, both fast 2.04: SGPR spills); 19x19 both fast 1.63 (1.72); 13x13 / 9x9
+  // mag_sqrt + predicated min-max 1.44 / 1.30 (1.54 / 1.34; masked: SGPR spills, 2.8 / 1.7)
+  constexpr bool GS_FAST = W != 25, GS_MASK = W == 25 || W == 19;
   extern __shared__ __attribute__((aligned(16))) uint8_t gface[];  // (H + 2R) x GP reflect-101 padded face
   __shared__ float vg[GS_BY * C::VP];
   __shared__ f2 vq[4][GS_BY * C::VP];
   const FaceDesc fd = faces[blockIdx.x];
   if (!fd.valid || fd.nochan) return;
+  if (EXACT && !redo[blockIdx.x]) return;  // the fast instance's mag_sqrt was exact for this face
+  uint32_t tiny = 0xFFFFFFFFu;
   const int FW = fd.W, FH = fd.H, NPC = FW + 2 * R;
   const uint8_t* g = gray + fd.gray_off;
   const float* cv = coef + C::V_OFF;
@@ -426,7 +480,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
   const int tid = threadIdx.x;
   uint32_t mn[7], mx[7];
 #pragma unroll
-  for (int o = 0; o < 7; o++) mn[o] = mx[o] = 0xFFFFFFFFu;
+  for (int o = 0; o < 7; o++) { mn[o] = 0xFFFFFFFFu; mx[o] = 0u; }
 
   {  // the whole reflect-101 padded face, once: (row, 4-column group) items, u32 LDS stores; rows up
      // to the last band's end (ceil(FH / GS_BY) * GS_BY + 2R: every row the V pass reads is staged)
@@ -555,8 +609,8 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
         for (int k = 0; k < 4; k++) {
           const float re = fmaf(-cdc, dc[k], acc[k][o].x), im = acc[k][o].y;
           const float i2 = im * im, r2 = re * re;
-          m4[k] = __builtin_sqrtf(i2 + r2);
-          minmax_update(mn[o], mx[o], m4[k], x0 + k < FW);
+          m4[k] = mag_of<EXACT, GS_FAST>(i2 + r2, tiny);
+          minmax_update<GS_MASK>(mn[o], mx[o], m4[k], x0 + k < FW);
         }
         // columns >= W land in the row's pitch padding, never read
 #if FFD_GABOR_PROBE != 1 && FFD_GABOR_PROBE != 4  // 4: epilogue reads whatever the buffer holds
@@ -570,6 +624,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
   if (mn[0] == 0x12345u && mx[1] == 0x6789u) mag[0] = 0.f;
   return;
 #endif
+  mag_flag<EXACT>(tiny, redo, force);
   gabor_normalise_integrate<GS_THREADS / 64>(fd, NU, mn, mx, mag, chan);
 }
 
@@ -1258,11 +1313,40 @@ constexpr int MS_RA = FFD_MS_RA;  // serial phase: LDS reads in flight ahead of 
 // (double sqrt, rounded to float), w = weight * expf(-d / lamda).  lam_y > 0: RN(1 / lamda) for the
 // exact ffd_div_rcp quotient (lamda == 10 only, checked for every float in tests/test_numerics.py);
 // the argument of the exponential is <= 0, where ffd_expf_nonpos == ffd_expf.
+// ffd_expf_nonpos (include/ffd_numerics.h) with its Horner steps as three-address v_fma_f64: the
+// compiler's accumulating v_fmac_f64 form needs a v_mov_b64 copy of every register-held coefficient
+// per step.  Same operations, same roundings (MeanShift 2.50 -> 2.41 ms at C2).
+__device__ __forceinline__ double fma3_f64(double a, double b, double c) {
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ float ms_expf_nonpos(float xf) {
+  const int under = xf < -104.0f;
+  const double x = (double)(under ? -104.0f : xf);
+  int k;
+  const double r = ffd_exp_reduce(x, &k);
+  double p = 1.0 / 39916800.0;
+  p = fma3_f64(p, r, 1.0 / 3628800.0);
+  p = fma3_f64(p, r, 1.0 / 362880.0);
+  p = fma3_f64(p, r, 1.0 / 40320.0);
+  p = fma3_f64(p, r, 1.0 / 5040.0);
+  p = fma3_f64(p, r, 1.0 / 720.0);
+  p = fma3_f64(p, r, 1.0 / 120.0);
+  p = fma3_f64(p, r, 1.0 / 24.0);
+  p = fma3_f64(p, r, 1.0 / 6.0);
+  p = __builtin_fma(p, r, 0.5);
+  p = __builtin_fma(p, r, 1.0);
+  p = __builtin_fma(p, r, 1.0);
+  const float e = (float)__builtin_ldexp(p, k);
+  return under ? 0.0f : e;
+}
+
 __device__ __forceinline__ float ms_weight(float mx, float my, float x, float y, float w, float lamda, float lam_y) {
   const float dx = mx - x, dy = my - y;
   const float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
   const float q = lam_y > 0.f ? ffd_div_rcp(-d, lamda, lam_y) : -d / lamda;
-  return w * ffd_expf_nonpos(q);
+  return w * ms_expf_nonpos(q);
 }
 
 // 8 waves per SIMD (<= 64 VGPRs): 8 workgroups per CU, so C2's 2048 workgroups run as one round
@@ -1546,16 +1630,43 @@ int gabor_face_lds(int R, int max_h) {
 }
 
 void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t* gray, const float* coef, float* mag,
-                  uint16_t* chan, hipStream_t s) {
+                  uint16_t* chan, int* redo, int force_exact, hipStream_t s) {
   if (n <= 0) return;
   const float* c = coef + GABOR_OFFS[nu];
-  switch (nu) {
-    case 4: k_gabor_sep<25><<<n, GS_THREADS, gabor_face_lds(12, max_h), s>>>(faces, gray, c, mag, chan); break;
-    case 3: k_gabor_sep<19><<<n, GS_THREADS, gabor_face_lds(9, max_h), s>>>(faces, gray, c, mag, chan); break;
-    case 2: k_gabor_sep<13><<<n, GS_THREADS, gabor_face_lds(6, max_h), s>>>(faces, gray, c, mag, chan); break;
-    case 1: k_gabor_sep<9><<<n, GS_THREADS, gabor_face_lds(4, max_h), s>>>(faces, gray, c, mag, chan); break;
-    default: k_gabor7<<<n, GB_THREADS, 0, s>>>(faces, gray, reinterpret_cast<const float4*>(c), mag, chan); break;
+  // the fast instance, then the exact one over the faces it flagged (an empty pass in practice)
+  int* rd = redo + (int64_t)nu * n;  // one flag array per scale: the scales may run on fork streams
+  for (int exact = 0; exact < 2; exact++) {
+#define FFD_GABOR_LAUNCH(WV, RV)                                                                              \
+  (exact ? k_gabor_sep<WV, true> : k_gabor_sep<WV, false>)<<<n, GS_THREADS, gabor_face_lds(RV, max_h), s>>>(faces, gray, c, \
+                                                                                                  mag, chan, rd, force_exact)
+    switch (nu) {
+      case 4: FFD_GABOR_LAUNCH(25, 12); break;
+      case 3: FFD_GABOR_LAUNCH(19, 9); break;
+      case 2: FFD_GABOR_LAUNCH(13, 6); break;
+      case 1: FFD_GABOR_LAUNCH(9, 4); break;
+      default:
+        (exact ? k_gabor7<true> : k_gabor7<false>)<<<n, GB_THREADS, 0, s>>>(faces, gray, reinterpret_cast<const float4*>(c),
+                                                                          mag, chan, rd, force_exact);
+        break;
+    }
+#undef FFD_GABOR_LAUNCH
   }
+}
+
+// Exhaustive device check of mag_sqrt against sqrtf (ffd_check_mag_sqrt): the n floats with bits
+// [lo, lo + n); one mismatch count per wave (plain vector stores).
+__global__ __launch_bounds__(256) void k_check_mag_sqrt(uint32_t lo, uint32_t n, uint32_t* __restrict__ bad) {
+  uint32_t cnt = 0;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+    const float s = __uint_as_float(lo + i);
+    cnt += __float_as_uint(mag_sqrt(s)) != __float_as_uint(__builtin_sqrtf(s)) ? 1u : 0u;
+  }
+  for (int sh = 32; sh >= 1; sh >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, sh);
+  if ((threadIdx.x & 63) == 0) bad[blockIdx.x * 4 + (threadIdx.x >> 6)] = cnt;
+}
+
+void launch_check_mag_sqrt(uint32_t lo, uint32_t n, uint32_t* bad, int blocks, hipStream_t s) {
+  k_check_mag_sqrt<<<blocks, 256, 0, s>>>(lo, n, bad);
 }
 
 void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t* chan, hipStream_t s) {
@@ -1612,8 +1723,10 @@ void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, TravShape g
 
 hipError_t set_gabor_lds_limit(int bytes) {
   hipError_t e = hipSuccess;
-  const void* fns[] = {(const void*)k_gabor_sep<9>, (const void*)k_gabor_sep<13>, (const void*)k_gabor_sep<19>,
-                       (const void*)k_gabor_sep<25>};
+  const void* fns[] = {(const void*)k_gabor_sep<9, false>,  (const void*)k_gabor_sep<13, false>,
+                       (const void*)k_gabor_sep<19, false>, (const void*)k_gabor_sep<25, false>,
+                       (const void*)k_gabor_sep<9, true>,   (const void*)k_gabor_sep<13, true>,
+                       (const void*)k_gabor_sep<19, true>,  (const void*)k_gabor_sep<25, true>};
   for (const void* f : fns) {
     hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (r != hipSuccess) e = r;

@@ -26,8 +26,9 @@ void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uin
 // Gabor scale nu (0..4): magnitudes of the 7 orientations, face-wide min-max normalisation,
 // quantisation and integration of the 7 channels (one workgroup per face)
 // max_h: the tallest scaled face of the batch (sizes the padded-face LDS copy)
+void launch_check_mag_sqrt(uint32_t lo, uint32_t n, uint32_t* bad, int blocks, hipStream_t s);
 void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t* gray, const float* coef, float* mag,
-                  uint16_t* chan, hipStream_t s);
+                  uint16_t* chan, int* redo, int force_exact, hipStream_t s);
 hipError_t set_gabor_lds_limit(int bytes);
 // integral channels 0 (gray), 36, 37 (Sobel)
 void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t* chan, hipStream_t s);

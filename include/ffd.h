@@ -188,6 +188,11 @@ typedef struct {
 
 ffd_status ffd_get_trace(ffd_engine* engine, int32_t index, ffd_trace* trace);
 
+/* Diagnostic: the Gabor kernels' branch-free magnitude sqrt (mag_sqrt, csrc/ffd_kernels.hip) checked
+ * on the device against sqrtf for every float of its exact domain (+0 and all finite s >= 2^-96);
+ * magnitudes outside it make the fast Gabor pass hand the face to its exact (sqrtf) instance. */
+ffd_status ffd_check_mag_sqrt(ffd_engine* engine, uint64_t* checked, uint64_t* mismatches);
+
 /* Per-stage device time of the pipeline, measured with hipEvents on the engine stream
  * (kernel boundaries only; used by bench.py for the roofline of the dominant kernel).
  * ffd_set_profiling(e, 1) enables and resets the accumulators. */

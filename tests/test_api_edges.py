@@ -7,8 +7,9 @@
   face (125 x 375); and the per-face statuses of the boxes it rejects;
 * the multi-device entry points on the one device a box has (ffd_group_*, ffd_engine_join +
   ffd_gather_faces through RCCL);
-* the engine's non-default configurations (3 x 3 patch blocks, FFD_CHANNEL_STREAMS=2, two streams), read at
-  ffd_engine_create."""
+* the engine's non-default configurations (3 x 3 patch blocks, FFD_CHANNEL_STREAMS=2, two streams, every
+  face through the exact Gabor instance), read at ffd_engine_create;
+* the Gabor kernels' branch-free magnitude sqrt against sqrtf for every float of its domain."""
 import os
 
 import numpy as np
@@ -100,7 +101,7 @@ def test_rccl_join_and_gather_single_rank(engine):
 
 
 @pytest.mark.parametrize("env", [{"FFD_TRAV_G_FFD": "3", "FFD_TRAV_G_HP": "3"}, {"FFD_CHANNEL_STREAMS": "2"},
-                                 {"FFD_STREAMS": "2", "FFD_CHUNK": "5"}])
+                                 {"FFD_STREAMS": "2", "FFD_CHUNK": "5"}, {"FFD_GABOR_EXACT": "1"}])
 def test_engine_variants_bit_exact(model_path, oracle_mod, env):
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
@@ -121,3 +122,10 @@ def test_engine_variants_bit_exact(model_path, oracle_mod, env):
             assert np.float32(f.headpose) == np.float32(ref["headpose"])
     finally:
         ff.close()
+
+
+def test_mag_sqrt_exhaustive(engine):
+    """mag_sqrt (csrc/ffd_kernels.hip) == sqrtf on the device for +0 and every finite s >= 2^-96."""
+    checked, bad = engine.check_mag_sqrt()
+    assert checked == 1 + (0x7F800000 - 0x0F800000)
+    assert bad == 0
