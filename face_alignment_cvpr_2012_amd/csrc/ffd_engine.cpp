@@ -162,7 +162,7 @@ static void encode_test(const uint4& n, uint32_t& lo, uint32_t& hi) {
     throw std::runtime_error("split outside the pair-record encoding");
   const uint32_t t = (uint32_t)thr & 0x3FFu;
   lo = x1 | y1 << 5 | x2 << 10 | y2 << 15 | ch << 20 | (t & 63u) << 26;
-  hi = (w1 - 1) | (h1 - 1) << 5 | (w2 - 1) << 10 | (h2 - 1) << 15 | (t >> 6) << 20;
+  hi = w1 | h1 << 5 | w2 << 10 | h2 << 15 | (t >> 6) << 20;  // sides as they are: no +1 in the walk
 }
 
 // Depth-first pair layout: a pair (a, b) is followed by the pair of a's children and a's whole

@@ -665,9 +665,11 @@ __device__ __forceinline__ int node_off(uint32_t enc, int ld) {
 // halves split at h >> 1 rows, each exact modulo 2^16 (rect_mean16), and the quotient
 // (int)(R / (float)(w*h)) as fma(R, rcp(area), 0.00075) truncated: equal to the integer quotient
 // for every R in [0, 255 area], area in [1, 484], with rcp off by up to 2 ulp (tests/test_numerics.py).
-__device__ __forceinline__ int rect_mean_lds(const unsigned char* __restrict__ p, uint32_t w, uint32_t h, int ld2) {
+// hh = h >> 1 (taken by the caller straight from the record's bits).
+__device__ __forceinline__ int rect_mean_lds(const unsigned char* __restrict__ p, uint32_t w, uint32_t h, uint32_t hh,
+                                             int ld2) {
   const int wb = (int)(2u * w);
-  const int r1 = (int)__umul24(h >> 1, (unsigned)ld2), r2 = (int)__umul24(h, (unsigned)ld2);
+  const int r1 = (int)__umul24(hh, (unsigned)ld2), r2 = (int)__umul24(h, (unsigned)ld2);
   const uint32_t a = *reinterpret_cast<const uint16_t*>(p), b = *reinterpret_cast<const uint16_t*>(p + wb);
   const uint32_t c = *reinterpret_cast<const uint16_t*>(p + r1), d = *reinterpret_cast<const uint16_t*>(p + r1 + wb);
   const uint32_t f0 = *reinterpret_cast<const uint16_t*>(p + r2), f1 = *reinterpret_cast<const uint16_t*>(p + r2 + wb);
@@ -821,12 +823,16 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       const unsigned char* base = reinterpret_cast<const unsigned char*>(win) +
                                   2 * ((yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh);
       auto test = [&](uint32_t lo, uint32_t hi) {
-        const unsigned char* cb = base + __umul24((lo >> 20) & 63u, (unsigned)chs2);
-        const int p1 = rect_mean_lds(cb + 2 * (int)__umul24((lo >> 5) & 31u, (unsigned)LW) + 2 * (int)(lo & 31u),
-                                     (hi & 31u) + 1u, ((hi >> 5) & 31u) + 1u, ld2);
-        const int p2 = rect_mean_lds(cb + 2 * (int)__umul24((lo >> 15) & 31u, (unsigned)LW) + 2 * (int)((lo >> 10) & 31u),
-                                     ((hi >> 10) & 31u) + 1u, ((hi >> 15) & 31u) + 1u, ld2);
-        const int thr = (int)(((lo >> 26) | (hi >> 20) << 6) << 22) >> 22;  // 10-bit two's complement
+        // (fields by bit-field extracts; bits of hi above 23 are the record's child offset, never read)
+        const unsigned char* cb = base + __umul24(__builtin_amdgcn_ubfe(lo, 20, 6), (unsigned)chs2);
+        const int p1 = rect_mean_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 0, 5),
+                                     __builtin_amdgcn_ubfe(hi, 0, 5), __builtin_amdgcn_ubfe(hi, 5, 5),
+                                     __builtin_amdgcn_ubfe(hi, 6, 4), ld2);
+        const int p2 = rect_mean_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 15, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 10, 5),
+                                     __builtin_amdgcn_ubfe(hi, 10, 5), __builtin_amdgcn_ubfe(hi, 15, 5),
+                                     __builtin_amdgcn_ubfe(hi, 16, 4), ld2);
+        // 10-bit two's complement: sign-extended thr[9:6] (hi[23:20]) above thr[5:0] (lo[31:26])
+        const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | (lo >> 26));
         return (p1 - p2) <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
       };
       // levels 0..log2(topn): heap-ordered pair records in LDS (the children pair of node (h, s) is
@@ -834,7 +840,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       const uint4* trec = top_rec + t * topn;
       uint32_t h = 0, s = 0;
       uint4 R = trec[0];
-      uint32_t lo = R.x, hi = R.z & 0xFFFFFFu;
+      uint32_t lo = R.x, hi = R.z;
       while (((lo >> 20) & 63u) != 63u) {
         const uint32_t h2 = h ? 2u * h + s : 1u;
         if (h2 >= (uint32_t)topn) break;
@@ -843,7 +849,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         h = h2;
         R = N;
         lo = s ? R.y : R.x;
-        hi = (s ? R.w : R.z) & 0xFFFFFFu;
+        hi = s ? R.w : R.z;
       }
       uint32_t P = top_i[t * topn + h];
       // deeper levels: pair records from HBM (L2), the children pair requested before the test
@@ -857,7 +863,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         P = Q;
         R = N;
         lo = s ? R.y : R.x;
-        hi = (s ? R.w : R.z) & 0xFFFFFFu;
+        hi = s ? R.w : R.z;
       }
       out[(xi * B.ny + yi) * B.T + t] = (int32_t)((lo & 0xFFFFFu) | hi << 20);  // reference order
     }
