@@ -37,10 +37,10 @@ constexpr uint32_t LEAF_BIT = 0x80000000u;
 // Pair records (k_traverse): 16 bytes = the two children (c0, c1) of one internal node, each as
 // a 56-bit test, plus a 16-bit offset.  Words: x = lo(c0), y = lo(c1), z = hi(c0) | off1[7:0] << 24,
 // w = hi(c1) | off1[15:8] << 24, where for a split node
-//   lo = x1 | y1 << 5 | x2 << 10 | y2 << 15 | ch << 20 | thr[5:0] << 26
+//   lo = x1 | y1 << 5 | x2 << 10 | y2 << 15 | thr[5:0] << 20 | ch << 26
 //   hi = w1 | h1 << 5 | w2 << 10 | h2 << 15 | thr[9:6] << 20
 // (rectangles patch-relative, sides 1..22, threshold 10-bit two's complement), and for a leaf
-// ch = 63 with the leaf ordinal = lo[19:0] | hi << 20.  Depth-first layout per tree: the pair of
+// ch = 63 (lo >= 63 << 26) with the leaf ordinal = lo[19:0] | hi << 20.  Depth-first layout per tree: the pair of
 // c0's children is the next record, c1's children are off1 records ahead (off1 = 0: the 32-bit
 // offset is far[pair]).  Each tree starts with a root pair (root, unused leaf).
 // Source fields: ThresholdSplit<SimplePatchFeature> (ThresholdSplit.hpp:51-67, ImageSample.hpp:83-90).

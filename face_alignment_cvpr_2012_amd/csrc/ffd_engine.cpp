@@ -148,7 +148,7 @@ void flatten_forest(const ModelFile& m, const std::string& p, std::vector<uint4>
 static void encode_test(const uint4& n, uint32_t& lo, uint32_t& hi) {
   if (n.x & LEAF_BIT) {
     const uint64_t ord = n.x & ~LEAF_BIT;
-    lo = (uint32_t)(ord & 0xFFFFFu) | 63u << 20;
+    lo = (uint32_t)(ord & 0xFFFFFu) | 63u << 26;
     hi = (uint32_t)(ord >> 20) & 0xFFFFFFu;
     return;
   }
@@ -161,7 +161,7 @@ static void encode_test(const uint4& n, uint32_t& lo, uint32_t& hi) {
       w2 > 22 || h2 < 1 || h2 > 22 || thr < -512 || thr > 511)
     throw std::runtime_error("split outside the pair-record encoding");
   const uint32_t t = (uint32_t)thr & 0x3FFu;
-  lo = x1 | y1 << 5 | x2 << 10 | y2 << 15 | ch << 20 | (t & 63u) << 26;
+  lo = x1 | y1 << 5 | x2 << 10 | y2 << 15 | (t & 63u) << 20 | ch << 26;  // ch on top: leaf = lo >= 63 << 26
   hi = w1 | h1 << 5 | w2 << 10 | h2 << 15 | (t >> 6) << 20;  // sides as they are: no +1 in the walk
 }
 
@@ -228,7 +228,7 @@ void ffd_host::build_tree_tops(const std::vector<uint4>& pairs, const std::vecto
                                std::vector<uint32_t>& top_idx) {
   tops.assign(proots.size() * TOP_CAP, make_uint4(0, 0, 0, 0));
   top_idx.assign(proots.size() * TOP_CAP, 0u);
-  auto leaf = [](uint32_t lo) { return ((lo >> 20) & 63u) == 63u; };
+  auto leaf = [](uint32_t lo) { return (lo >> 26) == 63u; };
   for (size_t t = 0; t < proots.size(); t++) {
     uint4* rec = &tops[t * TOP_CAP];
     uint32_t* idx = &top_idx[t * TOP_CAP];

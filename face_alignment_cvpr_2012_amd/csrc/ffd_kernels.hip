@@ -673,8 +673,10 @@ __device__ __forceinline__ int rect_mean_lds(const unsigned char* __restrict__ p
   const uint32_t a = *reinterpret_cast<const uint16_t*>(p), b = *reinterpret_cast<const uint16_t*>(p + wb);
   const uint32_t c = *reinterpret_cast<const uint16_t*>(p + r1), d = *reinterpret_cast<const uint16_t*>(p + r1 + wb);
   const uint32_t f0 = *reinterpret_cast<const uint16_t*>(p + r2), f1 = *reinterpret_cast<const uint16_t*>(p + r2 + wb);
-  const uint32_t top = (d - c - b + a) & 0xFFFFu, bot = (f1 - f0 - d + c) & 0xFFFFu;
-  return (int)__builtin_fmaf((float)(top + bot), __builtin_amdgcn_rcpf((float)__umul24(w, h)), 0.00075f);
+  // top = (a - b) + (d - c), bot = (f1 - f0) - (d - c), each mod 2^16 (u16 arithmetic), R = top + bot
+  typedef unsigned short u16;
+  const u16 dc = (u16)(d - c), top = (u16)((u16)(a - b) + dc), bot = (u16)((u16)(f1 - f0) - dc);
+  return (int)__builtin_fmaf((float)((uint32_t)top + bot), __builtin_amdgcn_rcpf((float)__umul24(w, h)), 0.00075f);
 }
 
 // Tree<S>::evaluateMT over global u16 planes (ffd_forest_eval_leaves hook).
@@ -824,15 +826,15 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
                                   2 * ((yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh);
       auto test = [&](uint32_t lo, uint32_t hi) {
         // (fields by bit-field extracts; bits of hi above 23 are the record's child offset, never read)
-        const unsigned char* cb = base + __umul24(__builtin_amdgcn_ubfe(lo, 20, 6), (unsigned)chs2);
+        const unsigned char* cb = base + __umul24(lo >> 26, (unsigned)chs2);
         const int p1 = rect_mean_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 0, 5),
                                      __builtin_amdgcn_ubfe(hi, 0, 5), __builtin_amdgcn_ubfe(hi, 5, 5),
                                      __builtin_amdgcn_ubfe(hi, 6, 4), ld2);
         const int p2 = rect_mean_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 15, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 10, 5),
                                      __builtin_amdgcn_ubfe(hi, 10, 5), __builtin_amdgcn_ubfe(hi, 15, 5),
                                      __builtin_amdgcn_ubfe(hi, 16, 4), ld2);
-        // 10-bit two's complement: sign-extended thr[9:6] (hi[23:20]) above thr[5:0] (lo[31:26])
-        const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | (lo >> 26));
+        // 10-bit two's complement: sign-extended thr[9:6] (hi[23:20]) above thr[5:0] (lo[25:20])
+        const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
         return (p1 - p2) <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
       };
       // levels 0..log2(topn): heap-ordered pair records in LDS (the children pair of node (h, s) is
@@ -841,7 +843,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       uint32_t h = 0, s = 0;
       uint4 R = trec[0];
       uint32_t lo = R.x, hi = R.z;
-      while (((lo >> 20) & 63u) != 63u) {
+      while (lo < (63u << 26)) {  // not a leaf (ch = 63)
         const uint32_t h2 = h ? 2u * h + s : 1u;
         if (h2 >= (uint32_t)topn) break;
         const uint4 N = trec[h2];
@@ -853,7 +855,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       }
       uint32_t P = top_i[t * topn + h];
       // deeper levels: pair records from HBM (L2), the children pair requested before the test
-      while (((lo >> 20) & 63u) != 63u) {
+      while (lo < (63u << 26)) {  // not a leaf (ch = 63)
         // children pair of the current node: right after its pair (child 0), or off1 away (child 1)
         const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
         uint32_t Q = P + (s ? off1 : 1u);
