@@ -65,6 +65,28 @@ def make_crops(n, size=150, seed=2012, fixtures=None):
     return out, src
 
 
+def crop_ground_truth(n, size=150, seed=2012, fixtures=None):
+    """The annotated landmarks (data/imgs/index_random_subset.txt, faces.npz 'parts', box-relative) of the n
+    crops make_crops(n, size, seed) returns, mapped into crop pixel coordinates, float64 [n, 10, 2].
+    analyzeFace(crop, Rect(0, 0, size, size)) reports bbox-relative points, i.e. the same frame.
+    The jitter / scale draws are the first two of make_crops' generator, so they are re-drawn here."""
+    fx = fixtures or load_fixtures()
+    boxes, parts = fx["boxes"], fx["parts"].astype(np.float64)
+    rng = np.random.default_rng(seed)
+    src = np.arange(n) % len(boxes)
+    jit = rng.integers(-6, 7, size=(n, 2))
+    scl = rng.uniform(0.95, 1.05, size=n)
+    x, y, w, h = (boxes[src, j].astype(np.float64) for j in range(4))
+    cx = x + w / 2.0 + jit[:, 0]
+    cy = y + h / 2.0 + jit[:, 1]
+    side = w * scl
+    # make_crops samples crop pixel u at source coordinate cx - side/2 + (u + 0.5) side/size - 0.5
+    gt = np.empty((n, parts.shape[1], 2), np.float64)
+    gt[:, :, 0] = (parts[src, :, 0] + x[:, None] + 0.5 - (cx - side / 2.0)[:, None]) * (size / side)[:, None] - 0.5
+    gt[:, :, 1] = (parts[src, :, 1] + y[:, None] + 0.5 - (cy - side / 2.0)[:, None]) * (size / side)[:, None] - 0.5
+    return gt
+
+
 def _interp_matrix(n, m, cell=64.0):
     """(n, m) matrix of linear interpolation weights: output i samples coarse coordinate
     (i + 0.5) / cell (edge clamped), as _bilinear does along one axis."""

@@ -100,3 +100,18 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run"],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_bench_uneven_rank_counts_gather():
+    """Ranks with different face counts (--detect / ragged frame shards): every rank pads
+    to the MAX local count (records_per_rank), so no rank overruns its buffer and nothing is dropped."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "3", "--dry-run", "--uneven",
+                        "--faces", "10"], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 3 and line["faces"] == 3 + 4 + 5 and line["gather_ok"]

@@ -57,9 +57,10 @@ def test_many_faces_per_image(engine, oracle_mod, fixtures):
         dx, dy, dw = (int(v) for v in rng.integers(-8, 9, size=3))
         boxes.append((max(0, x + dx), max(0, y + dy), w + dw, w + dw))
     faces = engine.analyzeFaces([img], boxes, np.zeros(64, np.int32))
-    for i in (0, 17, 63):
+    for i in range(64):
         ref, _ = oracle_mod.analyze_face(img, boxes[i], threads=8)
         assert np.array_equal(faces[i].ffd_cordinates, ref["points"]), i
+        assert np.float32(faces[i].headpose).tobytes() == np.float32(ref["headpose"]).tobytes(), i
 
 
 @pytest.mark.gpu
