@@ -467,6 +467,7 @@ def main():
     geo = [ff.geometry(int(b[2]), int(b[3])) for b in wl.boxes[:256]]
     mean_wh = (float(np.mean([g[0] for g in geo])), float(np.mean([g[1] for g in geo])))
     d_root = None
+    rccl_ranks = None  # no communicator at N = 1 (nothing to gather)
     if world > 1:
         # the engines join one RCCL communicator inside libffd.so (ffd_engine_join); the 128-byte id
         # travels over the launcher's process group
@@ -474,6 +475,10 @@ def main():
                            device=dev)
         dist.broadcast(cid, 0)
         ff.join(bytes(cid.cpu().tolist()), world, rank)
+        rccl_ranks, rccl_rank = ff.comm_info()  # ncclCommCount / ncclCommUserRank on libffd.so's communicator
+        if (rccl_ranks, rccl_rank) != (world, rank):
+            raise SystemExit(f"bench.py: libffd.so's RCCL communicator has {rccl_ranks} ranks (this rank {rccl_rank}), "
+                             f"expected {world} (rank {rank})")
         if rank == 0:
             d_root = torch.zeros(world * per * rec, dtype=torch.uint8, device=dev)
 
@@ -575,6 +580,7 @@ def main():
                     "pretrained reference forests converted to model/ffd_model.bin",
             "config": {"workload": wl.describe, "faces_per_gpu": n, "mean_face": [round(W, 1), round(H, 1)],
                        "parallelism": f"faces sharded x{world}"},
+            "rccl_ranks": rccl_ranks,
             "landmark_px_error_vs_cpu": px["vs_cpu_px"],
             "landmark_px_error": px,
             "roofline": {"bound": bound, "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": unit,

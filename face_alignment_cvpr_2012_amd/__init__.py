@@ -86,6 +86,16 @@ class _Desc(ctypes.Structure):
                 ("hp_option", _HpOpt), ("mp_option", _MpOpt), ("ms_option", _MsOpt)]
 
 
+class _HpLeaf(ctypes.Structure):          # ffd_headpose_leaf = HeadPoseLeaf (HeadPoseSample.hpp:144-162)
+    _fields_ = [("hp_nsamples", ctypes.c_int32), ("hp_foreground", ctypes.c_float), ("hp_labels", ctypes.c_int32 * 5)]
+
+
+class _MpLeaf(ctypes.Structure):          # ffd_mp_leaf = MPLeaf (MPSample.hpp:137-159)
+    _fields_ = [("mp_samples", ctypes.c_int32), ("mp_foreground", ctypes.c_float),
+                ("mp_parts_offset", (ctypes.c_int32 * 2) * 10), ("mp_parts_variance", ctypes.c_float * 10),
+                ("mp_prob_foreground", ctypes.c_float * 10)]
+
+
 class _DetOpt(ctypes.Structure):
     _fields_ = [("min_feature_size", ctypes.c_int32), ("min_neighbors", ctypes.c_int32),
                 ("search_scale_factor", ctypes.c_float), ("widen", ctypes.c_int32)]
@@ -103,9 +113,9 @@ EXPORTED_SYMBOLS = (
     "ffd_engine_desc_init", "ffd_engine_create", "ffd_engine_destroy", "ffd_last_error", "ffd_face_geometry",
     "ffd_analyze_faces", "ffd_analyze_faces_device", "ffd_synchronize", "ffd_stream", "ffd_extract_channels",
     "ffd_forest_eval_leaves", "ffd_get_trace", "ffd_version", "ffd_set_profiling", "ffd_get_stage_times", "ffd_check_mag_sqrt",
-    "ffd_stage_name", "ffd_status_string", "ffd_estimate_headpose", "ffd_estimate_facial_features",
+    "ffd_stage_name", "ffd_status_string", "ffd_estimate_headpose", "ffd_estimate_facial_features", "ffd_forest_leaves",
     "ffd_group_create", "ffd_group_destroy", "ffd_group_last_error", "ffd_group_size", "ffd_group_engine",
-    "ffd_group_analyze_faces", "ffd_comm_id", "ffd_engine_join", "ffd_gather_faces",
+    "ffd_group_analyze_faces", "ffd_comm_id", "ffd_engine_join", "ffd_gather_faces", "ffd_engine_comm_info",
     "ffd_detect_options_init", "ffd_detect_faces", "ffd_detect_faces_device", "ffd_analyze_images",
     "ffd_detect_candidates", "ffd_model_open", "ffd_model_close", "ffd_model_last_error", "ffd_model_num_trees", "ffd_model_tree_save_path",
     "ffd_model_tree_archive", "ffd_model_save_tree",
@@ -154,9 +164,10 @@ def lib():
     L.ffd_status_string.argtypes = [ctypes.c_int32]
     L.ffd_status_string.restype = ctypes.c_char_p
     L.ffd_estimate_headpose.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
-                                        P(_Rect), P(ctypes.c_float), P(ctypes.c_float)]
+                                        P(_Rect), P(_HpOpt), P(ctypes.c_float), P(ctypes.c_float)]
     L.ffd_estimate_facial_features.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
-                                               P(_Rect), ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+                                               P(_Rect), ctypes.c_void_p, ctypes.c_int32, P(_MpOpt), ctypes.c_void_p]
+    L.ffd_forest_leaves.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
     L.ffd_group_create.argtypes = [P(_Desc), ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_void_p)]
     L.ffd_group_destroy.argtypes = [ctypes.c_void_p]
     L.ffd_group_last_error.argtypes = [ctypes.c_void_p]
@@ -169,6 +180,7 @@ def lib():
     L.ffd_comm_id.argtypes = [ctypes.c_void_p]
     L.ffd_engine_join.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
     L.ffd_gather_faces.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
+    L.ffd_engine_comm_info.argtypes = [ctypes.c_void_p, P(ctypes.c_int32), P(ctypes.c_int32)]
     L.ffd_detect_options_init.argtypes = [P(_DetOpt)]
     L.ffd_detect_faces.argtypes = [ctypes.c_void_p, P(_Image), ctypes.c_int32, P(_DetOpt), ctypes.c_void_p,
                                    ctypes.c_void_p, ctypes.c_int32, P(ctypes.c_int32)]
@@ -193,8 +205,8 @@ def lib():
                  "ffd_model_open", "ffd_model_tree_save_path", "ffd_model_tree_archive", "ffd_model_save_tree","ffd_engine_create", "ffd_face_geometry", "ffd_analyze_faces", "ffd_analyze_faces_device",
                  "ffd_synchronize", "ffd_extract_channels", "ffd_forest_eval_leaves", "ffd_get_trace",
                  "ffd_set_profiling", "ffd_get_stage_times", "ffd_estimate_headpose",
-                 "ffd_estimate_facial_features", "ffd_group_create", "ffd_group_analyze_faces", "ffd_comm_id",
-                 "ffd_engine_join", "ffd_gather_faces", "ffd_group_size"):
+                 "ffd_estimate_facial_features", "ffd_forest_leaves", "ffd_group_create", "ffd_group_analyze_faces", "ffd_comm_id",
+                 "ffd_engine_join", "ffd_gather_faces", "ffd_engine_comm_info", "ffd_group_size"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
@@ -496,35 +508,69 @@ class FaceForest:
         _check(lib().ffd_extract_channels(self._h, g.ctypes.data, w, h, out.ctypes.data), self._h)
         return out
 
-    def estimateHeadPose(self, channels, face_bbox=None):
+    def estimateHeadPose(self, channels, face_bbox=None, options=None):
         """FaceForest::estimateHeadPose (src/FaceForest.cpp:60-72) on an image sample's 38 integral
-        channels (extract_channels layout); face_bbox = the patch region (default: whole sample).
-        Returns (headpose, variance)."""
+        channels (extract_channels layout); face_bbox = the patch region (default: whole sample);
+        options: a HeadPoseEstimatorOption (default: the engine's).  Returns (headpose, variance)."""
         ch = np.ascontiguousarray(channels, np.uint32)
         _, h1, w1 = ch.shape
         r = _Rect(*[int(v) for v in (face_bbox or (0, 0, w1 - 1, h1 - 1))])
+        o = None
+        if options is not None:
+            o = _HpOpt(options.num_head_pose_labels, options.step_size, options.min_foreground_probability)
         hp, var = ctypes.c_float(), ctypes.c_float()
-        _check(lib().ffd_estimate_headpose(self._h, ch.ctypes.data, w1 - 1, h1 - 1, ctypes.byref(r), ctypes.byref(hp),
+        _check(lib().ffd_estimate_headpose(self._h, ch.ctypes.data, w1 - 1, h1 - 1, ctypes.byref(r),
+                                           ctypes.byref(o) if o is not None else None, ctypes.byref(hp),
                                            ctypes.byref(var)), self._h)
         return hp.value, var.value
 
-    def estimateFacialFeatures(self, channels, face_bbox, tree_ids):
+    def estimateFacialFeatures(self, channels, face_bbox, tree_ids, options=None):
         """FaceForest::estimateFacialFeatures (src/FaceForest.cpp:74-95): the FFD forest made of the
-        global tree ids (forest * 20 + tree), default MeanShiftOption; 10 x 2 int landmarks in sample
-        coordinates."""
+        global tree ids (forest * 20 + tree), options: a MultiPartEstimatorOption (default: the
+        engine's), default MeanShiftOption; 10 x 2 int landmarks in sample coordinates ((0, 0) past
+        num_parts)."""
         ch = np.ascontiguousarray(channels, np.uint32)
         _, h1, w1 = ch.shape
         r = _Rect(*[int(v) for v in (face_bbox or (0, 0, w1 - 1, h1 - 1))])
         t = np.ascontiguousarray(tree_ids, np.int32)
+        o = None
+        if options is not None:
+            o = _MpOpt(options.num_parts, options.step_size, options.min_samples, options.min_forground,
+                       options.min_pf, options.max_variance, options.step_size_y)
         pts = np.zeros((10, 2), np.int32)
         _check(lib().ffd_estimate_facial_features(self._h, ch.ctypes.data, w1 - 1, h1 - 1, ctypes.byref(r),
-                                                  t.ctypes.data, t.size, pts.ctypes.data), self._h)
+                                                  t.ctypes.data, t.size, ctypes.byref(o) if o is not None else None,
+                                                  pts.ctypes.data), self._h)
         return pts
+
+    def leaves(self, kind, leaf_ids):
+        """Leaf payloads (HeadPoseLeaf / MPLeaf members as a dict of arrays) of model leaf ordinals
+        (ffd_forest_leaves), what Forest<S>::evaluateMT's Leaf* gives the reference's callers."""
+        ids = np.ascontiguousarray(leaf_ids, np.int32).reshape(-1)
+        T = _HpLeaf if kind == FOREST_HEADPOSE else _MpLeaf
+        out = (T * max(1, ids.size))()
+        _check(lib().ffd_forest_leaves(self._h, kind, ids.ctypes.data, ids.size, out), self._h)
+        recs = out[: ids.size]
+        if kind == FOREST_HEADPOSE:
+            return dict(hp_nsamples=np.array([r.hp_nsamples for r in recs], np.int32),
+                        hp_foreground=np.array([r.hp_foreground for r in recs], np.float32),
+                        hp_labels=np.array([list(r.hp_labels) for r in recs], np.int32).reshape(-1, 5))
+        return dict(mp_samples=np.array([r.mp_samples for r in recs], np.int32),
+                    mp_foreground=np.array([r.mp_foreground for r in recs], np.float32),
+                    mp_parts_offset=np.array([[list(p) for p in r.mp_parts_offset] for r in recs], np.int32).reshape(-1, 10, 2),
+                    mp_parts_variance=np.array([list(r.mp_parts_variance) for r in recs], np.float32).reshape(-1, 10),
+                    mp_prob_foreground=np.array([list(r.mp_prob_foreground) for r in recs], np.float32).reshape(-1, 10))
 
     def join(self, comm_id, n_ranks, rank):
         """Join the RCCL communicator `comm_id` (bytes from comm_id() on one rank) as `rank`."""
         buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(bytes(comm_id))
         _check(lib().ffd_engine_join(self._h, buf, n_ranks, rank), self._h)
+
+    def comm_info(self):
+        """(ranks, this rank) of the RCCL communicator the engine joined (ncclCommCount / ncclCommUserRank)."""
+        n, r = ctypes.c_int32(), ctypes.c_int32()
+        _check(lib().ffd_engine_comm_info(self._h, ctypes.byref(n), ctypes.byref(r)), self._h)
+        return n.value, r.value
 
     def gather(self, d_local, n_per_rank, d_root, root=0):
         """Enqueue the RCCL gather of n_per_rank ffd_face records per rank into d_root on `root`."""

@@ -291,82 +291,106 @@ void ffd_engine::load_model(const std::string& path) {
   upload(mp_sizes, sizes, main_stream());
   HIP_CHECK(hipStreamSynchronize(main_stream()));  // host vectors are reused below
 
-  // head-pose leaf value m (face_utils.cpp:223-228), -1 when the leaf is filtered out
+  // option-dependent leaf tables (head-pose values, FFD vote records) for desc's options
+  hp_leaves = (int64_t)m.get("hp.leaf_n").count();
+  mp_leaves = (int64_t)m.get("mp.leaf_n").count();
+  upload(hp_m, hp_leaf_values(m, desc.hp_option), main_stream());
   {
-    const auto& n = m.get("hp.leaf_n");
-    const auto& fg = m.get("hp.leaf_fg");
-    const auto& lb = m.get("hp.leaf_labels");
-    hp_leaves = (int64_t)n.count();
-    std::vector<float> mv(hp_leaves);
-    const int nl = std::min(desc.hp_option.num_head_pose_labels, (int)FFD_NUM_HP_LABELS);
-    for (int64_t L = 0; L < hp_leaves; L++) {
-      const float f = fg.as<float>()[L];
-      if (f > desc.hp_option.min_foreground_probability) {
-        float v = 0;
-        for (int j = 0; j < nl; j++) v += lb.as<int32_t>()[L * 5 + j] * j;
-        v /= (n.as<int32_t>()[L] * f);
-        mv[L] = v;
-      } else {
-        mv[L] = -1.f;
-      }
-    }
-    upload(hp_m, mv, main_stream());
-  }
-  // FFD leaf vote mask / weight / offsets (face_utils.cpp:283-298)
-  {
-    const auto& n = m.get("mp.leaf_n");
-    const auto& fg = m.get("mp.leaf_fg");
-    const auto& off = m.get("mp.leaf_offset");
-    const auto& var = m.get("mp.leaf_var");
-    const auto& pf = m.get("mp.leaf_pf");
-    mp_leaves = (int64_t)n.count();
-    // per-leaf vote records for k_votes: the filter of face_utils.cpp:276-290 precomputed as a
-    // part mask, fg, and the offsets of the voting parts.  Compact 32-B records (offsets as u8
-    // pairs relative to per-axis biases) when every voting offset fits, else 64-B records.
-    const auto& op = desc.mp_option;
-    const int np = std::min(op.num_parts, NPARTS);
-    std::vector<uint32_t> mask(mp_leaves);
-    int mnx = 1 << 30, mny = 1 << 30, mxx = -(1 << 30), mxy = -(1 << 30);
-    for (int64_t L = 0; L < mp_leaves; L++) {
-      uint32_t mk = 0;
-      const float f = fg.as<float>()[L];
-      for (int i = 0; i < np; i++) {
-        float min_pf = op.min_pf;
-        if (i == 0 || i == 7) min_pf *= 1.5;  // outer eye corners
-        if (f > op.min_forground && pf.as<float>()[L * 10 + i] > min_pf && var.as<float>()[L * 10 + i] < op.max_variance &&
-            n.as<int32_t>()[L] > op.min_samples) {
-          mk |= 1u << i;
-          const int x = off.as<int16_t>()[(L * 10 + i) * 2], y = off.as<int16_t>()[(L * 10 + i) * 2 + 1];
-          mnx = std::min(mnx, x); mxx = std::max(mxx, x);
-          mny = std::min(mny, y); mxy = std::max(mxy, y);
-        }
-      }
-      mask[L] = mk;
-    }
-    vote_rec_compact = mxx - mnx <= 255 && mxy - mny <= 255;
-    vote_bias_x = vote_rec_compact && mnx <= mxx ? mnx : 0;
-    vote_bias_y = vote_rec_compact && mny <= mxy ? mny : 0;
-    const int words = vote_rec_compact ? 8 : 16;
-    std::vector<uint32_t> rec(mp_leaves * words, 0);
-    for (int64_t L = 0; L < mp_leaves; L++) {
-      uint32_t* r = &rec[L * words];
-      r[0] = mask[L];
-      std::memcpy(&r[1], &fg.as<float>()[L], 4);
-      for (int i = 0; i < NPARTS; i++) {
-        const int x = off.as<int16_t>()[(L * 10 + i) * 2], y = off.as<int16_t>()[(L * 10 + i) * 2 + 1];
-        if (vote_rec_compact) {
-          if (!((mask[L] >> i) & 1u)) continue;  // offsets of non-voting parts are never read
-          const uint32_t u = (uint32_t)(x - vote_bias_x) | (uint32_t)(y - vote_bias_y) << 8;
-          r[2 + i / 2] |= u << (16 * (i & 1));
-        } else {
-          r[2 + i] = (uint32_t)(uint16_t)x | (uint32_t)(uint16_t)y << 16;
-        }
-      }
-    }
-    upload(mp_rec, rec, main_stream());
+    VoteTable vt = mp_vote_records(m, desc.mp_option);
+    vote_rec_compact = vt.compact;
+    vote_bias_x = vt.bias_x;
+    vote_bias_y = vt.bias_y;
+    upload(mp_rec, vt.rec, main_stream());
   }
   load_cascade(m);
   HIP_CHECK(hipStreamSynchronize(main_stream()));
+}
+
+// head-pose leaf value m (face_utils.cpp:223-228): sum_j labels[j] * j over the option's labels,
+// divided by (n * fg); -1 when the leaf fails the option's foreground test (it then casts no value).
+std::vector<float> ffd_host::hp_leaf_values(const ffd::ModelFile& m, const ffd_headpose_option& o) {
+  const auto& n = m.get("hp.leaf_n");
+  const auto& fg = m.get("hp.leaf_fg");
+  const auto& lb = m.get("hp.leaf_labels");
+  const int64_t L = (int64_t)n.count();
+  std::vector<float> mv(L);
+  const int nl = std::max(0, std::min(o.num_head_pose_labels, (int)FFD_NUM_HP_LABELS));
+  for (int64_t i = 0; i < L; i++) {
+    const float f = fg.as<float>()[i];
+    if (f > o.min_foreground_probability) {
+      float v = 0;
+      for (int j = 0; j < nl; j++) v += lb.as<int32_t>()[i * 5 + j] * j;
+      v /= (n.as<int32_t>()[i] * f);
+      mv[i] = v;
+    } else {
+      mv[i] = -1.f;
+    }
+  }
+  return mv;
+}
+
+// FFD leaf vote records for k_votes: the filter of face_utils.cpp:276-290 under the option
+// precomputed as a part mask, fg, and the offsets of the voting parts.  Compact 32-B records (offsets
+// as u8 pairs relative to per-axis biases) when every voting offset fits, else 64-B records.
+ffd_host::VoteTable ffd_host::mp_vote_records(const ffd::ModelFile& m, const ffd_multipart_option& op) {
+  const auto& n = m.get("mp.leaf_n");
+  const auto& fg = m.get("mp.leaf_fg");
+  const auto& off = m.get("mp.leaf_offset");
+  const auto& var = m.get("mp.leaf_var");
+  const auto& pf = m.get("mp.leaf_pf");
+  const int64_t leaves = (int64_t)n.count();
+  const int np = std::max(0, std::min(op.num_parts, NPARTS));
+  std::vector<uint32_t> mask(leaves);
+  int mnx = 1 << 30, mny = 1 << 30, mxx = -(1 << 30), mxy = -(1 << 30);
+  for (int64_t L = 0; L < leaves; L++) {
+    uint32_t mk = 0;
+    const float f = fg.as<float>()[L];
+    for (int i = 0; i < np; i++) {
+      float min_pf = op.min_pf;
+      if (i == 0 || i == 7) min_pf *= 1.5;  // outer eye corners
+      if (f > op.min_forground && pf.as<float>()[L * 10 + i] > min_pf && var.as<float>()[L * 10 + i] < op.max_variance &&
+          n.as<int32_t>()[L] > op.min_samples) {
+        mk |= 1u << i;
+        const int x = off.as<int16_t>()[(L * 10 + i) * 2], y = off.as<int16_t>()[(L * 10 + i) * 2 + 1];
+        mnx = std::min(mnx, x); mxx = std::max(mxx, x);
+        mny = std::min(mny, y); mxy = std::max(mxy, y);
+      }
+    }
+    mask[L] = mk;
+  }
+  VoteTable vt;
+  vt.compact = mxx - mnx <= 255 && mxy - mny <= 255;
+  vt.bias_x = vt.compact && mnx <= mxx ? mnx : 0;
+  vt.bias_y = vt.compact && mny <= mxy ? mny : 0;
+  const int words = vt.compact ? 8 : 16;
+  vt.rec.assign(leaves * words, 0);
+  for (int64_t L = 0; L < leaves; L++) {
+    uint32_t* r = &vt.rec[L * words];
+    r[0] = mask[L];
+    std::memcpy(&r[1], &fg.as<float>()[L], 4);
+    for (int i = 0; i < NPARTS; i++) {
+      const int x = off.as<int16_t>()[(L * 10 + i) * 2], y = off.as<int16_t>()[(L * 10 + i) * 2 + 1];
+      if (vt.compact) {
+        if (!((mask[L] >> i) & 1u)) continue;  // offsets of non-voting parts are never read
+        const uint32_t u = (uint32_t)(x - vt.bias_x) | (uint32_t)(y - vt.bias_y) << 8;
+        r[2 + i / 2] |= u << (16 * (i & 1));
+      } else {
+        r[2 + i] = (uint32_t)(uint16_t)x | (uint32_t)(uint16_t)y << 16;
+      }
+    }
+  }
+  return vt;
+}
+
+// The model's leaf payload arrays, read from the model file on first use (per-call estimator
+// options, ffd_forest_leaves); the pipeline itself only uses the device tables.
+const ffd::ModelFile& ffd_engine::leaf_arrays() {
+  if (!leaf_model) {
+    auto m = std::make_shared<ffd::ModelFile>();
+    m->load(model_path, "leaf_");
+    leaf_model = m;
+  }
+  return *leaf_model;
 }
 
 // Gabor coefficients: scale 0 = createKernel / initGaborKernels (FeatureChannelFactory.hpp:186-251)
@@ -750,6 +774,7 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
       }
       e->ws.push_back(std::move(w));
     }
+    e->model_path = d->model_path;
     e->load_model(d->model_path);
     e->check_traverse_lds();
     e->build_gabor();
@@ -982,7 +1007,8 @@ namespace {
 // patch grid covers the region (face_utils.cpp:197-207,255-265: x from bbox.x while
 // x < bbox.x + bbox.width - patch) and votes keep sample coordinates (vox, voy).  The channel stage
 // is skipped (nochan); the caller launches the forest stages.
-FaceDesc stage_sample(ffd_engine* e, Workspace& w, const uint32_t* ch, int W, int H, const ffd_rect& r) {
+FaceDesc stage_sample(ffd_engine* e, Workspace& w, const uint32_t* ch, int W, int H, const ffd_rect& r, int hp_step,
+                      int mp_step_x, int mp_step_y) {
   FaceDesc f;
   std::memset(&f, 0, sizeof(f));
   const int rw = r.width, rh = r.height;
@@ -993,10 +1019,10 @@ FaceDesc stage_sample(ffd_engine* e, Workspace& w, const uint32_t* ch, int W, in
     return n;
   };
   f.W = rw; f.H = rh; f.bw = rw; f.bh = rh; f.scale = 1.f;
-  f.nhx = cnt(rw, e->desc.hp_option.step_size);
-  f.nhy = cnt(rh, e->desc.hp_option.step_size);
-  f.nmx = cnt(rw, e->desc.mp_option.step_size);
-  f.nmy = cnt(rh, e->mp_step_y());
+  f.nhx = cnt(rw, hp_step);
+  f.nhy = cnt(rh, hp_step);
+  f.nmx = cnt(rw, mp_step_x);
+  f.nmy = cnt(rh, mp_step_y);
   f.vox = r.x; f.voy = r.y;
   f.valid = 1; f.nochan = 1;
   f.plane = (int64_t)(rh + 1) * PITCH;
@@ -1027,6 +1053,45 @@ FaceDesc stage_sample(ffd_engine* e, Workspace& w, const uint32_t* ch, int W, in
   return f;
 }
 
+// Leaf tables for per-call estimator options: desc's own tables when the options match, else the
+// tables built for the last differing options (rebuilt when they change).
+bool same(const ffd_headpose_option& a, const ffd_headpose_option& b) {
+  return a.num_head_pose_labels == b.num_head_pose_labels &&
+         a.min_foreground_probability == b.min_foreground_probability;
+}
+bool same(const ffd_multipart_option& a, const ffd_multipart_option& b) {
+  return a.num_parts == b.num_parts && a.min_samples == b.min_samples && a.min_forground == b.min_forground &&
+         a.min_pf == b.min_pf && a.max_variance == b.max_variance;
+}
+const float* hp_table(ffd_engine* e, const ffd_headpose_option& o) {
+  if (same(o, e->desc.hp_option)) return e->hp_m.as<float>();
+  if (!e->alt.hp_ok || !same(o, e->alt.hp)) {
+    e->sync_all();
+    upload(e->alt.hp_m, hp_leaf_values(e->leaf_arrays(), o), e->main_stream());
+    HIP_CHECK(hipStreamSynchronize(e->main_stream()));
+    e->alt.hp = o;
+    e->alt.hp_ok = true;
+  }
+  return e->alt.hp_m.as<float>();
+}
+const uint4* mp_table(ffd_engine* e, const ffd_multipart_option& o, bool& compact, int& bx, int& by) {
+  if (same(o, e->desc.mp_option)) {
+    compact = e->vote_rec_compact; bx = e->vote_bias_x; by = e->vote_bias_y;
+    return e->mp_rec.as<uint4>();
+  }
+  if (!e->alt.mp_ok || !same(o, e->alt.mp)) {
+    e->sync_all();
+    VoteTable vt = mp_vote_records(e->leaf_arrays(), o);
+    upload(e->alt.mp_rec, vt.rec, e->main_stream());
+    HIP_CHECK(hipStreamSynchronize(e->main_stream()));
+    e->alt.compact = vt.compact; e->alt.bias_x = vt.bias_x; e->alt.bias_y = vt.bias_y;
+    e->alt.mp = o;
+    e->alt.mp_ok = true;
+  }
+  compact = e->alt.compact; bx = e->alt.bias_x; by = e->alt.bias_y;
+  return e->alt.mp_rec.as<uint4>();
+}
+
 bool region_ok(int W, int H, const ffd_rect* r) {
   return r && r->x >= 0 && r->y >= 0 && r->width > 0 && r->height > 0 && (int64_t)r->x + r->width <= W &&
          (int64_t)r->y + r->height <= H && r->width <= PITCH - 3 && r->height <= MAX_FACE_H;
@@ -1037,24 +1102,30 @@ bool region_ok(int W, int H, const ffd_rect* r) {
 extern "C" {
 
 ffd_status ffd_estimate_headpose(ffd_engine* e, const uint32_t* channels, int32_t W, int32_t H,
-                                 const ffd_rect* region, float* headpose, float* variance) {
+                                 const ffd_rect* region, const ffd_headpose_option* options, float* headpose,
+                                 float* variance) {
   return guarded(e, [&]() -> ffd_status {
     if (!channels || W < 1 || H < 1) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     const ffd_rect full{0, 0, W, H};
     if (!region) region = &full;
     if (!region_ok(W, H, region)) return fail(e, FFD_ERR_INVALID_ARGUMENT, "face_bbox outside the image sample");
+    const ffd_headpose_option o = options ? *options : e->desc.hp_option;
+    if (o.step_size <= 0) return fail(e, FFD_ERR_INVALID_ARGUMENT, "invalid HeadPoseEstimatorOption");
+    const float* hp_m = hp_table(e, o);
+    const TravShape g = ffd_engine::fit_shape(e->trav_g_hp, true, o.step_size, o.step_size);
     e->sync_all();
     Workspace& w = *e->ws[0];
-    const FaceDesc f = stage_sample(e, w, channels, W, H, *region);
+    const FaceDesc f = stage_sample(e, w, channels, W, H, *region, o.step_size, e->desc.mp_option.step_size,
+                                    e->mp_step_y());
     const FaceDesc* dfd = w.faces.as<FaceDesc>();
     std::vector<FaceDesc> fv{f};
     e->out.ensure(sizeof(FaceOut));
-    launch_traverse(true, dfd, 1, blocks_per_face(fv, true, e->trav_g_hp), e->trav_g_hp, e->hp_pairs.as<uint4>(),
-                    e->hp_tops.as<uint4>(), e->hp_topi.as<uint32_t>(), e->trav_top_max, e->hp_far.as<uint32_t>(),
-                    nullptr, e->hp_trees, e->desc.hp_option.step_size, e->desc.hp_option.step_size, f.plane,
-                    w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), e->trav_wg, TRAV_LDS_CAP, w.stream);
-    launch_hp_pose(dfd, 1, w.hpleaf.as<int32_t>(), e->hp_m.as<float>(), e->hp_trees, e->n_forests,
-                   e->ntrees_per_forest, w.state.as<HpState>(), e->out.as<FaceOut>(), w.stream);
+    launch_traverse(true, dfd, 1, blocks_per_face(fv, true, g), g, e->hp_pairs.as<uint4>(), e->hp_tops.as<uint4>(),
+                    e->hp_topi.as<uint32_t>(), e->trav_top_max, e->hp_far.as<uint32_t>(), nullptr, e->hp_trees,
+                    o.step_size, o.step_size, f.plane, w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), e->trav_wg,
+                    TRAV_LDS_CAP, w.stream);
+    launch_hp_pose(dfd, 1, w.hpleaf.as<int32_t>(), hp_m, e->hp_trees, e->n_forests, e->ntrees_per_forest,
+                   w.state.as<HpState>(), e->out.as<FaceOut>(), w.stream);
     HIP_CHECK(hipGetLastError());
     HpState hs;
     HIP_CHECK(hipMemcpyAsync(&hs, w.state.p, sizeof(hs), hipMemcpyDeviceToHost, w.stream));
@@ -1067,7 +1138,7 @@ ffd_status ffd_estimate_headpose(ffd_engine* e, const uint32_t* channels, int32_
 
 ffd_status ffd_estimate_facial_features(ffd_engine* e, const uint32_t* channels, int32_t W, int32_t H,
                                         const ffd_rect* region, const int32_t* tree_ids, int32_t n_trees,
-                                        int32_t* points) {
+                                        const ffd_multipart_option* options, int32_t* points) {
   return guarded(e, [&]() -> ffd_status {
     if (!channels || !points || W < 1 || H < 1 || n_trees < 1 || n_trees > MAX_TREES || !tree_ids)
       return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
@@ -1077,9 +1148,16 @@ ffd_status ffd_estimate_facial_features(ffd_engine* e, const uint32_t* channels,
     const int ntot = e->n_forests * e->ntrees_per_forest;
     for (int t = 0; t < n_trees; t++)
       if (tree_ids[t] < 0 || tree_ids[t] >= ntot) return fail(e, FFD_ERR_INVALID_ARGUMENT, "tree id out of range");
+    const ffd_multipart_option o = options ? *options : e->desc.mp_option;
+    if (o.step_size <= 0 || o.step_size_y < 0) return fail(e, FFD_ERR_INVALID_ARGUMENT, "invalid MultiPartEstimatorOption");
+    const int step_y = o.step_size_y > 0 ? o.step_size_y : o.step_size;
+    bool compact = false;
+    int bias_x = 0, bias_y = 0;
+    const uint4* rec = mp_table(e, o, compact, bias_x, bias_y);
+    const TravShape g = ffd_engine::fit_shape(e->trav_g_mp, false, o.step_size, step_y);
     e->sync_all();
     Workspace& w = *e->ws[0];
-    const FaceDesc f = stage_sample(e, w, channels, W, H, *region);
+    const FaceDesc f = stage_sample(e, w, channels, W, H, *region, e->desc.hp_option.step_size, o.step_size, step_y);
     const FaceDesc* dfd = w.faces.as<FaceDesc>();
     std::vector<FaceDesc> fv{f};
     HpState hs;
@@ -1088,24 +1166,66 @@ ffd_status ffd_estimate_facial_features(ffd_engine* e, const uint32_t* channels,
     for (int t = 0; t < n_trees; t++) hs.trees[t] = tree_ids[t];
     HIP_CHECK(hipMemcpyAsync(w.state.p, &hs, sizeof(hs), hipMemcpyHostToDevice, w.stream));
     e->out.ensure(sizeof(FaceOut));
-    const int n_parts = std::min(e->desc.mp_option.num_parts, NPARTS);
-    launch_traverse(false, dfd, 1, blocks_per_face(fv, false, e->trav_g_mp), e->trav_g_mp, e->mp_pairs.as<uint4>(),
-                    e->mp_tops.as<uint4>(), e->mp_topi.as<uint32_t>(), e->trav_top_max, e->mp_far.as<uint32_t>(),
-                    w.state.as<HpState>(), 0, e->desc.mp_option.step_size, e->mp_step_y(), f.plane,
-                    w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), e->trav_wg, TRAV_LDS_CAP, w.stream);
-    launch_votes(dfd, 1, w.mpleaf.as<int32_t>(), e->mp_rec.as<uint4>(), e->vote_rec_compact, e->vote_bias_x,
-                 e->vote_bias_y, w.state.as<HpState>(), MAX_TREES, e->desc.mp_option.step_size, e->mp_step_y(),
-                 e->patch / 2, n_parts, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), w.stream);
+    const int n_parts = std::max(0, std::min(o.num_parts, NPARTS));
+    launch_traverse(false, dfd, 1, blocks_per_face(fv, false, g), g, e->mp_pairs.as<uint4>(), e->mp_tops.as<uint4>(),
+                    e->mp_topi.as<uint32_t>(), e->trav_top_max, e->mp_far.as<uint32_t>(), w.state.as<HpState>(), 0,
+                    o.step_size, step_y, f.plane, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), e->trav_wg,
+                    TRAV_LDS_CAP, w.stream);
+    launch_votes(dfd, 1, w.mpleaf.as<int32_t>(), rec, compact, bias_x, bias_y, w.state.as<HpState>(), MAX_TREES,
+                 o.step_size, step_y, e->patch / 2, n_parts, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), w.stream);
     // FaceForest::estimateFacialFeatures shifts with a default MeanShiftOption (FaceForest.cpp:89-92)
     launch_meanshift(dfd, 1, w.state.as<HpState>(), MAX_TREES, n_parts, 10.f, 7, 0.05f, w.votes.as<Vote>(),
                      w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(), e->out.as<FaceOut>(), w.stream);
     HIP_CHECK(hipGetLastError());
-    FaceOut o;
-    HIP_CHECK(hipMemcpyAsync(&o, e->out.p, sizeof(o), hipMemcpyDeviceToHost, w.stream));
+    FaceOut out;
+    HIP_CHECK(hipMemcpyAsync(&out, e->out.p, sizeof(out), hipMemcpyDeviceToHost, w.stream));
     HIP_CHECK(hipStreamSynchronize(w.stream));
-    for (int i = 0; i < n_parts; i++) {  // scale 1: cvRound of the MeanShift mode, sample coordinates
-      points[2 * i] = o.points[i][0];
-      points[2 * i + 1] = o.points[i][1];
+    for (int i = 0; i < NPARTS; i++) {  // scale 1: cvRound of the MeanShift mode, sample coordinates
+      points[2 * i] = i < n_parts ? out.points[i][0] : 0;
+      points[2 * i + 1] = i < n_parts ? out.points[i][1] : 0;
+    }
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_forest_leaves(ffd_engine* e, int32_t kind, const int32_t* leaf_ids, int32_t n, void* out) {
+  return guarded(e, [&]() -> ffd_status {
+    if ((n > 0 && (!leaf_ids || !out)) || n < 0) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (kind != FFD_FOREST_HEADPOSE && kind != FFD_FOREST_FFD) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad forest kind");
+    const int64_t L = kind == FFD_FOREST_HEADPOSE ? e->hp_leaves : e->mp_leaves;
+    for (int i = 0; i < n; i++)
+      if (leaf_ids[i] < 0 || leaf_ids[i] >= L) return fail(e, FFD_ERR_INVALID_ARGUMENT, "leaf ordinal out of range");
+    if (n == 0) return FFD_OK;
+    const ffd::ModelFile& m = e->leaf_arrays();
+    if (kind == FFD_FOREST_HEADPOSE) {  // HeadPoseLeaf (HeadPoseSample.hpp:144-162)
+      const int32_t* ln = m.get("hp.leaf_n").as<int32_t>();
+      const float* fg = m.get("hp.leaf_fg").as<float>();
+      const int32_t* lb = m.get("hp.leaf_labels").as<int32_t>();
+      ffd_headpose_leaf* o = static_cast<ffd_headpose_leaf*>(out);
+      for (int i = 0; i < n; i++) {
+        const int64_t k = leaf_ids[i];
+        o[i].hp_nsamples = ln[k];
+        o[i].hp_foreground = fg[k];
+        for (int j = 0; j < FFD_NUM_HP_LABELS; j++) o[i].hp_labels[j] = lb[k * FFD_NUM_HP_LABELS + j];
+      }
+    } else {  // MPLeaf (MPSample.hpp:137-159)
+      const int32_t* ln = m.get("mp.leaf_n").as<int32_t>();
+      const float* fg = m.get("mp.leaf_fg").as<float>();
+      const int16_t* off = m.get("mp.leaf_offset").as<int16_t>();
+      const float* var = m.get("mp.leaf_var").as<float>();
+      const float* pf = m.get("mp.leaf_pf").as<float>();
+      ffd_mp_leaf* o = static_cast<ffd_mp_leaf*>(out);
+      for (int i = 0; i < n; i++) {
+        const int64_t k = leaf_ids[i];
+        o[i].mp_samples = ln[k];
+        o[i].mp_foreground = fg[k];
+        for (int j = 0; j < FFD_NUM_LANDMARKS; j++) {
+          o[i].mp_parts_offset[j][0] = off[(k * 10 + j) * 2];
+          o[i].mp_parts_offset[j][1] = off[(k * 10 + j) * 2 + 1];
+          o[i].mp_parts_variance[j] = var[k * 10 + j];
+          o[i].mp_prob_foreground[j] = pf[k * 10 + j];
+        }
+      }
     }
     return FFD_OK;
   });

@@ -137,6 +137,21 @@ struct ffd_engine {
   std::vector<int32_t> hp_roots_h, mp_roots_h;
   bool vote_rec_compact = false;     // 32-B vote records (else 64-B), see load_model
   int vote_bias_x = 0, vote_bias_y = 0;
+  std::string model_path;            // the FFDMODEL file (re-read for option-dependent tables)
+
+  // Option-dependent leaf tables (head-pose values m, FFD vote records) for per-call estimator
+  // options that differ from desc's (the static estimateHeadPose / estimateFacialFeatures take their
+  // options per call, FaceForest.hpp:97-115), built on first use from the model's leaf payloads.
+  struct AltTables {
+    bool hp_ok = false, mp_ok = false;
+    ffd_headpose_option hp{};
+    ffd_multipart_option mp{};
+    DevBuf hp_m, mp_rec;
+    bool compact = false;
+    int bias_x = 0, bias_y = 0;
+  } alt;
+  std::shared_ptr<ffd::ModelFile> leaf_model;  // leaf payload arrays (hp.leaf_*, mp.leaf_*), lazily
+  const ffd::ModelFile& leaf_arrays();
 
   // Haar face detector (ffd_detect.cpp): the model's cascade, when it has one
   bool have_haar = false;
@@ -224,20 +239,20 @@ struct ffd_engine {
   int mp_step_y() const { return desc.mp_option.step_size_y > 0 ? desc.mp_option.step_size_y : desc.mp_option.step_size; }
   // Fit the traversal window into the CU's 160 KB of LDS (and the staging registers), shrinking
   // the patch block if needed, and raise the kernels' dynamic-LDS limit.
+  // The preferred patch-block shape, else the shapes below it (instantiated in ffd_kernels.hip)
+  // whose window fits the LDS at these grid steps.
+  static TravShape fit_shape(TravShape g, bool hp, int step, int step_y) {
+    const TravShape cands[] = {g, {5, 5}, {5, 4}, {4, 4}, {3, 3}};
+    for (const TravShape& c : cands)
+      if (c.gx * c.gy <= g.gx * g.gy && traverse_shape_supported(c, hp) &&
+          traverse_window_fits(c, hp, step, step_y, TRAV_LDS_CAP))
+        return c;
+    throw std::runtime_error("traversal window does not fit in LDS (step size too large)");
+  }
   void check_traverse_lds() {
     const int cap = TRAV_LDS_CAP;
-    // the preferred shape, else the shapes below it (instantiated in ffd_kernels.hip) that fit
-    auto fit = [&](TravShape& g, bool hp, int step, int step_y) {
-      const TravShape cands[] = {g, {5, 5}, {5, 4}, {4, 4}, {3, 3}};
-      for (const TravShape& c : cands)
-        if (c.gx * c.gy <= g.gx * g.gy && traverse_shape_supported(c, hp) && traverse_window_fits(c, hp, step, step_y, cap)) {
-          g = c;
-          return;
-        }
-      throw std::runtime_error("traversal window does not fit in LDS (step size too large)");
-    };
-    fit(trav_g_hp, true, desc.hp_option.step_size, desc.hp_option.step_size);
-    fit(trav_g_mp, false, desc.mp_option.step_size, mp_step_y());
+    trav_g_hp = fit_shape(trav_g_hp, true, desc.hp_option.step_size, desc.hp_option.step_size);
+    trav_g_mp = fit_shape(trav_g_mp, false, desc.mp_option.step_size, mp_step_y());
     auto pairs = [&](std::vector<uint4>& h, std::vector<int32_t>& roots, DevBuf& d, DevBuf& droots, DevBuf& dfar,
                      DevBuf& dtops, DevBuf& dtopi) {
       std::vector<uint4> pr, tops;
@@ -268,6 +283,14 @@ struct ffd_engine {
 };
 
 namespace ffd_host {
+// option-dependent leaf tables (ffd_engine.cpp)
+std::vector<float> hp_leaf_values(const ffd::ModelFile& m, const ffd_headpose_option& o);
+struct VoteTable {
+  std::vector<uint32_t> rec;
+  bool compact = false;
+  int bias_x = 0, bias_y = 0;
+};
+VoteTable mp_vote_records(const ffd::ModelFile& m, const ffd_multipart_option& o);
 // status + message helpers shared by the C entry points
 ffd_status fail(ffd_engine* e, ffd_status s, const std::string& msg);
 // analyzeFace over host images: upload, descriptors, pipeline; results left in d_out (device)

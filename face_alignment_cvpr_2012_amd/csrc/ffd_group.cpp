@@ -13,6 +13,7 @@
 
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -81,21 +82,34 @@ template <class F> ffd_status group_guarded(ffd_group* g, F&& fn) {
   }
 }
 
-// per-rank communicators of engines that joined one (ffd_engine_join), released with the engine
+// per-rank communicators of engines that joined one (ffd_engine_join), released with the engine.
+// Several engines of one process may join, gather and be destroyed on different threads: every map
+// access holds comm_mu, which is never held across ncclCommInitRank (that call blocks until all the
+// communicator's ranks have joined, possibly from other threads of this process).
+std::mutex comm_mu;
 std::map<const ffd_engine*, ncclComm_t>& rank_comms() {
   static std::map<const ffd_engine*, ncclComm_t> m;
   return m;
+}
+ncclComm_t find_comm(const ffd_engine* e) {
+  std::lock_guard<std::mutex> lk(comm_mu);
+  auto it = rank_comms().find(e);
+  return it == rank_comms().end() ? nullptr : it->second;
 }
 
 }  // namespace
 
 void ffd_host::release_comm(const ffd_engine* e) {
-  auto& m = rank_comms();
-  auto it = m.find(e);
-  if (it != m.end()) {
-    (void)ncclCommDestroy(it->second);
+  ncclComm_t c = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(comm_mu);
+    auto& m = rank_comms();
+    auto it = m.find(e);
+    if (it == m.end()) return;
+    c = it->second;
     m.erase(it);
   }
+  (void)ncclCommDestroy(c);
 }
 
 extern "C" {
@@ -232,6 +246,7 @@ ffd_status ffd_engine_join(ffd_engine* e, const uint8_t* id, int32_t n_ranks, in
     std::memcpy(&u, id, sizeof(u));
     ncclComm_t c = nullptr;
     NCCL_CHECK(ncclCommInitRank(&c, n_ranks, u, rank));
+    std::lock_guard<std::mutex> lk(comm_mu);
     rank_comms()[e] = c;
     return FFD_OK;
   } catch (const std::exception& x) {
@@ -242,14 +257,30 @@ ffd_status ffd_engine_join(ffd_engine* e, const uint8_t* id, int32_t n_ranks, in
 ffd_status ffd_gather_faces(ffd_engine* e, const void* d_local, int32_t n_per_rank, void* d_root, int32_t root) {
   if (!e || (n_per_rank > 0 && !d_local) || n_per_rank < 0) return FFD_ERR_INVALID_ARGUMENT;
   try {
-    auto it = rank_comms().find(e);
-    if (it == rank_comms().end()) return fail(e, FFD_ERR_NOT_INITIALIZED, "engine has not joined a communicator");
+    const ncclComm_t c = find_comm(e);
+    if (!c) return fail(e, FFD_ERR_NOT_INITIALIZED, "engine has not joined a communicator");
     HIP_CHECK(hipSetDevice(e->device));
     int rank = 0;
-    NCCL_CHECK(ncclCommUserRank(it->second, &rank));
+    NCCL_CHECK(ncclCommUserRank(c, &rank));
     if (rank == root && !d_root) return fail(e, FFD_ERR_INVALID_ARGUMENT, "root needs a receive buffer");
     NCCL_CHECK(ncclGather(d_local, rank == root ? d_root : nullptr, (size_t)n_per_rank * REC, ncclUint8, root,
-                          it->second, e->main_stream()));
+                          c, e->main_stream()));
+    return FFD_OK;
+  } catch (const std::exception& x) {
+    return fail(e, FFD_ERR_DEVICE, x.what());
+  }
+}
+
+ffd_status ffd_engine_comm_info(ffd_engine* e, int32_t* n_ranks, int32_t* rank) {
+  if (!e || !n_ranks || !rank) return FFD_ERR_INVALID_ARGUMENT;
+  try {
+    const ncclComm_t c = find_comm(e);
+    if (!c) return fail(e, FFD_ERR_NOT_INITIALIZED, "engine has not joined a communicator");
+    int n = 0, r = 0;
+    NCCL_CHECK(ncclCommCount(c, &n));
+    NCCL_CHECK(ncclCommUserRank(c, &r));
+    *n_ranks = n;
+    *rank = r;
     return FFD_OK;
   } catch (const std::exception& x) {
     return fail(e, FFD_ERR_DEVICE, x.what());

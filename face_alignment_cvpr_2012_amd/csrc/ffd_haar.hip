@@ -268,22 +268,24 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
           // two-rectangle features carry w2 = 0 and an empty rect 2: + (+0) leaves ret unchanged
           // (up to the sign of a zero, which no comparison below distinguishes)
           ret += c.w2 * (float)rs(c.r2);
-          return (float)((double)ret * f);
+          // HaarEvaluator::operator() (cascadedetect.hpp, 2.4.9) returns double: calc() * varianceNormFactor,
+          // compared unrounded with the float threshold in predictOrderedStump
+          return (double)ret * f;
         };
         int i = st.first;
         const int e = st.first + st.ntrees;
         for (; i + 4 <= e; i += 4) {
           const HaarWeak c0 = weak[i], c1 = weak[i + 1], c2 = weak[i + 2], c3 = weak[i + 3];
-          const float v0 = value_of(c0), v1 = value_of(c1), v2 = value_of(c2), v3 = value_of(c3);
-          acc += (double)(v0 < c0.thr ? c0.leaf0 : c0.leaf1);
-          acc += (double)(v1 < c1.thr ? c1.leaf0 : c1.leaf1);
-          acc += (double)(v2 < c2.thr ? c2.leaf0 : c2.leaf1);
-          acc += (double)(v3 < c3.thr ? c3.leaf0 : c3.leaf1);
+          const double v0 = value_of(c0), v1 = value_of(c1), v2 = value_of(c2), v3 = value_of(c3);
+          acc += (double)(v0 < (double)c0.thr ? c0.leaf0 : c0.leaf1);
+          acc += (double)(v1 < (double)c1.thr ? c1.leaf0 : c1.leaf1);
+          acc += (double)(v2 < (double)c2.thr ? c2.leaf0 : c2.leaf1);
+          acc += (double)(v3 < (double)c3.thr ? c3.leaf0 : c3.leaf1);
         }
         for (; i < e; i++) {
           const HaarWeak c = weak[i];
-          const float v = value_of(c);
-          acc += (double)(v < c.thr ? c.leaf0 : c.leaf1);
+          const double v = value_of(c);
+          acc += (double)(v < (double)c.thr ? c.leaf0 : c.leaf1);
         }
         if (acc < (double)st.thr) break;
       }

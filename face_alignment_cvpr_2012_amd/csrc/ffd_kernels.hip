@@ -707,7 +707,7 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 // evaluated (one 16-byte load per visit; the CU's vector-memory return path is the traversal's
 // bottleneck, profiles/r2a), and the test picks the child.
 #ifndef FFD_TRAV_PROBE
-#define FFD_TRAV_PROBE 0  // timing probes (tools/probe.sh): 1 = stage only, 2 = walk only
+#define FFD_TRAV_PROBE 0  // timing probes (tools/probe.sh): 1 = stage only, 2 = walk only, 3 = one tree per block
 #endif
 // Walker threads per workgroup by patch-block edge G: a block's G*G*T walks run in one round (T = 20
 // FFD trees: 4x4 -> 320, 5x5 -> 500 of 512), the other threads stage the next window.  A block costs
@@ -927,7 +927,11 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         for (int u = 0; u < TU; u++) {
           const int e = tid - NW + u * NS;
           if (e < B.T * topn) {
+#if FFD_TRAV_PROBE == 3 || defined(FFD_TRAV_SAMETREE)  // locality probe: every tree slot walks the block's first tree
+            const int j = e >> lg, tree = HP ? 0 : A.hp_state[B.f].trees[0];
+#else
             const int j = e >> lg, tree = HP ? j : A.hp_state[B.f].trees[j];
+#endif
             const int g = tree * TOP_CAP + (e & (topn - 1));
             top_nd[u] = reinterpret_cast<const rec_t*>(A.tops)[g];
             top_p[u] = A.top_idx[g];

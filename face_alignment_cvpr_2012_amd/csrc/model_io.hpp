@@ -97,7 +97,8 @@ class ModelFile {
     if (std::fclose(f) != 0) throw std::runtime_error("write failed: " + path);
   }
 
-  void load(const std::string& path) {
+  // only: load just the arrays whose name contains this substring (empty: all of them)
+  void load(const std::string& path, const std::string& only = std::string()) {
     FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) throw std::runtime_error("cannot open model file " + path);
     char magic[8];
@@ -117,6 +118,7 @@ class ModelFile {
     }
     arrays.clear();
     for (auto& e : ents) {
+      if (!only.empty() && std::string(e.name, strnlen(e.name, sizeof(e.name))).find(only) == std::string::npos) continue;
       ModelArray a;
       a.dtype = std::string(e.dtype, strnlen(e.dtype, sizeof(e.dtype)));
       for (uint32_t i = 0; i < e.ndim && i < 4; i++) a.shape.push_back(e.shape[i]);

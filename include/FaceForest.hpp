@@ -12,7 +12,8 @@
 //   FaceForest::estimateHeadPose / estimateFacialFeatures (static, FaceForest.hpp:97-115,
 //                                                   FaceForest.cpp:60-95) over an ImageSample
 //   ImageSample(img, features, useIntegral)         (ImageSample.cpp:11-20, channels on the GPU)
-//   Forest<HeadPoseSample|MPSample>::evaluateMT     (Forest.hpp:80-90; leaves as model ordinals)
+//   Forest<HeadPoseSample|MPSample>::evaluateMT     (Forest.hpp:80-90; S::Leaf** with the reference's
+//                                                   HeadPoseLeaf / MPLeaf members, or model leaf ordinals)
 // With OpenCV available, Mat / Rect / Point are cv::Mat / cv::Rect / cv::Point; otherwise the
 // minimal PODs below.  FaceForestOptions carries the converted model path instead of the
 // reference's per-forest tree directories (convert once with ffd_convert).
@@ -26,6 +27,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <map>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -150,27 +153,68 @@ class ImageSample {
   std::vector<uint32_t> ch_;
 };
 
+// Leaf payloads (HeadPoseSample.hpp:144-162, MPSample.hpp:137-159), same member names, so the
+// reference's callers (face_utils.cpp:223-228, 289-295) read them through Leaf* unchanged.
+struct HeadPoseLeaf {
+  int hp_nsamples = 0;          // number of patches reached the leaf
+  float hp_foreground = 0.f;    // positive patches percentage
+  std::vector<int> hp_labels;   // number of patches for each class
+};
+struct MPLeaf {
+  int mp_samples = 0;                      // number of patches reached the leaf
+  std::vector<Point> mp_parts_offset;      // vector of facial points
+  std::vector<float> mp_parts_variance;    // variance of the votes
+  std::vector<float> mp_prob_foreground;   // probability of foreground per each point
+  float mp_foreground = 0.f;               // probability of face
+};
+
 // HeadPoseSample / MPSample test constructors (HeadPoseSample.hpp:49-54, MPSample.hpp:47-52): a
 // 31 x 31 patch of an ImageSample.
 struct HeadPoseSample {
+  typedef HeadPoseLeaf Leaf;
   const ImageSample* image;
   Rect roi;
   HeadPoseSample(const ImageSample* i, Rect r) : image(i), roi(r) {}
+  Rect getPatch() const { return roi; }
 };
 struct MPSample {
+  typedef MPLeaf Leaf;
   const ImageSample* image;
   Rect roi;
   MPSample(const ImageSample* i, Rect r) : image(i), roi(r) {}
+  Rect getPatch() const { return roi; }
 };
 template <class S> struct ForestKind;
-template <> struct ForestKind<HeadPoseSample> { static constexpr int value = FFD_FOREST_HEADPOSE; };
-template <> struct ForestKind<MPSample> { static constexpr int value = FFD_FOREST_FFD; };
+template <> struct ForestKind<HeadPoseSample> {
+  static constexpr int value = FFD_FOREST_HEADPOSE;
+  typedef ffd_headpose_leaf Raw;
+  static void fill(const Raw& r, HeadPoseLeaf& l) {
+    l.hp_nsamples = r.hp_nsamples;
+    l.hp_foreground = r.hp_foreground;
+    l.hp_labels.assign(r.hp_labels, r.hp_labels + FFD_NUM_HP_LABELS_MAX);
+  }
+};
+template <> struct ForestKind<MPSample> {
+  static constexpr int value = FFD_FOREST_FFD;
+  typedef ffd_mp_leaf Raw;
+  static void fill(const Raw& r, MPLeaf& l) {
+    l.mp_samples = r.mp_samples;
+    l.mp_foreground = r.mp_foreground;
+    l.mp_parts_offset.clear();
+    for (int i = 0; i < FFD_NUM_LANDMARKS; i++) l.mp_parts_offset.emplace_back(r.mp_parts_offset[i][0], r.mp_parts_offset[i][1]);
+    l.mp_parts_variance.assign(r.mp_parts_variance, r.mp_parts_variance + FFD_NUM_LANDMARKS);
+    l.mp_prob_foreground.assign(r.mp_prob_foreground, r.mp_prob_foreground + FFD_NUM_LANDMARKS);
+  }
+};
 
 // Forest<S> (include/Forest.hpp): a list of the engine's trees; evaluateMT walks every tree for
-// one patch on the GPU (Forest.hpp:80-90).  Leaves are returned as model leaf ordinals (the
-// converted model's order) instead of Leaf* (the payloads stay on the device).
+// one patch on the GPU (Forest.hpp:80-90).  Two forms: leaf ordinals (the converted model's order),
+// or the reference's `S::Leaf**` (Forest.hpp:80: leafs[t] = the leaf tree t reached), whose payloads
+// (ffd_forest_leaves) the Forest owns and keeps for its lifetime, so the pointers stay valid as the
+// reference's tree-owned leaves do.
 template <class S> class Forest {
  public:
+  typedef typename S::Leaf Leaf;
   Forest(ffd_engine* e, std::vector<int32_t> trees) : engine_(e), trees_(std::move(trees)) {}
   int numberOfTrees() const { return (int)trees_.size(); }
   const std::vector<int32_t>& treeIds() const { return trees_; }
@@ -182,10 +226,28 @@ template <class S> class Forest {
                                                  im.height(), xy, 1, trees_.data(), (int32_t)trees_.size(), leafs);
     if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(engine_));
   }
+  // Forest<S>::evaluateMT(const S* sample, typename S::Leaf** leafs) const (Forest.hpp:80-90)
+  void evaluateMT(const S* sample, Leaf** leafs) const {
+    std::vector<int32_t> ids(trees_.size());
+    evaluateMT(sample, ids.data());
+    for (size_t t = 0; t < ids.size(); t++) leafs[t] = &leaf(ids[t]);
+  }
+  // the payload of a leaf ordinal (cached; the reference: TreeNode::getLeaf, TreeNode.hpp:61-66)
+  Leaf& leaf(int32_t ordinal) const {
+    auto it = leaves_.find(ordinal);
+    if (it != leaves_.end()) return *it->second;
+    typename ForestKind<S>::Raw raw;
+    const ffd_status st = ffd_forest_leaves(engine_, ForestKind<S>::value, &ordinal, 1, &raw);
+    if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(engine_));
+    std::unique_ptr<Leaf> l(new Leaf());
+    ForestKind<S>::fill(raw, *l);
+    return *(leaves_[ordinal] = std::move(l));
+  }
 
  private:
   ffd_engine* engine_;
   std::vector<int32_t> trees_;
+  mutable std::map<int32_t, std::unique_ptr<Leaf>> leaves_;
 };
 
 class FaceForest {
@@ -309,25 +371,28 @@ class FaceForest {
     return Forest<MPSample>(engine_, t);
   }
 
-  // FaceForest::estimateHeadPose (static, FaceForest.cpp:60-72).  The estimator options are the
-  // engine's (fixed at construction); `options` must equal them.
+  // FaceForest::estimateHeadPose (static, FaceForest.cpp:60-72) with the call's options (step_size,
+  // num_head_pose_labels, min_foreground_probability), as getHeadPoseVotesMT uses them.
   static void estimateHeadPose(const ImageSample& sample, const Rect& face_bbox, const Forest<HeadPoseSample>& forest,
                                HeadPoseEstimatorOption options, float* headpose, float* variance) {
-    (void)options;
     const ffd_rect r{face_bbox.x, face_bbox.y, face_bbox.width, face_bbox.height};
-    const ffd_status st =
-        ffd_estimate_headpose(forest.engine(), sample.channels(), sample.width(), sample.height(), &r, headpose, variance);
+    const ffd_headpose_option o{options.num_head_pose_labels, options.step_size, options.min_foreground_probability};
+    const ffd_status st = ffd_estimate_headpose(forest.engine(), sample.channels(), sample.width(), sample.height(), &r,
+                                                &o, headpose, variance);
     if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(forest.engine()));
   }
 
-  // FaceForest::estimateFacialFeatures (static, FaceForest.cpp:74-95): landmarks in sample
-  // coordinates (cvRound of the MeanShift modes).
+  // FaceForest::estimateFacialFeatures (static, FaceForest.cpp:74-95) with the call's
+  // MultiPartEstimatorOption (every field, getFacialFeaturesVotesMT); a default MeanShiftOption as in
+  // the reference.  Landmarks in sample coordinates (cvRound of the MeanShift modes), num_parts of them.
   static void estimateFacialFeatures(const ImageSample& sample, const Rect face_bbox, const Forest<MPSample>& forest,
                                      MultiPartEstimatorOption options, std::vector<Point>& ffd_cordinates) {
     const ffd_rect r{face_bbox.x, face_bbox.y, face_bbox.width, face_bbox.height};
+    const ffd_multipart_option o{options.num_parts, options.step_size,  options.min_samples, options.min_forground,
+                                 options.min_pf,    options.max_variance, 0};
     int32_t pts[FFD_NUM_LANDMARKS * 2];
     const ffd_status st = ffd_estimate_facial_features(forest.engine(), sample.channels(), sample.width(), sample.height(),
-                                                       &r, forest.treeIds().data(), forest.numberOfTrees(), pts);
+                                                       &r, forest.treeIds().data(), forest.numberOfTrees(), &o, pts);
     if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(forest.engine()));
     ffd_cordinates.clear();
     for (int i = 0; i < options.num_parts && i < FFD_NUM_LANDMARKS; i++) ffd_cordinates.emplace_back(pts[2 * i], pts[2 * i + 1]);

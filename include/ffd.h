@@ -16,7 +16,7 @@
  *                          (Tree<S>::evaluateMT, include/Tree.hpp:173-191)
  *   ffd_get_trace          per-stage intermediates of the last batch (test hook; the reference has
  *                          plotVotes/show for the same purpose, src/face_utils.cpp:348-376)
- *   ffd_engine_destroy     FaceForest::~FaceForest                        include/FaceForest.hpp:351-353
+ *   ffd_engine_destroy     FaceForest::~FaceForest                        include/FaceForest.hpp:93-95
  *   ffd_last_error         the reference prints ERROR(...) and leaves is_inizialized=false
  *                          (src/FaceForest.cpp:23-56); here a status code + message
  *
@@ -66,7 +66,7 @@ typedef struct {                                                       /* cv::Ma
 #define FFD_MAX_TREES 32
 
 typedef struct {                                                       /* struct Face */
-  float headpose;            /* Face::headpose                       FaceForest.hpp:330 */
+  float headpose;            /* Face::headpose                       FaceForest.hpp:72 */
   float pose_variance;       /* variance from getHeadPoseVotesMT    face_utils.cpp:235-238 */
   ffd_rect bbox;             /* Face::bbox = input box              FaceForest.cpp:192 */
   int32_t points[FFD_NUM_LANDMARKS][2]; /* Face::ffd_cordinates (bbox-relative) */
@@ -158,20 +158,44 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* engine, int32_t forest_kind, const
                                   int32_t n_patches, const int32_t* tree_ids, int32_t n_trees,
                                   int32_t* leaf_ids);
 
-/* FaceForest::estimateHeadPose (src/FaceForest.cpp:60-72 -> getHeadPoseVotesMT,
- * src/face_utils.cpp:183-242) on an image sample given as 38 integral planes (layout of
- * ffd_extract_channels), patches over `region` (the reference's face_bbox; NULL = the whole
- * sample).  headpose / variance as Face::headpose and getHeadPoseVotesMT's variance. */
+/* FaceForest::estimateHeadPose (static, include/FaceForest.hpp:97-105, src/FaceForest.cpp:60-72 ->
+ * getHeadPoseVotesMT, src/face_utils.cpp:183-242) on an image sample given as 38 integral planes
+ * (layout of ffd_extract_channels), patches over `region` (the reference's face_bbox; NULL = the
+ * whole sample), with the call's HeadPoseEstimatorOption (NULL = the engine's desc->hp_option):
+ * step_size, num_head_pose_labels and min_foreground_probability all apply.  headpose / variance as
+ * Face::headpose and getHeadPoseVotesMT's variance. */
 ffd_status ffd_estimate_headpose(ffd_engine* engine, const uint32_t* channels, int32_t face_w, int32_t face_h,
-                                 const ffd_rect* region, float* headpose, float* variance);
+                                 const ffd_rect* region, const ffd_headpose_option* options, float* headpose,
+                                 float* variance);
 
-/* FaceForest::estimateFacialFeatures (src/FaceForest.cpp:74-95): the FFD forest made of the given
- * global tree ids (forest*20 + tree, at most FFD_MAX_TREES), votes over the patches of `region`
- * (getFacialFeaturesVotesMT, src/face_utils.cpp:244-302) and MeanShift::shift with a default
- * MeanShiftOption; points[2*i], points[2*i+1] = landmark i in sample coordinates (cvRound). */
+/* FaceForest::estimateFacialFeatures (static, include/FaceForest.hpp:107-115, src/FaceForest.cpp:74-95):
+ * the FFD forest made of the given global tree ids (forest*20 + tree, at most FFD_MAX_TREES), votes over
+ * the patches of `region` (getFacialFeaturesVotesMT, src/face_utils.cpp:244-302) under the call's
+ * MultiPartEstimatorOption (NULL = the engine's desc->mp_option; every field applies), then
+ * MeanShift::shift with a default MeanShiftOption as the reference does; points[2*i], points[2*i+1] =
+ * landmark i in sample coordinates (cvRound), (0, 0) for i >= num_parts. */
 ffd_status ffd_estimate_facial_features(ffd_engine* engine, const uint32_t* channels, int32_t face_w,
                                         int32_t face_h, const ffd_rect* region, const int32_t* tree_ids,
-                                        int32_t n_trees, int32_t* points);
+                                        int32_t n_trees, const ffd_multipart_option* options, int32_t* points);
+
+/* Leaf payloads by model leaf ordinal (the ids ffd_forest_eval_leaves returns): what the reference's
+ * callers read through the Leaf* of Forest<S>::evaluateMT (src/face_utils.cpp:223-228, 289-295).
+ * Host-side copies from the model file (read on first use); out is an array of n ffd_headpose_leaf
+ * (forest_kind FFD_FOREST_HEADPOSE) or ffd_mp_leaf (FFD_FOREST_FFD). */
+#define FFD_NUM_HP_LABELS_MAX 5
+typedef struct {             /* HeadPoseLeaf, include/HeadPoseSample.hpp:144-162 */
+  int32_t hp_nsamples;
+  float hp_foreground;
+  int32_t hp_labels[FFD_NUM_HP_LABELS_MAX];
+} ffd_headpose_leaf;
+typedef struct {             /* MPLeaf, include/MPSample.hpp:137-159 */
+  int32_t mp_samples;
+  float mp_foreground;
+  int32_t mp_parts_offset[FFD_NUM_LANDMARKS][2];
+  float mp_parts_variance[FFD_NUM_LANDMARKS];
+  float mp_prob_foreground[FFD_NUM_LANDMARKS];
+} ffd_mp_leaf;
+ffd_status ffd_forest_leaves(ffd_engine* engine, int32_t forest_kind, const int32_t* leaf_ids, int32_t n, void* out);
 
 /* Intermediates of face `index` of the most recent ffd_analyze_faces[_device] batch.
  * Any pointer may be NULL; sizes as documented per field (from ffd_face_geometry). */
@@ -227,6 +251,9 @@ ffd_status ffd_group_analyze_faces(ffd_group* group, const ffd_image* imgs, int3
 ffd_status ffd_comm_id(uint8_t* id /* FFD_COMM_ID_BYTES */);
 ffd_status ffd_engine_join(ffd_engine* engine, const uint8_t* id, int32_t n_ranks, int32_t rank);
 ffd_status ffd_gather_faces(ffd_engine* engine, const void* d_local, int32_t n_per_rank, void* d_root, int32_t root);
+/* The joined communicator's size and this engine's rank as RCCL reports them (ncclCommCount /
+ * ncclCommUserRank); FFD_ERR_NOT_INITIALIZED when the engine has not joined. */
+ffd_status ffd_engine_comm_info(ffd_engine* engine, int32_t* n_ranks, int32_t* rank);
 
 /* ---- Haar face detector and the frame-level API ---------------------------
  * ffd_detect_faces      FaceForest::detectFace   src/FaceForest.cpp:136-159: the model's Haar cascade
@@ -238,6 +265,9 @@ ffd_status ffd_gather_faces(ffd_engine* engine, const void* d_local, int32_t n_p
  *                       every box (all boxes of all frames as one batch); faces in frame order, then
  *                       detection order; face_img[i] = the frame of face i.
  * Boxes beyond max_boxes / max_faces are counted in *n_boxes / *n_faces but not written.
+ * Limit (not in the reference): the grouping step holds 8,192 raw (ungrouped) detections per frame; a
+ * frame with more makes the call fail with FFD_ERR_UNSUPPORTED, the message naming the frame (natural
+ * 1080p frames give a few hundred).
  * Parity: bit-exact with the CPU restatement (oracle/); with OpenCV itself unpinned (no OpenCV here). */
 typedef struct {
   int32_t min_feature_size;    /* FaceDetectionOption (include/FaceForest.hpp:21-32): 30 */

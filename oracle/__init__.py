@@ -38,6 +38,16 @@ class OracleTrace(ctypes.Structure):
     ]
 
 
+class OracleOptions(ctypes.Structure):
+    """HeadPoseEstimatorOption / MultiPartEstimatorOption (FaceForest.hpp:34-58) + analyzeFace's
+    MeanShiftOption (MeanShift.hpp:16-25); defaults = the reference constructors."""
+    _fields_ = [("hp_num_labels", ctypes.c_int32), ("hp_step", ctypes.c_int32), ("hp_min_fg", ctypes.c_float),
+                ("mp_num_parts", ctypes.c_int32), ("mp_step_x", ctypes.c_int32), ("mp_step_y", ctypes.c_int32),
+                ("mp_min_samples", ctypes.c_int32), ("mp_min_fg", ctypes.c_float), ("mp_min_pf", ctypes.c_float),
+                ("mp_max_var", ctypes.c_float), ("ms_kernel", ctypes.c_int32), ("ms_iter", ctypes.c_int32),
+                ("ms_stop", ctypes.c_float)]
+
+
 _lib = None
 
 
@@ -49,6 +59,8 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         L.oracle_load_model.argtypes = [ctypes.c_char_p]
         L.oracle_set_steps.argtypes = [ctypes.c_int32] * 3
+        L.oracle_set_options.argtypes = [ctypes.POINTER(OracleOptions)]
+        L.oracle_get_options.argtypes = [ctypes.POINTER(OracleOptions)]
         L.oracle_last_error.restype = ctypes.c_char_p
         L.oracle_analyze_face.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 8 + [
             ctypes.POINTER(OracleFace), ctypes.POINTER(OracleTrace)]
@@ -91,6 +103,28 @@ def set_steps(hp_step=4, mp_step_x=3, mp_step_y=3):
     """Patch-grid steps used by analyze_face / geometry (reference defaults 4, 3, 3)."""
     if lib().oracle_set_steps(hp_step, mp_step_x, mp_step_y) != 0:
         raise RuntimeError(lib().oracle_last_error().decode())
+
+
+def get_options():
+    o = OracleOptions()
+    lib().oracle_get_options(ctypes.byref(o))
+    return {k: getattr(o, k) for k, _ in OracleOptions._fields_}
+
+
+def set_options(**kw):
+    """Set estimator options (unnamed ones keep their current values); set_options() with no
+    arguments is NOT a reset: use reset_options()."""
+    cur = get_options()
+    for k in kw:
+        if k not in cur:
+            raise KeyError(k)
+    cur.update(kw)
+    if lib().oracle_set_options(ctypes.byref(OracleOptions(**cur))) != 0:
+        raise RuntimeError(lib().oracle_last_error().decode())
+
+
+def reset_options():
+    lib().oracle_set_options(None)
 
 
 def _p(a):

@@ -556,9 +556,14 @@ inline int to_int_trunc(float v) {  // static_cast<int>(float) on x86-64 (cvttss
 
 struct Geometry { int W, H, patch, nhx, nhy, nmx, nmy; float scale; };
 
-// patch-grid steps: HeadPoseEstimatorOption::step_size 4, MultiPartEstimatorOption::step_size 3
-// (FaceForest.hpp:34-58); the FFD y step may differ only for SURVEY.md's C4 stress grid
-int g_hp_step = 4, g_mp_step_x = 3, g_mp_step_y = 3;
+// The estimator options (HeadPoseEstimatorOption / MultiPartEstimatorOption, FaceForest.hpp:34-58,
+// defaults as their constructors; MeanShiftOption, MeanShift.hpp:16-25).  The FFD y step may differ
+// only for SURVEY.md's C4 stress grid; the MeanShift option of analyzeFace is the engine's extension
+// (the reference always shifts with a default MeanShiftOption, FaceForest.cpp:89-92).
+oracle_options g_opt = {5, 4, 0.5f, 10, 3, 3, 2, 0.5f, 0.25f, 25.f, 10, 7, 0.05f};
+#define g_hp_step g_opt.hp_step
+#define g_mp_step_x g_opt.mp_step_x
+#define g_mp_step_y g_opt.mp_step_y
 
 bool geometry(int bw, int bh, Geometry& g) {
   if (bw <= 0 || bh <= 0) return false;
@@ -593,9 +598,9 @@ void estimate_headpose(const uint32_t* ch, int W, int H, int rx, int ry, int rw,
   float n = 0, sum = 0, sum_sq = 0;
   for (size_t i = 0; i < hp_leafs.size(); ++i) {
     int L = hp_leafs[i];
-    if (g_hp.hp_fg[L] > 0.5f) {  // HeadPoseEstimatorOption::min_foreground_probability
+    if (g_hp.hp_fg[L] > g_opt.hp_min_fg) {  // HeadPoseEstimatorOption::min_foreground_probability
       float m = 0;
-      for (int j = 0; j < FFD_NUM_HP_LABELS; j++) m += g_hp.hp_labels[L * 5 + j] * j;
+      for (int j = 0; j < std::min(g_opt.hp_num_labels, FFD_NUM_HP_LABELS); j++) m += g_hp.hp_labels[L * 5 + j] * j;
       m /= (g_hp.hp_n[L] * g_hp.hp_fg[L]);
       sum += m;
       sum_sq += m * m;
@@ -611,12 +616,15 @@ void estimate_headpose(const uint32_t* ch, int W, int H, int rx, int ry, int rw,
 }
 
 // getFacialFeaturesVotesMT (face_utils.cpp:244-302) over the region with the given trees, then
-// MeanShift::shift per part (MeanShift.hpp:41-135; kernel 10, 7 iterations, 0.05) as
-// FaceForest::estimateFacialFeatures (FaceForest.cpp:74-95): pts = cvRound of the modes, in sample
-// coordinates.
+// MeanShift::shift per part (MeanShift.hpp:41-135; kernel `ms_kernel`, `ms_iter` iterations, stop
+// `ms_stop`: 10 / 7 / 0.05 as FaceForest::estimateFacialFeatures, FaceForest.cpp:74-95): pts = cvRound
+// of the modes, in sample coordinates.  Parts >= num_parts (the reference's vectors are num_parts long)
+// are reported as (0, 0) with no votes.
 void estimate_facial_features(const uint32_t* ch, int W, int H, int rx, int ry, int rw, int rh,
                               const std::vector<int>& trees, int threads, int pts[][2], float* ms_mean,
-                              int* vote_counts, std::vector<int>& mp_leafs) {
+                              int* vote_counts, std::vector<int>& mp_leafs, int ms_kernel = 10, int ms_iter = 7,
+                              float ms_stop = 0.05f) {
+  const int NP = std::max(0, std::min(g_opt.mp_num_parts, FFD_NUM_PARTS));
   const int P = (int)std::round(g_hp.face_size * g_hp.patch_ratio);
   const int MT = (int)trees.size();
   std::vector<std::pair<int, int>> mp_patches;
@@ -632,11 +640,11 @@ void estimate_facial_features(const uint32_t* ch, int W, int H, int rx, int ry, 
   for (size_t k = 0; k < mp_leafs.size(); k++) {
     int L = mp_leafs[k];
     int ox = mp_patches[k / MT].first + P / 2, oy = mp_patches[k / MT].second + P / 2;
-    for (int i = 0; i < FFD_NUM_PARTS; i++) {
-      float min_pf = 0.25f;             // MultiPartEstimatorOption::min_pf
+    for (int i = 0; i < NP; i++) {
+      float min_pf = g_opt.mp_min_pf;   // MultiPartEstimatorOption::min_pf
       if (i == 0 || i == 7) min_pf *= 1.5;
-      if (g_mp.mp_fg[L] > 0.5f && g_mp.mp_pf[L * 10 + i] > min_pf && g_mp.mp_var[L * 10 + i] < 25.f &&
-          g_mp.mp_n[L] > 2)
+      if (g_mp.mp_fg[L] > g_opt.mp_min_fg && g_mp.mp_pf[L * 10 + i] > min_pf && g_mp.mp_var[L * 10 + i] < g_opt.mp_max_var &&
+          g_mp.mp_n[L] > g_opt.mp_min_samples)
         votes[i].push_back({g_mp.mp_off[(L * 10 + i) * 2] + ox, g_mp.mp_off[(L * 10 + i) * 2 + 1] + oy, g_mp.mp_fg[L]});
     }
   }
@@ -647,8 +655,8 @@ void estimate_facial_features(const uint32_t* ch, int W, int H, int rx, int ry, 
     for (const auto& v : V) { float w = v.w; mx += v.x * w; my += v.y * w; sw += w; }
     if (sw > 0) { mx /= sw; my /= sw; }
     bool conv = false;
-    const float lamda = 10.f, stop = 0.05f;
-    for (int it = 0; it < 7 && !conv; it++) {
+    const float lamda = (float)ms_kernel, stop = ms_stop;
+    for (int it = 0; it < ms_iter && !conv; it++) {
       float sx = 0, sy = 0, s = 0;
       for (const auto& v : V) {
         float dx = mx - (float)v.x, dy = my - (float)v.y;
@@ -664,8 +672,8 @@ void estimate_facial_features(const uint32_t* ch, int W, int H, int rx, int ry, 
     }
     ms_mean[2 * i] = mx;
     ms_mean[2 * i + 1] = my;
-    pts[i][0] = cv_round(mx);
-    pts[i][1] = cv_round(my);
+    pts[i][0] = i < NP ? cv_round(mx) : 0;
+    pts[i][1] = i < NP ? cv_round(my) : 0;
   }
 }
 
@@ -690,7 +698,7 @@ namespace {
 //   HaarEvaluator::setImage / setWindow  integral sum (int) + sqsum (double) of the scaled image;
 //                        normrect (1, 1, 18, 18); nf = 324 sqsum - sum^2 (double), sqrt if > 0 else 1,
 //                        varianceNormFactor = 1 / nf
-//   Feature::calc        float: w0 * S0 + w1 * S1 (+ w2 * S2 when w2 != 0); value = (float)(calc * vnf)
+//   Feature::calc        float: w0 * S0 + w1 * S1 (+ w2 * S2 when w2 != 0); value = (double)calc * vnf (double)
 //   predictOrderedStump  sum (double) += leaf[value < thr ? 0 : 1]; stage fails if sum < (float)stage
 //                        threshold - 1e-5f (Data::read THRESHOLD_EPS); returns -stage or 1
 //   groupRectangles      (objdetect/cascadedetect.cpp) partition by SimilarRects(0.2), classes with
@@ -751,8 +759,10 @@ int haar_run_at(const int32_t* sum, const double* sq, int P, int x, int y) {
       };
       float ret = w[0] * (float)S(0) + w[1] * (float)S(1);
       if (w[2] != 0.0f) ret += w[2] * (float)S(2);
-      const float value = (float)((double)ret * vnf);
-      acc += (double)H.leaves[2 * i + (value < H.weak_thr[i] ? 0 : 1)];
+      // HaarEvaluator::operator() returns double (float calc() * double varianceNormFactor), and
+      // predictOrderedStump compares that double with the stump's float threshold
+      const double value = (double)ret * vnf;
+      acc += (double)H.leaves[2 * i + (value < (double)H.weak_thr[i] ? 0 : 1)];
     }
     if (acc < (double)H.stage_thr[s]) return -(int)s;
   }
@@ -899,6 +909,20 @@ const char* oracle_last_error(void) { return g_err.c_str(); }
 int oracle_set_steps(int32_t hp_step, int32_t mp_step_x, int32_t mp_step_y) {
   if (hp_step <= 0 || mp_step_x <= 0 || mp_step_y <= 0) { g_err = "bad step"; return -1; }
   g_hp_step = hp_step; g_mp_step_x = mp_step_x; g_mp_step_y = mp_step_y;
+  return 0;
+}
+
+int oracle_set_options(const oracle_options* o) {
+  static const oracle_options defaults = {5, 4, 0.5f, 10, 3, 3, 2, 0.5f, 0.25f, 25.f, 10, 7, 0.05f};
+  if (!o) { g_opt = defaults; return 0; }
+  if (o->hp_step <= 0 || o->mp_step_x <= 0 || o->mp_step_y <= 0 || o->ms_kernel == 0) { g_err = "bad options"; return -1; }
+  g_opt = *o;
+  return 0;
+}
+
+int oracle_get_options(oracle_options* o) {
+  if (!o) return -1;
+  *o = g_opt;
   return 0;
 }
 
@@ -1051,7 +1075,8 @@ int oracle_analyze_face(const uint8_t* bgr, int32_t iw, int32_t ih, int32_t stri
   int pts[FFD_NUM_PARTS][2];
   float msm[2 * FFD_NUM_PARTS];
   int vc[FFD_NUM_PARTS];
-  estimate_facial_features(ch.data(), W, H, 0, 0, W, H, trees, threads, pts, msm, vc, mp_leafs);
+  estimate_facial_features(ch.data(), W, H, 0, 0, W, H, trees, threads, pts, msm, vc, mp_leafs, g_opt.ms_kernel,
+                           g_opt.ms_iter, g_opt.ms_stop);
   if (tr && tr->mp_leaves) std::memcpy(tr->mp_leaves, mp_leafs.data(), mp_leafs.size() * 4);
   if (tr && tr->vote_counts) std::memcpy(tr->vote_counts, vc, sizeof(vc));
   if (tr && tr->ms_mean) std::memcpy(tr->ms_mean, msm, sizeof(msm));

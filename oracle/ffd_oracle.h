@@ -45,6 +45,27 @@ typedef struct {
   float* ms_mean;
 } oracle_trace;
 
+/* Estimator options (global, not thread-safe): HeadPoseEstimatorOption / MultiPartEstimatorOption
+ * (include/FaceForest.hpp:34-58) and analyzeFace's MeanShiftOption (MeanShift.hpp:16-25; the
+ * reference's is always the default, the engine's ffd_meanshift_option is an extension).
+ * NULL restores the reference defaults. */
+typedef struct {
+  int32_t hp_num_labels;  /* 5 */
+  int32_t hp_step;        /* 4 */
+  float hp_min_fg;        /* 0.5 */
+  int32_t mp_num_parts;   /* 10 */
+  int32_t mp_step_x, mp_step_y;  /* 3, 3 */
+  int32_t mp_min_samples; /* 2 */
+  float mp_min_fg;        /* 0.5 */
+  float mp_min_pf;        /* 0.25 */
+  float mp_max_var;       /* 25 */
+  int32_t ms_kernel;      /* 10 */
+  int32_t ms_iter;        /* 7 */
+  float ms_stop;          /* 0.05 */
+} oracle_options;
+int oracle_set_options(const oracle_options* options);
+int oracle_get_options(oracle_options* options);
+
 int oracle_load_model(const char* path);
 /* Patch-grid steps (defaults 4 / 3 / 3 = the reference's options; global, not thread-safe). */
 int oracle_set_steps(int32_t hp_step, int32_t mp_step_x, int32_t mp_step_y);

@@ -17,6 +17,15 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "reference: needs the read-only reference tree at /root/reference")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first():
+    """PyTorch's HIP runtime first: a test that creates an engine before any torch.cuda call would
+    otherwise leave torch without devices for the tests that hand it torch buffers."""
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
+
+
 @pytest.fixture(scope="session")
 def model_path():
     if not os.path.exists(MODEL):

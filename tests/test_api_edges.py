@@ -87,11 +87,29 @@ def test_group_on_one_device_equals_engine(model_path, engine, fixtures):
         assert np.array_equal(a.ffd_cordinates, b.ffd_cordinates) and a.headpose == b.headpose
 
 
+def test_group_two_devices_uneven_shards(model_path, engine, fixtures):
+    """ffd_group_* over 2 devices (ncclCommInitAll, image remapping per device, padded shards, one
+    ncclGather, ordered D2H): 5 faces = 3 + 2, byte-for-byte equal to one engine.  Needs 2 devices."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two HIP devices")
+    imgs = list(fixtures["images"][:3])
+    boxes = [tuple(int(v) for v in fixtures["boxes"][i]) for i in (0, 1, 2)] + [(40, 40, 150, 150), (0, 0, 120, 130)]
+    box_img = [0, 1, 2, 1, 0]
+    want = engine.analyzeFaces(imgs, boxes, box_img)
+    with ffd.FaceForestGroup([0, 1], ffd.FaceForestOptions(model_path=model_path)) as g:
+        got = g.analyzeFaces(imgs, boxes, box_img)
+    for a, b in zip(got, want):
+        assert np.array_equal(a.ffd_cordinates, b.ffd_cordinates) and a.bbox == b.bbox
+        assert np.float32(a.headpose).tobytes() == np.float32(b.headpose).tobytes()
+
+
 def test_rccl_join_and_gather_single_rank(engine):
     import torch
     cid = ffd.comm_id()
     assert len(cid) == ffd.COMM_ID_BYTES
     engine.join(cid, 1, 0)
+    assert engine.comm_info() == (1, 0)
     n = 7
     local = torch.arange(n * ffd.FACE_RECORD_BYTES, dtype=torch.int64, device="cuda").to(torch.uint8)
     root = torch.zeros_like(local)

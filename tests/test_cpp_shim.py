@@ -65,6 +65,32 @@ def test_shim_estimators_and_forest(model_path, fixtures, engine, oracle_mod, tm
     import face_alignment_cvpr_2012_amd as ffd
     want = ffd.Forest(engine, ffd.FOREST_HEADPOSE).evaluate(ch, [region[:2]], list(range(15)))[0]
     assert np.array_equal(leaves, want)
+    # Forest<MPSample>::evaluateMT(const MPSample*, MPLeaf**): the reference's Leaf members
+    from face_alignment_cvpr_2012_amd import model as fm
+    m = fm.load(model_path)
+    ids = ffd.Forest(engine, ffd.FOREST_FFD).evaluate(ch, [region[:2]], list(range(pose_bin * 20, pose_bin * 20 + 20)))[0]
+    got = np.array(lines[3].split(), np.float64).reshape(20, 4)
+    np.testing.assert_array_equal(got[:, 0], m["mp.leaf_n"][ids])
+    np.testing.assert_array_equal(got[:, 1].astype(np.float32), m["mp.leaf_fg"][ids])
+    np.testing.assert_array_equal(got[:, 2:].astype(np.int32), m["mp.leaf_offset"][ids][:, 0, :])
+
+    # the static estimators honour their options argument (the engine keeps its defaults)
+    extra = ["hp_min_fg=0.6", "hp_step=5", "mp_min_pf=0.3", "mp_max_var=20", "mp_parts=8", "mp_step=4"]
+    r = subprocess.run([exe, model_path, str(path), str(w), str(h)] + [str(v) for v in region] + [str(pose_bin)] + extra,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    oracle_mod.set_options(hp_min_fg=0.6, hp_step=5, mp_min_pf=0.3, mp_max_var=20.0, mp_num_parts=8, mp_step_x=4,
+                           mp_step_y=4)
+    try:
+        hp, var = oracle_mod.estimate_headpose(ch, region)
+        want_pts = oracle_mod.estimate_facial_features(ch, region, range(pose_bin * 20, pose_bin * 20 + 20))
+    finally:
+        oracle_mod.reset_options()
+    got_hp, got_var = (float(v) for v in lines[0].split())
+    assert np.float32(got_hp) == np.float32(hp) and np.float32(got_var) == np.float32(var)
+    pts = np.array(lines[1].split(), np.int32).reshape(8, 2)
+    assert np.array_equal(pts, want_pts[:8])
 
 
 @pytest.mark.gpu

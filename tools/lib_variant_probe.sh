@@ -11,5 +11,5 @@ for lib in face_alignment_cvpr_2012_amd/lib/libffd.so "$@"; do
 import json, sys, os
 d = json.loads(sys.stdin.read())
 st = os.environ.get('STAGES', os.environ.get('STAGE', 'meanshift')).split(',')
-print(d['value'], 'spot', d.get('parity_spot_check'), ' '.join('%s=%s' % (s, d['stage_ms_per_step'].get(s)) for s in st))")" | tee -a gpurun_out/variants.txt
+print(d['value'], 'spot', d.get('landmark_px_error',{}).get('faces_identical'), ' '.join('%s=%s' % (s, d['stage_ms_per_step'].get(s)) for s in st))")" | tee -a gpurun_out/variants.txt
 done

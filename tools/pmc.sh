@@ -9,7 +9,7 @@ OUT=$R/gpurun_out/pmc_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
-BARGS=${BENCH_ARGS:---faces 1024 --steps 1 --warmup 1 --no-cpu-baseline}
+BARGS=${BENCH_ARGS:---faces 1024 --steps 1 --warmup 1 --no-cpu-baseline --no-host-paths}
 i=0
 while read -r grp; do
   [ -z "$grp" ] && continue

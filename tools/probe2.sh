@@ -20,5 +20,5 @@ for cfg in "$@"; do
   rc=$?
   cat gpurun_out/probe2_tmp.log >> gpurun_out/probe2_$TAG.log
   if [ $rc -ne 0 ]; then echo "rc=$rc ($cfg)"; tail -5 gpurun_out/probe2_tmp.log; exit $rc; fi
-  python3 -c "import json,sys; d=json.loads(open('gpurun_out/probe2_tmp.log').read().strip().splitlines()[-1]); s=d['stage_ms_per_step']; print(json.dumps({'cfg': sys.argv[1], 'value': d['value'], 'ok': d['parity_spot_check'], 'hp': s['headpose_traverse'], 'ffd': s['ffd_traverse'], 'ms': d['ms_per_step']}))" "$cfg" | tee -a "$OUT"
+  python3 -c "import json,sys; d=json.loads(open('gpurun_out/probe2_tmp.log').read().strip().splitlines()[-1]); s=d['stage_ms_per_step']; print(json.dumps({'cfg': sys.argv[1], 'value': d['value'], 'ok': d.get('landmark_px_error',{}).get('faces_identical'), 'hp': s['headpose_traverse'], 'ffd': s['ffd_traverse'], 'ms': d['ms_per_step']}))" "$cfg" | tee -a "$OUT"
 done
