@@ -18,13 +18,14 @@ ORACLE    := oracle/build/libffd_oracle.so
 MODEL     := model/ffd_model.bin
 EXAMPLE   := examples/build/analyze_face
 EXAMPLE2  := examples/build/estimate
+EXAMPLE3  := examples/build/bench_host
 
 HIP_OBJS  := $(PKG)/lib/ffd_kernels.o $(PKG)/lib/ffd_engine.o $(PKG)/lib/ffd_group.o $(PKG)/lib/ffd_archive.o \
              $(PKG)/lib/ffd_haar.o $(PKG)/lib/ffd_detect.o
 HDRS      := include/ffd.h include/ffd_numerics.h include/ffd_gabor.h include/ffd_model_format.h $(CSRC)/ffd_device.hpp \
              $(CSRC)/ffd_kernels.hpp $(CSRC)/model_io.hpp $(CSRC)/ffd_engine_impl.hpp $(CSRC)/ffd_haar.hpp
 
-all: $(LIB) $(CONVERT) $(SYNTH) $(ORACLE) $(EXAMPLE) $(EXAMPLE2)
+all: $(LIB) $(CONVERT) $(SYNTH) $(ORACLE) $(EXAMPLE) $(EXAMPLE2) $(EXAMPLE3)
 
 $(PKG)/lib/ffd_kernels.o: $(CSRC)/ffd_kernels.hip $(HDRS)
 	@mkdir -p $(@D)
@@ -83,5 +84,8 @@ $(EXAMPLE): examples/analyze_face.cpp include/FaceForest.hpp include/ffd.h $(LIB
 $(EXAMPLE2): examples/estimate.cpp include/FaceForest.hpp include/ffd.h $(LIB)
 	@mkdir -p $(@D)
 	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(PKG)/lib -lffd -Wl,-rpath,'$$ORIGIN/../../$(PKG)/lib'
-example: $(EXAMPLE) $(EXAMPLE2)
+$(EXAMPLE3): examples/bench_host.cpp include/FaceForest.hpp include/ffd.h $(LIB)
+	@mkdir -p $(@D)
+	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(PKG)/lib -lffd -Wl,-rpath,'$$ORIGIN/../../$(PKG)/lib'
+example: $(EXAMPLE) $(EXAMPLE2) $(EXAMPLE3)
 .PHONY: example

@@ -329,6 +329,32 @@ def host_inclusive(ff, wl, iw, ih, steps, chunks=4):
                                                    "stream overlapping the previous chunk's compute"}
 
 
+def cxx_host_path(wl, reps=5):
+    """The C ABI's host-buffer path timed from C++ (examples/bench_host.cpp through include/FaceForest.hpp):
+    FaceForest::analyzeFaces over the whole batch (pageable host crops in, host records out) and the
+    reference's one-analyzeFace-per-call latency (eval_ffd.cpp:89).  Runs as a child process BEFORE this
+    process touches the GPU (nothing here has initialised HIP yet)."""
+    import tempfile
+    exe = os.path.join(REPO, "examples", "build", "bench_host")
+    if not os.path.exists(exe):
+        return None
+    n, ih, iw = wl.n, wl.images.shape[1], wl.images.shape[2]
+    with tempfile.NamedTemporaryFile(suffix=".bgr", delete=False) as fh:
+        np.ascontiguousarray(wl.images[:n]).tofile(fh)
+        path = fh.name
+    try:
+        r = subprocess.run([exe, wl.model, path, str(n), str(iw), str(ih), str(reps)], capture_output=True, text=True,
+                           timeout=300)
+    finally:
+        os.unlink(path)
+    if r.returncode != 0:
+        return {"error": r.stderr.strip()[-300:]}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    d["note"] = ("examples/bench_host.cpp: FaceForest::analyzeFaces (C++ shim -> ffd_analyze_faces) on pageable "
+                 "host crops, median of %d batch calls; latency = analyzeFace per call, median of 50" % reps)
+    return d
+
+
 def single_face_latency(ff, wl, reps=50):
     """The reference's call pattern (eval_ffd.cpp:89): one analyzeFace per call, host image in,
     host record out, through ffd_analyze_faces (the C ABI the C++ shim calls)."""
@@ -450,6 +476,9 @@ def main():
 
     faces = args.faces or (1024 if args.workload == "c4" else 4096)
     wl = make_workload(args.workload, rank, world, faces, args.frames)
+    cxx_host = None
+    if world == 1 and wl.name == "c2" and not args.no_host_paths:
+        cxx_host = cxx_host_path(wl)  # a child process, before this one initialises the GPU
     n = wl.n
     n_img, ih, iw = wl.n_images, wl.images.shape[1], wl.images.shape[2]
     d_images = torch.from_numpy(np.ascontiguousarray(wl.images)).to(dev)
@@ -595,6 +624,10 @@ def main():
         if host_incl is not None:
             out["host_inclusive"] = host_incl
             out["analyze_face_latency"] = latency
+        if cxx_host is not None:
+            out["cxx_host_path"] = cxx_host
+            if host_incl is not None and "batch_faces_per_s" in cxx_host:
+                cxx_host["vs_host_inclusive"] = round(cxx_host["batch_faces_per_s"] / host_incl["value"], 3)
         if detect_ms is not None:
             out["detect"] = {"frames_per_step": wl.n_images * world, "faces_found": wl.total_faces,
                              "detect_ms_per_step": round(detect_ms, 3),

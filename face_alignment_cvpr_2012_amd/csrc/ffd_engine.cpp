@@ -513,10 +513,12 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   const FaceDesc* dfd = w.faces.as<FaceDesc>();
   stage(0, st, [&] { launch_gray_resize(dfd, n, d_images, w.gray.as<uint8_t>(), st); });
   // channel stage: Gabor scales 4..0 and the gray / Sobel integrals, dealt over the fork streams
-  const int nfork = (int)w.fork.size();
+  // (a large chunk fills the chip with one kernel at a time, so it forks only when FFD_CHANNEL_STREAMS
+  // asks; a small one runs all six channel kernels side by side: single-face latency)
+  const int nfork = n <= small_batch ? (int)w.fork.size() : std::min((int)w.fork.size(), channel_streams - 1);
   if (nfork > 0) {
     HIP_CHECK(hipEventRecord(w.fork_ev[0], st));
-    for (auto f : w.fork) HIP_CHECK(hipStreamWaitEvent(f, w.fork_ev[0], 0));
+    for (int i = 0; i < nfork; i++) HIP_CHECK(hipStreamWaitEvent(w.fork[i], w.fork_ev[0], 0));
   }
   auto cs = [&](int i) { return i % (nfork + 1) == 0 ? st : w.fork[i % (nfork + 1) - 1]; };
   for (int nu = 4; nu >= 0; nu--) {  // largest kernels first
@@ -572,7 +574,8 @@ void ffd_engine::analyze(const uint8_t* d_images, const std::vector<FaceDesc>& a
   for (int first = 0; first < n; first += max_chunk, k++) {
     const int cnt = std::min(max_chunk, n - first);
     Workspace& w = *ws[k % ws.size()];
-    if (w.pending) HIP_CHECK(hipEventSynchronize(w.done));  // its host staging is free again
+    // (h_fds reaches the device by a pageable copy, staged before the call returns, and the device
+    // buffers are reused in stream order: the host need not wait for the workspace's last chunk)
     w.h_fds.assign(all.begin() + first, all.begin() + first + cnt);
     run_chunk(w, d_images, d_out + first);
     w.desc = w.h_fds;
@@ -656,20 +659,25 @@ template <class F> ffd_status guarded(ffd_engine* e, F&& fn) {
 
 // Host images in, results in device memory (d_out, n_faces FaceOut), everything enqueued on the
 // engine's streams; main_stream() is ordered after the batch on return.  Throws HipError.
+// The images are uploaded on the engine's copy stream in host chunks of host_chunk faces, each chunk's
+// new images (contiguous host runs coalesced into one copy) ahead of its compute, so the upload of
+// chunk k + 1 overlaps the kernels of chunk k (SURVEY.md §8(d)'s H2D -> D2H timing rule, through the
+// C ABI the C++ shim calls).
 ffd_status ffd_host::analyze_host(ffd_engine* e, const ffd_image* imgs, int32_t n_img, const ffd_rect* boxes,
                                   const int32_t* box_img, int32_t n_faces, void* d_out) {
   if (n_faces < 0 || (n_faces > 0 && (!imgs || !boxes || !d_out)) || n_img < 0)
     return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
   if (!box_img && n_img != n_faces) return fail(e, FFD_ERR_INVALID_ARGUMENT, "box_img NULL requires n_img == n_faces");
   if (n_faces == 0) return FFD_OK;
-  // pack the images into one device buffer
+  // device offsets: images packed back to back (the kernels read bytes), so host images that are
+  // contiguous in memory stay contiguous and upload as one copy
   std::vector<int64_t> img_off(n_img);
   int64_t total = 0;
   for (int i = 0; i < n_img; i++) {
     if (!imgs[i].bgr || imgs[i].width <= 0 || imgs[i].height <= 0 || imgs[i].stride < 3 * imgs[i].width)
       return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad image " + std::to_string(i));
     img_off[i] = total;
-    total += align_up((int64_t)imgs[i].stride * imgs[i].height, 256);
+    total += (int64_t)imgs[i].stride * imgs[i].height;
   }
   std::vector<FaceDesc> fds(n_faces);
   for (int i = 0; i < n_faces; i++) {
@@ -678,14 +686,37 @@ ffd_status ffd_host::analyze_host(ffd_engine* e, const ffd_image* imgs, int32_t 
     make_desc(e, img_off[k], imgs[k].width, imgs[k].height, imgs[k].stride, boxes[i], fds[i]);
   }
   e->sync_all();  // the staging buffer may still be read by the previous batch
-  e->images.ensure(total);
-  for (int i = 0; i < n_img; i++)
-    HIP_CHECK(hipMemcpyAsync(e->images.as<uint8_t>() + img_off[i], imgs[i].bgr, (size_t)imgs[i].stride * imgs[i].height,
-                             hipMemcpyHostToDevice, e->main_stream()));
-  // the other streams must see the uploaded images
-  HIP_CHECK(hipEventRecord(e->ws[0]->done, e->main_stream()));
-  for (size_t i = 1; i < e->ws.size(); i++) HIP_CHECK(hipStreamWaitEvent(e->ws[i]->stream, e->ws[0]->done, 0));
-  e->analyze(e->images.as<uint8_t>(), fds, static_cast<FaceOut*>(d_out));
+  e->images.ensure(total + 16);
+  uint8_t* dimg = e->images.as<uint8_t>();
+  std::vector<char> sent(n_img, 0);
+  const int hc = std::max(1, std::min(e->host_chunk, e->max_chunk));
+  for (int lo = 0; lo < n_faces; lo += hc) {
+    const int hi = std::min(n_faces, lo + hc);
+    // this chunk's images not uploaded yet, in index order, coalesced into contiguous host runs
+    std::vector<int> need;
+    for (int i = lo; i < hi; i++) {
+      const int k = box_img ? box_img[i] : i;
+      if (!sent[k]) { sent[k] = 1; need.push_back(k); }
+    }
+    std::sort(need.begin(), need.end());
+    for (size_t a = 0; a < need.size();) {
+      size_t b = a + 1;
+      int64_t bytes = (int64_t)imgs[need[a]].stride * imgs[need[a]].height;
+      while (b < need.size() && need[b] == need[b - 1] + 1 &&
+             imgs[need[b]].bgr == imgs[need[b - 1]].bgr + (int64_t)imgs[need[b - 1]].stride * imgs[need[b - 1]].height) {
+        bytes += (int64_t)imgs[need[b]].stride * imgs[need[b]].height;
+        b++;
+      }
+      HIP_CHECK(hipMemcpyAsync(dimg + img_off[need[a]], imgs[need[a]].bgr, (size_t)bytes, hipMemcpyHostToDevice,
+                               e->copy_stream));
+      a = b;
+    }
+    // every compute stream waits for the chunk's images
+    HIP_CHECK(hipEventRecord(e->copy_done, e->copy_stream));
+    for (auto& w : e->ws) HIP_CHECK(hipStreamWaitEvent(w->stream, e->copy_done, 0));
+    std::vector<FaceDesc> part(fds.begin() + lo, fds.begin() + hi);
+    e->analyze(dimg, part, static_cast<FaceOut*>(d_out) + lo);
+  }
   return FFD_OK;
 }
 
@@ -748,7 +779,9 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   if (const char* v = std::getenv("FFD_TRAV_WG")) e->trav_wg = std::max(8, std::atoi(v));
   if (const char* v = std::getenv("FFD_TRAV_TOPMAX")) e->trav_top_max = std::max(1, std::min(TOP_CAP, std::atoi(v)));
   if (const char* v = std::getenv("FFD_GABOR_EXACT")) e->gabor_exact = std::atoi(v) != 0;
-  if (const char* v = std::getenv("FFD_CHANNEL_STREAMS")) e->channel_streams = std::max(1, std::min(4, std::atoi(v)));
+  if (const char* v = std::getenv("FFD_CHANNEL_STREAMS")) e->channel_streams = std::max(1, std::min(6, std::atoi(v)));
+  if (const char* v = std::getenv("FFD_SMALL_BATCH")) e->small_batch = std::max(0, std::atoi(v));
+  if (const char* v = std::getenv("FFD_HOST_CHUNK")) e->host_chunk = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("FFD_CHUNK")) e->max_chunk = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("FFD_STREAMS")) e->n_streams = std::max(1, std::min(8, std::atoi(v)));
   if (d->max_chunk_faces > 0) e->max_chunk = d->max_chunk_faces;
@@ -762,18 +795,20 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
       auto w = std::make_unique<Workspace>();
       HIP_CHECK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
       HIP_CHECK(hipEventCreateWithFlags(&w->done, hipEventDisableTiming));
-      for (int j = 1; j < e->channel_streams; j++) {
+      for (int j = 1; j < std::max(e->channel_streams, 6); j++) {
         hipStream_t f;
         HIP_CHECK(hipStreamCreateWithFlags(&f, hipStreamNonBlocking));
         w->fork.push_back(f);
       }
-      for (int j = 0; j < e->channel_streams; j++) {
+      for (int j = 0; j < std::max(e->channel_streams, 6); j++) {
         hipEvent_t ev;
         HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         w->fork_ev.push_back(ev);
       }
       e->ws.push_back(std::move(w));
     }
+    HIP_CHECK(hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&e->copy_done, hipEventDisableTiming));
     e->model_path = d->model_path;
     e->load_model(d->model_path);
     e->check_traverse_lds();

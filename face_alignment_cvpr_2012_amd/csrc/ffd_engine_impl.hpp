@@ -116,6 +116,10 @@ struct ffd_engine {
   int n_streams = 1;
   int gabor_exact = 0;      // FFD_GABOR_EXACT=1: every face through the exact (sqrtf) Gabor instance (tests)
   int channel_streams = 1;  // streams the channel stage is spread over (FFD_CHANNEL_STREAMS; 2-4 measured no gain)
+  int host_chunk = 1024;    // faces per upload chunk of the host-buffer API (FFD_HOST_CHUNK)
+  hipStream_t copy_stream = nullptr;  // H2D of the host-buffer API's images
+  hipEvent_t copy_done = nullptr;
+  int small_batch = 64;     // chunks of at most this many faces spread the channel stage over 6 streams (FFD_SMALL_BATCH)
   // traversal tuning: patch block edge G (a workgroup walks all trees of a G x G block of patches
   // over an LDS copy of the block's integral window) and the persistent workgroups (one per CU).
   // Overridable with FFD_TRAV_G_{HP,FFD} / FFD_TRAV_WG / FFD_CHUNK / FFD_STREAMS.
@@ -190,6 +194,7 @@ struct ffd_engine {
     pending.push_back(p);
   }
   void sync_all() {
+    if (copy_stream) HIP_CHECK(hipStreamSynchronize(copy_stream));
     for (auto& w : ws) {
       for (auto f : w->fork) HIP_CHECK(hipStreamSynchronize(f));
       HIP_CHECK(hipStreamSynchronize(w->stream));
@@ -212,6 +217,8 @@ struct ffd_engine {
   ~ffd_engine() {
     for (auto& p : pending) { event_pool.push_back(p.a); event_pool.push_back(p.b); }
     for (auto e : event_pool) (void)hipEventDestroy(e);
+    if (copy_done) (void)hipEventDestroy(copy_done);
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
   }
 
   Geometry geometry(int bw, int bh) const {

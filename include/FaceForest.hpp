@@ -358,6 +358,35 @@ class FaceForest {
     }
   }
 
+  // analyzeFace over many images at once (box i on imgs[i]; the reference calls analyzeFace per face,
+  // eval_ffd.cpp:89): one GPU batch through ffd_analyze_faces, whose image upload overlaps the
+  // kernels chunk by chunk.  Replaces `faces` (one Face per box, in order).
+  void analyzeFaces(const std::vector<Mat>& imgs, const std::vector<Rect>& boxes, std::vector<Face>& faces) {
+    if (!engine_) throw std::runtime_error("FaceForest not initialised: " + err_);
+    if (imgs.size() != boxes.size()) throw std::invalid_argument("analyzeFaces: one box per image");
+    std::vector<ffd_image> im(imgs.size());
+    std::vector<ffd_rect> r(boxes.size());
+    for (size_t i = 0; i < imgs.size(); i++) {
+      im[i] = ffd_image{mat_data(imgs[i]), imgs[i].cols, imgs[i].rows, mat_step(imgs[i])};
+      r[i] = {boxes[i].x, boxes[i].y, boxes[i].width, boxes[i].height};
+    }
+    out_.resize(boxes.size());
+    const ffd_status st = ffd_analyze_faces(engine_, im.data(), (int32_t)im.size(), r.data(), nullptr,
+                                            (int32_t)r.size(), out_.data());
+    if (st == FFD_ERR_INVALID_ARGUMENT) throw std::invalid_argument(ffd_last_error(engine_));
+    if (st != FFD_OK) throw std::runtime_error(ffd_last_error(engine_));
+    faces.resize(out_.size());
+    for (size_t i = 0; i < out_.size(); i++) {
+      if (out_[i].status != FFD_OK)
+        throw std::invalid_argument("face " + std::to_string(i) + ": " + ffd_status_string(out_[i].status));
+      Face& f = faces[i];
+      f.headpose = out_[i].headpose;
+      f.bbox = boxes[i];
+      f.ffd_cordinates.resize(FFD_NUM_LANDMARKS);
+      for (int k = 0; k < FFD_NUM_LANDMARKS; k++) f.ffd_cordinates[k] = Point(out_[i].points[k][0], out_[i].points[k][1]);
+    }
+  }
+
   // The engine's forests: the head-pose forest (15 trees) and pose forest i of the FFD jungle
   // (m_mp_jungle[i], 20 trees, global ids i*20 .. i*20+19).
   Forest<HeadPoseSample> headPoseForest() const {
@@ -412,6 +441,7 @@ class FaceForest {
   ffd_engine* engine_ = nullptr;
   std::string err_;
   FaceDetectionOption fd_option_;
+  std::vector<ffd_face> out_;  // analyzeFaces' result records (reused across calls)
 };
 
 }  // namespace ffd
