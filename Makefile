@@ -21,7 +21,7 @@ EXAMPLE2  := examples/build/estimate
 EXAMPLE3  := examples/build/bench_host
 
 HIP_OBJS  := $(PKG)/lib/ffd_kernels.o $(PKG)/lib/ffd_engine.o $(PKG)/lib/ffd_group.o $(PKG)/lib/ffd_archive.o \
-             $(PKG)/lib/ffd_haar.o $(PKG)/lib/ffd_detect.o
+             $(PKG)/lib/ffd_haar.o $(PKG)/lib/ffd_detect.o $(PKG)/lib/ffd_train_k.o $(PKG)/lib/ffd_train.o
 HDRS      := include/ffd.h include/ffd_numerics.h include/ffd_gabor.h include/ffd_model_format.h $(CSRC)/ffd_device.hpp \
              $(CSRC)/ffd_kernels.hpp $(CSRC)/model_io.hpp $(CSRC)/ffd_engine_impl.hpp $(CSRC)/ffd_haar.hpp
 
@@ -48,6 +48,14 @@ $(PKG)/lib/ffd_detect.o: $(CSRC)/ffd_detect.cpp $(HDRS)
 	@mkdir -p $(@D)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(PKG)/lib/ffd_train_k.o: $(CSRC)/ffd_train.hip $(CSRC)/ffd_train.hpp include/ffd_numerics.h include/ffd_gabor.h
+	@mkdir -p $(@D)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(PKG)/lib/ffd_train.o: $(CSRC)/ffd_train.cpp $(CSRC)/ffd_train.hpp $(HDRS)
+	@mkdir -p $(@D)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(PKG)/lib/ffd_group.o: $(CSRC)/ffd_group.cpp $(HDRS)
 	@mkdir -p $(@D)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -65,9 +73,9 @@ $(CONVERT): $(CSRC)/ffd_convert.cpp $(CSRC)/model_io.hpp include/ffd_model_forma
 	@mkdir -p $(@D)
 	$(CXX) $(CXXFLAGS) -o $@ $<
 
-$(ORACLE): oracle/ffd_oracle.cpp oracle/ffd_oracle.h include/ffd_numerics.h include/ffd_gabor.h include/ffd_model_format.h
+$(ORACLE): oracle/ffd_oracle.cpp oracle/ffd_train_oracle.cpp oracle/ffd_oracle.h include/ffd_numerics.h include/ffd_gabor.h include/ffd_model_format.h
 	@mkdir -p $(@D)
-	$(CXX) $(CXXFLAGS) -shared -pthread -o $@ $<
+	$(CXX) $(CXXFLAGS) -shared -pthread -o $@ oracle/ffd_oracle.cpp oracle/ffd_train_oracle.cpp
 
 model: $(CONVERT)
 	@mkdir -p model

@@ -119,6 +119,9 @@ EXPORTED_SYMBOLS = (
     "ffd_detect_options_init", "ffd_detect_faces", "ffd_detect_faces_device", "ffd_analyze_images",
     "ffd_detect_candidates", "ffd_model_open", "ffd_model_close", "ffd_model_last_error", "ffd_model_num_trees", "ffd_model_tree_save_path",
     "ffd_model_tree_archive", "ffd_model_save_tree",
+    "ffd_train_param_init", "ffd_train_mp_tree", "ffd_train_last_error", "ffd_trained_tree_num_nodes",
+    "ffd_trained_tree_num_leaves", "ffd_trained_tree_arrays", "ffd_trained_tree_stats", "ffd_trained_tree_archive",
+    "ffd_trained_tree_save", "ffd_trained_tree_free",
 )
 COMM_ID_BYTES = 128
 STATUS_OK, STATUS_INVALID_ARGUMENT, STATUS_UNSUPPORTED = 0, 1, 7

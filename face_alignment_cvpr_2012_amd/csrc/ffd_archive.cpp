@@ -158,12 +158,10 @@ const T* opt(const ffd::ModelFile& m, const std::string& name) {
   return m.has(name) ? m.get(name).as<T>() : nullptr;
 }
 
-ffd_status archive_tree(const ffd_model* model, int32_t kind, int32_t tree, std::string& out) {
-  if (!model) return fail(FFD_ERR_INVALID_ARGUMENT, "model is NULL");
+ffd_status archive_tree(const ffd::ModelFile& m, int32_t kind, int32_t tree, std::string& out) {
   const char* p = prefix_of(kind);
   if (!p) return fail(FFD_ERR_INVALID_ARGUMENT, "forest_kind must be FFD_FOREST_HEADPOSE or FFD_FOREST_FFD");
   const std::string P = p;
-  const ffd::ModelFile& m = model->file;
   try {
     const auto& toff = m.get(P + ".tree_node_off");
     const int64_t T = (int64_t)toff.count() - 1;
@@ -248,7 +246,21 @@ ffd_status archive_tree(const ffd_model* model, int32_t kind, int32_t tree, std:
   return FFD_OK;
 }
 
+ffd_status archive_tree(const ffd_model* model, int32_t kind, int32_t tree, std::string& out) {
+  if (!model) return fail(FFD_ERR_INVALID_ARGUMENT, "model is NULL");
+  return archive_tree(model->file, kind, tree, out);
+}
+
 }  // namespace
+
+namespace ffd_host {
+// Boost text archive of tree `tree` of an in-memory FFDMODEL container (trained trees, ffd_train.cpp)
+ffd_status archive_model_tree(const ffd::ModelFile& m, int32_t kind, int32_t tree, std::string& out, std::string& err) {
+  const ffd_status st = archive_tree(m, kind, tree, out);
+  if (st != FFD_OK) err = g_model_error;
+  return st;
+}
+}  // namespace ffd_host
 
 extern "C" {
 

@@ -160,3 +160,41 @@ def make_frames(n_frames, faces_per_frame=8, width=1920, height=1080, seed=1080,
             boxes[f, k] = face_box_from_detection(det, width, height)
         frames[f] = frame
     return frames, boxes, paste
+
+
+def training_rois(n, face_size=125, seed=7, fixtures=None):
+    """Training ROIs for facial-feature tree training, following trainTree
+    (src/train_ffd.cpp:82-99): image k = bundled fixture k mod 20 (k >= 20: horizontally jittered,
+    rescaled and noised variants, seeded), scaled so the face box is face_size wide (bilinear,
+    edge-clamped; not OpenCV's resize, the ROIs are inputs, not parity subjects), then the box
+    enlarged by 10 % per side and clipped to the image (face_utils.cpp enlargeFace).  Returns
+    (list of uint8 gray ROIs, int32 [n, 10, 2] landmarks in ROI pixels).  The LFW training set the
+    reference trains on (config_ffd.txt) is not in the repository."""
+    fx = fixtures or load_fixtures()
+    imgs, boxes, parts = fx["images"], fx["boxes"], fx["parts"]
+    rng = np.random.default_rng(seed)
+    rois, pts = [], np.zeros((n, 10, 2), np.int32)
+    for k in range(n):
+        i = k % len(imgs)
+        x, y, w, h = (float(v) for v in boxes[i])
+        p = parts[i].astype(np.float64) + np.array([x, y])  # image coordinates
+        jit = np.zeros(2) if k < len(imgs) else rng.uniform(-4, 4, size=2)
+        scl = 1.0 if k < len(imgs) else rng.uniform(0.93, 1.07)
+        s = face_size / (w * scl)
+        H, W = imgs[i].shape[:2]
+        sw, sh = int(W * s), int(H * s)
+        xs = (np.arange(sw) + 0.5) / s - 0.5 + jit[0]
+        ys = (np.arange(sh) + 0.5) / s - 0.5 + jit[1]
+        bgr = _bilinear(imgs[i], xs, ys)
+        gray = (bgr[..., 0] * 0.114 + bgr[..., 1] * 0.587 + bgr[..., 2] * 0.299)
+        if k >= len(imgs):
+            gray = gray + rng.normal(0.0, 2.0, size=gray.shape)
+        gray = np.clip(np.rint(gray), 0, 255).astype(np.uint8)
+        bx, by, bw, bh = int((x - jit[0]) * s), int((y - jit[1]) * s), int(w * s), int(h * s)
+        ox, oy = int(bw * 0.1), int(bh * 0.1)
+        x0, y0 = max(bx - ox, 0), max(by - oy, 0)
+        x1, y1 = min(bx - ox + bw + 2 * ox, sw), min(by - oy + bh + 2 * oy, sh)
+        rois.append(np.ascontiguousarray(gray[y0:y1, x0:x1]))
+        q = (p - jit) * s
+        pts[k] = np.rint(q - np.array([x0, y0])).astype(np.int32)
+    return rois, pts

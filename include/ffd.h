@@ -307,6 +307,68 @@ ffd_status ffd_model_tree_archive(const ffd_model* model, int32_t forest_kind, i
                                   int64_t* size);
 ffd_status ffd_model_save_tree(const ffd_model* model, int32_t forest_kind, int32_t tree, const char* path);
 
+/* ---- Facial-feature tree training ----------------------------------------
+ * Replaces trainTree (src/train_ffd.cpp:34-123) from the training ROIs on: the patch sampling, the
+ * MPSample ctor (src/MPSample.cpp:13-41), Tree<MPSample>(samples, param, rng, save_path)
+ * (include/Tree.hpp:43-63) with grow / findOptimalSplit / applyOptimalSplit (Tree.hpp:102-171,261-308),
+ * SplitGen::generate / generateMT / findThreshold / splitSamples (include/SplitGen.hpp:62-231) and
+ * MPSample::generateSplit / evalSplit / makeLeaf (src/MPSample.cpp:86-297).  The split search of every
+ * node of a tree level runs on the GPU (one wave per (node, stripe)); the result is the reference's
+ * Tree archive (Tree<S>::save, Tree.hpp:239-256) through the writer above.
+ * Seeds: tree_seed is trainTree's rng.seed(idx_tree + 1); split_seed stands for the std::time(NULL) of
+ * SplitGen::generateMT (SplitGen.hpp:78), which makes the reference's training irreproducible: stripe s
+ * of the node with heap index h (root 1, children 2h, 2h + 1) uses mt19937((s + 1) * (split_seed + h)).
+ * Definitions the reference leaves open are listed in oracle/ffd_train_oracle.cpp (parity unpinned). */
+typedef struct {                 /* ForestParam, include/Constants.hpp:24-60 (config_ffd.txt values) */
+  int32_t max_depth;             /* 20 */
+  int32_t min_patches;           /* 20 */
+  int32_t ntests;                /* 2500 */
+  int32_t ntrees;                /* 20  (archived) */
+  int32_t nimages;               /* 600 (archived) */
+  int32_t npatches;              /* 150 patches per image */
+  int32_t face_size;             /* 125 */
+  float patch_size_ratio;        /* 0.25: patch size round(face_size * ratio) = 31 */
+  const char* tree_path;         /* archived ForestParam::tree_path ("data/trees_ffd") */
+  const char* image_path;        /* archived ForestParam::image_path */
+  const char* save_path;         /* archived Tree::m_save_path */
+  uint32_t tree_seed;            /* rng.seed(idx_tree + 1), train_ffd.cpp:66-67 */
+  uint32_t split_seed;           /* std::time(NULL)'s stand-in, see above */
+  int32_t device;                /* HIP device ordinal */
+} ffd_train_param;
+
+typedef struct {                 /* one training image: the ROI of train_ffd.cpp:82-99 */
+  const uint8_t* gray;           /* enlarged face at face_size scale, 8-bit gray */
+  int32_t width, height, stride;
+  const int32_t* parts;          /* 10 x (x, y) landmarks in ROI pixels (annotations[i].parts) */
+} ffd_train_image;
+
+typedef struct {                 /* where the time went (host wall clock, ms) */
+  double channels_ms, search_ms, partition_ms, leaves_ms, total_ms;
+  int64_t samples, items;        /* patches; (node, stripe) items evaluated over all levels */
+  int32_t levels;
+} ffd_train_stats;
+
+typedef struct ffd_trained_tree ffd_trained_tree;
+
+void ffd_train_param_init(ffd_train_param* p);
+ffd_status ffd_train_mp_tree(const ffd_train_param* p, const ffd_train_image* images, int32_t n_images,
+                             ffd_trained_tree** out);
+const char* ffd_train_last_error(void);  /* this thread's last ffd_train_* failure */
+int64_t ffd_trained_tree_num_nodes(const ffd_trained_tree* t);
+int64_t ffd_trained_tree_num_leaves(const ffd_trained_tree* t);
+/* pre-order node arrays in the FFDMODEL layout (node_leaf: leaf ordinal or -1; node_split: channel, rect1,
+ * rect2, threshold as 10 x i16; node_info: the split's information gain) and the MPLeaf payloads
+ * (leaf_offset: 10 x (x, y) i16, leaf_var / leaf_pf: 10 x f32); samples_xy: (image, x, y) per patch.
+ * Any pointer may be NULL. */
+ffd_status ffd_trained_tree_arrays(const ffd_trained_tree* t, int32_t* node_leaf, int16_t* node_split,
+                                   double* node_info, int32_t* leaf_n, float* leaf_fg, int16_t* leaf_offset,
+                                   float* leaf_var, float* leaf_pf, int32_t* samples_xy);
+ffd_status ffd_trained_tree_stats(const ffd_trained_tree* t, ffd_train_stats* stats);
+/* Tree<MPSample>::save's archive bytes (buf == NULL: only *size) / to a file */
+ffd_status ffd_trained_tree_archive(const ffd_trained_tree* t, char* buf, int64_t cap, int64_t* size);
+ffd_status ffd_trained_tree_save(const ffd_trained_tree* t, const char* path);
+void ffd_trained_tree_free(ffd_trained_tree* t);
+
 /* Library version string. */
 const char* ffd_version(void);
 

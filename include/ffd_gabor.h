@@ -77,4 +77,26 @@ static inline void ffd_gabor_sep_init(int nu, ffd_gabor_sep* s) {
   }
 }
 
+/* The reference's 2-D kernel of scale nu, orientation mu (createKernel, FeatureChannelFactory.hpp:186-205)
+ * as floats, [row j = y + R][column i = x + R]; returns the width 2R + 1 (re / im hold width^2 taps). */
+static inline int ffd_gabor_taps(int nu, int mu, float* re, float* im) {
+  const double CV_PI = 3.1415926535897932384626433832795;
+  const double sigma = 1.0 / 2.0 * CV_PI, F = std::sqrt(2.0);
+  const double k = (CV_PI / 2) / std::pow(F, (double)nu), phi = CV_PI * mu / 8;
+  double width = std::round((sigma / k) * 6 + 1);
+  if (std::fmod(width, 2.0) == 0.0) width++;
+  const int W = (int)width, off = (int)((width - 1) / 2);
+  for (int i = 0; i < W; i++)
+    for (int j = 0; j < W; j++) {
+      const int x = i - off, y = j - off;
+      const double t1 = (std::pow(k, 2) / std::pow(sigma, 2)) *
+                        std::exp(-(std::pow((double)x, 2) + std::pow((double)y, 2)) * std::pow(k, 2) / (2 * std::pow(sigma, 2)));
+      const double t2 = std::cos(k * std::cos(phi) * x + k * std::sin(phi) * y) - std::exp(-(std::pow(sigma, 2) / 2));
+      const double t3 = std::sin(k * std::cos(phi) * x + k * std::sin(phi) * y);
+      re[j * W + i] = (float)(t1 * t2);
+      im[j * W + i] = (float)(t1 * t3);
+    }
+  return W;
+}
+
 #endif /* FFD_GABOR_H */

@@ -127,6 +127,35 @@ FFD_HD float ffd_expf_nonpos(float xf) {
   return under ? 0.0f : e;
 }
 
+/* log(x) in binary64 for finite x > 0 (the entropy terms of forest training, MPSample::entropie_parts,
+ * /root/reference/src/MPSample.cpp:276-297): x = 2^k m with m in [sqrt(2)/2, sqrt(2)), f = m - 1,
+ * s = f / (2 + f), log(m) = f - s (f - R(s^2)) with fdlibm's e_log.c minimax coefficients, only +, -,
+ * *, / (no fma), so the oracle and the kernels produce the same bits; within 1 ulp of libm's log
+ * (tests/test_numerics.py).  Subnormal x is scaled by 2^54 first. */
+FFD_HD double ffd_log(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01;  /* 0x3FE62E42FEE00000 */
+  const double ln2_lo = 1.90821492927058770002e-10;  /* 0x3DEA39EF35793C76 */
+  const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
+               Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  int k = 0;
+  if (x < 2.2250738585072014e-308) { x = x * 18014398509481984.0; k = -54; } /* 2^54 */
+  int e;
+#ifdef __cplusplus
+  double m = std::frexp(x, &e);  /* x = m 2^e, m in [0.5, 1): exact */
+#else
+  double m = frexp(x, &e);
+#endif
+  if (m < 0.70710678118654752440) { m = m + m; e -= 1; }
+  k += e;
+  const double f = m - 1.0;  /* exact (Sterbenz) */
+  const double s = f / (2.0 + f), z = s * s, w = z * z;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  const double R = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
 /* a / b for a divisor b whose reciprocal y = RN(1/b) is given: q = RN(a y), r = a - b q (exact with
  * an fma), RN(q + r y) (Markstein's correction).  It is the correctly rounded quotient whenever the
  * premises of Markstein's theorem hold (not for subnormal quotients: |a| <= 2^-100 divides

@@ -270,3 +270,65 @@ def estimate_facial_features(channels, region, tree_ids):
                                              pts.ctypes.data) != 0:
         raise RuntimeError(lib().oracle_last_error().decode())
     return pts
+
+
+class OracleTrainParam(ctypes.Structure):
+    """ForestParam (Constants.hpp:24-60) + the seeds (oracle/ffd_oracle.h oracle_train_param)."""
+    _fields_ = [("max_depth", ctypes.c_int32), ("min_patches", ctypes.c_int32), ("ntests", ctypes.c_int32),
+                ("ntrees", ctypes.c_int32), ("nimages", ctypes.c_int32), ("npatches", ctypes.c_int32),
+                ("face_size", ctypes.c_int32), ("patch_size_ratio", ctypes.c_float),
+                ("num_thresholds", ctypes.c_int32), ("tree_seed", ctypes.c_uint32), ("split_seed", ctypes.c_uint32),
+                ("lamda", ctypes.c_float)]
+
+
+def train_mp_tree(rois, parts, max_depth=20, min_patches=20, ntests=2500, npatches=150, face_size=125,
+                  patch_size_ratio=0.25, tree_seed=1, split_seed=1, ntrees=20, nimages=600):
+    """The CPU restatement of trainTree + Tree<MPSample> growth (oracle/ffd_train_oracle.cpp): returns the
+    pre-order node arrays, MPLeaf payloads, sampled patches and i_node."""
+    L = lib()
+    if not getattr(L, "_train_bound", False):
+        L.oracle_train_mp_tree.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(OracleTrainParam),
+                                           ctypes.POINTER(ctypes.c_void_p)]
+        L.oracle_train_tree_size.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int64)] * 3
+        L.oracle_train_tree_get.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 9
+        L.oracle_train_tree_free.argtypes = [ctypes.c_void_p]
+        L.oracle_train_last_error.restype = ctypes.c_char_p
+        L.oracle_log.argtypes = [ctypes.c_double]
+        L.oracle_log.restype = ctypes.c_double
+        L._train_bound = True
+    rois = [np.ascontiguousarray(r, np.uint8) for r in rois]
+    parts = np.ascontiguousarray(parts, np.int32)
+    n = len(rois)
+    ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in rois])
+    ws = np.array([r.shape[1] for r in rois], np.int32)
+    hs = np.array([r.shape[0] for r in rois], np.int32)
+    p = OracleTrainParam(max_depth, min_patches, ntests, ntrees, nimages, npatches, face_size, patch_size_ratio,
+                         25, tree_seed, split_seed, 0.125)
+    h = ctypes.c_void_p()
+    if L.oracle_train_mp_tree(ptrs, ws.ctypes.data, hs.ctypes.data, parts.ctypes.data, n, parts.shape[1],
+                              ctypes.byref(p), ctypes.byref(h)) != 0:
+        raise RuntimeError("oracle_train_mp_tree: " + L.oracle_train_last_error().decode())
+    try:
+        nn, nl, inode = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        L.oracle_train_tree_size(h, ctypes.byref(nn), ctypes.byref(nl), ctypes.byref(inode))
+        N, Lf = nn.value, nl.value
+        a = {"node_leaf": np.zeros(N, np.int32), "node_split": np.zeros((N, 10), np.int16),
+             "node_info": np.zeros(N, np.float64), "leaf_n": np.zeros(Lf, np.int32), "leaf_fg": np.zeros(Lf, np.float32),
+             "leaf_offset": np.zeros((Lf, 10, 2), np.int16), "leaf_var": np.zeros((Lf, 10), np.float32),
+             "leaf_pf": np.zeros((Lf, 10), np.float32), "samples": np.zeros((n * npatches, 3), np.int32)}
+        L.oracle_train_tree_get(h, *(a[k].ctypes.data for k in ("node_leaf", "node_split", "node_info", "leaf_n",
+                                                                 "leaf_fg", "leaf_offset", "leaf_var", "leaf_pf",
+                                                                 "samples")))
+        a["i_node"] = inode.value
+        return a
+    finally:
+        L.oracle_train_tree_free(h)
+
+
+def log(x):
+    lib()
+    if not getattr(lib(), "_train_bound", False):
+        lib().oracle_log.argtypes = [ctypes.c_double]
+        lib().oracle_log.restype = ctypes.c_double
+    return lib().oracle_log(x)

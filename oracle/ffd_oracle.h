@@ -98,6 +98,31 @@ int oracle_detect_faces(const uint8_t* bgr, int32_t w, int32_t h, int32_t stride
                         int32_t min_neighbors, float scale_factor, int32_t widen, int32_t* boxes, int32_t cap,
                         int32_t* n_boxes, int32_t* raw, int32_t raw_cap, int32_t* n_raw);
 
+/* Facial-feature tree training (oracle/ffd_train_oracle.cpp): ForestParam
+ * (Constants.hpp:24-60) plus the seeds the reference takes from idx_tree and std::time(NULL). */
+typedef struct {
+  int32_t max_depth, min_patches, ntests, ntrees, nimages, npatches, face_size;
+  float patch_size_ratio;
+  int32_t num_thresholds;  /* 25 (MPSample::generateSplit) */
+  uint32_t tree_seed;      /* rng.seed(idx_tree + 1) (train_ffd.cpp:66-67) */
+  uint32_t split_seed;     /* stands for std::time(NULL) in SplitGen::generateMT (+ the node's heap index) */
+  float lamda;             /* MPSample ctor's lamda, 0.125 */
+} oracle_train_param;
+typedef struct oracle_train_tree oracle_train_tree;
+/* images: n_images gray training ROIs (rows packed, stride = width); parts: n_images x n_parts x (x, y). */
+int oracle_train_mp_tree(const uint8_t* const* images, const int32_t* widths, const int32_t* heights,
+                         const int32_t* parts, int32_t n_images, int32_t n_parts, const oracle_train_param* p,
+                         oracle_train_tree** out);
+int oracle_train_tree_size(const oracle_train_tree* t, int64_t* n_nodes, int64_t* n_leaves, int64_t* i_node);
+/* Pre-order node arrays in the FFDMODEL layout (node_split: 10 x i16 per node) and MPLeaf payloads;
+ * samples_xy: (image, x, y) of every sampled patch.  Any pointer may be NULL. */
+int oracle_train_tree_get(const oracle_train_tree* t, int32_t* node_leaf, int16_t* node_split, double* node_info,
+                          int32_t* leaf_n, float* leaf_fg, int16_t* leaf_offset, float* leaf_var, float* leaf_pf,
+                          int32_t* samples_xy);
+void oracle_train_tree_free(oracle_train_tree* t);
+const char* oracle_train_last_error(void);
+double oracle_log(double x);
+
 /* Stage hooks for known-answer tests. */
 int oracle_bgr2gray(const uint8_t* bgr, int32_t w, int32_t h, int32_t stride, uint8_t* gray);
 int oracle_resize(const uint8_t* src, int32_t sw, int32_t sh, int32_t sstride, int32_t dw,

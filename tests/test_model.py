@@ -83,8 +83,9 @@ def test_structure_invariants(m):
     assert off[..., 1].min() == -92 and off[..., 1].max() == 142
 
 
-def _parse_archive(path, hp):
-    """Independent minimal reader of one Boost text archive (grammar: SURVEY.md App. A)."""
+def _parse_archive(path, hp, infos=None):
+    """Independent minimal reader of one Boost text archive (grammar: SURVEY.md App. A); infos, if a
+    list, receives every split's archived ThresholdSplit::info token in pre-order."""
     toks = open(path).read().split()
     it = iter(toks)
     nx = lambda: next(it)  # noqa: E731
@@ -132,7 +133,9 @@ def _parse_archive(path, hp):
             if first["split"]:
                 nx(); nx(); first["split"] = False  # noqa: E702
             r = [int(nx()) for _ in range(8)]
-            nx()
+            info = nx()
+            if infos is not None:
+                infos.append(info)
             splits.append([ch] + r + [int(nx())])
         if not is_leaf:
             assert nx() == "3"
