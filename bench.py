@@ -621,6 +621,22 @@ def main():
                                   "frac": round(value * b_face / 1e9 / HBM_PEAK_GBS, 4)},
             "stage_ms_per_step": {k: round(v[0] / max(1, args.steps), 3) for k, v in stages.items()},
         }
+        # the Gabor stage's FP32 fraction beside the HBM figure, per scale
+        gab = {}
+        for k, (ms_k, nl) in stages.items():
+            if k.startswith("gabor_") and ms_k > 0:
+                w = int(k.split("_")[1].split("x")[0])
+                fpp = gabor_flops_per_pixel(w, W)
+                tf = n * args.steps * W * H * fpp / (ms_k / 1e3) / 1e12
+                gab[k] = {"flops_per_px": round(fpp, 1), "tflops": round(tf, 2), "fp32_frac": round(tf / FP32_PEAK_TFLOPS, 4)}
+        if gab:
+            tot_ms = sum(stages[k][0] for k in gab) / max(1, args.steps)
+            tot_tf = sum(n * W * H * gabor_flops_per_pixel(int(k.split("_")[1].split("x")[0]), W) for k in gab) / (tot_ms / 1e3) / 1e12
+            out["gabor_fp32"] = {"per_scale": gab, "all_scales_ms": round(tot_ms, 3), "tflops": round(tot_tf, 2),
+                                 "fp32_frac": round(tot_tf / FP32_PEAK_TFLOPS, 4), "peak_tflops": FP32_PEAK_TFLOPS}
+        if wl.name == "c4":  # faces/s, patches/s, HBM fraction
+            out["c4"] = {"patches_per_face": round(n_mp, 1), "patches_per_s": round(value * n_mp, 1),
+                         "walks_per_s": round(value * n_mp * 20, 1), "forest_depth": 20}
         if host_incl is not None:
             out["host_inclusive"] = host_incl
             out["analyze_face_latency"] = latency

@@ -660,6 +660,9 @@ __device__ __forceinline__ int node_off(uint32_t enc, int ld) {
   return (int)__umul24(enc >> 7, (unsigned)ld) + (int)(enc & 127u);
 }
 
+#ifndef FFD_TRAV_MID_ALWAYS
+#define FFD_TRAV_MID_ALWAYS 1  // 0: middle row only for area > 257 (exec-masked; measured slower: FFD 8.42 -> 8.52 ms)
+#endif
 // ImageSample::evalTest's rectangle mean over the LDS window (k_traverse): p = byte address of the
 // rectangle's top-left integral corner, ld2 = window row pitch in bytes.  The sum is taken as two
 // halves split at h >> 1 rows, each exact modulo 2^16 (rect_mean16), and the quotient
@@ -670,13 +673,26 @@ __device__ __forceinline__ int rect_mean_lds(const unsigned char* __restrict__ p
                                              int ld2) {
   const int wb = (int)(2u * w);
   const int r1 = (int)__umul24(hh, (unsigned)ld2), r2 = (int)__umul24(h, (unsigned)ld2);
+  const uint32_t area = __umul24(w, h);
   const uint32_t a = *reinterpret_cast<const uint16_t*>(p), b = *reinterpret_cast<const uint16_t*>(p + wb);
-  const uint32_t c = *reinterpret_cast<const uint16_t*>(p + r1), d = *reinterpret_cast<const uint16_t*>(p + r1 + wb);
   const uint32_t f0 = *reinterpret_cast<const uint16_t*>(p + r2), f1 = *reinterpret_cast<const uint16_t*>(p + r2 + wb);
+#if FFD_TRAV_MID_ALWAYS
+  const uint32_t c = *reinterpret_cast<const uint16_t*>(p + r1), d = *reinterpret_cast<const uint16_t*>(p + r1 + wb);
+#else
+  // The middle row only for rectangles whose sum can reach 2^16 (area > 257, ~15 % of the model's
+  // rectangles): below that the 4-corner sum mod 2^16 is exact, and c = a, d = b turn the formula
+  // below into it (top = 0, bot = the whole rectangle).  The reads are exec-masked, so the lanes at
+  // small rectangles take no part in their bank conflicts.
+  uint32_t c = a, d = b;
+  if (area > 257u) {
+    c = *reinterpret_cast<const uint16_t*>(p + r1);
+    d = *reinterpret_cast<const uint16_t*>(p + r1 + wb);
+  }
+#endif
   // top = (a - b) + (d - c), bot = (f1 - f0) - (d - c), each mod 2^16 (u16 arithmetic), R = top + bot
   typedef unsigned short u16;
   const u16 dc = (u16)(d - c), top = (u16)((u16)(a - b) + dc), bot = (u16)((u16)(f1 - f0) - dc);
-  return (int)__builtin_fmaf((float)((uint32_t)top + bot), __builtin_amdgcn_rcpf((float)__umul24(w, h)), 0.00075f);
+  return (int)__builtin_fmaf((float)((uint32_t)top + bot), __builtin_amdgcn_rcpf((float)area), 0.00075f);
 }
 
 // Tree<S>::evaluateMT over global u16 planes (ffd_forest_eval_leaves hook).
@@ -707,8 +723,10 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 // evaluated (one 16-byte load per visit; the CU's vector-memory return path is the traversal's
 // bottleneck, profiles/r2a), and the test picks the child.
 #ifndef FFD_TRAV_PROBE
-#define FFD_TRAV_PROBE 0  // timing probes (tools/probe.sh): 1 = stage only, 2 = walk only, 3 = one tree per block
-#endif
+#define FFD_TRAV_PROBE 0  // timing probes (tools/probe.sh): 1 = stage only, 2 = walk only, 3 = one tree per block,
+#endif                    // 4 = walk only without window reads, 5 = 4 with staging, 6 = deep records from 4096 pairs,
+                          // 7 = walk only reading rect 1 only, 8 = 7 with staging
+#define FFD_TRAV_NOSTAGE (FFD_TRAV_PROBE == 2 || FFD_TRAV_PROBE == 4 || FFD_TRAV_PROBE == 6 || FFD_TRAV_PROBE == 7)
 // Walker threads per workgroup by patch-block edge G: a block's G*G*T walks run in one round (T = 20
 // FFD trees: 4x4 -> 320, 5x5 -> 500 of 512), the other threads stage the next window.  A block costs
 // about its longest walk chain, so the walks a window holds per block set the throughput: FFD 5x5
@@ -825,14 +843,21 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       const unsigned char* base = reinterpret_cast<const unsigned char*>(win) +
                                   2 * ((yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh);
       auto test = [&](uint32_t lo, uint32_t hi) {
+#if FFD_TRAV_PROBE == 4 || FFD_TRAV_PROBE == 5
+        return ((lo ^ (hi >> 3)) >> 9) & 1u;  // probe: no window reads
+#endif
         // (fields by bit-field extracts; bits of hi above 23 are the record's child offset, never read)
         const unsigned char* cb = base + __umul24(lo >> 26, (unsigned)chs2);
         const int p1 = rect_mean_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 0, 5),
                                      __builtin_amdgcn_ubfe(hi, 0, 5), __builtin_amdgcn_ubfe(hi, 5, 5),
                                      __builtin_amdgcn_ubfe(hi, 6, 4), ld2);
+#if FFD_TRAV_PROBE == 7 || FFD_TRAV_PROBE == 8  // probe: the second rectangle is not read
+        const int p2 = (int)(hi >> 24);
+#else
         const int p2 = rect_mean_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 15, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 10, 5),
                                      __builtin_amdgcn_ubfe(hi, 10, 5), __builtin_amdgcn_ubfe(hi, 15, 5),
                                      __builtin_amdgcn_ubfe(hi, 16, 4), ld2);
+#endif
         // 10-bit two's complement: sign-extended thr[9:6] (hi[23:20]) above thr[5:0] (lo[25:20])
         const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
         return (p1 - p2) <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
@@ -854,13 +879,21 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         hi = s ? R.w : R.z;
       }
       uint32_t P = top_i[t * topn + h];
+#if FFD_TRAV_PROBE == 6
+      int probe_depth = 0;
+#endif
       // deeper levels: pair records from HBM (L2), the children pair requested before the test
       while (lo < (63u << 26)) {  // not a leaf (ch = 63)
         // children pair of the current node: right after its pair (child 0), or off1 away (child 1)
         const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
         uint32_t Q = P + (s ? off1 : 1u);
         if (s && off1 == 0u) Q = P + A.far[P];
+#if FFD_TRAV_PROBE == 6
+        const uint4 N = A.pairs[Q & 4095u];
+        if (++probe_depth > 24) break;
+#else
         const uint4 N = A.pairs[Q];
+#endif
         s = test(lo, hi);
         P = Q;
         R = N;
@@ -879,10 +912,9 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   if (tid >= NW) {
     // Staging: chunk i = (channel c, window row r, 8-column group q), i = (c * WH + r) * nq + q, goes
     // to LDS chunk i; staging thread s owns chunks s + u * NS.  Their face-relative source byte
-    // offsets c * plane + r * PITCH * 2 + q * 8 are computed once (every face of a batch has the
-    // same plane stride, TravArgs::plane), so a block costs one load per chunk.
+    // offsets c * plane + r * PITCH * 2 + q * 8 are the same for every block (every face of a batch has
+    // the same plane stride, TravArgs::plane).
     chunk_t st[U];
-    int voff[U];
     // tree tops of the next block (entry e = j + u * NS of its T x TOPN tables), reloaded only when
     // the face (and so the tree set) changes
     constexpr int TU = (TRAV_TOP_ENTRIES + NS - 1) / NS;
@@ -891,22 +923,12 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     uint32_t top_p[TU];
     int top_face = -1;  // face whose tops the LDS holds after the next commit
     bool top_new = false;
-    auto stage_offsets = [&](int plane_b) {
-      const int s = tid - NW;
-      const int dq = NS % nq, dr = (NS / nq) % WH, dc = NS / (nq * WH);
-      int q = s % nq, r = (s / nq) % WH, c = s / (nq * WH);
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        voff[u] = min(c, NCH) * plane_b + r * (PITCH * 2) + q * CB;
-        q += dq;
-        int cr = q >= nq;
-        q -= cr ? nq : 0;
-        r += dr + cr;
-        cr = r >= WH;
-        r -= cr ? WH : 0;
-        c += dc + cr;
-      }
-    };
+    // chunk (c, r, q) of this thread's first chunk and the (c, r, q) step between its chunks: the source
+    // offsets are rebuilt per block from these six registers (an array of U offsets made the stager
+    // role spill at U = 22)
+    const int s0 = tid - NW;
+    const int dq = NS % nq, dr = (NS / nq) % WH, dc = NS / (nq * WH);
+    const int q0 = s0 % nq, r0 = (s0 / nq) % WH, c0 = s0 / (nq * WH);
     auto prefetch = [&](const Blk& B) {
       if (!B.ok) return;
       const FaceDesc& fd = A.faces[B.f];
@@ -938,11 +960,21 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
           }
         }
       }
-#if FFD_TRAV_PROBE != 2
+#if !FFD_TRAV_NOSTAGE
+      const int plane_b = A.plane * 2;
+      int q = q0, r = r0, c = c0;
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff[u], base_b, 0);
-        else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff[u], base_b, 0);
+        const int voff = min(c, NCH) * plane_b + r * (PITCH * 2) + q * CB;
+        if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, base_b, 0);
+        else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, base_b, 0);
+        q += dq;
+        int cr = q >= nq;
+        q -= cr ? nq : 0;
+        r += dr + cr;
+        cr = r >= WH;
+        r -= cr ? WH : 0;
+        c += dc + cr;
       }
 #endif
     };
@@ -961,14 +993,13 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
           }
         }
       }
-#if FFD_TRAV_PROBE != 2  // the walk-only probe keeps the tree tops (walks need valid records)
+#if !FFD_TRAV_NOSTAGE  // the walk-only probes keep the tree tops (walks need valid records)
 #pragma unroll
       for (int u = 0; u < U; u++)
         if (u * NS + s < total) dst[u * NS + s] = st[u];
 #endif
     };
 
-    stage_offsets(A.plane * 2);
     Blk cur = block(lb);
     prefetch(cur);
     for (; lb < end; lb += nk) {
@@ -1320,6 +1351,15 @@ constexpr int MS_FPW = (MS_FACES + 3) / 4;  // faces per wave
 #define FFD_MS_RA 4
 #endif
 constexpr int MS_RA = FFD_MS_RA;  // serial phase: LDS reads in flight ahead of the adds
+#ifndef FFD_MS_DEFAULT
+#define FFD_MS_DEFAULT 1  // k_meanshift (1) or the overlapped k_meanshift3 (3)
+#endif
+#ifndef FFD_MS_UDEF
+#define FFD_MS_UDEF 4
+#endif
+#ifndef FFD_MS_PROBE
+#define FFD_MS_PROBE 0  // timing probes (bits): 1 = no serial phase, 2 = cheap weights, 4 = no early convergence
+#endif
 
 // MeanShift::getWeightedMean's weight of one vote (MeanShift.hpp:122-124): d = cv::norm(mean - pos)
 // (double sqrt, rounded to float), w = weight * expf(-d / lamda).  lam_y > 0: RN(1 / lamda) for the
@@ -1428,14 +1468,18 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         if (p >= MS_FACES || !s_live[p] || k0 + j >= s_cnt[p]) continue;
         const Vote v = vv[i];
         const float fx = (float)v.x, fy = (float)v.y;
+#if FFD_MS_PROBE & 2
+        const float w = pass < 0 ? v.w : v.w * (s_mx[p] - fx);
+#else
         const float w = pass < 0 ? v.w : ms_weight(s_mx[p], s_my[p], fx, fy, v.w, lamda, lam_y);
+#endif
         tx[j * MS_LD + p] = fx * w;
         ty[j * MS_LD + p] = fy * w;
         tw[j * MS_LD + p] = w;
       }
       if (k0 + MS_TILE < maxcnt) load_tile(k0 + MS_TILE);  // in flight during the serial phase
       __syncthreads();
-      if (tid < MS_FACES && s_live[tid]) {  // serial phase, in list order
+      if (!(FFD_MS_PROBE & 1) && tid < MS_FACES && s_live[tid]) {  // serial phase, in list order
         const int lim = min(MS_TILE, s_cnt[tid] - k0);
         int j = 0;
         for (; j + MS_RA <= lim; j += MS_RA) {  // LDS reads of MS_RA terms ahead of their in-order adds
@@ -1468,7 +1512,7 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         s_my[tid] = ay;
       } else {
         const float ddx = ax - s_mx[tid], ddy = ay - s_my[tid];
-        if (__builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) s_live[tid] = 0;  // converged
+        if (!(FFD_MS_PROBE & 4) && __builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) s_live[tid] = 0;  // converged
         s_mx[tid] = ax;
         s_my[tid] = ay;
       }
@@ -1490,32 +1534,29 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
   }
 }
 
-// MeanShift, chain-parallel form (FFD_MS_KERNEL=2; measured 3.3 ms vs 3.0 ms for k_meanshift at C2,
-// profiles/r2 notes, so k_meanshift stays the default).  A "chain"
-// is one (face, landmark) vote list; a 256-thread workgroup runs 64 chains (64 faces, one landmark)
-// through MeanShift::shift (MeanShift.hpp:41-135) in tiles of MS2_T votes per chain:
-//   terms   all 256 threads compute the per-vote terms (x*w, y*w, w) of the next tile (the votes
-//           were loaded into registers one tile ahead), into a double-buffered LDS tile;
-//   sums    lane c of wave 0 adds chain c's MS2_T terms in list order (one ds_read_b128 each),
-// so every running sum is the reference's sequential float sum bit for bit, every lane of wave 0
-// carries a chain during the serial part, and one barrier per tile orders the two buffers.
-#ifndef FFD_MS2_CH
-#define FFD_MS2_CH 32
-#endif
-constexpr int MS2_CH = FFD_MS2_CH, MS2_T = 32, MS2_THREADS = 256, MS2_U = MS2_CH * MS2_T / MS2_THREADS;
-
-__global__ __launch_bounds__(MS2_THREADS) void k_meanshift2(const FaceDesc* __restrict__ faces, int n_faces,
-                                                            int tslots, int n_parts, float lamda, int max_iter,
-                                                            float stop, const Vote* __restrict__ votes,
-                                                            const int32_t* __restrict__ vote_counts,
-                                                            float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
-  __shared__ float4 term[2][MS2_T][MS2_CH];  // [buffer][vote j][chain c] = (x*w, y*w, w, 0)
-  __shared__ float s_mx[MS2_CH], s_my[MS2_CH];
-  __shared__ int s_cnt[MS2_CH], s_live[MS2_CH];
-  __shared__ int64_t s_vb[MS2_CH];
-  __shared__ int s_maxcnt;
-  const int part = blockIdx.y, f0 = blockIdx.x * MS2_CH, tid = threadIdx.x;
-  if (tid < MS2_CH) {
+// MeanShift, overlapped form (FFD_MS_KERNEL=3): a 256-thread workgroup runs F chains (F faces, one
+// landmark; a chain = one face's vote list for that landmark) through MeanShift::shift (MeanShift.hpp:41-135)
+// in tiles of T = 256 U / F votes per chain, double-buffered in LDS:
+//   terms   all 256 threads compute tile k + 1's per-vote terms (x*w, y*w, w) — U per thread, the votes
+//           loaded into registers a tile ahead — into one buffer,
+//   sums    while lanes 0..F-1 of wave 0 add tile k's terms (the other buffer) in list order,
+// one barrier per tile.  Every running sum is the reference's sequential float sum bit for bit; the terms
+// use ms_weight (the exact fast quotient at lamda = 10).  F is chosen per batch (launch_meanshift) so
+// that the grid still has two workgroups per CU.
+template <int F, int U>
+__global__ __launch_bounds__(256) void k_meanshift3(const FaceDesc* __restrict__ faces, int n_faces, int tslots,
+                                                   int n_parts, float lamda, float lam_y, int max_iter, float stop,
+                                                   const Vote* __restrict__ votes, const int32_t* __restrict__ vote_counts,
+                                                   float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
+  constexpr int T = 256 * U / F, CSTEP = 256 / T;  // votes per chain per tile; chain stride of a thread's items
+  static_assert(T * CSTEP == 256 && CSTEP * U == F && T >= 8, "tile shape");
+  __shared__ float4 term[2][T][F];  // [buffer][vote j][chain slot (c + j) mod F] = (x*w, y*w, w, 0)
+  __shared__ float s_mx[F], s_my[F];
+  __shared__ int s_cnt[F], s_live[F];
+  __shared__ int64_t s_vb[F];
+  __shared__ int s_maxcnt, s_any;
+  const int part = blockIdx.y, f0 = blockIdx.x * F, tid = threadIdx.x;
+  if (tid < F) {
     const int f = f0 + tid;
     int cnt = 0, live = 0;
     int64_t vb = 0;
@@ -1531,60 +1572,68 @@ __global__ __launch_bounds__(MS2_THREADS) void k_meanshift2(const FaceDesc* __re
     s_mx[tid] = 0.f;
     s_my[tid] = 0.f;
   }
-  // this thread's items: vote j = tid % T of chains c = tid / T + u * (256 / T) of each tile
-  constexpr int CSTEP = MS2_THREADS / MS2_T;
-  const int j = tid % MS2_T, cb = tid / MS2_T;
-  float ax = 0, ay = 0, aw = 0;  // lane c < 64 of wave 0: chain c's running sums
+  const int j = tid % T, cb = tid / T;
+  float ax = 0, ay = 0, aw = 0;  // lane c < F of wave 0: chain c's running sums
   for (int pass = -1; pass < max_iter; pass++) {
-    if (tid == 0) s_maxcnt = 0;
+    if (tid == 0) { s_maxcnt = 0; s_any = 0; }
     __syncthreads();  // s_mx / s_my / s_live of the previous pass are final
-    if (tid < MS2_CH && s_live[tid]) atomicMax(&s_maxcnt, s_cnt[tid]);
-    __syncthreads();
-    const int maxcnt = s_maxcnt;
-    if (pass >= 0 && maxcnt == 0) {  // no live chain with votes left: every chain has converged
-      bool any = false;
-      for (int c = 0; c < MS2_CH; c++) any |= s_live[c] != 0;
-      if (!any) break;
+    if (tid < F && s_live[tid]) {
+      atomicMax(&s_maxcnt, s_cnt[tid]);
+      atomicOr(&s_any, 1);
     }
+    __syncthreads();
+    if (!s_any) break;  // every chain converged
+    const int maxcnt = s_maxcnt;
     ax = ay = aw = 0;
-    Vote v[MS2_U];
-    auto load_tile = [&](int k0) {
+    int lim[U];
+    float mx[U], my[U];
+    const Vote* vp[U];
 #pragma unroll
-      for (int u = 0; u < MS2_U; u++) {
-        const int c = cb + CSTEP * u, k = k0 + j;
-        v[u] = (s_live[c] && k < s_cnt[c]) ? votes[s_vb[c] + k] : Vote{0, 0, -1.f};
+    for (int u = 0; u < U; u++) {
+      const int c = cb + CSTEP * u;
+      lim[u] = s_live[c] ? s_cnt[c] : 0;
+      mx[u] = s_mx[c];
+      my[u] = s_my[c];
+      vp[u] = votes + s_vb[c];
+    }
+    Vote v[U];
+    auto load = [&](int k0) {
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (k0 + j < lim[u]) v[u] = vp[u][k0 + j];
+    };
+    auto terms = [&](int buf, int k0) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int c = cb + CSTEP * u;
+        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (k0 + j < lim[u]) {
+          const float fx = (float)v[u].x, fy = (float)v[u].y;
+          const float w = pass < 0 ? v[u].w : ms_weight(mx[u], my[u], fx, fy, v[u].w, lamda, lam_y);
+          t = make_float4(fx * w, fy * w, w, 0.f);
+        }
+        term[buf][j][(c + j) & (F - 1)] = t;
       }
     };
-    load_tile(0);
     int buf = 0;
-    for (int k0 = 0; k0 < maxcnt; k0 += MS2_T, buf ^= 1) {
-#pragma unroll
-      for (int u = 0; u < MS2_U; u++) {
-        const int c = cb + CSTEP * u;
-        float px = 0.f, py = 0.f, w = 0.f;
-        if (v[u].w >= 0.f) {  // real weights are fg > 0.5
-          if (pass < 0) {
-            w = v[u].w;
-          } else {
-            const float dx = s_mx[c] - (float)v[u].x, dy = s_my[c] - (float)v[u].y;
-            float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
-            d = ffd_expf(-d / lamda);
-            w = v[u].w * d;  // (the default kernel uses ms_weight's exact fast path)
-          }
-          px = v[u].x * w;
-          py = v[u].y * w;
-        }
-        term[buf][j][(c + j) & (MS2_CH - 1)] = make_float4(px, py, w, 0.f);  // skewed: conflict-free
+    if (maxcnt > 0) {
+      load(0);
+      terms(0, 0);
+      if (T < maxcnt) load(T);
+    }
+    __syncthreads();
+    for (int k0 = 0; k0 < maxcnt; k0 += T, buf ^= 1) {
+      if (k0 + T < maxcnt) {  // the next tile's terms into the other buffer
+        terms(buf ^ 1, k0 + T);
+        if (k0 + 2 * T < maxcnt) load(k0 + 2 * T);
       }
-      if (k0 + MS2_T < maxcnt) load_tile(k0 + MS2_T);  // in flight during the serial part
-      __syncthreads();  // tile k0's terms are in term[buf]; term[buf ^ 1] was consumed last tile
-      if (tid < MS2_CH && s_live[tid]) {
-        const int lim = min(MS2_T, s_cnt[tid] - k0);
+      if (tid < F && s_live[tid]) {  // this tile's sums, in list order
+        const int n = min(T, s_cnt[tid] - k0);
         int q = 0;
-        for (; q + 8 <= lim; q += 8) {  // LDS reads 8 ahead of their in-order adds
+        for (; q + 8 <= n; q += 8) {  // LDS reads 8 ahead of their in-order adds
           float4 t[8];
 #pragma unroll
-          for (int e = 0; e < 8; e++) t[e] = term[buf][q + e][(tid + q + e) & (MS2_CH - 1)];
+          for (int e = 0; e < 8; e++) t[e] = term[buf][q + e][(tid + q + e) & (F - 1)];
 #pragma unroll
           for (int e = 0; e < 8; e++) {
             ax += t[e].x;
@@ -1592,30 +1641,30 @@ __global__ __launch_bounds__(MS2_THREADS) void k_meanshift2(const FaceDesc* __re
             aw += t[e].z;
           }
         }
-        for (; q < lim; q++) {
-          const float4 t = term[buf][q][(tid + q) & (MS2_CH - 1)];
+        for (; q < n; q++) {
+          const float4 t = term[buf][q][(tid + q) & (F - 1)];
           ax += t.x;
           ay += t.y;
           aw += t.z;
         }
       }
+      __syncthreads();  // tile k0 + T's terms are complete; tile k0's buffer is free
     }
-    __syncthreads();  // every chain's sums are complete before the means change
-    if (tid < MS2_CH && s_live[tid]) {
+    if (tid < F && s_live[tid]) {
       if (aw > 0) { ax /= aw; ay /= aw; }
       if (pass < 0) {
         s_mx[tid] = ax;
         s_my[tid] = ay;
       } else {
         const float ddx = ax - s_mx[tid], ddy = ay - s_my[tid];
-        if (__builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) s_live[tid] = 0;  // converged
+        if (!(FFD_MS_PROBE & 4) && __builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) s_live[tid] = 0;  // converged
         s_mx[tid] = ax;
         s_my[tid] = ay;
       }
     }
   }
   __syncthreads();
-  if (tid < MS2_CH) {
+  if (tid < F) {
     const int f = f0 + tid;
     if (f < n_faces && faces[f].valid) {
       const float mx = s_mx[tid], my = s_my[tid];
@@ -1800,18 +1849,29 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
   (void)state;
   static const int which = [] {
     const char* v = std::getenv("FFD_MS_KERNEL");
-    return v ? std::atoi(v) : 1;
+    return v ? std::atoi(v) : FFD_MS_DEFAULT;
   }();
+  const float lam_y = lamda == 10.f ? 1.f / 10.f : 0.f;  // the verified fast quotient (ffd_div_rcp)
   if (which == 1) {
     dim3 grid((n + MS_FACES - 1) / MS_FACES, NPARTS);
-    const float lam_y = lamda == 10.f ? 1.f / 10.f : 0.f;  // the verified fast quotient (ffd_div_rcp)
     k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes,
                                             vote_counts, ms_mean, out);
-  } else {
-    dim3 grid((n + MS2_CH - 1) / MS2_CH, NPARTS);
-    k_meanshift2<<<grid, MS2_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, max_iter, stop, votes, vote_counts,
-                                              ms_mean, out);
+    return;
   }
+  // overlapped form: the most chains per workgroup that still gives >= 512 workgroups (two per CU)
+  static const int ms_u = [] {
+    const char* v = std::getenv("FFD_MS_U");
+    return v ? std::atoi(v) : FFD_MS_UDEF;
+  }();
+  auto grid_for = [&](int F) { return dim3((n + F - 1) / F, NPARTS); };
+#define FFD_MS3(FV, UV) k_meanshift3<FV, UV><<<grid_for(FV), 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out)
+  const int64_t lists = (int64_t)n * NPARTS;
+  if (ms_u == 8) {
+    if (lists >= 64 * 512) FFD_MS3(64, 8); else if (lists >= 32 * 512) FFD_MS3(32, 8); else FFD_MS3(16, 8);
+  } else {
+    if (lists >= 64 * 512) FFD_MS3(64, 4); else if (lists >= 32 * 512) FFD_MS3(32, 4); else FFD_MS3(16, 4);
+  }
+#undef FFD_MS3
 }
 
 }  // namespace ffd
