@@ -1352,10 +1352,13 @@ constexpr int MS_FPW = (MS_FACES + 3) / 4;  // faces per wave
 #endif
 constexpr int MS_RA = FFD_MS_RA;  // serial phase: LDS reads in flight ahead of the adds
 #ifndef FFD_MS_DEFAULT
-#define FFD_MS_DEFAULT 1  // k_meanshift (1) or the overlapped k_meanshift3 (3)
+#define FFD_MS_DEFAULT 0  // 0: chosen per batch (launch_meanshift); 1 k_meanshift, 3 k_meanshift3, 4 k_meanshift4
 #endif
 #ifndef FFD_MS_UDEF
 #define FFD_MS_UDEF 4
+#endif
+#ifndef FFD_MS_K
+#define FFD_MS_K 4  // k_meanshift4: votes per lane per tile
 #endif
 #ifndef FFD_MS_PROBE
 #define FFD_MS_PROBE 0  // timing probes (bits): 1 = no serial phase, 2 = cheap weights, 4 = no early convergence
@@ -1679,6 +1682,144 @@ __global__ __launch_bounds__(256) void k_meanshift3(const FaceDesc* __restrict__
   }
 }
 
+// MeanShift, wave-independent form (FFD_MS_KERNEL=4, the default): each wave runs C chains (a chain =
+// one (face, landmark) vote list) through MeanShift::shift (MeanShift.hpp:41-135) on its own — no
+// workgroup barriers, so a wave's passes end when ITS chains converge and its tiles end at ITS longest
+// list.  A tile is 64 / C votes of each chain:
+//   terms  lane l computes the term (x*w, y*w, w) of vote l mod V of chain l / V (V = 64 / C) into the
+//          wave's LDS tile,
+//   sums   lane 3c + e (e = x, y, w) adds component e of chain c's V terms in list order,
+// in program order within the wave (LDS operations of one wave complete in order).  Every running sum
+// is the reference's sequential float sum bit for bit; the terms use ms_weight.
+template <int C, int K>
+__global__ __launch_bounds__(256) void k_meanshift4(const FaceDesc* __restrict__ faces, int n_faces, int tslots,
+                                                   int n_parts, float lamda, float lam_y, int max_iter, float stop,
+                                                   const Vote* __restrict__ votes, const int32_t* __restrict__ vote_counts,
+                                                   float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
+  constexpr int V = 64 / C, TV = V * K;  // term lanes per chain; votes per chain per tile
+  static_assert(3 * C <= 64 && V * C == 64, "chains per wave");
+  __shared__ float4 term[4][TV][C];  // per wave: [vote j][chain c] = (x*w, y*w, w, 0)
+  __shared__ float s_mean[4][C][2];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t n_chains = (int64_t)n_faces * NPARTS;
+  const int64_t ch0 = ((int64_t)blockIdx.x * 4 + wv) * C;
+  if (ch0 >= n_chains) return;  // whole waves; no workgroup barrier below
+  // term lanes: chain tc = lane / V, vote offset tk = lane % V
+  const int tc = lane / V, tk = lane - tc * V;
+  auto chain_info = [&](int c, int& cnt, int64_t& vb, int& valid) {
+    const int64_t g = ch0 + c;
+    cnt = 0;
+    vb = 0;
+    valid = 0;
+    if (g < n_chains) {
+      const int f = (int)(g / NPARTS), part = (int)(g - (int64_t)f * NPARTS);
+      const FaceDesc& fd = faces[f];
+      if (fd.valid) {
+        valid = 1;
+        cnt = part < n_parts ? vote_counts[(int64_t)f * NPARTS + part] : 0;
+        vb = fd.vote_off + (int64_t)part * tslots * fd.nmx * fd.nmy;
+      }
+    }
+  };
+  int t_cnt, t_valid;
+  int64_t t_vb;
+  chain_info(tc, t_cnt, t_vb, t_valid);
+  // sum lanes: chain sc = lane / 3, component se = lane % 3 (lanes >= 3C idle in the sums)
+  const int sc = lane / 3, se = lane - 3 * sc;
+  const bool sum_lane = lane < 3 * C;
+  int s_cnt = 0, s_valid = 0;
+  int64_t s_vb = 0;
+  if (sum_lane) chain_info(sc, s_cnt, s_vb, s_valid);
+  int live = t_valid;                    // the term lane's chain is live
+  int s_live = s_valid;                  // the sum lane's chain is live
+  float mx = 0.f, my = 0.f;              // term lane: its chain's current mean
+  float smx = 0.f, smy = 0.f;            // sum lane: its chain's current mean
+  const Vote* vp = votes + t_vb;
+  for (int pass = -1; pass < max_iter; pass++) {
+    if (__ballot(live) == 0ull) break;  // every chain of the wave converged
+    int lim = live ? t_cnt : 0;
+    int maxcnt = lim;
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) maxcnt = max(maxcnt, __shfl_xor(maxcnt, sh));
+    const int slim = s_live ? s_cnt : 0;
+    float acc = 0.f;
+    Vote v[K];
+#pragma unroll
+    for (int u = 0; u < K; u++) {
+      v[u] = Vote{0, 0, 0.f};
+      if (tk + V * u < lim) v[u] = vp[tk + V * u];
+    }
+    for (int k0 = 0; k0 < maxcnt; k0 += TV) {
+#pragma unroll
+      for (int u = 0; u < K; u++) {
+        const int k = k0 + tk + V * u;
+        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (k < lim) {
+          const float fx = (float)v[u].x, fy = (float)v[u].y;
+          const float w = pass < 0 ? v[u].w : ms_weight(mx, my, fx, fy, v[u].w, lamda, lam_y);
+          t = make_float4(fx * w, fy * w, w, 0.f);
+        }
+        if (k + TV < lim) v[u] = vp[k + TV];  // the next tile's votes, in flight during the sums
+        term[wv][tk + V * u][tc] = t;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (sum_lane) {
+        const int n = min(TV, slim - k0);
+        const float* tp = reinterpret_cast<const float*>(&term[wv][0][sc]) + se;
+        int j = 0;
+        for (; j + 4 <= n; j += 4) {  // LDS reads ahead of their in-order adds
+          const float a0 = tp[(j + 0) * C * 4], a1 = tp[(j + 1) * C * 4], a2 = tp[(j + 2) * C * 4], a3 = tp[(j + 3) * C * 4];
+          acc += a0;
+          acc += a1;
+          acc += a2;
+          acc += a3;
+        }
+        for (; j < n; j++) acc += tp[j * C * 4];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // chain sc's (x, y, w) sums sit on lanes 3sc, 3sc + 1, 3sc + 2
+    const int b = 3 * sc;
+    float ax = __shfl(acc, b), ay = __shfl(acc, b + 1), aw = __shfl(acc, b + 2);
+    if (sum_lane && se == 0 && s_live) {
+      if (aw > 0) { ax /= aw; ay /= aw; }
+      if (pass >= 0) {
+        const float ddx = ax - smx, ddy = ay - smy;
+        if (!(FFD_MS_PROBE & 4) && __builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) s_live = 0;
+      }
+      smx = ax;
+      smy = ay;
+      s_mean[wv][sc][0] = ax;
+      s_mean[wv][sc][1] = ay;
+    }
+    // liveness of every chain to its sum lanes (from lane 3c) and term lanes
+    s_live = __shfl(s_live, b) ;
+    smx = __shfl(smx, b);
+    smy = __shfl(smy, b);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    live = __shfl(s_live, 3 * tc) && t_valid;
+    mx = s_mean[wv][tc][0];
+    my = s_mean[wv][tc][1];
+  }
+  if (sum_lane && se == 0 && s_valid) {
+    const int64_t g = ch0 + sc;
+    const int f = (int)(g / NPARTS), part = (int)(g - (int64_t)f * NPARTS);
+    if (part < n_parts) {
+      ms_mean[((int64_t)f * NPARTS + part) * 2] = smx;
+      ms_mean[((int64_t)f * NPARTS + part) * 2 + 1] = smy;
+    }
+    const float inv = 1.0f / faces[f].scale;  // FaceForest.cpp:255-257
+    out[f].points[part][0] = part < n_parts ? cv_round((float)cv_round(smx) * inv) : 0;
+    out[f].points[part][1] = part < n_parts ? cv_round((float)cv_round(smy) * inv) : 0;
+  }
+}
+
 // ------------------------------------------------------------------ launch --
 void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s) {
   k_gray_resize<<<n, 256, 0, s>>>(faces, images, gray);
@@ -1847,10 +1988,14 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
                       int max_iter, float stop, const Vote* votes, const int32_t* vote_counts, float* ms_mean,
                       FaceOut* out, hipStream_t s) {
   (void)state;
-  static const int which = [] {
+  // k_meanshift (1) when the batch has chains for >= 4 of its workgroups per CU (C2: 2,048 workgroups,
+  // 2.45 ms, where k_meanshift4 takes 3.1 ms: its fp64 term chains run at lower occupancy); else the
+  // wave-independent k_meanshift4 (4) (C4, 10,240 chains of ~30 k votes: 16.2 -> 9.4 ms; small batches)
+  static const int forced = [] {
     const char* v = std::getenv("FFD_MS_KERNEL");
     return v ? std::atoi(v) : FFD_MS_DEFAULT;
   }();
+  const int which = forced ? forced : ((int64_t)n * NPARTS >= (int64_t)20 * 4 * 256 ? 1 : 4);
   const float lam_y = lamda == 10.f ? 1.f / 10.f : 0.f;  // the verified fast quotient (ffd_div_rcp)
   if (which == 1) {
     dim3 grid((n + MS_FACES - 1) / MS_FACES, NPARTS);
@@ -1858,20 +2003,41 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
                                             vote_counts, ms_mean, out);
     return;
   }
-  // overlapped form: the most chains per workgroup that still gives >= 512 workgroups (two per CU)
-  static const int ms_u = [] {
-    const char* v = std::getenv("FFD_MS_U");
-    return v ? std::atoi(v) : FFD_MS_UDEF;
-  }();
-  auto grid_for = [&](int F) { return dim3((n + F - 1) / F, NPARTS); };
-#define FFD_MS3(FV, UV) k_meanshift3<FV, UV><<<grid_for(FV), 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out)
   const int64_t lists = (int64_t)n * NPARTS;
-  if (ms_u == 8) {
-    if (lists >= 64 * 512) FFD_MS3(64, 8); else if (lists >= 32 * 512) FFD_MS3(32, 8); else FFD_MS3(16, 8);
-  } else {
-    if (lists >= 64 * 512) FFD_MS3(64, 4); else if (lists >= 32 * 512) FFD_MS3(32, 4); else FFD_MS3(16, 4);
-  }
+  if (which == 3) {  // overlapped form: the most chains per workgroup that still gives >= 512 workgroups
+    static const int ms_u = [] {
+      const char* v = std::getenv("FFD_MS_U");
+      return v ? std::atoi(v) : FFD_MS_UDEF;
+    }();
+    auto grid_for = [&](int F) { return dim3((n + F - 1) / F, NPARTS); };
+#define FFD_MS3(FV, UV) k_meanshift3<FV, UV><<<grid_for(FV), 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out)
+    if (ms_u == 8) {
+      if (lists >= 64 * 512) FFD_MS3(64, 8); else if (lists >= 32 * 512) FFD_MS3(32, 8); else FFD_MS3(16, 8);
+    } else {
+      if (lists >= 64 * 512) FFD_MS3(64, 4); else if (lists >= 32 * 512) FFD_MS3(32, 4); else FFD_MS3(16, 4);
+    }
 #undef FFD_MS3
+    return;
+  }
+  // wave-independent form: the most chains per wave (fewer idle lanes in the sums) that still gives
+  // >= FFD_MS_WAVES waves (default 4096: four per SIMD)
+  static const int64_t want = [] {
+    const char* v = std::getenv("FFD_MS_WAVES");
+    return v ? std::atoll(v) : (int64_t)4096;
+  }();
+  auto launch4 = [&](int C) {
+    const int64_t waves = (lists + C - 1) / C;
+    const dim3 grid((unsigned)((waves + 3) / 4));
+    switch (C) {
+      case 16: k_meanshift4<16, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out); break;
+      case 8: k_meanshift4<8, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out); break;
+      case 4: k_meanshift4<4, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out); break;
+      default: k_meanshift4<2, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out); break;
+    }
+  };
+  int C = 16;
+  while (C > 2 && (lists + C - 1) / C < want) C >>= 1;
+  launch4(C);
 }
 
 }  // namespace ffd
