@@ -23,7 +23,8 @@ constexpr int NGABOR = 35;
 constexpr int NPARTS = 10;
 constexpr int NHP_LABELS = 5;
 constexpr int MAX_TREES = 32;     // FFD_MAX_TREES
-constexpr int MAX_FACE_H = 600;   // scaled face height limit (box aspect h/w <= 4.8); taller -> FFD_ERR_UNSUPPORTED
+constexpr int MAX_FACE_H = 600;   // scaled faces up to this height stage whole into the Gabor kernels' LDS (box aspect h/w <= 4.8)
+constexpr int MAX_FACE_H_TALL = 4096;  // taller ones band by band (k_gabor_sep<..., TALL>) up to this (aspect 32.8); beyond: FFD_ERR_UNSUPPORTED
 constexpr uint32_t LEAF_BIT = 0x80000000u;
 
 // Flattened tree node (16 B), breadth-first per tree, children adjacent:

@@ -598,7 +598,7 @@ ffd_status ffd_host::fail(ffd_engine* e, ffd_status s, const std::string& msg) {
 // Fill the per-face descriptor (geometry + resize parameters) for a box on an image.  Returns the
 // face's status: FFD_OK, FFD_ERR_INVALID_ARGUMENT (box outside the image or an empty scaled face:
 // the reference's cv::Mat ROI / resize assertions throw) or FFD_ERR_UNSUPPORTED (scaled face taller
-// than MAX_FACE_H).  A face on which no head-pose patch fits runs like the reference: 0/0 head pose
+// than MAX_FACE_H_TALL).  A face on which no head-pose patch fits runs like the reference: 0/0 head pose
 // (NaN), trees 0..19 of forest 0, no votes, landmarks (0, 0); its channels are never read, so the
 // channel stage skips it.
 ffd_status ffd_host::make_desc(const ffd_engine* e, int64_t img_off, int iw, int ih, int stride, const ffd_rect& b,
@@ -613,7 +613,7 @@ ffd_status ffd_host::make_desc(const ffd_engine* e, int64_t img_off, int iw, int
     return FFD_ERR_INVALID_ARGUMENT;
   Geometry g = e->geometry(b.width, b.height);
   if (g.W < 1 || g.H < 1 || g.W > PITCH - 3) return FFD_ERR_INVALID_ARGUMENT;
-  if (g.H > MAX_FACE_H) {
+  if (g.H > MAX_FACE_H_TALL) {
     f.reject = FFD_ERR_UNSUPPORTED;
     return FFD_ERR_UNSUPPORTED;
   }
@@ -733,7 +733,7 @@ const char* ffd_status_string(int32_t s) {
     case FFD_ERR_OUT_OF_MEMORY: return "out of memory";
     case FFD_ERR_NOT_INITIALIZED: return "not initialised";
     case FFD_ERR_INTERNAL: return "internal error";
-    case FFD_ERR_UNSUPPORTED: return "unsupported face geometry (scaled face taller than 600 rows)";
+    case FFD_ERR_UNSUPPORTED: return "unsupported face geometry (scaled face taller than 4096 rows)";
     default: return "unknown status";
   }
 }
@@ -993,7 +993,7 @@ ffd_status ffd_get_trace(ffd_engine* e, int32_t index, ffd_trace* tr) {
 
 ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t W, int32_t H, uint32_t* out) {
   return guarded(e, [&]() -> ffd_status {
-    if (!gray_face || !out || W < 2 || H < 2 || W > PITCH - 3 || H > MAX_FACE_H)
+    if (!gray_face || !out || W < 2 || H < 2 || W > PITCH - 3 || H > MAX_FACE_H_TALL)
       return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     // the face itself is the "image" (copy mode): one BGR image whose gray equals the input
     e->sync_all();
@@ -1129,7 +1129,7 @@ const uint4* mp_table(ffd_engine* e, const ffd_multipart_option& o, bool& compac
 
 bool region_ok(int W, int H, const ffd_rect* r) {
   return r && r->x >= 0 && r->y >= 0 && r->width > 0 && r->height > 0 && (int64_t)r->x + r->width <= W &&
-         (int64_t)r->y + r->height <= H && r->width <= PITCH - 3 && r->height <= MAX_FACE_H;
+         (int64_t)r->y + r->height <= H && r->width <= PITCH - 3 && r->height <= MAX_FACE_H_TALL;
 }
 
 }  // namespace
@@ -1271,7 +1271,7 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* c
                                   int32_t* leaf_ids) {
   return guarded(e, [&]() -> ffd_status {
     if (!channels || (!patches_xy && n_patches) || (!tree_ids && n_trees) || (!leaf_ids && n_patches * n_trees) ||
-        W < 1 || H < 1 || W > PITCH - 3 || H > MAX_FACE_H || n_patches < 0 || n_trees < 0)
+        W < 1 || H < 1 || W > PITCH - 3 || H > MAX_FACE_H_TALL || n_patches < 0 || n_trees < 0)
       return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     if (kind != FFD_FOREST_HEADPOSE && kind != FFD_FOREST_FFD) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad forest kind");
     const int ntot = kind == FFD_FOREST_HEADPOSE ? e->hp_trees : e->n_forests * e->ntrees_per_forest;

@@ -452,7 +452,10 @@ template <int R> struct GSep {
   static constexpr int V_OFF = 4, H_OFF = 4 + 12 * (R + 1);
 };
 
-template <int W, bool EXACT>
+// TALL: the instance for faces taller than MAX_FACE_H (box aspect h/w > 4.8), whose padded face does not
+// fit the LDS: each band stages only its GS_BY + 2R rows (4x re-staging at 25x25; such faces are rare).
+// Each instance skips the other's faces.
+template <int W, bool EXACT, bool TALL>
 __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __restrict__ faces,
                                                           const uint8_t* __restrict__ gray,
                                                           const float* __restrict__ coef,
@@ -469,7 +472,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
   __shared__ float vg[GS_BY * C::VP];
   __shared__ f2 vq[4][GS_BY * C::VP];
   const FaceDesc fd = faces[blockIdx.x];
-  if (!fd.valid || fd.nochan) return;
+  if (!fd.valid || fd.nochan || (fd.H > MAX_FACE_H) != TALL) return;
   if (EXACT && !redo[blockIdx.x]) return;  // the fast instance's mag_sqrt was exact for this face
   uint32_t tiny = 0xFFFFFFFFu;
   const int FW = fd.W, FH = fd.H, NPC = FW + 2 * R;
@@ -482,13 +485,13 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
 #pragma unroll
   for (int o = 0; o < 7; o++) { mn[o] = 0xFFFFFFFFu; mx[o] = 0u; }
 
-  {  // the whole reflect-101 padded face, once: (row, 4-column group) items, u32 LDS stores; rows up
-     // to the last band's end (ceil(FH / GS_BY) * GS_BY + 2R: every row the V pass reads is staged)
+  // the reflect-101 padded face rows [r0, r0 + rows) (padded-row index: face row + R) to LDS rows
+  // [0, rows): (row, 4-column group) items, u32 LDS stores
+  auto stage_rows = [&](int r0, int rows) {
     constexpr int NQ = C::GP / 4;
-    const int rows = (FH + GS_BY - 1) / GS_BY * GS_BY + 2 * R;
     for (int i = tid; i < rows * NQ; i += GS_THREADS) {
       const int r = i / NQ, j = i - r * NQ;
-      const uint8_t* row = g + reflect101(r - R, FH) * PITCH;
+      const uint8_t* row = g + reflect101(r0 + r - R, FH) * PITCH;
       uint32_t v = 0;
 #pragma unroll
       for (int e = 0; e < 4; e++) {
@@ -500,17 +503,24 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
       }
       *reinterpret_cast<uint32_t*>(&gface[r * C::GP + 4 * j]) = v;
     }
-  }
+  };
+  // the whole padded face, once: rows up to the last band's end (ceil(FH / GS_BY) * GS_BY + 2R: every
+  // row the V pass reads is staged)
+  if (!TALL) stage_rows(0, (FH + GS_BY - 1) / GS_BY * GS_BY + 2 * R);
 
 #pragma unroll 1
   for (int y0 = 0; y0 < (FFD_GABOR_PROBE == 5 ? 0 : FH); y0 += GS_BY) {  // probe 5: epilogue only
     __syncthreads();  // the face is staged; the previous H pass is done with vg / vq
+    if (TALL) {       // (the previous V pass is done with gface: the barrier before the H pass)
+      stage_rows(y0, GS_BY + 2 * R);
+      __syncthreads();
+    }
     // ---- V pass
 #pragma unroll 1
     for (int i = tid; i < (FFD_GABOR_PROBE == 3 ? 0 : GS_BY * C::SC); i += GS_THREADS) {
       const int r = i / C::SC, cc = i - r * C::SC;
       if (cc >= NPC) continue;
-      const uint8_t* col = &gface[(y0 + r + R) * C::GP + cc];
+      const uint8_t* col = &gface[((TALL ? 0 : y0) + r + R) * C::GP + cc];
       float vgv = 0.f;
       f2 vqv[4];
 #pragma unroll
@@ -1839,7 +1849,10 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t
   int* rd = redo + (int64_t)nu * n;  // one flag array per scale: the scales may run on fork streams
   for (int exact = 0; exact < 2; exact++) {
 #define FFD_GABOR_LAUNCH(WV, RV)                                                                              \
-  (exact ? k_gabor_sep<WV, true> : k_gabor_sep<WV, false>)<<<n, GS_THREADS, gabor_face_lds(RV, max_h), s>>>(faces, gray, c, \
+  (exact ? k_gabor_sep<WV, true, false> : k_gabor_sep<WV, false, false>)<<<n, GS_THREADS, gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, \
+                                                                                                  mag, chan, rd, force_exact); \
+  if (max_h > MAX_FACE_H)                                                                                        \
+    (exact ? k_gabor_sep<WV, true, true> : k_gabor_sep<WV, false, true>)<<<n, GS_THREADS, (GS_BY + 2 * RV) * ((PITCH + 2 * RV + 3) / 4 * 4), s>>>(faces, gray, c, \
                                                                                                   mag, chan, rd, force_exact)
     switch (nu) {
       case 4: FFD_GABOR_LAUNCH(25, 12); break;
@@ -1925,10 +1938,10 @@ void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, TravShape g
 
 hipError_t set_gabor_lds_limit(int bytes) {
   hipError_t e = hipSuccess;
-  const void* fns[] = {(const void*)k_gabor_sep<9, false>,  (const void*)k_gabor_sep<13, false>,
-                       (const void*)k_gabor_sep<19, false>, (const void*)k_gabor_sep<25, false>,
-                       (const void*)k_gabor_sep<9, true>,   (const void*)k_gabor_sep<13, true>,
-                       (const void*)k_gabor_sep<19, true>,  (const void*)k_gabor_sep<25, true>};
+  const void* fns[] = {(const void*)k_gabor_sep<9, false, false>,  (const void*)k_gabor_sep<13, false, false>,
+                       (const void*)k_gabor_sep<19, false, false>, (const void*)k_gabor_sep<25, false, false>,
+                       (const void*)k_gabor_sep<9, true, false>,   (const void*)k_gabor_sep<13, true, false>,
+                       (const void*)k_gabor_sep<19, true, false>,  (const void*)k_gabor_sep<25, true, false>};
   for (const void* f : fns) {
     hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (r != hipSuccess) e = r;

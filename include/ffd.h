@@ -47,7 +47,7 @@ typedef enum {
   FFD_ERR_OUT_OF_MEMORY = 4,
   FFD_ERR_NOT_INITIALIZED = 5,
   FFD_ERR_INTERNAL = 6,
-  FFD_ERR_UNSUPPORTED = 7    /* per face: scaled face taller than the engine supports (box h/w > 4.8) */
+  FFD_ERR_UNSUPPORTED = 7    /* per face: scaled face taller than 4,096 rows (box h/w > 32.8; the reference has no limit) */
 } ffd_status;
 
 /* Human-readable meaning of a status code (call or per-face). */

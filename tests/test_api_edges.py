@@ -4,7 +4,8 @@
   sample's channels, whole sample and a sub-region (face_bbox with a non-zero origin);
 * edge-case boxes the reference accepts: a face on which no head-pose patch fits (the reference
   averages 0/0: NaN head pose, trees 0..19 of forest 0, landmarks (0, 0)), W = 124 rounding, a tall
-  face (125 x 375); and the per-face statuses of the boxes it rejects;
+  face (125 x 375), faces taller than the whole-face Gabor staging (125 x 625, 125 x 1500); and the
+  per-face statuses of the boxes it rejects;
 * the multi-device entry points on the one device a box has (ffd_group_*, ffd_engine_join +
   ffd_gather_faces through RCCL);
 * the engine's non-default configurations (3 x 3 patch blocks, FFD_CHANNEL_STREAMS=2, two streams, every
@@ -65,9 +66,23 @@ def test_edge_boxes_match_oracle(engine, oracle_mod, fixtures):
             assert np.float32(f.headpose) == np.float32(ref["headpose"]), box
 
 
+def test_very_tall_faces_match_oracle(engine, oracle_mod, fixtures):
+    """Scaled faces taller than MAX_FACE_H (600 rows) run through the band-staged Gabor instance
+    (k_gabor_sep<..., TALL>): a 125 x 625 face in one batch with an ordinary one."""
+    img = fixtures["images"][0]
+    boxes = [(61, 72, 130, 130), (40, 10, 48, 240)]
+    faces = engine.analyzeFaces([img], boxes, [0] * len(boxes))
+    for f, box in zip(faces, boxes):
+        ref, _ = oracle_mod.analyze_face(img, box, threads=8)
+        assert f.status == 0, (box, f.status)
+        assert f.n_trees == ref["n_trees"], box
+        assert np.array_equal(f.ffd_cordinates, ref["points"]), box
+        assert np.float32(f.headpose) == np.float32(ref["headpose"]), box
+
+
 def test_rejected_boxes_get_truthful_status(engine, fixtures):
     img = fixtures["images"][0]
-    boxes = [(100, 5, 20, 240), (200, 200, 100, 100), (-1, 0, 50, 50), (61, 72, 130, 130), (10, 10, 200, 1)]
+    boxes = [(100, 5, 6, 240), (200, 200, 100, 100), (-1, 0, 50, 50), (61, 72, 130, 130), (10, 10, 200, 1)]
     faces = engine.analyzeFaces([img], boxes, [0] * len(boxes))
     assert [f.status for f in faces] == [ffd.STATUS_UNSUPPORTED, ffd.STATUS_INVALID_ARGUMENT,
                                         ffd.STATUS_INVALID_ARGUMENT, 0, ffd.STATUS_INVALID_ARGUMENT]
