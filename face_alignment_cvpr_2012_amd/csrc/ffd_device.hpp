@@ -73,7 +73,9 @@ struct FaceDesc {
                           //    no head-pose patch fits, the reference then averages 0/0)
   int32_t reject;         // ffd_status of a rejected face
   int32_t vox, voy;       // patch-grid origin in the image sample (estimateFacialFeatures' face_bbox)
-  int32_t pad_;
+  int32_t fint;           // 1: an integral value may reach 2^24 (255 W H >= 2^24, a tall face), where the
+                          //    reference's CV_32F integral rounds: float-accumulated integrals, and the
+                          //    traversals' exact walker k_walk_fint instead of k_traverse
 };
 
 struct FaceOut {          // == ffd_face

@@ -47,9 +47,10 @@ void widen_integrals(const uint16_t* J, int64_t plane, int W, int H, uint32_t* o
       uint32_t run = 0;
       o[(y + 1) * ow] = 0;
       for (int x = 0; x < W; x++) {
-        const uint16_t v = (uint16_t)(j[(y + 1) * PITCH + x + 1] - j[y * PITCH + x + 1] - j[(y + 1) * PITCH + x] +
-                                      j[y * PITCH + x]);
-        run += v;
+        // (signed: a float-integral face's rounded values have second differences in [-16, 271])
+        const int16_t v = (int16_t)(uint16_t)(j[(y + 1) * PITCH + x + 1] - j[y * PITCH + x + 1] - j[(y + 1) * PITCH + x] +
+                                              j[y * PITCH + x]);
+        run += (uint32_t)(int32_t)v;
         o[(y + 1) * ow + x + 1] = o[y * ow + x + 1] + run;
       }
     }
@@ -60,7 +61,7 @@ void widen_integrals(const uint16_t* J, int64_t plane, int W, int H, uint32_t* o
 int blocks_per_face(const std::vector<FaceDesc>& fds, bool hp, TravShape g) {
   int m = 0;
   for (const auto& f : fds)
-    if (f.valid) {
+    if (f.valid && !f.fint) {  // float-integral faces are walked by k_walk_fint
       const int nx = hp ? f.nhx : f.nmx, ny = hp ? f.nhy : f.nmy;
       m = std::max(m, ((nx + g.gx - 1) / g.gx) * ((ny + g.gy - 1) / g.gy));
     }
@@ -476,10 +477,12 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   // one channel plane stride for the whole batch (the traversal's window staging assumes it)
   int64_t plane = PITCH;
   int max_h = 1;
+  bool any_fint = false;
   for (const auto& f : fds)
     if (f.valid) {
       plane = std::max(plane, (int64_t)(f.H + 1) * PITCH);
       max_h = std::max(max_h, f.H);
+      any_fint |= f.fint != 0;
     }
   for (auto& f : fds) {
     if (!f.valid) continue;
@@ -541,6 +544,9 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
                     hp_tops.as<uint4>(), hp_topi.as<uint32_t>(), trav_top_max, hp_far.as<uint32_t>(), nullptr,
                     hp_trees, desc.hp_option.step_size, desc.hp_option.step_size, plane, w.chan.as<uint16_t>(),
                     w.hpleaf.as<int32_t>(), trav_wg, TRAV_LDS_CAP, st);
+    if (any_fint)
+      launch_walk_fint(true, dfd, n, hp_nodes.as<uint4>(), hp_roots.as<int32_t>(), hp_trees, nullptr,
+                       desc.hp_option.step_size, desc.hp_option.step_size, w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), st);
   });
   stage(8, st, [&] {
     launch_hp_pose(dfd, n, w.hpleaf.as<int32_t>(), hp_m.as<float>(), hp_trees, n_forests, ntrees_per_forest,
@@ -551,6 +557,9 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
                     mp_tops.as<uint4>(), mp_topi.as<uint32_t>(), trav_top_max, mp_far.as<uint32_t>(),
                     w.state.as<HpState>(), 0, desc.mp_option.step_size, mp_step_y(), plane, w.chan.as<uint16_t>(),
                     w.mpleaf.as<int32_t>(), trav_wg, TRAV_LDS_CAP, st);
+    if (any_fint)
+      launch_walk_fint(false, dfd, n, mp_nodes.as<uint4>(), mp_roots.as<int32_t>(), 0, w.state.as<HpState>(),
+                       desc.mp_option.step_size, mp_step_y(), w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), st);
   });
   const int n_parts = std::min(desc.mp_option.num_parts, NPARTS);
   stage(10, st, [&] {
@@ -618,6 +627,7 @@ ffd_status ffd_host::make_desc(const ffd_engine* e, int64_t img_off, int iw, int
     return FFD_ERR_UNSUPPORTED;
   }
   f.W = g.W; f.H = g.H; f.scale = g.scale;
+  f.fint = (int64_t)255 * g.W * g.H >= (int64_t)1 << 24 ? 1 : 0;  // an integral value may reach 2^24
   f.nhx = g.nhx; f.nhy = g.nhy; f.nmx = g.nmx; f.nmy = g.nmy;
   f.nochan = (f.nhx * f.nhy == 0 || g.W < 2 || g.H < 2) ? 1 : 0;
   if (g.W == b.width && g.H == b.height) {
@@ -1006,6 +1016,7 @@ ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t
     FaceDesc f;
     std::memset(&f, 0, sizeof(f));
     f.img_w = W; f.img_h = H; f.img_stride = 3 * W; f.bw = W; f.bh = H; f.W = W; f.H = H;
+    f.fint = (int64_t)255 * W * H >= (int64_t)1 << 24 ? 1 : 0;  // OpenCV's float integral rounds past 2^24
     f.scale = 1.f; f.mode = 0; f.valid = 1;
     f.plane = (int64_t)(H + 1) * PITCH;
     w.gray.ensure((size_t)H * PITCH + 256);
@@ -1064,13 +1075,18 @@ FaceDesc stage_sample(ffd_engine* e, Workspace& w, const uint32_t* ch, int W, in
   f.hp_off = f.mp_off = f.vote_off = f.ch_off = 0;
   std::vector<uint16_t> J((size_t)NCH * f.plane, 0);
   const size_t ow = (size_t)W + 1, oplane = ((size_t)H + 1) * ow;
+  uint32_t vmax = 0;
   for (int c = 0; c < NCH; c++) {
     const uint32_t* I = ch + c * oplane;
     for (int y = 0; y <= rh; y++)
-      for (int x = 0; x <= rw; x++)
+      for (int x = 0; x <= rw; x++) {
+        const uint32_t v = I[(r.y + y) * ow + r.x + x];
+        vmax = std::max(vmax, v);
         J[(size_t)c * f.plane + (size_t)y * PITCH + x] =
-            (uint16_t)(I[(r.y + y) * ow + r.x + x] - I[r.y * ow + r.x + x] - I[(r.y + y) * ow + r.x] + I[r.y * ow + r.x]);
+            (uint16_t)(v - I[r.y * ow + r.x + x] - I[(r.y + y) * ow + r.x] + I[r.y * ow + r.x]);
+      }
   }
+  f.fint = vmax >= (1u << 24) ? 1 : 0;  // float-rounded integrals (CV_32F past 2^24): k_walk_fint
   w.chan.ensure(J.size() * 2 + 512);  // slack: traversal windows read past a row
   HIP_CHECK(hipMemcpyAsync(w.chan.p, J.data(), J.size() * 2, hipMemcpyHostToDevice, w.stream));
   w.hpleaf.ensure(((size_t)e->hp_trees * f.nhx * f.nhy + 64) * 4);
@@ -1159,6 +1175,9 @@ ffd_status ffd_estimate_headpose(ffd_engine* e, const uint32_t* channels, int32_
                     e->hp_topi.as<uint32_t>(), e->trav_top_max, e->hp_far.as<uint32_t>(), nullptr, e->hp_trees,
                     o.step_size, o.step_size, f.plane, w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), e->trav_wg,
                     TRAV_LDS_CAP, w.stream);
+    if (f.fint)
+      launch_walk_fint(true, dfd, 1, e->hp_nodes.as<uint4>(), e->hp_roots.as<int32_t>(), e->hp_trees, nullptr, o.step_size,
+                       o.step_size, w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), w.stream);
     launch_hp_pose(dfd, 1, w.hpleaf.as<int32_t>(), hp_m, e->hp_trees, e->n_forests, e->ntrees_per_forest,
                    w.state.as<HpState>(), e->out.as<FaceOut>(), w.stream);
     HIP_CHECK(hipGetLastError());
@@ -1206,6 +1225,9 @@ ffd_status ffd_estimate_facial_features(ffd_engine* e, const uint32_t* channels,
                     e->mp_topi.as<uint32_t>(), e->trav_top_max, e->mp_far.as<uint32_t>(), w.state.as<HpState>(), 0,
                     o.step_size, step_y, f.plane, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), e->trav_wg,
                     TRAV_LDS_CAP, w.stream);
+    if (f.fint)
+      launch_walk_fint(false, dfd, 1, e->mp_nodes.as<uint4>(), e->mp_roots.as<int32_t>(), 0, w.state.as<HpState>(),
+                       o.step_size, step_y, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), w.stream);
     launch_votes(dfd, 1, w.mpleaf.as<int32_t>(), rec, compact, bias_x, bias_y, w.state.as<HpState>(), MAX_TREES,
                  o.step_size, step_y, e->patch / 2, n_parts, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), w.stream);
     // FaceForest::estimateFacialFeatures shifts with a default MeanShiftOption (FaceForest.cpp:89-92)

@@ -151,23 +151,39 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 
 // The scan of one channel by one wave.  value(y, b) returns the u8 values of columns 2l, 2l+1 of
 // row y for b = 0..RB-1 batches (all of a batch's loads are issued before its scans).
+// One integral row from this row's values v0, v1 (columns 2l, 2l + 1): exact (c0, c1: running column
+// sums, the row's entries by a prefix scan of them) or, for a float-integral face (FaceDesc::fint), as
+// OpenCV's integral_ in float (f0, f1: the entries of the row above; + this row's prefix s, rounded):
+// the same values until one reaches 2^24.  Returns entries 2l | 2l + 1 << 16, modulo 2^16 each.
+__device__ __forceinline__ uint32_t integral_row(bool fl, uint32_t v0, uint32_t v1, uint32_t& c0, uint32_t& c1,
+                                                 float& f0, float& f1) {
+  if (!fl) {
+    c0 += v0;
+    c1 += v1;
+    const uint32_t s2 = c0 + c1;
+    const uint32_t excl = wave_incl_scan(s2) - s2;
+    return (excl & 0xFFFFu) | ((excl + c0) << 16);
+  }
+  const uint32_t p = v0 + v1, s = wave_incl_scan(p) - p;  // this row's prefix up to column 2l - 1 (exact)
+  f0 = f0 + (float)s;
+  f1 = f1 + (float)(s + v0);
+  return ((uint32_t)f0 & 0xFFFFu) | ((uint32_t)f1 << 16);
+}
+
 template <int RB = 8, class RowFn>
-__device__ __forceinline__ void integral_scan(uint16_t* __restrict__ out, int W, int H, int lane, RowFn row_values) {
+__device__ __forceinline__ void integral_scan(uint16_t* __restrict__ out, int W, int H, int lane, bool fl, RowFn row_values) {
   for (int x = lane; x <= W; x += 64) out[x] = 0;  // row 0 of the integral image
   uint32_t c0 = 0, c1 = 0;
+  float f0 = 0.f, f1 = 0.f;
   for (int y0 = 0; y0 < H; y0 += RB) {
     uint32_t v0[RB], v1[RB];
     row_values(y0, v0, v1);
 #pragma unroll
     for (int b = 0; b < RB; b++) {
       if (y0 + b >= H) break;
-      c0 += v0[b];
-      c1 += v1[b];
-      const uint32_t s2 = c0 + c1;
-      const uint32_t excl = wave_incl_scan(s2) - s2;
       uint32_t* r = reinterpret_cast<uint32_t*>(out + (int64_t)(y0 + b + 1) * PITCH);
       // entries >= W+1 land in the row's pitch padding (never read by a patch)
-      r[lane] = (excl & 0xFFFFu) | ((excl + c0) << 16);
+      r[lane] = integral_row(fl, v0[b], v1[b], c0, c1, f0, f1);
     }
   }
 }
@@ -183,7 +199,7 @@ __global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ f
   const int c = wv == 0 ? 0 : 35 + wv;
   const int W = fd.W, H = fd.H, x0 = 2 * lane;
   const uint8_t* g = gray + fd.gray_off;
-  integral_scan(chan + fd.ch_off + (int64_t)c * fd.plane, W, H, lane, [&](int y0, uint32_t* v0, uint32_t* v1) {
+  integral_scan(chan + fd.ch_off + (int64_t)c * fd.plane, W, H, lane, fd.fint != 0, [&](int y0, uint32_t* v0, uint32_t* v1) {
 #pragma unroll
     for (int b = 0; b < 8; b++) {
       const int y = min(y0 + b, H - 1);
@@ -289,6 +305,8 @@ __device__ __forceinline__ void gabor_normalise_integrate(const FaceDesc& fd, in
     uint16_t* out = chan + fd.ch_off + (int64_t)(1 + nu * 7 + o) * fd.plane;
     for (int x = lane; x <= FW; x += 64) out[x] = 0;  // row 0 of the integral image
     uint32_t c0 = 0, c1 = 0;
+    float f0 = 0.f, f1 = 0.f;
+    const bool fl = fd.fint != 0;
     auto load = [&](int y0, rowbuf& mv) {
 #pragma unroll
       for (int b = 0; b < RB; b++)
@@ -298,12 +316,10 @@ __device__ __forceinline__ void gabor_normalise_integrate(const FaceDesc& fd, in
 #pragma unroll
       for (int b = 0; b < RB; b++) {
         if (y0 + b >= FH) break;
-        c0 += (x0 < FW) ? gabor_quantise(mv[b].x, sf, hf) : 0u;
-        c1 += (x0 + 1 < FW) ? gabor_quantise(mv[b].y, sf, hf) : 0u;
-        const uint32_t s2 = c0 + c1;
-        const uint32_t excl = wave_incl_scan(s2) - s2;
+        const uint32_t q0 = (x0 < FW) ? gabor_quantise(mv[b].x, sf, hf) : 0u;
+        const uint32_t q1 = (x0 + 1 < FW) ? gabor_quantise(mv[b].y, sf, hf) : 0u;
         // entries >= W+1 land in the row's pitch padding (never read by a patch)
-        reinterpret_cast<uint32_t*>(out + (int64_t)(y0 + b + 1) * PITCH)[lane] = (excl & 0xFFFFu) | ((excl + c0) << 16);
+        reinterpret_cast<uint32_t*>(out + (int64_t)(y0 + b + 1) * PITCH)[lane] = integral_row(fl, q0, q1, c0, c1, f0, f1);
       }
     };
     rowbuf A, B;
@@ -670,6 +686,9 @@ __device__ __forceinline__ int node_off(uint32_t enc, int ld) {
   return (int)__umul24(enc >> 7, (unsigned)ld) + (int)(enc & 127u);
 }
 
+#ifndef FFD_TRAV_VOFF_ARRAY
+#define FFD_TRAV_VOFF_ARRAY 0
+#endif
 #ifndef FFD_TRAV_MID_ALWAYS
 #define FFD_TRAV_MID_ALWAYS 1  // 0: middle row only for area > 257 (exec-masked; measured slower: FFD 8.42 -> 8.52 ms)
 #endif
@@ -831,7 +850,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     B.px0 = B.xi0 * step;
     B.py0 = B.yi0 * stepy;
     B.T = 0;
-    if (fd.valid && B.nx > 0 && b < gbx * gby) {
+    if (fd.valid && !fd.fint && B.nx > 0 && b < gbx * gby) {  // (float-integral faces: k_walk_fint)
       B.ok = true;
       B.T = HP ? A.ntrees_hp : A.hp_state[B.f].n_trees;
     }
@@ -939,6 +958,23 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     const int s0 = tid - NW;
     const int dq = NS % nq, dr = (NS / nq) % WH, dc = NS / (nq * WH);
     const int q0 = s0 % nq, r0 = (s0 / nq) % WH, c0 = s0 / (nq * WH);
+#if FFD_TRAV_VOFF_ARRAY  // round-2 form: the U offsets precomputed once (spills the stager role at U = 22)
+    int voffs[U];
+    {
+      int q = q0, r = r0, c = c0;
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        voffs[u] = min(c, NCH) * A.plane * 2 + r * (PITCH * 2) + q * CB;
+        q += dq;
+        int cr = q >= nq;
+        q -= cr ? nq : 0;
+        r += dr + cr;
+        cr = r >= WH;
+        r -= cr ? WH : 0;
+        c += dc + cr;
+      }
+    }
+#endif
     auto prefetch = [&](const Blk& B) {
       if (!B.ok) return;
       const FaceDesc& fd = A.faces[B.f];
@@ -975,7 +1011,11 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       int q = q0, r = r0, c = c0;
 #pragma unroll
       for (int u = 0; u < U; u++) {
+#if FFD_TRAV_VOFF_ARRAY
+        const int voff = voffs[u];
+#else
         const int voff = min(c, NCH) * plane_b + r * (PITCH * 2) + q * CB;
+#endif
         if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, base_b, 0);
         else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, base_b, 0);
         q += dq;
@@ -1045,6 +1085,54 @@ __global__ void k_eval_patches(const uint4* __restrict__ nodes, const int32_t* _
   const int p = i / n_trees, t = i % n_trees;
   const uint16_t* I = chan + patches[2 * p + 1] * PITCH + patches[2 * p];
   leaf_ids[i] = (int32_t)walk16(nodes, (uint32_t)roots[tree_ids[t]], I, plane);
+}
+
+// The traversals of float-integral faces (FaceDesc::fint: the reference's CV_32F integral may round,
+// FeatureChannelFactory.hpp:46-57 with OpenCV's float integral_): evalTest (ImageSample.cpp:48-63) on
+// the rounded integral values, (int)((float)(d - b - c + a) / (float)area).  A rectangle half's mod-2^16
+// combination is recovered in the window [-128, 65407]: its true value is the exact half sum (<= 61,710)
+// plus the rounding errors of at most 11 row additions in each of two columns (each <= 4 below 2^27):
+// |error| <= 88.  Sums may then be negative or exceed 255 area, so the quotient is an IEEE division
+// with truncation, as in the reference.  Grid (slices, faces); other faces exit at once.
+__device__ __forceinline__ int rect_mean_fint(const uint16_t* __restrict__ I, int ld, int w, int h) {
+  const int h1 = h >> 1;
+  const uint32_t a = I[0], b = I[w], c = I[h1 * ld], d = I[h1 * ld + w], e = I[h * ld], f = I[h * ld + w];
+  auto half = [](uint32_t v) {
+    v &= 0xFFFFu;
+    return (int)v - (v >= 0xFF80u ? 65536 : 0);
+  };
+  const int R = half(d - c - b + a) + half(f - e - d + c);
+  return (int)((float)R / (float)(w * h));
+}
+
+template <bool HP>
+__global__ __launch_bounds__(256) void k_walk_fint(const FaceDesc* __restrict__ faces, const uint4* __restrict__ nodes,
+                                                  const int32_t* __restrict__ roots, int ntrees_hp,
+                                                  const HpState* __restrict__ state, int step, int step_y,
+                                                  const uint16_t* __restrict__ chan, int32_t* __restrict__ leaf_out) {
+  const int f = blockIdx.y;
+  const FaceDesc& fd = faces[f];
+  if (!fd.valid || !fd.fint) return;
+  const int nx = HP ? fd.nhx : fd.nmx, ny = HP ? fd.nhy : fd.nmy;
+  const int T = HP ? ntrees_hp : state[f].n_trees;
+  const int items = nx * ny * T;
+  int32_t* out = leaf_out + (HP ? fd.hp_off : fd.mp_off);
+  const uint16_t* base = chan + fd.ch_off;
+  for (int it = blockIdx.x * 256 + threadIdx.x; it < items; it += gridDim.x * 256) {
+    const int p = it / T, t = it - p * T;  // p = xi * ny + yi: the reference's patch order
+    const int xi = p / ny, yi = p - xi * ny;
+    const uint16_t* P = base + (yi * step_y) * PITCH + xi * step;
+    uint32_t node = (uint32_t)roots[HP ? t : state[f].trees[t]];
+    uint4 nd = nodes[node];
+    while (!(nd.x & LEAF_BIT)) {
+      const uint16_t* I = P + (int64_t)(nd.y & 63u) * fd.plane;
+      const int p1 = rect_mean_fint(I + node_off(nd.w & 0xFFFFu, PITCH), PITCH, (nd.y >> 6) & 31u, (nd.y >> 11) & 31u);
+      const int p2 = rect_mean_fint(I + node_off(nd.w >> 16, PITCH), PITCH, (nd.y >> 16) & 31u, (nd.y >> 21) & 31u);
+      node = nd.x + ((p1 - p2) <= (int)nd.z ? 0u : 1u);
+      nd = nodes[node];
+    }
+    out[it] = (int32_t)(nd.x & ~LEAF_BIT);
+  }
 }
 
 // -------------------------------------------------- head pose + tree choice --
@@ -1959,6 +2047,14 @@ hipError_t set_traverse_lds_limit(int bytes) {
   FFD_TRAV_SHAPES(FFD_TRAV_ATTR)
 #undef FFD_TRAV_ATTR
   return e;
+}
+
+void launch_walk_fint(bool hp, const FaceDesc* faces, int n, const uint4* nodes, const int32_t* roots, int ntrees_hp,
+                      const HpState* state, int step, int step_y, const uint16_t* chan, int32_t* leaf_out, hipStream_t s) {
+  if (n <= 0) return;
+  const dim3 grid(64, n);
+  if (hp) k_walk_fint<true><<<grid, 256, 0, s>>>(faces, nodes, roots, ntrees_hp, state, step, step_y, chan, leaf_out);
+  else k_walk_fint<false><<<grid, 256, 0, s>>>(faces, nodes, roots, ntrees_hp, state, step, step_y, chan, leaf_out);
 }
 
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,

@@ -49,6 +49,9 @@ void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, TravShape g
                      int step, int step_y, int64_t plane, const uint16_t* chan, int32_t* leaf_out, int n_wg,
                      int lds_cap, hipStream_t s);
 hipError_t set_traverse_lds_limit(int bytes);
+// the traversals of float-integral faces (FaceDesc::fint) over the 16-B node arrays
+void launch_walk_fint(bool hp, const FaceDesc* faces, int n, const uint4* nodes, const int32_t* roots, int ntrees_hp,
+                      const HpState* state, int step, int step_y, const uint16_t* chan, int32_t* leaf_out, hipStream_t s);
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
                          const int32_t* patches, int n_patches, const uint16_t* chan, int64_t plane,
                          int32_t* leaf_ids, hipStream_t s);

@@ -299,16 +299,19 @@ void cv_resize(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, in
   }
 }
 
-// cv::integral(img, sum, CV_32F): exact integer sums (< 2^24), stored as u32.
+// cv::integral(img, sum, CV_32F): OpenCV 2.4.9 integral_<uchar, float, double> accumulates in float,
+// s += src[x]; sum[x] = sum[x - sumstep] + s (every add rounded), so once a value passes 2^24 (a tall
+// face: 255 W H >= 2^24) the integral is rounded; below that it is the exact integer sum.  Stored as
+// u32 (every value is an integer-valued float < 2^32).
 void integral(const uint8_t* img, int w, int h, uint32_t* out) {
   int W1 = w + 1;
   for (int x = 0; x <= w; x++) out[x] = 0;
   for (int y = 0; y < h; y++) {
-    uint32_t s = 0;
+    float s = 0;
     out[(y + 1) * W1] = 0;
     for (int x = 0; x < w; x++) {
       s += img[y * w + x];
-      out[(y + 1) * W1 + x + 1] = out[y * W1 + x + 1] + s;
+      out[(y + 1) * W1 + x + 1] = (uint32_t)((float)out[y * W1 + x + 1] + s);
     }
   }
 }

@@ -68,9 +68,11 @@ def test_edge_boxes_match_oracle(engine, oracle_mod, fixtures):
 
 def test_very_tall_faces_match_oracle(engine, oracle_mod, fixtures):
     """Scaled faces taller than MAX_FACE_H (600 rows) run through the band-staged Gabor instance
-    (k_gabor_sep<..., TALL>): a 125 x 625 face in one batch with an ordinary one."""
+    (k_gabor_sep<..., TALL>), and faces whose integrals may reach 2^24 (255 W H >= 2^24), where the
+    reference's CV_32F integral rounds, through float-accumulated integrals and the exact walker
+    k_walk_fint: 125 x 1500, 125 x 625 and 125 x 3125 faces in one batch with an ordinary one."""
     img = fixtures["images"][0]
-    boxes = [(61, 72, 130, 130), (40, 10, 48, 240)]
+    boxes = [(100, 5, 20, 240), (61, 72, 130, 130), (40, 10, 48, 240), (120, 0, 10, 250)]
     faces = engine.analyzeFaces([img], boxes, [0] * len(boxes))
     for f, box in zip(faces, boxes):
         ref, _ = oracle_mod.analyze_face(img, box, threads=8)
