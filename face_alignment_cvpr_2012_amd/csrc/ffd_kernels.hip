@@ -687,7 +687,7 @@ __device__ __forceinline__ int node_off(uint32_t enc, int ld) {
 }
 
 #ifndef FFD_TRAV_VOFF_ARRAY
-#define FFD_TRAV_VOFF_ARRAY 0
+#define FFD_TRAV_VOFF_ARRAY 1  // precomputed staging offsets (0: rebuilt per block from 6 registers, no spill: FFD 8.39 -> 8.67 ms)
 #endif
 #ifndef FFD_TRAV_MID_ALWAYS
 #define FFD_TRAV_MID_ALWAYS 1  // 0: middle row only for area > 257 (exec-masked; measured slower: FFD 8.42 -> 8.52 ms)
