@@ -75,7 +75,7 @@ def source_digest():
     return h.hexdigest()[:16]
 
 
-def measured_traffic(stage, faces_per_launch, workload="c2"):
+def measured_traffic(stage, faces_per_launch, workload="c2", key="traffic_bytes"):
     """HBM bytes per launch of `stage`'s kernel from the committed PMC summary of THIS source tree
     (profiles/<round>/traffic.json with a matching source_digest, written by tools/pmc_traffic.py
     from tools/profile_round.sh's FETCH_SIZE / WRITE_SIZE passes over the same workload), or None
@@ -93,8 +93,8 @@ def measured_traffic(stage, faces_per_launch, workload="c2"):
             continue
         pre = STAGE_KERNELS.get(stage)
         for name, v in doc.get("kernels", {}).items():
-            if pre and name.startswith(pre) and v.get("traffic_bytes"):
-                return v["traffic_bytes"]
+            if pre and name.startswith(pre) and v.get(key):
+                return v[key]
     return None
 
 
@@ -585,6 +585,7 @@ def main():
         amount, unit, bound = stage_work(dom, faces_per_launch, W=W, H=H, n_hp=n_hp, n_mp=n_mp)
         achieved = amount / (avg_ms / 1e3)
         traffic = measured_traffic(dom, faces_per_launch) if wl.name == "c2" else None  # PMC bytes/launch
+        traffic_raw = measured_traffic(dom, faces_per_launch, key="traffic_bytes_uncorrected") if wl.name == "c2" else None
         if traffic is not None:
             traffic = int(traffic)
         peak = FP32_PEAK_TFLOPS if unit == "TFLOP/s" else HBM_PEAK_GBS
@@ -616,7 +617,11 @@ def main():
                          "frac": round(achieved / peak, 4), "traffic": traffic,
                          "avg_launch_ms": round(avg_ms, 4), "faces_per_launch": faces_per_launch,
                          "algorithmic_bytes": int(amount * 1e9) if unit == "GB/s" else None,
-                         "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"},
+                         "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_uncorrected": int(traffic_raw) if traffic_raw else None,
+                         "traffic_note": "FETCH_SIZE x2 is the guide's correction for wide streaming reads; this kernel "
+                                         "also gathers 16-B node records, so its HBM bytes lie between "
+                                         "traffic_uncorrected (FETCH_SIZE x1) and traffic"},
             "path_hbm_roofline": {"b_face": b_face, "achieved_GBs": round(value * b_face / 1e9, 1),
                                   "frac": round(value * b_face / 1e9 / HBM_PEAK_GBS, 4)},
             "stage_ms_per_step": {k: round(v[0] / max(1, args.steps), 3) for k, v in stages.items()},

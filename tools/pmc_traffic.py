@@ -37,10 +37,12 @@ def main():
             continue
         f = fetch.get(k, [])
         w = write.get(k, [])
-        fb = 2.0 * sum(f) / len(f) if f else None
+        fr = sum(f) / len(f) if f else None
+        fb = 2.0 * fr if f else None
         wb = sum(w) / len(w) if w else None
-        out[k] = {"fetch_bytes": fb, "write_bytes": wb, "launches": max(len(f), len(w)),
-                  "traffic_bytes": (fb or 0.0) + (wb or 0.0)}
+        out[k] = {"fetch_bytes": fb, "fetch_bytes_raw": fr, "write_bytes": wb, "launches": max(len(f), len(w)),
+                  "traffic_bytes": (fb or 0.0) + (wb or 0.0),
+                  "traffic_bytes_uncorrected": (fr or 0.0) + (wb or 0.0)}
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
     from bench import source_digest
     workload = sys.argv[3] if len(sys.argv) > 3 else "c2"
@@ -50,6 +52,11 @@ def main():
     text = json.dumps({"source": root, "source_digest": digest, "workload": workload,
                        "faces_per_launch": per_launch,
                        "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KiB -> bytes",
+                       "correction_note": ("the guide states the x2 FETCH_SIZE correction for wide coalesced streaming "
+                                           "reads; kernels whose reads are mostly gathers (k_traverse's 16-B node records "
+                                           "beside its 16-B window staging chunks, k_votes' 32-B leaf records, "
+                                           "k_meanshift's 8-B votes) may be over-stated by it: their true HBM bytes lie "
+                                           "between traffic_bytes_uncorrected and traffic_bytes"),
                        "kernels": out}, indent=1)
     if len(sys.argv) > 2:
         open(sys.argv[2], "w").write(text + "\n")
