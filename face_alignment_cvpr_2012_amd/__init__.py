@@ -122,6 +122,8 @@ EXPORTED_SYMBOLS = (
     "ffd_train_param_init", "ffd_train_mp_tree", "ffd_train_last_error", "ffd_trained_tree_num_nodes",
     "ffd_trained_tree_num_leaves", "ffd_trained_tree_arrays", "ffd_trained_tree_stats", "ffd_trained_tree_archive",
     "ffd_trained_tree_save", "ffd_trained_tree_free",
+    "ffd_train_hp_param_init", "ffd_train_hp_tree", "ffd_trained_tree_kind", "ffd_trained_tree_num_samples",
+    "ffd_trained_tree_hp_arrays",
 )
 COMM_ID_BYTES = 128
 STATUS_OK, STATUS_INVALID_ARGUMENT, STATUS_UNSUPPORTED = 0, 1, 7

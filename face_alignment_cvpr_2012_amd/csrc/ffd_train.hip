@@ -14,6 +14,7 @@
 //   applyOptimalSplit (Tree.hpp:291-308, SplitGen.hpp:103-167):             k_tr_partition
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdint>
 
 #include "../../include/ffd_numerics.h"
@@ -229,14 +230,8 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   return y;
 }
 
-// one thread per item (node, stripe): the stripe generator of SplitGen::generateMT, seeded with
-// (stripe + 1) * (split_seed + heap index of the node) (oracle/ffd_train_oracle.cpp: time(NULL)'s stand-in)
-__global__ __launch_bounds__(256) void k_tr_mt(const TrNode* __restrict__ nodes, int n_items, int ntests,
-                                              uint32_t split_seed, uint32_t* __restrict__ raw) {
-  const int item = blockIdx.x * blockDim.x + threadIdx.x;
-  if (item >= n_items) return;
-  const int node = item / ntests, stripe = item - node * ntests;
-  const uint32_t seed = (uint32_t)((uint64_t)(stripe + 1) * (uint64_t)(split_seed + nodes[node].heap));
+// The first MT_WIN outputs of mt19937(seed) into o[] (one thread).
+__device__ __forceinline__ void mt_first(uint32_t seed, uint32_t* __restrict__ o) {
   uint32_t x[MT_WIN + 1];
   uint32_t cur = seed;
   x[0] = cur;
@@ -247,13 +242,22 @@ __global__ __launch_bounds__(256) void k_tr_mt(const TrNode* __restrict__ nodes,
   }
 #pragma unroll 4
   for (int j = MT_WIN + 1; j < 397; j++) cur = 1812433253u * (cur ^ (cur >> 30)) + (uint32_t)j;
-  uint32_t* o = raw + (size_t)item * MT_WIN;
 #pragma unroll
   for (int i = 0; i < MT_WIN; i++) {
     cur = 1812433253u * (cur ^ (cur >> 30)) + (uint32_t)(397 + i);
     const uint32_t y = (x[i] & 0x80000000u) | (x[i + 1] & 0x7fffffffu);
     o[i] = mt_temper(cur ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u));
   }
+}
+
+// one thread per item (node, stripe): the stripe generator of SplitGen::generateMT, seeded with
+// (stripe + 1) * (split_seed + heap index of the node) (oracle/ffd_train_oracle.cpp: time(NULL)'s stand-in)
+__global__ __launch_bounds__(256) void k_tr_mt(const TrNode* __restrict__ nodes, int n_items, int ntests,
+                                              uint32_t split_seed, uint32_t* __restrict__ raw) {
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= n_items) return;
+  const int node = item / ntests, stripe = item - node * ntests;
+  mt_first((uint32_t)((uint64_t)(stripe + 1) * (uint64_t)(split_seed + nodes[node].heap)), raw + (size_t)item * MT_WIN);
 }
 
 // Boost.Random generate_uniform_int over a window of engine outputs (wave-uniform): bucket division
@@ -588,6 +592,209 @@ __global__ __launch_bounds__(64) void k_tr_partition(const TrNode* __restrict__ 
   scatter_sorted(imgs, samples, list + nd.beg, n, f, chan, hist, next + nd.beg);
 }
 
+
+// ----------------------------------------------------------- head pose ----
+// HeadPoseSample::evalSplit (HeadPoseSample.cpp:64-87) from the class counts of the two sides:
+// c[0..4] = positives per label, c[5] = background.  entropie (:120-143) and gain2 (:228-248) sum 1s,
+// labels and squared labels in double in the reference: exact integers, equal to the counts' values.
+__device__ __forceinline__ double hp_entropie(double p, int size) {
+  double e = 0;
+  const double p_pos = p / (double)size;
+  if (p_pos > 0) e += p_pos * ffd_log(p_pos);
+  const double p_neg = ((double)size - p) / (double)size;
+  if (p_neg > 0) e += p_neg * ffd_log(p_neg);
+  return e;
+}
+__device__ __forceinline__ double hp_gain2(double n, double sum, double sq_sum) {
+  const double mean = sum / n;
+  const double variance = (sq_sum / n) - (mean * mean);
+  return -variance;
+}
+__device__ __forceinline__ double hp_eval_split(const int* a, const int* b, int mode) {
+  int pa = 0, pb = 0, sa = 0, sb = 0, qa = 0, qb = 0;
+#pragma unroll
+  for (int l = 0; l < 5; l++) {
+    pa += a[l]; pb += b[l];
+    sa += l * a[l]; sb += l * b[l];
+    qa += l * l * a[l]; qb += l * l * b[l];
+  }
+  const int na = pa + a[5], nb = pb + b[5];
+  if (mode < 50) {
+    const double ea = hp_entropie((double)pa, na), eb = hp_entropie((double)pb, nb);
+    return (ea * (double)na + eb * (double)nb) / (double)(na + nb);
+  }
+  const double ga = hp_gain2((double)pa, (double)sa, (double)qa), gb = hp_gain2((double)pb, (double)sb, (double)qb);
+  return (ga * (double)pa + gb * (double)pb) / (double)(pb + pa);
+}
+
+// One workgroup per stripe of ONE node (the depth-first search order fixes the node's split mode):
+// the stripe's feature, every sample's value into a per-class histogram (6 x 512 bins in LDS), its
+// exclusive prefix, the 25 thresholds, the class counts below each threshold (lower_bound) and the
+// information gains; the stripe's best threshold is the first strict maximum (SplitGen.hpp:170-231).
+__global__ __launch_bounds__(256) void k_hp_items(HpItemsArgs A) {
+  __shared__ uint32_t raw[MT_WIN];
+  __shared__ int hist[6][512];
+  __shared__ int s_lo, s_hi;
+  __shared__ double s_info[TR_THR];
+  __shared__ int s_thr[TR_THR];
+  const int stripe = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) {
+    mt_first((uint32_t)((uint64_t)(stripe + 1) * (uint64_t)A.T), raw);
+    s_lo = 1 << 20;
+    s_hi = -(1 << 20);
+  }
+  for (int b = tid; b < 6 * 512; b += 256) (&hist[0][0])[b] = 0;
+  __syncthreads();
+  Draws d{raw, 0, false};
+  const TrFeature f = gen_feature(d, A.ps, A.smax);
+  int vmin = 1 << 20, vmax = -(1 << 20);
+  for (int i = tid; i < A.n; i += 256) {
+    const int gid = A.list[i];
+    const int v = eval_sample(A.imgs, A.samples[gid], f, A.chan);
+    vmin = min(vmin, v);
+    vmax = max(vmax, v);
+    atomicAdd(&hist[A.cls[gid]][v + 255], 1);
+  }
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) {
+    vmin = min(vmin, __shfl_xor(vmin, sh));
+    vmax = max(vmax, __shfl_xor(vmax, sh));
+  }
+  if (lane == 0) {
+    atomicMin(&s_lo, vmin);
+    atomicMax(&s_hi, vmax);
+  }
+  __syncthreads();
+  for (int c = wv; c < 6; c += 4) {  // exclusive prefix per class, 8 bins per lane
+    int loc[8], run = 0;
+#pragma unroll
+    for (int u = 0; u < 8; u++) { loc[u] = hist[c][lane * 8 + u]; run += loc[u]; }
+    int incl = run;
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+      const int t = __shfl_up(incl, sh);
+      if (lane >= sh) incl += t;
+    }
+    int ex = incl - run;
+#pragma unroll
+    for (int u = 0; u < 8; u++) { hist[c][lane * 8 + u] = ex; ex += loc[u]; }
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  const int lo = s_lo, range = s_hi - lo;
+  double info = -1.7976931348623157e308;
+  int thr = 0;
+  if (range > 0) {
+    int my_t = 0;
+    for (int j = 0; j < A.nthr; j++) {  // wave-uniform draws
+      const int t = d(0, range) + lo;
+      if (lane == j) my_t = t;
+    }
+    if (lane < A.nthr) {
+      int a[6], b[6], na = 0;
+#pragma unroll
+      for (int c = 0; c < 6; c++) {
+        a[c] = hist[c][my_t + 255];
+        b[c] = hist[c][511] - a[c];  // bin 511 is never filled: its prefix is the class total
+        na += a[c];
+      }
+      const bool ok = na >= 2 && A.n - na >= 2;
+      s_info[lane] = ok ? hp_eval_split(a, b, A.mode) : 0.0;
+      s_thr[lane] = ok ? my_t : INT_MIN;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0)
+      for (int j = 0; j < A.nthr; j++)
+        if (s_thr[j] != INT_MIN && s_info[j] > info) { info = s_info[j]; thr = s_thr[j]; }
+  }
+  if (lane == 0) {
+    if (d.bad) atomicOr(A.error, 1);
+    A.out_info[stripe] = info;
+    A.out_thr[stripe] = thr;
+  }
+}
+
+// findOptimalSplit + applyOptimalSplit for one node (Tree.hpp:135-166,261-308): the first stripe with the
+// strictly largest gain, its feature from the stripe's generator, and the node's samples split at the
+// threshold (value < threshold -> left) into out[0, nA) and out[nA, n), with each side's class counts.
+// The order inside a side is free: every head-pose quantity is a count.  One workgroup.
+__global__ __launch_bounds__(1024) void k_hp_split(HpSplitArgs A) {
+  __shared__ double sb[1024];
+  __shared__ int ss[1024];
+  __shared__ uint32_t raw[MT_WIN];
+  __shared__ int cnt[2], hs[2][6];
+  const int tid = threadIdx.x, lane = tid & 63;
+  double b = -1.7976931348623157e308;
+  int bs = -1;
+  for (int s = tid; s < A.ntests; s += 1024)
+    if (A.info[s] > b) { b = A.info[s]; bs = s; }
+  sb[tid] = b;
+  ss[tid] = bs;
+  if (tid < 2) cnt[tid] = 0;
+  if (tid < 12) (&hs[0][0])[tid] = 0;
+  __syncthreads();
+  for (int w = 512; w >= 1; w >>= 1) {
+    if (tid < w) {
+      const double o = sb[tid + w];
+      const int os = ss[tid + w];
+      if (os >= 0 && (ss[tid] < 0 || o > sb[tid] || (o == sb[tid] && os < ss[tid]))) {
+        sb[tid] = o;
+        ss[tid] = os;
+      }
+    }
+    __syncthreads();
+  }
+  const int best = ss[0];
+  if (best < 0) {
+    if (tid == 0) A.res->stripe = -1;
+    return;
+  }
+  if (tid == 0) mt_first((uint32_t)((uint64_t)(best + 1) * (uint64_t)A.T), raw);
+  __syncthreads();
+  Draws d{raw, 0, false};
+  const TrFeature f = gen_feature(d, A.ps, A.smax);
+  const int thr = A.thr[best];
+  const uint64_t below = lanes_below();
+  for (int i0 = tid - lane; i0 < A.n; i0 += 1024) {  // whole waves: uniform trip count for the ballots
+    const int i = i0 + lane;
+    const bool act = i < A.n;
+    int gid = 0, c = 0;
+    bool left = false;
+    if (act) {
+      gid = A.list[i];
+      c = A.cls[gid];
+      left = eval_sample(A.imgs, A.samples[gid], f, A.chan) < thr;
+    }
+    const uint64_t mA = __ballot(act && left), mB = __ballot(act && !left);
+    int baseA = 0, baseB = 0;
+    if (lane == 0) {
+      baseA = atomicAdd(&cnt[0], __popcll(mA));
+      baseB = atomicAdd(&cnt[1], __popcll(mB));
+    }
+    baseA = __shfl(baseA, 0);
+    baseB = __shfl(baseB, 0);
+    if (act) {
+      if (left) A.out[baseA + __popcll(mA & below)] = gid;
+      else A.out[A.n - 1 - (baseB + __popcll(mB & below))] = gid;
+      atomicAdd(&hs[left ? 0 : 1][c], 1);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    HpSplitResult r;
+    r.info = sb[0];
+    r.stripe = best;
+    r.thr = thr;
+    r.na = cnt[0];
+    r.nb = cnt[1];
+    r.ch = f.ch;
+    for (int j = 0; j < 8; j++) r.rect[j] = f.r[j];
+    for (int c = 0; c < 6; c++) { r.ha[c] = hs[0][c]; r.hb[c] = hs[1][c]; }
+    r.bad = d.bad ? 1 : 0;
+    *A.res = r;
+  }
+}
+
 // ------------------------------------------------------------ launchers ----
 void launch_channels(const TrImage* d_imgs, int n_img, int max_px, const uint8_t* gray, const ffd_gabor_sep* sep,
                      const float* taps7, uint8_t* u8, float* mag, float* vbuf, uint32_t* chan, hipStream_t s) {
@@ -610,6 +817,14 @@ void launch_items(const TrItemsArgs& a, hipStream_t s) {
 
 void launch_select(int n_nodes, int ntests, const double* info, const int* thr, const int* k, TrBest* best, hipStream_t s) {
   hipLaunchKernelGGL(k_tr_select, dim3(n_nodes), dim3(256), 0, s, ntests, info, thr, k, best);
+}
+
+void launch_hp_items(const HpItemsArgs& a, int ntests, hipStream_t s) {
+  hipLaunchKernelGGL(k_hp_items, dim3(ntests), dim3(256), 0, s, a);
+}
+
+void launch_hp_split(const HpSplitArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_hp_split, dim3(1), dim3(1024), 0, s, a);
 }
 
 void launch_partition(int n_nodes, const TrNode* nodes, const TrFeature* feats, const TrImage* imgs, const TrSample* samples,

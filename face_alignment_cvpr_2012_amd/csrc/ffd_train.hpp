@@ -61,11 +61,50 @@ struct TrItemsArgs {
   int* error;
 };
 
+// head pose: one node's stripes (k_hp_items) and its split (k_hp_split)
+struct HpItemsArgs {
+  const int32_t* list;        // the node's samples (global sample ids)
+  int n;
+  uint32_t T;                 // split_seed + heap index: stripe s uses mt19937((s + 1) * T)
+  int mode;                   // split_mode drawn for the node (< 50: entropie, else gain2)
+  int nthr, ps, smax;
+  const TrImage* imgs;
+  const TrSample* samples;
+  const int8_t* cls;          // per sample: label 0..4, or 5 for background
+  const uint32_t* chan;
+  double* out_info;           // [ntests]
+  int32_t* out_thr;
+  int* error;
+};
+
+struct HpSplitResult {
+  double info;
+  int32_t stripe, thr, na, nb, ch, rect[8], ha[6], hb[6], bad, pad;
+};
+
+struct HpSplitArgs {
+  int ntests;
+  const double* info;
+  const int32_t* thr;
+  uint32_t T;
+  int ps, smax;
+  const int32_t* list;
+  int n;
+  int32_t* out;               // [n]: left side first, then the right side
+  const TrImage* imgs;
+  const TrSample* samples;
+  const int8_t* cls;
+  const uint32_t* chan;
+  HpSplitResult* res;
+};
+
 void launch_channels(const TrImage* d_imgs, int n_img, int max_px, const uint8_t* gray, const ffd_gabor_sep* sep,
                      const float* taps7, uint8_t* u8, float* mag, float* vbuf, uint32_t* chan, hipStream_t s);
 void launch_mt(const TrNode* nodes, int n_items, int ntests, uint32_t split_seed, uint32_t* raw, hipStream_t s);
 void launch_items(const TrItemsArgs& a, hipStream_t s);
 void launch_select(int n_nodes, int ntests, const double* info, const int* thr, const int* k, TrBest* best, hipStream_t s);
+void launch_hp_items(const HpItemsArgs& a, int ntests, hipStream_t s);
+void launch_hp_split(const HpSplitArgs& a, hipStream_t s);
 void launch_partition(int n_nodes, const TrNode* nodes, const TrFeature* feats, const TrImage* imgs, const TrSample* samples,
                       const uint32_t* chan, const int32_t* list, int32_t* next, hipStream_t s);
 

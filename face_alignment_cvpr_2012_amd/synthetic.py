@@ -198,3 +198,36 @@ def training_rois(n, face_size=125, seed=7, fixtures=None):
         q = (p - jit) * s
         pts[k] = np.rint(q - np.array([x0, y0])).astype(np.int32)
     return rois, pts
+
+
+def headpose_training_images(n, face_size=125, seed=11, margin=40, fixtures=None):
+    """Training images for head-pose tree training, following train_headpose.cpp's
+    trainTree (src/train_headpose.cpp:83-96): image k = bundled fixture k mod 20 (k >= 20: jittered,
+    rescaled and noised variants, seeded), scaled so the face box is face_size wide (bilinear,
+    edge-clamped; not OpenCV's resize: the images are inputs, not parity subjects) and cut to the face
+    box plus `margin` pixels on every side (edge-clamped where that leaves the photograph), so that
+    every positive patch lies inside the image and the negatives have room around the face.  The
+    fixtures carry no head-pose annotation, so the pose label is synthetic: k mod 5 - 2.  Returns (list
+    of uint8 gray images, int32 [n, 4] boxes (x, y, w, h) in them, int32 [n] poses)."""
+    fx = fixtures or load_fixtures()
+    imgs, boxes = fx["images"], fx["boxes"]
+    rng = np.random.default_rng(seed)
+    out, bx_out, poses = [], np.zeros((n, 4), np.int32), np.zeros(n, np.int32)
+    for k in range(n):
+        i = k % len(imgs)
+        x, y, w, h = (float(v) for v in boxes[i])
+        jit = np.zeros(2) if k < len(imgs) else rng.uniform(-4, 4, size=2)
+        scl = 1.0 if k < len(imgs) else rng.uniform(0.93, 1.07)
+        s = face_size / (w * scl)
+        bx, by, bw, bh = int(x * s), int(y * s), int(w * s), int(h * s)
+        ow, oh = max(bw, face_size) + 2 * margin, max(bh, face_size) + 2 * margin
+        xs = (np.arange(bx - margin, bx - margin + ow) + 0.5) / s - 0.5 + jit[0]
+        ys = (np.arange(by - margin, by - margin + oh) + 0.5) / s - 0.5 + jit[1]
+        bgr = _bilinear(imgs[i], xs, ys)
+        gray = (bgr[..., 0] * 0.114 + bgr[..., 1] * 0.587 + bgr[..., 2] * 0.299)
+        if k >= len(imgs):
+            gray = gray + rng.normal(0.0, 2.0, size=gray.shape)
+        out.append(np.clip(np.rint(gray), 0, 255).astype(np.uint8))
+        bx_out[k] = (margin, margin, bw, bh)
+        poses[k] = k % 5 - 2
+    return out, bx_out, poses

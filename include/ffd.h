@@ -364,10 +364,38 @@ ffd_status ffd_trained_tree_arrays(const ffd_trained_tree* t, int32_t* node_leaf
                                    double* node_info, int32_t* leaf_n, float* leaf_fg, int16_t* leaf_offset,
                                    float* leaf_var, float* leaf_pf, int32_t* samples_xy);
 ffd_status ffd_trained_tree_stats(const ffd_trained_tree* t, ffd_train_stats* stats);
-/* Tree<MPSample>::save's archive bytes (buf == NULL: only *size) / to a file */
+/* Tree<MPSample>::save's (Tree<HeadPoseSample>::save's) archive bytes (buf == NULL: only *size) / to a file */
 ffd_status ffd_trained_tree_archive(const ffd_trained_tree* t, char* buf, int64_t cap, int64_t* size);
 ffd_status ffd_trained_tree_save(const ffd_trained_tree* t, const char* path);
 void ffd_trained_tree_free(ffd_trained_tree* t);
+
+/* ---- Head-pose tree training -------------------------------------------------
+ * Replaces train_headpose.cpp's trainTree (src/train_headpose.cpp:40-143) from the scaled images on:
+ * positive / negative patch sampling (:98-134), Tree<HeadPoseSample> growth with the reference's
+ * split-mode draw per searched node (include/Tree.hpp:102-171,261-289) and HeadPoseSample::generateSplit /
+ * evalSplit / entropie / gain2 / makeLeaf (src/HeadPoseSample.cpp:48-248).  The mode of a node is the
+ * tree generator's next draw in DEPTH-FIRST order, so nodes are searched one at a time in that order
+ * (every stripe of the node in parallel on the GPU), not a level at a time.  Seeds as above.
+ * ffd_trained_tree_archive / _save give Tree<HeadPoseSample>::save's archive for such a tree. */
+typedef struct {                 /* one training image of train_headpose.cpp:83-96 */
+  const uint8_t* gray;           /* the whole image, scaled so the face box is face_size wide, 8-bit gray */
+  int32_t width, height, stride;
+  ffd_rect face;                 /* annotations[i].bbox after the scaling; positives lie in
+                                    [face.x, face.x + face_size - 1) x [face.y, face.y + face_size - 1) */
+  int32_t pose;                  /* annotations[i].pose in [-2, 2] (label pose + 2) */
+} ffd_train_hp_image;
+
+void ffd_train_hp_param_init(ffd_train_param* p);  /* config_headpose.txt: depth 15, 2000 tests, 200 patches */
+ffd_status ffd_train_hp_tree(const ffd_train_param* p, const ffd_train_hp_image* images, int32_t n_images,
+                             ffd_trained_tree** out);
+int32_t ffd_trained_tree_kind(const ffd_trained_tree* t);          /* FFD_FOREST_FFD or FFD_FOREST_HEADPOSE */
+int64_t ffd_trained_tree_num_samples(const ffd_trained_tree* t);   /* sampled patches */
+/* A head-pose tree's pre-order arrays (node_mode: the split mode drawn for each split node, -1 for a
+ * leaf), HeadPoseLeaf payloads (leaf_labels: 5 x i32 per leaf) and patches (image, x, y, label; label -1
+ * for background).  Any pointer may be NULL. */
+ffd_status ffd_trained_tree_hp_arrays(const ffd_trained_tree* t, int32_t* node_leaf, int16_t* node_split,
+                                      double* node_info, int32_t* node_mode, int32_t* leaf_n, float* leaf_fg,
+                                      int32_t* leaf_labels, int32_t* samples);
 
 /* Library version string. */
 const char* ffd_version(void);

@@ -326,6 +326,50 @@ def train_mp_tree(rois, parts, max_depth=20, min_patches=20, ntests=2500, npatch
         L.oracle_train_tree_free(h)
 
 
+def train_hp_tree(images, faces, poses, max_depth=15, min_patches=20, ntests=2000, npatches=200, face_size=125,
+                  patch_size_ratio=0.25, tree_seed=1, split_seed=1, ntrees=15, nimages=400):
+    """The CPU restatement of train_headpose.cpp's trainTree + Tree<HeadPoseSample> growth
+    (oracle/ffd_train_oracle.cpp): images already scaled so the face box is face_size wide, faces
+    [n, 4] (x, y, w, h), poses [n] in [-2, 2].  Returns the pre-order node arrays, the split modes,
+    HeadPoseLeaf payloads, the sampled patches (image, x, y, label) and i_node."""
+    L = lib()
+    if not getattr(L, "_train_hp_bound", False):
+        L.oracle_train_hp_tree.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int32, ctypes.POINTER(OracleTrainParam),
+                                                                   ctypes.POINTER(ctypes.c_void_p)]
+        L.oracle_train_hp_tree_size.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int64)] * 4
+        L.oracle_train_hp_tree_get.argtypes = [ctypes.c_void_p] * 9
+        L.oracle_train_hp_tree_free.argtypes = [ctypes.c_void_p]
+        L.oracle_train_last_error.restype = ctypes.c_char_p
+        L._train_hp_bound = True
+    images = [np.ascontiguousarray(r, np.uint8) for r in images]
+    faces = np.ascontiguousarray(faces, np.int32).reshape(-1, 4)
+    poses = np.ascontiguousarray(poses, np.int32)
+    n = len(images)
+    ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in images])
+    ws = np.array([r.shape[1] for r in images], np.int32)
+    hs = np.array([r.shape[0] for r in images], np.int32)
+    p = OracleTrainParam(max_depth, min_patches, ntests, ntrees, nimages, npatches, face_size, patch_size_ratio,
+                         25, tree_seed, split_seed, 0.125)
+    h = ctypes.c_void_p()
+    if L.oracle_train_hp_tree(ptrs, ws.ctypes.data, hs.ctypes.data, faces.ctypes.data, poses.ctypes.data, n,
+                              ctypes.byref(p), ctypes.byref(h)) != 0:
+        raise RuntimeError("oracle_train_hp_tree: " + L.oracle_train_last_error().decode())
+    try:
+        nn, nl, inode, ns = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        L.oracle_train_hp_tree_size(h, ctypes.byref(nn), ctypes.byref(nl), ctypes.byref(inode), ctypes.byref(ns))
+        N, Lf = nn.value, nl.value
+        a = {"node_leaf": np.zeros(N, np.int32), "node_split": np.zeros((N, 10), np.int16),
+             "node_info": np.zeros(N, np.float64), "node_mode": np.zeros(N, np.int32), "leaf_n": np.zeros(Lf, np.int32),
+             "leaf_fg": np.zeros(Lf, np.float32), "leaf_labels": np.zeros((Lf, 5), np.int32),
+             "samples": np.zeros((ns.value, 4), np.int32)}
+        L.oracle_train_hp_tree_get(h, *(a[k].ctypes.data for k in ("node_leaf", "node_split", "node_info", "node_mode",
+                                                                    "leaf_n", "leaf_fg", "leaf_labels", "samples")))
+        a["i_node"] = inode.value
+        return a
+    finally:
+        L.oracle_train_hp_tree_free(h)
+
+
 def log(x):
     lib()
     if not getattr(lib(), "_train_bound", False):

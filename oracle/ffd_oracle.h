@@ -120,6 +120,20 @@ int oracle_train_tree_get(const oracle_train_tree* t, int32_t* node_leaf, int16_
                           int32_t* leaf_n, float* leaf_fg, int16_t* leaf_offset, float* leaf_var, float* leaf_pf,
                           int32_t* samples_xy);
 void oracle_train_tree_free(oracle_train_tree* t);
+/* Head-pose tree training (Tree<HeadPoseSample>, train_headpose.cpp): images are the gray images already
+ * scaled so the face box is face_size wide; faces: n x (x, y, w, h) in those images; poses in [-2, 2]. */
+typedef struct oracle_hp_tree oracle_hp_tree;
+int oracle_train_hp_tree(const uint8_t* const* images, const int32_t* widths, const int32_t* heights,
+                         const int32_t* faces, const int32_t* poses, int32_t n_images, const oracle_train_param* p,
+                         oracle_hp_tree** out);
+int oracle_train_hp_tree_size(const oracle_hp_tree* t, int64_t* n_nodes, int64_t* n_leaves, int64_t* i_node,
+                              int64_t* n_samples);
+/* node_mode: the split_mode drawn for each split node (-1 for leaves); leaf_labels: 5 per leaf;
+ * samples: (image, x, y, label) per patch, label -1 for background. */
+int oracle_train_hp_tree_get(const oracle_hp_tree* t, int32_t* node_leaf, int16_t* node_split, double* node_info,
+                             int32_t* node_mode, int32_t* leaf_n, float* leaf_fg, int32_t* leaf_labels,
+                             int32_t* samples);
+void oracle_train_hp_tree_free(oracle_hp_tree* t);
 const char* oracle_train_last_error(void);
 double oracle_log(double x);
 

@@ -1,4 +1,5 @@
-// ffd_train_oracle.cpp — CPU restatement of the reference's facial-feature (MPSample) tree training.
+// ffd_train_oracle.cpp — CPU restatement of the reference's tree training: facial-feature
+// (Tree<MPSample>) and head-pose (Tree<HeadPoseSample>, below) trees.
 //
 // TEST INFRASTRUCTURE ONLY: the checker for the HIP training path (csrc/ffd_train.*).  Only tests/
 // and tools/ load it; the product library never links or calls it.
@@ -140,6 +141,7 @@ struct Trainer {
   }
 
   // stable sort of list positions by value (std::sort of (value, index) pairs)
+ public:
   static void sort_by_value(const std::vector<int>& vals, std::vector<int>& order) {
     const int n = (int)vals.size();
     int cnt[512] = {0};
@@ -255,6 +257,175 @@ struct Trainer {
   }
 };
 
+// ---------------------------------------------------------------- head pose --
+// Tree<HeadPoseSample> training (src/train_headpose.cpp:40-143, src/HeadPoseSample.cpp:30-248).
+//   * trainTree's samples: per image (the caller's gray image already scaled so the face box is
+//     face_size wide, train_headpose.cpp:83-96), npatches * (1 - 0.2f) positive patches at
+//     box.(x, y) + U{0 .. face_size - ps - 1} (label pose + 2), then npatches * 0.2f negative patches
+//     at U{0 .. cols - ps - 1} x U{0 .. rows - ps - 1} that miss the face box (intersect(),
+//     face_utils.cpp:325-346), up to 100 attempts each (a patch whose 100th attempt is reached is
+//     dropped, as the reference's `attempt == max_attempts` test does even when that attempt missed
+//     the box); every draw from the tree's mt19937 (seed idx_tree + 1), x before y.
+//   * findOptimalSplit draws split_mode = U{0..100} from the TREE's generator once per searched node
+//     (Tree.hpp:267-274), so the nodes' modes follow the depth-first order of the search.
+//   * evalSplit (HeadPoseSample.cpp:64-87): split_mode < 50 -> size-weighted entropie (the fg / bg
+//     entropy, :120-143), else gain2 (the negative variance of the positive labels, :228-248) weighted
+//     by the positive counts; both are functions of the class counts of each side.
+//   * makeLeaf (:89-118): fg fraction, sample count, histogram of the positive labels.
+struct HPSample {
+  int img, x, y, label;
+};
+
+// HeadPoseSample::entropie (HeadPoseSample.cpp:120-143) over the set's class counts
+double hp_entropie(double p, int64_t size) {
+  double e = 0;
+  const double p_pos = p / (double)size;
+  if (p_pos > 0) e += p_pos * ffd_log(p_pos);
+  const double p_neg = ((double)size - p) / (double)size;
+  if (p_neg > 0) e += p_neg * ffd_log(p_neg);
+  return e;
+}
+
+// HeadPoseSample::gain2 (HeadPoseSample.cpp:228-248): n positives, label sum and sum of squares
+double hp_gain2(double n, double sum, double sq_sum) {
+  const double mean = sum / n;
+  const double variance = (sq_sum / n) - (mean * mean);
+  return -variance;
+}
+
+struct HPTrainer {
+  const oracle_train_param* P;
+  int ps;
+  std::vector<Image> imgs;
+  std::vector<HPSample> samples;
+  std::mt19937 tree_rng;
+  std::vector<int32_t> node_leaf;
+  std::vector<int16_t> node_split;
+  std::vector<double> node_info;
+  std::vector<int32_t> leaf_n, leaf_labels, node_mode;
+  std::vector<float> leaf_fg;
+  int64_t i_node = 0;
+
+  int eval(const Feature& f, const HPSample& s) const {
+    const Image& im = imgs[s.img];
+    const int W1 = im.w + 1;
+    const uint32_t* I = im.ch.data() + (size_t)f.ch * W1 * (im.h + 1);
+    auto rect = [&](const int* r) {
+      const int x = s.x + r[0], y = s.y + r[1], w = r[2], h = r[3];
+      const int64_t S = (int64_t)I[(y + h) * W1 + x + w] - I[y * W1 + x + w] - I[(y + h) * W1 + x] + I[y * W1 + x];
+      return (int)((double)S / (double)(float)(w * h));
+    };
+    return rect(f.r1) - rect(f.r2);
+  }
+
+  // evalSplit over the two sets list[order[0..k)], list[order[k..n)], literally: counts by loops
+  double eval_split(const std::vector<int>& order, const std::vector<int>& list, int k, int mode) const {
+    const int n = (int)order.size();
+    auto stats = [&](int a, int b, double& p, double& sum, double& sq) {
+      p = 0; sum = 0; sq = 0;
+      for (int i = a; i < b; i++) {
+        const HPSample& s = samples[list[order[i]]];
+        if (s.label >= 0) {
+          p += 1;
+          sum += s.label;
+          sq += s.label * s.label;
+        }
+      }
+    };
+    double pa, sa, qa, pb, sb, qb;
+    stats(0, k, pa, sa, qa);
+    stats(k, n, pb, sb, qb);
+    if (mode < 50) {
+      const double ea = hp_entropie(pa, k), eb = hp_entropie(pb, n - k);
+      return (ea * (double)k + eb * (double)(n - k)) / (double)(k + n - k);
+    }
+    const int size_a = (int)pa, size_b = (int)pb;
+    const double ga = hp_gain2(pa, sa, qa), gb = hp_gain2(pb, sb, qb);
+    return (ga * size_a + gb * size_b) / (double)(size_b + size_a);
+  }
+
+  void make_leaf(const std::vector<int>& list) {
+    const int l = (int)leaf_n.size();
+    const int n = (int)list.size();
+    int size = 0;
+    for (int i : list) size += samples[i].label >= 0 ? 1 : 0;
+    leaf_n.push_back(n);
+    leaf_fg.push_back((float)size / (float)n);
+    for (int j = 0; j < 5; j++) leaf_labels.push_back(0);
+    if (size > 0)
+      for (int i : list)
+        if (samples[i].label >= 0) leaf_labels[l * 5 + samples[i].label]++;
+    node_leaf.push_back(l);
+    for (int j = 0; j < 10; j++) node_split.push_back(0);
+    node_info.push_back(0.0);
+    node_mode.push_back(-1);
+  }
+
+  void grow(const std::vector<int>& list, int depth, uint32_t heap) {
+    const int n = (int)list.size();
+    if (n < P->min_patches || depth >= P->max_depth) {
+      make_leaf(list);
+      i_node += (int64_t)(std::pow(2.0f, (float)(P->max_depth - depth)) - 1);
+      return;
+    }
+    const int mode = uniform_int(tree_rng, 0, 100);  // rand_split() (Tree.hpp:267-274)
+    const uint32_t T = P->split_seed + heap;
+    Feature best_f{};
+    double best_info = -DBL_MAX;
+    int best_thr = 0;
+    std::vector<int> vals(n), order;
+    for (int stripe = 0; stripe < P->ntests; stripe++) {
+      std::mt19937 rng((uint32_t)((uint64_t)(stripe + 1) * (uint64_t)T));
+      const Feature f = generate(ps, rng);
+      for (int i = 0; i < n; i++) vals[i] = eval(f, samples[list[i]]);
+      Trainer::sort_by_value(vals, order);
+      double info = -DBL_MAX;
+      int thr = 0;
+      const int vmin = vals[order.front()], vmax = vals[order.back()], range = vmax - vmin;
+      if (range > 0) {
+        for (int j = 0; j < P->num_thresholds; j++) {
+          const int t = uniform_int(rng, 0, range) + vmin;
+          int k = 0;
+          while (k < n && vals[order[k]] < t) k++;
+          if (k < 2 || n - k < 2) continue;
+          const double v = eval_split(order, list, k, mode);
+          if (v > info) { info = v; thr = t; }
+        }
+      }
+      if (info > best_info) { best_info = info; best_thr = thr; best_f = f; }
+    }
+    if (best_info == -DBL_MAX) {
+      make_leaf(list);
+      i_node += (int64_t)(std::pow(2.0f, (float)(P->max_depth - depth)) - 1);
+      return;
+    }
+    for (int i = 0; i < n; i++) vals[i] = eval(best_f, samples[list[i]]);
+    Trainer::sort_by_value(vals, order);
+    int k = 0;
+    while (k < n && vals[order[k]] < best_thr) k++;
+    std::vector<int> A(k), B(n - k);
+    for (int i = 0; i < k; i++) A[i] = list[order[i]];
+    for (int i = k; i < n; i++) B[i - k] = list[order[i]];
+    node_leaf.push_back(-1);
+    const int16_t s[10] = {(int16_t)best_f.ch, (int16_t)best_f.r1[0], (int16_t)best_f.r1[1], (int16_t)best_f.r1[2],
+                           (int16_t)best_f.r1[3], (int16_t)best_f.r2[0], (int16_t)best_f.r2[1], (int16_t)best_f.r2[2],
+                           (int16_t)best_f.r2[3], (int16_t)best_thr};
+    node_split.insert(node_split.end(), s, s + 10);
+    node_info.push_back(best_info);
+    node_mode.push_back(mode);
+    i_node++;
+    grow(A, depth + 1, 2 * heap);
+    grow(B, depth + 1, 2 * heap + 1);
+  }
+};
+
+// intersect (face_utils.cpp:325-346) is empty
+bool hp_disjoint(int ax, int ay, int aw, int ah, int bx, int by, int bw, int bh) {
+  const int x = ax < bx ? bx : ax, y = ay < by ? by : ay;
+  const int w = (ax + aw < bx + bw ? ax + aw : bx + bw) - x, h = (ay + ah < by + bh ? ay + ah : by + bh) - y;
+  return w <= 0 || h <= 0;
+}
+
 std::string g_err;
 
 }  // namespace
@@ -354,6 +525,106 @@ int oracle_train_tree_get(const oracle_train_tree* h, int32_t* node_leaf, int16_
 }
 
 void oracle_train_tree_free(oracle_train_tree* h) { delete h; }
+
+struct oracle_hp_tree {
+  HPTrainer t;
+};
+
+int oracle_train_hp_tree(const uint8_t* const* images, const int32_t* widths, const int32_t* heights,
+                         const int32_t* faces, const int32_t* poses, int32_t n_images, const oracle_train_param* p,
+                         oracle_hp_tree** out) {
+  try {
+    if (!images || !widths || !heights || !faces || !poses || !p || !out || n_images <= 0)
+      throw std::runtime_error("bad arguments");
+    auto* h = new oracle_hp_tree;
+    HPTrainer& T = h->t;
+    T.P = p;
+    T.ps = (int)std::round(p->face_size * p->patch_size_ratio);
+    T.tree_rng.seed(p->tree_seed);
+    T.imgs.resize(n_images);
+    const int npos_hi = 0;
+    (void)npos_hi;
+    for (int i = 0; i < n_images; i++) {
+      Image& im = T.imgs[i];
+      im.w = widths[i];
+      im.h = heights[i];
+      const int* b = faces + 4 * i;
+      if (im.w < T.ps + 1 || im.h < T.ps + 1 || b[0] < 0 || b[1] < 0 || b[0] + p->face_size - 1 > im.w ||
+          b[1] + p->face_size - 1 > im.h || poses[i] < -2 || poses[i] > 2)
+        throw std::runtime_error("image " + std::to_string(i) + ": face box or size out of range");
+      im.ch.resize((size_t)NCH * (im.w + 1) * (im.h + 1));
+      if (oracle_channels(images[i], im.w, im.h, im.ch.data()) != 0) throw std::runtime_error("channels failed");
+      // positives (train_headpose.cpp:101-109)
+      for (int j = 0; j < p->npatches * (1 - 0.2f); j++) {
+        HPSample s;
+        s.img = i;
+        s.x = b[0] + uniform_int(T.tree_rng, 0, p->face_size - T.ps - 1);
+        s.y = b[1] + uniform_int(T.tree_rng, 0, p->face_size - T.ps - 1);
+        s.label = poses[i] + 2;
+        T.samples.push_back(s);
+      }
+      // negatives (train_headpose.cpp:111-127)
+      for (int j = 0; j < p->npatches * 0.2f; j++) {
+        int x, y, attempt = 0;
+        bool miss;
+        do {
+          x = uniform_int(T.tree_rng, 0, im.w - T.ps - 1);
+          y = uniform_int(T.tree_rng, 0, im.h - T.ps - 1);
+          miss = hp_disjoint(x, y, T.ps, T.ps, b[0], b[1], b[2], b[3]);
+          attempt++;
+        } while (!miss && attempt < 100);
+        if (attempt == 100) continue;
+        T.samples.push_back({i, x, y, -1});
+      }
+    }
+    if (T.samples.empty()) throw std::runtime_error("no training patches");
+    std::vector<int> all(T.samples.size());
+    for (size_t i = 0; i < all.size(); i++) all[i] = (int)i;
+    T.grow(all, 0, 1u);
+    *out = h;
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
+int oracle_train_hp_tree_size(const oracle_hp_tree* h, int64_t* n_nodes, int64_t* n_leaves, int64_t* i_node,
+                              int64_t* n_samples) {
+  if (!h) return -1;
+  if (n_nodes) *n_nodes = (int64_t)h->t.node_leaf.size();
+  if (n_leaves) *n_leaves = (int64_t)h->t.leaf_n.size();
+  if (i_node) *i_node = h->t.i_node;
+  if (n_samples) *n_samples = (int64_t)h->t.samples.size();
+  return 0;
+}
+
+int oracle_train_hp_tree_get(const oracle_hp_tree* h, int32_t* node_leaf, int16_t* node_split, double* node_info,
+                             int32_t* node_mode, int32_t* leaf_n, float* leaf_fg, int32_t* leaf_labels,
+                             int32_t* samples) {
+  if (!h) return -1;
+  const HPTrainer& t = h->t;
+  auto cp = [](auto* dst, const auto& v) {
+    if (dst && !v.empty()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));
+  };
+  cp(node_leaf, t.node_leaf);
+  cp(node_split, t.node_split);
+  cp(node_info, t.node_info);
+  cp(node_mode, t.node_mode);
+  cp(leaf_n, t.leaf_n);
+  cp(leaf_fg, t.leaf_fg);
+  cp(leaf_labels, t.leaf_labels);
+  if (samples)
+    for (size_t i = 0; i < t.samples.size(); i++) {
+      samples[4 * i] = t.samples[i].img;
+      samples[4 * i + 1] = t.samples[i].x;
+      samples[4 * i + 2] = t.samples[i].y;
+      samples[4 * i + 3] = t.samples[i].label;
+    }
+  return 0;
+}
+
+void oracle_train_hp_tree_free(oracle_hp_tree* h) { delete h; }
 
 const char* oracle_train_last_error(void) { return g_err.c_str(); }
 
