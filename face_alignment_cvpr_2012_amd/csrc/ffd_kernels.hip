@@ -1308,34 +1308,165 @@ __global__ __launch_bounds__(256) void k_hp_pose(const FaceDesc* __restrict__ fa
   }
 }
 
-// ------------------------------------------------------------ vote lists ----
-// getFacialFeaturesVotesMT vote filter (face_utils.cpp:276-301).  One wave per face walks the
-// FFD leaves in reference order (patch-major x-outer, tree-minor), 64 at a time; for each
-// landmark a ballot + popcount gives every voting lane its slot, so the compacted list keeps
-// the reference's vote order exactly.
-template <bool compact>
-__global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ faces, int n_faces,
-                                               const int32_t* __restrict__ mp_leaf,
-                                               const uint4* __restrict__ leaf_rec, int bias_x,
-                                               int bias_y, const HpState* __restrict__ state,
-                                               int tslots, int step, int step_y, int half_patch, int n_parts,
-                                               Vote* __restrict__ votes, int32_t* __restrict__ vote_counts) {
-  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+// The same reduction for one face per workgroup (small batches: single-face latency).  The face's leaf
+// values arrive in tiles of 1024 leaves (every thread gathers 4, values one tile ahead), double-buffered
+// in LDS as (m, m * m); lanes 0 and 1 of wave 0 add the two components in leaf order (LDS reads one group
+// of 8 ahead) while the other waves gather the next tile.  The pose-bin integrals: lane b walks bin b's
+// abscissae (x += step, sequential as the reference's loop), every thread evaluates the Gaussian terms,
+// lane b adds them in order; lane 0 selects the trees.
+__global__ __launch_bounds__(256) void k_hp_pose1(const FaceDesc* __restrict__ faces, int n_faces,
+                                                  const int32_t* __restrict__ hp_leaf, const float* __restrict__ hp_m,
+                                                  int hp_trees, int n_forests, int ntrees_per_forest,
+                                                  HpState* __restrict__ state, FaceOut* __restrict__ out) {
+  constexpr int T1 = 1024, U1 = T1 / 256, NX = 224;  // bins span <= 2.15 / 0.01 + 1 abscissae
+  __shared__ float2 tv[2][T1];
+  __shared__ double s_x[5][NX], s_t[5][NX];
+  __shared__ int s_nx[5], s_cnt[4];
+  __shared__ float s_sum[2], s_area[8];
+  const int f = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   if (f >= n_faces) return;
   const FaceDesc& fd = faces[f];
-  if (!fd.valid) return;
-  const int nx = fd.nmx, ny = fd.nmy, n = nx * ny, T = state[f].n_trees, total = n * T;
-  const int64_t cap = (int64_t)tslots * n;
-  const int32_t* L = mp_leaf + fd.mp_off;
-  Vote* V = votes + fd.vote_off;
-  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  int cnt[NPARTS];
+  FaceOut& o = out[f];
+  if (tid == 0) { o.bbox[0] = fd.bx; o.bbox[1] = fd.by; o.bbox[2] = fd.bw; o.bbox[3] = fd.bh; }
+  if (!fd.valid) {
+    if (tid == 0) { o.status = fd.reject; o.n_trees = 0; state[f].n_trees = 0; }
+    return;
+  }
+  const int total = fd.nhx * fd.nhy * hp_trees;
+  const int32_t* ids = hp_leaf + fd.hp_off;
+  float v[U1];
+  int count = 0;
+  auto gather = [&](int k0) {
+    int id[U1];
 #pragma unroll
-  for (int i = 0; i < NPARTS; i++) cnt[i] = 0;
+    for (int u = 0; u < U1; u++) id[u] = k0 + tid + 256 * u < total ? ids[k0 + tid + 256 * u] : -1;
+#pragma unroll
+    for (int u = 0; u < U1; u++) v[u] = id[u] >= 0 ? hp_m[id[u]] : -1.f;  // -1: filtered leaf or past the end
+  };
+  auto put = [&](int buf, int k0) {
+#pragma unroll
+    for (int u = 0; u < U1; u++) {
+      const bool in = v[u] >= 0.f;
+      const float m = in ? v[u] : 0.f;  // filtered leaves add +0 (a non-negative float sum is unchanged)
+      count += in ? 1 : 0;
+      tv[buf][tid + 256 * u] = make_float2(m, in ? m * m : 0.f);
+    }
+  };
+  float acc = 0.f;
+  int buf = 0;
+  if (total > 0) {
+    gather(0);
+    put(0, 0);
+    if (T1 < total) gather(T1);
+  }
+  __syncthreads();
+  for (int k0 = 0; k0 < total; k0 += T1, buf ^= 1) {
+    if (k0 + T1 < total) {
+      put(buf ^ 1, k0 + T1);
+      if (k0 + 2 * T1 < total) gather(k0 + 2 * T1);
+    }
+    if (tid < 2) {  // component tid (sum m, sum m * m) in leaf order
+      const float* tp = reinterpret_cast<const float*>(&tv[buf][0]) + tid;
+      const int n = min(T1, total - k0);
+      int j = 0;
+      float a[8];
+      if (n >= 8) {
+#pragma unroll
+        for (int e = 0; e < 8; e++) a[e] = tp[e * 2];
+      }
+      for (; j + 16 <= n; j += 8) {
+        float b[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) b[e] = tp[(j + 8 + e) * 2];
+#pragma unroll
+        for (int e = 0; e < 8; e++) acc += a[e];
+#pragma unroll
+        for (int e = 0; e < 8; e++) a[e] = b[e];
+      }
+      if (j + 8 <= n) {
+#pragma unroll
+        for (int e = 0; e < 8; e++) acc += a[e];
+        j += 8;
+      }
+      for (; j < n; j++) acc += tp[j * 2];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) count += __shfl_xor(count, sh);
+  if (lane == 0) s_cnt[wv] = count;
+  if (tid < 2) s_sum[tid] = acc;
+  __syncthreads();
+  const float cnt = (float)(s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3]);  // exact below 2^24
+  float mean = s_sum[0] / cnt;
+  float var = (s_sum[1] / cnt) - (mean * mean);
+  mean -= 2;
+  var *= 0.05f;  // NORM_HEADPOSE_VARIANCE_FACTOR
+  const double dmean = (double)mean, dstd = __builtin_sqrt((double)var);
+  const float poseT[6] = {-2.5f, -0.35f, -0.20f, 0.20f, 0.35f, 2.5f};
+  const int nb = min(n_forests, 5);
+  const double step = 0.01;
+  if (tid < nb) {  // the abscissae of bin tid, accumulated as the reference's loop does
+    int m = 0;
+    for (double x = poseT[tid]; x < (double)poseT[tid + 1] && m < NX; x += step) s_x[tid][m++] = x;
+    s_nx[tid] = m;
+  }
+  __syncthreads();
+  for (int b = 0; b < nb; b++)
+    for (int k = tid; k < s_nx[b]; k += 256) {
+      const double tt = (s_x[b][k] - dmean) / dstd;
+      s_t[b][k] = ffd_exp(-0.5 * (tt * tt)) * step;
+    }
+  __syncthreads();
+  if (tid < nb) {
+    double a = 0;
+    for (int k = 0; k < s_nx[tid]; k++) a += s_t[tid][k];
+    s_area[tid] = (float)(a * 1.0 / (dstd * 2.5066282746310002));
+  }
+  __syncthreads();
+  if (tid == 0) {
+    o.status = 0;
+    o.headpose = mean;
+    o.pose_variance = var;
+    HpState& st = state[f];
+    st.headpose = mean;
+    st.variance = var;
+    float max_area = 0;
+    int dominant = 0;  // first strict maximum
+    for (int jj = 0; jj < n_forests; jj++) {
+      const float a = s_area[jj];
+      st.pose_freq[jj] = a;
+      if (max_area < a) { max_area = a; dominant = jj; }
+    }
+    int nt_total = 0;
+    for (int i = 0; i < n_forests; i++) {
+      const float vv = floorf(st.pose_freq[i] * (float)ntrees_per_forest);
+      int kk = (vv > -2147483649.0f && vv < 2147483648.0f) ? (int)vv : (int)0x80000000;
+      kk = min(kk, ntrees_per_forest);
+      for (int jj = 0; jj < kk && nt_total < MAX_TREES; jj++) st.trees[nt_total++] = i * ntrees_per_forest + jj;
+    }
+    for (int i = nt_total; i < ntrees_per_forest; i++) st.trees[nt_total++] = dominant * ntrees_per_forest + i;
+    st.n_trees = nt_total;
+    o.n_trees = nt_total;
+  }
+}
+
+// ------------------------------------------------------------ vote lists ----
+// getFacialFeaturesVotesMT vote filter (face_utils.cpp:276-301).  A wave walks the face's FFD leaves
+// [beg, end) in reference order (patch-major x-outer, tree-minor), 64 at a time; for each landmark a
+// ballot + popcount gives every voting lane its slot after cnt[i], so the compacted list keeps the
+// reference's vote order exactly.
 #ifndef FFD_VOTE_U
 #define FFD_VOTE_U 2
 #endif
+template <bool compact>
+__device__ __forceinline__ void votes_range(const FaceDesc& fd, const int32_t* __restrict__ L,
+                                            const uint4* __restrict__ leaf_rec, int bias_x, int bias_y, int T,
+                                            int step, int step_y, int half_patch, int beg, int end,
+                                            Vote* __restrict__ V, int64_t cap, int (&cnt)[NPARTS]) {
+  const int lane = __lane_id();
+  const int ny = fd.nmy;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   constexpr int U = FFD_VOTE_U;  // 64-item batches whose loads are in flight together
   // software pipeline over groups of U batches: the leaf ids of group g + 2 and the leaf records of
   // group g + 1 are in flight while group g is filtered
@@ -1349,7 +1480,7 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
       const int k = base + u * 64 + lane;
       G.leaf[u] = -1;
       G.vx0[u] = G.vy0[u] = 0;
-      if (k < total) {
+      if (k < end) {
         const int pr = idiv_small(k, T), xi = idiv_small(pr, ny), yi = pr - xi * ny;
         G.leaf[u] = L[k];  // leaves are stored in the reference order
         G.vx0[u] = fd.vox + xi * step + half_patch;  // patch.x + 15 (face_utils.cpp:257-293)
@@ -1372,12 +1503,12 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
     }
   };
   Grp cur, nxt;
-  load_ids(0, cur);
+  load_ids(beg, cur);
   load_recs(cur);
-  load_ids(64 * U, nxt);
-  for (int base = 0; base < total; base += 64 * U) {
+  load_ids(beg + 64 * U, nxt);
+  for (int base = beg; base < end; base += 64 * U) {
     Grp nn;
-    const bool more = base + 64 * U < total;
+    const bool more = base + 64 * U < end;
     if (more) {
       load_recs(nxt);
       load_ids(base + 2 * 64 * U, nn);
@@ -1417,7 +1548,91 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
     cur = nxt;
     nxt = nn;
   }
+}
+
+// One wave per face (large batches).
+template <bool compact>
+__global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ faces, int n_faces,
+                                               const int32_t* __restrict__ mp_leaf,
+                                               const uint4* __restrict__ leaf_rec, int bias_x,
+                                               int bias_y, const HpState* __restrict__ state,
+                                               int tslots, int step, int step_y, int half_patch, int n_parts,
+                                               Vote* __restrict__ votes, int32_t* __restrict__ vote_counts) {
+  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (f >= n_faces) return;
+  const FaceDesc& fd = faces[f];
+  if (!fd.valid) return;
+  const int n = fd.nmx * fd.nmy, T = state[f].n_trees;
+  int cnt[NPARTS];
+#pragma unroll
+  for (int i = 0; i < NPARTS; i++) cnt[i] = 0;
+  votes_range<compact>(fd, mp_leaf + fd.mp_off, leaf_rec, bias_x, bias_y, T, step, step_y, half_patch, 0, n * T,
+                       votes + fd.vote_off, (int64_t)tslots * n, cnt);
   if (lane < n_parts) {
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < NPARTS; i++)
+      if (i == lane) c = cnt[i];
+    vote_counts[(int64_t)f * NPARTS + lane] = c;
+  }
+}
+
+// A workgroup of 16 waves per face (small batches: single-face latency).  The face's leaf list is cut
+// into 16 contiguous segments of whole 64-item batches; every wave first counts its segment's votes
+// per landmark (the vote masks only), then, after a prefix over the waves, walks its segment again
+// writing each vote at its final slot.  Same order, same lists as k_votes.
+constexpr int VOTES_WG_WAVES = 16;
+template <bool compact>
+__global__ __launch_bounds__(64 * VOTES_WG_WAVES) void k_votes_wg(const FaceDesc* __restrict__ faces, int n_faces,
+                                                                 const int32_t* __restrict__ mp_leaf,
+                                                                 const uint4* __restrict__ leaf_rec, int bias_x,
+                                                                 int bias_y, const HpState* __restrict__ state,
+                                                                 int tslots, int step, int step_y, int half_patch,
+                                                                 int n_parts, Vote* __restrict__ votes,
+                                                                 int32_t* __restrict__ vote_counts) {
+  __shared__ int s_cnt[VOTES_WG_WAVES][NPARTS];
+  const int f = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (f >= n_faces) return;
+  const FaceDesc& fd = faces[f];
+  if (!fd.valid) return;  // whole workgroup
+  const int n = fd.nmx * fd.nmy, T = state[f].n_trees, total = n * T;
+  const int seg = (total + 64 * VOTES_WG_WAVES - 1) / (64 * VOTES_WG_WAVES) * 64;
+  const int beg = min(total, wv * seg), end = min(total, beg + seg);
+  const int32_t* L = mp_leaf + fd.mp_off;
+  // pass 1: this segment's votes per landmark (the masks, 4 batches in flight)
+  int cnt[NPARTS];
+#pragma unroll
+  for (int i = 0; i < NPARTS; i++) cnt[i] = 0;
+  for (int b0 = beg; b0 < end; b0 += 4 * 64) {
+    uint32_t mk[4];
+    int leaf[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int k = b0 + u * 64 + lane;
+      leaf[u] = k < end ? L[k] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) mk[u] = leaf[u] >= 0 ? leaf_rec[(int64_t)leaf[u] * (compact ? 2 : 4)].x : 0u;
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+#pragma unroll
+      for (int i = 0; i < NPARTS; i++) cnt[i] += __popcll(__ballot((mk[u] >> i) & 1u));
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < NPARTS; i++) s_cnt[wv][i] = cnt[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NPARTS; i++) {
+    int b = 0;
+    for (int w = 0; w < wv; w++) b += s_cnt[w][i];
+    cnt[i] = b;
+  }
+  // pass 2: the votes at their final slots
+  votes_range<compact>(fd, L, leaf_rec, bias_x, bias_y, T, step, step_y, half_patch, beg, end, votes + fd.vote_off,
+                       (int64_t)tslots * n, cnt);
+  if (wv == VOTES_WG_WAVES - 1 && lane < n_parts) {
     int c = 0;
 #pragma unroll
     for (int i = 0; i < NPARTS; i++)
@@ -1457,6 +1672,12 @@ constexpr int MS_RA = FFD_MS_RA;  // serial phase: LDS reads in flight ahead of 
 #endif
 #ifndef FFD_MS_K
 #define FFD_MS_K 4  // k_meanshift4: votes per lane per tile
+#endif
+#ifndef FFD_VOTES_WG_MAX
+#define FFD_VOTES_WG_MAX 64  // batches of up to 64 faces: k_votes_wg (16 waves per face)
+#endif
+#ifndef FFD_MS5_CHAINS
+#define FFD_MS5_CHAINS 640  // batches of up to 64 faces: k_meanshift5 (a workgroup per chain)
 #endif
 #ifndef FFD_MS_PROBE
 #define FFD_MS_PROBE 0  // timing probes (bits): 1 = no serial phase, 2 = cheap weights, 4 = no early convergence
@@ -1918,6 +2139,120 @@ __global__ __launch_bounds__(256) void k_meanshift4(const FaceDesc* __restrict__
   }
 }
 
+// MeanShift, chain-per-workgroup form for small batches (single-face latency): one 256-thread
+// workgroup runs ONE chain (a face's vote list for one landmark) through MeanShift::shift
+// (MeanShift.hpp:41-135), in tiles of 256 U votes double-buffered in LDS: all four waves compute tile
+// k + 1's terms (x*w, y*w, w) while lanes 0..2 of wave 0 add the three components of tile k in list order
+// (LDS reads one group of 8 ahead of the adds), one barrier per tile.  The sums are the reference's
+// sequential float sums bit for bit; the terms use ms_weight.  A batch of a few faces has only
+// 10 chains per face, so what bounds the pass is one chain's serial adds, not the term arithmetic.
+template <int U>
+__global__ __launch_bounds__(256) void k_meanshift5(const FaceDesc* __restrict__ faces, int n_faces, int tslots,
+                                                   int n_parts, float lamda, float lam_y, int max_iter, float stop,
+                                                   const Vote* __restrict__ votes, const int32_t* __restrict__ vote_counts,
+                                                   float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
+  constexpr int T = 256 * U;
+  __shared__ float4 term[2][T];
+  __shared__ float s_acc[3], s_m[2];
+  __shared__ int s_live;
+  const int tid = threadIdx.x;
+  const int f = blockIdx.x / NPARTS, part = blockIdx.x - f * NPARTS;
+  if (f >= n_faces || !faces[f].valid) return;  // whole workgroup
+  const FaceDesc& fd = faces[f];
+  const int cnt = part < n_parts ? vote_counts[(int64_t)f * NPARTS + part] : 0;
+  const Vote* vp = votes + fd.vote_off + (int64_t)part * tslots * fd.nmx * fd.nmy;
+  float mx = 0.f, my = 0.f;
+  for (int pass = -1; pass < max_iter; pass++) {
+    Vote v[U];
+    auto load = [&](int k0) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int k = k0 + tid + 256 * u;
+        if (k < cnt) v[u] = vp[k];
+      }
+    };
+    auto terms = [&](int buf, int k0) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int k = k0 + tid + 256 * u;
+        if (k < cnt) {
+          const float fx = (float)v[u].x, fy = (float)v[u].y;
+          const float w = pass < 0 ? v[u].w : ms_weight(mx, my, fx, fy, v[u].w, lamda, lam_y);
+          term[buf][tid + 256 * u] = make_float4(fx * w, fy * w, w, 0.f);
+        }
+      }
+    };
+    float acc = 0.f;
+    int buf = 0;
+    if (cnt > 0) {
+      load(0);
+      terms(0, 0);
+      if (T < cnt) load(T);
+    }
+    __syncthreads();
+    for (int k0 = 0; k0 < cnt; k0 += T, buf ^= 1) {
+      if (k0 + T < cnt) {
+        terms(buf ^ 1, k0 + T);
+        if (k0 + 2 * T < cnt) load(k0 + 2 * T);
+      }
+      if (tid < 3) {  // component tid of this tile's terms, in list order
+        const float* tp = reinterpret_cast<const float*>(&term[buf][0]) + tid;
+        const int n = min(T, cnt - k0);
+        int j = 0;
+        float a[8];
+        if (n >= 8) {
+#pragma unroll
+          for (int e = 0; e < 8; e++) a[e] = tp[e * 4];
+        }
+        for (; j + 16 <= n; j += 8) {
+          float b[8];
+#pragma unroll
+          for (int e = 0; e < 8; e++) b[e] = tp[(j + 8 + e) * 4];
+#pragma unroll
+          for (int e = 0; e < 8; e++) acc += a[e];
+#pragma unroll
+          for (int e = 0; e < 8; e++) a[e] = b[e];
+        }
+        if (j + 8 <= n) {
+#pragma unroll
+          for (int e = 0; e < 8; e++) acc += a[e];
+          j += 8;
+        }
+        for (; j < n; j++) acc += tp[j * 4];
+      }
+      __syncthreads();
+    }
+    if (tid < 3) s_acc[tid] = acc;
+    __syncthreads();
+    if (tid == 0) {
+      float ax = s_acc[0], ay = s_acc[1];
+      const float aw = s_acc[2];
+      if (aw > 0) { ax /= aw; ay /= aw; }
+      int live = 1;
+      if (pass >= 0) {
+        const float ddx = ax - mx, ddy = ay - my;
+        if (__builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) live = 0;  // converged
+      }
+      s_m[0] = ax;
+      s_m[1] = ay;
+      s_live = live;
+    }
+    __syncthreads();
+    mx = s_m[0];
+    my = s_m[1];
+    if (!s_live) break;
+  }
+  if (tid == 0) {
+    if (part < n_parts) {
+      ms_mean[((int64_t)f * NPARTS + part) * 2] = mx;
+      ms_mean[((int64_t)f * NPARTS + part) * 2 + 1] = my;
+    }
+    const float inv = 1.0f / fd.scale;  // FaceForest.cpp:255-257
+    out[f].points[part][0] = part < n_parts ? cv_round((float)cv_round(mx) * inv) : 0;
+    out[f].points[part][1] = part < n_parts ? cv_round((float)cv_round(my) * inv) : 0;
+  }
+}
+
 // ------------------------------------------------------------------ launch --
 void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s) {
   k_gray_resize<<<n, 256, 0, s>>>(faces, images, gray);
@@ -2073,6 +2408,14 @@ void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const 
     const int k = v ? std::atoi(v) : 8;
     return k == 4 || k == 16 ? k : 8;
   }();
+  static const int one_max = [] {  // faces up to which a workgroup reduces each face (k_hp_pose1)
+    const char* v = std::getenv("FFD_HP_ONE_MAX");
+    return v ? std::atoi(v) : 64;
+  }();
+  if (n <= one_max) {
+    k_hp_pose1<<<n, 256, 0, s>>>(faces, n, hp_leaf, hp_m, hp_trees, n_forests, ntrees_per_forest, state, out);
+    return;
+  }
   if (nf == 16)
     k_hp_pose<16><<<(n + 15) / 16, 256, 0, s>>>(faces, n, hp_leaf, hp_m, hp_trees, n_forests, ntrees_per_forest, state, out);
   else if (nf == 8)
@@ -2085,6 +2428,19 @@ void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const ui
                   int bias_x, int bias_y, const HpState* state,
                   int tslots, int step, int step_y, int half_patch, int n_parts, Vote* votes, int32_t* vote_counts,
                   hipStream_t s) {
+  static const int wg_max = [] {  // faces up to which a workgroup of 16 waves filters each face
+    const char* v = std::getenv("FFD_VOTES_WG_MAX");
+    return v ? std::atoi(v) : FFD_VOTES_WG_MAX;
+  }();
+  if (n <= wg_max) {
+    if (compact)
+      k_votes_wg<true><<<n, 64 * VOTES_WG_WAVES, 0, s>>>(faces, n, mp_leaf, leaf_rec, bias_x, bias_y, state, tslots, step,
+                                                         step_y, half_patch, n_parts, votes, vote_counts);
+    else
+      k_votes_wg<false><<<n, 64 * VOTES_WG_WAVES, 0, s>>>(faces, n, mp_leaf, leaf_rec, bias_x, bias_y, state, tslots, step,
+                                                          step_y, half_patch, n_parts, votes, vote_counts);
+    return;
+  }
   if (compact)
     k_votes<true><<<(n + 3) / 4, 256, 0, s>>>(faces, n, mp_leaf, leaf_rec, bias_x, bias_y, state, tslots, step, step_y,
                                               half_patch, n_parts, votes, vote_counts);
@@ -2097,15 +2453,26 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
                       int max_iter, float stop, const Vote* votes, const int32_t* vote_counts, float* ms_mean,
                       FaceOut* out, hipStream_t s) {
   (void)state;
-  // k_meanshift (1) when the batch has chains for >= 4 of its workgroups per CU (C2: 2,048 workgroups,
-  // 2.45 ms, where k_meanshift4 takes 3.1 ms: its fp64 term chains run at lower occupancy); else the
-  // wave-independent k_meanshift4 (4) (C4, 10,240 chains of ~30 k votes: 16.2 -> 9.4 ms; small batches)
+  // k_meanshift5 (5) for a few chains (single-face latency: one workgroup per chain); k_meanshift (1) when
+  // the batch has chains for >= 4 of its workgroups per CU (C2: 2,048 workgroups, 2.45 ms, where
+  // k_meanshift4 takes 3.1 ms: its fp64 term chains run at lower occupancy); else the wave-independent
+  // k_meanshift4 (4) (C4, 10,240 chains of ~30 k votes: 16.2 -> 9.4 ms)
   static const int forced = [] {
     const char* v = std::getenv("FFD_MS_KERNEL");
     return v ? std::atoi(v) : FFD_MS_DEFAULT;
   }();
-  const int which = forced ? forced : ((int64_t)n * NPARTS >= (int64_t)20 * 4 * 256 ? 1 : 4);
+  static const int64_t ms5_max = [] {  // chains up to which the chain-per-workgroup form runs
+    const char* v = std::getenv("FFD_MS5_CHAINS");
+    return v ? std::atoll(v) : (int64_t)FFD_MS5_CHAINS;
+  }();
+  const int64_t chains = (int64_t)n * NPARTS;
+  const int which = forced ? forced : (chains <= ms5_max ? 5 : chains >= (int64_t)20 * 4 * 256 ? 1 : 4);
   const float lam_y = lamda == 10.f ? 1.f / 10.f : 0.f;  // the verified fast quotient (ffd_div_rcp)
+  if (which == 5) {
+    k_meanshift5<4><<<(unsigned)chains, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes,
+                                                     vote_counts, ms_mean, out);
+    return;
+  }
   if (which == 1) {
     dim3 grid((n + MS_FACES - 1) / MS_FACES, NPARTS);
     k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes,
