@@ -510,6 +510,10 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   w.ms_mean.ensure((size_t)n * NPARTS * 2 * 4);
   w.vote_counts.ensure((size_t)n * NPARTS * 4);
   w.gabor_redo.ensure((size_t)n * 5 * 4);  // 5 scales
+  if (w.gabor_mm.n < (size_t)n * 5 * 64) {  // the banded instances leave their slots zeroed
+    w.gabor_mm.ensure((size_t)n * 5 * 64);
+    HIP_CHECK(hipMemsetAsync(w.gabor_mm.p, 0, w.gabor_mm.n, st));
+  }
   upload(w.faces, fds, st);
   HIP_CHECK(hipMemsetAsync(d_out, 0, (size_t)n * sizeof(FaceOut), st));
 
@@ -528,12 +532,12 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
     const hipStream_t s2 = cs(4 - nu);
     stage(1 + (4 - nu), s2, [&] {
       launch_gabor(nu, dfd, n, max_h, w.gray.as<uint8_t>(), gabor_coef.as<float>(), w.mag.as<float>(),
-                   w.chan.as<uint16_t>(), w.gabor_redo.as<int>(), gabor_exact, s2);
+                   w.chan.as<uint16_t>(), w.gabor_redo.as<int>(), gabor_exact, w.gabor_mm.as<uint32_t>(), s2);
     });
   }
   {
     const hipStream_t s2 = cs(5);
-    stage(6, s2, [&] { launch_integral(dfd, n, w.gray.as<uint8_t>(), w.chan.as<uint16_t>(), s2); });
+    stage(6, s2, [&] { launch_integral(dfd, n, max_h, w.gray.as<uint8_t>(), w.chan.as<uint16_t>(), s2); });
   }
   for (int i = 0; i < nfork; i++) {
     HIP_CHECK(hipEventRecord(w.fork_ev[1 + i], w.fork[i]));
@@ -1023,14 +1027,18 @@ ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t
     w.mag.ensure((size_t)NGABOR * H * PITCH * 4 + 256);
     w.chan.ensure((size_t)NCH * f.plane * 2 + 256);
     w.gabor_redo.ensure(5 * 4);
+    if (w.gabor_mm.n < 5 * 64) {
+      w.gabor_mm.ensure(5 * 64);
+      HIP_CHECK(hipMemsetAsync(w.gabor_mm.p, 0, w.gabor_mm.n, w.stream));
+    }
     std::vector<FaceDesc> one{f};
     upload(w.faces, one, w.stream);
     const FaceDesc* dfd = w.faces.as<FaceDesc>();
     launch_gray_resize(dfd, 1, e->scratch_a.as<uint8_t>(), w.gray.as<uint8_t>(), w.stream);
     for (int nu = 4; nu >= 0; nu--)
       launch_gabor(nu, dfd, 1, H, w.gray.as<uint8_t>(), e->gabor_coef.as<float>(), w.mag.as<float>(),
-                   w.chan.as<uint16_t>(), w.gabor_redo.as<int>(), e->gabor_exact, w.stream);
-    launch_integral(dfd, 1, w.gray.as<uint8_t>(), w.chan.as<uint16_t>(), w.stream);
+                   w.chan.as<uint16_t>(), w.gabor_redo.as<int>(), e->gabor_exact, w.gabor_mm.as<uint32_t>(), w.stream);
+    launch_integral(dfd, 1, H, w.gray.as<uint8_t>(), w.chan.as<uint16_t>(), w.stream);
     HIP_CHECK(hipGetLastError());
     std::vector<uint16_t> v((size_t)NCH * f.plane);
     HIP_CHECK(hipMemcpyAsync(v.data(), w.chan.p, v.size() * 2, hipMemcpyDeviceToHost, w.stream));

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void k_gray_resize(const FaceDesc* __restrict_
     return gray_px(img + (int64_t)(fd.by + y) * fd.img_stride + 3 * (fd.bx + x));
   };
   const int sw = fd.bw, sh = fd.bh;
-  for (int i = threadIdx.x; i < fd.W * fd.H; i += blockDim.x) {
+  for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < fd.W * fd.H; i += gridDim.y * blockDim.x) {
     int dy = i / fd.W, dx = i % fd.W;
     int v;
     if (fd.mode == 0) {
@@ -190,15 +190,26 @@ __device__ __forceinline__ void integral_scan(uint16_t* __restrict__ out, int W,
 
 // gray (channel 0) and the two Sobel channels (36 d/dy, 37 d/dx); the 35 Gabor channels are
 // integrated by the Gabor kernels themselves.  One 4-wave workgroup per face (the 4th wave idles).
+// STAGE (small batches): the face's gray rows are first copied to LDS by all four waves, so the three
+// sequential scans read their values at LDS rather than L2 latency.
+template <bool STAGE>
 __global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ faces,
                                                   const uint8_t* __restrict__ gray,
                                                   uint16_t* __restrict__ chan) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_gray[];  // STAGE: H x PITCH
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const FaceDesc fd = faces[blockIdx.x];
-  if (!fd.valid || fd.nochan || wv >= 3) return;
-  const int c = wv == 0 ? 0 : 35 + wv;
+  if (!fd.valid || fd.nochan) return;
   const int W = fd.W, H = fd.H, x0 = 2 * lane;
   const uint8_t* g = gray + fd.gray_off;
+  if (STAGE) {
+    for (int i = threadIdx.x; i < H * (PITCH / 16); i += 256)
+      reinterpret_cast<uint4*>(s_gray)[i] = reinterpret_cast<const uint4*>(g)[i];
+    __syncthreads();
+    g = s_gray;
+  }
+  if (wv >= 3) return;
+  const int c = wv == 0 ? 0 : 35 + wv;
   integral_scan(chan + fd.ch_off + (int64_t)c * fd.plane, W, H, lane, fd.fint != 0, [&](int y0, uint32_t* v0, uint32_t* v1) {
 #pragma unroll
     for (int b = 0; b < 8; b++) {
@@ -351,6 +362,54 @@ __device__ __forceinline__ void minmax_update(uint32_t& mn, uint32_t& mx, float 
   }
 }
 
+// Banded (SPLIT) Gabor instances for small batches: a face's bands (sep) or tiles (7x7) are spread over
+// gridDim.y workgroups, each of which writes its magnitudes and folds its min / max (and the fast
+// instance's tiny-magnitude vote) into the face's 16-word slot mm = [~min x 7, max x 7, flag, arrivals]
+// with device-scope atomics; the workgroup that arrives last takes the totals (resetting the slot to
+// zero for the next launch) and runs the normalise / integrate epilogue over the whole face.
+// Returns true in that workgroup only; its thread 0 then holds the face's min / max in mn / mx.
+template <bool EXACT>
+__device__ __forceinline__ bool split_finish(uint32_t (&mn)[7], uint32_t (&mx)[7], uint32_t tiny, int force,
+                                             uint32_t* __restrict__ mm, int nwg, int* __restrict__ redo_f) {
+  __shared__ uint32_t s_mm[16];
+  __shared__ int s_last;
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (tid < 16) s_mm[tid] = 0u;
+  __syncthreads();
+#pragma unroll
+  for (int o = 0; o < 7; o++) {
+    uint32_t a = mn[o], b = mx[o];
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+      a = min(a, (uint32_t)__shfl_xor((int)a, sh));
+      b = max(b, (uint32_t)__shfl_xor((int)b, sh));
+    }
+    if (lane == 0) {
+      atomicMax(&s_mm[o], ~a);
+      atomicMax(&s_mm[7 + o], b);
+    }
+  }
+  const int any = EXACT ? 0 : __syncthreads_or(tiny < 0x0F7FFFFFu || force ? 1 : 0);
+  __syncthreads();
+  if (tid < 14 && s_mm[tid]) atomicMax(&mm[tid], s_mm[tid]);
+  if (tid == 14 && any) atomicOr(&mm[14], 1u);
+  __threadfence();  // this workgroup's magnitudes and slot updates before its arrival
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(&mm[15], 1u) == (uint32_t)(nwg - 1) ? 1 : 0;
+  __syncthreads();
+  if (!s_last) return false;
+  __threadfence();  // every other workgroup's magnitudes are visible from here
+  if (tid < 16) s_mm[tid] = atomicExch(&mm[tid], 0u);
+  __syncthreads();
+#pragma unroll
+  for (int o = 0; o < 7; o++) {
+    mn[o] = tid == 0 ? ~s_mm[o] : 0xFFFFFFFFu;
+    mx[o] = tid == 0 ? s_mm[7 + o] : 0u;
+  }
+  if (!EXACT && tid == 0) *redo_f = s_mm[14] != 0u ? 1 : 0;
+  return true;
+}
+
 // 7x7 (scale 0): OpenCV 2.4.9's direct Filter2D (49 taps < dft_filter_size 50), restated bit-exactly.
 // Coefficients (host-built from createKernel, FeatureChannelFactory.hpp:186-251), 16 floats per tap
 // in row-major order: [re0, im0, re1, im1, ..., re6, im6, 0, 0].
@@ -360,12 +419,13 @@ __device__ __forceinline__ void minmax_update(uint32_t& mn, uint32_t& mx, float 
 // operands are wave-uniform scalar loads (SGPR pairs).
 constexpr int GB_TX = 64, GB_TY = 32, GB_THREADS = 512;
 
-template <bool EXACT>
+template <bool EXACT, bool SPLIT>
 __global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restrict__ faces,
                                                        const uint8_t* __restrict__ gray,
                                                        const float4* __restrict__ coef_g,
                                                        float* __restrict__ mag,
-                                                       uint16_t* __restrict__ chan, int* __restrict__ redo, int force) {
+                                                       uint16_t* __restrict__ chan, int* __restrict__ redo, int force,
+                                                       uint32_t* __restrict__ split_mm) {
   constexpr int R = 3;
   // row stride (floats) == 1 mod 4: the 4 rows a 32-lane group touches fall on disjoint banks
   constexpr int LW = ((GB_TX + 2 * R + 3) / 4) * 4 + 1;
@@ -376,13 +436,21 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restric
   if (EXACT && !redo[blockIdx.x]) return;  // the fast instance's mag_sqrt was exact for this face
   uint32_t tiny = 0xFFFFFFFFu;
   const int tiles_x = (fd.W + GB_TX - 1) / GB_TX, tiles = tiles_x * ((fd.H + GB_TY - 1) / GB_TY);
+  int tl0 = 0, tl1 = tiles, nwg = 1;
+  if (SPLIT) {  // this workgroup's share of the face's tiles
+    const int per = (tiles + gridDim.y - 1) / gridDim.y;
+    nwg = (tiles + per - 1) / per;
+    if ((int)blockIdx.y >= nwg) return;
+    tl0 = blockIdx.y * per;
+    tl1 = min(tiles, tl0 + per);
+  }
   const uint8_t* g = gray + fd.gray_off;
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   uint32_t mn[7], mx[7];
 #pragma unroll
   for (int o = 0; o < 7; o++) { mn[o] = 0xFFFFFFFFu; mx[o] = 0u; }
 #pragma unroll 1
-  for (int tl = 0; tl < tiles; tl++) {
+  for (int tl = tl0; tl < tl1; tl++) {
     const int tx0 = (tl % tiles_x) * GB_TX, ty0 = (tl / tiles_x) * GB_TY;
     __syncthreads();  // the previous tile's reads of `tile` are done
     for (int i = threadIdx.x; i < LH * (GB_TX + 2 * R); i += GB_THREADS) {
@@ -436,7 +504,13 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restric
             make_float4(m4[0], m4[1], m4[2], m4[3]);
     }
   }
-  mag_flag<EXACT>(tiny, redo, force);
+  if (SPLIT) {
+    if (!split_finish<EXACT>(mn, mx, tiny, force, split_mm + ((int64_t)blockIdx.x * 5 + 0) * 16, nwg,
+                             redo + blockIdx.x))
+      return;
+  } else {
+    mag_flag<EXACT>(tiny, redo, force);
+  }
   gabor_normalise_integrate<GB_THREADS / 64>(fd, 0, mn, mx, mag, chan);
 }
 
@@ -458,6 +532,12 @@ constexpr int GS_THREADS = 256, GS_BY = 8;
 #ifndef FFD_GABOR_PROBE
 #define FFD_GABOR_PROBE 0
 #endif
+#ifndef FFD_GABOR_SPLIT_MAX
+#define FFD_GABOR_SPLIT_MAX 16  // batches of up to 16 faces: banded Gabor instances (SPLIT)
+#endif
+#ifndef FFD_GABOR_SPLIT_WG
+#define FFD_GABOR_SPLIT_WG 16   // workgroups per face and scale in the banded instances
+#endif
 
 
 template <int R> struct GSep {
@@ -471,12 +551,14 @@ template <int R> struct GSep {
 // TALL: the instance for faces taller than MAX_FACE_H (box aspect h/w > 4.8), whose padded face does not
 // fit the LDS: each band stages only its GS_BY + 2R rows (4x re-staging at 25x25; such faces are rare).
 // Each instance skips the other's faces.
-template <int W, bool EXACT, bool TALL>
+template <int W, bool EXACT, bool TALL, bool SPLIT = false>
 __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __restrict__ faces,
                                                           const uint8_t* __restrict__ gray,
                                                           const float* __restrict__ coef,
                                                           float* __restrict__ mag,
-                                                          uint16_t* __restrict__ chan, int* __restrict__ redo, int force) {
+                                                          uint16_t* __restrict__ chan, int* __restrict__ redo, int force,
+                                                          uint32_t* __restrict__ split_mm) {
+  static_assert(!(TALL && SPLIT), "tall faces are not banded across workgroups");
   constexpr int R = (W - 1) / 2;
   using C = GSep<R>;
   constexpr int NU = W == 9 ? 1 : W == 13 ? 2 : W == 19 ? 3 : 4;
@@ -520,12 +602,21 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
       *reinterpret_cast<uint32_t*>(&gface[r * C::GP + 4 * j]) = v;
     }
   };
-  // the whole padded face, once: rows up to the last band's end (ceil(FH / GS_BY) * GS_BY + 2R: every
-  // row the V pass reads is staged)
-  if (!TALL) stage_rows(0, (FH + GS_BY - 1) / GS_BY * GS_BY + 2 * R);
+  // this workgroup's rows [yb, ye): the whole face, or (SPLIT) its share of the face's bands
+  int yb = 0, ye = FH, nwg = 1;
+  if (SPLIT) {
+    const int nbands = (FH + GS_BY - 1) / GS_BY, per = (nbands + gridDim.y - 1) / gridDim.y;
+    nwg = (nbands + per - 1) / per;
+    if ((int)blockIdx.y >= nwg) return;
+    yb = blockIdx.y * per * GS_BY;
+    ye = min(FH, yb + per * GS_BY);
+  }
+  // the padded rows of those bands, once: up to the last band's end (whole bands + 2R: every row the V
+  // pass reads is staged)
+  if (!TALL) stage_rows(yb, (ye - yb + GS_BY - 1) / GS_BY * GS_BY + 2 * R);
 
 #pragma unroll 1
-  for (int y0 = 0; y0 < (FFD_GABOR_PROBE == 5 ? 0 : FH); y0 += GS_BY) {  // probe 5: epilogue only
+  for (int y0 = yb; y0 < (FFD_GABOR_PROBE == 5 ? 0 : ye); y0 += GS_BY) {  // probe 5: epilogue only
     __syncthreads();  // the face is staged; the previous H pass is done with vg / vq
     if (TALL) {       // (the previous V pass is done with gface: the barrier before the H pass)
       stage_rows(y0, GS_BY + 2 * R);
@@ -536,7 +627,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
     for (int i = tid; i < (FFD_GABOR_PROBE == 3 ? 0 : GS_BY * C::SC); i += GS_THREADS) {
       const int r = i / C::SC, cc = i - r * C::SC;
       if (cc >= NPC) continue;
-      const uint8_t* col = &gface[((TALL ? 0 : y0) + r + R) * C::GP + cc];
+      const uint8_t* col = &gface[((TALL ? 0 : y0 - yb) + r + R) * C::GP + cc];
       float vgv = 0.f;
       f2 vqv[4];
 #pragma unroll
@@ -650,7 +741,13 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
   if (mn[0] == 0x12345u && mx[1] == 0x6789u) mag[0] = 0.f;
   return;
 #endif
-  mag_flag<EXACT>(tiny, redo, force);
+  if (SPLIT) {
+    if (!split_finish<EXACT>(mn, mx, tiny, force, split_mm + ((int64_t)blockIdx.x * 5 + NU) * 16, nwg,
+                             redo + blockIdx.x))
+      return;
+  } else {
+    mag_flag<EXACT>(tiny, redo, force);
+  }
   gabor_normalise_integrate<GS_THREADS / 64>(fd, NU, mn, mx, mag, chan);
 }
 
@@ -1135,6 +1232,53 @@ __global__ __launch_bounds__(256) void k_walk_fint(const FaceDesc* __restrict__ 
   }
 }
 
+// Sequential float sum acc += tp[0] + ... + tp[n - 1] in index order (one lane; tp 16-byte aligned):
+// ds_read_b128 of 4 values at a time, a group of G reads in flight ahead of the adds.
+__device__ __forceinline__ float serial_sum(const float* __restrict__ tp, int n, float acc) {
+  constexpr int G = 4;
+  const float4* t4 = reinterpret_cast<const float4*>(tp);
+  const int n4 = n >> 2;
+  int j = 0;
+  float4 a[G];
+  if (n4 >= G) {
+#pragma unroll
+    for (int e = 0; e < G; e++) a[e] = t4[e];
+  }
+  for (; j + 2 * G <= n4; j += G) {
+    float4 b[G];
+#pragma unroll
+    for (int e = 0; e < G; e++) b[e] = t4[j + G + e];
+#pragma unroll
+    for (int e = 0; e < G; e++) {
+      acc += a[e].x;
+      acc += a[e].y;
+      acc += a[e].z;
+      acc += a[e].w;
+    }
+#pragma unroll
+    for (int e = 0; e < G; e++) a[e] = b[e];
+  }
+  if (j + G <= n4) {
+#pragma unroll
+    for (int e = 0; e < G; e++) {
+      acc += a[e].x;
+      acc += a[e].y;
+      acc += a[e].z;
+      acc += a[e].w;
+    }
+    j += G;
+  }
+  for (; j < n4; j++) {
+    const float4 x = t4[j];
+    acc += x.x;
+    acc += x.y;
+    acc += x.z;
+    acc += x.w;
+  }
+  for (int q = n4 * 4; q < n; q++) acc += tp[q];
+  return acc;
+}
+
 // -------------------------------------------------- head pose + tree choice --
 // getHeadPoseVotesMT reduction (face_utils.cpp:218-241) + areaUnderCurve (face_utils.cpp:304-323)
 // + tree selection (FaceForest.cpp:214-250).  A 256-thread workgroup per HP_FACES faces.  The
@@ -1308,22 +1452,23 @@ __global__ __launch_bounds__(256) void k_hp_pose(const FaceDesc* __restrict__ fa
   }
 }
 
-// The same reduction for one face per workgroup (small batches: single-face latency).  The face's leaf
-// values arrive in tiles of 1024 leaves (every thread gathers 4, values one tile ahead), double-buffered
-// in LDS as (m, m * m); lanes 0 and 1 of wave 0 add the two components in leaf order (LDS reads one group
-// of 8 ahead) while the other waves gather the next tile.  The pose-bin integrals: lane b walks bin b's
+// The same reduction for one face per workgroup (small batches: single-face latency).  Waves 1..3
+// gather the face's leaf values in tiles of 768 leaves (4 per thread, values one tile ahead) into LDS
+// (component-major: m and m * m planes, double-buffered); lanes 0 and 1 of wave 0 add the two planes in
+// leaf order (serial_sum) while the next tile is gathered.  The pose-bin integrals: lane b walks bin b's
 // abscissae (x += step, sequential as the reference's loop), every thread evaluates the Gaussian terms,
 // lane b adds them in order; lane 0 selects the trees.
 __global__ __launch_bounds__(256) void k_hp_pose1(const FaceDesc* __restrict__ faces, int n_faces,
                                                   const int32_t* __restrict__ hp_leaf, const float* __restrict__ hp_m,
                                                   int hp_trees, int n_forests, int ntrees_per_forest,
                                                   HpState* __restrict__ state, FaceOut* __restrict__ out) {
-  constexpr int T1 = 1024, U1 = T1 / 256, NX = 224;  // bins span <= 2.15 / 0.01 + 1 abscissae
-  __shared__ float2 tv[2][T1];
+  constexpr int NT = 192, U1 = 4, T1 = NT * U1, NX = 224;  // bins span <= 2.15 / 0.01 + 1 abscissae
+  __shared__ __attribute__((aligned(16))) float tv[2][2][T1];
   __shared__ double s_x[5][NX], s_t[5][NX];
   __shared__ int s_nx[5], s_cnt[4];
   __shared__ float s_sum[2], s_area[8];
-  const int f = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int f = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, tt = tid - 64;
+  const bool gather_thread = tid >= 64;
   if (f >= n_faces) return;
   const FaceDesc& fd = faces[f];
   FaceOut& o = out[f];
@@ -1339,56 +1484,36 @@ __global__ __launch_bounds__(256) void k_hp_pose1(const FaceDesc* __restrict__ f
   auto gather = [&](int k0) {
     int id[U1];
 #pragma unroll
-    for (int u = 0; u < U1; u++) id[u] = k0 + tid + 256 * u < total ? ids[k0 + tid + 256 * u] : -1;
+    for (int u = 0; u < U1; u++) id[u] = k0 + tt + NT * u < total ? ids[k0 + tt + NT * u] : -1;
 #pragma unroll
     for (int u = 0; u < U1; u++) v[u] = id[u] >= 0 ? hp_m[id[u]] : -1.f;  // -1: filtered leaf or past the end
   };
-  auto put = [&](int buf, int k0) {
+  auto put = [&](int buf) {
 #pragma unroll
     for (int u = 0; u < U1; u++) {
       const bool in = v[u] >= 0.f;
       const float m = in ? v[u] : 0.f;  // filtered leaves add +0 (a non-negative float sum is unchanged)
       count += in ? 1 : 0;
-      tv[buf][tid + 256 * u] = make_float2(m, in ? m * m : 0.f);
+      tv[buf][0][tt + NT * u] = m;
+      tv[buf][1][tt + NT * u] = in ? m * m : 0.f;
     }
   };
   float acc = 0.f;
   int buf = 0;
-  if (total > 0) {
+  if (gather_thread && total > 0) {
     gather(0);
-    put(0, 0);
+    put(0);
     if (T1 < total) gather(T1);
   }
   __syncthreads();
   for (int k0 = 0; k0 < total; k0 += T1, buf ^= 1) {
-    if (k0 + T1 < total) {
-      put(buf ^ 1, k0 + T1);
-      if (k0 + 2 * T1 < total) gather(k0 + 2 * T1);
-    }
-    if (tid < 2) {  // component tid (sum m, sum m * m) in leaf order
-      const float* tp = reinterpret_cast<const float*>(&tv[buf][0]) + tid;
-      const int n = min(T1, total - k0);
-      int j = 0;
-      float a[8];
-      if (n >= 8) {
-#pragma unroll
-        for (int e = 0; e < 8; e++) a[e] = tp[e * 2];
+    if (gather_thread) {
+      if (k0 + T1 < total) {
+        put(buf ^ 1);
+        if (k0 + 2 * T1 < total) gather(k0 + 2 * T1);
       }
-      for (; j + 16 <= n; j += 8) {
-        float b[8];
-#pragma unroll
-        for (int e = 0; e < 8; e++) b[e] = tp[(j + 8 + e) * 2];
-#pragma unroll
-        for (int e = 0; e < 8; e++) acc += a[e];
-#pragma unroll
-        for (int e = 0; e < 8; e++) a[e] = b[e];
-      }
-      if (j + 8 <= n) {
-#pragma unroll
-        for (int e = 0; e < 8; e++) acc += a[e];
-        j += 8;
-      }
-      for (; j < n; j++) acc += tp[j * 2];
+    } else if (tid < 2) {  // plane tid (sum m, sum m * m) in leaf order
+      acc = serial_sum(&tv[buf][tid][0], min(T1, total - k0), acc);
     }
     __syncthreads();
   }
@@ -2141,21 +2266,22 @@ __global__ __launch_bounds__(256) void k_meanshift4(const FaceDesc* __restrict__
 
 // MeanShift, chain-per-workgroup form for small batches (single-face latency): one 256-thread
 // workgroup runs ONE chain (a face's vote list for one landmark) through MeanShift::shift
-// (MeanShift.hpp:41-135), in tiles of 256 U votes double-buffered in LDS: all four waves compute tile
-// k + 1's terms (x*w, y*w, w) while lanes 0..2 of wave 0 add the three components of tile k in list order
-// (LDS reads one group of 8 ahead of the adds), one barrier per tile.  The sums are the reference's
-// sequential float sums bit for bit; the terms use ms_weight.  A batch of a few faces has only
-// 10 chains per face, so what bounds the pass is one chain's serial adds, not the term arithmetic.
+// (MeanShift.hpp:41-135), in tiles of 192 U votes double-buffered in LDS (component-major: x*w, y*w, w
+// planes): waves 1..3 compute tile k + 1's terms while lanes 0..2 of wave 0 add the three components of
+// tile k in list order (serial_sum), one barrier per tile.  The sums are the reference's sequential
+// float sums bit for bit; the terms use ms_weight.  A batch of a few faces has only 10 chains per face,
+// so what bounds the pass is one chain's serial adds, not the term arithmetic.
 template <int U>
 __global__ __launch_bounds__(256) void k_meanshift5(const FaceDesc* __restrict__ faces, int n_faces, int tslots,
                                                    int n_parts, float lamda, float lam_y, int max_iter, float stop,
                                                    const Vote* __restrict__ votes, const int32_t* __restrict__ vote_counts,
                                                    float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
-  constexpr int T = 256 * U;
-  __shared__ float4 term[2][T];
+  constexpr int NT = 192, T = NT * U;
+  __shared__ __attribute__((aligned(16))) float tc[2][3][T];
   __shared__ float s_acc[3], s_m[2];
   __shared__ int s_live;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, tt = tid - 64;
+  const bool term_thread = tid >= 64;
   const int f = blockIdx.x / NPARTS, part = blockIdx.x - f * NPARTS;
   if (f >= n_faces || !faces[f].valid) return;  // whole workgroup
   const FaceDesc& fd = faces[f];
@@ -2167,58 +2293,39 @@ __global__ __launch_bounds__(256) void k_meanshift5(const FaceDesc* __restrict__
     auto load = [&](int k0) {
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const int k = k0 + tid + 256 * u;
+        const int k = k0 + tt + NT * u;
         if (k < cnt) v[u] = vp[k];
       }
     };
     auto terms = [&](int buf, int k0) {
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const int k = k0 + tid + 256 * u;
+        const int k = k0 + tt + NT * u;
         if (k < cnt) {
           const float fx = (float)v[u].x, fy = (float)v[u].y;
           const float w = pass < 0 ? v[u].w : ms_weight(mx, my, fx, fy, v[u].w, lamda, lam_y);
-          term[buf][tid + 256 * u] = make_float4(fx * w, fy * w, w, 0.f);
+          tc[buf][0][tt + NT * u] = fx * w;
+          tc[buf][1][tt + NT * u] = fy * w;
+          tc[buf][2][tt + NT * u] = w;
         }
       }
     };
     float acc = 0.f;
     int buf = 0;
-    if (cnt > 0) {
+    if (term_thread && cnt > 0) {
       load(0);
       terms(0, 0);
       if (T < cnt) load(T);
     }
     __syncthreads();
     for (int k0 = 0; k0 < cnt; k0 += T, buf ^= 1) {
-      if (k0 + T < cnt) {
-        terms(buf ^ 1, k0 + T);
-        if (k0 + 2 * T < cnt) load(k0 + 2 * T);
-      }
-      if (tid < 3) {  // component tid of this tile's terms, in list order
-        const float* tp = reinterpret_cast<const float*>(&term[buf][0]) + tid;
-        const int n = min(T, cnt - k0);
-        int j = 0;
-        float a[8];
-        if (n >= 8) {
-#pragma unroll
-          for (int e = 0; e < 8; e++) a[e] = tp[e * 4];
+      if (term_thread) {
+        if (k0 + T < cnt) {
+          terms(buf ^ 1, k0 + T);
+          if (k0 + 2 * T < cnt) load(k0 + 2 * T);
         }
-        for (; j + 16 <= n; j += 8) {
-          float b[8];
-#pragma unroll
-          for (int e = 0; e < 8; e++) b[e] = tp[(j + 8 + e) * 4];
-#pragma unroll
-          for (int e = 0; e < 8; e++) acc += a[e];
-#pragma unroll
-          for (int e = 0; e < 8; e++) a[e] = b[e];
-        }
-        if (j + 8 <= n) {
-#pragma unroll
-          for (int e = 0; e < 8; e++) acc += a[e];
-          j += 8;
-        }
-        for (; j < n; j++) acc += tp[j * 4];
+      } else if (tid < 3) {  // component tid of this tile's terms, in list order
+        acc = serial_sum(&tc[buf][tid][0], min(T, cnt - k0), acc);
       }
       __syncthreads();
     }
@@ -2255,7 +2362,8 @@ __global__ __launch_bounds__(256) void k_meanshift5(const FaceDesc* __restrict__
 
 // ------------------------------------------------------------------ launch --
 void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s) {
-  k_gray_resize<<<n, 256, 0, s>>>(faces, images, gray);
+  // small batches: a face's pixels spread over 8 workgroups (single-face latency)
+  k_gray_resize<<<dim3(n, n <= FFD_GABOR_SPLIT_MAX ? 8 : 1), 256, 0, s>>>(faces, images, gray);
 }
 
 // dynamic LDS of k_gabor_sep: the padded u8 face of the tallest face of the batch, its rows rounded up
@@ -2265,26 +2373,53 @@ int gabor_face_lds(int R, int max_h) {
 }
 
 void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t* gray, const float* coef, float* mag,
-                  uint16_t* chan, int* redo, int force_exact, hipStream_t s) {
+                  uint16_t* chan, int* redo, int force_exact, uint32_t* split_mm, hipStream_t s) {
   if (n <= 0) return;
   const float* c = coef + GABOR_OFFS[nu];
+  // small batches: a face's bands / tiles spread over workgroups (split_mm: n x 5 zeroed 16-word slots)
+  static const int split_max = [] {
+    const char* v = std::getenv("FFD_GABOR_SPLIT_MAX");
+    return v ? std::atoi(v) : FFD_GABOR_SPLIT_MAX;
+  }();
+  const bool split = split_mm && n <= split_max && max_h <= MAX_FACE_H;
   // the fast instance, then the exact one over the faces it flagged (an empty pass in practice)
   int* rd = redo + (int64_t)nu * n;  // one flag array per scale: the scales may run on fork streams
   for (int exact = 0; exact < 2; exact++) {
+    if (split) {
+      const int nbands = (max_h + GS_BY - 1) / GS_BY, nb = std::min(nbands, FFD_GABOR_SPLIT_WG);
+      const int per = (nbands + nb - 1) / nb;
+#define FFD_GABOR_SPLIT(WV, RV)                                                                                   \
+  (exact ? k_gabor_sep<WV, true, false, true> : k_gabor_sep<WV, false, false, true>)<<<dim3(n, nb), GS_THREADS,     \
+      (per * GS_BY + 2 * RV) * ((PITCH + 2 * RV + 3) / 4 * 4), s>>>(faces, gray, c, mag, chan, rd, force_exact, split_mm)
+      switch (nu) {
+        case 4: FFD_GABOR_SPLIT(25, 12); break;
+        case 3: FFD_GABOR_SPLIT(19, 9); break;
+        case 2: FFD_GABOR_SPLIT(13, 6); break;
+        case 1: FFD_GABOR_SPLIT(9, 4); break;
+        default: {
+          const int tiles = ((PITCH - 3 + GB_TX - 1) / GB_TX) * ((max_h + GB_TY - 1) / GB_TY);
+          (exact ? k_gabor7<true, true> : k_gabor7<false, true>)<<<dim3(n, tiles), GB_THREADS, 0, s>>>(
+              faces, gray, reinterpret_cast<const float4*>(c), mag, chan, rd, force_exact, split_mm);
+          break;
+        }
+      }
+#undef FFD_GABOR_SPLIT
+      continue;
+    }
 #define FFD_GABOR_LAUNCH(WV, RV)                                                                              \
   (exact ? k_gabor_sep<WV, true, false> : k_gabor_sep<WV, false, false>)<<<n, GS_THREADS, gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, \
-                                                                                                  mag, chan, rd, force_exact); \
+                                                                                                  mag, chan, rd, force_exact, nullptr); \
   if (max_h > MAX_FACE_H)                                                                                        \
     (exact ? k_gabor_sep<WV, true, true> : k_gabor_sep<WV, false, true>)<<<n, GS_THREADS, (GS_BY + 2 * RV) * ((PITCH + 2 * RV + 3) / 4 * 4), s>>>(faces, gray, c, \
-                                                                                                  mag, chan, rd, force_exact)
+                                                                                                  mag, chan, rd, force_exact, nullptr)
     switch (nu) {
       case 4: FFD_GABOR_LAUNCH(25, 12); break;
       case 3: FFD_GABOR_LAUNCH(19, 9); break;
       case 2: FFD_GABOR_LAUNCH(13, 6); break;
       case 1: FFD_GABOR_LAUNCH(9, 4); break;
       default:
-        (exact ? k_gabor7<true> : k_gabor7<false>)<<<n, GB_THREADS, 0, s>>>(faces, gray, reinterpret_cast<const float4*>(c),
-                                                                          mag, chan, rd, force_exact);
+        (exact ? k_gabor7<true, false> : k_gabor7<false, false>)<<<n, GB_THREADS, 0, s>>>(faces, gray, reinterpret_cast<const float4*>(c),
+                                                                          mag, chan, rd, force_exact, nullptr);
         break;
     }
 #undef FFD_GABOR_LAUNCH
@@ -2307,8 +2442,12 @@ void launch_check_mag_sqrt(uint32_t lo, uint32_t n, uint32_t* bad, int blocks, h
   k_check_mag_sqrt<<<blocks, 256, 0, s>>>(lo, n, bad);
 }
 
-void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t* chan, hipStream_t s) {
-  if (n > 0) k_integral<<<n, 256, 0, s>>>(faces, gray, chan);
+void launch_integral(const FaceDesc* faces, int n, int max_h, const uint8_t* gray, uint16_t* chan, hipStream_t s) {
+  if (n <= 0) return;
+  if (n <= FFD_GABOR_SPLIT_MAX && max_h <= MAX_FACE_H)  // small batches: the face staged in LDS (<= 75 KB)
+    k_integral<true><<<n, 256, (size_t)max_h * PITCH, s>>>(faces, gray, chan);
+  else
+    k_integral<false><<<n, 256, 0, s>>>(faces, gray, chan);
 }
 
 int traverse_lds_bytes(TravShape g, int step, int step_y) {
@@ -2364,7 +2503,8 @@ hipError_t set_gabor_lds_limit(int bytes) {
   const void* fns[] = {(const void*)k_gabor_sep<9, false, false>,  (const void*)k_gabor_sep<13, false, false>,
                        (const void*)k_gabor_sep<19, false, false>, (const void*)k_gabor_sep<25, false, false>,
                        (const void*)k_gabor_sep<9, true, false>,   (const void*)k_gabor_sep<13, true, false>,
-                       (const void*)k_gabor_sep<19, true, false>,  (const void*)k_gabor_sep<25, true, false>};
+                       (const void*)k_gabor_sep<19, true, false>,  (const void*)k_gabor_sep<25, true, false>,
+                       (const void*)k_integral<true>};
   for (const void* f : fns) {
     hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (r != hipSuccess) e = r;

@@ -28,10 +28,10 @@ void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uin
 // max_h: the tallest scaled face of the batch (sizes the padded-face LDS copy)
 void launch_check_mag_sqrt(uint32_t lo, uint32_t n, uint32_t* bad, int blocks, hipStream_t s);
 void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t* gray, const float* coef, float* mag,
-                  uint16_t* chan, int* redo, int force_exact, hipStream_t s);
+                  uint16_t* chan, int* redo, int force_exact, uint32_t* split_mm, hipStream_t s);
 hipError_t set_gabor_lds_limit(int bytes);
 // integral channels 0 (gray), 36, 37 (Sobel)
-void launch_integral(const FaceDesc* faces, int n, const uint8_t* gray, uint16_t* chan, hipStream_t s);
+void launch_integral(const FaceDesc* faces, int n, int max_h, const uint8_t* gray, uint16_t* chan, hipStream_t s);
 constexpr int TRAV_LDS_CAP = 160 * 1024;  // one traversal workgroup per CU: all of its LDS
 // patch block of a traversal workgroup: gx x gy patches of one face's grid
 struct TravShape {
