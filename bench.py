@@ -432,6 +432,46 @@ def dry_run(args, world, rank):
     dist.destroy_process_group()
 
 
+def run_group(args):
+    """--group: the single-process multi-device shape of the C ABI (include/ffd.h
+    ffd_group_*): one engine per device, faces sharded in contiguous blocks, the records gathered to
+    device 0 with ONE RCCL gather and copied to the host.  A step = ffd_group_analyze_faces over
+    --gpus x 4096 C2 crops from pageable host memory (host-inclusive, like the reference's C++
+    caller); weak scaling.  The driver's N-GPU runs use the one-rank-per-GPU shape instead."""
+    import torch
+
+    import face_alignment_cvpr_2012_amd as ffd
+    if args.workload != "c2":
+        raise SystemExit("--group runs the c2 workload")
+    faces = args.faces or 4096
+    wl = make_workload("c2", 0, 1, faces * args.gpus, args.frames)
+    n = wl.n
+    imgs = [wl.images[i] for i in range(len(wl.images))]
+    boxes = [tuple(int(v) for v in b) for b in wl.boxes]
+    grp = ffd.FaceForestGroup(list(range(args.gpus)), ffd.FaceForestOptions(model_path=wl.model))
+    try:
+        for _ in range(args.warmup):
+            grp.analyzeFaces(imgs, boxes)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            res = grp.analyzeFaces(imgs, boxes)
+        elapsed = time.perf_counter() - t0
+        torch.cuda.synchronize()
+    finally:
+        grp.close()
+    ok = sum(1 for r in res if r.status == 0)
+    print(json.dumps({
+        "metric": "faces/sec (whole node) on pretrained FFD forest; mean landmark px error",
+        "value": round(n * args.steps / elapsed, 1), "unit": "faces/s", "n_gpus": args.gpus, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8/u16/i32/f32",
+        "data": "synthetic (face_alignment_cvpr_2012_amd/synthetic.py) from the 20 bundled LFW faces",
+        "config": {"workload": wl.describe, "faces_per_gpu": faces,
+                   "parallelism": f"group x{args.gpus}: one process, ffd_group_analyze_faces (ncclCommInitAll), "
+                                  "host crops in, host records out (host-inclusive)"},
+        "records_ok": ok}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -450,9 +490,14 @@ def main():
     ap.add_argument("--no-host-paths", action="store_true", help="skip the host-inclusive and latency lines")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
     ap.add_argument("--dry-run", action="store_true", help="launcher + gather only, gloo, no GPU")
+    ap.add_argument("--group", action="store_true",
+                    help="ONE process driving --gpus devices through the C ABI's ffd_group_analyze_faces "
+                         "(ncclCommInitAll, host crops in / host records out) instead of one rank per GPU")
     ap.add_argument("--uneven", action="store_true", help="--dry-run: a different face count on every rank")
     args = ap.parse_args()
 
+    if args.group:
+        return run_group(args)
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))  # one process per GPU, started before any GPU call
