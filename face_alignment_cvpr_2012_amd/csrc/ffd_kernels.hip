@@ -532,6 +532,9 @@ constexpr int GS_THREADS = 256, GS_BY = 8;
 #ifndef FFD_GABOR_PROBE
 #define FFD_GABOR_PROBE 0
 #endif
+#ifndef FFD_GABOR_BAND_ALL
+#define FFD_GABOR_BAND_ALL 0  // 1: every face through the band-staged (TALL) instance (LDS 66 -> 49 KB per workgroup)
+#endif
 #ifndef FFD_GABOR_SPLIT_MAX
 #define FFD_GABOR_SPLIT_MAX 16  // batches of up to 16 faces: banded Gabor instances (SPLIT)
 #endif
@@ -570,7 +573,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
   __shared__ float vg[GS_BY * C::VP];
   __shared__ f2 vq[4][GS_BY * C::VP];
   const FaceDesc fd = faces[blockIdx.x];
-  if (!fd.valid || fd.nochan || (fd.H > MAX_FACE_H) != TALL) return;
+  if (!fd.valid || fd.nochan || ((FFD_GABOR_BAND_ALL && !SPLIT) ? !TALL : (fd.H > MAX_FACE_H) != TALL)) return;
   if (EXACT && !redo[blockIdx.x]) return;  // the fast instance's mag_sqrt was exact for this face
   uint32_t tiny = 0xFFFFFFFFu;
   const int FW = fd.W, FH = fd.H, NPC = FW + 2 * R;
@@ -2409,7 +2412,7 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t
 #define FFD_GABOR_LAUNCH(WV, RV)                                                                              \
   (exact ? k_gabor_sep<WV, true, false> : k_gabor_sep<WV, false, false>)<<<n, GS_THREADS, gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, \
                                                                                                   mag, chan, rd, force_exact, nullptr); \
-  if (max_h > MAX_FACE_H)                                                                                        \
+  if (max_h > MAX_FACE_H || FFD_GABOR_BAND_ALL)                                                                 \
     (exact ? k_gabor_sep<WV, true, true> : k_gabor_sep<WV, false, true>)<<<n, GS_THREADS, (GS_BY + 2 * RV) * ((PITCH + 2 * RV + 3) / 4 * 4), s>>>(faces, gray, c, \
                                                                                                   mag, chan, rd, force_exact, nullptr)
     switch (nu) {
