@@ -43,30 +43,38 @@ void ffd_engine::load_cascade(const ffd::ModelFile& m) {
   const auto& fr = m.get("haar.feature_rect");
   const auto& fw = m.get("haar.feature_weight");
   const int64_t nw = (int64_t)wf.count(), nf = (int64_t)fw.count() / 3;
-  std::vector<HaarWeak> weak(nw);
-  for (int64_t i = 0; i < nw; i++) {
-    const int f = wf.as<int32_t>()[i];
-    if (f < 0 || f >= nf) throw std::runtime_error("cascade feature index out of range");
-    const int32_t* r = fr.as<int32_t>() + f * 12;
-    auto pack = [&](int k) {
-      for (int j = 0; j < 4; j++)
-        if (r[4 * k + j] < 0 || r[4 * k + j] > 255) throw std::runtime_error("cascade rectangle out of range");
-      if (r[4 * k] + r[4 * k + 2] > haar_ww || r[4 * k + 1] + r[4 * k + 3] > haar_wh)
-        throw std::runtime_error("cascade rectangle outside the window");
-      return (uint32_t)r[4 * k] | (uint32_t)r[4 * k + 1] << 8 | (uint32_t)r[4 * k + 2] << 16 | (uint32_t)r[4 * k + 3] << 24;
-    };
-    HaarWeak& w = weak[i];
-    std::memset(&w, 0, sizeof(w));
-    w.r0 = pack(0);
-    w.r1 = pack(1);
-    w.w0 = fw.as<float>()[f * 3];
-    w.w1 = fw.as<float>()[f * 3 + 1];
-    w.w2 = fw.as<float>()[f * 3 + 2];
-    w.r2 = w.w2 != 0.0f ? pack(2) : 0u;
-    w.thr = wt.as<float>()[i];
-    w.leaf0 = wl.as<float>()[2 * i];
-    w.leaf1 = wl.as<float>()[2 * i + 1];
+  // one table per ystep (1: factor > 2, 2 otherwise; detectMultiScale's yStep): the corner offsets
+  // depend on the LDS window's row pitch
+  std::vector<HaarWeak> weak(2 * nw);
+  for (int ys = 1; ys <= 2; ys++) {
+    const int WC = haar_window_cols(ys, haar_ww);
+    for (int64_t i = 0; i < nw; i++) {
+      const int f = wf.as<int32_t>()[i];
+      if (f < 0 || f >= nf) throw std::runtime_error("cascade feature index out of range");
+      const int32_t* r = fr.as<int32_t>() + f * 12;
+      HaarWeak& w = weak[(ys - 1) * nw + i];
+      std::memset(&w, 0, sizeof(w));
+      w.w0 = fw.as<float>()[f * 3];
+      w.w1 = fw.as<float>()[f * 3 + 1];
+      w.w2 = fw.as<float>()[f * 3 + 2];
+      for (int k = 0; k < 3; k++) {
+        if (k == 2 && w.w2 == 0.0f) break;  // two-rectangle feature: rect 2 stays empty (offsets 0)
+        for (int j = 0; j < 4; j++)
+          if (r[4 * k + j] < 0 || r[4 * k + j] > 255) throw std::runtime_error("cascade rectangle out of range");
+        if (r[4 * k] + r[4 * k + 2] > haar_ww || r[4 * k + 1] + r[4 * k + 3] > haar_wh)
+          throw std::runtime_error("cascade rectangle outside the window");
+        const uint32_t a = (uint32_t)(r[4 * k + 1] * WC + r[4 * k]), b = a + (uint32_t)r[4 * k + 2];
+        const uint32_t c = a + (uint32_t)(r[4 * k + 3] * WC), d = c + (uint32_t)r[4 * k + 2];
+        if (d > 0xFFFFu) throw std::runtime_error("cascade window too large");
+        w.o[2 * k] = a | b << 16;
+        w.o[2 * k + 1] = c | d << 16;
+      }
+      w.thr = wt.as<float>()[i];
+      w.leaf0 = wl.as<float>()[2 * i];
+      w.leaf1 = wl.as<float>()[2 * i + 1];
+    }
   }
+  haar_nweak = (int)nw;
   for (const auto& s : stages)
     if (s.first < 0 || s.ntrees < 0 || s.first + s.ntrees > nw) throw std::runtime_error("cascade stage range");
   upload(haar_weak, weak, main_stream());
@@ -215,7 +223,7 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
       const int lds = haar_cascade_lds(max_ystep, e->haar_ww, e->haar_wh);
       if (lds > 64 * 1024) return fail(e, FFD_ERR_UNSUPPORTED, "cascade window too large for the LDS tile");
       launch_haar_cascade(e->det_levels.as<HaarLevel>(), nL, max_tiles, e->det_sum.as<int32_t>(),
-                          e->det_sq.as<uint64_t>(), e->haar_weak.as<HaarWeak>(), e->haar_stage.as<HaarStage>(),
+                          e->det_sq.as<uint64_t>(), e->haar_weak.as<HaarWeak>(), e->haar_nweak, e->haar_stage.as<HaarStage>(),
                           e->haar_stages, e->haar_ww, e->haar_wh, e->det_res.as<int8_t>(), lds, s);
     }
     launch_haar_group(e->det_frames.as<HaarFrame>(), nF, nL > 0 ? e->det_levels.as<HaarLevel>() : nullptr,

@@ -192,14 +192,18 @@ __global__ __launch_bounds__(256) void k_haar_cols(const HaarLevel* __restrict__
 // Each stage's sum restarts at 0, so splitting at stage boundaries is exact.
 // Result per position: 1 (face) or -stage (stage 0 -> 0), as int8.
 constexpr int HT_X = 64, HT_Y = 8, HT_THREADS = 256, HT_POS = HT_X * HT_Y;
+#ifndef FFD_HAAR_PASSES
+#define FFD_HAAR_PASSES 5  // survivor-compaction passes over the stages (5: [0,1) [1,2) [2,4) [4,7) [7,n))
+#endif
 
+static_assert(HT_X == HAAR_TILE_X && HT_Y == HAAR_TILE_Y, "host offset tables assume this tile");
 __host__ __device__ constexpr int haar_win_cols(int ystep, int ww) { return HT_X * ystep + ww; }
 __host__ __device__ constexpr int haar_win_rows(int ystep, int wh) { return HT_Y * ystep + wh; }
 
 __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __restrict__ levels,
                                                              const int32_t* __restrict__ sum,
                                                              const uint64_t* __restrict__ sq,
-                                                             const HaarWeak* __restrict__ weak,
+                                                             const HaarWeak* __restrict__ weak_tables, int n_weak,
                                                              const HaarStage* __restrict__ stages, int n_stages,
                                                              int ww, int wh, int8_t* __restrict__ result) {
   extern __shared__ __attribute__((aligned(16))) int32_t win[];
@@ -213,6 +217,7 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
   const int ys = L.ystep, P = L.sw + 1;
   const int WC = haar_win_cols(ys, ww), WR = haar_win_rows(ys, wh);
   const int x0 = tx * HT_X * ys, y0 = ty * HT_Y * ys;
+  const HaarWeak* __restrict__ weak = weak_tables + (ys == 2 ? n_weak : 0);  // offsets for this window pitch
   const int32_t* S = sum + L.sum_off;
   const uint64_t* Q = sq + L.sum_off;
   for (int i = threadIdx.x; i < WC * WR; i += HT_THREADS) {
@@ -239,10 +244,16 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
     list[0][atomicAdd(&n_list[0], 1)] = (uint16_t)p;  // order within a pass does not matter
   }
   __syncthreads();
-  const int bounds[6] = {0, 1, 2, 4, 7, n_stages};
+#if FFD_HAAR_PASSES == 8
+  constexpr int NP = 8;
+  const int bounds[NP + 1] = {0, 1, 2, 4, 7, 10, 13, 17, n_stages};
+#else
+  constexpr int NP = 5;
+  const int bounds[NP + 1] = {0, 1, 2, 4, 7, n_stages};
+#endif
   int cur = 0;
-  for (int pass = 0; pass < 5; pass++) {
-    const int s0 = min(bounds[pass], n_stages), s1 = pass == 4 ? n_stages : min(bounds[pass + 1], n_stages);
+  for (int pass = 0; pass < NP; pass++) {
+    const int s0 = min(bounds[pass], n_stages), s1 = pass == NP - 1 ? n_stages : min(bounds[pass + 1], n_stages);
     if (s0 >= s1) continue;
     const int n = n_list[cur];
     if (threadIdx.x == 0) n_list[cur ^ 1] = 0;
@@ -259,15 +270,13 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
         // 4 weak classifiers per step: their records (wave-uniform scalar loads) and all 36 window
         // reads are issued together; the sum still accumulates in classifier order
         auto value_of = [&](const HaarWeak& c) {
-          auto rs = [&](uint32_t r) {
-            const int rx = r & 255u, ry = (r >> 8) & 255u, rw = (r >> 16) & 255u, rh = r >> 24;
-            const int p0 = ry * WC + rx, p2 = p0 + rh * WC;
-            return w0[p0] - w0[p0 + rw] - w0[p2] + w0[p2 + rw];
+          auto rs = [&](uint32_t ab, uint32_t cd) {  // corner offsets precomputed for this window pitch
+            return w0[ab & 0xFFFFu] - w0[ab >> 16] - w0[cd & 0xFFFFu] + w0[cd >> 16];
           };
-          float ret = c.w0 * (float)rs(c.r0) + c.w1 * (float)rs(c.r1);
+          float ret = c.w0 * (float)rs(c.o[0], c.o[1]) + c.w1 * (float)rs(c.o[2], c.o[3]);
           // two-rectangle features carry w2 = 0 and an empty rect 2: + (+0) leaves ret unchanged
           // (up to the sign of a zero, which no comparison below distinguishes)
-          ret += c.w2 * (float)rs(c.r2);
+          ret += c.w2 * (float)rs(c.o[4], c.o[5]);
           // HaarEvaluator::operator() (cascadedetect.hpp, 2.4.9) returns double: calc() * varianceNormFactor,
           // compared unrounded with the float threshold in predictOrderedStump
           return (double)ret * f;
@@ -556,10 +565,10 @@ int haar_cascade_lds(int max_ystep, int ww, int wh) {
 }
 
 void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint64_t* sq,
-                         const HaarWeak* weak, const HaarStage* stages, int n_stages, int ww, int wh, int8_t* result,
+                         const HaarWeak* weak, int n_weak, const HaarStage* stages, int n_stages, int ww, int wh, int8_t* result,
                          int lds_bytes, hipStream_t s) {
-  k_haar_cascade<<<dim3(max_tiles, n_levels), HT_THREADS, lds_bytes, s>>>(levels, sum, sq, weak, stages, n_stages, ww,
-                                                                           wh, result);
+  k_haar_cascade<<<dim3(max_tiles, n_levels), HT_THREADS, lds_bytes, s>>>(levels, sum, sq, weak, n_weak, stages,
+                                                                           n_stages, ww, wh, result);
 }
 
 void launch_haar_group(const HaarFrame* frames, int n_frames, const HaarLevel* levels, const int8_t* result, int cap,

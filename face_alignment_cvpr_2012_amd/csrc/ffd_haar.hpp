@@ -35,12 +35,14 @@ struct HaarLevel {
   int32_t frame;
 };
 
-// One stump weak classifier with its Haar feature (HaarEvaluator::Feature + DTreeNode + 2 leaves).
+// One stump weak classifier with its Haar feature (HaarEvaluator::Feature + DTreeNode + 2 leaves), its
+// rectangles as corner offsets into the cascade kernel's LDS window (row pitch haar_win_cols(ystep, ww),
+// so one table per ystep): rect k sums win[a] - win[b] - win[c] + win[d] with a | b << 16 = o[2k],
+// c | d << 16 = o[2k + 1] (the rectangle (x, y, w, h): a = y W + x, b = a + w, c = a + h W, d = c + w).
 struct HaarWeak {
-  uint32_t r0, r1, r2;  // rect x | y << 8 | w << 16 | h << 24
-  float w0, w1, w2;     // rect weights (w2 == 0: two-rectangle feature)
+  uint32_t o[6];
+  float w0, w1, w2;     // rect weights (w2 == 0: two-rectangle feature, rect 2 empty)
   float thr, leaf0, leaf1;
-  uint32_t pad[3];
 };
 static_assert(sizeof(HaarWeak) == 48, "HaarWeak is 48 bytes");
 
@@ -58,9 +60,11 @@ void launch_haar_pyramid(const HaarLevel* levels, int n_levels, int max_pixels, 
 // lds_bytes = haar_cascade_lds(largest ystep of the batch, ww, wh) (dynamic LDS: the integral window)
 constexpr int HAAR_TILE_X = 64, HAAR_TILE_Y = 8;
 int haar_cascade_lds(int max_ystep, int ww, int wh);
+// weak: the ystep-1 table, then (at weak + n_weak) the ystep-2 table
 void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint64_t* sq,
-                         const HaarWeak* weak, const HaarStage* stages, int n_stages, int ww, int wh, int8_t* result,
-                         int lds_bytes, hipStream_t s);
+                         const HaarWeak* weak, int n_weak, const HaarStage* stages, int n_stages, int ww, int wh,
+                         int8_t* result, int lds_bytes, hipStream_t s);
+constexpr int haar_window_cols(int ystep, int ww) { return HAAR_TILE_X * ystep + ww; }
 // pack every frame's boxes (cap apart) contiguously: packed[i], owner[i]; totals[0] = box count
 void launch_haar_pack(int n_frames, int cap, const int4* boxes, const int32_t* n_boxes, int4* packed, int32_t* owner,
                       hipStream_t s);
