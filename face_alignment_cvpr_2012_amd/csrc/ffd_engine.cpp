@@ -509,6 +509,7 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   w.state.ensure((size_t)n * sizeof(HpState));
   w.ms_mean.ensure((size_t)n * NPARTS * 2 * 4);
   w.vote_counts.ensure((size_t)n * NPARTS * 4);
+  w.ms_order.ensure((size_t)n * NPARTS * 4);
   w.gabor_redo.ensure((size_t)n * 5 * 4);  // 5 scales
   if (w.gabor_mm.n < (size_t)n * 5 * 64) {  // the banded instances leave their slots zeroed
     w.gabor_mm.ensure((size_t)n * 5 * 64);
@@ -574,7 +575,7 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   stage(11, st, [&] {
     launch_meanshift(dfd, n, w.state.as<HpState>(), MAX_TREES, n_parts, (float)desc.ms_option.kernel_size,
                      desc.ms_option.max_iterations, desc.ms_option.stopping_criteria, w.votes.as<Vote>(),
-                     w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(), d_out, st);
+                     w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(), d_out, w.ms_order.as<int32_t>(), st);
   });
   HIP_CHECK(hipGetLastError());
 }
@@ -1240,7 +1241,7 @@ ffd_status ffd_estimate_facial_features(ffd_engine* e, const uint32_t* channels,
                  o.step_size, step_y, e->patch / 2, n_parts, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), w.stream);
     // FaceForest::estimateFacialFeatures shifts with a default MeanShiftOption (FaceForest.cpp:89-92)
     launch_meanshift(dfd, 1, w.state.as<HpState>(), MAX_TREES, n_parts, 10.f, 7, 0.05f, w.votes.as<Vote>(),
-                     w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(), e->out.as<FaceOut>(), w.stream);
+                     w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(), e->out.as<FaceOut>(), nullptr, w.stream);
     HIP_CHECK(hipGetLastError());
     FaceOut out;
     HIP_CHECK(hipMemcpyAsync(&out, e->out.p, sizeof(out), hipMemcpyDeviceToHost, w.stream));

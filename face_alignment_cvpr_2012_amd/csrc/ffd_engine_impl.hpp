@@ -87,6 +87,7 @@ struct Workspace {
   bool pending = false;
   DevBuf faces, gray, mag, chan, hpleaf, mpleaf, votes, state, ms_mean, vote_counts;
   DevBuf gabor_redo;  // per scale and face: the fast Gabor instance flags faces for the exact one
+  DevBuf ms_order;    // MeanShift chains sorted by list length (k_ms_order)
   DevBuf gabor_mm;    // per face and scale: the banded Gabor instances' 16-word slots (zero between launches)
   std::vector<FaceDesc> h_fds;  // host staging, reused only after `done`
   std::vector<FaceDesc> desc;   // descriptors of the chunk last run here (ffd_get_trace)

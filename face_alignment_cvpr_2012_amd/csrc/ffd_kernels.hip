@@ -1798,6 +1798,9 @@ constexpr int MS_RA = FFD_MS_RA;  // serial phase: LDS reads in flight ahead of 
 #ifndef FFD_MS_UDEF
 #define FFD_MS_UDEF 4
 #endif
+#ifndef FFD_MS_SORT
+#define FFD_MS_SORT 1  // k_meanshift over chains sorted by list length (k_ms_order)
+#endif
 #ifndef FFD_MS_K
 #define FFD_MS_K 4  // k_meanshift4: votes per lane per tile
 #endif
@@ -1852,21 +1855,37 @@ __device__ __forceinline__ float ms_weight(float mx, float my, float x, float y,
 }
 
 // 8 waves per SIMD (<= 64 VGPRs): 8 workgroups per CU, so C2's 2048 workgroups run as one round
+// The MS_FACES chains (face, landmark) of a workgroup run their passes and tiles in lockstep, so a
+// workgroup costs about its LONGEST list times its slowest chain's passes.  order (k_ms_order): the
+// chains sorted by list length, longest first, dealt MS_FACES per workgroup — similar lengths share a
+// workgroup and the longest start first.  Without it: workgroup (x, y) = faces [20x, 20x + 20), landmark y.
+// A chain's arithmetic does not depend on its slot, so the order changes no result.
 __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_meanshift(const FaceDesc* __restrict__ faces, int n_faces,
                                                    int tslots, int n_parts, float lamda, float lam_y, int max_iter,
                                                    float stop, const Vote* __restrict__ votes,
                                                    const int32_t* __restrict__ vote_counts,
-                                                   float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
+                                                   float* __restrict__ ms_mean, FaceOut* __restrict__ out,
+                                                   const int32_t* __restrict__ order) {
   __shared__ float tx[MS_TILE * MS_LD], ty[MS_TILE * MS_LD], tw[MS_TILE * MS_LD];
   __shared__ float s_mx[MS_FACES], s_my[MS_FACES];
-  __shared__ int s_cnt[MS_FACES], s_live[MS_FACES];
+  __shared__ int s_cnt[MS_FACES], s_live[MS_FACES], s_chain[MS_FACES];
   __shared__ int64_t s_vb[MS_FACES];
   __shared__ int s_maxcnt, s_nlive;
-  const int part = blockIdx.y, f0 = blockIdx.x * MS_FACES, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   if (tid == 0) { s_maxcnt = 0; s_nlive = 0; }
   __syncthreads();
   if (tid < MS_FACES) {
-    const int f = f0 + tid;
+    const int64_t n_chains = (int64_t)n_faces * NPARTS;
+    int64_t chain;
+    if (order) {
+      const int64_t k = (int64_t)blockIdx.x * MS_FACES + tid;
+      chain = k < n_chains ? order[k] : n_chains;
+    } else {
+      chain = (int64_t)(blockIdx.x * MS_FACES + tid) * NPARTS + blockIdx.y;
+      if (blockIdx.x * MS_FACES + tid >= n_faces) chain = n_chains;
+    }
+    s_chain[tid] = (int)chain;
+    const int f = chain < n_chains ? (int)(chain / NPARTS) : n_faces, part = (int)(chain % NPARTS);
     int cnt = 0;
     int64_t vb = 0;
     if (f < n_faces && faces[f].valid) {
@@ -1884,7 +1903,7 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
   }
   __syncthreads();
   const int maxcnt = s_maxcnt;
-  // lane p of wave 0 owns face f0 + p; its sums live in registers
+  // lane p of wave 0 owns chain s_chain[p]; its sums live in registers
   float ax = 0, ay = 0, aw = 0;
   // pass = -1: getMean (terms x*w, y*w, w); pass >= 0: getWeightedMean iteration
   for (int pass = -1; pass < max_iter; pass++) {
@@ -1970,7 +1989,8 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
     __syncthreads();
   }
   if (tid < MS_FACES) {
-    const int f = f0 + tid;
+    const int chain = s_chain[tid];
+    const int f = chain < n_faces * NPARTS ? chain / NPARTS : n_faces, part = chain % NPARTS;
     if (f < n_faces && faces[f].valid) {
       const float mx = s_mx[tid], my = s_my[tid];
       if (part < n_parts) {
@@ -2592,9 +2612,43 @@ void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const ui
                                                half_patch, n_parts, votes, vote_counts);
 }
 
+// The chains (face, landmark) sorted by list length, longest first (counting sort on length / 32, one
+// workgroup; the order within a bucket is the atomics' and changes no result).
+constexpr int MS_ORDER_BUCKETS = 1024;
+__global__ __launch_bounds__(1024) void k_ms_order(const FaceDesc* __restrict__ faces, int n_faces, int n_parts,
+                                                   const int32_t* __restrict__ vote_counts, int32_t* __restrict__ order) {
+  __shared__ int hist[MS_ORDER_BUCKETS];
+  __shared__ int wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int n_chains = n_faces * NPARTS;
+  auto bucket = [&](int c) {  // descending length -> ascending bucket
+    const int f = c / NPARTS, part = c - f * NPARTS;
+    const int cnt = (part < n_parts && faces[f].valid) ? vote_counts[c] : 0;
+    return MS_ORDER_BUCKETS - 1 - min(cnt >> 5, MS_ORDER_BUCKETS - 1);
+  };
+  hist[tid] = 0;
+  __syncthreads();
+  for (int c = tid; c < n_chains; c += 1024) atomicAdd(&hist[bucket(c)], 1);
+  __syncthreads();
+  const int v = hist[tid];
+  int incl = v;
+#pragma unroll
+  for (int sh = 1; sh < 64; sh <<= 1) {
+    const int t = __shfl_up(incl, sh);
+    if (lane >= sh) incl += t;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  int base = 0;
+  for (int w = 0; w < wv; w++) base += wsum[w];
+  hist[tid] = base + incl - v;  // bucket start
+  __syncthreads();
+  for (int c = tid; c < n_chains; c += 1024) order[atomicAdd(&hist[bucket(c)], 1)] = c;
+}
+
 void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int tslots, int n_parts, float lamda,
                       int max_iter, float stop, const Vote* votes, const int32_t* vote_counts, float* ms_mean,
-                      FaceOut* out, hipStream_t s) {
+                      FaceOut* out, int32_t* order, hipStream_t s) {
   (void)state;
   // k_meanshift5 (5) for a few chains (single-face latency: one workgroup per chain); k_meanshift (1) when
   // the batch has chains for >= 4 of its workgroups per CU (C2: 2,048 workgroups, 2.45 ms, where
@@ -2617,9 +2671,16 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
     return;
   }
   if (which == 1) {
-    dim3 grid((n + MS_FACES - 1) / MS_FACES, NPARTS);
-    k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes,
-                                            vote_counts, ms_mean, out);
+    if (FFD_MS_SORT && order) {  // chains sorted by list length, MS_FACES per workgroup
+      k_ms_order<<<1, 1024, 0, s>>>(faces, n, n_parts, vote_counts, order);
+      const dim3 grid((unsigned)((chains + MS_FACES - 1) / MS_FACES));
+      k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes,
+                                              vote_counts, ms_mean, out, order);
+    } else {
+      const dim3 grid((n + MS_FACES - 1) / MS_FACES, NPARTS);
+      k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes,
+                                              vote_counts, ms_mean, out, nullptr);
+    }
     return;
   }
   const int64_t lists = (int64_t)n * NPARTS;

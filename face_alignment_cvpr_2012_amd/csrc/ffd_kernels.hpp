@@ -65,6 +65,6 @@ void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const ui
                   hipStream_t s);
 void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int tslots, int n_parts, float lamda,
                       int max_iter, float stop, const Vote* votes, const int32_t* vote_counts, float* ms_mean,
-                      FaceOut* out, hipStream_t s);
+                      FaceOut* out, int32_t* order, hipStream_t s);
 
 }  // namespace ffd
