@@ -2162,7 +2162,8 @@ template <int C, int K>
 __global__ __launch_bounds__(256) void k_meanshift4(const FaceDesc* __restrict__ faces, int n_faces, int tslots,
                                                    int n_parts, float lamda, float lam_y, int max_iter, float stop,
                                                    const Vote* __restrict__ votes, const int32_t* __restrict__ vote_counts,
-                                                   float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
+                                                   float* __restrict__ ms_mean, FaceOut* __restrict__ out,
+                                                   const int32_t* __restrict__ order) {
   constexpr int V = 64 / C, TV = V * K;  // term lanes per chain; votes per chain per tile
   static_assert(3 * C <= 64 && V * C == 64, "chains per wave");
   __shared__ float4 term[4][TV][C];  // per wave: [vote j][chain c] = (x*w, y*w, w, 0)
@@ -2173,8 +2174,13 @@ __global__ __launch_bounds__(256) void k_meanshift4(const FaceDesc* __restrict__
   if (ch0 >= n_chains) return;  // whole waves; no workgroup barrier below
   // term lanes: chain tc = lane / V, vote offset tk = lane % V
   const int tc = lane / V, tk = lane - tc * V;
+  // order (k_ms_order): chains sorted by list length, so a wave's C chains have similar lengths
+  auto chain_of = [&](int c) -> int64_t {
+    const int64_t k = ch0 + c;
+    return order ? (k < n_chains ? (int64_t)order[k] : n_chains) : k;
+  };
   auto chain_info = [&](int c, int& cnt, int64_t& vb, int& valid) {
-    const int64_t g = ch0 + c;
+    const int64_t g = chain_of(c);
     cnt = 0;
     vb = 0;
     valid = 0;
@@ -2275,7 +2281,7 @@ __global__ __launch_bounds__(256) void k_meanshift4(const FaceDesc* __restrict__
     my = s_mean[wv][tc][1];
   }
   if (sum_lane && se == 0 && s_valid) {
-    const int64_t g = ch0 + sc;
+    const int64_t g = chain_of(sc);
     const int f = (int)(g / NPARTS), part = (int)(g - (int64_t)f * NPARTS);
     if (part < n_parts) {
       ms_mean[((int64_t)f * NPARTS + part) * 2] = smx;
@@ -2705,14 +2711,19 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
     const char* v = std::getenv("FFD_MS_WAVES");
     return v ? std::atoll(v) : (int64_t)4096;
   }();
+  const int32_t* ord = nullptr;
+  if (FFD_MS_SORT && order) {
+    k_ms_order<<<1, 1024, 0, s>>>(faces, n, n_parts, vote_counts, order);
+    ord = order;
+  }
   auto launch4 = [&](int C) {
     const int64_t waves = (lists + C - 1) / C;
     const dim3 grid((unsigned)((waves + 3) / 4));
     switch (C) {
-      case 16: k_meanshift4<16, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out); break;
-      case 8: k_meanshift4<8, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out); break;
-      case 4: k_meanshift4<4, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out); break;
-      default: k_meanshift4<2, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out); break;
+      case 16: k_meanshift4<16, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out, ord); break;
+      case 8: k_meanshift4<8, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out, ord); break;
+      case 4: k_meanshift4<4, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out, ord); break;
+      default: k_meanshift4<2, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out, ord); break;
     }
   };
   int C = 16;
