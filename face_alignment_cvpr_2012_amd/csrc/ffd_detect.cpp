@@ -226,7 +226,10 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
                           e->det_sq.as<uint64_t>(), e->haar_weak.as<HaarWeak>(), e->haar_nweak, e->haar_stage.as<HaarStage>(),
                           e->haar_stages, e->haar_ww, e->haar_wh, e->det_res.as<int8_t>(), lds, s);
     }
-    launch_haar_group(e->det_frames.as<HaarFrame>(), nF, nL > 0 ? e->det_levels.as<HaarLevel>() : nullptr,
+    int max_frame_rows = 0;
+    for (const auto& f : frames) max_frame_rows = std::max(max_frame_rows, f.rows);
+    e->det_rowcnt.ensure((size_t)nF * std::max(1, max_frame_rows) * 4);
+    launch_haar_group(e->det_frames.as<HaarFrame>(), nF, max_frame_rows, e->det_rowcnt.as<int32_t>(), nL > 0 ? e->det_levels.as<HaarLevel>() : nullptr,
                       nL > 0 ? e->det_res.as<int8_t>() : nullptr, cap, e->det_cand.as<int4>(), n_cand,
                       o.min_neighbors, o.widen, e->det_clsrect.as<int4>(), e->det_clssum.as<int>(),
                       e->det_boxes.as<int4>(), n_boxes, s);

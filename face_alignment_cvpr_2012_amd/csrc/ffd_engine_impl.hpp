@@ -164,7 +164,7 @@ struct ffd_engine {
   int haar_ww = 0, haar_wh = 0, haar_stages = 0;
   DevBuf haar_weak, haar_stage;
   int haar_nweak = 0;  // weak classifiers per ystep table (haar_weak holds two)
-  DevBuf det_frames, det_levels, det_gray, det_scaled, det_sum, det_sq, det_res, det_cand, det_ncand, det_clsrect,
+  DevBuf det_frames, det_levels, det_gray, det_scaled, det_sum, det_sq, det_res, det_cand, det_ncand, det_rowcnt, det_clsrect,
       det_clssum, det_boxes, det_packed;
   int n_cu = 256;  // compute units of the device (survivor-pass grids)
 

@@ -310,6 +310,9 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
 
 // ------------------------------------------------------------------------ collect ----
 constexpr int HC_THREADS = 1024;
+#ifndef FFD_HAAR_COLLECT_SERIAL
+#define FFD_HAAR_COLLECT_SERIAL 0  // 1: the thread-per-row scan (k_haar_collect)
+#endif
 
 __device__ __forceinline__ int block_excl_scan(int v, int* sh, int& total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -381,6 +384,89 @@ __global__ __launch_bounds__(HC_THREADS) void k_haar_collect(const HaarFrame* __
     base += tot;
   }
   if (threadIdx.x == 0) n_cand[blockIdx.x] = base;
+}
+
+// Default form of the same scan, spread over (frame, block of HR_THREADS rows) workgroups: the
+// per-frame form above runs one workgroup per frame (64 per group of frames, a quarter of the CUs).
+// k_haar_rowcount walks each row once for its candidate count; k_haar_emit sums the counts of the
+// frame's earlier rows, scans its own and walks again, writing each candidate at its slot.  Same
+// walk, same candidate order, same cap rule.
+constexpr int HR_THREADS = 256;
+
+__device__ __forceinline__ int haar_row_walk(const HaarFrame& f, const HaarLevel* __restrict__ levels,
+                                             const int8_t* __restrict__ result, int r, bool emit, int at, int cap,
+                                             int4* __restrict__ out) {
+  int lv = f.level0;
+  while (lv + 1 < f.level1 && levels[lv + 1].row0 <= r) lv++;
+  const HaarLevel& L = levels[lv];
+  const int iy = r - L.row0;
+  const int8_t* row = result + L.res_off + (int64_t)iy * L.nx;
+  int n = 0, ix = 0;
+  for (int c0 = 0; c0 < L.nx; c0 += 16) {
+    int8_t v16[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) v16[k] = c0 + k < L.nx ? row[c0 + k] : (int8_t)-1;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      if (ix != c0 + k) continue;
+      const int v = v16[k];
+      if (c0 + k >= L.nx) break;
+      if (v > 0) {
+        if (emit && at + n < cap) {
+          const int x = ix * L.ystep, y = iy * L.ystep;
+          out[at + n] = make_int4(hround_d(x * L.factor), hround_d(y * L.factor), L.win_w, L.win_h);
+        }
+        n++;
+      }
+      ix += v == 0 ? 2 : 1;
+    }
+  }
+  return n;
+}
+
+__global__ __launch_bounds__(HR_THREADS) void k_haar_rowcount(const HaarFrame* __restrict__ frames,
+                                                               const HaarLevel* __restrict__ levels,
+                                                               const int8_t* __restrict__ result, int pitch,
+                                                               int32_t* __restrict__ rowcnt) {
+  const HaarFrame f = frames[blockIdx.x];
+  const int r = blockIdx.y * HR_THREADS + threadIdx.x;
+  if (r >= f.rows) return;
+  rowcnt[(int64_t)blockIdx.x * pitch + r] = haar_row_walk(f, levels, result, r, false, 0, 0, nullptr);
+}
+
+__global__ __launch_bounds__(HR_THREADS) void k_haar_emit(const HaarFrame* __restrict__ frames,
+                                                           const HaarLevel* __restrict__ levels,
+                                                           const int8_t* __restrict__ result, int pitch,
+                                                           const int32_t* __restrict__ rowcnt, int cap,
+                                                           int4* __restrict__ cand, int32_t* __restrict__ n_cand) {
+  __shared__ int sh[HR_THREADS / 64 + 1];
+  const HaarFrame f = frames[blockIdx.x];
+  const int r0 = blockIdx.y * HR_THREADS;
+  if (r0 >= f.rows && !(r0 == 0 && f.rows == 0)) return;  // whole workgroup
+  const int32_t* rc = rowcnt + (int64_t)blockIdx.x * pitch;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int before = 0;
+  for (int i = threadIdx.x; i < r0; i += HR_THREADS) before += rc[i];
+  before = __shfl((int)wave_scan_u32((uint32_t)before), 63);
+  if (lane == 0) sh[wv] = before;
+  __syncthreads();
+  before = 0;
+#pragma unroll
+  for (int w = 0; w < HR_THREADS / 64; w++) before += sh[w];
+  __syncthreads();
+  const int r = r0 + threadIdx.x;
+  const int cnt = r < f.rows ? rc[r] : 0;
+  const int incl = (int)wave_scan_u32((uint32_t)cnt);
+  if (lane == 63) sh[wv] = incl;
+  __syncthreads();
+  int off = before + incl - cnt, tot = before;
+#pragma unroll
+  for (int w = 0; w < HR_THREADS / 64; w++) {
+    off += w < wv ? sh[w] : 0;
+    tot += sh[w];
+  }
+  if (cnt > 0) (void)haar_row_walk(f, levels, result, r, true, off, cap, cand + (int64_t)blockIdx.x * cap);
+  if (threadIdx.x == 0 && (f.rows == 0 || blockIdx.y == (f.rows - 1) / HR_THREADS)) n_cand[blockIdx.x] = tot;
 }
 
 // -------------------------------------------------------------------------- group ----
@@ -571,10 +657,19 @@ void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, c
                                                                            n_stages, ww, wh, result);
 }
 
-void launch_haar_group(const HaarFrame* frames, int n_frames, const HaarLevel* levels, const int8_t* result, int cap,
-                       int4* cand, int32_t* n_cand, int min_neighbors, int widen, int4* cls_rect, int* cls_sum,
-                       int4* boxes, int32_t* n_boxes, hipStream_t s) {
+void launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows, int32_t* rowcnt,
+                       const HaarLevel* levels, const int8_t* result, int cap, int4* cand, int32_t* n_cand,
+                       int min_neighbors, int widen, int4* cls_rect, int* cls_sum, int4* boxes, int32_t* n_boxes,
+                       hipStream_t s) {
+#if FFD_HAAR_COLLECT_SERIAL
+  (void)max_frame_rows;
+  (void)rowcnt;
   k_haar_collect<<<n_frames, HC_THREADS, 0, s>>>(frames, levels, result, cap, cand, n_cand);
+#else
+  const int rb = std::max(1, (max_frame_rows + HR_THREADS - 1) / HR_THREADS);
+  if (max_frame_rows > 0) k_haar_rowcount<<<dim3(n_frames, rb), HR_THREADS, 0, s>>>(frames, levels, result, max_frame_rows, rowcnt);
+  k_haar_emit<<<dim3(n_frames, rb), HR_THREADS, 0, s>>>(frames, levels, result, max_frame_rows, rowcnt, cap, cand, n_cand);
+#endif
   k_haar_group<<<n_frames, HC_THREADS, 0, s>>>(frames, cap, cand, n_cand, min_neighbors, widen, cls_rect, cls_sum,
                                               boxes, n_boxes);
 }

@@ -70,8 +70,8 @@ void launch_haar_pack(int n_frames, int cap, const int4* boxes, const int32_t* n
                       hipStream_t s);
 // candidates (cap per frame) in scan order, then grouped + widened boxes (cap per frame);
 // cls_rect: cap int4 per frame, cls_sum: 5 cap ints per frame (scratch)
-void launch_haar_group(const HaarFrame* frames, int n_frames, const HaarLevel* levels, const int8_t* result, int cap,
-                       int4* cand, int32_t* n_cand, int min_neighbors, int widen, int4* cls_rect, int* cls_sum,
+void launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows, int32_t* rowcnt,
+                       const HaarLevel* levels, const int8_t* result, int cap, int4* cand, int32_t* n_cand, int min_neighbors, int widen, int4* cls_rect, int* cls_sum,
                        int4* boxes, int32_t* n_boxes, hipStream_t s);
 
 }  // namespace ffd

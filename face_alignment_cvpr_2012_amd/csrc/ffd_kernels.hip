@@ -727,7 +727,6 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
-    using I4 = std::integral_constant<int, 4>;
     using BT = std::integral_constant<bool, true>;
     using BF = std::integral_constant<bool, false>;
       // two plane halves (V planes 1-2 + Vg, then 3-4): half the V-plane LDS, 3 workgroups per CU
@@ -1212,15 +1211,19 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         }
       }
 #if !FFD_TRAV_NOSTAGE
+#if FFD_TRAV_VOFF_ARRAY
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int voff = voffs[u];
+        if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, base_b, 0);
+        else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, base_b, 0);
+      }
+#else
       const int plane_b = A.plane * 2;
       int q = q0, r = r0, c = c0;
 #pragma unroll
       for (int u = 0; u < U; u++) {
-#if FFD_TRAV_VOFF_ARRAY
-        const int voff = voffs[u];
-#else
         const int voff = min(c, NCH) * plane_b + r * (PITCH * 2) + q * CB;
-#endif
         if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, base_b, 0);
         else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, base_b, 0);
         q += dq;
@@ -1231,6 +1234,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         r -= cr ? WH : 0;
         c += dc + cr;
       }
+#endif
 #endif
     };
     auto commit = [&](const Blk& B) {
