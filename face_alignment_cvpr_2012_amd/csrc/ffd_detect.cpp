@@ -35,7 +35,7 @@ void ffd_engine::load_cascade(const ffd::ModelFile& m) {
     stages[s].first = sf.as<int32_t>()[s];
     stages[s].ntrees = sn.as<int32_t>()[s];
     stages[s].thr = st.as<float>()[s] - 1e-5f;  // CascadeClassifier::Data::read THRESHOLD_EPS
-    stages[s].pad = 0;
+    stages[s].n_two = 0;
   }
   const auto& wf = m.get("haar.weak_feature");
   const auto& wt = m.get("haar.weak_threshold");
@@ -63,9 +63,11 @@ void ffd_engine::load_cascade(const ffd::ModelFile& m) {
           if (r[4 * k + j] < 0 || r[4 * k + j] > 255) throw std::runtime_error("cascade rectangle out of range");
         if (r[4 * k] + r[4 * k + 2] > haar_ww || r[4 * k + 1] + r[4 * k + 3] > haar_wh)
           throw std::runtime_error("cascade rectangle outside the window");
-        const uint32_t a = (uint32_t)(r[4 * k + 1] * WC + r[4 * k]), b = a + (uint32_t)r[4 * k + 2];
-        const uint32_t c = a + (uint32_t)(r[4 * k + 3] * WC), d = c + (uint32_t)r[4 * k + 2];
-        if (d > 0xFFFFu) throw std::runtime_error("cascade window too large");
+        const int x = r[4 * k], y = r[4 * k + 1], rw = r[4 * k + 2], rh = r[4 * k + 3];
+        const uint32_t a = (uint32_t)haar_window_offset(ys, WC, y, x), b = (uint32_t)haar_window_offset(ys, WC, y, x + rw);
+        const uint32_t c = (uint32_t)haar_window_offset(ys, WC, y + rh, x);
+        const uint32_t d = (uint32_t)haar_window_offset(ys, WC, y + rh, x + rw);
+        if (d > 0xFFFFu || b > 0xFFFFu) throw std::runtime_error("cascade window too large");
         w.o[2 * k] = a | b << 16;
         w.o[2 * k + 1] = c | d << 16;
       }
@@ -77,6 +79,38 @@ void ffd_engine::load_cascade(const ffd::ModelFile& m) {
   haar_nweak = (int)nw;
   for (const auto& s : stages)
     if (s.first < 0 || s.ntrees < 0 || s.first + s.ntrees > nw) throw std::runtime_error("cascade stage range");
+  // Two-rectangle classifiers first within each stage (HaarStage::n_two of them), so the kernel reads
+  // 8 window corners for those instead of 12.  This reorders predictOrderedStump's double sum of the
+  // stage's float leaves, which is exact in any order when every partial sum is representable:
+  // all leaves are integer multiples of 2^e (e = the smallest leaf's last mantissa bit) and the sum of
+  // the largest |leaf| per classifier stays below 2^(53 + e).  A stage that fails the check keeps its
+  // order (n_two = 0: every classifier through the 12-corner form, which covers rect 2 empty).
+  for (auto& st : stages) {
+    int emin = INT32_MAX;
+    double bound = 0.0;
+    for (int i = st.first; i < st.first + st.ntrees; i++) {
+      const HaarWeak& w = weak[i];
+      for (float l : {w.leaf0, w.leaf1})
+        if (l != 0.0f) {
+          int ex;
+          std::frexp((double)l, &ex);
+          emin = std::min(emin, ex - 24);
+        }
+      bound += std::max(std::fabs((double)w.leaf0), std::fabs((double)w.leaf1));
+    }
+    st.n_two = 0;
+    if (st.ntrees == 0 || emin == INT32_MAX || !(bound < std::ldexp(1.0, 52 + emin))) continue;
+    std::vector<int> two, three;
+    for (int i = st.first; i < st.first + st.ntrees; i++) (weak[i].w2 == 0.0f ? two : three).push_back(i);
+    std::vector<HaarWeak> perm;
+    for (int t = 0; t < 2; t++) {
+      perm.clear();
+      for (int i : two) perm.push_back(weak[t * nw + i]);
+      for (int i : three) perm.push_back(weak[t * nw + i]);
+      std::copy(perm.begin(), perm.end(), weak.begin() + t * nw + st.first);
+    }
+    st.n_two = (int)two.size();
+  }
   upload(haar_weak, weak, main_stream());
   upload(haar_stage, stages, main_stream());
 }

@@ -223,18 +223,19 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
   for (int i = threadIdx.x; i < WC * WR; i += HT_THREADS) {
     const int r = i / WC, c = i - r * WC;
     const int gy = y0 + r, gx = x0 + c;
-    win[i] = (gy <= L.sh && gx < P) ? S[(int64_t)gy * P + gx] : 0;
+    win[haar_window_offset(ys, WC, r, c)] = (gy <= L.sh && gx < P) ? S[(int64_t)gy * P + gx] : 0;
   }
   if (threadIdx.x == 0) { n_list[0] = 0; n_list[1] = 0; }
   __syncthreads();
   // setWindow for every position of the tile: normrect (1, 1, ww - 2, wh - 2)
-  const int na = WC + 1, nb = na + (ww - 2), nc = (wh - 1) * WC + 1, nd = nc + (ww - 2);
+  const int na = haar_window_offset(ys, WC, 1, 1), nb = haar_window_offset(ys, WC, 1, ww - 1);
+  const int nc = haar_window_offset(ys, WC, wh - 1, 1), nd = haar_window_offset(ys, WC, wh - 1, ww - 1);
   const int qa = P + 1, qb = qa + (ww - 2), qc = (wh - 1) * P + 1, qd = qc + (ww - 2);
   for (int p = threadIdx.x; p < HT_POS; p += HT_THREADS) {
     const int lx = p & (HT_X - 1), ly = p / HT_X;
     const int ix = tx * HT_X + lx, iy = ty * HT_Y + ly;
     if (ix >= L.nx || iy >= L.ny) continue;
-    const int o = ly * ys * WC + lx * ys;
+    const int o = ly * ys * WC + lx;  // window(ys ly, ys lx): see haar_window_offset
     const int valsum = win[o + na] - win[o + nb] - win[o + nc] + win[o + nd];
     const uint64_t* q = Q + (int64_t)(y0 + ly * ys) * P + x0 + lx * ys;
     const double valsq = (double)(int64_t)(q[qa] - q[qb] - q[qc] + q[qd]);
@@ -261,41 +262,45 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
     for (int k = threadIdx.x; k < n; k += HT_THREADS) {
       const int p = list[cur][k];
       const int lx = p & (HT_X - 1), ly = p / HT_X;
-      const int32_t* w0 = win + ly * ys * WC + lx * ys;
+      const int32_t* w0 = win + ly * ys * WC + lx;
       const double f = vnf[p];
       int s = s0;
       for (; s < s1; s++) {
         const HaarStage st = stages[s];
         double acc = 0.0;
-        // 4 weak classifiers per step: their records (wave-uniform scalar loads) and all 36 window
-        // reads are issued together; the sum still accumulates in classifier order
-        auto value_of = [&](const HaarWeak& c) {
-          auto rs = [&](uint32_t ab, uint32_t cd) {  // corner offsets precomputed for this window pitch
-            return w0[ab & 0xFFFFu] - w0[ab >> 16] - w0[cd & 0xFFFFu] + w0[cd >> 16];
-          };
+        // 4 weak classifiers per step: their records (wave-uniform scalar loads) and all window reads
+        // are issued together; the sum accumulates in record order (two-rectangle classifiers first:
+        // the host checked that this stage's sum is exact in any order, HaarStage::n_two)
+        auto rs = [&](uint32_t ab, uint32_t cd) {  // corner offsets precomputed for this window pitch
+          return w0[ab & 0xFFFFu] - w0[ab >> 16] - w0[cd & 0xFFFFu] + w0[cd >> 16];
+        };
+        auto value_of = [&](const HaarWeak& c, auto three) {
           float ret = c.w0 * (float)rs(c.o[0], c.o[1]) + c.w1 * (float)rs(c.o[2], c.o[3]);
-          // two-rectangle features carry w2 = 0 and an empty rect 2: + (+0) leaves ret unchanged
-          // (up to the sign of a zero, which no comparison below distinguishes)
-          ret += c.w2 * (float)rs(c.o[4], c.o[5]);
+          if constexpr (decltype(three)::value) ret += c.w2 * (float)rs(c.o[4], c.o[5]);
           // HaarEvaluator::operator() (cascadedetect.hpp, 2.4.9) returns double: calc() * varianceNormFactor,
           // compared unrounded with the float threshold in predictOrderedStump
           return (double)ret * f;
         };
-        int i = st.first;
-        const int e = st.first + st.ntrees;
-        for (; i + 4 <= e; i += 4) {
-          const HaarWeak c0 = weak[i], c1 = weak[i + 1], c2 = weak[i + 2], c3 = weak[i + 3];
-          const double v0 = value_of(c0), v1 = value_of(c1), v2 = value_of(c2), v3 = value_of(c3);
-          acc += (double)(v0 < (double)c0.thr ? c0.leaf0 : c0.leaf1);
-          acc += (double)(v1 < (double)c1.thr ? c1.leaf0 : c1.leaf1);
-          acc += (double)(v2 < (double)c2.thr ? c2.leaf0 : c2.leaf1);
-          acc += (double)(v3 < (double)c3.thr ? c3.leaf0 : c3.leaf1);
-        }
-        for (; i < e; i++) {
-          const HaarWeak c = weak[i];
-          const double v = value_of(c);
-          acc += (double)(v < (double)c.thr ? c.leaf0 : c.leaf1);
-        }
+        auto run = [&](int i, int e, auto three) {
+          for (; i + 4 <= e; i += 4) {
+            const HaarWeak c0 = weak[i], c1 = weak[i + 1], c2 = weak[i + 2], c3 = weak[i + 3];
+            const double v0 = value_of(c0, three), v1 = value_of(c1, three), v2 = value_of(c2, three),
+                         v3 = value_of(c3, three);
+            acc += (double)(v0 < (double)c0.thr ? c0.leaf0 : c0.leaf1);
+            acc += (double)(v1 < (double)c1.thr ? c1.leaf0 : c1.leaf1);
+            acc += (double)(v2 < (double)c2.thr ? c2.leaf0 : c2.leaf1);
+            acc += (double)(v3 < (double)c3.thr ? c3.leaf0 : c3.leaf1);
+          }
+          for (; i < e; i++) {
+            const HaarWeak c = weak[i];
+            const double v = value_of(c, three);
+            acc += (double)(v < (double)c.thr ? c.leaf0 : c.leaf1);
+          }
+        };
+        // two-rectangle features: rect 2 is empty (w2 = 0), and + 0 * 0 leaves ret unchanged up to the
+        // sign of a zero, which no comparison distinguishes
+        run(st.first, st.first + st.n_two, std::false_type{});
+        run(st.first + st.n_two, st.first + st.ntrees, std::true_type{});
         if (acc < (double)st.thr) break;
       }
       const int ix = tx * HT_X + lx, iy = ty * HT_Y + ly;

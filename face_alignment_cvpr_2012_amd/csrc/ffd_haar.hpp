@@ -49,7 +49,7 @@ static_assert(sizeof(HaarWeak) == 48, "HaarWeak is 48 bytes");
 struct HaarStage {
   int32_t first, ntrees;
   float thr;  // (float)stageThreshold - 1e-5f (CascadeClassifier::Data::read THRESHOLD_EPS)
-  int32_t pad;
+  int32_t n_two;  // its first n_two classifiers are two-rectangle features (ffd_detect.cpp load_cascade)
 };
 
 void launch_haar_gray(const HaarFrame* frames, int n_frames, int max_pixels, const uint8_t* images, uint8_t* gray,
@@ -65,6 +65,14 @@ void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, c
                          const HaarWeak* weak, int n_weak, const HaarStage* stages, int n_stages, int ww, int wh,
                          int8_t* result, int lds_bytes, hipStream_t s);
 constexpr int haar_window_cols(int ystep, int ww) { return HAAR_TILE_X * ystep + ww; }
+// Element (row y, column x) of a tile's LDS integral window.  ystep 2 stores the even columns, then
+// the odd ones (half = ceil(cols / 2)): the 64 positions of a tile row are 2 columns apart, so a
+// corner read by a wave hits consecutive words (no 2-way bank conflict), and because a corner's
+// column parity is the same for every position, the offset stays position-independent:
+// window(2 ly + y, 2 lx + x) = [2 ly * cols + lx] + haar_window_offset(2, cols, y, x).
+constexpr int haar_window_offset(int ystep, int cols, int y, int x) {
+  return y * cols + (ystep == 2 ? (x & 1) * ((cols + 1) >> 1) + (x >> 1) : x);
+}
 // pack every frame's boxes (cap apart) contiguously: packed[i], owner[i]; totals[0] = box count
 void launch_haar_pack(int n_frames, int cap, const int4* boxes, const int32_t* n_boxes, int4* packed, int32_t* owner,
                       hipStream_t s);
