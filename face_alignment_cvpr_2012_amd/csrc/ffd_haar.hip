@@ -191,7 +191,10 @@ __global__ __launch_bounds__(256) void k_haar_cols(const HaarLevel* __restrict__
 // lane alive through the early stages and runs ~100 weak classifiers for lanes that need ~10).
 // Each stage's sum restarts at 0, so splitting at stage boundaries is exact.
 // Result per position: 1 (face) or -stage (stage 0 -> 0), as int8.
-constexpr int HT_X = 64, HT_Y = 8, HT_THREADS = 256, HT_POS = HT_X * HT_Y;
+#ifndef FFD_HAAR_THREADS
+#define FFD_HAAR_THREADS 256
+#endif
+constexpr int HT_X = 64, HT_Y = FFD_HAAR_TILE_Y, HT_THREADS = FFD_HAAR_THREADS, HT_POS = HT_X * HT_Y;
 #ifndef FFD_HAAR_PASSES
 #define FFD_HAAR_PASSES 5  // survivor-compaction passes over the stages (5: [0,1) [1,2) [2,4) [4,7) [7,n))
 #endif

@@ -58,7 +58,10 @@ void launch_haar_pyramid(const HaarLevel* levels, int n_levels, int max_pixels, 
                          const uint8_t* gray, uint8_t* scaled, int32_t* sum, uint64_t* sq, hipStream_t s);
 // a workgroup per 64 x 8 scan positions: max_tiles = the largest level's ceil(nx / 64) * ceil(ny / 8);
 // lds_bytes = haar_cascade_lds(largest ystep of the batch, ww, wh) (dynamic LDS: the integral window)
-constexpr int HAAR_TILE_X = 64, HAAR_TILE_Y = 8;
+#ifndef FFD_HAAR_TILE_Y
+#define FFD_HAAR_TILE_Y 8  // scan rows per cascade workgroup tile
+#endif
+constexpr int HAAR_TILE_X = 64, HAAR_TILE_Y = FFD_HAAR_TILE_Y;
 int haar_cascade_lds(int max_ystep, int ww, int wh);
 // weak: the ystep-1 table, then (at weak + n_weak) the ystep-2 table
 void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint64_t* sq,
