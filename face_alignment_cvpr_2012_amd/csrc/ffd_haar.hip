@@ -191,6 +191,9 @@ __global__ __launch_bounds__(256) void k_haar_cols(const HaarLevel* __restrict__
 // lane alive through the early stages and runs ~100 weak classifiers for lanes that need ~10).
 // Each stage's sum restarts at 0, so splitting at stage boundaries is exact.
 // Result per position: 1 (face) or -stage (stage 0 -> 0), as int8.
+#ifndef FFD_HAAR_BATCH2
+#define FFD_HAAR_BATCH2 4  // two-rectangle classifiers evaluated per step (their corner reads issued together)
+#endif
 #ifndef FFD_HAAR_THREADS
 #define FFD_HAAR_THREADS 256
 #endif
@@ -285,14 +288,16 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
           return (double)ret * f;
         };
         auto run = [&](int i, int e, auto three) {
-          for (; i + 4 <= e; i += 4) {
-            const HaarWeak c0 = weak[i], c1 = weak[i + 1], c2 = weak[i + 2], c3 = weak[i + 3];
-            const double v0 = value_of(c0, three), v1 = value_of(c1, three), v2 = value_of(c2, three),
-                         v3 = value_of(c3, three);
-            acc += (double)(v0 < (double)c0.thr ? c0.leaf0 : c0.leaf1);
-            acc += (double)(v1 < (double)c1.thr ? c1.leaf0 : c1.leaf1);
-            acc += (double)(v2 < (double)c2.thr ? c2.leaf0 : c2.leaf1);
-            acc += (double)(v3 < (double)c3.thr ? c3.leaf0 : c3.leaf1);
+          constexpr int NB = decltype(three)::value ? 4 : FFD_HAAR_BATCH2;
+          for (; i + NB <= e; i += NB) {
+            HaarWeak c[NB];
+            double v[NB];
+#pragma unroll
+            for (int j = 0; j < NB; j++) c[j] = weak[i + j];
+#pragma unroll
+            for (int j = 0; j < NB; j++) v[j] = value_of(c[j], three);
+#pragma unroll
+            for (int j = 0; j < NB; j++) acc += (double)(v[j] < (double)c[j].thr ? c[j].leaf0 : c[j].leaf1);
           }
           for (; i < e; i++) {
             const HaarWeak c = weak[i];
