@@ -85,6 +85,7 @@ void ffd_engine::load_cascade(const ffd::ModelFile& m) {
   // all leaves are integer multiples of 2^e (e = the smallest leaf's last mantissa bit) and the sum of
   // the largest |leaf| per classifier stays below 2^(53 + e).  A stage that fails the check keeps its
   // order (n_two = 0: every classifier through the 12-corner form, which covers rect 2 empty).
+  haar_order_free = 1;
   for (auto& st : stages) {
     int emin = INT32_MAX;
     double bound = 0.0;
@@ -99,7 +100,11 @@ void ffd_engine::load_cascade(const ffd::ModelFile& m) {
       bound += std::max(std::fabs((double)w.leaf0), std::fabs((double)w.leaf1));
     }
     st.n_two = 0;
-    if (st.ntrees == 0 || emin == INT32_MAX || !(bound < std::ldexp(1.0, 52 + emin))) continue;
+    if (st.ntrees == 0 || emin == INT32_MAX) continue;  // a sum of zeros: exact in any order
+    if (!(bound < std::ldexp(1.0, 52 + emin))) {
+      haar_order_free = 0;
+      continue;
+    }
     std::vector<int> two, three;
     for (int i = st.first; i < st.first + st.ntrees; i++) (weak[i].w2 == 0.0f ? two : three).push_back(i);
     std::vector<HaarWeak> perm;
@@ -258,7 +263,7 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
       if (lds > 64 * 1024) return fail(e, FFD_ERR_UNSUPPORTED, "cascade window too large for the LDS tile");
       launch_haar_cascade(e->det_levels.as<HaarLevel>(), nL, max_tiles, e->det_sum.as<int32_t>(),
                           e->det_sq.as<uint64_t>(), e->haar_weak.as<HaarWeak>(), e->haar_nweak, e->haar_stage.as<HaarStage>(),
-                          e->haar_stages, e->haar_ww, e->haar_wh, e->det_res.as<int8_t>(), lds, s);
+                          e->haar_stages, e->haar_ww, e->haar_wh, e->haar_order_free, e->det_res.as<int8_t>(), lds, s);
     }
     int max_frame_rows = 0;
     for (const auto& f : frames) max_frame_rows = std::max(max_frame_rows, f.rows);

@@ -191,6 +191,12 @@ __global__ __launch_bounds__(256) void k_haar_cols(const HaarLevel* __restrict__
 // lane alive through the early stages and runs ~100 weak classifiers for lanes that need ~10).
 // Each stage's sum restarts at 0, so splitting at stage boundaries is exact.
 // Result per position: 1 (face) or -stage (stage 0 -> 0), as int8.
+#ifndef FFD_HAAR_GROUP_LANES
+#define FFD_HAAR_GROUP_LANES 8  // lanes per survivor in the last FFD_HAAR_GROUP_PASSES passes (1: a lane each)
+#endif
+#ifndef FFD_HAAR_GROUP_PASSES
+#define FFD_HAAR_GROUP_PASSES 1
+#endif
 #ifndef FFD_HAAR_BATCH2
 #define FFD_HAAR_BATCH2 4  // two-rectangle classifiers evaluated per step (their corner reads issued together)
 #endif
@@ -211,7 +217,8 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
                                                              const uint64_t* __restrict__ sq,
                                                              const HaarWeak* __restrict__ weak_tables, int n_weak,
                                                              const HaarStage* __restrict__ stages, int n_stages,
-                                                             int ww, int wh, int8_t* __restrict__ result) {
+                                                             int ww, int wh, int order_free,
+                                                             int8_t* __restrict__ result) {
   extern __shared__ __attribute__((aligned(16))) int32_t win[];
   __shared__ double vnf[HT_POS];
   __shared__ uint16_t list[2][HT_POS];
@@ -265,6 +272,59 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
     const int n = n_list[cur];
     if (threadIdx.x == 0) n_list[cur ^ 1] = 0;
     __syncthreads();
+#if FFD_HAAR_GROUP_LANES > 1
+    if (order_free && pass >= NP - FFD_HAAR_GROUP_PASSES) {
+      // Sparse late passes: FFD_HAAR_GROUP_LANES lanes per survivor, each summing every G-th classifier
+      // of a stage (records as vector loads), the partial sums combined across the group.  Valid
+      // because the host proved every stage's double leaf sum exact in any order (order_free).
+      constexpr int G = FFD_HAAR_GROUP_LANES;
+      const int sub = threadIdx.x & (G - 1);
+      for (int k = threadIdx.x / G; k < n; k += HT_THREADS / G) {
+        const int p = list[cur][k];
+        const int lx = p & (HT_X - 1), ly = p / HT_X;
+        const int32_t* w0 = win + ly * ys * WC + lx;
+        const double f = vnf[p];
+        auto rs = [&](uint32_t ab, uint32_t cd) {
+          return w0[ab & 0xFFFFu] - w0[ab >> 16] - w0[cd & 0xFFFFu] + w0[cd >> 16];
+        };
+        int s = s0;
+        for (; s < s1; s++) {
+          const HaarStage st = stages[s];
+          double acc = 0.0;
+          const int e = st.first + st.ntrees;
+          for (int i = st.first + sub; i < e; i += G) {
+            const HaarWeak c = weak[i];
+            float ret = c.w0 * (float)rs(c.o[0], c.o[1]) + c.w1 * (float)rs(c.o[2], c.o[3]);
+            if (c.w2 != 0.0f) ret += c.w2 * (float)rs(c.o[4], c.o[5]);  // rect 2 empty: + 0 (see above)
+            const double v = (double)ret * f;
+            acc += (double)(v < (double)c.thr ? c.leaf0 : c.leaf1);
+          }
+#pragma unroll
+          for (int d = 1; d < G; d <<= 1) acc += __shfl_xor(acc, d);
+          if (acc < (double)st.thr) break;
+        }
+        if (sub == 0) {
+          const int ix = tx * HT_X + lx, iy = ty * HT_Y + ly;
+          if (s < s1) result[L.res_off + (int64_t)iy * L.nx + ix] = (int8_t)(-s);
+          else if (s1 == n_stages) result[L.res_off + (int64_t)iy * L.nx + ix] = 1;
+          else list[cur ^ 1][atomicAdd(&n_list[cur ^ 1], 1)] = (uint16_t)p;
+        }
+      }
+      __syncthreads();
+      cur ^= 1;
+      continue;
+    }
+#endif
+#ifdef FFD_HAAR_PROBE_SKIPFROM  // timing probe only (wrong results): passes >= this reject without evaluating
+    if (pass >= FFD_HAAR_PROBE_SKIPFROM) {
+      for (int k = threadIdx.x; k < n; k += HT_THREADS) {
+        const int p = list[cur][k];
+        const int ix = tx * HT_X + (p & (HT_X - 1)), iy = ty * HT_Y + p / HT_X;
+        result[L.res_off + (int64_t)iy * L.nx + ix] = (int8_t)(-s0);
+      }
+      break;
+    }
+#endif
     for (int k = threadIdx.x; k < n; k += HT_THREADS) {
       const int p = list[cur][k];
       const int lx = p & (HT_X - 1), ly = p / HT_X;
@@ -664,10 +724,10 @@ int haar_cascade_lds(int max_ystep, int ww, int wh) {
 }
 
 void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint64_t* sq,
-                         const HaarWeak* weak, int n_weak, const HaarStage* stages, int n_stages, int ww, int wh, int8_t* result,
-                         int lds_bytes, hipStream_t s) {
+                         const HaarWeak* weak, int n_weak, const HaarStage* stages, int n_stages, int ww, int wh,
+                         int order_free, int8_t* result, int lds_bytes, hipStream_t s) {
   k_haar_cascade<<<dim3(max_tiles, n_levels), HT_THREADS, lds_bytes, s>>>(levels, sum, sq, weak, n_weak, stages,
-                                                                           n_stages, ww, wh, result);
+                                                                           n_stages, ww, wh, order_free, result);
 }
 
 void launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows, int32_t* rowcnt,

@@ -66,7 +66,7 @@ int haar_cascade_lds(int max_ystep, int ww, int wh);
 // weak: the ystep-1 table, then (at weak + n_weak) the ystep-2 table
 void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint64_t* sq,
                          const HaarWeak* weak, int n_weak, const HaarStage* stages, int n_stages, int ww, int wh,
-                         int8_t* result, int lds_bytes, hipStream_t s);
+                         int order_free, int8_t* result, int lds_bytes, hipStream_t s);
 constexpr int haar_window_cols(int ystep, int ww) { return HAAR_TILE_X * ystep + ww; }
 // Element (row y, column x) of a tile's LDS integral window.  ystep 2 stores the even columns, then
 // the odd ones (half = ceil(cols / 2)): the 64 positions of a tile row are 2 columns apart, so a
