@@ -515,7 +515,7 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
     w.gabor_mm.ensure((size_t)n * 5 * 64);
     HIP_CHECK(hipMemsetAsync(w.gabor_mm.p, 0, w.gabor_mm.n, st));
   }
-  upload(w.faces, fds, st);
+  upload_descriptors(w.faces, fds, st);
   HIP_CHECK(hipMemsetAsync(d_out, 0, (size_t)n * sizeof(FaceOut), st));
 
   const FaceDesc* dfd = w.faces.as<FaceDesc>();
@@ -588,8 +588,9 @@ void ffd_engine::analyze(const uint8_t* d_images, const std::vector<FaceDesc>& a
   for (int first = 0; first < n; first += max_chunk, k++) {
     const int cnt = std::min(max_chunk, n - first);
     Workspace& w = *ws[k % ws.size()];
-    // (h_fds reaches the device by a pageable copy, staged before the call returns, and the device
-    // buffers are reused in stream order: the host need not wait for the workspace's last chunk)
+    // (h_fds reaches the device through a pinned staging slot that is reused only after its copy ran,
+    // upload_descriptors; the device buffers are reused in stream order, so the host need not wait for
+    // the workspace's last chunk)
     w.h_fds.assign(all.begin() + first, all.begin() + first + cnt);
     run_chunk(w, d_images, d_out + first);
     w.desc = w.h_fds;

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstring>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -218,7 +219,43 @@ struct ffd_engine {
     pending.clear();
   }
 
+  // Pinned staging of the per-chunk face descriptors: a ring of slots, each reused only after the
+  // copy that last read it has run (its event), so the host can refill descriptors for the next
+  // chunk while earlier copies are still queued.
+  struct PinnedSlot {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool used = false;
+  };
+  PinnedSlot desc_pin[8];
+  int desc_pin_next = 0;
+  void upload_descriptors(DevBuf& dst, const std::vector<FaceDesc>& fds, hipStream_t st) {
+    const size_t bytes = fds.size() * sizeof(FaceDesc);
+    dst.ensure(bytes);
+    if (!bytes) return;
+    PinnedSlot& s = desc_pin[desc_pin_next++ & 7];
+    if (!s.ev) HIP_CHECK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+    if (s.used) HIP_CHECK(hipEventSynchronize(s.ev));
+    if (s.cap < bytes) {
+      if (s.p) HIP_CHECK(hipHostFree(s.p));
+      s.p = nullptr;
+      s.cap = 0;
+      HIP_CHECK(hipHostMalloc(&s.p, bytes, hipHostMallocDefault));
+      s.cap = bytes;
+    }
+    std::memcpy(s.p, fds.data(), bytes);
+    HIP_CHECK(hipMemcpyAsync(dst.p, s.p, bytes, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipEventRecord(s.ev, st));
+    s.used = true;
+  }
+
   ~ffd_engine() {
+    for (auto& s : desc_pin) {
+      if (s.used) (void)hipEventSynchronize(s.ev);
+      if (s.ev) (void)hipEventDestroy(s.ev);
+      if (s.p) (void)hipHostFree(s.p);
+    }
     for (auto& p : pending) { event_pool.push_back(p.a); event_pool.push_back(p.b); }
     for (auto e : event_pool) (void)hipEventDestroy(e);
     if (copy_done) (void)hipEventDestroy(copy_done);

@@ -1030,6 +1030,27 @@ __host__ __device__ __forceinline__ int trav_top_n(int T, int free_bytes, int to
 
 constexpr int BUF_WORD3 = 0x00020000;  // raw buffer resource word 3 (gfx950: 32-bit data format)
 
+// Walk statistics (measurement builds only, tools/trav_stats.py): per (workgroup, block iteration,
+// wave) one record of 8 u32 — walker waves 0..7: {t0 (shader clock, low 32 bits, after the window
+// barrier), walk cycles, visits in the LDS tops, deep visits (node fetches), longest walk of the wave,
+// walks, longest deep part, block}; slot 8 (first stager wave): {t after barrier 1, commit cycles
+// (waits for its window loads), 0, 0, 0, 0, 0, block}.
+#ifndef FFD_TRAV_STATS
+#define FFD_TRAV_STATS 0
+#endif
+#if FFD_TRAV_STATS
+constexpr int TRAV_STATS_ITERS = 1024, TRAV_STATS_SLOTS = 9;
+__device__ uint32_t* g_trav_stats[2];  // [hp]
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+  for (int o = 32; o; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o, 64));
+  return v;
+}
+#endif
+
 struct TravArgs {
   const FaceDesc* faces;
   int n_faces, bpf;        // blocks per face: ceil(nx/G) * ceil(ny/G) (max over the batch)
@@ -1088,6 +1109,9 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     return B;
   };
 
+#if FFD_TRAV_STATS
+  uint32_t st_top = 0, st_deep = 0, st_max = 0, st_walks = 0, st_maxdeep = 0, st_ttest = 0, st_tfetch = 0;
+#endif
   auto walk_block = [&](const Blk& B) {
     const FaceDesc& fd = A.faces[B.f];
     const int items = GG * B.T, sh = B.px0 & 3;
@@ -1128,10 +1152,16 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       uint32_t h = 0, s = 0;
       uint4 R = trec[0];
       uint32_t lo = R.x, hi = R.z;
+#if FFD_TRAV_STATS
+      uint32_t wt = 0, wd = 0;
+#endif
       while (lo < (63u << 26)) {  // not a leaf (ch = 63)
         const uint32_t h2 = h ? 2u * h + s : 1u;
         if (h2 >= (uint32_t)topn) break;
         const uint4 N = trec[h2];
+#if FFD_TRAV_STATS
+        wt++;
+#endif
         s = test(lo, hi);
         h = h2;
         R = N;
@@ -1154,12 +1184,32 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
 #else
         const uint4 N = A.pairs[Q];
 #endif
+#if FFD_TRAV_STATS
+        wd++;
+#endif
+#if FFD_TRAV_STATS == 2  // step timing: test (LDS reads + VALU) vs the wait for the fetched record
+        uint64_t ta, tb, tc;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ta)::"memory");
+#endif
         s = test(lo, hi);
+#if FFD_TRAV_STATS == 2
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tb) : "v"(s) : "memory");
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tc) : "v"(N.x), "v"(N.w) : "memory");
+        st_ttest += (uint32_t)(tb - ta);
+        st_tfetch += (uint32_t)(tc - tb);
+#endif
         P = Q;
         R = N;
         lo = s ? R.y : R.x;
         hi = s ? R.w : R.z;
       }
+#if FFD_TRAV_STATS
+      st_top += wt;
+      st_deep += wd;
+      st_max = max(st_max, wt + wd);
+      st_maxdeep = max(st_maxdeep, wd);
+      st_walks++;
+#endif
       out[(xi * B.ny + yi) * B.T + t] = (int32_t)((lo & 0xFFFFFu) | hi << 20);  // reference order
     }
   };
@@ -1288,9 +1338,24 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
 
     Blk cur = block(lb);
     prefetch(cur);
+#if FFD_TRAV_STATS
+    int iter = 0;
+#endif
     for (; lb < end; lb += nk) {
       __syncthreads();  // the previous block's walks are done with the window
+#if FFD_TRAV_STATS
+      const uint64_t tc0 = __builtin_amdgcn_s_memtime();
+#endif
       commit(cur);
+#if FFD_TRAV_STATS
+      __builtin_amdgcn_s_waitcnt(0);
+      const uint64_t tc1 = __builtin_amdgcn_s_memtime();
+      if (tid == NW && iter < TRAV_STATS_ITERS) {
+        uint32_t* r = g_trav_stats[HP] + ((size_t)(blockIdx.x * TRAV_STATS_ITERS + iter) * TRAV_STATS_SLOTS + 8) * 8;
+        r[0] = (uint32_t)tc0; r[1] = (uint32_t)(tc1 - tc0); r[7] = (uint32_t)lb;
+      }
+      iter++;
+#endif
       __syncthreads();  // the window holds block lb
       Blk nxt;
       nxt.ok = false;
@@ -1299,12 +1364,37 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       cur = nxt;
     }
   } else {
+#if FFD_TRAV_STATS
+    int iter = 0;
+#endif
     for (; lb < end; lb += nk) {
       __syncthreads();
       __syncthreads();
+#if FFD_TRAV_STATS
+      const uint64_t t0 = __builtin_amdgcn_s_memtime();
+      st_top = st_deep = st_max = st_walks = st_maxdeep = 0;
+#endif
 #if FFD_TRAV_PROBE != 1
       const Blk cur = block(lb);
       if (cur.ok) walk_block(cur);
+#endif
+#if FFD_TRAV_STATS
+#if FFD_TRAV_STATS == 2  // per wave: test cycles and fetch-wait cycles summed over its deep steps
+      const uint32_t a0 = wave_max(st_ttest), a1 = wave_max(st_tfetch), a2 = wave_max(st_max), a3 = wave_sum(st_walks),
+                     a4 = wave_max(st_maxdeep);
+      st_ttest = st_tfetch = 0;
+#else
+      const uint32_t a0 = wave_sum(st_top), a1 = wave_sum(st_deep), a2 = wave_max(st_max), a3 = wave_sum(st_walks),
+                     a4 = wave_max(st_maxdeep);
+#endif
+      __builtin_amdgcn_s_waitcnt(0);
+      const uint64_t t1 = __builtin_amdgcn_s_memtime();
+      if ((tid & 63) == 0 && iter < TRAV_STATS_ITERS) {
+        uint32_t* r = g_trav_stats[HP] + ((size_t)(blockIdx.x * TRAV_STATS_ITERS + iter) * TRAV_STATS_SLOTS + (tid >> 6)) * 8;
+        r[0] = (uint32_t)t0; r[1] = (uint32_t)(t1 - t0); r[2] = a0; r[3] = a1; r[4] = a2; r[5] = a3; r[6] = a4;
+        r[7] = (uint32_t)lb;
+      }
+      iter++;
 #endif
     }
   }
@@ -2676,6 +2766,25 @@ hipError_t set_gabor_lds_limit(int bytes) {
   }
   return e;
 }
+
+#if FFD_TRAV_STATS
+// Measurement builds: allocate / read the walk statistics (tools/trav_stats.py).
+extern "C" int ffd_trav_stats_enable(void) {
+  for (int k = 0; k < 2; k++) {
+    uint32_t* p = nullptr;
+    const size_t bytes = (size_t)256 * TRAV_STATS_ITERS * TRAV_STATS_SLOTS * 8 * 4;
+    if (hipMalloc(&p, bytes) != hipSuccess || hipMemset(p, 0, bytes) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_trav_stats), &p, sizeof(p), k * sizeof(p)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+extern "C" int ffd_trav_stats_read(int hp, void* dst, size_t bytes) {
+  uint32_t* p[2];
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(p, HIP_SYMBOL(g_trav_stats), sizeof(p)) != hipSuccess) return -2;
+  return hipMemcpy(dst, p[hp ? 1 : 0], bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+}
+#endif
 
 hipError_t set_traverse_lds_limit(int bytes) {
   hipError_t e = hipSuccess;

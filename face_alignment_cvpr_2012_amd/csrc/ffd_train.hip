@@ -296,8 +296,11 @@ __device__ __forceinline__ TrFeature gen_feature(Draws& d, int ps, int smax) {
 }
 
 // ImageSample::evalTest, non-integral branch (ImageSample.cpp:40-47): rectangle sums from the exact
-// integral planes, (int)(sum / (float)area) = floor(sum / area) computed as (int)fma(sum, rcp(area),
-// 0.00075) (equal for every sum in [0, 255 area], area <= 484: tests/test_numerics.py).
+// integral planes, (int)(sum / (float)area) = floor(sum / area) (for sum < 2^24 the float quotient
+// never rounds up to the next integer: the gap k - sum / area >= 1 / area > k 2^-24).  Computed as
+// (int)fma(sum, rcp(area), 0.00075) for area <= 484, i.e. patch sizes up to 31 (equal for every sum in
+// [0, 255 area]: tests/test_numerics.py), and as the integer quotient above that (patch sizes up to 64
+// give areas up to 47 x 47; the rectangle is wave-uniform, so the branch does not diverge).
 __device__ __forceinline__ int eval_sample(const TrImage* __restrict__ imgs, const TrSample& s, const TrFeature& f,
                                            const uint32_t* __restrict__ chan) {
   const TrImage im = imgs[s.img];
@@ -306,7 +309,9 @@ __device__ __forceinline__ int eval_sample(const TrImage* __restrict__ imgs, con
   auto mean = [&](int rx, int ry, int rw, int rh) {
     const uint32_t* p = I + (size_t)(s.y + ry) * W1 + (s.x + rx);
     const uint32_t S = p[(size_t)rh * W1 + rw] - p[rw] - p[(size_t)rh * W1] + p[0];
-    return (int)__builtin_fmaf((float)S, __builtin_amdgcn_rcpf((float)(rw * rh)), 0.00075f);
+    const uint32_t area = (uint32_t)(rw * rh);
+    if (area > 484u) return (int)(S / area);
+    return (int)__builtin_fmaf((float)S, __builtin_amdgcn_rcpf((float)area), 0.00075f);
   };
   return mean(f.r[0], f.r[1], f.r[2], f.r[3]) - mean(f.r[4], f.r[5], f.r[6], f.r[7]);
 }

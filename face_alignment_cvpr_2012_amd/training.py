@@ -148,8 +148,14 @@ class TrainedTree:
     def num_samples(self):
         return int(_lib().ffd_trained_tree_num_samples(self._h))
 
-    def arrays(self, n_samples=0):
+    def arrays(self, n_samples=None, samples=None):
+        """The tree's pre-order arrays.  The sampled training patches are included when `samples` is true
+        (facial-feature trees; head-pose trees always include them); the buffer is sized from
+        num_samples.  `n_samples` is accepted for compatibility and must equal num_samples when given."""
         n, l = self.num_nodes, self.num_leaves
+        if n_samples is not None and n_samples != self.num_samples:
+            raise ValueError(f"n_samples {n_samples} != num_samples {self.num_samples}")
+        want = bool(samples) if samples is not None else bool(n_samples)
         if self.kind == 0:  # HeadPoseLeaf payloads, split modes, (image, x, y, label) patches
             a = {"node_leaf": np.zeros(n, np.int32), "node_split": np.zeros((n, 10), np.int16),
                  "node_info": np.zeros(n, np.float64), "node_mode": np.zeros(n, np.int32),
@@ -162,10 +168,11 @@ class TrainedTree:
         a = {"node_leaf": np.zeros(n, np.int32), "node_split": np.zeros((n, 10), np.int16),
              "node_info": np.zeros(n, np.float64), "leaf_n": np.zeros(l, np.int32), "leaf_fg": np.zeros(l, np.float32),
              "leaf_offset": np.zeros((l, 10, 2), np.int16), "leaf_var": np.zeros((l, 10), np.float32),
-             "leaf_pf": np.zeros((l, 10), np.float32), "samples": np.zeros((n_samples, 3), np.int32)}
+             "leaf_pf": np.zeros((l, 10), np.float32),
+             "samples": np.zeros((self.num_samples if want else 0, 3), np.int32)}
         _check(_lib().ffd_trained_tree_arrays(self._h, *(a[k].ctypes.data for k in
                ("node_leaf", "node_split", "node_info", "leaf_n", "leaf_fg", "leaf_offset", "leaf_var", "leaf_pf")),
-               a["samples"].ctypes.data if n_samples else None))
+               a["samples"].ctypes.data if want else None))
         return a
 
     @property
