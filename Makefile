@@ -19,13 +19,16 @@ MODEL     := model/ffd_model.bin
 EXAMPLE   := examples/build/analyze_face
 EXAMPLE2  := examples/build/estimate
 EXAMPLE3  := examples/build/bench_host
+EXAMPLE4  := examples/build/evaluate_mt
+EXAMPLE5  := examples/build/reference_main
 
 HIP_OBJS  := $(PKG)/lib/ffd_kernels.o $(PKG)/lib/ffd_engine.o $(PKG)/lib/ffd_group.o $(PKG)/lib/ffd_archive.o \
-             $(PKG)/lib/ffd_haar.o $(PKG)/lib/ffd_detect.o $(PKG)/lib/ffd_train_k.o $(PKG)/lib/ffd_train.o
+             $(PKG)/lib/ffd_haar.o $(PKG)/lib/ffd_detect.o $(PKG)/lib/ffd_train_k.o $(PKG)/lib/ffd_train.o \
+             $(PKG)/lib/ffd_convert.o
 HDRS      := include/ffd.h include/ffd_numerics.h include/ffd_gabor.h include/ffd_model_format.h $(CSRC)/ffd_device.hpp \
              $(CSRC)/ffd_kernels.hpp $(CSRC)/model_io.hpp $(CSRC)/ffd_engine_impl.hpp $(CSRC)/ffd_haar.hpp
 
-all: $(LIB) $(CONVERT) $(SYNTH) $(ORACLE) $(EXAMPLE) $(EXAMPLE2) $(EXAMPLE3)
+all: $(LIB) $(CONVERT) $(SYNTH) $(ORACLE) $(EXAMPLE) $(EXAMPLE2) $(EXAMPLE3) $(EXAMPLE4) $(EXAMPLE5)
 
 $(PKG)/lib/ffd_kernels.o: $(CSRC)/ffd_kernels.hip $(HDRS)
 	@mkdir -p $(@D)
@@ -37,6 +40,11 @@ $(PKG)/lib/ffd_engine.o: $(CSRC)/ffd_engine.cpp $(HDRS)
 
 # host-only (the archive writer): plain g++
 $(PKG)/lib/ffd_archive.o: $(CSRC)/ffd_archive.cpp include/ffd.h include/ffd_model_format.h $(CSRC)/model_io.hpp
+	@mkdir -p $(@D)
+	$(CXX) $(CXXFLAGS) -Iinclude -c $< -o $@
+
+# the archive converter (ffd_model_convert) in the library; the CLI below is the same file with main()
+$(PKG)/lib/ffd_convert.o: $(CSRC)/ffd_convert.cpp $(CSRC)/model_io.hpp include/ffd_model_format.h include/ffd.h
 	@mkdir -p $(@D)
 	$(CXX) $(CXXFLAGS) -Iinclude -c $< -o $@
 
@@ -69,9 +77,9 @@ $(SYNTH): $(CSRC)/ffd_synth_forest.cpp $(CSRC)/model_io.hpp include/ffd_model_fo
 	@mkdir -p $(@D)
 	$(CXX) $(CXXFLAGS) -o $@ $<
 
-$(CONVERT): $(CSRC)/ffd_convert.cpp $(CSRC)/model_io.hpp include/ffd_model_format.h
+$(CONVERT): $(CSRC)/ffd_convert.cpp $(CSRC)/model_io.hpp include/ffd_model_format.h include/ffd.h
 	@mkdir -p $(@D)
-	$(CXX) $(CXXFLAGS) -o $@ $<
+	$(CXX) $(CXXFLAGS) -DFFD_CONVERT_MAIN -o $@ $<
 
 $(ORACLE): oracle/ffd_oracle.cpp oracle/ffd_train_oracle.cpp oracle/ffd_oracle.h include/ffd_numerics.h include/ffd_gabor.h include/ffd_model_format.h
 	@mkdir -p $(@D)
@@ -95,5 +103,11 @@ $(EXAMPLE2): examples/estimate.cpp include/FaceForest.hpp include/ffd.h $(LIB)
 $(EXAMPLE3): examples/bench_host.cpp include/FaceForest.hpp include/ffd.h $(LIB)
 	@mkdir -p $(@D)
 	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(PKG)/lib -lffd -Wl,-rpath,'$$ORIGIN/../../$(PKG)/lib'
-example: $(EXAMPLE) $(EXAMPLE2) $(EXAMPLE3)
+$(EXAMPLE4): examples/evaluate_mt.cpp include/FaceForest.hpp include/ffd.h $(LIB)
+	@mkdir -p $(@D)
+	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(PKG)/lib -lffd -Wl,-rpath,'$$ORIGIN/../../$(PKG)/lib'
+$(EXAMPLE5): examples/reference_main.cpp include/FaceForest.hpp include/ffd.h $(LIB)
+	@mkdir -p $(@D)
+	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(PKG)/lib -lffd -Wl,-rpath,'$$ORIGIN/../../$(PKG)/lib'
+example: $(EXAMPLE) $(EXAMPLE2) $(EXAMPLE3) $(EXAMPLE4) $(EXAMPLE5) $(EXAMPLE5)
 .PHONY: example

@@ -288,7 +288,7 @@ def landmark_error(wl, d_out, budget_s=10.0):
     return out
 
 
-def host_inclusive(ff, wl, iw, ih, steps, chunks=4):
+def host_inclusive(ff, wl, iw, ih, steps, warmup=1, chunks=4):
     """SURVEY.md §8(d)'s timing rule for the host API: batch in pinned host memory -> H2D -> the
     path -> D2H of the records, in `chunks` chunks whose H2D (own stream) overlaps the previous
     chunk's compute (engine stream).  C2-shaped workloads only (one image per face)."""
@@ -319,12 +319,14 @@ def host_inclusive(ff, wl, iw, ih, steps, chunks=4):
         ff.synchronize()
         torch.cuda.synchronize()
 
-    run()
+    for _ in range(max(1, warmup)):
+        run()
     t0 = time.perf_counter()
     for _ in range(steps):
         run()
     dt = (time.perf_counter() - t0) / steps
     return {"value": round(n / dt, 1), "unit": "faces/s", "ms_per_step": round(dt * 1e3, 3), "chunks": chunks,
+            "steps": steps, "warmup": max(1, warmup),
             "h2d_bytes": int(n * per_img), "note": "pinned host batch in, host records out; chunked H2D on its own "
                                                    "stream overlapping the previous chunk's compute"}
 
@@ -353,6 +355,39 @@ def cxx_host_path(wl, reps=5):
     d["note"] = ("examples/bench_host.cpp: FaceForest::analyzeFaces (C++ shim -> ffd_analyze_faces) on pageable "
                  "host crops, median of %d batch calls; latency = analyzeFace per call, median of 50" % reps)
     return d
+
+
+def evaluate_mt_path(wl):
+    """The reference's low-level call pattern (getFacialFeaturesVotesMT, src/face_utils.cpp:244-302) from C++
+    (examples/evaluate_mt.cpp through include/FaceForest.hpp): ImageSample on the device, one
+    Forest<MPSample>::evaluateMT per patch (1,024 calls on copies of the forest), the vote filter, MeanShift per
+    landmark, for face 0 of the workload; timings of the third repetition.  A child process, run before this one
+    initialises the GPU."""
+    import tempfile
+    exe = os.path.join(REPO, "examples", "build", "evaluate_mt")
+    if not os.path.exists(exe):
+        return None
+    img, box = wl.face(0)
+    ih, iw = img.shape[:2]
+    with tempfile.NamedTemporaryFile(suffix=".bgr", delete=False) as fh:
+        np.ascontiguousarray(img).tofile(fh)
+        path = fh.name
+    try:
+        r = subprocess.run([exe, wl.model, "--crop", path, str(iw), str(ih)] + [str(int(v)) for v in box],
+                           capture_output=True, text=True, timeout=300)
+    finally:
+        os.unlink(path)
+    if r.returncode != 0:
+        return {"error": r.stderr.strip()[-300:]}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    keep = ("patches", "trees", "sample_ms", "first_call_ms", "other_calls_mean_us", "all_calls_ms", "vote_filter_ms",
+            "meanshift_ms", "cold_first_call_ms", "reps")
+    out = {k: d[k] for k in keep}
+    out["per_call_us"] = round(d["all_calls_ms"] * 1e3 / d["patches"], 4)
+    out["note"] = ("examples/evaluate_mt.cpp: Forest<MPSample>::evaluateMT once per patch as face_utils.cpp:267-274; "
+                   "the first call of a sample evaluates its patch grid in one launch (ffd_sample_eval_grid), the "
+                   "others read that result")
+    return out
 
 
 def single_face_latency(ff, wl, reps=50):
@@ -530,9 +565,10 @@ def main():
 
     faces = args.faces or (1024 if args.workload == "c4" else 4096)
     wl = make_workload(args.workload, rank, world, faces, args.frames)
-    cxx_host = None
+    cxx_host = eval_mt = None
     if world == 1 and wl.name == "c2" and not args.no_host_paths:
-        cxx_host = cxx_host_path(wl)  # a child process, before this one initialises the GPU
+        cxx_host = cxx_host_path(wl)  # child processes, before this one initialises the GPU
+        eval_mt = evaluate_mt_path(wl)
     n = wl.n
     n_img, ih, iw = wl.n_images, wl.images.shape[1], wl.images.shape[2]
     d_images = torch.from_numpy(np.ascontiguousarray(wl.images)).to(dev)
@@ -612,7 +648,7 @@ def main():
     ff.set_profiling(False)
     host_incl = latency = None
     if world == 1 and wl.name == "c2" and not args.no_host_paths:
-        host_incl = host_inclusive(ff, wl, iw, ih, max(1, min(args.steps, 3)))
+        host_incl = host_inclusive(ff, wl, iw, ih, args.steps, args.warmup)
         latency = single_face_latency(ff, wl)
     detect_ms = None
     if args.detect:  # the detector alone, same frames (its share of the step)
@@ -697,12 +733,23 @@ def main():
             out["c4"] = {"patches_per_face": round(n_mp, 1), "patches_per_s": round(value * n_mp, 1),
                          "walks_per_s": round(value * n_mp * 20, 1), "forest_depth": 20}
         if host_incl is not None:
+            # SURVEY.md §8(d)'s rule (H2D of the batch -> D2H of the records), same steps and warm-ups as `value`;
+            # `value` is the device-resident throughput (inputs already in HBM, results left there)
+            host_incl["rule"] = "SURVEY.md 8(d): H2D of the batch to D2H of results"
             out["host_inclusive"] = host_incl
+            out["headline"] = ("value = device-resident throughput (batch in HBM); host_inclusive.value = the "
+                               "SURVEY 8(d) H2D->D2H figure at the same steps / warm-ups")
             out["analyze_face_latency"] = latency
         if cxx_host is not None:
             out["cxx_host_path"] = cxx_host
             if host_incl is not None and "batch_faces_per_s" in cxx_host:
                 cxx_host["vs_host_inclusive"] = round(cxx_host["batch_faces_per_s"] / host_incl["value"], 3)
+        if eval_mt is not None:
+            out["evaluate_mt_path"] = eval_mt
+            if "all_calls_ms" in eval_mt:
+                per_face_us = elapsed / total_faces * 1e6  # the batched path's per-face cost
+                eval_mt["batched_per_face_us"] = round(per_face_us, 3)
+                eval_mt["calls_vs_batched_per_face"] = round(eval_mt["all_calls_ms"] * 1e3 / per_face_us, 2)
         if detect_ms is not None:
             out["detect"] = {"frames_per_step": wl.n_images * world, "faces_found": wl.total_faces,
                              "detect_ms_per_step": round(detect_ms, 3),

@@ -19,7 +19,7 @@ import numpy as np
 __all__ = [
     "FaceForestOptions", "HeadPoseEstimatorOption", "MultiPartEstimatorOption", "MeanShiftOption",
     "Face", "FaceForest", "FaceForestGroup", "Forest", "FFDError", "default_model_path", "library_path",
-    "comm_id", "status_string",
+    "comm_id", "status_string", "ImageSample", "meanshift",
     "FOREST_HEADPOSE", "FOREST_FFD", "LANDMARK_NAMES",
 ]
 
@@ -124,6 +124,10 @@ EXPORTED_SYMBOLS = (
     "ffd_trained_tree_save", "ffd_trained_tree_free",
     "ffd_train_hp_param_init", "ffd_train_hp_tree", "ffd_trained_tree_kind", "ffd_trained_tree_num_samples",
     "ffd_trained_tree_hp_arrays",
+    "ffd_sample_create", "ffd_sample_create_from_channels", "ffd_sample_destroy", "ffd_sample_size",
+    "ffd_sample_channels", "ffd_sample_eval_leaves", "ffd_sample_eval_grid", "ffd_sample_estimate_headpose",
+    "ffd_sample_estimate_facial_features", "ffd_meanshift", "ffd_model_convert", "ffd_model_convert_last_error",
+    "ffd_forest_subdirs",
 )
 COMM_ID_BYTES = 128
 STATUS_OK, STATUS_INVALID_ARGUMENT, STATUS_UNSUPPORTED = 0, 1, 7
@@ -206,6 +210,23 @@ def lib():
     L.ffd_model_tree_archive.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                          ctypes.c_int64, P(ctypes.c_int64)]
     L.ffd_model_save_tree.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p]
+    vp, i32 = ctypes.c_void_p, ctypes.c_int32
+    L.ffd_sample_create.argtypes = [vp, vp, i32, i32, i32, P(vp)]
+    L.ffd_sample_create_from_channels.argtypes = [vp, vp, i32, i32, P(vp)]
+    L.ffd_sample_destroy.argtypes = [vp]
+    L.ffd_sample_destroy.restype = None
+    L.ffd_sample_size.argtypes = [vp, P(i32), P(i32)]
+    L.ffd_sample_channels.argtypes = [vp, vp]
+    L.ffd_sample_eval_leaves.argtypes = [vp, i32, vp, i32, vp, i32, vp]
+    L.ffd_sample_eval_grid.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, i32, vp]
+    L.ffd_sample_estimate_headpose.argtypes = [vp, P(_Rect), P(_HpOpt), P(ctypes.c_float), P(ctypes.c_float)]
+    L.ffd_sample_estimate_facial_features.argtypes = [vp, P(_Rect), vp, i32, P(_MpOpt), vp]
+    L.ffd_meanshift.argtypes = [vp, vp, i32, P(_MsOpt), vp]
+    L.ffd_model_convert_last_error.restype = ctypes.c_char_p
+    for name in ("ffd_sample_create", "ffd_sample_create_from_channels", "ffd_sample_size", "ffd_sample_channels",
+                 "ffd_sample_eval_leaves", "ffd_sample_eval_grid", "ffd_sample_estimate_headpose",
+                 "ffd_sample_estimate_facial_features", "ffd_meanshift"):
+        getattr(L, name).restype = ctypes.c_int
     for name in ("ffd_detect_faces", "ffd_detect_faces_device", "ffd_analyze_images", "ffd_detect_candidates",
                  "ffd_model_open", "ffd_model_tree_save_path", "ffd_model_tree_archive", "ffd_model_save_tree","ffd_engine_create", "ffd_face_geometry", "ffd_analyze_faces", "ffd_analyze_faces_device",
                  "ffd_synchronize", "ffd_extract_channels", "ffd_forest_eval_leaves", "ffd_get_trace",
@@ -652,6 +673,104 @@ class FaceForestGroup:
         if st != 0:
             raise FFDError(st, lib().ffd_group_last_error(self._h).decode(errors="replace"))
         return [_face_from_record(r) for r in out]
+
+
+class ImageSample:
+    """ImageSample (src/ImageSample.cpp:11-20, include/ImageSample.hpp:146-190) kept in HBM (ffd_sample_create):
+    the 38 integral channels of an 8-bit gray face, with Forest<S>::evaluateMT on its patches (a list or the
+    estimators' grid) and the static estimators of FaceForest on it.  Owned by the FaceForest that made it;
+    close() (or a with-block) frees it."""
+
+    def __init__(self, face_forest, gray=None, channels=None):
+        self.ff = face_forest
+        h = ctypes.c_void_p()
+        if channels is not None:
+            ch = np.ascontiguousarray(channels, np.uint32)
+            _check(lib().ffd_sample_create_from_channels(face_forest.handle, ch.ctypes.data, ch.shape[2] - 1,
+                                                         ch.shape[1] - 1, ctypes.byref(h)), face_forest.handle)
+        else:
+            g = np.ascontiguousarray(gray, np.uint8)
+            if g.ndim != 2:
+                raise ValueError("ImageSample: an 8-bit single-channel (gray) face")
+            _check(lib().ffd_sample_create(face_forest.handle, g.ctypes.data, g.shape[1], g.shape[0], g.strides[0],
+                                           ctypes.byref(h)), face_forest.handle)
+        self._h = h.value
+        w, hh = ctypes.c_int32(), ctypes.c_int32()
+        lib().ffd_sample_size(self._h, ctypes.byref(w), ctypes.byref(hh))
+        self.width, self.height = w.value, hh.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ffd_sample_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def channels(self):
+        out = np.zeros((38, self.height + 1, self.width + 1), np.uint32)
+        _check(lib().ffd_sample_channels(self._h, out.ctypes.data), self.ff.handle)
+        return out
+
+    def eval_leaves(self, kind, patches_xy, tree_ids):
+        p = np.ascontiguousarray(patches_xy, np.int32).reshape(-1, 2)
+        t = np.ascontiguousarray(tree_ids, np.int32)
+        out = np.zeros((p.shape[0], t.size), np.int32)
+        _check(lib().ffd_sample_eval_leaves(self._h, kind, p.ctypes.data, p.shape[0], t.ctypes.data, t.size,
+                                            out.ctypes.data), self.ff.handle)
+        return out
+
+    def eval_grid(self, kind, x0, y0, step, nx, ny, tree_ids):
+        t = np.ascontiguousarray(tree_ids, np.int32)
+        out = np.zeros((nx * ny, t.size), np.int32)
+        _check(lib().ffd_sample_eval_grid(self._h, kind, x0, y0, step, nx, ny, t.ctypes.data, t.size, out.ctypes.data),
+               self.ff.handle)
+        return out
+
+    def estimateHeadPose(self, face_bbox=None, options=None):
+        r = _Rect(*face_bbox) if face_bbox is not None else None
+        o = None
+        if options is not None:
+            o = _HpOpt(options.num_head_pose_labels, options.step_size, options.min_foreground_probability)
+        hp, var = ctypes.c_float(), ctypes.c_float()
+        _check(lib().ffd_sample_estimate_headpose(self._h, ctypes.byref(r) if r else None, ctypes.byref(o) if o else None,
+                                                  ctypes.byref(hp), ctypes.byref(var)), self.ff.handle)
+        return hp.value, var.value
+
+    def estimateFacialFeatures(self, face_bbox, tree_ids, options=None):
+        r = _Rect(*face_bbox) if face_bbox is not None else None
+        t = np.ascontiguousarray(tree_ids, np.int32)
+        o = None
+        if options is not None:
+            o = _MpOpt(options.num_parts, options.step_size, options.min_samples, options.min_forground,
+                       options.min_pf, options.max_variance, getattr(options, "step_size_y", 0))
+        pts = np.zeros((10, 2), np.int32)
+        _check(lib().ffd_sample_estimate_facial_features(self._h, ctypes.byref(r) if r else None, t.ctypes.data, t.size,
+                                                         ctypes.byref(o) if o else None, pts.ctypes.data), self.ff.handle)
+        return pts
+
+
+def meanshift(face_forest, votes, option=None):
+    """MeanShift::shift (include/MeanShift.hpp:41-76) of one vote list on the GPU: votes = [(x, y, weight, check)];
+    returns the mode before rounding (the reference's Point_<int> result is its cvRound)."""
+    v = np.zeros(len(votes), dtype=[("x", "<i4"), ("y", "<i4"), ("w", "<f4"), ("c", "<i4")])
+    for i, (x, y, w, c) in enumerate(votes):
+        v[i] = (x, y, w, int(bool(c)))
+    o = option or MeanShiftOption()
+    mo = _MsOpt(o.kernel_size, o.max_iterations, o.stopping_criteria)
+    out = np.zeros(2, np.float32)
+    _check(lib().ffd_meanshift(face_forest.handle, v.ctypes.data if len(v) else None, len(v), ctypes.byref(mo),
+                               out.ctypes.data), face_forest.handle)
+    return out
 
 
 class Forest:

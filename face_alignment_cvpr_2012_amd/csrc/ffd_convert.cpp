@@ -12,10 +12,12 @@
 // Archive grammar: SURVEY.md Appendix A.  Trees whose i_node != m_num_nodes are
 // rejected exactly like Forest::load_tree (Forest.hpp:142-152).
 //
-// usage: ffd_convert <reference_root> <out.bin>
+// usage: ffd_convert <reference_root> <out.bin>   (built with -DFFD_CONVERT_MAIN)
 //   reads <root>/data/config_headpose.txt and <root>/data/config_ffd.txt, then
 //   the tree directories they name (relative to <root>); the FFD directory is
 //   scanned for sub-directories which are sorted (FaceForest.cpp:39-45).
+// The same conversion is in libffd.so as ffd_model_convert (the C++ FaceForest shim runs it for
+// reference-style FaceForestOptions: tree directories instead of a converted model).
 #include <dirent.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -23,6 +25,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstring>
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
@@ -34,6 +37,7 @@
 #include <vector>
 
 #include "model_io.hpp"
+#include "../../include/ffd.h"
 
 namespace {
 
@@ -46,7 +50,7 @@ struct ForestParam {  // Constants.hpp:24-60
 };
 
 // loadConfigFile (face_utils.cpp:50-140): fixed order of (comment line, value line) pairs.
-bool load_config(const std::string& path, ForestParam& p) {
+[[maybe_unused]] bool load_config(const std::string& path, ForestParam& p) {
   std::ifstream f(path);
   if (!f.is_open()) return false;
   std::string line;
@@ -59,14 +63,22 @@ bool load_config(const std::string& path, ForestParam& p) {
   std::string v;
   if (!next_value(p.image_path)) return false;
   if (!next_value(p.tree_path)) return false;
-  if (!next_value(v)) return false; p.ntrees = std::stoi(v);
-  if (!next_value(v)) return false; p.ntests = std::stoi(v);
-  if (!next_value(v)) return false; p.max_depth = std::stoi(v);
-  if (!next_value(v)) return false; p.min_patches = std::stoi(v);
-  if (!next_value(v)) return false; p.nimages = std::stoi(v);
-  if (!next_value(v)) return false; p.npatches = std::stoi(v);
-  if (!next_value(v)) return false; p.face_size = std::stoi(v);
-  if (!next_value(v)) return false; p.patch_size_ratio = std::stof(v);
+  if (!next_value(v)) return false;
+  p.ntrees = std::stoi(v);
+  if (!next_value(v)) return false;
+  p.ntests = std::stoi(v);
+  if (!next_value(v)) return false;
+  p.max_depth = std::stoi(v);
+  if (!next_value(v)) return false;
+  p.min_patches = std::stoi(v);
+  if (!next_value(v)) return false;
+  p.nimages = std::stoi(v);
+  if (!next_value(v)) return false;
+  p.npatches = std::stoi(v);
+  if (!next_value(v)) return false;
+  p.face_size = std::stoi(v);
+  if (!next_value(v)) return false;
+  p.patch_size_ratio = std::stof(v);
   if (!next_value(v)) return false;
   std::istringstream ss(v);
   std::string tok;
@@ -464,8 +476,117 @@ void put_cascade(ffd::ModelFile& m, const Cascade& c) {
   m.put<float>("haar.feature_weight", "f32", {F, 3}, c.feature_weight);
 }
 
+
+// Convert the archives of one head-pose forest (hp.ntrees trees in hp_dir, Forest::load Forest.hpp:116-127)
+// and of the pose-conditional FFD forests (mp.ntrees trees in each of mp_dirs, already in the reference's
+// sorted order, FaceForest.cpp:39-55) plus an optional Haar cascade into an FFDMODEL file.
+std::string convert_model(const ForestParam& hp, const std::string& hp_dir, const ForestParam& mp,
+                          const std::vector<std::string>& mp_dirs, const std::string& cascade_xml,
+                          const std::string& outp) {
+  ffd::ModelFile m;
+  ForestOut hpo;
+  char buf[4096];
+  for (int i = 0; i < hp.ntrees; i++) {  // Forest::load (Forest.hpp:116-127)
+    std::snprintf(buf, sizeof buf, "%s/tree_%03d.txt", hp_dir.c_str(), i);
+    parse_tree(buf, HP, hpo);
+  }
+  put_params(m, "hp", hp, 1);
+  put_forest(m, "hp", HP, hpo);
+  if (mp_dirs.empty()) throw std::runtime_error("no FFD forest directories");
+  ForestOut mpo;
+  for (auto& d : mp_dirs)
+    for (int i = 0; i < mp.ntrees; i++) {
+      std::snprintf(buf, sizeof buf, "%s/tree_%03d.txt", d.c_str(), i);
+      parse_tree(buf, MP, mpo);
+    }
+  put_params(m, "mp", mp, (int)mp_dirs.size());
+  put_forest(m, "mp", MP, mpo);
+  Cascade cas;  // FaceDetectionOption::path_face_cascade as demo.cpp:186 / eval_ffd.cpp:143 set it
+  const bool have_cascade = !cascade_xml.empty() && parse_cascade(cascade_xml, cas);
+  if (have_cascade) put_cascade(m, cas);
+  std::string tmp = outp + ".tmp";
+  m.save(tmp);
+  if (std::rename(tmp.c_str(), outp.c_str()) != 0) throw std::runtime_error("rename failed: " + outp);
+  std::string msg = "hp " + std::to_string(hpo.tree_node_off.size() - 1) + " trees " +
+                    std::to_string(hpo.node_leaf.size()) + " nodes " + std::to_string(hpo.leaf_n.size()) +
+                    " leaves; mp " + std::to_string(mp_dirs.size()) + " forests " +
+                    std::to_string(mpo.tree_node_off.size() - 1) + " trees " + std::to_string(mpo.node_leaf.size()) +
+                    " nodes " + std::to_string(mpo.leaf_n.size()) + " leaves -> " + outp;
+  if (have_cascade)
+    msg += "\nhaar cascade " + std::to_string(cas.win_w) + "x" + std::to_string(cas.win_h) + ", " +
+           std::to_string(cas.stage_threshold.size()) + " stages, " + std::to_string(cas.weak_feature.size()) +
+           " weak classifiers, " + std::to_string(cas.feature_weight.size() / 3) + " features";
+  return msg;
+}
+
+thread_local std::string g_convert_error;
+
+ForestParam from_c(const ffd_forest_param& c) {
+  ForestParam p;
+  p.max_depth = c.max_depth; p.min_patches = c.min_patches; p.ntests = c.ntests; p.ntrees = c.ntrees;
+  p.nimages = c.nimages; p.npatches = c.npatches; p.face_size = c.face_size;
+  p.patch_size_ratio = c.patch_size_ratio;
+  p.tree_path = c.tree_path ? c.tree_path : "";
+  p.image_path = c.image_path ? c.image_path : "";
+  for (int i = 0; i < c.n_features; i++) p.features.push_back(c.features[i]);
+  return p;
+}
+
 }  // namespace
 
+extern "C" {
+
+ffd_status ffd_model_convert(const ffd_forest_param* hp, const ffd_forest_param* mp, const char* const* mp_dirs,
+                             int32_t n_mp_dirs, const char* cascade_xml, const char* out_path) {
+  if (!hp || !mp || !out_path || !hp->tree_path || n_mp_dirs < 0 || (n_mp_dirs && !mp_dirs) ||
+      (hp->n_features && !hp->features) || (mp->n_features && !mp->features)) {
+    g_convert_error = "bad arguments";
+    return FFD_ERR_INVALID_ARGUMENT;
+  }
+  try {
+    std::vector<std::string> dirs;
+    for (int i = 0; i < n_mp_dirs; i++) dirs.push_back(mp_dirs[i]);
+    (void)convert_model(from_c(*hp), hp->tree_path, from_c(*mp), dirs, cascade_xml ? cascade_xml : "", out_path);
+    return FFD_OK;
+  } catch (const std::exception& e) {
+    g_convert_error = e.what();
+    return FFD_ERR_MODEL;
+  }
+}
+
+const char* ffd_model_convert_last_error(void) { return g_convert_error.c_str(); }
+
+ffd_status ffd_forest_subdirs(const char* dir, char* buf, int64_t cap, int64_t* size) {
+  if (!dir || !size) {
+    g_convert_error = "bad arguments";
+    return FFD_ERR_INVALID_ARGUMENT;
+  }
+  try {
+    std::string all;
+    for (auto& d : sorted_subdirs(dir)) {
+      all += d;
+      all.push_back('\0');
+    }
+    *size = (int64_t)all.size();
+    if (buf) {
+      if (cap < (int64_t)all.size()) {
+        g_convert_error = "buffer too small";
+        return FFD_ERR_INVALID_ARGUMENT;
+      }
+      std::memcpy(buf, all.data(), all.size());
+    }
+    return FFD_OK;
+  } catch (const std::exception& e) {
+    g_convert_error = e.what();
+    return FFD_ERR_MODEL;
+  }
+}
+
+}  // extern "C"
+
+#ifdef FFD_CONVERT_MAIN
+// usage: ffd_convert <reference_root> <out.bin>: the configs and tree directories the reference's mains use
+// (eval_ffd.cpp:137-143), relative to <reference_root>.
 int main(int argc, char** argv) {
   if (argc != 3) {
     std::fprintf(stderr, "usage: %s <reference_root> <out.bin>\n", argv[0]);
@@ -478,40 +599,13 @@ int main(int argc, char** argv) {
       throw std::runtime_error("cannot parse config_headpose.txt");
     if (!load_config(root + "/data/config_ffd.txt", mp))
       throw std::runtime_error("cannot parse config_ffd.txt");
-    ffd::ModelFile m;
-    ForestOut hpo;
-    char buf[512];
-    for (int i = 0; i < hp.ntrees; i++) {  // Forest::load (Forest.hpp:116-127)
-      std::snprintf(buf, sizeof buf, "%s/%s/tree_%03d.txt", root.c_str(), hp.tree_path.c_str(), i);
-      parse_tree(buf, HP, hpo);
-    }
-    put_params(m, "hp", hp, 1);
-    put_forest(m, "hp", HP, hpo);
-    std::vector<std::string> dirs = sorted_subdirs(root + "/" + mp.tree_path);
-    if (dirs.empty()) throw std::runtime_error("no FFD forest directories");
-    ForestOut mpo;
-    for (auto& d : dirs)
-      for (int i = 0; i < mp.ntrees; i++) {
-        std::snprintf(buf, sizeof buf, "%s/tree_%03d.txt", d.c_str(), i);
-        parse_tree(buf, MP, mpo);
-      }
-    put_params(m, "mp", mp, (int)dirs.size());
-    put_forest(m, "mp", MP, mpo);
-    Cascade cas;  // FaceDetectionOption::path_face_cascade as demo.cpp:186 / eval_ffd.cpp:143 set it
-    const bool have_cascade = parse_cascade(root + "/data/haarcascade_frontalface_alt.xml", cas);
-    if (have_cascade) put_cascade(m, cas);
-    std::string tmp = outp + ".tmp";
-    m.save(tmp);
-    if (std::rename(tmp.c_str(), outp.c_str()) != 0) throw std::runtime_error("rename failed");
-    std::printf("ffd_convert: hp %zu trees %zu nodes %zu leaves; mp %zu forests %zu trees %zu nodes %zu leaves -> %s\n",
-                hpo.tree_node_off.size() - 1, hpo.node_leaf.size(), hpo.leaf_n.size(), dirs.size(),
-                mpo.tree_node_off.size() - 1, mpo.node_leaf.size(), mpo.leaf_n.size(), outp.c_str());
-    if (have_cascade)
-      std::printf("ffd_convert: haar cascade %dx%d, %zu stages, %zu weak classifiers, %zu features\n", cas.win_w,
-                  cas.win_h, cas.stage_threshold.size(), cas.weak_feature.size(), cas.feature_weight.size() / 3);
+    const std::string msg = convert_model(hp, root + "/" + hp.tree_path, mp, sorted_subdirs(root + "/" + mp.tree_path),
+                                          root + "/data/haarcascade_frontalface_alt.xml", outp);
+    std::printf("ffd_convert: %s\n", msg.c_str());
   } catch (const std::exception& e) {
     std::fprintf(stderr, "ffd_convert: ERROR: %s\n", e.what());
     return 1;
   }
   return 0;
 }
+#endif

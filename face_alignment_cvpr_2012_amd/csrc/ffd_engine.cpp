@@ -1063,8 +1063,11 @@ namespace {
 // patch grid covers the region (face_utils.cpp:197-207,255-265: x from bbox.x while
 // x < bbox.x + bbox.width - patch) and votes keep sample coordinates (vox, voy).  The channel stage
 // is skipped (nochan); the caller launches the forest stages.
-FaceDesc stage_sample(ffd_engine* e, Workspace& w, const uint32_t* ch, int W, int H, const ffd_rect& r, int hp_step,
-                      int mp_step_x, int mp_step_y) {
+void stage_desc(ffd_engine* e, Workspace& w, const FaceDesc& f);
+
+// The descriptor of a sample region: patch grids over the region (face_utils.cpp:197-207,255-265: x from
+// bbox.x while x < bbox.x + bbox.width - patch), votes in sample coordinates (vox, voy), channels staged.
+FaceDesc region_desc(const ffd_engine* e, const ffd_rect& r, int hp_step, int mp_step_x, int mp_step_y) {
   FaceDesc f;
   std::memset(&f, 0, sizeof(f));
   const int rw = r.width, rh = r.height;
@@ -1083,6 +1086,13 @@ FaceDesc stage_sample(ffd_engine* e, Workspace& w, const uint32_t* ch, int W, in
   f.valid = 1; f.nochan = 1;
   f.plane = (int64_t)(rh + 1) * PITCH;
   f.hp_off = f.mp_off = f.vote_off = f.ch_off = 0;
+  return f;
+}
+
+FaceDesc stage_sample(ffd_engine* e, Workspace& w, const uint32_t* ch, int W, int H, const ffd_rect& r, int hp_step,
+                      int mp_step_x, int mp_step_y) {
+  FaceDesc f = region_desc(e, r, hp_step, mp_step_x, mp_step_y);
+  const int rw = r.width, rh = r.height;
   std::vector<uint16_t> J((size_t)NCH * f.plane, 0);
   const size_t ow = (size_t)W + 1, oplane = ((size_t)H + 1) * ow;
   uint32_t vmax = 0;
@@ -1099,6 +1109,12 @@ FaceDesc stage_sample(ffd_engine* e, Workspace& w, const uint32_t* ch, int W, in
   f.fint = vmax >= (1u << 24) ? 1 : 0;  // float-rounded integrals (CV_32F past 2^24): k_walk_fint
   w.chan.ensure(J.size() * 2 + 512);  // slack: traversal windows read past a row
   HIP_CHECK(hipMemcpyAsync(w.chan.p, J.data(), J.size() * 2, hipMemcpyHostToDevice, w.stream));
+  stage_desc(e, w, f);
+  return f;
+}
+
+// The one-face descriptor of a staged sample region and the forest stages' buffers on workspace 0.
+void stage_desc(ffd_engine* e, Workspace& w, const FaceDesc& f) {
   w.hpleaf.ensure(((size_t)e->hp_trees * f.nhx * f.nhy + 64) * 4);
   w.mpleaf.ensure(((size_t)MAX_TREES * f.nmx * f.nmy + 64) * 4);
   w.votes.ensure(((size_t)NPARTS * MAX_TREES * f.nmx * f.nmy + 64) * sizeof(Vote));
@@ -1107,11 +1123,10 @@ FaceDesc stage_sample(ffd_engine* e, Workspace& w, const uint32_t* ch, int W, in
   w.vote_counts.ensure(NPARTS * 4);
   std::vector<FaceDesc> one{f};
   upload(w.faces, one, w.stream);
-  HIP_CHECK(hipStreamSynchronize(w.stream));  // J is released on return
+  HIP_CHECK(hipStreamSynchronize(w.stream));  // the staging vectors are released on return
   w.count = 0;  // the workspace no longer holds a batch for ffd_get_trace
   w.pending = false;
   if (e->last_ws == 0) e->last_ws = -1;
-  return f;
 }
 
 // Leaf tables for per-call estimator options: desc's own tables when the options match, else the
@@ -1158,6 +1173,77 @@ bool region_ok(int W, int H, const ffd_rect* r) {
          (int64_t)r->y + r->height <= H && r->width <= PITCH - 3 && r->height <= MAX_FACE_H_TALL;
 }
 
+// getHeadPoseVotesMT + the pose reduction (FaceForest.cpp:60-72, face_utils.cpp:183-242) on the staged
+// one-face chunk f of workspace w whose planes are `chan`.
+HpState run_headpose(ffd_engine* e, Workspace& w, const FaceDesc& f, const uint16_t* chan, const ffd_headpose_option& o) {
+  const float* hp_m = hp_table(e, o);
+  const TravShape g = ffd_engine::fit_shape(e->trav_g_hp, true, o.step_size, o.step_size);
+  const FaceDesc* dfd = w.faces.as<FaceDesc>();
+  std::vector<FaceDesc> fv{f};
+  e->out.ensure(sizeof(FaceOut));
+  launch_traverse(true, dfd, 1, blocks_per_face(fv, true, g), g, e->hp_pairs.as<uint4>(), e->hp_tops.as<uint4>(),
+                  e->hp_topi.as<uint32_t>(), e->trav_top_max, e->hp_far.as<uint32_t>(), nullptr, e->hp_trees,
+                  o.step_size, o.step_size, f.plane, chan, w.hpleaf.as<int32_t>(), e->trav_wg, TRAV_LDS_CAP, w.stream);
+  if (f.fint)
+    launch_walk_fint(true, dfd, 1, e->hp_nodes.as<uint4>(), e->hp_roots.as<int32_t>(), e->hp_trees, nullptr, o.step_size,
+                     o.step_size, chan, w.hpleaf.as<int32_t>(), w.stream);
+  launch_hp_pose(dfd, 1, w.hpleaf.as<int32_t>(), hp_m, e->hp_trees, e->n_forests, e->ntrees_per_forest,
+                 w.state.as<HpState>(), e->out.as<FaceOut>(), w.stream);
+  HIP_CHECK(hipGetLastError());
+  HpState hs;
+  HIP_CHECK(hipMemcpyAsync(&hs, w.state.p, sizeof(hs), hipMemcpyDeviceToHost, w.stream));
+  HIP_CHECK(hipStreamSynchronize(w.stream));
+  return hs;
+}
+
+ffd_status check_mp_call(ffd_engine* e, const int32_t* tree_ids, int n_trees, const ffd_multipart_option& o) {
+  if (n_trees < 1 || n_trees > MAX_TREES || !tree_ids) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+  const int ntot = e->n_forests * e->ntrees_per_forest;
+  for (int t = 0; t < n_trees; t++)
+    if (tree_ids[t] < 0 || tree_ids[t] >= ntot) return fail(e, FFD_ERR_INVALID_ARGUMENT, "tree id out of range");
+  if (o.step_size <= 0 || o.step_size_y < 0) return fail(e, FFD_ERR_INVALID_ARGUMENT, "invalid MultiPartEstimatorOption");
+  return FFD_OK;
+}
+
+// getFacialFeaturesVotesMT + MeanShift (FaceForest.cpp:74-95, face_utils.cpp:244-302) on the staged one-face
+// chunk f of workspace w (planes `chan`) with the given trees; points in sample coordinates.
+void run_facial_features(ffd_engine* e, Workspace& w, const FaceDesc& f, const uint16_t* chan, const int32_t* tree_ids,
+                         int n_trees, const ffd_multipart_option& o, int32_t* points) {
+  const int step_y = o.step_size_y > 0 ? o.step_size_y : o.step_size;
+  bool compact = false;
+  int bias_x = 0, bias_y = 0;
+  const uint4* rec = mp_table(e, o, compact, bias_x, bias_y);
+  const TravShape g = ffd_engine::fit_shape(e->trav_g_mp, false, o.step_size, step_y);
+  const FaceDesc* dfd = w.faces.as<FaceDesc>();
+  std::vector<FaceDesc> fv{f};
+  HpState hs;
+  std::memset(&hs, 0, sizeof(hs));
+  hs.n_trees = n_trees;
+  for (int t = 0; t < n_trees; t++) hs.trees[t] = tree_ids[t];
+  HIP_CHECK(hipMemcpyAsync(w.state.p, &hs, sizeof(hs), hipMemcpyHostToDevice, w.stream));
+  e->out.ensure(sizeof(FaceOut));
+  const int n_parts = std::max(0, std::min(o.num_parts, NPARTS));
+  launch_traverse(false, dfd, 1, blocks_per_face(fv, false, g), g, e->mp_pairs.as<uint4>(), e->mp_tops.as<uint4>(),
+                  e->mp_topi.as<uint32_t>(), e->trav_top_max, e->mp_far.as<uint32_t>(), w.state.as<HpState>(), 0,
+                  o.step_size, step_y, f.plane, chan, w.mpleaf.as<int32_t>(), e->trav_wg, TRAV_LDS_CAP, w.stream);
+  if (f.fint)
+    launch_walk_fint(false, dfd, 1, e->mp_nodes.as<uint4>(), e->mp_roots.as<int32_t>(), 0, w.state.as<HpState>(),
+                     o.step_size, step_y, chan, w.mpleaf.as<int32_t>(), w.stream);
+  launch_votes(dfd, 1, w.mpleaf.as<int32_t>(), rec, compact, bias_x, bias_y, w.state.as<HpState>(), MAX_TREES,
+               o.step_size, step_y, e->patch / 2, n_parts, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), w.stream);
+  // FaceForest::estimateFacialFeatures shifts with a default MeanShiftOption (FaceForest.cpp:89-92)
+  launch_meanshift(dfd, 1, w.state.as<HpState>(), MAX_TREES, n_parts, 10.f, 7, 0.05f, w.votes.as<Vote>(),
+                   w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(), e->out.as<FaceOut>(), nullptr, w.stream);
+  HIP_CHECK(hipGetLastError());
+  FaceOut out;
+  HIP_CHECK(hipMemcpyAsync(&out, e->out.p, sizeof(out), hipMemcpyDeviceToHost, w.stream));
+  HIP_CHECK(hipStreamSynchronize(w.stream));
+  for (int i = 0; i < NPARTS; i++) {  // scale 1: cvRound of the MeanShift mode, sample coordinates
+    points[2 * i] = i < n_parts ? out.points[i][0] : 0;
+    points[2 * i + 1] = i < n_parts ? out.points[i][1] : 0;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1172,28 +1258,11 @@ ffd_status ffd_estimate_headpose(ffd_engine* e, const uint32_t* channels, int32_
     if (!region_ok(W, H, region)) return fail(e, FFD_ERR_INVALID_ARGUMENT, "face_bbox outside the image sample");
     const ffd_headpose_option o = options ? *options : e->desc.hp_option;
     if (o.step_size <= 0) return fail(e, FFD_ERR_INVALID_ARGUMENT, "invalid HeadPoseEstimatorOption");
-    const float* hp_m = hp_table(e, o);
-    const TravShape g = ffd_engine::fit_shape(e->trav_g_hp, true, o.step_size, o.step_size);
     e->sync_all();
     Workspace& w = *e->ws[0];
     const FaceDesc f = stage_sample(e, w, channels, W, H, *region, o.step_size, e->desc.mp_option.step_size,
                                     e->mp_step_y());
-    const FaceDesc* dfd = w.faces.as<FaceDesc>();
-    std::vector<FaceDesc> fv{f};
-    e->out.ensure(sizeof(FaceOut));
-    launch_traverse(true, dfd, 1, blocks_per_face(fv, true, g), g, e->hp_pairs.as<uint4>(), e->hp_tops.as<uint4>(),
-                    e->hp_topi.as<uint32_t>(), e->trav_top_max, e->hp_far.as<uint32_t>(), nullptr, e->hp_trees,
-                    o.step_size, o.step_size, f.plane, w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), e->trav_wg,
-                    TRAV_LDS_CAP, w.stream);
-    if (f.fint)
-      launch_walk_fint(true, dfd, 1, e->hp_nodes.as<uint4>(), e->hp_roots.as<int32_t>(), e->hp_trees, nullptr, o.step_size,
-                       o.step_size, w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), w.stream);
-    launch_hp_pose(dfd, 1, w.hpleaf.as<int32_t>(), hp_m, e->hp_trees, e->n_forests, e->ntrees_per_forest,
-                   w.state.as<HpState>(), e->out.as<FaceOut>(), w.stream);
-    HIP_CHECK(hipGetLastError());
-    HpState hs;
-    HIP_CHECK(hipMemcpyAsync(&hs, w.state.p, sizeof(hs), hipMemcpyDeviceToHost, w.stream));
-    HIP_CHECK(hipStreamSynchronize(w.stream));
+    const HpState hs = run_headpose(e, w, f, w.chan.as<uint16_t>(), o);
     if (headpose) *headpose = hs.headpose;
     if (variance) *variance = hs.variance;
     return FFD_OK;
@@ -1204,53 +1273,18 @@ ffd_status ffd_estimate_facial_features(ffd_engine* e, const uint32_t* channels,
                                         const ffd_rect* region, const int32_t* tree_ids, int32_t n_trees,
                                         const ffd_multipart_option* options, int32_t* points) {
   return guarded(e, [&]() -> ffd_status {
-    if (!channels || !points || W < 1 || H < 1 || n_trees < 1 || n_trees > MAX_TREES || !tree_ids)
-      return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (!channels || !points || W < 1 || H < 1) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     const ffd_rect full{0, 0, W, H};
     if (!region) region = &full;
     if (!region_ok(W, H, region)) return fail(e, FFD_ERR_INVALID_ARGUMENT, "face_bbox outside the image sample");
-    const int ntot = e->n_forests * e->ntrees_per_forest;
-    for (int t = 0; t < n_trees; t++)
-      if (tree_ids[t] < 0 || tree_ids[t] >= ntot) return fail(e, FFD_ERR_INVALID_ARGUMENT, "tree id out of range");
     const ffd_multipart_option o = options ? *options : e->desc.mp_option;
-    if (o.step_size <= 0 || o.step_size_y < 0) return fail(e, FFD_ERR_INVALID_ARGUMENT, "invalid MultiPartEstimatorOption");
+    const ffd_status st = check_mp_call(e, tree_ids, n_trees, o);
+    if (st != FFD_OK) return st;
     const int step_y = o.step_size_y > 0 ? o.step_size_y : o.step_size;
-    bool compact = false;
-    int bias_x = 0, bias_y = 0;
-    const uint4* rec = mp_table(e, o, compact, bias_x, bias_y);
-    const TravShape g = ffd_engine::fit_shape(e->trav_g_mp, false, o.step_size, step_y);
     e->sync_all();
     Workspace& w = *e->ws[0];
     const FaceDesc f = stage_sample(e, w, channels, W, H, *region, e->desc.hp_option.step_size, o.step_size, step_y);
-    const FaceDesc* dfd = w.faces.as<FaceDesc>();
-    std::vector<FaceDesc> fv{f};
-    HpState hs;
-    std::memset(&hs, 0, sizeof(hs));
-    hs.n_trees = n_trees;
-    for (int t = 0; t < n_trees; t++) hs.trees[t] = tree_ids[t];
-    HIP_CHECK(hipMemcpyAsync(w.state.p, &hs, sizeof(hs), hipMemcpyHostToDevice, w.stream));
-    e->out.ensure(sizeof(FaceOut));
-    const int n_parts = std::max(0, std::min(o.num_parts, NPARTS));
-    launch_traverse(false, dfd, 1, blocks_per_face(fv, false, g), g, e->mp_pairs.as<uint4>(), e->mp_tops.as<uint4>(),
-                    e->mp_topi.as<uint32_t>(), e->trav_top_max, e->mp_far.as<uint32_t>(), w.state.as<HpState>(), 0,
-                    o.step_size, step_y, f.plane, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), e->trav_wg,
-                    TRAV_LDS_CAP, w.stream);
-    if (f.fint)
-      launch_walk_fint(false, dfd, 1, e->mp_nodes.as<uint4>(), e->mp_roots.as<int32_t>(), 0, w.state.as<HpState>(),
-                       o.step_size, step_y, w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), w.stream);
-    launch_votes(dfd, 1, w.mpleaf.as<int32_t>(), rec, compact, bias_x, bias_y, w.state.as<HpState>(), MAX_TREES,
-                 o.step_size, step_y, e->patch / 2, n_parts, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), w.stream);
-    // FaceForest::estimateFacialFeatures shifts with a default MeanShiftOption (FaceForest.cpp:89-92)
-    launch_meanshift(dfd, 1, w.state.as<HpState>(), MAX_TREES, n_parts, 10.f, 7, 0.05f, w.votes.as<Vote>(),
-                     w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(), e->out.as<FaceOut>(), nullptr, w.stream);
-    HIP_CHECK(hipGetLastError());
-    FaceOut out;
-    HIP_CHECK(hipMemcpyAsync(&out, e->out.p, sizeof(out), hipMemcpyDeviceToHost, w.stream));
-    HIP_CHECK(hipStreamSynchronize(w.stream));
-    for (int i = 0; i < NPARTS; i++) {  // scale 1: cvRound of the MeanShift mode, sample coordinates
-      points[2 * i] = i < n_parts ? out.points[i][0] : 0;
-      points[2 * i + 1] = i < n_parts ? out.points[i][1] : 0;
-    }
+    run_facial_features(e, w, f, w.chan.as<uint16_t>(), tree_ids, n_trees, o, points);
     return FFD_OK;
   });
 }
@@ -1336,6 +1370,366 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* c
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipMemcpyAsync(leaf_ids, outb.p, (size_t)n_patches * n_trees * 4, hipMemcpyDeviceToHost, e->main_stream()));
     HIP_CHECK(hipStreamSynchronize(e->main_stream()));  // `narrow` outlives the upload
+    return FFD_OK;
+  });
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ image samples --
+// ImageSample kept on the device (ffd.h "Device-resident image samples").
+struct ffd_sample {
+  ffd_engine* e = nullptr;
+  int W = 0, H = 0;
+  int64_t plane = 0;  // (H + 1) * PITCH
+  DevBuf chan;        // u16 [NCH][H + 1][PITCH], integrals mod 2^16
+};
+
+namespace {
+
+// A sample's channel planes as a one-face chunk of workspace 0 (region = the whole sample).
+FaceDesc sample_desc(ffd_sample* s, int hp_step, int mp_step_x, int mp_step_y) {
+  const ffd_rect full{0, 0, s->W, s->H};
+  FaceDesc f = region_desc(s->e, full, hp_step, mp_step_x, mp_step_y);
+  f.plane = s->plane;
+  return f;
+}
+
+bool sample_size_ok(int W, int H) {
+  // (255 W H >= 2^24: the reference's CV_32F integrals round; the sample path walks exact integrals only)
+  return W >= 2 && H >= 2 && W <= PITCH - 3 && (int64_t)255 * W * H < ((int64_t)1 << 24);
+}
+
+ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, int32_t n_patches, int x0, int y0,
+                       int step, int nx, int ny, const int32_t* tree_ids, int32_t n_trees, int32_t* leaf_ids) {
+  ffd_engine* e = s->e;
+  const bool grid = patches_xy == nullptr;
+  if (kind != FFD_FOREST_HEADPOSE && kind != FFD_FOREST_FFD) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad forest kind");
+  if (n_trees < 0 || n_trees > MAX_TREES || (n_trees && !tree_ids) || n_patches < 0)
+    return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+  const int ntot = kind == FFD_FOREST_HEADPOSE ? e->hp_trees : e->n_forests * e->ntrees_per_forest;
+  for (int t = 0; t < n_trees; t++)
+    if (tree_ids[t] < 0 || tree_ids[t] >= ntot) return fail(e, FFD_ERR_INVALID_ARGUMENT, "tree id out of range");
+  const int P = e->patch;
+  if (grid) {
+    if (nx < 0 || ny < 0 || (nx && ny && (step <= 0 || x0 < 0 || y0 < 0 || x0 + (int64_t)(nx - 1) * step + P > s->W ||
+                                          y0 + (int64_t)(ny - 1) * step + P > s->H)))
+      return fail(e, FFD_ERR_INVALID_ARGUMENT, "patch grid outside the image sample");
+    n_patches = nx * ny;
+  } else {
+    for (int p = 0; p < n_patches; p++) {
+      const int x = patches_xy[2 * p], y = patches_xy[2 * p + 1];
+      if (x < 0 || y < 0 || x + P > s->W || y + P > s->H)
+        return fail(e, FFD_ERR_INVALID_ARGUMENT, "patch outside the image sample");
+    }
+  }
+  if (n_patches == 0 || n_trees == 0) return FFD_OK;
+  if (!leaf_ids) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+  const bool hp = kind == FFD_FOREST_HEADPOSE;
+  // A grid from the origin with the estimators' rule (face_utils.cpp:197-207,255-265) runs as the batch path's
+  // traversal of a one-face chunk (k_traverse: LDS windows, tree tops, pair records), which writes the leaves in
+  // exactly the grid order; the grid asked for is a leading sub-grid of it.
+  bool all_hp_trees = hp && n_trees == e->hp_trees;
+  for (int t = 0; all_hp_trees && t < n_trees; t++) all_hp_trees = tree_ids[t] == t;
+  if (grid && x0 == 0 && y0 == 0 && (!hp || all_hp_trees) && step <= 32 && n_trees <= MAX_TREES) {
+    const FaceDesc f = sample_desc(s, hp ? step : e->desc.hp_option.step_size, hp ? e->desc.mp_option.step_size : step,
+                                   hp ? e->mp_step_y() : step);
+    const int gx = hp ? f.nhx : f.nmx, gy = hp ? f.nhy : f.nmy;
+    if (nx <= gx && ny <= gy) {
+      e->sync_all();
+      Workspace& w = *e->ws[0];
+      stage_desc(e, w, f);
+      const TravShape g = ffd_engine::fit_shape(hp ? e->trav_g_hp : e->trav_g_mp, hp, step, step);
+      std::vector<FaceDesc> fv{f};
+      int32_t* leaf_dev = hp ? w.hpleaf.as<int32_t>() : w.mpleaf.as<int32_t>();
+      if (!hp) {
+        HpState hs;
+        std::memset(&hs, 0, sizeof(hs));
+        hs.n_trees = n_trees;
+        for (int t = 0; t < n_trees; t++) hs.trees[t] = tree_ids[t];
+        HIP_CHECK(hipMemcpyAsync(w.state.p, &hs, sizeof(hs), hipMemcpyHostToDevice, w.stream));
+      }
+      launch_traverse(hp, w.faces.as<FaceDesc>(), 1, blocks_per_face(fv, hp, g), g,
+                      hp ? e->hp_pairs.as<uint4>() : e->mp_pairs.as<uint4>(), hp ? e->hp_tops.as<uint4>() : e->mp_tops.as<uint4>(),
+                      hp ? e->hp_topi.as<uint32_t>() : e->mp_topi.as<uint32_t>(), e->trav_top_max,
+                      hp ? e->hp_far.as<uint32_t>() : e->mp_far.as<uint32_t>(), hp ? nullptr : w.state.as<HpState>(),
+                      hp ? e->hp_trees : 0, step, step, f.plane, s->chan.as<uint16_t>(), leaf_dev, e->trav_wg,
+                      TRAV_LDS_CAP, w.stream);
+      HIP_CHECK(hipGetLastError());
+      const size_t all = (size_t)gx * gy * n_trees * 4;
+      int32_t* pin = static_cast<int32_t*>(e->pin_leaf.ensure(all));
+      HIP_CHECK(hipMemcpyAsync(pin, leaf_dev, all, hipMemcpyDeviceToHost, w.stream));
+      HIP_CHECK(hipStreamSynchronize(w.stream));
+      for (int i = 0; i < nx; i++)  // rows of the sub-grid: patch (i, j) of the full grid is i * gy + j
+        std::memcpy(leaf_ids + (size_t)i * ny * n_trees, pin + (size_t)i * gy * n_trees, (size_t)ny * n_trees * 4);
+      return FFD_OK;
+    }
+  }
+  const hipStream_t st = e->main_stream();
+  SampleEvalArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.nodes = hp ? e->hp_nodes.as<uint4>() : e->mp_nodes.as<uint4>();
+  a.roots = hp ? e->hp_roots.as<int32_t>() : e->mp_roots.as<int32_t>();
+  a.chan = s->chan.as<uint16_t>();
+  a.plane = s->plane;
+  a.n_patches = n_patches;
+  a.n_trees = n_trees;
+  for (int t = 0; t < n_trees; t++) a.trees[t] = tree_ids[t];
+  if (grid) {
+    a.grid_ny = ny;
+    a.x0 = x0;
+    a.y0 = y0;
+    a.step = step;
+  } else if (n_patches <= SAMPLE_INLINE) {
+    for (int i = 0; i < 2 * n_patches; i++) a.inl[i] = patches_xy[i];
+  } else {
+    const size_t b = (size_t)n_patches * 8;
+    std::memcpy(e->pin_patch.ensure(b), patches_xy, b);
+    e->sample_patches.ensure(b);
+    HIP_CHECK(hipMemcpyAsync(e->sample_patches.p, e->pin_patch.p, b, hipMemcpyHostToDevice, st));
+    a.patches = e->sample_patches.as<int32_t>();
+  }
+  const size_t ob = (size_t)n_patches * n_trees * 4;
+  a.leaf_out = static_cast<int32_t*>(e->pin_leaf.ensure(ob));  // host-mapped: the kernel writes the results here
+  launch_sample_eval(a, st);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipStreamSynchronize(st));
+  std::memcpy(leaf_ids, e->pin_leaf.p, ob);
+  return FFD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+ffd_status ffd_sample_create(ffd_engine* e, const uint8_t* gray, int32_t W, int32_t H, int32_t stride, ffd_sample** out) {
+  return guarded(e, [&]() -> ffd_status {
+    if (!gray || !out || stride < W) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    *out = nullptr;
+    if (!sample_size_ok(W, H)) return fail(e, FFD_ERR_UNSUPPORTED, "image sample size unsupported (2..125 wide, 255 W H < 2^24)");
+    std::unique_ptr<ffd_sample> s(new ffd_sample);
+    s->e = e;
+    s->W = W;
+    s->H = H;
+    s->plane = (int64_t)(H + 1) * PITCH;
+    s->chan.ensure((size_t)NCH * s->plane * 2 + 512);  // slack: traversal windows read past a row
+    // the face itself is the "image" (copy mode) as in ffd_extract_channels; the channel kernels write
+    // straight into the sample's planes
+    e->sync_all();
+    Workspace& w = *e->ws[0];
+    std::vector<uint8_t> bgr((size_t)W * H * 3);
+    for (int y = 0; y < H; y++)
+      for (int x = 0; x < W; x++) {
+        const uint8_t v = gray[(size_t)y * stride + x];  // BGR2GRAY of (v, v, v) is v
+        uint8_t* p = &bgr[((size_t)y * W + x) * 3];
+        p[0] = p[1] = p[2] = v;
+      }
+    e->scratch_a.ensure(bgr.size());
+    HIP_CHECK(hipMemcpyAsync(e->scratch_a.p, bgr.data(), bgr.size(), hipMemcpyHostToDevice, w.stream));
+    FaceDesc f;
+    std::memset(&f, 0, sizeof(f));
+    f.img_w = W; f.img_h = H; f.img_stride = 3 * W; f.bw = W; f.bh = H; f.W = W; f.H = H;
+    f.scale = 1.f; f.mode = 0; f.valid = 1;
+    f.plane = s->plane;
+    w.gray.ensure((size_t)H * PITCH + 256);
+    w.mag.ensure((size_t)NGABOR * H * PITCH * 4 + 256);
+    w.gabor_redo.ensure(5 * 4);
+    if (w.gabor_mm.n < 5 * 64) {
+      w.gabor_mm.ensure(5 * 64);
+      HIP_CHECK(hipMemsetAsync(w.gabor_mm.p, 0, w.gabor_mm.n, w.stream));
+    }
+    std::vector<FaceDesc> one{f};
+    upload(w.faces, one, w.stream);
+    const FaceDesc* dfd = w.faces.as<FaceDesc>();
+    launch_gray_resize(dfd, 1, e->scratch_a.as<uint8_t>(), w.gray.as<uint8_t>(), w.stream);
+    for (int nu = 4; nu >= 0; nu--)
+      launch_gabor(nu, dfd, 1, H, w.gray.as<uint8_t>(), e->gabor_coef.as<float>(), w.mag.as<float>(),
+                   s->chan.as<uint16_t>(), w.gabor_redo.as<int>(), e->gabor_exact, w.gabor_mm.as<uint32_t>(), w.stream);
+    launch_integral(dfd, 1, H, w.gray.as<uint8_t>(), s->chan.as<uint16_t>(), w.stream);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(w.stream));  // bgr is released on return
+    w.count = 0;
+    w.pending = false;
+    if (e->last_ws == 0) e->last_ws = -1;
+    *out = s.release();
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_sample_create_from_channels(ffd_engine* e, const uint32_t* channels, int32_t W, int32_t H,
+                                           ffd_sample** out) {
+  return guarded(e, [&]() -> ffd_status {
+    if (!channels || !out) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    *out = nullptr;
+    if (!sample_size_ok(W, H)) return fail(e, FFD_ERR_UNSUPPORTED, "image sample size unsupported (2..125 wide, 255 W H < 2^24)");
+    std::unique_ptr<ffd_sample> s(new ffd_sample);
+    s->e = e;
+    s->W = W;
+    s->H = H;
+    s->plane = (int64_t)(H + 1) * PITCH;
+    std::vector<uint16_t> J((size_t)NCH * s->plane, 0);
+    for (int c = 0; c < NCH; c++)
+      for (int y = 0; y <= H; y++)
+        for (int x = 0; x <= W; x++)
+          J[(size_t)c * s->plane + (size_t)y * PITCH + x] = (uint16_t)channels[((size_t)c * (H + 1) + y) * (W + 1) + x];
+    s->chan.ensure(J.size() * 2 + 512);
+    HIP_CHECK(hipMemcpyAsync(s->chan.p, J.data(), J.size() * 2, hipMemcpyHostToDevice, e->main_stream()));
+    HIP_CHECK(hipStreamSynchronize(e->main_stream()));
+    *out = s.release();
+    return FFD_OK;
+  });
+}
+
+void ffd_sample_destroy(ffd_sample* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->e->device);
+  (void)hipStreamSynchronize(s->e->main_stream());
+  delete s;
+}
+
+ffd_status ffd_sample_size(const ffd_sample* s, int32_t* W, int32_t* H) {
+  if (!s) return FFD_ERR_INVALID_ARGUMENT;
+  if (W) *W = s->W;
+  if (H) *H = s->H;
+  return FFD_OK;
+}
+
+ffd_status ffd_sample_channels(const ffd_sample* s, uint32_t* out) {
+  if (!s) return FFD_ERR_INVALID_ARGUMENT;
+  return guarded(s->e, [&]() -> ffd_status {
+    if (!out) return fail(s->e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    std::vector<uint16_t> v((size_t)NCH * s->plane);
+    HIP_CHECK(hipMemcpyAsync(v.data(), s->chan.p, v.size() * 2, hipMemcpyDeviceToHost, s->e->main_stream()));
+    HIP_CHECK(hipStreamSynchronize(s->e->main_stream()));
+    widen_integrals(v.data(), s->plane, s->W, s->H, out);
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_sample_eval_leaves(ffd_sample* s, int32_t kind, const int32_t* patches_xy, int32_t n_patches,
+                                  const int32_t* tree_ids, int32_t n_trees, int32_t* leaf_ids) {
+  if (!s) return FFD_ERR_INVALID_ARGUMENT;
+  return guarded(s->e, [&]() -> ffd_status {
+    if (!patches_xy && n_patches) return fail(s->e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    static const int32_t none[2] = {0, 0};
+    return sample_eval(s, kind, patches_xy ? patches_xy : none, n_patches, 0, 0, 0, 0, 0, tree_ids, n_trees, leaf_ids);
+  });
+}
+
+ffd_status ffd_sample_eval_grid(ffd_sample* s, int32_t kind, int32_t x0, int32_t y0, int32_t step, int32_t nx,
+                                int32_t ny, const int32_t* tree_ids, int32_t n_trees, int32_t* leaf_ids) {
+  if (!s) return FFD_ERR_INVALID_ARGUMENT;
+  return guarded(s->e, [&]() -> ffd_status {
+    return sample_eval(s, kind, nullptr, 0, x0, y0, step, nx, ny, tree_ids, n_trees, leaf_ids);
+  });
+}
+
+ffd_status ffd_sample_estimate_headpose(ffd_sample* s, const ffd_rect* region, const ffd_headpose_option* options,
+                                        float* headpose, float* variance) {
+  if (!s) return FFD_ERR_INVALID_ARGUMENT;
+  ffd_engine* e = s->e;
+  return guarded(e, [&]() -> ffd_status {
+    const ffd_rect full{0, 0, s->W, s->H};
+    if (!region) region = &full;
+    if (!region_ok(s->W, s->H, region)) return fail(e, FFD_ERR_INVALID_ARGUMENT, "face_bbox outside the image sample");
+    const ffd_headpose_option o = options ? *options : e->desc.hp_option;
+    if (o.step_size <= 0) return fail(e, FFD_ERR_INVALID_ARGUMENT, "invalid HeadPoseEstimatorOption");
+    e->sync_all();
+    Workspace& w = *e->ws[0];
+    HpState hs;
+    if (region->x == 0 && region->y == 0 && region->width == s->W && region->height == s->H) {
+      const FaceDesc f = sample_desc(s, o.step_size, e->desc.mp_option.step_size, e->mp_step_y());
+      stage_desc(e, w, f);
+      hs = run_headpose(e, w, f, s->chan.as<uint16_t>(), o);
+    } else {  // a sub-region: its integrals relative to the region origin (stage_sample)
+      std::vector<uint32_t> ch((size_t)NCH * (s->H + 1) * (s->W + 1));
+      const ffd_status st = ffd_sample_channels(s, ch.data());
+      if (st != FFD_OK) return st;
+      const FaceDesc f = stage_sample(e, w, ch.data(), s->W, s->H, *region, o.step_size, e->desc.mp_option.step_size,
+                                      e->mp_step_y());
+      hs = run_headpose(e, w, f, w.chan.as<uint16_t>(), o);
+    }
+    if (headpose) *headpose = hs.headpose;
+    if (variance) *variance = hs.variance;
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_sample_estimate_facial_features(ffd_sample* s, const ffd_rect* region, const int32_t* tree_ids,
+                                               int32_t n_trees, const ffd_multipart_option* options, int32_t* points) {
+  if (!s) return FFD_ERR_INVALID_ARGUMENT;
+  ffd_engine* e = s->e;
+  return guarded(e, [&]() -> ffd_status {
+    if (!points) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    const ffd_rect full{0, 0, s->W, s->H};
+    if (!region) region = &full;
+    if (!region_ok(s->W, s->H, region)) return fail(e, FFD_ERR_INVALID_ARGUMENT, "face_bbox outside the image sample");
+    const ffd_multipart_option o = options ? *options : e->desc.mp_option;
+    const ffd_status cst = check_mp_call(e, tree_ids, n_trees, o);
+    if (cst != FFD_OK) return cst;
+    const int step_y = o.step_size_y > 0 ? o.step_size_y : o.step_size;
+    e->sync_all();
+    Workspace& w = *e->ws[0];
+    if (region->x == 0 && region->y == 0 && region->width == s->W && region->height == s->H) {
+      const FaceDesc f = sample_desc(s, e->desc.hp_option.step_size, o.step_size, step_y);
+      stage_desc(e, w, f);
+      run_facial_features(e, w, f, s->chan.as<uint16_t>(), tree_ids, n_trees, o, points);
+    } else {
+      std::vector<uint32_t> ch((size_t)NCH * (s->H + 1) * (s->W + 1));
+      const ffd_status st = ffd_sample_channels(s, ch.data());
+      if (st != FFD_OK) return st;
+      const FaceDesc f = stage_sample(e, w, ch.data(), s->W, s->H, *region, e->desc.hp_option.step_size, o.step_size,
+                                      step_y);
+      run_facial_features(e, w, f, w.chan.as<uint16_t>(), tree_ids, n_trees, o, points);
+    }
+    return FFD_OK;
+  });
+}
+
+// MeanShift::shift (MeanShift.hpp:41-76) of one vote list: the list as landmark 0 of a one-face chunk
+// (tslots 1, nmx = the list length) through the engine's MeanShift kernel.
+ffd_status ffd_meanshift(ffd_engine* e, const ffd_vote* votes, int32_t n, const ffd_meanshift_option* option,
+                         float* mean_xy) {
+  return guarded(e, [&]() -> ffd_status {
+    if ((n && !votes) || n < 0 || !mean_xy) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    const ffd_meanshift_option o = option ? *option : e->desc.ms_option;
+    if (o.max_iterations < 0 || o.kernel_size <= 0) return fail(e, FFD_ERR_INVALID_ARGUMENT, "invalid MeanShiftOption");
+    std::vector<Vote> v;
+    v.reserve(n);
+    for (int i = 0; i < n; i++) {
+      if (!votes[i].check) continue;  // getMean / getWeightedMean skip unchecked votes
+      if (votes[i].x < -32768 || votes[i].x > 32767 || votes[i].y < -32768 || votes[i].y > 32767)
+        return fail(e, FFD_ERR_UNSUPPORTED, "vote position outside the 16-bit range");
+      v.push_back(Vote{(int16_t)votes[i].x, (int16_t)votes[i].y, votes[i].weight});
+    }
+    e->sync_all();
+    Workspace& w = *e->ws[0];
+    FaceDesc f;
+    std::memset(&f, 0, sizeof(f));
+    f.valid = 1; f.nochan = 1; f.scale = 1.f;
+    f.nmx = std::max<int>(1, (int)v.size());
+    f.nmy = 1;
+    int32_t counts[NPARTS] = {(int32_t)v.size()};
+    w.votes.ensure(std::max<size_t>(1, v.size()) * sizeof(Vote));
+    if (!v.empty()) HIP_CHECK(hipMemcpyAsync(w.votes.p, v.data(), v.size() * sizeof(Vote), hipMemcpyHostToDevice, w.stream));
+    w.vote_counts.ensure(sizeof(counts));
+    HIP_CHECK(hipMemcpyAsync(w.vote_counts.p, counts, sizeof(counts), hipMemcpyHostToDevice, w.stream));
+    w.ms_mean.ensure(NPARTS * 2 * 4);
+    e->out.ensure(sizeof(FaceOut));
+    std::vector<FaceDesc> one{f};
+    upload(w.faces, one, w.stream);
+    launch_meanshift(w.faces.as<FaceDesc>(), 1, nullptr, 1, 1, (float)o.kernel_size, o.max_iterations,
+                     o.stopping_criteria, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(),
+                     e->out.as<FaceOut>(), nullptr, w.stream);
+    HIP_CHECK(hipGetLastError());
+    float m[2];
+    HIP_CHECK(hipMemcpyAsync(m, w.ms_mean.p, sizeof(m), hipMemcpyDeviceToHost, w.stream));
+    HIP_CHECK(hipStreamSynchronize(w.stream));
+    w.count = 0;
+    w.pending = false;
+    if (e->last_ws == 0) e->last_ws = -1;
+    mean_xy[0] = m[0];
+    mean_xy[1] = m[1];
     return FFD_OK;
   });
 }

@@ -172,6 +172,23 @@ struct ffd_engine {
 
   std::vector<std::unique_ptr<Workspace>> ws;
   DevBuf images, out, scratch_a, scratch_b, scratch_c;  // host-API staging (ws[0] stream)
+  // image samples (ffd_sample_*): pinned host buffers the evaluation kernel writes its leaf ordinals to,
+  // and the staging of long patch lists
+  struct Pinned {
+    void* p = nullptr;
+    size_t n = 0;
+    void* ensure(size_t bytes) {
+      if (bytes <= n) return p;
+      if (p) (void)hipHostFree(p);
+      p = nullptr;
+      n = 0;
+      HIP_CHECK(hipHostMalloc(&p, std::max<size_t>(bytes, 4096), hipHostMallocDefault));
+      n = std::max<size_t>(bytes, 4096);
+      return p;
+    }
+    ~Pinned() { if (p) (void)hipHostFree(p); }
+  } pin_leaf, pin_patch;
+  DevBuf sample_patches;
   int last_ws = -1;
 
   hipStream_t main_stream() const { return ws[0]->stream; }

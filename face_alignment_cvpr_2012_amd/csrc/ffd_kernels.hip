@@ -1111,6 +1111,11 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
 
 #if FFD_TRAV_STATS
   uint32_t st_top = 0, st_deep = 0, st_max = 0, st_walks = 0, st_maxdeep = 0, st_ttest = 0, st_tfetch = 0;
+  uint32_t st_ph[4] = {0, 0, 0, 0};  // FFD_TRAV_STATS == 3: setup, top levels, deep levels, store (cycles)
+  uint64_t st_t0 = 0;
+#define TRAV_STAMP(v) \
+  uint64_t v;         \
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory")
 #endif
   auto walk_block = [&](const Blk& B) {
     const FaceDesc& fd = A.faces[B.f];
@@ -1123,6 +1128,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       const int t = item / GG, pl = item - t * GG;
       const int xi = B.xi0 + pl % GX, yi = B.yi0 + pl / GX;
       if (xi >= B.nx || yi >= B.ny) continue;
+#if FFD_TRAV_STATS == 3
+      TRAV_STAMP(ph_a);
+      st_ph[0] += (uint32_t)(ph_a - st_t0);
+#endif
       // byte address of the patch's top-left integral corner in channel 0's window plane
       const unsigned char* base = reinterpret_cast<const unsigned char*>(win) +
                                   2 * ((yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh);
@@ -1169,6 +1178,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         hi = s ? R.w : R.z;
       }
       uint32_t P = top_i[t * topn + h];
+#if FFD_TRAV_STATS == 3
+      TRAV_STAMP(ph_b);
+      st_ph[1] += (uint32_t)(ph_b - ph_a);
+#endif
 #if FFD_TRAV_PROBE == 6
       int probe_depth = 0;
 #endif
@@ -1203,6 +1216,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         lo = s ? R.y : R.x;
         hi = s ? R.w : R.z;
       }
+#if FFD_TRAV_STATS == 3
+      TRAV_STAMP(ph_c);
+      st_ph[2] += (uint32_t)(ph_c - ph_b);
+#endif
 #if FFD_TRAV_STATS
       st_top += wt;
       st_deep += wd;
@@ -1211,6 +1228,11 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       st_walks++;
 #endif
       out[(xi * B.ny + yi) * B.T + t] = (int32_t)((lo & 0xFFFFFu) | hi << 20);  // reference order
+#if FFD_TRAV_STATS == 3
+      __builtin_amdgcn_s_waitcnt(0);
+      TRAV_STAMP(ph_d);
+      st_ph[3] += (uint32_t)(ph_d - ph_c);
+#endif
     }
   };
 
@@ -1373,6 +1395,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
 #if FFD_TRAV_STATS
       const uint64_t t0 = __builtin_amdgcn_s_memtime();
       st_top = st_deep = st_max = st_walks = st_maxdeep = 0;
+      st_t0 = t0;
 #endif
 #if FFD_TRAV_PROBE != 1
       const Blk cur = block(lb);
@@ -1383,6 +1406,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       const uint32_t a0 = wave_max(st_ttest), a1 = wave_max(st_tfetch), a2 = wave_max(st_max), a3 = wave_sum(st_walks),
                      a4 = wave_max(st_maxdeep);
       st_ttest = st_tfetch = 0;
+#elif FFD_TRAV_STATS == 3  // per wave: the phases (setup, top levels, deep levels, store) in fields 2, 3, 4, 6
+      const uint32_t a0 = wave_max(st_ph[0]), a1 = wave_max(st_ph[1]), a2 = wave_max(st_ph[2]), a3 = wave_sum(st_walks),
+                     a4 = wave_max(st_ph[3]);
+      st_ph[0] = st_ph[1] = st_ph[2] = st_ph[3] = 0;
 #else
       const uint32_t a0 = wave_sum(st_top), a1 = wave_sum(st_deep), a2 = wave_max(st_max), a3 = wave_sum(st_walks),
                      a4 = wave_max(st_maxdeep);
@@ -1411,6 +1438,38 @@ __global__ void k_eval_patches(const uint4* __restrict__ nodes, const int32_t* _
   const int p = i / n_trees, t = i % n_trees;
   const uint16_t* I = chan + patches[2 * p + 1] * PITCH + patches[2 * p];
   leaf_ids[i] = (int32_t)walk16(nodes, (uint32_t)roots[tree_ids[t]], I, plane);
+}
+
+// Forest<S>::evaluateMT on patches of a device-resident ImageSample (ffd_sample_eval_leaves): one lane
+// per (patch, tree) walk (Tree<S>::evaluateMT, Tree.hpp:173-191) over the 16-B nodes and the sample's u16
+// planes.  Patches are either a list (inline in the argument block up to SAMPLE_INLINE, else `patches`) or
+// a grid (x0 + xi step, y0 + yi step; patch p = xi * grid_ny + yi, the reference's x-major order).  The
+// leaf ordinals go straight to leaf_out, which may be host-mapped pinned memory: a one-patch call is one
+// launch and one stream synchronisation, no copies.
+__global__ __launch_bounds__(256) void k_sample_eval(SampleEvalArgs A) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.n_patches * A.n_trees) return;
+  const int p = i / A.n_trees, t = i - p * A.n_trees;
+  int x, y;
+  if (A.grid_ny > 0) {
+    const int xi = p / A.grid_ny, yi = p - xi * A.grid_ny;
+    x = A.x0 + xi * A.step;
+    y = A.y0 + yi * A.step;
+  } else if (A.n_patches <= SAMPLE_INLINE) {
+    x = A.inl[2 * p];
+    y = A.inl[2 * p + 1];
+  } else {
+    x = A.patches[2 * p];
+    y = A.patches[2 * p + 1];
+  }
+  const uint16_t* I = A.chan + (int64_t)y * PITCH + x;
+  A.leaf_out[i] = (int32_t)walk16(A.nodes, (uint32_t)A.roots[A.trees[t]], I, A.plane);
+}
+
+void launch_sample_eval(const SampleEvalArgs& a, hipStream_t s) {
+  const int total = a.n_patches * a.n_trees;
+  if (total <= 0) return;
+  k_sample_eval<<<(total + 255) / 256, 256, 0, s>>>(a);
 }
 
 // The traversals of float-integral faces (FaceDesc::fint: the reference's CV_32F integral may round,

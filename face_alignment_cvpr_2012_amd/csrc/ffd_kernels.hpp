@@ -55,6 +55,21 @@ void launch_walk_fint(bool hp, const FaceDesc* faces, int n, const uint4* nodes,
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
                          const int32_t* patches, int n_patches, const uint16_t* chan, int64_t plane,
                          int32_t* leaf_ids, hipStream_t s);
+// Forest<S>::evaluateMT on a device-resident image sample (k_sample_eval): a patch list or a patch grid
+constexpr int SAMPLE_INLINE = 16;  // patches passed in the argument block
+struct SampleEvalArgs {
+  const uint4* nodes;      // 16-B nodes (breadth-first) of the forest kind
+  const int32_t* roots;    // root node per tree id
+  const uint16_t* chan;    // the sample's planes: [38][H + 1][PITCH] integrals mod 2^16
+  int64_t plane;           // plane stride (elements)
+  int32_t* leaf_out;       // [patch][tree] leaf ordinals (device or host-mapped memory)
+  const int32_t* patches;  // (x, y) pairs when n_patches > SAMPLE_INLINE and not a grid
+  int n_patches, n_trees;
+  int grid_ny, x0, y0, step;  // grid mode when grid_ny > 0 (n_patches = grid_nx * grid_ny)
+  int32_t trees[MAX_TREES];
+  int32_t inl[2 * SAMPLE_INLINE];
+};
+void launch_sample_eval(const SampleEvalArgs& a, hipStream_t s);
 void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const float* hp_m, int hp_trees,
                     int n_forests, int ntrees_per_forest, HpState* state, FaceOut* out, hipStream_t s);
 // leaf_rec per FFD leaf: compact (32 B) = {vote mask, fg, 10 x u16 (x - bias_x) | (y - bias_y) << 8, pad},

@@ -2,41 +2,66 @@
 // (/root/reference/include/FaceForest.hpp:21-157) over the C ABI in ffd.h.
 //
 // Same type and method names as the reference:
-//   HeadPoseEstimatorOption, MultiPartEstimatorOption, FaceDetectionOption, FaceForestOptions,
-//   Face { headpose, bbox, ffd_cordinates }, FaceForest(FaceForestOptions),
-//   FaceForest::analyzeFace(img, bbox, Face&)      (FaceForest.cpp:183-258)
-//   FaceForest::analyzeImage(img, faces)           (FaceForest.cpp:161-181: the GPU Haar detector, then
+//   ForestParam                                     (Constants.hpp:24-60), loadConfigFile, loadAnnotations,
+//                                                   FaceAnnotation, intersect, enlargeFace (face_utils.cpp:18-181,
+//                                                   325-346), Vote (face_utils.hpp:34-42)
+//   HeadPoseEstimatorOption, MultiPartEstimatorOption, FaceDetectionOption, FaceForestOptions (with
+//   hp_forest_param / mp_forest_param / mp_forest_paths), Face { headpose, bbox, ffd_cordinates },
+//   FaceForest(FaceForestOptions)                   (FaceForest.cpp:15-58: the tree directories of the options are
+//                                                   converted once by ffd_model_convert and cached; or a converted
+//                                                   model via the extension field model_path / $FFD_MODEL)
+//   FaceForest::analyzeFace(img, bbox, Face&)       (FaceForest.cpp:183-258)
+//   FaceForest::analyzeImage(img, faces)            (FaceForest.cpp:161-181: the GPU Haar detector, then
 //                                                   analyzeFace on every box, one GPU batch)
-//   FaceForest::detectFace(img, boxes)             (FaceForest.cpp:136-159, the model's cascade)
-//   FaceForest::analyzeImage(img, boxes, faces)    (the same with the caller's own boxes)
-//   FaceForest::estimateHeadPose / estimateFacialFeatures (static, FaceForest.hpp:97-115,
-//                                                   FaceForest.cpp:60-95) over an ImageSample
-//   ImageSample(img, features, useIntegral)         (ImageSample.cpp:11-20, channels on the GPU)
-//   Forest<HeadPoseSample|MPSample>::evaluateMT     (Forest.hpp:80-90; S::Leaf** with the reference's
-//                                                   HeadPoseLeaf / MPLeaf members, or model leaf ordinals)
-// With OpenCV available, Mat / Rect / Point are cv::Mat / cv::Rect / cv::Point; otherwise the
-// minimal PODs below.  FaceForestOptions carries the converted model path instead of the
-// reference's per-forest tree directories (convert once with ffd_convert).
+//   FaceForest::detectFace(img, cascade, fd_option, boxes) (static, FaceForest.cpp:136-159)
+//   FaceForest::estimateHeadPose / estimateFacialFeatures (static, FaceForest.hpp:97-115, FaceForest.cpp:60-95)
+//   ImageSample(img, features, use_integral)        (ImageSample.cpp:11-20: the channels computed on the GPU and
+//                                                   kept there, ffd_sample_create)
+//   Forest<HeadPoseSample|MPSample>                 (Forest.hpp: load, evaluateMT(const S*, S::Leaf**),
+//                                                   numberOfTrees, getTree / addTree / cleanForest / setParam)
+//   MeanShift::shift                                (MeanShift.hpp:41-76, on the GPU)
+// With OpenCV available, Mat / Rect / Point / CascadeClassifier are OpenCV's; otherwise the minimal PODs below.
+// Define FFD_GLOBAL_NAMES (or include the forwarding headers Constants.hpp / face_utils.hpp / MeanShift.hpp of
+// this directory) for the reference's global names.
 //
-// Errors: like the reference constructor (FaceForest.cpp:23-56) a failed construction leaves
-// the object uninitialised (is_initialized() == false, message in last_error()); analyzeFace
-// on a bad box throws std::invalid_argument where the reference's CV_Assert throws.
+// Forest<S>::evaluateMT, the reference's per-patch call (face_utils.cpp:210-216, 267-274: one thread-pool task
+// per patch, the Forest bound BY VALUE), evaluates on the GPU: the first call for an image sample walks every
+// tree for the whole patch grid that contains the requested patch (step 3 for MPSample, 4 for HeadPoseSample,
+// the estimators' defaults; Forest::setGridStep changes it) in one launch over the device-resident sample
+// (ffd_sample_eval_grid), and the later calls of that sample — from any copy of the Forest, from any thread —
+// read their leaves from that result.  A patch off the grid is one launch of its own (ffd_sample_eval_leaves).
+// The leaves are exactly the ones Tree<S>::evaluateMT reaches; only when they are computed differs.
+//
+// Errors: like the reference constructor (FaceForest.cpp:23-56) a failed construction leaves the object
+// uninitialised (is_initialized() == false, message in last_error()); analyzeFace on a bad box throws
+// std::invalid_argument where the reference's CV_Assert throws.
 //
 // Link: -lffd (face_alignment_cvpr_2012_amd/lib/libffd.so) -lamdhip64.
 #pragma once
 
+#include <sys/stat.h>
+
 #include <algorithm>
+#include <atomic>
+#include <cmath>
 #include <cstdint>
-#include <map>
+#include <cstdio>
+#include <cstdlib>
+#include <deque>
+#include <fstream>
 #include <memory>
+#include <mutex>
+#include <sstream>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "ffd.h"
 
 #if defined(FFD_WITH_OPENCV) || (defined(__has_include) && __has_include(<opencv2/core/core.hpp>) && !defined(FFD_NO_OPENCV))
 #include <opencv2/core/core.hpp>
+#include <opencv2/objdetect/objdetect.hpp>
 #define FFD_HAVE_OPENCV 1
 #endif
 
@@ -46,6 +71,7 @@ namespace ffd {
 using Mat = cv::Mat;
 using Rect = cv::Rect;
 using Point = cv::Point;
+using CascadeClassifier = cv::CascadeClassifier;
 inline const uint8_t* mat_data(const Mat& m) { return m.data; }
 inline int mat_step(const Mat& m) { return (int)m.step; }
 #else
@@ -58,33 +84,153 @@ struct Point {
   int x = 0, y = 0;
   Point() = default;
   Point(int x_, int y_) : x(x_), y(y_) {}
+  Point& operator+=(const Point& o) { x += o.x; y += o.y; return *this; }
 };
-struct Mat {  // BGR 8UC3 view (cv::Mat data / rows / cols / step)
+struct Mat {  // 8-bit image view (cv::Mat data / rows / cols / step / channels): BGR 8UC3 or gray 8UC1
   const uint8_t* data = nullptr;
   int rows = 0, cols = 0;
   size_t step = 0;
+  int cn = 3;
   Mat() = default;
-  Mat(int rows_, int cols_, const uint8_t* data_, size_t step_ = 0)
-      : data(data_), rows(rows_), cols(cols_), step(step_ ? step_ : (size_t)cols_ * 3) {}
+  Mat(int rows_, int cols_, const uint8_t* data_, size_t step_ = 0, int channels_ = 3)
+      : data(data_), rows(rows_), cols(cols_), step(step_ ? step_ : (size_t)cols_ * channels_), cn(channels_) {}
+  int channels() const { return cn; }
+  bool empty() const { return !data || rows <= 0 || cols <= 0; }
+};
+// cv::CascadeClassifier stand-in: remembers the XML path (the detector itself is the converted cascade of the
+// engine, ffd_detect_faces)
+struct CascadeClassifier {
+  std::string path;
+  bool load(const std::string& p) {
+    struct stat st;
+    if (stat(p.c_str(), &st) != 0) return false;
+    path = p;
+    return true;
+  }
+  bool empty() const { return path.empty(); }
 };
 inline const uint8_t* mat_data(const Mat& m) { return m.data; }
 inline int mat_step(const Mat& m) { return (int)m.step; }
 #endif
 
-struct FaceDetectionOption {  // include/FaceForest.hpp:21-32 (the cascade comes from the converted model)
+// ---------------------------------------------------------------- parameters --
+struct ForestParam {  // include/Constants.hpp:24-60
+  int max_depth = 0;          // tree stopping criteria
+  int min_patches = 0;        // tree stopping criteria
+  int ntests = 0;             // number of tests to find the optimal split
+  int ntrees = 0;             // number of trees per forest
+  int nimages = 0;            // number of images per class
+  int npatches = 0;           // number of patches per image
+  int face_size = 0;          // face size in pixels
+  float patch_size_ratio = 0; // patch size ratio
+  std::string tree_path;      // path to load or save the trees
+  std::string image_path;     // path to load images
+  std::vector<int> features;  // feature channels
+  int getPatchSize() { return static_cast<int>(std::round(face_size * patch_size_ratio)); }
+};
+
+// loadConfigFile (face_utils.cpp:50-140): (caption line, value line) pairs in a fixed order; the reference's
+// defaults when the file cannot be opened (and false).
+inline bool loadConfigFile(std::string path, ForestParam& param) {
+  std::ifstream f(path);
+  if (f.is_open()) {
+    std::string line;
+    auto value = [&]() {
+      std::getline(f, line);
+      std::getline(f, line);
+      return line;
+    };
+    param.image_path = value();
+    param.tree_path = value();
+    param.ntrees = std::stoi(value());
+    param.ntests = std::stoi(value());
+    param.max_depth = std::stoi(value());
+    param.min_patches = std::stoi(value());
+    param.nimages = std::stoi(value());
+    param.npatches = std::stoi(value());
+    param.face_size = std::stoi(value());
+    param.patch_size_ratio = std::stof(value());
+    std::istringstream ss(value());
+    std::string tok;
+    while (std::getline(ss, tok, ' ')) param.features.push_back((int)std::stof(tok));
+    return true;
+  }
+  param.max_depth = 15;
+  param.min_patches = 20;
+  param.ntests = 250;
+  param.ntrees = 10;
+  param.nimages = 500;
+  param.npatches = 200;
+  param.face_size = 100;
+  param.patch_size_ratio = 0.25f;
+  return false;
+}
+
+struct FaceAnnotation {  // include/face_utils.hpp:23-29
+  std::vector<Point> parts;
+  std::string url;
+  Rect bbox;
+  int pose = 0;
+};
+
+// loadAnnotations (face_utils.cpp:143-181): "url x y w h pose n x0 y0 ..." per line, '#' lines skipped.
+inline bool loadAnnotations(std::string path, std::vector<FaceAnnotation>& annotations) {
+  std::ifstream f(path);
+  if (!f.is_open()) return false;
+  std::string line;
+  while (std::getline(f, line)) {
+    std::vector<std::string> s;
+    std::string tok;
+    std::istringstream ss(line);
+    while (std::getline(ss, tok, ' ')) s.push_back(tok);
+    if (!line.empty() && line.back() == ' ') s.push_back("");
+    if (s.empty() || s[0] == "#") continue;
+    FaceAnnotation a;
+    a.url = s.at(0);
+    a.bbox = Rect(std::stoi(s.at(1)), std::stoi(s.at(2)), std::stoi(s.at(3)), std::stoi(s.at(4)));
+    a.pose = std::stoi(s.at(5));
+    const int n = std::stoi(s.at(6));
+    for (int i = 0; i < n; i++) a.parts.push_back(Point(std::stoi(s.at(7 + 2 * i)), std::stoi(s.at(8 + 2 * i))));
+    annotations.push_back(a);
+  }
+  return true;
+}
+
+// intersect (face_utils.cpp:325-346)
+inline Rect intersect(const Rect r1, const Rect r2) {
+  Rect i;
+  i.x = (r1.x < r2.x) ? r2.x : r1.x;
+  i.y = (r1.y < r2.y) ? r2.y : r1.y;
+  i.width = ((r1.x + r1.width < r2.x + r2.width) ? r1.x + r1.width : r2.x + r2.width) - i.x;
+  i.height = ((r1.y + r1.height < r2.y + r2.height) ? r1.y + r1.height : r2.y + r2.height) - i.y;
+  if (i.width <= 0 || i.height <= 0) i = Rect(0, 0, 0, 0);
+  return i;
+}
+
+// enlargeFace (face_utils.cpp:30-48)
+inline void enlargeFace(Mat img, Rect& enlarge_bbox, FaceAnnotation& annotation) {
+  const Point offset((int)(annotation.bbox.width * 0.1), (int)(annotation.bbox.height * 0.1));
+  const Rect aux(annotation.bbox.x - offset.x, annotation.bbox.y - offset.y, annotation.bbox.width + offset.x * 2,
+                 annotation.bbox.height + offset.y * 2);
+  enlarge_bbox = intersect(aux, Rect(0, 0, img.cols, img.rows));
+  annotation.bbox = Rect(0, 0, enlarge_bbox.width, enlarge_bbox.height);
+  for (auto& p : annotation.parts) p += offset;
+}
+
+struct FaceDetectionOption {  // include/FaceForest.hpp:21-32
   int min_feature_size = 30;
   int min_neighbors = 1;
   float search_scale_factor = 1.3f;
-  std::string path_face_cascade;  // unused: ffd_convert puts data/haarcascade_frontalface_alt.xml in the model
+  std::string path_face_cascade;
 };
 
-struct HeadPoseEstimatorOption {
+struct HeadPoseEstimatorOption {  // include/FaceForest.hpp:34-43
   int num_head_pose_labels = 5;
   int step_size = 4;
   float min_foreground_probability = 0.5f;
 };
 
-struct MultiPartEstimatorOption {
+struct MultiPartEstimatorOption {  // include/FaceForest.hpp:45-58
   int num_parts = 10;
   int step_size = 3;
   int min_samples = 2;
@@ -99,19 +245,29 @@ struct MeanShiftOption {  // include/MeanShift.hpp:16-25
   float stopping_criteria = 0.05f;
 };
 
-struct FaceForestOptions {
-  std::string model_path;  // FFDMODEL file (replaces hp_forest_param / mp_forest_paths)
-  int device = 0;          // HIP device ordinal
+struct FaceForestOptions {  // include/FaceForest.hpp:60-68
+  ForestParam hp_forest_param;
+  ForestParam mp_forest_param;
   FaceDetectionOption fd_option;
   HeadPoseEstimatorOption hp_option;
   MultiPartEstimatorOption mp_option;
+  std::vector<std::string> mp_forest_paths;
+  // extensions (not in the reference)
+  std::string model_path;  // a converted FFDMODEL file instead of the tree directories ($FFD_MODEL)
+  int device = 0;          // HIP device ordinal
   MeanShiftOption ms_option;
 };
 
-struct Face {
+struct Face {  // include/FaceForest.hpp:70-75
   float headpose = 0.f;
   Rect bbox;
   std::vector<Point> ffd_cordinates;  // 10 bbox-relative landmarks (reference spelling)
+};
+
+struct Vote {  // include/face_utils.hpp:34-42
+  Point pos;
+  float weight = 0.f;
+  bool check = false;
 };
 
 namespace detail {
@@ -119,38 +275,125 @@ inline ffd_engine*& current_engine() {  // the most recently constructed FaceFor
   static ffd_engine* e = nullptr;
   return e;
 }
+// tree directories -> (forest kind, first global tree id) of the engine built from them (Forest<S>::load)
+struct ForestDirs {
+  ffd_engine* engine = nullptr;
+  std::string hp_dir;
+  std::vector<std::string> mp_dirs;
+  int mp_ntrees = 20;
+};
+inline ForestDirs& forest_dirs() {
+  static ForestDirs d;
+  return d;
+}
+inline uint64_t next_sample_id() {
+  static std::atomic<uint64_t> n{0};
+  return ++n;
+}
+inline std::string model_cache_path(const std::string& key) {
+  uint64_t h = 1469598103934665603ull;  // FNV-1a of the inputs (paths, sizes, modification times)
+  for (unsigned char c : key) h = (h ^ c) * 1099511628211ull;
+  const char* dir = std::getenv("FFD_MODEL_CACHE");
+  std::string d = dir ? dir : "";
+  if (d.empty()) {
+    const char* xdg = std::getenv("XDG_CACHE_HOME");
+    const char* home = std::getenv("HOME");
+    d = xdg ? std::string(xdg) + "/ffd" : home ? std::string(home) + "/.cache/ffd" : "/tmp";
+  }
+  std::string p;
+  for (size_t i = 1; i <= d.size(); i++)  // mkdir -p
+    if (i == d.size() || d[i] == '/') (void)mkdir(d.substr(0, i).c_str(), 0755);
+  char name[64];
+  std::snprintf(name, sizeof name, "/ffd_model_%016llx.bin", (unsigned long long)h);
+  return d + name;
+}
+inline std::string file_key(const std::string& p) {
+  struct stat st;
+  if (stat(p.c_str(), &st) != 0) return p + "|missing";
+  return p + "|" + std::to_string((long long)st.st_size) + "|" + std::to_string((long long)st.st_mtime);
+}
+inline ffd_forest_param to_c(const ForestParam& p) {
+  ffd_forest_param c;
+  c.max_depth = p.max_depth; c.min_patches = p.min_patches; c.ntests = p.ntests; c.ntrees = p.ntrees;
+  c.nimages = p.nimages; c.npatches = p.npatches; c.face_size = p.face_size;
+  c.patch_size_ratio = p.patch_size_ratio;
+  c.tree_path = p.tree_path.c_str();
+  c.image_path = p.image_path.c_str();
+  c.features = reinterpret_cast<const int32_t*>(p.features.data());
+  c.n_features = (int32_t)p.features.size();
+  return c;
+}
+inline std::vector<std::string> subdirs(const std::string& dir) {
+  int64_t n = 0;
+  std::vector<std::string> out;
+  if (ffd_forest_subdirs(dir.c_str(), nullptr, 0, &n) != FFD_OK) return out;
+  std::string buf((size_t)n, '\0');
+  if (ffd_forest_subdirs(dir.c_str(), &buf[0], n, &n) != FFD_OK) return out;
+  for (size_t b = 0; b < buf.size();) {
+    const size_t e = buf.find('\0', b);
+    out.push_back(buf.substr(b, e - b));
+    b = e + 1;
+  }
+  return out;
+}
+inline float cv_round_f(float v) { return std::nearbyint(v); }  // cvRound: round half to even
 }  // namespace detail
 
-// ImageSample (include/ImageSample.hpp, src/ImageSample.cpp:11-20,77-90): the 38 integral feature
-// channels of a scaled gray face, extracted by the engine's HIP kernels (ffd_extract_channels).
-// img: 8-bit single-channel face (data, rows, cols, step in bytes); features must be {0, 1, 2} and
-// useIntegral true (the only configuration the pretrained forests use, data/config_ffd.txt).
+// ------------------------------------------------------------------ ImageSample --
+// ImageSample (include/ImageSample.hpp:146-190, src/ImageSample.cpp:11-20,77-90): the 38 integral feature
+// channels of a scaled gray face, extracted by the engine's HIP kernels and kept in HBM (ffd_sample_create).
+// features must be {0, 1, 2} (the configuration of the pretrained forests, data/config_ffd.txt); use_integral
+// selects how the reference evaluates a test (integral image or pixel sums), which gives the same value, so
+// both are accepted.
 class ImageSample {
  public:
+  ImageSample(const Mat img, std::vector<int> features, bool use_integral = false, ffd_engine* engine = nullptr)
+      : ImageSample(mat_data(img), img.cols, img.rows, (size_t)mat_step(img), features, use_integral, engine) {
+    if (img.channels() != 1) throw std::invalid_argument("ImageSample: the image must be 8-bit single-channel (gray)");
+  }
   ImageSample(const uint8_t* gray, int cols, int rows, size_t step, const std::vector<int>& features = {0, 1, 2},
               bool useIntegral = true, ffd_engine* engine = nullptr)
-      : engine_(engine ? engine : detail::current_engine()), w_(cols), h_(rows) {
+      : st_(std::make_shared<State>()) {
+    (void)useIntegral;
+    st_->engine = engine ? engine : detail::current_engine();
     std::vector<int> f(features);
     std::sort(f.begin(), f.end());
-    if (f != std::vector<int>({0, 1, 2}) || !useIntegral)
-      throw std::invalid_argument("ImageSample: only features {0,1,2} with integral channels are supported");
-    if (!engine_) throw std::runtime_error("ImageSample: no FaceForest engine");
-    std::vector<uint8_t> packed((size_t)cols * rows);
-    for (int y = 0; y < rows; y++)
-      for (int x = 0; x < cols; x++) packed[(size_t)y * cols + x] = gray[(size_t)y * step + x];
-    ch_.resize((size_t)38 * (rows + 1) * (cols + 1));
-    const ffd_status st = ffd_extract_channels(engine_, packed.data(), cols, rows, ch_.data());
-    if (st != FFD_OK) throw std::runtime_error(std::string("ImageSample: ") + ffd_last_error(engine_));
+    if (f != std::vector<int>({0, 1, 2}))
+      throw std::invalid_argument("ImageSample: only features {0,1,2} are supported (the pretrained forests' channels)");
+    if (!st_->engine) throw std::runtime_error("ImageSample: no FaceForest engine");
+    const ffd_status s = ffd_sample_create(st_->engine, gray, cols, rows, (int32_t)step, &st_->h);
+    if (s != FFD_OK) throw std::runtime_error(std::string("ImageSample: ") + ffd_last_error(st_->engine));
+    st_->w = cols;
+    st_->hgt = rows;
+    st_->id = detail::next_sample_id();
   }
-  int width() const { return w_; }
-  int height() const { return h_; }
-  const uint32_t* channels() const { return ch_.data(); }  // [38][rows+1][cols+1]
-  ffd_engine* engine() const { return engine_; }
+  int width() const { return st_->w; }
+  int height() const { return st_->hgt; }
+  ffd_engine* engine() const { return st_->engine; }
+  ffd_sample* handle() const { return st_->h; }
+  uint64_t id() const { return st_->id; }
+  // the channels as 38 u32 integral planes [38][rows+1][cols+1] (downloaded on first use)
+  const uint32_t* channels() const {
+    std::lock_guard<std::mutex> g(st_->mu);
+    if (st_->ch.empty()) {
+      st_->ch.resize((size_t)38 * (st_->hgt + 1) * (st_->w + 1));
+      if (ffd_sample_channels(st_->h, st_->ch.data()) != FFD_OK)
+        throw std::runtime_error(std::string("ImageSample: ") + ffd_last_error(st_->engine));
+    }
+    return st_->ch.data();
+  }
 
  private:
-  ffd_engine* engine_;
-  int w_, h_;
-  std::vector<uint32_t> ch_;
+  struct State {
+    ffd_engine* engine = nullptr;
+    ffd_sample* h = nullptr;
+    int w = 0, hgt = 0;
+    uint64_t id = 0;
+    std::mutex mu;
+    std::vector<uint32_t> ch;
+    ~State() { ffd_sample_destroy(h); }
+  };
+  std::shared_ptr<State> st_;  // copies share the device sample (the reference copies cv::Mat headers)
 };
 
 // Leaf payloads (HeadPoseSample.hpp:144-162, MPSample.hpp:137-159), same member names, so the
@@ -172,6 +415,7 @@ struct MPLeaf {
 // 31 x 31 patch of an ImageSample.
 struct HeadPoseSample {
   typedef HeadPoseLeaf Leaf;
+  static constexpr int default_step = 4;  // HeadPoseEstimatorOption::step_size
   const ImageSample* image;
   Rect roi;
   HeadPoseSample(const ImageSample* i, Rect r) : image(i), roi(r) {}
@@ -179,6 +423,7 @@ struct HeadPoseSample {
 };
 struct MPSample {
   typedef MPLeaf Leaf;
+  static constexpr int default_step = 3;  // MultiPartEstimatorOption::step_size
   const ImageSample* image;
   Rect roi;
   MPSample(const ImageSample* i, Rect r) : image(i), roi(r) {}
@@ -207,56 +452,230 @@ template <> struct ForestKind<MPSample> {
   }
 };
 
-// Forest<S> (include/Forest.hpp): a list of the engine's trees; evaluateMT walks every tree for
-// one patch on the GPU (Forest.hpp:80-90).  Two forms: leaf ordinals (the converted model's order),
-// or the reference's `S::Leaf**` (Forest.hpp:80: leafs[t] = the leaf tree t reached), whose payloads
-// (ffd_forest_leaves) the Forest owns and keeps for its lifetime, so the pointers stay valid as the
-// reference's tree-owned leaves do.
+// Tree<S> (include/Tree.hpp): a tree of the engine's model, by global id (head pose 0..14, FFD forest*20 + t).
+template <class S> struct Tree {
+  int32_t id = -1;
+  ffd_engine* engine = nullptr;
+};
+
+// Forest<S> (include/Forest.hpp): a list of the engine's trees (value semantics, as the reference's vector of
+// Tree*).  Copies share the leaf payloads and the per-sample evaluation cache (the reference binds the Forest
+// BY VALUE into every pool task, face_utils.cpp:215,273), so the Leaf* of evaluateMT stay valid while any copy
+// lives and every task's copy reads the one grid evaluation.
 template <class S> class Forest {
  public:
   typedef typename S::Leaf Leaf;
-  Forest(ffd_engine* e, std::vector<int32_t> trees) : engine_(e), trees_(std::move(trees)) {}
-  int numberOfTrees() const { return (int)trees_.size(); }
-  const std::vector<int32_t>& treeIds() const { return trees_; }
+  Forest() : cache_(std::make_shared<Cache>()) {}
+  Forest(ffd_engine* e, std::vector<int32_t> trees) : engine_(e), cache_(std::make_shared<Cache>()) {
+    for (int32_t t : trees) addTree(t);
+  }
+  int numberOfTrees() const { return (int)ids_.size(); }
+  const std::vector<int32_t>& treeIds() const { return ids_; }
   ffd_engine* engine() const { return engine_; }
-  void evaluateMT(const S* sample, int32_t* leafs) const {
-    const ImageSample& im = *sample->image;
-    const int32_t xy[2] = {sample->roi.x, sample->roi.y};
-    const ffd_status st = ffd_forest_eval_leaves(engine_, ForestKind<S>::value, im.channels(), im.width(),
-                                                 im.height(), xy, 1, trees_.data(), (int32_t)trees_.size(), leafs);
-    if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(engine_));
+  void setParam(ForestParam fp) { param_ = fp; }
+  ForestParam getParam() const { return param_; }
+  // Forest::addTree / getTree / cleanForest (Forest.hpp:41-68), as FaceForest::analyzeFace composes the
+  // per-face forest from the jungle (FaceForest.cpp:239-250)
+  void addTree(Tree<S>* tree) {
+    if (!engine_) engine_ = tree->engine;
+    addTree(tree->id);
   }
-  // Forest<S>::evaluateMT(const S* sample, typename S::Leaf** leafs) const (Forest.hpp:80-90)
+  void addTree(int32_t id) {
+    ids_.push_back(id);
+    trees_.push_back(Tree<S>{id, engine_});
+  }
+  Tree<S>* getTree(int idx) { return &trees_.at(idx); }
+  void cleanForest() {
+    ids_.clear();
+    trees_.clear();
+  }
+  // the patch grid step of the speculative evaluation (0: S::default_step)
+  void setGridStep(int step) { grid_step_ = step; }
+
+  // Forest<S>::load(path, ForestParam, max_trees) (Forest.hpp:103-129): the forest of the current engine that
+  // was converted from the tree directory `path` (FaceForest(FaceForestOptions) records them), its first trees
+  // as the reference's loop admits them.  false (with an ERROR line on stderr, as Forest::load_tree) when no
+  // engine holds that directory.
+  bool load(std::string path, ForestParam fp, int max_trees = -1) {
+    setParam(fp);
+    if (max_trees == -1) max_trees = fp.ntrees;
+    const detail::ForestDirs& d = detail::forest_dirs();
+    auto same = [](const std::string& a, const std::string& b) {
+      char ra[4096], rb[4096];
+      return a == b || (realpath(a.c_str(), ra) && realpath(b.c_str(), rb) && std::string(ra) == std::string(rb));
+    };
+    int base = -1;
+    if (ForestKind<S>::value == FFD_FOREST_HEADPOSE && !d.hp_dir.empty() && same(path, d.hp_dir)) base = 0;
+    if (ForestKind<S>::value == FFD_FOREST_FFD)
+      for (size_t i = 0; i < d.mp_dirs.size(); i++)
+        if (same(path, d.mp_dirs[i])) base = (int)i * d.mp_ntrees;
+    if (base < 0 || !d.engine) {
+      std::fprintf(stderr, "ERROR: Forest::load: no engine holds the trees of %s\n", path.c_str());
+      return false;
+    }
+    engine_ = d.engine;
+    for (int i = 0; i < fp.ntrees; i++) {
+      if (numberOfTrees() > max_trees) continue;
+      addTree(base + i);
+    }
+    return true;
+  }
+
+  // Forest<S>::evaluateMT(const S*, S::Leaf**) (Forest.hpp:80-90): leafs[t] = the leaf tree t reaches.
   void evaluateMT(const S* sample, Leaf** leafs) const {
-    std::vector<int32_t> ids(trees_.size());
-    evaluateMT(sample, ids.data());
-    for (size_t t = 0; t < ids.size(); t++) leafs[t] = &leaf(ids[t]);
+    const size_t T = ids_.size();
+    std::lock_guard<std::mutex> g(cache_->mu);
+    const size_t row = grid_row(sample);
+    if (row != npos) {
+      Leaf* const* lp = &cache_->grid_leaf[row];
+      for (size_t t = 0; t < T; t++) leafs[t] = lp[t];
+      return;
+    }
+    std::vector<int32_t> ids(T);
+    eval_one(sample, ids.data());
+    for (size_t t = 0; t < T; t++) leafs[t] = leaf_locked(ids[t]);
   }
-  // the payload of a leaf ordinal (cached; the reference: TreeNode::getLeaf, TreeNode.hpp:61-66)
+  // the same with the model's leaf ordinals (ffd_forest_leaves gives their payloads)
+  void evaluateMT(const S* sample, int32_t* leafs) const {
+    const size_t T = ids_.size();
+    std::lock_guard<std::mutex> g(cache_->mu);
+    const size_t row = grid_row(sample);
+    if (row != npos) {
+      std::copy(&cache_->grid_ids[row], &cache_->grid_ids[row] + T, leafs);
+      return;
+    }
+    eval_one(sample, leafs);
+  }
+  // the payload of a leaf ordinal (the reference: TreeNode::getLeaf, TreeNode.hpp:61-66)
   Leaf& leaf(int32_t ordinal) const {
-    auto it = leaves_.find(ordinal);
-    if (it != leaves_.end()) return *it->second;
-    typename ForestKind<S>::Raw raw;
-    const ffd_status st = ffd_forest_leaves(engine_, ForestKind<S>::value, &ordinal, 1, &raw);
-    if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(engine_));
-    std::unique_ptr<Leaf> l(new Leaf());
-    ForestKind<S>::fill(raw, *l);
-    return *(leaves_[ordinal] = std::move(l));
+    std::lock_guard<std::mutex> g(cache_->mu);
+    return *leaf_locked(ordinal);
   }
 
  private:
-  ffd_engine* engine_;
-  std::vector<int32_t> trees_;
-  mutable std::map<int32_t, std::unique_ptr<Leaf>> leaves_;
+  static constexpr size_t npos = ~(size_t)0;
+  struct Cache {
+    std::mutex mu;
+    std::unordered_map<int32_t, std::unique_ptr<Leaf>> leaves;
+    // the speculative grid evaluation of the last (sample, tree list): patches (x0 + i step, y0 + j step)
+    uint64_t sample = 0;
+    std::vector<int32_t> ids;
+    int x0 = 0, y0 = 0, step = 0, nx = 0, ny = 0;
+    std::vector<int32_t> grid_ids;  // [(i * ny + j) * T + t]
+    std::vector<Leaf*> grid_leaf;   // the payloads of grid_ids
+  };
+  ffd_engine* engine_ = nullptr;
+  ForestParam param_;
+  std::vector<int32_t> ids_;
+  std::deque<Tree<S>> trees_;
+  int grid_step_ = 0;
+  std::shared_ptr<Cache> cache_;
+
+  void check(ffd_status st) const {
+    if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(engine_));
+  }
+  Leaf* leaf_locked(int32_t ordinal) const {
+    auto it = cache_->leaves.find(ordinal);
+    if (it != cache_->leaves.end()) return it->second.get();
+    typename ForestKind<S>::Raw raw;
+    check(ffd_forest_leaves(engine_, ForestKind<S>::value, &ordinal, 1, &raw));
+    std::unique_ptr<Leaf> l(new Leaf());
+    ForestKind<S>::fill(raw, *l);
+    return (cache_->leaves[ordinal] = std::move(l)).get();
+  }
+  void eval_one(const S* sample, int32_t* ids) const {
+    const int32_t xy[2] = {sample->roi.x, sample->roi.y};
+    check(ffd_sample_eval_leaves(sample->image->handle(), ForestKind<S>::value, xy, 1, ids_.data(),
+                                 (int32_t)ids_.size(), ids));
+  }
+  // The offset of the sample patch's leaf row in the grid evaluation, evaluating the grid that contains the patch
+  // first when the cache holds another sample or tree list; npos for a patch off the grid.
+  size_t grid_row(const S* sample) const {
+    Cache& c = *cache_;
+    const ImageSample& im = *sample->image;
+    const int x = sample->roi.x, y = sample->roi.y, P = 31, T = (int)ids_.size();
+    if (c.sample != im.id() || c.ids != ids_) {
+      const int step = grid_step_ > 0 ? grid_step_ : S::default_step;
+      if (x < 0 || y < 0 || x + P > im.width() || y + P > im.height() || T == 0) return npos;
+      c.sample = 0;
+      c.ids = ids_;
+      c.x0 = x % step;
+      c.y0 = y % step;
+      c.step = step;
+      c.nx = (im.width() - P - c.x0) / step + 1;
+      c.ny = (im.height() - P - c.y0) / step + 1;
+      c.grid_ids.resize((size_t)c.nx * c.ny * T);
+      check(ffd_sample_eval_grid(im.handle(), ForestKind<S>::value, c.x0, c.y0, step, c.nx, c.ny, ids_.data(), T,
+                                 c.grid_ids.data()));
+      // the payloads of every leaf reached, fetched once
+      std::vector<int32_t> uniq;
+      for (int32_t v : c.grid_ids)
+        if (!c.leaves.count(v)) uniq.push_back(v);
+      std::sort(uniq.begin(), uniq.end());
+      uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+      if (!uniq.empty()) {
+        std::vector<typename ForestKind<S>::Raw> raw(uniq.size());
+        check(ffd_forest_leaves(engine_, ForestKind<S>::value, uniq.data(), (int32_t)uniq.size(), raw.data()));
+        for (size_t i = 0; i < uniq.size(); i++) {
+          std::unique_ptr<Leaf> l(new Leaf());
+          ForestKind<S>::fill(raw[i], *l);
+          c.leaves[uniq[i]] = std::move(l);
+        }
+      }
+      c.grid_leaf.resize(c.grid_ids.size());
+      for (size_t i = 0; i < c.grid_ids.size(); i++) c.grid_leaf[i] = c.leaves[c.grid_ids[i]].get();
+      c.sample = im.id();
+    }
+    const int dx = x - c.x0, dy = y - c.y0;
+    if (dx < 0 || dy < 0 || dx % c.step || dy % c.step) return npos;
+    const int i = dx / c.step, j = dy / c.step;
+    if (i >= c.nx || j >= c.ny) return npos;
+    return ((size_t)i * c.ny + j) * T;
+  }
 };
 
+// ------------------------------------------------------------------ MeanShift --
+// MeanShift::shift (include/MeanShift.hpp:41-76) on the GPU (ffd_meanshift) with the current engine.
+class MeanShift {
+ public:
+  static void shift(const std::vector<Vote>& votes, Point& result, MeanShiftOption& option) {
+    shift(votes, result, option.max_iterations, option.kernel_size, option.stopping_criteria);
+  }
+  static void shift(const std::vector<Vote>& votes, Point& result, int num_iterations, int kernel,
+                    float stopping_criteria) {
+    float m[2];
+    mode(votes, m, num_iterations, kernel, stopping_criteria);
+    result = Point((int)detail::cv_round_f(m[0]), (int)detail::cv_round_f(m[1]));  // Point_<float> -> Point_<int>
+  }
+  // the mode before rounding
+  static void mode(const std::vector<Vote>& votes, float* mean_xy, int num_iterations = 7, int kernel = 10,
+                   float stopping_criteria = 0.05f) {
+    ffd_engine* e = detail::current_engine();
+    if (!e) throw std::runtime_error("MeanShift: no FaceForest engine");
+    std::vector<ffd_vote> v(votes.size());
+    for (size_t i = 0; i < votes.size(); i++)
+      v[i] = ffd_vote{votes[i].pos.x, votes[i].pos.y, votes[i].weight, votes[i].check ? 1 : 0};
+    const ffd_meanshift_option o{kernel, num_iterations, stopping_criteria};
+    if (ffd_meanshift(e, v.data(), (int32_t)v.size(), &o, mean_xy) != FFD_OK)
+      throw std::runtime_error(std::string("MeanShift: ") + ffd_last_error(e));
+  }
+};
+
+// ------------------------------------------------------------------ FaceForest --
 class FaceForest {
  public:
   FaceForest() = default;
-  explicit FaceForest(const FaceForestOptions& option) {
+  explicit FaceForest(const FaceForestOptions& option) : options_(option) {
+    std::string model = option.model_path;
+    if (model.empty() && std::getenv("FFD_MODEL")) model = std::getenv("FFD_MODEL");
+    if (model.empty() && !option.hp_forest_param.tree_path.empty() && !convert(model)) return;
+    if (model.empty()) {
+      err_ = "FaceForestOptions: neither model_path / $FFD_MODEL nor hp_forest_param.tree_path is set";
+      return;
+    }
     ffd_engine_desc d;
     ffd_engine_desc_init(&d);
-    d.model_path = option.model_path.c_str();
+    d.model_path = model.c_str();
     d.device = option.device;
     d.hp_option = {option.hp_option.num_head_pose_labels, option.hp_option.step_size,
                    option.hp_option.min_foreground_probability};
@@ -267,8 +686,16 @@ class FaceForest {
     if (ffd_engine_create(&d, &engine_) != FFD_OK) {
       err_ = ffd_last_error(nullptr);
       engine_ = nullptr;
+      std::fprintf(stderr, "ERROR: (!) Error loading the forests: %s\n", err_.c_str());
     }
-    if (engine_) detail::current_engine() = engine_;
+    if (engine_) {
+      detail::current_engine() = engine_;
+      detail::ForestDirs& fd = detail::forest_dirs();
+      fd.engine = engine_;
+      fd.hp_dir = options_.hp_forest_param.tree_path;
+      fd.mp_dirs = options_.mp_forest_paths;
+      if (options_.mp_forest_param.ntrees > 0) fd.mp_ntrees = options_.mp_forest_param.ntrees;
+    }
     fd_option_ = option.fd_option;
   }
   FaceForest(const FaceForest&) = delete;
@@ -278,11 +705,13 @@ class FaceForest {
   }
   virtual ~FaceForest() {
     if (engine_ && detail::current_engine() == engine_) detail::current_engine() = nullptr;
+    if (engine_ && detail::forest_dirs().engine == engine_) detail::forest_dirs() = detail::ForestDirs();
     ffd_engine_destroy(engine_);
   }
 
   bool is_initialized() const { return engine_ != nullptr; }
   std::string last_error() const { return engine_ ? ffd_last_error(engine_) : err_; }
+  const FaceForestOptions& options() const { return options_; }
 
   // FaceForest::analyzeFace (FaceForest.cpp:183-258)
   void analyzeFace(const Mat img, Rect face_bbox, Face& face) {
@@ -292,29 +721,22 @@ class FaceForest {
   }
 
   // FaceForest::detectFace (FaceForest.cpp:136-159) with this object's fd_option, on the GPU.
-  void detectFace(const Mat img, std::vector<Rect>& faces_bboxes) {
-    if (!engine_) throw std::runtime_error("FaceForest not initialised: " + err_);
-    ffd_image im{mat_data(img), img.cols, img.rows, mat_step(img)};
-    const ffd_detect_options o = detect_options();
-    std::vector<ffd_rect> r(64);
-    int32_t n = 0;
-    for (int pass = 0; pass < 2; pass++) {
-      const ffd_status st = ffd_detect_faces(engine_, &im, 1, &o, r.data(), nullptr, (int32_t)r.size(), &n);
-      if (st != FFD_OK) throw std::runtime_error(ffd_last_error(engine_));
-      if (n <= (int32_t)r.size()) break;
-      r.resize(n);
-    }
-    faces_bboxes.clear();
-    for (int32_t i = 0; i < n; i++) faces_bboxes.emplace_back(r[i].x, r[i].y, r[i].width, r[i].height);
+  void detectFace(const Mat img, std::vector<Rect>& faces_bboxes) { detect(engine_, img, fd_option_, faces_bboxes); }
+
+  // static FaceForest::detectFace (include/FaceForest.hpp:125-132): the current engine's converted cascade (the
+  // XML of FaceDetectionOption::path_face_cascade) runs in place of the CascadeClassifier argument.
+  static void detectFace(const Mat& img, CascadeClassifier& face_cascade, FaceDetectionOption fd_option,
+                         std::vector<Rect>& faces_bboxes) {
+    (void)face_cascade;
+    detect(detail::current_engine(), img, fd_option, faces_bboxes);
   }
 
   // FaceForest::analyzeImage (FaceForest.cpp:161-181): detectFace, then analyzeFace on every box (one
-  // GPU batch).  Appends to `faces` like the reference; faces with no usable analysis are skipped
-  // only if the reference would throw for them (never for detector boxes, which lie in the image).
+  // GPU batch).  Appends to `faces` like the reference.
   void analyzeImage(const Mat img, std::vector<Face>& faces) {
     if (!engine_) throw std::runtime_error("FaceForest not initialised: " + err_);
     ffd_image im{mat_data(img), img.cols, img.rows, mat_step(img)};
-    const ffd_detect_options o = detect_options();
+    const ffd_detect_options o = detect_options(fd_option_);
     std::vector<ffd_face> out(64);
     int32_t n = 0;
     for (int pass = 0; pass < 2; pass++) {
@@ -392,12 +814,16 @@ class FaceForest {
   Forest<HeadPoseSample> headPoseForest() const {
     std::vector<int32_t> t(15);
     for (int i = 0; i < 15; i++) t[i] = i;
-    return Forest<HeadPoseSample>(engine_, t);
+    Forest<HeadPoseSample> f(engine_, t);
+    f.setParam(forest_param(15));
+    return f;
   }
   Forest<MPSample> ffdForest(int pose_bin) const {
     std::vector<int32_t> t(20);
     for (int i = 0; i < 20; i++) t[i] = pose_bin * 20 + i;
-    return Forest<MPSample>(engine_, t);
+    Forest<MPSample> f(engine_, t);
+    f.setParam(forest_param(20));
+    return f;
   }
 
   // FaceForest::estimateHeadPose (static, FaceForest.cpp:60-72) with the call's options (step_size,
@@ -406,9 +832,9 @@ class FaceForest {
                                HeadPoseEstimatorOption options, float* headpose, float* variance) {
     const ffd_rect r{face_bbox.x, face_bbox.y, face_bbox.width, face_bbox.height};
     const ffd_headpose_option o{options.num_head_pose_labels, options.step_size, options.min_foreground_probability};
-    const ffd_status st = ffd_estimate_headpose(forest.engine(), sample.channels(), sample.width(), sample.height(), &r,
-                                                &o, headpose, variance);
-    if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(forest.engine()));
+    const ffd_status st = ffd_sample_estimate_headpose(sample.handle(), &r, &o, headpose, variance);
+    if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(sample.engine()));
+    (void)forest;
   }
 
   // FaceForest::estimateFacialFeatures (static, FaceForest.cpp:74-95) with the call's
@@ -420,9 +846,10 @@ class FaceForest {
     const ffd_multipart_option o{options.num_parts, options.step_size,  options.min_samples, options.min_forground,
                                  options.min_pf,    options.max_variance, 0};
     int32_t pts[FFD_NUM_LANDMARKS * 2];
-    const ffd_status st = ffd_estimate_facial_features(forest.engine(), sample.channels(), sample.width(), sample.height(),
-                                                       &r, forest.treeIds().data(), forest.numberOfTrees(), &o, pts);
-    if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(forest.engine()));
+    const std::vector<int32_t> ids = forest.treeIds();
+    const ffd_status st =
+        ffd_sample_estimate_facial_features(sample.handle(), &r, ids.data(), (int32_t)ids.size(), &o, pts);
+    if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(sample.engine()));
     ffd_cordinates.clear();
     for (int i = 0; i < options.num_parts && i < FFD_NUM_LANDMARKS; i++) ffd_cordinates.emplace_back(pts[2 * i], pts[2 * i + 1]);
   }
@@ -430,14 +857,78 @@ class FaceForest {
   ffd_engine* engine() const { return engine_; }
 
  private:
-  ffd_detect_options detect_options() const {
+  // The reference-style options: the head-pose tree directory, the FFD forest directories (the given
+  // mp_forest_paths plus the sorted sub-directories of mp_forest_param.tree_path, FaceForest.cpp:39-45) and the
+  // cascade, converted once into a cached FFDMODEL file keyed by their paths, sizes and modification times.
+  bool convert(std::string& model) {
+    FaceForestOptions& o = options_;
+    for (const std::string& d : detail::subdirs(o.mp_forest_param.tree_path)) o.mp_forest_paths.push_back(d);
+    std::sort(o.mp_forest_paths.begin(), o.mp_forest_paths.end());
+    std::string key = "hp:" + o.hp_forest_param.tree_path + ":" + std::to_string(o.hp_forest_param.ntrees);
+    for (int i = 0; i < o.hp_forest_param.ntrees; i++) {
+      char b[32];
+      std::snprintf(b, sizeof b, "/tree_%03d.txt", i);
+      key += ";" + detail::file_key(o.hp_forest_param.tree_path + b);
+    }
+    key += "|mp:" + std::to_string(o.mp_forest_param.ntrees);
+    for (const std::string& d : o.mp_forest_paths)
+      for (int i = 0; i < o.mp_forest_param.ntrees; i++) {
+        char b[32];
+        std::snprintf(b, sizeof b, "/tree_%03d.txt", i);
+        key += ";" + detail::file_key(d + b);
+      }
+    key += "|fd:" + detail::file_key(o.fd_option.path_face_cascade);
+    model = detail::model_cache_path(key);
+    struct stat st;
+    if (stat(model.c_str(), &st) == 0) return true;
+    const ffd_forest_param hp = detail::to_c(o.hp_forest_param), mp = detail::to_c(o.mp_forest_param);
+    std::vector<const char*> dirs;
+    for (const std::string& d : o.mp_forest_paths) dirs.push_back(d.c_str());
+    const char* cascade = o.fd_option.path_face_cascade.empty() ? nullptr : o.fd_option.path_face_cascade.c_str();
+    if (ffd_model_convert(&hp, &mp, dirs.data(), (int32_t)dirs.size(), cascade, model.c_str()) != FFD_OK) {
+      err_ = std::string("(!) Error loading the forests: ") + ffd_model_convert_last_error();
+      std::fprintf(stderr, "ERROR: %s\n", err_.c_str());
+      model.clear();
+      return false;
+    }
+    return true;
+  }
+  // the pretrained forests' ForestParam (config_*.txt: face size 125, patch ratio 0.25) unless the options
+  // carry the reference's own
+  ForestParam forest_param(int ntrees) const {
+    ForestParam p = ntrees == 15 ? options_.hp_forest_param : options_.mp_forest_param;
+    if (p.face_size <= 0) {
+      p.face_size = 125;
+      p.patch_size_ratio = 0.25f;
+      p.ntrees = ntrees;
+      p.features = {0, 1, 2};
+    }
+    return p;
+  }
+  static ffd_detect_options detect_options(const FaceDetectionOption& f) {
     ffd_detect_options o;
     ffd_detect_options_init(&o);
-    o.min_feature_size = fd_option_.min_feature_size;
-    o.min_neighbors = fd_option_.min_neighbors;
-    o.search_scale_factor = fd_option_.search_scale_factor;
+    o.min_feature_size = f.min_feature_size;
+    o.min_neighbors = f.min_neighbors;
+    o.search_scale_factor = f.search_scale_factor;
     return o;
   }
+  static void detect(ffd_engine* e, const Mat& img, const FaceDetectionOption& fo, std::vector<Rect>& faces_bboxes) {
+    if (!e) throw std::runtime_error("FaceForest not initialised");
+    ffd_image im{mat_data(img), img.cols, img.rows, mat_step(img)};
+    const ffd_detect_options o = detect_options(fo);
+    std::vector<ffd_rect> r(64);
+    int32_t n = 0;
+    for (int pass = 0; pass < 2; pass++) {
+      const ffd_status st = ffd_detect_faces(e, &im, 1, &o, r.data(), nullptr, (int32_t)r.size(), &n);
+      if (st != FFD_OK) throw std::runtime_error(ffd_last_error(e));
+      if (n <= (int32_t)r.size()) break;
+      r.resize(n);
+    }
+    faces_bboxes.clear();
+    for (int32_t i = 0; i < n; i++) faces_bboxes.emplace_back(r[i].x, r[i].y, r[i].width, r[i].height);
+  }
+  FaceForestOptions options_;
   ffd_engine* engine_ = nullptr;
   std::string err_;
   FaceDetectionOption fd_option_;
@@ -447,14 +938,35 @@ class FaceForest {
 }  // namespace ffd
 
 #ifdef FFD_GLOBAL_NAMES  // drop-in: the reference's global names
+#ifndef FFD_HAVE_OPENCV
+namespace cv {  // the reference spells the image types cv::Mat / cv::Rect / cv::Point (the PODs above without OpenCV)
+using ffd::CascadeClassifier;
+using ffd::Mat;
+using ffd::Point;
+using ffd::Rect;
+}  // namespace cv
+#endif
+using ffd::CascadeClassifier;
 using ffd::Face;
+using ffd::FaceAnnotation;
 using ffd::FaceDetectionOption;
 using ffd::FaceForest;
 using ffd::FaceForestOptions;
 using ffd::Forest;
+using ffd::ForestParam;
+using ffd::HeadPoseEstimatorOption;
+using ffd::HeadPoseLeaf;
 using ffd::HeadPoseSample;
 using ffd::ImageSample;
+using ffd::MeanShift;
+using ffd::MeanShiftOption;
+using ffd::MPLeaf;
 using ffd::MPSample;
-using ffd::HeadPoseEstimatorOption;
 using ffd::MultiPartEstimatorOption;
+using ffd::Tree;
+using ffd::Vote;
+using ffd::enlargeFace;
+using ffd::intersect;
+using ffd::loadAnnotations;
+using ffd::loadConfigFile;
 #endif

@@ -14,6 +14,8 @@
  *                          -> FeatureChannelFactory::extractChannel       include/FeatureChannelFactory.hpp:35-183
  *   ffd_forest_eval_leaves Forest<S>::evaluateMT over a batch of patches  include/Forest.hpp:80-90
  *                          (Tree<S>::evaluateMT, include/Tree.hpp:173-191)
+ *   ffd_sample_*           ImageSample kept in HBM + Forest<S>::evaluateMT  src/ImageSample.cpp:11-20,
+ *                          per patch / per grid; MeanShift::shift           include/MeanShift.hpp:41-76
  *   ffd_get_trace          per-stage intermediates of the last batch (test hook; the reference has
  *                          plotVotes/show for the same purpose, src/face_utils.cpp:348-376)
  *   ffd_engine_destroy     FaceForest::~FaceForest                        include/FaceForest.hpp:93-95
@@ -197,6 +199,50 @@ typedef struct {             /* MPLeaf, include/MPSample.hpp:137-159 */
 } ffd_mp_leaf;
 ffd_status ffd_forest_leaves(ffd_engine* engine, int32_t forest_kind, const int32_t* leaf_ids, int32_t n, void* out);
 
+/* ---- Device-resident image samples (ImageSample + Forest<S>::evaluateMT, the reference's low-level API) ----
+ * ffd_sample_create      ImageSample(img, features, use_integral)     src/ImageSample.cpp:11-20,77-90: the 38
+ *                        integral channels of an 8-bit gray face computed on the GPU and KEPT in HBM (u16 planes
+ *                        mod 2^16, exact for every rectangle a split reads); no host copy is made.
+ * ffd_sample_eval_leaves Forest<S>::evaluateMT(const S*, S::Leaf**)   include/Forest.hpp:80-90 for patches of the
+ *                        sample: one launch writing the leaf ordinals to pinned host memory and one stream
+ *                        synchronisation (no upload, no allocation, no host narrowing per call).
+ * ffd_sample_eval_grid   the same for the patch grid x0 + i*step, y0 + j*step (i < nx, j < ny): the patches
+ *                        getHeadPoseVotesMT / getFacialFeaturesVotesMT (src/face_utils.cpp:197-207,255-265)
+ *                        evaluate one by one, in ONE launch; leaf_ids[(i*ny + j)*n_trees + t].
+ * ffd_sample_estimate_headpose / ffd_sample_estimate_facial_features: FaceForest::estimateHeadPose /
+ *                        estimateFacialFeatures (static, src/FaceForest.cpp:60-95) on the sample, as
+ *                        ffd_estimate_headpose / ffd_estimate_facial_features.
+ * ffd_meanshift          MeanShift::shift (include/MeanShift.hpp:41-76) of one vote list on the GPU: votes
+ *                        with check == 0 are skipped as in getMean / getWeightedMean; result = the mode before
+ *                        rounding (the reference's Point_<int> result is cvRound of it).
+ * A sample belongs to the engine that made it (destroy it before the engine).  Samples taller than 525
+ * rows at width 125 (255 W H >= 2^24: the reference's float integrals round) are FFD_ERR_UNSUPPORTED. */
+typedef struct ffd_sample ffd_sample;
+ffd_status ffd_sample_create(ffd_engine* engine, const uint8_t* gray, int32_t width, int32_t height, int32_t stride,
+                             ffd_sample** out);
+/* from 38 integral planes in the layout of ffd_extract_channels (e.g. the reference's own channels) */
+ffd_status ffd_sample_create_from_channels(ffd_engine* engine, const uint32_t* channels, int32_t width,
+                                           int32_t height, ffd_sample** out);
+void ffd_sample_destroy(ffd_sample* sample);
+ffd_status ffd_sample_size(const ffd_sample* sample, int32_t* width, int32_t* height);
+/* the channels back as 38 u32 integral planes (ffd_extract_channels layout) */
+ffd_status ffd_sample_channels(const ffd_sample* sample, uint32_t* out);
+ffd_status ffd_sample_eval_leaves(ffd_sample* sample, int32_t forest_kind, const int32_t* patches_xy,
+                                  int32_t n_patches, const int32_t* tree_ids, int32_t n_trees, int32_t* leaf_ids);
+ffd_status ffd_sample_eval_grid(ffd_sample* sample, int32_t forest_kind, int32_t x0, int32_t y0, int32_t step,
+                                int32_t nx, int32_t ny, const int32_t* tree_ids, int32_t n_trees, int32_t* leaf_ids);
+ffd_status ffd_sample_estimate_headpose(ffd_sample* sample, const ffd_rect* region, const ffd_headpose_option* options,
+                                        float* headpose, float* variance);
+ffd_status ffd_sample_estimate_facial_features(ffd_sample* sample, const ffd_rect* region, const int32_t* tree_ids,
+                                               int32_t n_trees, const ffd_multipart_option* options, int32_t* points);
+typedef struct {             /* Vote, include/face_utils.hpp:34-42 */
+  int32_t x, y;              /* pos */
+  float weight;
+  int32_t check;
+} ffd_vote;
+ffd_status ffd_meanshift(ffd_engine* engine, const ffd_vote* votes, int32_t n, const ffd_meanshift_option* option,
+                         float* mean_xy);
+
 /* Intermediates of face `index` of the most recent ffd_analyze_faces[_device] batch.
  * Any pointer may be NULL; sizes as documented per field (from ffd_face_geometry). */
 typedef struct {
@@ -306,6 +352,27 @@ ffd_status ffd_model_tree_save_path(const ffd_model* model, int32_t forest_kind,
 ffd_status ffd_model_tree_archive(const ffd_model* model, int32_t forest_kind, int32_t tree, char* buf, int64_t cap,
                                   int64_t* size);
 ffd_status ffd_model_save_tree(const ffd_model* model, int32_t forest_kind, int32_t tree, const char* path);
+
+/* ---- Model conversion (the reference's FaceForest ctor / Forest<S>::load inputs) -------------------
+ * ffd_model_convert  FaceForest::FaceForest's loads (src/FaceForest.cpp:15-58): hp->ntrees head-pose trees
+ *                    from hp->tree_path, mp->ntrees trees from each of mp_dirs (in the given order; the
+ *                    reference sorts the sub-directories of mp_forest_param.tree_path, FaceForest.cpp:39-45,
+ *                    which ffd_forest_subdirs lists), through Forest<S>::load / Tree<S>::load
+ *                    (include/Forest.hpp:103-153, Tree.hpp:193-237), and the Haar cascade XML (may be NULL),
+ *                    into the FFDMODEL file ffd_engine_create loads.  Host only.
+ * ffd_forest_subdirs the sorted sub-directories of dir, NUL-separated, into buf (NULL: only *size). */
+typedef struct {                 /* ForestParam, include/Constants.hpp:24-60 */
+  int32_t max_depth, min_patches, ntests, ntrees, nimages, npatches, face_size;
+  float patch_size_ratio;
+  const char* tree_path;
+  const char* image_path;
+  const int32_t* features;
+  int32_t n_features;
+} ffd_forest_param;
+ffd_status ffd_model_convert(const ffd_forest_param* hp, const ffd_forest_param* mp, const char* const* mp_dirs,
+                             int32_t n_mp_dirs, const char* cascade_xml, const char* out_path);
+const char* ffd_model_convert_last_error(void);  /* this thread's last ffd_model_convert / ffd_forest_subdirs failure */
+ffd_status ffd_forest_subdirs(const char* dir, char* buf, int64_t cap, int64_t* size);
 
 /* ---- Facial-feature tree training ----------------------------------------
  * Replaces trainTree (src/train_ffd.cpp:34-123) from the training ROIs on: the patch sampling, the

@@ -83,6 +83,9 @@ def lib():
         L.oracle_detect_faces.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 5 + [ctypes.c_float, ctypes.c_int32,
             ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), ctypes.c_void_p, ctypes.c_int32,
             ctypes.POINTER(ctypes.c_int32)]
+        L.oracle_eval_patches.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 3 + [ctypes.c_void_p, ctypes.c_int32,
+                                                                                      ctypes.c_void_p, ctypes.c_int32,
+                                                                                      ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -246,6 +249,19 @@ def exp(x):
 
 def expf(x):
     return lib().oracle_expf(x)
+
+
+def eval_patches(channels, xy, kind, tree_ids):
+    """Tree<S>::evaluateMT for a patch list: [n_patches][n_trees] leaf ordinals (kind 0 head pose, 1 FFD)."""
+    ch = np.ascontiguousarray(channels, np.uint32)
+    _, h1, w1 = ch.shape
+    p = np.ascontiguousarray(xy, np.int32).reshape(-1, 2)
+    t = np.ascontiguousarray(tree_ids, np.int32)
+    out = np.zeros((p.shape[0], t.size), np.int32)
+    if lib().oracle_eval_patches(ch.ctypes.data, w1 - 1, h1 - 1, int(kind), p.ctypes.data, p.shape[0], t.ctypes.data,
+                                 t.size, out.ctypes.data) != 0:
+        raise RuntimeError(lib().oracle_last_error().decode())
+    return out
 
 
 def estimate_headpose(channels, region=None):

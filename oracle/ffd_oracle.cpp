@@ -1118,4 +1118,16 @@ int oracle_estimate_facial_features(const uint32_t* channels, int32_t W, int32_t
   return 0;
 }
 
+// Tree<S>::evaluateMT (Tree.hpp:173-191) for an explicit patch list: leaf[p * n_trees + t] of tree tree_ids[t]
+// (kind 0 head pose, 1 FFD global id) from the patch at (xy[2p], xy[2p + 1]).
+int oracle_eval_patches(const uint32_t* channels, int32_t W, int32_t H, int32_t kind, const int32_t* xy, int32_t n,
+                        const int32_t* tree_ids, int32_t n_trees, int32_t* leaf) {
+  if (!g_loaded) { g_err = "model not loaded"; return -1; }
+  const Forest& F = kind == 0 ? g_hp : g_mp;
+  for (int p = 0; p < n; p++)
+    for (int t = 0; t < n_trees; t++)
+      leaf[p * n_trees + t] = walk(F, F.roots[tree_ids[t]], channels, W, H, xy[2 * p], xy[2 * p + 1]);
+  return 0;
+}
+
 }  // extern "C"

@@ -10,5 +10,5 @@ mkdir -p build/$NAME
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
   -Iinclude $X -c face_alignment_cvpr_2012_amd/csrc/ffd_kernels.hip -o build/$NAME/ffd_kernels.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/$NAME/libffd.so build/$NAME/ffd_kernels.o \
-  $L/ffd_engine.o $L/ffd_group.o $L/ffd_archive.o $L/ffd_haar.o $L/ffd_detect.o $L/ffd_train_k.o $L/ffd_train.o -L/opt/rocm/lib -lrccl
+  $L/ffd_engine.o $L/ffd_group.o $L/ffd_archive.o $L/ffd_haar.o $L/ffd_detect.o $L/ffd_train_k.o $L/ffd_train.o $L/ffd_convert.o -L/opt/rocm/lib -lrccl
 echo "build/$NAME/libffd.so: $X"

@@ -36,6 +36,15 @@ def summarise_timing(rec, nw_waves):
             "walk_cycles_per_wave_mean": float(wk[..., 1][ok].mean())}
 
 
+def summarise_phases(rec, nw_waves):
+    """FFD_TRAV_STATS=3 builds: per wave, cycles of its walk phases (fields 2, 3, 4, 6) and the whole walk (1)."""
+    wk = rec[:, :, :nw_waves, :].astype(np.float64)
+    ok = wk[..., 5] > 0
+    return {"walk": float(wk[..., 1][ok].mean()), "setup": float(wk[..., 2][ok].mean()),
+            "top_levels": float(wk[..., 3][ok].mean()), "deep_levels": float(wk[..., 4][ok].mean()),
+            "store": float(wk[..., 6][ok].mean())}
+
+
 def summarise(rec, nw_waves, walker_lanes):
     # rec: [wg][iter][slot][8] u32
     wk = rec[:, :, :nw_waves, :].astype(np.float64)
@@ -92,6 +101,7 @@ def main():
     ap.add_argument("--faces", type=int, default=4096)
     ap.add_argument("--out", default="")
     ap.add_argument("--timing", action="store_true", help="FFD_TRAV_STATS=2 build: test / fetch-wait split")
+    ap.add_argument("--phases", action="store_true", help="FFD_TRAV_STATS=3 build: walk phases")
     args = ap.parse_args()
     import torch
 
@@ -122,7 +132,8 @@ def main():
     for hp, name, nw in ((1, "headpose", 320), (0, "ffd", 512)):
         buf = np.zeros((256, ITERS, SLOTS, 8), dtype=np.uint32)
         assert L.ffd_trav_stats_read(hp, buf.ctypes.data, buf.nbytes) == 0
-        res[name] = summarise_timing(buf, nw // 64) if args.timing else summarise(buf, nw // 64, nw)
+        res[name] = (summarise_timing(buf, nw // 64) if args.timing else
+                     summarise_phases(buf, nw // 64) if args.phases else summarise(buf, nw // 64, nw))
     print(json.dumps(res, indent=1))
     if args.out:
         with open(args.out, "w") as f:
