@@ -127,7 +127,7 @@ EXPORTED_SYMBOLS = (
     "ffd_sample_create", "ffd_sample_create_from_channels", "ffd_sample_destroy", "ffd_sample_size",
     "ffd_sample_channels", "ffd_sample_eval_leaves", "ffd_sample_eval_grid", "ffd_sample_estimate_headpose",
     "ffd_sample_estimate_facial_features", "ffd_meanshift", "ffd_model_convert", "ffd_model_convert_last_error",
-    "ffd_forest_subdirs",
+    "ffd_forest_subdirs", "ffd_group_debug_overlap",
 )
 COMM_ID_BYTES = 128
 STATUS_OK, STATUS_INVALID_ARGUMENT, STATUS_UNSUPPORTED = 0, 1, 7
@@ -223,6 +223,8 @@ def lib():
     L.ffd_sample_estimate_facial_features.argtypes = [vp, P(_Rect), vp, i32, P(_MpOpt), vp]
     L.ffd_meanshift.argtypes = [vp, vp, i32, P(_MsOpt), vp]
     L.ffd_model_convert_last_error.restype = ctypes.c_char_p
+    L.ffd_group_debug_overlap.argtypes = [i32, i32, P(ctypes.c_double)]
+    L.ffd_group_debug_overlap.restype = ctypes.c_int
     for name in ("ffd_sample_create", "ffd_sample_create_from_channels", "ffd_sample_size", "ffd_sample_channels",
                  "ffd_sample_eval_leaves", "ffd_sample_eval_grid", "ffd_sample_estimate_headpose",
                  "ffd_sample_estimate_facial_features", "ffd_meanshift"):

@@ -11,10 +11,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ffd_engine_impl.hpp"
@@ -42,6 +44,31 @@ void shard(int n, int world, int rank, int& lo, int& hi) {
 }
 
 thread_local std::string g_group_err;
+
+// Runs fn(d) for every device d < G, device 0 on the calling thread and the others on threads of their own:
+// a device's shard reaches it by pageable host copies that the runtime stages on the calling thread, so one
+// host thread per device lets the uploads (and the launches) of all devices proceed at once.  Returns the
+// per-device status; a device whose fn throws gets FFD_ERR_DEVICE / FFD_ERR_INTERNAL and its message.
+template <class F> std::vector<ffd_status> for_each_device(int G, std::vector<std::string>& errs, F&& fn) {
+  std::vector<ffd_status> st(G, FFD_OK);
+  errs.assign(G, std::string());
+  auto run = [&](int d) {
+    try {
+      st[d] = fn(d);
+    } catch (const HipError& x) {
+      st[d] = FFD_ERR_DEVICE;
+      errs[d] = x.what();
+    } catch (const std::exception& x) {
+      st[d] = FFD_ERR_INTERNAL;
+      errs[d] = x.what();
+    }
+  };
+  std::vector<std::thread> th;
+  for (int d = 1; d < G; d++) th.emplace_back(run, d);
+  run(0);
+  for (auto& t : th) t.join();
+  return st;
+}
 
 }  // namespace
 
@@ -169,35 +196,42 @@ ffd_status ffd_group_analyze_faces(ffd_group* g, const ffd_image* imgs, int32_t 
     }
     if (n_faces == 0) return FFD_OK;
     const int G = (int)g->engines.size(), per = (n_faces + G - 1) / G;
-    // every device: its contiguous face block, with only the images those faces reference
-    for (int d = 0; d < G; d++) {
+    for (int i = 0; i < n_faces; i++) {
+      const int k = box_img ? box_img[i] : i;
+      if (k < 0 || k >= n_img) {
+        g->err = "box_img out of range";
+        return FFD_ERR_INVALID_ARGUMENT;
+      }
+    }
+    // every device, on a host thread of its own: its contiguous face block, with only the images those faces
+    // reference (the engines are independent objects; each thread touches only its own)
+    std::vector<std::string> errs;
+    const std::vector<ffd_status> sts = for_each_device(G, errs, [&](int d) -> ffd_status {
       int lo, hi;
       shard(n_faces, G, d, lo, hi);
       HIP_CHECK(hipSetDevice(g->devices[d]));
       g->local[d]->ensure((size_t)per * REC);
       HIP_CHECK(hipMemsetAsync(g->local[d]->p, 0, (size_t)per * REC, (hipStream_t)ffd_stream(g->engines[d])));
-      if (hi <= lo) continue;
+      if (hi <= lo) return FFD_OK;
       std::vector<int32_t> remap(n_img, -1), sub_box_img;
       std::vector<ffd_image> sub_imgs;
       for (int i = lo; i < hi; i++) {
         const int k = box_img ? box_img[i] : i;
-        if (k < 0 || k >= n_img) {
-          g->err = "box_img out of range";
-          return FFD_ERR_INVALID_ARGUMENT;
-        }
         if (remap[k] < 0) {
           remap[k] = (int32_t)sub_imgs.size();
           sub_imgs.push_back(imgs[k]);
         }
         sub_box_img.push_back(remap[k]);
       }
-      const ffd_status st = analyze_host(g->engines[d], sub_imgs.data(), (int32_t)sub_imgs.size(), boxes + lo,
-                                         sub_box_img.data(), hi - lo, g->local[d]->p);
-      if (st != FFD_OK) {
-        g->err = std::string("device ") + std::to_string(g->devices[d]) + ": " + ffd_last_error(g->engines[d]);
-        return st;
+      return analyze_host(g->engines[d], sub_imgs.data(), (int32_t)sub_imgs.size(), boxes + lo, sub_box_img.data(),
+                          hi - lo, g->local[d]->p);
+    });
+    for (int d = 0; d < G; d++)
+      if (sts[d] != FFD_OK) {
+        g->err = std::string("device ") + std::to_string(g->devices[d]) + ": " +
+                 (errs[d].empty() ? std::string(ffd_last_error(g->engines[d])) : errs[d]);
+        return sts[d];
       }
-    }
     // one gather of every device's (padded) records to devices[0], on each engine's stream
     HIP_CHECK(hipSetDevice(g->devices[0]));
     g->gathered.ensure((size_t)G * per * REC);
@@ -222,6 +256,18 @@ ffd_status ffd_group_analyze_faces(ffd_group* g, const ffd_image* imgs, int32_t 
     }
     return FFD_OK;
   });
+}
+
+ffd_status ffd_group_debug_overlap(int32_t n, int32_t ms, double* wall_ms) {
+  if (n < 1 || ms < 0 || !wall_ms) return FFD_ERR_INVALID_ARGUMENT;
+  std::vector<std::string> errs;
+  const auto t0 = std::chrono::steady_clock::now();
+  for_each_device(n, errs, [&](int) -> ffd_status {
+    std::this_thread::sleep_for(std::chrono::milliseconds(ms));
+    return FFD_OK;
+  });
+  *wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return FFD_OK;
 }
 
 ffd_status ffd_comm_id(uint8_t* id) {

@@ -1139,6 +1139,22 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
 #if FFD_TRAV_PROBE == 4 || FFD_TRAV_PROBE == 5
         return ((lo ^ (hi >> 3)) >> 9) & 1u;  // probe: no window reads
 #endif
+#if FFD_TRAV_PROBE == 9  // probe: the 12 reads at wave-uniform addresses (LDS broadcast, no conflicts), same VALU
+        auto rect9 = [&](int k, uint32_t w, uint32_t h) {
+          const unsigned char* p = reinterpret_cast<const unsigned char*>(win) + 64 * k;
+          const uint32_t area = __umul24(w, h);
+          const uint32_t a = *reinterpret_cast<const uint16_t*>(p), b = *reinterpret_cast<const uint16_t*>(p + 8);
+          const uint32_t f0 = *reinterpret_cast<const uint16_t*>(p + 16), f1 = *reinterpret_cast<const uint16_t*>(p + 24);
+          const uint32_t c = *reinterpret_cast<const uint16_t*>(p + 32), d = *reinterpret_cast<const uint16_t*>(p + 40);
+          typedef unsigned short u16;
+          const u16 dc = (u16)(d - c + w), top = (u16)((u16)(a - b) + dc), bot = (u16)((u16)(f1 - f0) - dc);
+          return (int)__builtin_fmaf((float)((uint32_t)top + bot), __builtin_amdgcn_rcpf((float)area), 0.00075f);
+        };
+        const int q1 = rect9(0, __builtin_amdgcn_ubfe(hi, 0, 5), __builtin_amdgcn_ubfe(hi, 5, 5));
+        const int q2 = rect9(1, __builtin_amdgcn_ubfe(hi, 10, 5), __builtin_amdgcn_ubfe(hi, 15, 5));
+        const int thr9 = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
+        return (q1 - q2 + (int)(lo & 31u) - 16) <= thr9 ? 0u : 1u;
+#else
         // (fields by bit-field extracts; bits of hi above 23 are the record's child offset, never read)
         const unsigned char* cb = base + __umul24(lo >> 26, (unsigned)chs2);
         const int p1 = rect_mean_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 0, 5),
@@ -1154,6 +1170,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         // 10-bit two's complement: sign-extended thr[9:6] (hi[23:20]) above thr[5:0] (lo[25:20])
         const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
         return (p1 - p2) <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
+#endif
       };
       // levels 0..log2(topn): heap-ordered pair records in LDS (the children pair of node (h, s) is
       // entry 2h + s, of the root (h = 0) entry 1)

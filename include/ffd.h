@@ -288,6 +288,10 @@ ffd_engine* ffd_group_engine(ffd_group* group, int32_t index);  /* owned by the 
 ffd_status ffd_group_analyze_faces(ffd_group* group, const ffd_image* imgs, int32_t n_img, const ffd_rect* boxes,
                                    const int32_t* box_img, int32_t n_faces, ffd_face* out);
 
+/* Test hook: the group's per-device driver (one host thread per device) running n tasks that each sleep
+ * `ms` milliseconds; *wall_ms is the elapsed time (about ms when the devices' work is issued concurrently). */
+ffd_status ffd_group_debug_overlap(int32_t n, int32_t ms, double* wall_ms);
+
 /* One process per device: one rank creates the id (ncclGetUniqueId) and shares it with the others
  * (MPI / torch.distributed broadcast, a file ...); every rank joins with its engine
  * (ncclCommInitRank on the engine's device); ffd_gather_faces then gathers n_per_rank ffd_face

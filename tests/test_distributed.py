@@ -115,3 +115,16 @@ def test_bench_uneven_rank_counts_gather():
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert line["n_gpus"] == 3 and line["faces"] == 3 + 4 + 5 and line["gather_ok"]
+
+
+def test_group_issues_devices_concurrently():
+    """ffd_group_analyze_faces drives every device from a host thread of its own (csrc/ffd_group.cpp
+    for_each_device), so one device's pageable uploads do not wait for another's: the same driver running 4
+    tasks of 200 ms each takes about 200 ms, not 800."""
+    import ctypes
+
+    import face_alignment_cvpr_2012_amd as ffd
+    wall = ctypes.c_double()
+    assert ffd.lib().ffd_group_debug_overlap(4, 200, ctypes.byref(wall)) == 0
+    assert 195.0 <= wall.value < 400.0, wall.value
+    assert ffd.lib().ffd_group_debug_overlap(1, 50, ctypes.byref(wall)) == 0 and wall.value >= 49.0

@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--timing", action="store_true", help="FFD_TRAV_STATS=2 build: test / fetch-wait split")
     ap.add_argument("--phases", action="store_true", help="FFD_TRAV_STATS=3 build: walk phases")
+    ap.add_argument("--same-face", action="store_true", help="every face of the batch the same crop (L2-resident trees)")
     args = ap.parse_args()
     import torch
 
@@ -112,7 +113,9 @@ def main():
     L.ffd_trav_stats_enable.restype = ctypes.c_int
     L.ffd_trav_stats_read.restype = ctypes.c_int
     L.ffd_trav_stats_read.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
-    crops, _ = make_crops(args.faces, seed=2012)
+    crops, _ = make_crops(1 if args.same_face else args.faces, seed=2012)
+    if args.same_face:
+        crops = np.repeat(crops, args.faces, axis=0)
     dev = torch.device("cuda:0")
     d_img = torch.from_numpy(np.ascontiguousarray(crops)).to(dev)
     rec = ffd.FACE_RECORD_BYTES
