@@ -210,9 +210,11 @@ void build_levels(const ffd_engine* e, const std::vector<FrameIn>& in, const ffd
 // Run the detector over frames already in device memory (e->main_stream()); boxes per frame out.
 // Frames go through in groups (FFD_DETECT_GROUP frames, default 64) so the pyramid / integral /
 // survivor buffers stay bounded whatever the batch.
+// cap: raw candidates per frame the collection and grouping hold; a frame with more is run again on its own
+// with a capacity that holds all of them (detectMultiScale has no limit, FaceForest.cpp:146).
 ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vector<FrameIn>& all_in,
                         const ffd_detect_options& o, std::vector<std::vector<ffd_rect>>& out,
-                        std::vector<std::vector<ffd_rect>>* raw) {
+                        std::vector<std::vector<ffd_rect>>* raw, int cap = 0) {
   if (!e->have_haar) return fail(e, FFD_ERR_MODEL, "the model has no Haar cascade (convert it with ffd_convert)");
   if (!(o.search_scale_factor > 1.f) || o.min_feature_size < 0)
     return fail(e, FFD_ERR_INVALID_ARGUMENT, "search_scale_factor must be > 1 and min_feature_size >= 0");
@@ -223,7 +225,10 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
   int group = 64;
   if (const char* v = std::getenv("FFD_DETECT_GROUP")) group = std::max(1, std::atoi(v));
   hipStream_t s = e->main_stream();
-  const int cap = HAAR_MAX_CAND;
+  // (FFD_DETECT_CAP / FFD_DETECT_RERUN_CAP: test hooks that force the overflow re-runs with small frames)
+  const int rerun_min = std::getenv("FFD_DETECT_RERUN_CAP") ? std::atoi(std::getenv("FFD_DETECT_RERUN_CAP")) : 0;
+  if (cap <= 0) cap = std::getenv("FFD_DETECT_CAP") ? std::max(16, std::atoi(std::getenv("FFD_DETECT_CAP"))) : HAAR_MAX_CAND;
+  if (cap > HAAR_MAX_CAND) group = 1;
   for (size_t g0 = 0; g0 < all_in.size(); g0 += group) {
     const std::vector<FrameIn> in(all_in.begin() + g0, all_in.begin() + std::min(all_in.size(), g0 + group));
     std::vector<HaarFrame> frames;
@@ -239,6 +244,7 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
     e->det_clssum.ensure((size_t)nF * cap * 20);
     e->det_boxes.ensure((size_t)nF * cap * 16);
     e->det_packed.ensure((size_t)nF * cap * 20);
+    if (cap > HAAR_MAX_CAND) e->det_label.ensure((size_t)nF * cap * 4);
     int max_px = 0, max_lpx = 0, max_rows = 0, max_cols = 0, max_tiles = 0, max_ystep = 1;
     for (const auto& f : frames) max_px = std::max(max_px, f.w * f.h);
     for (const auto& L : levels) {
@@ -271,18 +277,22 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
     launch_haar_group(e->det_frames.as<HaarFrame>(), nF, max_frame_rows, e->det_rowcnt.as<int32_t>(), nL > 0 ? e->det_levels.as<HaarLevel>() : nullptr,
                       nL > 0 ? e->det_res.as<int8_t>() : nullptr, cap, e->det_cand.as<int4>(), n_cand,
                       o.min_neighbors, o.widen, e->det_clsrect.as<int4>(), e->det_clssum.as<int>(),
-                      e->det_boxes.as<int4>(), n_boxes, s);
+                      e->det_boxes.as<int4>(), n_boxes, cap > HAAR_MAX_CAND ? e->det_label.as<int>() : nullptr, s);
     int4* packed = e->det_packed.as<int4>();
     int32_t* owner = reinterpret_cast<int32_t*>(packed + (size_t)nF * cap);
     launch_haar_pack(nF, cap, e->det_boxes.as<int4>(), n_boxes, packed, owner, s);
     std::vector<int32_t> counts(2 * nF);
     HIP_CHECK(hipMemcpyAsync(counts.data(), n_cand, 2 * nF * 4, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    int64_t total = 0;
+    int64_t total = 0;  // packed boxes of the group, every frame's
+    std::vector<char> over(nF, 0);  // frames whose raw candidates exceed cap: boxes from a run of their own
     for (int k = 0; k < nF; k++) {
-      if (counts[k] > cap)
-        return fail(e, FFD_ERR_UNSUPPORTED, "frame " + std::to_string(g0 + k) + ": " + std::to_string(counts[k]) +
-                                                " raw detections exceed the grouping capacity " + std::to_string(cap));
+      if (counts[k] > cap) {
+        if (counts[k] > (1 << 24))
+          return fail(e, FFD_ERR_UNSUPPORTED, "frame " + std::to_string(g0 + k) + ": " + std::to_string(counts[k]) +
+                                                  " raw detections");
+        over[k] = 1;
+      }
       total += counts[nF + k];
     }
     std::vector<int4> pb(total);
@@ -292,9 +302,11 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
       HIP_CHECK(hipMemcpyAsync(po.data(), owner, total * sizeof(int32_t), hipMemcpyDeviceToHost, s));
       HIP_CHECK(hipStreamSynchronize(s));
     }
-    for (int64_t i = 0; i < total; i++) out[g0 + po[i]].push_back(ffd_rect{pb[i].x, pb[i].y, pb[i].z, pb[i].w});
+    for (int64_t i = 0; i < total; i++)
+      if (!over[po[i]]) out[g0 + po[i]].push_back(ffd_rect{pb[i].x, pb[i].y, pb[i].z, pb[i].w});
     if (raw) {
       for (int k = 0; k < nF; k++) {
+        if (over[k]) continue;
         std::vector<int4> tmp(counts[k]);
         if (counts[k] > 0) {
           HIP_CHECK(hipMemcpyAsync(tmp.data(), e->det_cand.as<int4>() + (int64_t)k * cap, counts[k] * sizeof(int4),
@@ -303,6 +315,15 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
         }
         for (const int4& b : tmp) (*raw)[g0 + k].push_back(ffd_rect{b.x, b.y, b.z, b.w});
       }
+    }
+    for (int k = 0; k < nF; k++) {
+      if (!over[k]) continue;
+      std::vector<std::vector<ffd_rect>> o1, r1;
+      const int cap1 = std::max(rerun_min, (counts[k] + 1023) / 1024 * 1024);
+      const ffd_status st = detect_batch(e, d_images, {in[k]}, o, o1, raw ? &r1 : nullptr, cap1);
+      if (st != FFD_OK) return st;
+      out[g0 + k] = o1[0];
+      if (raw) (*raw)[g0 + k] = r1[0];
     }
   }
   return FFD_OK;

@@ -1110,6 +1110,7 @@ FaceDesc stage_sample(ffd_engine* e, Workspace& w, const uint32_t* ch, int W, in
   w.chan.ensure(J.size() * 2 + 512);  // slack: traversal windows read past a row
   HIP_CHECK(hipMemcpyAsync(w.chan.p, J.data(), J.size() * 2, hipMemcpyHostToDevice, w.stream));
   stage_desc(e, w, f);
+  HIP_CHECK(hipStreamSynchronize(w.stream));  // J is released on return
   return f;
 }
 
@@ -1121,9 +1122,7 @@ void stage_desc(ffd_engine* e, Workspace& w, const FaceDesc& f) {
   w.state.ensure(sizeof(HpState));
   w.ms_mean.ensure(NPARTS * 2 * 4);
   w.vote_counts.ensure(NPARTS * 4);
-  std::vector<FaceDesc> one{f};
-  upload(w.faces, one, w.stream);
-  HIP_CHECK(hipStreamSynchronize(w.stream));  // the staging vectors are released on return
+  e->upload_descriptors(w.faces, std::vector<FaceDesc>{f}, w.stream);  // pinned staging: no synchronisation
   w.count = 0;  // the workspace no longer holds a batch for ffd_get_trace
   w.pending = false;
   if (e->last_ws == 0) e->last_ws = -1;

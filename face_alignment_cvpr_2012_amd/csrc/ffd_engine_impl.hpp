@@ -167,7 +167,7 @@ struct ffd_engine {
   int haar_order_free = 0;  // every stage's leaf sum is exact in any order (ffd_detect.cpp load_cascade)
   int haar_nweak = 0;  // weak classifiers per ystep table (haar_weak holds two)
   DevBuf det_frames, det_levels, det_gray, det_scaled, det_sum, det_sq, det_res, det_cand, det_ncand, det_rowcnt, det_clsrect,
-      det_clssum, det_boxes, det_packed;
+      det_clssum, det_boxes, det_packed, det_label;
   int n_cu = 256;  // compute units of the device (survivor-pass grids)
 
   std::vector<std::unique_ptr<Workspace>> ws;

@@ -553,13 +553,25 @@ __device__ __forceinline__ int ld_agent(const int* p) {  // coherent read of a v
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// GLOBAL: the component labels in global memory (label_g, cap per frame) for frames with more raw candidates
+// than the LDS holds (HAAR_MAX_CAND); the same algorithm, the labels read and written with relaxed atomics.
+template <bool GLOBAL>
 __global__ __launch_bounds__(HC_THREADS) void k_haar_group(const HaarFrame* __restrict__ frames, int cap,
                                                             const int4* __restrict__ cand,
                                                             const int32_t* __restrict__ n_cand, int min_neighbors,
                                                             int widen, int4* __restrict__ cls_rect,
                                                             int* __restrict__ cls_sum, int4* __restrict__ boxes,
-                                                            int32_t* __restrict__ n_boxes) {
-  __shared__ int label[HAAR_MAX_CAND];
+                                                            int32_t* __restrict__ n_boxes, int* __restrict__ label_g) {
+  __shared__ int label_s[GLOBAL ? 1 : HAAR_MAX_CAND];
+  int* const labp = GLOBAL ? label_g + (int64_t)blockIdx.x * cap : label_s;
+  auto lget = [&](int i) -> int {
+    if constexpr (GLOBAL) return __hip_atomic_load(labp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return labp[i];
+  };
+  auto lset = [&](int i, int v) {
+    if constexpr (GLOBAL) __hip_atomic_store(labp + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else labp[i] = v;
+  };
   __shared__ int sh[HC_THREADS / 64 + 1];
   __shared__ int changed;
   const HaarFrame f = frames[blockIdx.x];
@@ -573,22 +585,22 @@ __global__ __launch_bounds__(HC_THREADS) void k_haar_group(const HaarFrame* __re
     return;
   }
   // connected components of SimilarRects: every label converges to its component's smallest index
-  for (int i = threadIdx.x; i < N; i += HC_THREADS) label[i] = i;
+  for (int i = threadIdx.x; i < N; i += HC_THREADS) lset(i, i);
   for (;;) {
     if (threadIdx.x == 0) changed = 0;
     __syncthreads();
     for (int i = threadIdx.x; i < N; i += HC_THREADS) {
       const int4 ri = R[i];
-      int m = label[i];
+      int m = lget(i);
       for (int j = 0; j < N; j++)
-        if (j != i && label[j] < m && similar_rects(ri, R[j], eps)) m = label[j];
-      if (m < label[i]) { label[i] = m; changed = 1; }
+        if (j != i && lget(j) < m && similar_rects(ri, R[j], eps)) m = lget(j);
+      if (m < lget(i)) { lset(i, m); changed = 1; }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < N; i += HC_THREADS) {  // pointer jumping (labels only decrease)
-      int l = label[i];
-      while (label[l] != l) l = label[l];
-      label[i] = l;
+      int l = lget(i);
+      while (lget(l) != l) l = lget(l);
+      lset(i, l);
     }
     __syncthreads();
     if (!changed) break;
@@ -599,11 +611,11 @@ __global__ __launch_bounds__(HC_THREADS) void k_haar_group(const HaarFrame* __re
   int ncls = 0;
   for (int i0 = 0; i0 < N; i0 += HC_THREADS) {
     const int i = i0 + threadIdx.x;
-    const int is_root = (i < N && label[i] == i) ? 1 : 0;
+    const int is_root = (i < N && lget(i) == i) ? 1 : 0;
     int tot;
     const int id = block_excl_scan(is_root, sh, tot) + ncls;
     if (is_root) {
-      label[i] = -1 - id;  // roots now hold ~class id (members still point at the root index)
+      lset(i, -1 - id);  // roots now hold ~class id (members still point at the root index)
       for (int k = 0; k < 5; k++) __hip_atomic_store(&csum[id * 5 + k], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     ncls += tot;
@@ -611,8 +623,8 @@ __global__ __launch_bounds__(HC_THREADS) void k_haar_group(const HaarFrame* __re
   __threadfence();
   __syncthreads();
   for (int i = threadIdx.x; i < N; i += HC_THREADS) {
-    const int l = label[i];
-    const int id = l < 0 ? -1 - l : -1 - label[l];
+    const int l = lget(i);
+    const int id = l < 0 ? -1 - l : -1 - lget(l);
     const int4 r = R[i];
     atomicAdd(&csum[id * 5 + 0], r.x);
     atomicAdd(&csum[id * 5 + 1], r.y);
@@ -733,7 +745,7 @@ void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, c
 void launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows, int32_t* rowcnt,
                        const HaarLevel* levels, const int8_t* result, int cap, int4* cand, int32_t* n_cand,
                        int min_neighbors, int widen, int4* cls_rect, int* cls_sum, int4* boxes, int32_t* n_boxes,
-                       hipStream_t s) {
+                       int* label_g, hipStream_t s) {
 #if FFD_HAAR_COLLECT_SERIAL
   (void)max_frame_rows;
   (void)rowcnt;
@@ -743,8 +755,12 @@ void launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows
   if (max_frame_rows > 0) k_haar_rowcount<<<dim3(n_frames, rb), HR_THREADS, 0, s>>>(frames, levels, result, max_frame_rows, rowcnt);
   k_haar_emit<<<dim3(n_frames, rb), HR_THREADS, 0, s>>>(frames, levels, result, max_frame_rows, rowcnt, cap, cand, n_cand);
 #endif
-  k_haar_group<<<n_frames, HC_THREADS, 0, s>>>(frames, cap, cand, n_cand, min_neighbors, widen, cls_rect, cls_sum,
-                                              boxes, n_boxes);
+  if (cap > HAAR_MAX_CAND)
+    k_haar_group<true><<<n_frames, HC_THREADS, 0, s>>>(frames, cap, cand, n_cand, min_neighbors, widen, cls_rect, cls_sum,
+                                                     boxes, n_boxes, label_g);
+  else
+    k_haar_group<false><<<n_frames, HC_THREADS, 0, s>>>(frames, cap, cand, n_cand, min_neighbors, widen, cls_rect,
+                                                      cls_sum, boxes, n_boxes, nullptr);
 }
 
 }  // namespace ffd

@@ -315,9 +315,9 @@ ffd_status ffd_engine_comm_info(ffd_engine* engine, int32_t* n_ranks, int32_t* r
  *                       every box (all boxes of all frames as one batch); faces in frame order, then
  *                       detection order; face_img[i] = the frame of face i.
  * Boxes beyond max_boxes / max_faces are counted in *n_boxes / *n_faces but not written.
- * Limit (not in the reference): the grouping step holds 8,192 raw (ungrouped) detections per frame; a
- * frame with more makes the call fail with FFD_ERR_UNSUPPORTED, the message naming the frame (natural
- * 1080p frames give a few hundred).
+ * Frames are grouped on the GPU with up to 8,192 raw (ungrouped) detections each in LDS; a frame with more
+ * (natural 1080p frames give a few hundred) is run again on its own with a capacity that holds all of them
+ * (component labels in global memory), so there is no limit but 2^24 detections per frame.
  * Parity: bit-exact with the CPU restatement (oracle/); with OpenCV itself unpinned (no OpenCV here). */
 typedef struct {
   int32_t min_feature_size;    /* FaceDetectionOption (include/FaceForest.hpp:21-32): 30 */

@@ -89,3 +89,22 @@ def test_analyze_image_end_to_end(engine, oracle_mod, fixtures, frames):
             assert f.status == 0
             assert np.array_equal(f.ffd_cordinates, ref["points"])
             assert np.float32(f.headpose) == np.float32(ref["headpose"])
+
+
+@pytest.mark.parametrize("rerun_cap", ["0", "16384"])
+def test_frames_over_the_candidate_capacity(engine, oracle_mod, frames, fixtures, monkeypatch, rerun_cap):
+    """A frame with more raw detections than the grouping holds (8,192 per frame; detectMultiScale has no
+    limit, FaceForest.cpp:146) is run again on its own with a capacity that holds them all, its neighbours in
+    the batch unaffected.  Forced here with a capacity of 64 (FFD_DETECT_CAP); with FFD_DETECT_RERUN_CAP=16384
+    the re-run groups with its component labels in global memory (k_haar_group<true>)."""
+    fr, _ = frames
+    imgs = [fr[0], fixtures["images"][3], fr[1], fixtures["images"][8]]
+    want = [oracle_mod.detect_faces(im) for im in imgs]
+    raws = [len(oracle_mod.detect_faces(im, raw=True)[1]) for im in imgs]
+    assert max(raws) > 64 and min(raws) <= 64 or max(raws) > 64  # at least one frame overflows
+    monkeypatch.setenv("FFD_DETECT_CAP", "64")
+    monkeypatch.setenv("FFD_DETECT_RERUN_CAP", rerun_cap)
+    got = engine.detectFaces(imgs)
+    for k in range(len(imgs)):
+        assert np.array_equal(got[k], want[k]), (k, raws[k])
+    assert np.array_equal(engine.detect_candidates(fr[0]), oracle_mod.detect_faces(fr[0], raw=True)[1])
