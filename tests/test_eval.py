@@ -53,7 +53,7 @@ def test_oracle_fixture_errors_round_trip(oracle_mod, fixtures):
 @pytest.mark.gpu
 def test_engine_eval_cli(tmp_path, capsys):
     out = tmp_path / "errors.txt"
-    assert fe.main(["--out", str(out)]) == 0
+    assert fe.main(["--all", "--out", str(out)]) == 0  # all 20 annotated faces (default: the 10 % test split)
     e = fe.parse_errors(out.read_text())
     assert e.shape == (20, 10)
     r = fe.report(e)

@@ -45,7 +45,7 @@ def summarise_phases(rec, nw_waves):
             "store": float(wk[..., 6][ok].mean())}
 
 
-def summarise(rec, nw_waves, walker_lanes):
+def summarise(rec, nw_waves, walker_lanes, per_lane=1):
     # rec: [wg][iter][slot][8] u32
     wk = rec[:, :, :nw_waves, :].astype(np.float64)
     st = rec[:, :, 8, :].astype(np.float64)
@@ -84,7 +84,7 @@ def summarise(rec, nw_waves, walker_lanes):
                 busy.append(float(rec[g, i, w, 1]))
                 ml = float(rec[g, i, w, 4])
                 steps.append(float(rec[g, i, w, 1]) / max(ml, 1))
-                act.append(float(rec[g, i, w, 2] + rec[g, i, w, 3]) / (64.0 * max(ml, 1)))
+                act.append(float(rec[g, i, w, 2] + rec[g, i, w, 3]) / (64.0 * per_lane * max(ml, 1)))
     per = np.array(per)
     out["block_period_cycles_median"] = float(np.median(per))
     out["block_period_cycles_mean"] = float(per.mean())
@@ -92,7 +92,7 @@ def summarise(rec, nw_waves, walker_lanes):
     out["cycles_per_wave_step_mean"] = float(np.mean(steps))
     out["lane_activity_mean"] = float(np.mean(act))
     out["stager_commit_cycles_mean"] = float(st[..., 1][used].mean())
-    out["cycles_per_visit_per_walker_lane"] = float(walker_lanes * per.mean() / ((vis_top + vis_deep).mean()))
+    out["cycles_per_visit_per_walker_lane"] = float(walker_lanes * per_lane * per.mean() / ((vis_top + vis_deep).mean()))
     return out
 
 
@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--timing", action="store_true", help="FFD_TRAV_STATS=2 build: test / fetch-wait split")
     ap.add_argument("--phases", action="store_true", help="FFD_TRAV_STATS=3 build: walk phases")
+    ap.add_argument("--dual", action="store_true", help="FFD_TRAV_DUAL build: 192 / 256 walker lanes, 2 walks each")
     ap.add_argument("--same-face", action="store_true", help="every face of the batch the same crop (L2-resident trees)")
     args = ap.parse_args()
     import torch
@@ -132,11 +133,13 @@ def main():
     ff.synchronize()
     stages = ff.stage_times()
     res = {"faces": args.faces, "library": ffd.library_path(), "stage_ms": stages}
-    for hp, name, nw in ((1, "headpose", 320), (0, "ffd", 512)):
+    walkers = ((1, "headpose", 192), (0, "ffd", 256)) if args.dual else ((1, "headpose", 320), (0, "ffd", 512))
+    pl = 2 if args.dual else 1
+    for hp, name, nw in walkers:
         buf = np.zeros((256, ITERS, SLOTS, 8), dtype=np.uint32)
         assert L.ffd_trav_stats_read(hp, buf.ctypes.data, buf.nbytes) == 0
         res[name] = (summarise_timing(buf, nw // 64) if args.timing else
-                     summarise_phases(buf, nw // 64) if args.phases else summarise(buf, nw // 64, nw))
+                     summarise_phases(buf, nw // 64) if args.phases else summarise(buf, nw // 64, nw, pl))
     print(json.dumps(res, indent=1))
     if args.out:
         with open(args.out, "w") as f:
