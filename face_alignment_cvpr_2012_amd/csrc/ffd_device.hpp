@@ -45,6 +45,18 @@ constexpr uint32_t LEAF_BIT = 0x80000000u;
 // c0's children is the next record, c1's children are off1 records ahead (off1 = 0: the 32-bit
 // offset is far[pair]).  Each tree starts with a root pair (root, unused leaf).
 // Source fields: ThresholdSplit<SimplePatchFeature> (ThresholdSplit.hpp:51-67, ImageSample.hpp:83-90).
+//
+// FFD_PAIR_BLOCKS (default): the records are laid out in 128-byte blocks of 8 slots holding three pair
+// levels in heap order instead: the children pair of node s of the record in slot j <= 2 is slot 2j + 1 + s
+// of the same block; the children pairs of the nodes of slots 3..6 start new blocks, node s's at record
+// index P + off1 + 8 s (off1 = 0: far[P]; when both are internal the two blocks are adjacent).  A tree's
+// first block holds the root pair in slot 0 (root, unused leaf), so the root's children pair is slot 1.
+// A walk keeps its record's slot j; a miss brings a line that serves the next two steps of the walk
+// (the depth-first layout above serves the next step only after a left turn).
+#ifndef FFD_PAIR_BLOCKS
+#define FFD_PAIR_BLOCKS 0
+#endif
+constexpr uint32_t PAIR_SLOT_SHIFT = 29;  // tree-top pair indices carry the record's block slot in bits 29..31
 
 // Tree tops (k_traverse): per tree, TOP_CAP pair records of its top levels in heap order: entry 0
 // = the root pair, entry 1 = the root's children pair, entry 2h + s (h >= 1) = the children pair of

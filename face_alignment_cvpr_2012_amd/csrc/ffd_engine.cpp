@@ -170,14 +170,58 @@ static void encode_test(const uint4& n, uint32_t& lo, uint32_t& hi) {
 // subtree, then b's children pair at offset off1 (16 bits; 0 = look up far[pair]).  Each tree starts
 // with a root pair (root, unused leaf).  Leaves keep their model ordinals; speed-neutral for parity:
 // every walk visits the same nodes in the same order as Tree<S>::evaluateMT.
+// FFD_PAIR_BLOCKS: the blocked layout of ffd_device.hpp instead (same records, other positions).
 void ffd_host::build_pair_records(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots,
                                   std::vector<uint4>& out, std::vector<int32_t>& roots_out,
                                   std::vector<uint32_t>& far) {
   out.clear();
   roots_out.clear();
   far.clear();
-  auto internal = [&](uint32_t i) { return !(bfs[i].x & LEAF_BIT); };
   const uint4 unused_leaf = make_uint4(LEAF_BIT, 0u, 0u, 0u);
+  auto pack = [](const uint4& a, const uint4& b, uint32_t o16) {
+    uint32_t lo0, hi0, lo1, hi1;
+    encode_test(a, lo0, hi0);
+    encode_test(b, lo1, hi1);
+    return make_uint4(lo0, lo1, hi0 | (o16 & 0xFFu) << 24, hi1 | (o16 >> 8) << 24);
+  };
+  if (FFD_PAIR_BLOCKS) {
+    auto alloc = [&]() {  // one 8-record block
+      const size_t at = out.size();
+      out.resize(at + 8, make_uint4(0, 0, 0, 0));
+      far.resize(at + 8, 0u);
+      return at;
+    };
+    struct Item { size_t base; int slot; uint4 a, b; };
+    std::vector<Item> st;
+    for (int32_t root : roots) {
+      const size_t b0 = alloc();
+      roots_out.push_back((int32_t)b0);
+      st.push_back({b0, 0, bfs[(uint32_t)root], unused_leaf});
+      while (!st.empty()) {  // depth-first over blocks: a block's children blocks follow it closely
+        const Item it = st.back();
+        st.pop_back();
+        const size_t idx = it.base + (size_t)it.slot;
+        const bool ia = !(it.a.x & LEAF_BIT), ib = !(it.b.x & LEAF_BIT);
+        uint32_t o16 = 0;
+        if (it.slot <= 2) {
+          if (ib) st.push_back({it.base, 2 * it.slot + 2, bfs[it.b.x], bfs[it.b.x + 1]});
+          if (ia) st.push_back({it.base, 2 * it.slot + 1, bfs[it.a.x], bfs[it.a.x + 1]});
+        } else if (ia || ib) {
+          const size_t c0 = alloc();  // node a's children block (allocated even when a is a leaf and b is not)
+          if (ib) alloc();            // node b's: the next block
+          const uint64_t off = c0 - idx;
+          if (off > 0xFFFFFFFFull) throw std::runtime_error("pair array too large");
+          o16 = off <= 0xFFFFu ? (uint32_t)off : 0u;
+          if (o16 == 0) far[idx] = (uint32_t)off;
+          if (ib) st.push_back({c0 + 8, 0, bfs[it.b.x], bfs[it.b.x + 1]});
+          if (ia) st.push_back({c0, 0, bfs[it.a.x], bfs[it.a.x + 1]});
+        }
+        out[idx] = pack(it.a, it.b, o16);
+      }
+    }
+    if (out.size() >= ((size_t)1 << PAIR_SLOT_SHIFT)) throw std::runtime_error("pair array too large");
+    return;
+  }
   // iterative DFS: a frame places pair (a, b); phase 0 = a's children, 1 = b's children, 2 = done
   struct Frame { uint4 a, b; size_t idx; int phase; };
   for (int32_t root : roots) {
@@ -201,13 +245,10 @@ void ffd_host::build_pair_records(const std::vector<uint4>& bfs, const std::vect
       if (f.phase == 1) {
         f.phase = 2;
         const uint64_t off1 = out.size() - f.idx;  // where b's children pair goes
-        uint32_t lo0, hi0, lo1, hi1;
-        encode_test(f.a, lo0, hi0);
-        encode_test(f.b, lo1, hi1);
         uint32_t o16 = off1 <= 0xFFFFu ? (uint32_t)off1 : 0u;
         if (o16 == 0 && !(f.b.x & LEAF_BIT)) far[f.idx] = (uint32_t)off1;
         if (off1 > 0xFFFFFFFFull) throw std::runtime_error("pair array too large");
-        out[f.idx] = make_uint4(lo0, lo1, hi0 | (o16 & 0xFFu) << 24, hi1 | (o16 >> 8) << 24);
+        out[f.idx] = pack(f.a, f.b, o16);
         if (!(f.b.x & LEAF_BIT)) {
           const uint32_t c = f.b.x;
           const size_t at = out.size();
@@ -220,7 +261,6 @@ void ffd_host::build_pair_records(const std::vector<uint4>& bfs, const std::vect
       st.pop_back();
     }
   }
-  (void)internal;
   if (out.size() >= 0x80000000ull) throw std::runtime_error("pair array too large");
 }
 
@@ -230,9 +270,10 @@ void ffd_host::build_tree_tops(const std::vector<uint4>& pairs, const std::vecto
   tops.assign(proots.size() * TOP_CAP, make_uint4(0, 0, 0, 0));
   top_idx.assign(proots.size() * TOP_CAP, 0u);
   auto leaf = [](uint32_t lo) { return (lo >> 26) == 63u; };
+  const uint32_t pmask = (1u << PAIR_SLOT_SHIFT) - 1u;
   for (size_t t = 0; t < proots.size(); t++) {
     uint4* rec = &tops[t * TOP_CAP];
-    uint32_t* idx = &top_idx[t * TOP_CAP];
+    uint32_t* idx = &top_idx[t * TOP_CAP];  // pair index | slot << PAIR_SLOT_SHIFT (blocked layout)
     idx[0] = (uint32_t)proots[t];
     rec[0] = pairs[idx[0]];
     std::vector<bool> live(TOP_CAP, false);
@@ -240,14 +281,23 @@ void ffd_host::build_tree_tops(const std::vector<uint4>& pairs, const std::vecto
     for (int h = 0; h < TOP_CAP; h++) {
       if (!live[h]) continue;
       const uint4 R = rec[h];
+      const uint32_t p = idx[h] & pmask, j = idx[h] >> PAIR_SLOT_SHIFT;
       for (uint32_t s = 0; s < (h ? 2u : 1u); s++) {  // the root pair's second slot is an unused leaf
         if (leaf(s ? R.y : R.x)) continue;
         const int h2 = h ? 2 * h + (int)s : 1;
         if (h2 >= TOP_CAP) continue;
         const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
-        const uint32_t q = idx[h] + (s ? (off1 ? off1 : far[idx[h]]) : 1u);
+        uint32_t q, j2 = 0;
+        if (!FFD_PAIR_BLOCKS) {
+          q = p + (s ? (off1 ? off1 : far[p]) : 1u);
+        } else if (j <= 2) {
+          q = p + j + 1 + s;
+          j2 = 2 * j + 1 + s;
+        } else {
+          q = p + (off1 ? off1 : far[p]) + 8 * s;
+        }
         rec[h2] = pairs[q];
-        idx[h2] = q;
+        idx[h2] = q | j2 << PAIR_SLOT_SHIFT;
         live[h2] = true;
       }
     }

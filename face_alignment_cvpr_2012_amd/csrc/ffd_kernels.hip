@@ -955,6 +955,30 @@ __device__ __forceinline__ int rect_mean_lds(const unsigned char* __restrict__ p
   return (int)__builtin_fmaf((float)((uint32_t)top + bot), __builtin_amdgcn_rcpf((float)area), 0.00075f);
 }
 
+// rect_mean_lds split into its reads and its arithmetic, so that a walker can issue one walk's reads
+// and do another walk's arithmetic while they are in flight (k_traverse, FFD_TRAV_DUAL).
+struct RectRd {
+  uint32_t a, b, c, d, f0, f1;
+};
+__device__ __forceinline__ RectRd rect_read_lds(const unsigned char* __restrict__ p, uint32_t w, uint32_t h, uint32_t hh,
+                                               int ld2) {
+  const int wb = (int)(2u * w);
+  const int r1 = (int)__umul24(hh, (unsigned)ld2), r2 = (int)__umul24(h, (unsigned)ld2);
+  RectRd r;
+  r.a = *reinterpret_cast<const uint16_t*>(p);
+  r.b = *reinterpret_cast<const uint16_t*>(p + wb);
+  r.f0 = *reinterpret_cast<const uint16_t*>(p + r2);
+  r.f1 = *reinterpret_cast<const uint16_t*>(p + r2 + wb);
+  r.c = *reinterpret_cast<const uint16_t*>(p + r1);
+  r.d = *reinterpret_cast<const uint16_t*>(p + r1 + wb);
+  return r;
+}
+__device__ __forceinline__ int rect_mean_fin(const RectRd& r, uint32_t w, uint32_t h) {
+  typedef unsigned short u16;
+  const u16 dc = (u16)(r.d - r.c), top = (u16)((u16)(r.a - r.b) + dc), bot = (u16)((u16)(r.f1 - r.f0) - dc);
+  return (int)__builtin_fmaf((float)((uint32_t)top + bot), __builtin_amdgcn_rcpf((float)__umul24(w, h)), 0.00075f);
+}
+
 // Tree<S>::evaluateMT over global u16 planes (ffd_forest_eval_leaves hook).
 __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint32_t node,
                                            const uint16_t* __restrict__ chan, int64_t plane) {
@@ -992,13 +1016,35 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 // about its longest walk chain, so the walks a window holds per block set the throughput: FFD 5x5
 // blocks with 512 walkers took the FFD pass from 10.4 to 8.6 ms at C2 (profiles/r2c).
 constexpr int TRAV_NT = 1024;
-__host__ __device__ constexpr int trav_nw(int GX, int GY, bool HP) { return GX * GY * (HP ? 15 : 20) <= 320 ? 320 : 512; }
+#ifndef FFD_TRAV_DUAL
+#define FFD_TRAV_DUAL 0  // two walks per walker lane, software-pipelined (walk_block2): measured slower (FFD 8.9 -> 12.5 ms)
+#endif
+#ifndef FFD_TRAV_PAIR
+#define FFD_TRAV_PAIR 0  // two walker lanes per walk, one rectangle each: measured slower (FFD 8.5 -> 12.4 ms)
+#endif
+static_assert(!(FFD_PAIR_BLOCKS && (FFD_TRAV_DUAL)), "the dual walker follows the depth-first pair layout");
+#ifndef FFD_TRAV_PK
+#define FFD_TRAV_PK 0  // corners into packed u16 pairs (d16 loads)
+#endif
+__host__ __device__ constexpr int trav_nw(int GX, int GY, bool HP) {
+  return FFD_TRAV_DUAL ? ((GX * GY * (HP ? 15 : 20) + 1) / 2 + 63) / 64 * 64
+                       : (GX * GY * (HP ? 15 : 20) <= 320 ? 320 : 512);
+}
 // Window chunks held in registers per staging thread: 16-byte chunks when the window row pitch is
 // a multiple of 8 columns, else 8-byte chunks (the pitch also sets the LDS bank pattern of the
 // rectangle reads, so it is not padded up).
 template <int CB, int NS> struct TravStage;
 template <int NS> struct TravStage<8, NS> { static constexpr int U = (20480 + NS - 1) / NS; typedef uint32_t T __attribute__((ext_vector_type(2))); };
 template <int NS> struct TravStage<16, NS> { static constexpr int U = (11000 + NS - 1) / NS; typedef uint32_t T __attribute__((ext_vector_type(4))); };
+#ifndef FFD_TRAV_STAGE_ROWS
+#define FFD_TRAV_STAGE_ROWS 1  // staging threads own runs of window rows (affine offsets); 0: chunk i = s + u NS
+#endif
+// Row-run staging (FFD_TRAV_STAGE_ROWS): NS threads over NCH x nq chunk columns, nh row groups per column, RU
+// rows per group (the host checks RU <= TravStage::U, traverse_window_fits)
+__host__ __device__ constexpr int trav_stage_groups(int ns, int nq) { return ns / (NCH * nq); }
+__host__ __device__ constexpr int trav_stage_rows(int ns, int nq, int wh) {
+  return trav_stage_groups(ns, nq) > 0 ? (wh + trav_stage_groups(ns, nq) - 1) / trav_stage_groups(ns, nq) : 1 << 20;
+}
 
 // LDS row pitch (u16) of a traversal window WW columns wide staged from a 4-element aligned column:
 // a block starting at patch x px0 is staged from column px0 & ~3, so a block x-stride (gx * step)
@@ -1022,9 +1068,9 @@ __host__ __device__ __forceinline__ int trav_window_bytes(int WW, int WH, int xs
 // global pair index each (20 B).  TOPN = the largest power of two <= top_max whose T tables fit in
 // the LDS left over by the window (FFD 4x4 window, 20 trees: 64 entries = levels 0..6).
 constexpr int TRAV_TOP_ENTRIES = 1400;  // tree-top entries a block stages at most (2 per staging thread)
-__host__ __device__ __forceinline__ int trav_top_n(int T, int free_bytes, int top_max) {
+__host__ __device__ __forceinline__ int trav_top_n(int T, int free_bytes, int top_max, int cap = TRAV_TOP_ENTRIES) {
   int n = TOP_CAP;
-  while (n > 1 && (n > top_max || T * n * 20 > free_bytes || T * n > TRAV_TOP_ENTRIES)) n >>= 1;
+  while (n > 1 && (n > top_max || T * n * 20 > free_bytes || T * n > cap)) n >>= 1;
   return n;
 }
 
@@ -1051,6 +1097,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 }
 #endif
 
+constexpr int TRAV_BLK_BYTES = 64;  // the block descriptor the stagers hand to the walkers (end of the LDS)
 struct TravArgs {
   const FaceDesc* faces;
   int n_faces, bpf;        // blocks per face: ceil(nx/G) * ceil(ny/G) (max over the batch)
@@ -1063,6 +1110,7 @@ struct TravArgs {
   int ntrees_hp;           // head-pose pass: number of trees
   int step, step_y;        // patch grid steps (x, y)
   int plane;               // channel plane stride (elements), the same for every face of the batch
+  int lds_bytes;           // dynamic LDS of the workgroup
   const uint16_t* chan;
   int32_t* leaf_out;
 };
@@ -1073,6 +1121,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   uint16_t* win = reinterpret_cast<uint16_t*>(smem);
   constexpr int NW = trav_nw(GX, GY, HP), NS = TRAV_NT - NW, U = TravStage<CB, NS>::U, GG = GX * GY;
   typedef typename TravStage<CB, NS>::T chunk_t;
+  // tree-top entries a block stages at most: one per staging thread for the FFD 16-byte-chunk windows (the
+  // 44 x 44 window leaves LDS for 8 levels-0..2 entries per tree; more registers would spill the stager role)
+  constexpr int TOP_E = (!HP && CB == 16) ? NS : (TRAV_TOP_ENTRIES + NS - 1) / NS * NS;
+  constexpr bool ROWS = FFD_TRAV_STAGE_ROWS && !HP && CB == 16;  // row-run staging (below)
   const int tid = threadIdx.x;
   // window: WW integral columns x WH rows (steps may differ per axis: step_y, C4's (2, 1) grid)
   const int step = A.step, stepy = A.step_y, WW = 32 + step * (GX - 1), WH = 32 + stepy * (GY - 1);
@@ -1086,11 +1138,16 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
 
   struct Blk {
     int f, xi0, yi0, px0, py0, nx, ny, T;
-    bool ok;
+    int ok;
+    int out_lo, out_hi;  // element offset of the face's leaf block (FaceDesc hp_off / mp_off)
   };
+  // The block a window holds, computed by the stagers with the window's next fill and handed to the walkers
+  // through LDS at the end of the allocation (TRAV_BLK_BYTES), so the walkers start walking after the barrier
+  // instead of loading the face descriptor and tree count themselves.
+  Blk* blk_lds = reinterpret_cast<Blk*>(smem + A.lds_bytes - TRAV_BLK_BYTES);
   auto block = [&](int lb) {
     Blk B;
-    B.ok = false;
+    B.ok = 0;
     B.f = lb / A.bpf;
     const int b = lb - B.f * A.bpf;
     const FaceDesc& fd = A.faces[B.f];
@@ -1103,9 +1160,12 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     B.py0 = B.yi0 * stepy;
     B.T = 0;
     if (fd.valid && !fd.fint && B.nx > 0 && b < gbx * gby) {  // (float-integral faces: k_walk_fint)
-      B.ok = true;
+      B.ok = 1;
       B.T = HP ? A.ntrees_hp : A.hp_state[B.f].n_trees;
     }
+    const int64_t off = HP ? fd.hp_off : fd.mp_off;
+    B.out_lo = (int)(uint32_t)off;
+    B.out_hi = (int)(off >> 32);
     return B;
   };
 
@@ -1118,13 +1178,19 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory")
 #endif
   auto walk_block = [&](const Blk& B) {
-    const FaceDesc& fd = A.faces[B.f];
     const int items = GG * B.T, sh = B.px0 & 3;
-    int32_t* out = A.leaf_out + (HP ? fd.hp_off : fd.mp_off);
+    int32_t* out = A.leaf_out + (int64_t)(((uint64_t)(uint32_t)B.out_hi << 32) | (uint32_t)B.out_lo);
     const int ld2 = 2 * LW, chs2 = 2 * WH * LW;  // window row / channel-plane strides (bytes)
-    const int topn = trav_top_n(B.T, A.top_free, A.top_max);
+    const int topn = trav_top_n(B.T, A.top_free, A.top_max, TOP_E);
     const uint32_t* top_i = reinterpret_cast<const uint32_t*>(top_rec + B.T * topn);
+#if FFD_TRAV_PAIR
+    // pair walkers: lanes 2k and 2k + 1 walk the same (patch, tree), each reading one of the node's two
+    // rectangles (6 LDS reads per lane and step instead of 12); the means are swapped by a DPP quad permute
+    const int half = tid & 1;
+    for (int item = tid >> 1; item < items; item += NW / 2) {
+#else
     for (int item = tid; item < items; item += NW) {
+#endif
       const int t = item / GG, pl = item - t * GG;
       const int xi = B.xi0 + pl % GX, yi = B.yi0 + pl / GX;
       if (xi >= B.nx || yi >= B.ny) continue;
@@ -1154,6 +1220,43 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         const int q2 = rect9(1, __builtin_amdgcn_ubfe(hi, 10, 5), __builtin_amdgcn_ubfe(hi, 15, 5));
         const int thr9 = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
         return (q1 - q2 + (int)(lo & 31u) - 16) <= thr9 ? 0u : 1u;
+#elif FFD_TRAV_PAIR
+        // this lane's rectangle: fields at bit 0 (rectangle 1) or 10 (rectangle 2) of lo (x, y) and hi (w, h)
+        const unsigned char* cb = base + __umul24(lo >> 26, (unsigned)chs2);
+        const uint32_t f = half ? 10u : 0u;
+        const int pm = rect_mean_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, f + 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, f, 5),
+                                     __builtin_amdgcn_ubfe(hi, f, 5), __builtin_amdgcn_ubfe(hi, f + 5, 5),
+                                     __builtin_amdgcn_ubfe(hi, f + 6, 4), ld2);
+        const int po = __builtin_amdgcn_mov_dpp(pm, 0xB1, 0xF, 0xF, false);  // quad_perm [1, 0, 3, 2]: the partner's mean
+        const int d12 = half ? po - pm : pm - po;                              // p1 - p2 on both lanes
+        const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
+        return d12 <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
+#elif FFD_TRAV_PK
+        // both rectangles' corners loaded into the halves of packed u16 pairs (ds_read_u16_d16 / _d16_hi), the
+        // two halves' sums as packed u16 arithmetic (no repacking of separately loaded corners)
+        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+        const unsigned char* cb = base + __umul24(lo >> 26, (unsigned)chs2);
+        const unsigned char* q1 = cb + __umul24(__builtin_amdgcn_ubfe(lo, 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 0, 5);
+        const unsigned char* q2 = cb + __umul24(__builtin_amdgcn_ubfe(lo, 15, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 10, 5);
+        const uint32_t w1 = __builtin_amdgcn_ubfe(hi, 0, 5), h1 = __builtin_amdgcn_ubfe(hi, 5, 5);
+        const uint32_t w2 = __builtin_amdgcn_ubfe(hi, 10, 5), h2 = __builtin_amdgcn_ubfe(hi, 15, 5);
+        const int wb1 = (int)(2u * w1), wb2 = (int)(2u * w2);
+        const int m1 = (int)__umul24(__builtin_amdgcn_ubfe(hi, 6, 4), (unsigned)ld2), e1 = (int)__umul24(h1, (unsigned)ld2);
+        const int m2 = (int)__umul24(__builtin_amdgcn_ubfe(hi, 16, 4), (unsigned)ld2), e2 = (int)__umul24(h2, (unsigned)ld2);
+        auto ld = [](const unsigned char* p) { return *reinterpret_cast<const unsigned short*>(p); };
+        u16x2 a, b, c, d, e, f;
+        a.x = ld(q1); a.y = ld(q2);
+        b.x = ld(q1 + wb1); b.y = ld(q2 + wb2);
+        e.x = ld(q1 + e1); e.y = ld(q2 + e2);
+        f.x = ld(q1 + e1 + wb1); f.y = ld(q2 + e2 + wb2);
+        c.x = ld(q1 + m1); c.y = ld(q2 + m2);
+        d.x = ld(q1 + m1 + wb1); d.y = ld(q2 + m2 + wb2);
+        const u16x2 dc = d - c, top = (a - b) + dc, bot = (f - e) - dc;
+        const float ra = __builtin_amdgcn_rcpf((float)__umul24(w1, h1)), rb = __builtin_amdgcn_rcpf((float)__umul24(w2, h2));
+        const int p1 = (int)__builtin_fmaf((float)((uint32_t)top.x + bot.x), ra, 0.00075f);
+        const int p2 = (int)__builtin_fmaf((float)((uint32_t)top.y + bot.y), rb, 0.00075f);
+        const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
+        return (p1 - p2) <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
 #else
         // (fields by bit-field extracts; bits of hi above 23 are the record's child offset, never read)
         const unsigned char* cb = base + __umul24(lo >> 26, (unsigned)chs2);
@@ -1195,6 +1298,8 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         hi = s ? R.w : R.z;
       }
       uint32_t P = top_i[t * topn + h];
+      uint32_t j = P >> PAIR_SLOT_SHIFT;  // the record's block slot (FFD_PAIR_BLOCKS)
+      P &= (1u << PAIR_SLOT_SHIFT) - 1u;
 #if FFD_TRAV_STATS == 3
       TRAV_STAMP(ph_b);
       st_ph[1] += (uint32_t)(ph_b - ph_a);
@@ -1206,8 +1311,15 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       while (lo < (63u << 26)) {  // not a leaf (ch = 63)
         // children pair of the current node: right after its pair (child 0), or off1 away (child 1)
         const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
+#if FFD_PAIR_BLOCKS
+        // in-block children pair: slot 2j + 1 + s; from slots 3..6: block off1 (+ 8 for node 1) away
+        uint32_t Q = j <= 2u ? P + j + 1u + s : P + off1 + (s << 3);
+        if (j > 2u && off1 == 0u) Q = P + A.far[P] + (s << 3);
+        j = j <= 2u ? 2u * j + 1u + s : 0u;
+#else
         uint32_t Q = P + (s ? off1 : 1u);
         if (s && off1 == 0u) Q = P + A.far[P];
+#endif
 #if FFD_TRAV_PROBE == 6
         const uint4 N = A.pairs[Q & 4095u];
         if (++probe_depth > 24) break;
@@ -1244,6 +1356,9 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       st_maxdeep = max(st_maxdeep, wd);
       st_walks++;
 #endif
+#if FFD_TRAV_PAIR
+      if (!half)
+#endif
       out[(xi * B.ny + yi) * B.T + t] = (int32_t)((lo & 0xFFFFFu) | hi << 20);  // reference order
 #if FFD_TRAV_STATS == 3
       __builtin_amdgcn_s_waitcnt(0);
@@ -1252,6 +1367,200 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
 #endif
     }
   };
+
+  // Two walks per walker lane (FFD_TRAV_DUAL): items tid and tid + NW.  A step of one walk is a chain
+  // of a 16-byte record fetch (L2) and twelve LDS reads followed by the test's arithmetic; the walker
+  // interleaves the two chains so that one walk's reads are in flight while the other walk's test is
+  // computed (issue A, finish B, issue B, finish A), instead of a wave waiting on its own reads with
+  // every other walker wave queued on the same LDS (tools/trav_stats.py: the window reads' bank
+  // conflicts were ~40 % of a deep step).  Finished and empty walks keep stepping on a dummy state
+  // (channel 0 at the window origin, broadcast reads; record 0) until both walks of every lane of the
+  // wave are done; each walk's leaf is stored once, after the loop.
+#if FFD_TRAV_DUAL
+  auto walk_block2 = [&](const Blk& B) {
+    const int items = GG * B.T, sh = B.px0 & 3;
+    int32_t* out = A.leaf_out + (int64_t)(((uint64_t)(uint32_t)B.out_hi << 32) | (uint32_t)B.out_lo);
+    const int ld2 = 2 * LW, chs2 = 2 * WH * LW;
+    const int topn = trav_top_n(B.T, A.top_free, A.top_max, TOP_E), lgn = __builtin_ctz(topn);
+    const uint32_t* top_i = reinterpret_cast<const uint32_t*>(top_rec + B.T * topn);
+    const unsigned char* w0 = reinterpret_cast<const unsigned char*>(win);
+    constexpr uint32_t LEAF = 63u << 26;  // lo >= LEAF: a leaf (ch = 63)
+    struct Walk {
+      const unsigned char* base;  // the patch's top-left integral corner in channel 0's window plane
+      uint32_t lo, hi;            // the node's test fields (hi[31:24]: the pair's child offset byte)
+      uint32_t P, off1, s;        // its pair record's index, child 1's children-pair offset, sibling
+      uint32_t res;               // the leaf (reference leaf word), once reached
+      int oi, t;                  // output index (reference order; -1: no walk), tree slot
+      bool live;
+    };
+    auto init = [&](int item, Walk& w) {
+      w.base = w0;
+      w.lo = w.hi = w.P = w.off1 = w.s = w.res = 0;
+      w.oi = -1;
+      w.t = 0;
+      w.live = false;
+      if (item < items) {
+        const int t = item / GG, pl = item - t * GG;
+        const int xi = B.xi0 + pl % GX, yi = B.yi0 + pl / GX;
+        if (xi < B.nx && yi < B.ny) {
+          w.base = w0 + 2 * ((yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh);
+          w.oi = (xi * B.ny + yi) * B.T + t;
+          w.t = t;
+          w.live = true;
+        }
+      }
+    };
+    auto reads = [&](const Walk& w, RectRd& r1, RectRd& r2) {
+      const unsigned char* cb = w.base + __umul24(w.lo >> 26, (unsigned)chs2);
+      r1 = rect_read_lds(cb + __umul24(__builtin_amdgcn_ubfe(w.lo, 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(w.lo, 0, 5),
+                         __builtin_amdgcn_ubfe(w.hi, 0, 5), __builtin_amdgcn_ubfe(w.hi, 5, 5), __builtin_amdgcn_ubfe(w.hi, 6, 4), ld2);
+      r2 = rect_read_lds(cb + __umul24(__builtin_amdgcn_ubfe(w.lo, 15, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(w.lo, 10, 5),
+                         __builtin_amdgcn_ubfe(w.hi, 10, 5), __builtin_amdgcn_ubfe(w.hi, 15, 5), __builtin_amdgcn_ubfe(w.hi, 16, 4), ld2);
+    };
+    auto decide = [&](const Walk& w, const RectRd& r1, const RectRd& r2) -> uint32_t {
+      const int p1 = rect_mean_fin(r1, __builtin_amdgcn_ubfe(w.hi, 0, 5), __builtin_amdgcn_ubfe(w.hi, 5, 5));
+      const int p2 = rect_mean_fin(r2, __builtin_amdgcn_ubfe(w.hi, 10, 5), __builtin_amdgcn_ubfe(w.hi, 15, 5));
+      const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)w.hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(w.lo, 20, 6));
+      return (p1 - p2) <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
+    };
+    // a walk stands on a node: record R (its pair), s (which sibling); take that node's fields
+    auto stand = [&](Walk& w, const uint4& R, uint32_t s) {
+      w.s = s;
+      w.lo = s ? R.y : R.x;
+      w.hi = s ? R.w : R.z;
+      w.off1 = (R.z >> 24) | ((R.w >> 24) << 8);
+    };
+    // a walk that reached a leaf keeps its word and steps on the dummy state from then on
+    auto settle = [&](Walk& w) {
+      if (w.live && w.lo >= LEAF) {
+        w.res = (w.lo & 0xFFFFFu) | w.hi << 20;
+        w.live = false;
+      }
+      if (!w.live) {
+        w.base = w0;
+        w.lo = w.hi = w.s = w.off1 = w.P = 0;
+      }
+    };
+    // children pair of the node a walk stands on: right after its pair (child 0), or off1 away (child 1)
+    // (the far lookup is entered by whole waves and its result used inside: a load that may or may not have
+    // been issued before the join would make the record fetch wait for the other walk's fetch, vmcnt(0))
+    auto next_q = [&](const Walk& w) -> uint32_t {
+      uint32_t Q = w.P + (w.s ? w.off1 : 1u);
+      const bool fq = w.live && w.s && w.off1 == 0u;
+      if (__builtin_amdgcn_ballot_w64(fq)) {
+        const uint32_t fo = A.far[w.P];     // (far has an entry per pair; P of a finished walk is 0)
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), here rather than after the join
+        Q = fq ? w.P + fo : Q;
+      }
+      return w.live ? Q : 0u;
+    };
+    auto run = [&](int i0) {
+      Walk a, b;
+      init(i0 + tid, a);
+      init(i0 + tid + NW, b);
+#if FFD_TRAV_STATS
+      uint32_t la = 0, lb2 = 0, it = 0;  // visits of a / b, deep iterations
+#endif
+#if FFD_TRAV_STATS == 3
+      TRAV_STAMP(ph_a);
+      st_ph[0] += (uint32_t)(ph_a - st_t0);
+#endif
+      // levels 0..lgn-1: heap-ordered pair records in LDS (children pair of node (h, s): entry 2h + s, of the root 1)
+      {
+        const uint4* ra = top_rec + a.t * topn;
+        const uint4* rb = top_rec + b.t * topn;
+        uint32_t ha = 0, hb = 0;
+        stand(a, ra[0], 0);
+        stand(b, rb[0], 0);
+        settle(a);
+        settle(b);
+        for (int lv = 0; lv < lgn; lv++) {
+          const uint32_t h2a = ha ? 2u * ha + a.s : 1u, h2b = hb ? 2u * hb + b.s : 1u;
+          const uint4 Na = ra[a.live ? h2a : 0u], Nb = rb[b.live ? h2b : 0u];
+          RectRd a1, a2, b1, b2;
+          reads(a, a1, a2);
+          reads(b, b1, b2);
+          const uint32_t sa = decide(a, a1, a2), sb = decide(b, b1, b2);
+          if (a.live) {
+            ha = h2a;
+            stand(a, Na, sa);
+          }
+          if (b.live) {
+            hb = h2b;
+            stand(b, Nb, sb);
+          }
+          settle(a);
+          settle(b);
+        }
+        a.P = a.live ? top_i[a.t * topn + ha] : 0u;
+        b.P = b.live ? top_i[b.t * topn + hb] : 0u;
+#if FFD_TRAV_STATS
+        // (top visits: a walk that is live after the top levels made all lgn of them)
+        la = a.live ? lgn : 0;
+        lb2 = b.live ? lgn : 0;
+        st_top += la + lb2;
+#endif
+      }
+#if FFD_TRAV_STATS == 3
+      TRAV_STAMP(ph_b);
+      st_ph[1] += (uint32_t)(ph_b - ph_a);
+#endif
+      // deeper levels: pair records from L2; issue a, finish b, issue b, finish a
+      RectRd b1, b2;
+      uint32_t Qb = next_q(b);
+      uint4 Nb = A.pairs[Qb];
+      reads(b, b1, b2);
+      while (__builtin_amdgcn_ballot_w64(a.live || b.live)) {
+        const uint32_t Qa = next_q(a);
+        const uint4 Na = A.pairs[Qa];
+        RectRd a1, a2;
+        reads(a, a1, a2);
+#if FFD_TRAV_STATS
+        it++;
+        la += a.live;
+        lb2 += b.live;
+        st_deep += (uint32_t)a.live + (uint32_t)b.live;
+#endif
+        {
+          const uint32_t sb = decide(b, b1, b2);
+          if (b.live) {
+            b.P = Qb;
+            stand(b, Nb, sb);
+          }
+          settle(b);
+        }
+        Qb = next_q(b);
+        Nb = A.pairs[Qb];
+        reads(b, b1, b2);
+        {
+          const uint32_t sa = decide(a, a1, a2);
+          if (a.live) {
+            a.P = Qa;
+            stand(a, Na, sa);
+          }
+          settle(a);
+        }
+      }
+#if FFD_TRAV_STATS == 3
+      TRAV_STAMP(ph_c);
+      st_ph[2] += (uint32_t)(ph_c - ph_b);
+#endif
+      if (a.oi >= 0) out[a.oi] = (int32_t)a.res;
+      if (b.oi >= 0) out[b.oi] = (int32_t)b.res;
+#if FFD_TRAV_STATS
+      st_max = max(st_max, max(la, lb2));
+      st_maxdeep = max(st_maxdeep, it);
+      st_walks += (uint32_t)(a.oi >= 0) + (uint32_t)(b.oi >= 0);
+#endif
+#if FFD_TRAV_STATS == 3
+      __builtin_amdgcn_s_waitcnt(0);
+      TRAV_STAMP(ph_d);
+      st_ph[3] += (uint32_t)(ph_d - ph_c);
+#endif
+    };
+    for (int i0 = 0; i0 < items; i0 += 2 * NW) run(i0);
+  };
+#endif
 
   // Stager waves and walker waves run separate loops with the same barrier sequence per block
   // (waves are wholly one role), so the staging registers are live only in the stager loop and
@@ -1266,21 +1575,27 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     chunk_t st[U];
     // tree tops of the next block (entry e = j + u * NS of its T x TOPN tables), reloaded only when
     // the face (and so the tree set) changes
-    constexpr int TU = (TRAV_TOP_ENTRIES + NS - 1) / NS;
+    constexpr int TU = TOP_E / NS;
     typedef uint32_t rec_t __attribute__((ext_vector_type(4)));  // (a uint4 array lands in scratch)
     rec_t top_nd[TU];
     uint32_t top_p[TU];
     int top_face = -1;  // face whose tops the LDS holds after the next commit
     bool top_new = false;
-    // chunk (c, r, q) of this thread's first chunk and the (c, r, q) step between its chunks: the source
-    // offsets are rebuilt per block from these six registers (an array of U offsets made the stager
-    // role spill at U = 22)
-    const int s0 = tid - NW;
+    // Row runs (ROWS): staging thread s owns chunk column q of channel c over RU consecutive window rows
+    // [g RU, g RU + RU) (g < nh row groups): its source offsets (rows PITCH * 2 bytes apart) and LDS
+    // offsets (rows 2 LW bytes apart) are affine in the slot u, so both fold into instruction offsets
+    // and no per-slot offset registers are held (the offset array spilled the FFD stager role: 80 B of
+    // scratch per lane; FFD 8.91 -> 8.54 ms).  Used by the FFD 16-byte-chunk windows (5 x 5 at step 3); the
+    // head-pose pass (no spill) keeps chunk i = s + u NS: row runs measured slower there (4.38 -> 4.62 ms).
+    const int s0 = tid - NW, nh = trav_stage_groups(NS, nq), RU = trav_stage_rows(NS, nq, WH);
+    const int sc = s0 / (nq * nh), sg = (s0 / nq) % nh, sq = s0 % nq;
+    const int r_lo = sg * RU, r_n = sc < NCH ? max(0, min(RU, WH - r_lo)) : 0;  // this thread's rows
+    // (chunk index form) chunk (c, r, q) of this thread's first chunk and the (c, r, q) step between its chunks
     const int dq = NS % nq, dr = (NS / nq) % WH, dc = NS / (nq * WH);
     const int q0 = s0 % nq, r0 = (s0 / nq) % WH, c0 = s0 / (nq * WH);
-#if FFD_TRAV_VOFF_ARRAY  // round-2 form: the U offsets precomputed once (spills the stager role at U = 22)
-    int voffs[U];
-    {
+#if FFD_TRAV_VOFF_ARRAY  // round-2 form: the U offsets precomputed once
+    int voffs[ROWS ? 1 : U];
+    if constexpr (!ROWS) {
       int q = q0, r = r0, c = c0;
 #pragma unroll
       for (int u = 0; u < U; u++) {
@@ -1310,7 +1625,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       top_new = B.f != top_face;
       if (top_new) {
         top_face = B.f;
-        const int topn = trav_top_n(B.T, A.top_free, A.top_max), lg = __builtin_ctz(topn);
+        const int topn = trav_top_n(B.T, A.top_free, A.top_max, TOP_E), lg = __builtin_ctz(topn);
 #pragma unroll
         for (int u = 0; u < TU; u++) {
           const int e = tid - NW + u * NS;
@@ -1327,6 +1642,16 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         }
       }
 #if !FFD_TRAV_NOSTAGE
+      if constexpr (ROWS) {
+        const int vb = min(sc, NCH - 1) * A.plane * 2 + r_lo * (PITCH * 2) + sq * CB;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          if (u < r_n) {
+            if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, vb + u * (PITCH * 2), base_b, 0);
+            else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, vb + u * (PITCH * 2), base_b, 0);
+          }
+        }
+      } else {
 #if FFD_TRAV_VOFF_ARRAY
 #pragma unroll
       for (int u = 0; u < U; u++) {
@@ -1351,14 +1676,16 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         c += dc + cr;
       }
 #endif
+      }
 #endif
     };
     auto commit = [&](const Blk& B) {
+      if (tid == NW) *blk_lds = B;  // the walkers' block (read after the barrier)
       if (!B.ok) return;
       chunk_t* dst = reinterpret_cast<chunk_t*>(win);
       const int s = tid - NW;
       if (top_new) {
-        const int n = B.T * trav_top_n(B.T, A.top_free, A.top_max);
+        const int n = B.T * trav_top_n(B.T, A.top_free, A.top_max, TOP_E);
         uint32_t* top_i = reinterpret_cast<uint32_t*>(top_rec + n);
 #pragma unroll
         for (int u = 0; u < TU; u++) {
@@ -1369,9 +1696,16 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         }
       }
 #if !FFD_TRAV_NOSTAGE  // the walk-only probes keep the tree tops (walks need valid records)
+      if constexpr (ROWS) {
+        unsigned char* db = smem + ((sc * WH + r_lo) * nq + sq) * CB;
 #pragma unroll
-      for (int u = 0; u < U; u++)
-        if (u * NS + s < total) dst[u * NS + s] = st[u];
+        for (int u = 0; u < U; u++)
+          if (u < r_n) *reinterpret_cast<chunk_t*>(db + u * (2 * LW)) = st[u];
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          if (u * NS + s < total) dst[u * NS + s] = st[u];
+      }
 #endif
     };
 
@@ -1415,8 +1749,14 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       st_t0 = t0;
 #endif
 #if FFD_TRAV_PROBE != 1
-      const Blk cur = block(lb);
+      Blk cur = *blk_lds;
+      cur.ok = __builtin_amdgcn_readfirstlane(cur.ok);
+      cur.T = __builtin_amdgcn_readfirstlane(cur.T);
+#if FFD_TRAV_DUAL
+      if (cur.ok) walk_block2(cur);
+#else
       if (cur.ok) walk_block(cur);
+#endif
 #endif
 #if FFD_TRAV_STATS
 #if FFD_TRAV_STATS == 2  // per wave: test cycles and fetch-wait cycles summed over its deep steps
@@ -2783,15 +3123,16 @@ void launch_integral(const FaceDesc* faces, int n, int max_h, const uint8_t* gra
 
 int traverse_lds_bytes(TravShape g, int step, int step_y) {
   const int WW = 32 + step * (g.gx - 1), WH = 32 + step_y * (g.gy - 1);
-  return trav_window_bytes(WW, WH, g.gx * step) + MAX_TREES * 20;  // window + at least the block's root pairs
+  return trav_window_bytes(WW, WH, g.gx * step) + MAX_TREES * 20 + TRAV_BLK_BYTES;  // window + the block's root pairs + its descriptor
 }
 
 bool traverse_window_fits(TravShape g, bool hp, int step, int step_y, int lds_cap) {
   const int WW = 32 + step * (g.gx - 1), WH = 32 + step_y * (g.gy - 1);
   const int cb = trav_chunk_bytes(WW, g.gx * step);
   const int ns = TRAV_NT - trav_nw(g.gx, g.gy, hp);
-  const int u = ns == TRAV_NT - 512 ? (cb == 16 ? TravStage<16, TRAV_NT - 512>::U : TravStage<8, TRAV_NT - 512>::U)
-                                    : (cb == 16 ? TravStage<16, TRAV_NT - 320>::U : TravStage<8, TRAV_NT - 320>::U);
+  const int u = cb == 16 ? (11000 + ns - 1) / ns : (20480 + ns - 1) / ns;  // TravStage<cb, ns>::U
+  if (FFD_TRAV_STAGE_ROWS && !hp && cb == 16 && trav_stage_rows(ns, trav_row_pitch(WW, g.gx * step) * 2 / cb, WH) > u)
+    return false;
   return traverse_lds_bytes(g, step, step_y) <= lds_cap && NCH * WH * (trav_row_pitch(WW, g.gx * step) * 2 / cb) <= ns * u;
 }
 
@@ -2815,8 +3156,8 @@ void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, TravShape g
   if (total_blocks <= 0) return;
   // the window, then as many tree-top entries as the rest of the CU's LDS holds
   const int WW = 32 + step * (g.gx - 1), WH = 32 + step_y * (g.gy - 1), lds = lds_cap;
-  TravArgs A{faces, n, bpf, pairs, tops, top_idx, lds - trav_window_bytes(WW, WH, g.gx * step), top_max, far, state,
-             ntrees_hp, step, step_y, (int)plane, chan, leaf_out};
+  TravArgs A{faces, n, bpf, pairs, tops, top_idx, lds - trav_window_bytes(WW, WH, g.gx * step) - TRAV_BLK_BYTES, top_max,
+             far, state, ntrees_hp, step, step_y, (int)plane, lds, chan, leaf_out};
   const int grid = std::max(8, n_wg & ~7);
   const bool c16 = trav_chunk_bytes(WW, g.gx * step) == 16;
 #define FFD_TRAV_LAUNCH(HPV, GXV, GYV)                                                    \

@@ -121,3 +121,23 @@ def test_c5_bench_frame_all_faces(engine, oracle_mod):
         ref, _ = oracle_mod.analyze_face(crops[i], (0, 0, CROP, CROP), threads=8)
         np.testing.assert_array_equal(faces[i].ffd_cordinates, ref["points"], err_msg=f"face {i}")
         assert np.float32(faces[i].headpose).tobytes() == np.float32(ref["headpose"]).tobytes(), i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk,count", [(16, 4096), (1, 256)])
+def test_c2_small_batch_kernels_every_face(c2, chunk, count):
+    """The small-batch kernels (k_meanshift5 / k_hp_pose1 with their ds_read_b128 component-major serial sums,
+    k_votes_wg, the banded Gabor instances) on the C2 crops, in chunks of `chunk` faces, against the same
+    goldens: the face-major k_meanshift variant's mismatches (DESIGN §5 tried-table) do not occur in them."""
+    import face_alignment_cvpr_2012_amd as ffd
+    crops, g = c2
+    with ffd.FaceForest(ffd.FaceForestOptions(max_chunk_faces=chunk)) as ff:
+        faces = []
+        for lo in range(0, count, 256):
+            faces += ff.analyzeFaces(list(crops[lo:lo + 256]), [(0, 0, CROP, CROP)] * len(crops[lo:lo + 256]))
+    pts = np.stack([f.ffd_cordinates for f in faces]).astype(np.int16)
+    hp = np.array([f.headpose for f in faces], np.float32)
+    var = np.array([f.pose_variance for f in faces], np.float32)
+    nt = np.array([f.n_trees for f in faces], np.int32)
+    _compare(pts, hp, var, nt, {k: v[:count] for k, v in g.items() if k in ("points", "headpose", "pose_variance",
+                                                                            "n_trees")}, f"chunks of {chunk}")
