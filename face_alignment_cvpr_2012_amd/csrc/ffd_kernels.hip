@@ -1023,6 +1023,9 @@ constexpr int TRAV_NT = 1024;
 #define FFD_TRAV_PAIR 0  // two walker lanes per walk, one rectangle each: measured slower (FFD 8.5 -> 12.4 ms)
 #endif
 static_assert(!(FFD_PAIR_BLOCKS && (FFD_TRAV_DUAL)), "the dual walker follows the depth-first pair layout");
+#ifndef FFD_TRAV_SPLIT_RECTS
+#define FFD_TRAV_SPLIT_RECTS 0  // scheduling barrier between the two rectangles' reads
+#endif
 #ifndef FFD_TRAV_PK
 #define FFD_TRAV_PK 0  // corners into packed u16 pairs (d16 loads)
 #endif
@@ -1260,6 +1263,17 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
 #else
         // (fields by bit-field extracts; bits of hi above 23 are the record's child offset, never read)
         const unsigned char* cb = base + __umul24(lo >> 26, (unsigned)chs2);
+#if FFD_TRAV_SPLIT_RECTS  // rectangle 1's reads issued before rectangle 2's addresses are computed
+        const uint32_t w1 = __builtin_amdgcn_ubfe(hi, 0, 5), h1 = __builtin_amdgcn_ubfe(hi, 5, 5);
+        const RectRd r1 = rect_read_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 0, 5),
+                                        w1, h1, __builtin_amdgcn_ubfe(hi, 6, 4), ld2);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t w2 = __builtin_amdgcn_ubfe(hi, 10, 5), h2 = __builtin_amdgcn_ubfe(hi, 15, 5);
+        const RectRd r2 = rect_read_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 15, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 10, 5),
+                                        w2, h2, __builtin_amdgcn_ubfe(hi, 16, 4), ld2);
+        __builtin_amdgcn_sched_barrier(0);
+        const int p1 = rect_mean_fin(r1, w1, h1), p2 = rect_mean_fin(r2, w2, h2);
+#else
         const int p1 = rect_mean_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 0, 5),
                                      __builtin_amdgcn_ubfe(hi, 0, 5), __builtin_amdgcn_ubfe(hi, 5, 5),
                                      __builtin_amdgcn_ubfe(hi, 6, 4), ld2);
@@ -1269,6 +1283,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         const int p2 = rect_mean_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 15, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 10, 5),
                                      __builtin_amdgcn_ubfe(hi, 10, 5), __builtin_amdgcn_ubfe(hi, 15, 5),
                                      __builtin_amdgcn_ubfe(hi, 16, 4), ld2);
+#endif
 #endif
         // 10-bit two's complement: sign-extended thr[9:6] (hi[23:20]) above thr[5:0] (lo[25:20])
         const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
