@@ -111,8 +111,8 @@ def stage_work(stage, n_faces, W=125, H=125, n_hp=576, n_mp=1024, trees=20):
         return n_faces * (chan_bytes + n_hp * 15 * 4) / 1e9, "GB/s", "hbm"
     if stage == "ffd_traverse":
         return n_faces * (chan_bytes + n_mp * trees * 4) / 1e9, "GB/s", "hbm"
-    if stage == "votes":
-        return n_faces * (n_mp * trees * 4 + 1700 * 10 * 8) / 1e9, "GB/s", "hbm"
+    if stage == "votes":  # leaf ids in, each (patch, tree) leaf's 32-B vote record gathered, votes out
+        return n_faces * (n_mp * trees * (4 + 32) + 1700 * 10 * 8) / 1e9, "GB/s", "hbm"
     if stage == "meanshift":
         return n_faces * (1700 * 10 * 8 + 112) / 1e9, "GB/s", "hbm"
     if stage == "gray_resize":

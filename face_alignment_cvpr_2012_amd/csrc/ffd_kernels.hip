@@ -1246,6 +1246,26 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         const int wb1 = (int)(2u * w1), wb2 = (int)(2u * w2);
         const int m1 = (int)__umul24(__builtin_amdgcn_ubfe(hi, 6, 4), (unsigned)ld2), e1 = (int)__umul24(h1, (unsigned)ld2);
         const int m2 = (int)__umul24(__builtin_amdgcn_ubfe(hi, 16, 4), (unsigned)ld2), e2 = (int)__umul24(h2, (unsigned)ld2);
+#if FFD_TRAV_PK == 2
+        // rectangle 1's corner into the low half (ds_read_u16), rectangle 2's into the high half of the same
+        // register (ds_read_u16_d16_hi, LDS returns in order); the wait is explicit and name the six registers, so nothing that
+        // reads them is scheduled before the data has arrived
+        auto a32 = [](const unsigned char* p) { return (uint32_t)(uintptr_t)p; };
+        uint32_t ra, rb, rc, rd, re, rf;
+#define FFD_D16(R, P1, P2)                                                  \
+  asm volatile("ds_read_u16 %0, %1" : "=v"(R) : "v"(a32(P1)) : "memory"); \
+  asm volatile("ds_read_u16_d16_hi %0, %1" : "+v"(R) : "v"(a32(P2)) : "memory")
+        FFD_D16(ra, q1, q2);
+        FFD_D16(rb, q1 + wb1, q2 + wb2);
+        FFD_D16(re, q1 + e1, q2 + e2);
+        FFD_D16(rf, q1 + e1 + wb1, q2 + e2 + wb2);
+        FFD_D16(rc, q1 + m1, q2 + m2);
+        FFD_D16(rd, q1 + m1 + wb1, q2 + m2 + wb2);
+#undef FFD_D16
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ra), "+v"(rb), "+v"(rc), "+v"(rd), "+v"(re), "+v"(rf) : : "memory");
+        const u16x2 a = __builtin_bit_cast(u16x2, ra), b = __builtin_bit_cast(u16x2, rb), c = __builtin_bit_cast(u16x2, rc),
+                    d = __builtin_bit_cast(u16x2, rd), e = __builtin_bit_cast(u16x2, re), f = __builtin_bit_cast(u16x2, rf);
+#else
         auto ld = [](const unsigned char* p) { return *reinterpret_cast<const unsigned short*>(p); };
         u16x2 a, b, c, d, e, f;
         a.x = ld(q1); a.y = ld(q2);
@@ -1254,10 +1274,11 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         f.x = ld(q1 + e1 + wb1); f.y = ld(q2 + e2 + wb2);
         c.x = ld(q1 + m1); c.y = ld(q2 + m2);
         d.x = ld(q1 + m1 + wb1); d.y = ld(q2 + m2 + wb2);
+#endif
         const u16x2 dc = d - c, top = (a - b) + dc, bot = (f - e) - dc;
-        const float ra = __builtin_amdgcn_rcpf((float)__umul24(w1, h1)), rb = __builtin_amdgcn_rcpf((float)__umul24(w2, h2));
-        const int p1 = (int)__builtin_fmaf((float)((uint32_t)top.x + bot.x), ra, 0.00075f);
-        const int p2 = (int)__builtin_fmaf((float)((uint32_t)top.y + bot.y), rb, 0.00075f);
+        const float i1 = __builtin_amdgcn_rcpf((float)__umul24(w1, h1)), i2 = __builtin_amdgcn_rcpf((float)__umul24(w2, h2));
+        const int p1 = (int)__builtin_fmaf((float)((uint32_t)top.x + bot.x), i1, 0.00075f);
+        const int p2 = (int)__builtin_fmaf((float)((uint32_t)top.y + bot.y), i2, 0.00075f);
         const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
         return (p1 - p2) <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
 #else
