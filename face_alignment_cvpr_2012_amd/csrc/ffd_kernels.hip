@@ -1334,8 +1334,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         hi = s ? R.w : R.z;
       }
       uint32_t P = top_i[t * topn + h];
-      uint32_t j = P >> PAIR_SLOT_SHIFT;  // the record's block slot (FFD_PAIR_BLOCKS)
+#if FFD_PAIR_BLOCKS
+      uint32_t j = P >> PAIR_SLOT_SHIFT;  // the record's block slot
       P &= (1u << PAIR_SLOT_SHIFT) - 1u;
+#endif
 #if FFD_TRAV_STATS == 3
       TRAV_STAMP(ph_b);
       st_ph[1] += (uint32_t)(ph_b - ph_a);
