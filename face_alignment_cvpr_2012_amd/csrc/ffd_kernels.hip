@@ -1022,7 +1022,9 @@ constexpr int TRAV_NT = 1024;
 #ifndef FFD_TRAV_PAIR
 #define FFD_TRAV_PAIR 0  // two walker lanes per walk, one rectangle each: measured slower (FFD 8.5 -> 12.4 ms)
 #endif
-static_assert(!(FFD_PAIR_BLOCKS && (FFD_TRAV_DUAL)), "the dual walker follows the depth-first pair layout");
+#if FFD_PAIR_BLOCKS && FFD_TRAV_DUAL
+#error "the dual walker follows the depth-first pair layout"
+#endif
 #ifndef FFD_TRAV_SPLIT_RECTS
 #define FFD_TRAV_SPLIT_RECTS 0  // scheduling barrier between the two rectangles' reads
 #endif
