@@ -207,8 +207,17 @@ void ffd_host::build_pair_records(const std::vector<uint4>& bfs, const std::vect
           if (ib) st.push_back({it.base, 2 * it.slot + 2, bfs[it.b.x], bfs[it.b.x + 1]});
           if (ia) st.push_back({it.base, 2 * it.slot + 1, bfs[it.a.x], bfs[it.a.x + 1]});
         } else if (ia || ib) {
-          const size_t c0 = alloc();  // node a's children block (allocated even when a is a leaf and b is not)
-          if (ib) alloc();            // node b's: the next block
+          // node a's children block at idx + off, node b's at idx + off + 8: both allocated when both are
+          // internal; for b alone, off points one block before b's (a block is allocated first only when
+          // that would not leave off >= 1)
+          size_t c0;
+          if (ia) {
+            c0 = alloc();
+            if (ib) alloc();
+          } else {
+            if (out.size() < idx + 9) alloc();
+            c0 = alloc() - 8;
+          }
           const uint64_t off = c0 - idx;
           if (off > 0xFFFFFFFFull) throw std::runtime_error("pair array too large");
           o16 = off <= 0xFFFFu ? (uint32_t)off : 0u;

@@ -1,0 +1,150 @@
+// pair_layout_check.cpp — CPU check of the traversal's pair-record layouts (csrc/ffd_engine.cpp
+// ffd_host::build_pair_records / build_tree_tops, ffd_device.hpp "pair records"): random breadth-first trees
+// (one complete tree deep enough that child offsets exceed 16 bits and take the far table) are re-encoded by
+// the library, then walked the way k_traverse walks them (heap-ordered tops for the first LG levels, then the
+// pair records with the layout's child rule) and the breadth-first way, with the same node decisions; every walk
+// must reach the same leaf.  No device is used.
+//
+// usage: pair_layout_check BLOCKED(0|1) [TOP_LEVELS]   (BLOCKED must match the library's FFD_PAIR_BLOCKS)
+// build: hipcc -O2 -std=c++17 -Iface_alignment_cvpr_2012_amd/csrc -Iinclude tools/pair_layout_check.cpp -Lface_alignment_cvpr_2012_amd/lib -lffd
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+namespace ffd_host {
+void build_pair_records(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots, std::vector<uint4>& out,
+                        std::vector<int32_t>& roots_out, std::vector<uint32_t>& far);
+void build_tree_tops(const std::vector<uint4>& pairs, const std::vector<int32_t>& proots,
+                     const std::vector<uint32_t>& far, std::vector<uint4>& tops, std::vector<uint32_t>& top_idx);
+}  // namespace ffd_host
+
+static constexpr uint32_t LEAF_BIT = 0x80000000u;
+static constexpr int TOP_CAP = 64, PITCH = 128;
+static constexpr uint32_t SLOT_SHIFT = 29;
+
+// the record fields of a split node (ffd_device.hpp), for the walk decisions
+static void fields(const uint4& n, uint32_t& lo, uint32_t& hi) {
+  if (n.x & LEAF_BIT) {
+    const uint32_t ord = n.x & ~LEAF_BIT;
+    lo = (ord & 0xFFFFFu) | 63u << 26;
+    hi = ord >> 20;
+    return;
+  }
+  const uint32_t ch = n.y & 63u, w1 = (n.y >> 6) & 31u, h1 = (n.y >> 11) & 31u, w2 = (n.y >> 16) & 31u, h2 = (n.y >> 21) & 31u;
+  const uint32_t e1 = n.w & 0xFFFFu, e2 = n.w >> 16;
+  const uint32_t t = (uint32_t)(int)n.z & 0x3FFu;
+  lo = e1 % PITCH | (e1 / PITCH) << 5 | (e2 % PITCH) << 10 | (e2 / PITCH) << 15 | (t & 63u) << 20 | ch << 26;
+  hi = w1 | h1 << 5 | w2 << 10 | h2 << 15 | (t >> 6) << 20;
+}
+static uint32_t decide(uint32_t lo, uint32_t hi, uint32_t walk) {
+  uint64_t x = ((uint64_t)lo << 32 | (hi & 0xFFFFFFu)) ^ (0x9E3779B97F4A7C15ull * (walk + 1));
+  x ^= x >> 33;
+  x *= 0xFF51AFD7ED558CCDull;
+  x ^= x >> 33;
+  return (uint32_t)(x & 1u);
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) return 2;
+  const bool blocked = std::atoi(argv[1]) != 0;
+  const int lg = argc > 2 ? std::atoi(argv[2]) : 3;  // LDS top levels (topn = 2^lg)
+  std::mt19937 rng(7);
+  std::vector<uint4> bfs;
+  std::vector<int32_t> roots;
+  uint32_t ordinal = 0;
+  auto split = [&]() {
+    const uint32_t ch = rng() % 38, w1 = 1 + rng() % 22, h1 = 1 + rng() % 22, w2 = 1 + rng() % 22, h2 = 1 + rng() % 22;
+    const uint32_t x1 = rng() % 30, y1 = rng() % 30, x2 = rng() % 30, y2 = rng() % 30;
+    const int thr = (int)(rng() % 480) - 240;
+    return make_uint4(0, ch | w1 << 6 | h1 << 11 | w2 << 16 | h2 << 21, (uint32_t)thr, (y1 * PITCH + x1) | (y2 * PITCH + x2) << 16);
+  };
+  // trees: random shapes (leaf probability growing with depth) and one complete tree of depth 18
+  for (int t = 0; t < 24; t++) {
+    const bool full = t == 5;
+    roots.push_back((int32_t)bfs.size());
+    std::vector<std::pair<uint32_t, int>> level{{(uint32_t)bfs.size(), 0}};
+    bfs.push_back(uint4{});
+    while (!level.empty()) {
+      std::vector<std::pair<uint32_t, int>> next;
+      for (auto [i, d] : level) {
+        const bool leaf = full ? d >= 18 : (d >= 21 || (d >= 2 && rng() % 100 < (uint32_t)(d * 5)));
+        if (leaf) {
+          bfs[i] = make_uint4(LEAF_BIT | ordinal++, 0, 0, 0);
+          continue;
+        }
+        uint4 n = split();
+        n.x = (uint32_t)bfs.size();
+        bfs[i] = n;
+        bfs.push_back(uint4{});
+        bfs.push_back(uint4{});
+        next.push_back({n.x, d + 1});
+        next.push_back({n.x + 1, d + 1});
+      }
+      level.swap(next);
+    }
+  }
+  std::vector<uint4> pairs, tops;
+  std::vector<int32_t> proots;
+  std::vector<uint32_t> far, topi;
+  ffd_host::build_pair_records(bfs, roots, pairs, proots, far);
+  ffd_host::build_tree_tops(pairs, proots, far, tops, topi);
+  const int topn = 1 << lg;
+  long walks = 0, bad = 0, far_used = 0;
+  for (size_t t = 0; t < roots.size(); t++) {
+    for (uint32_t wk = 0; wk < 4000; wk++, walks++) {
+      // breadth-first walk
+      uint32_t node = (uint32_t)roots[t];
+      while (!(bfs[node].x & LEAF_BIT)) {
+        uint32_t lo, hi;
+        fields(bfs[node], lo, hi);
+        node = bfs[node].x + decide(lo, hi, wk);
+      }
+      const uint32_t want = bfs[node].x & ~LEAF_BIT;
+      // k_traverse's walk: LDS tops (heap), then pair records
+      const uint4* trec = &tops[t * TOP_CAP];
+      uint32_t h = 0, s = 0;
+      uint4 R = trec[0];
+      uint32_t lo = R.x, hi = R.z;
+      while (lo < (63u << 26)) {
+        const uint32_t h2 = h ? 2u * h + s : 1u;
+        if (h2 >= (uint32_t)topn) break;
+        const uint4 N = trec[h2];
+        s = decide(lo, hi, wk);
+        h = h2;
+        R = N;
+        lo = s ? R.y : R.x;
+        hi = s ? R.w : R.z;
+      }
+      uint32_t P = topi[t * TOP_CAP + h], j = P >> SLOT_SHIFT;
+      if (blocked) P &= (1u << SLOT_SHIFT) - 1u;
+      while (lo < (63u << 26)) {
+        const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
+        uint32_t Q;
+        if (blocked) {
+          Q = j <= 2u ? P + j + 1u + s : P + off1 + (s << 3);
+          if (j > 2u && off1 == 0u) { Q = P + far[P] + (s << 3); far_used++; }
+          j = j <= 2u ? 2u * j + 1u + s : 0u;
+        } else {
+          Q = P + (s ? off1 : 1u);
+          if (s && off1 == 0u) { Q = P + far[P]; far_used++; }
+        }
+        if (Q >= pairs.size()) { bad++; break; }
+        const uint4 N = pairs[Q];
+        s = decide(lo, hi, wk);
+        P = Q;
+        R = N;
+        lo = s ? R.y : R.x;
+        hi = s ? R.w : R.z;
+      }
+      const uint32_t got = (lo & 0xFFFFFu) | hi << 20;
+      if (got != want) bad++;
+    }
+  }
+  std::printf("{\"blocked\": %d, \"top_levels\": %d, \"nodes\": %zu, \"pairs\": %zu, \"walks\": %ld, \"far_steps\": %ld, "
+              "\"mismatches\": %ld}\n", blocked ? 1 : 0, lg, bfs.size(), pairs.size(), walks, far_used, bad);
+  return bad ? 1 : 0;
+}
