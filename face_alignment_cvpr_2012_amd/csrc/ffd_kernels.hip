@@ -1250,21 +1250,30 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         const int m2 = (int)__umul24(__builtin_amdgcn_ubfe(hi, 16, 4), (unsigned)ld2), e2 = (int)__umul24(h2, (unsigned)ld2);
 #if FFD_TRAV_PK == 2
         // rectangle 1's corner into the low half (ds_read_u16), rectangle 2's into the high half of the same
-        // register (ds_read_u16_d16_hi, LDS returns in order); the wait is explicit and name the six registers, so nothing that
-        // reads them is scheduled before the data has arrived
+        // register (ds_read_u16_d16_hi; LDS returns in order), in ONE asm statement ending with the wait: the
+        // compiler sees the six registers only once their data is there (with separate statements it could
+        // copy a register between its two loads, before the first had returned)
         auto a32 = [](const unsigned char* p) { return (uint32_t)(uintptr_t)p; };
         uint32_t ra, rb, rc, rd, re, rf;
-#define FFD_D16(R, P1, P2)                                                  \
-  asm volatile("ds_read_u16 %0, %1" : "=v"(R) : "v"(a32(P1)) : "memory"); \
-  asm volatile("ds_read_u16_d16_hi %0, %1" : "+v"(R) : "v"(a32(P2)) : "memory")
-        FFD_D16(ra, q1, q2);
-        FFD_D16(rb, q1 + wb1, q2 + wb2);
-        FFD_D16(re, q1 + e1, q2 + e2);
-        FFD_D16(rf, q1 + e1 + wb1, q2 + e2 + wb2);
-        FFD_D16(rc, q1 + m1, q2 + m2);
-        FFD_D16(rd, q1 + m1 + wb1, q2 + m2 + wb2);
-#undef FFD_D16
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ra), "+v"(rb), "+v"(rc), "+v"(rd), "+v"(re), "+v"(rf) : : "memory");
+        asm volatile(
+            "ds_read_u16 %0, %6\n\t"
+            "ds_read_u16 %1, %7\n\t"
+            "ds_read_u16 %2, %8\n\t"
+            "ds_read_u16 %3, %9\n\t"
+            "ds_read_u16 %4, %10\n\t"
+            "ds_read_u16 %5, %11\n\t"
+            "ds_read_u16_d16_hi %0, %12\n\t"
+            "ds_read_u16_d16_hi %1, %13\n\t"
+            "ds_read_u16_d16_hi %2, %14\n\t"
+            "ds_read_u16_d16_hi %3, %15\n\t"
+            "ds_read_u16_d16_hi %4, %16\n\t"
+            "ds_read_u16_d16_hi %5, %17\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(ra), "=&v"(rb), "=&v"(rc), "=&v"(rd), "=&v"(re), "=&v"(rf)
+            : "v"(a32(q1)), "v"(a32(q1 + wb1)), "v"(a32(q1 + m1)), "v"(a32(q1 + m1 + wb1)), "v"(a32(q1 + e1)),
+              "v"(a32(q1 + e1 + wb1)), "v"(a32(q2)), "v"(a32(q2 + wb2)), "v"(a32(q2 + m2)), "v"(a32(q2 + m2 + wb2)),
+              "v"(a32(q2 + e2)), "v"(a32(q2 + e2 + wb2))
+            : "memory");
         const u16x2 a = __builtin_bit_cast(u16x2, ra), b = __builtin_bit_cast(u16x2, rb), c = __builtin_bit_cast(u16x2, rc),
                     d = __builtin_bit_cast(u16x2, rd), e = __builtin_bit_cast(u16x2, re), f = __builtin_bit_cast(u16x2, rf);
 #else
