@@ -1028,9 +1028,6 @@ constexpr int TRAV_NT = 1024;
 #ifndef FFD_TRAV_SPLIT_RECTS
 #define FFD_TRAV_SPLIT_RECTS 0  // scheduling barrier between the two rectangles' reads
 #endif
-#ifndef FFD_TRAV_PK
-#define FFD_TRAV_PK 0  // corners into packed u16 pairs (d16 loads)
-#endif
 __host__ __device__ constexpr int trav_nw(int GX, int GY, bool HP) {
   return FFD_TRAV_DUAL ? ((GX * GY * (HP ? 15 : 20) + 1) / 2 + 63) / 64 * 64
                        : (GX * GY * (HP ? 15 : 20) <= 320 ? 320 : 512);
@@ -1236,62 +1233,6 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         const int d12 = half ? po - pm : pm - po;                              // p1 - p2 on both lanes
         const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
         return d12 <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
-#elif FFD_TRAV_PK
-        // both rectangles' corners loaded into the halves of packed u16 pairs (ds_read_u16_d16 / _d16_hi), the
-        // two halves' sums as packed u16 arithmetic (no repacking of separately loaded corners)
-        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-        const unsigned char* cb = base + __umul24(lo >> 26, (unsigned)chs2);
-        const unsigned char* q1 = cb + __umul24(__builtin_amdgcn_ubfe(lo, 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 0, 5);
-        const unsigned char* q2 = cb + __umul24(__builtin_amdgcn_ubfe(lo, 15, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 10, 5);
-        const uint32_t w1 = __builtin_amdgcn_ubfe(hi, 0, 5), h1 = __builtin_amdgcn_ubfe(hi, 5, 5);
-        const uint32_t w2 = __builtin_amdgcn_ubfe(hi, 10, 5), h2 = __builtin_amdgcn_ubfe(hi, 15, 5);
-        const int wb1 = (int)(2u * w1), wb2 = (int)(2u * w2);
-        const int m1 = (int)__umul24(__builtin_amdgcn_ubfe(hi, 6, 4), (unsigned)ld2), e1 = (int)__umul24(h1, (unsigned)ld2);
-        const int m2 = (int)__umul24(__builtin_amdgcn_ubfe(hi, 16, 4), (unsigned)ld2), e2 = (int)__umul24(h2, (unsigned)ld2);
-#if FFD_TRAV_PK == 2
-        // rectangle 1's corner into the low half (ds_read_u16), rectangle 2's into the high half of the same
-        // register (ds_read_u16_d16_hi; LDS returns in order), in ONE asm statement ending with the wait: the
-        // compiler sees the six registers only once their data is there (with separate statements it could
-        // copy a register between its two loads, before the first had returned)
-        auto a32 = [](const unsigned char* p) { return (uint32_t)(uintptr_t)p; };
-        uint32_t ra, rb, rc, rd, re, rf;
-        asm volatile(
-            "ds_read_u16 %0, %6\n\t"
-            "ds_read_u16 %1, %7\n\t"
-            "ds_read_u16 %2, %8\n\t"
-            "ds_read_u16 %3, %9\n\t"
-            "ds_read_u16 %4, %10\n\t"
-            "ds_read_u16 %5, %11\n\t"
-            "ds_read_u16_d16_hi %0, %12\n\t"
-            "ds_read_u16_d16_hi %1, %13\n\t"
-            "ds_read_u16_d16_hi %2, %14\n\t"
-            "ds_read_u16_d16_hi %3, %15\n\t"
-            "ds_read_u16_d16_hi %4, %16\n\t"
-            "ds_read_u16_d16_hi %5, %17\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(ra), "=&v"(rb), "=&v"(rc), "=&v"(rd), "=&v"(re), "=&v"(rf)
-            : "v"(a32(q1)), "v"(a32(q1 + wb1)), "v"(a32(q1 + m1)), "v"(a32(q1 + m1 + wb1)), "v"(a32(q1 + e1)),
-              "v"(a32(q1 + e1 + wb1)), "v"(a32(q2)), "v"(a32(q2 + wb2)), "v"(a32(q2 + m2)), "v"(a32(q2 + m2 + wb2)),
-              "v"(a32(q2 + e2)), "v"(a32(q2 + e2 + wb2))
-            : "memory");
-        const u16x2 a = __builtin_bit_cast(u16x2, ra), b = __builtin_bit_cast(u16x2, rb), c = __builtin_bit_cast(u16x2, rc),
-                    d = __builtin_bit_cast(u16x2, rd), e = __builtin_bit_cast(u16x2, re), f = __builtin_bit_cast(u16x2, rf);
-#else
-        auto ld = [](const unsigned char* p) { return *reinterpret_cast<const unsigned short*>(p); };
-        u16x2 a, b, c, d, e, f;
-        a.x = ld(q1); a.y = ld(q2);
-        b.x = ld(q1 + wb1); b.y = ld(q2 + wb2);
-        e.x = ld(q1 + e1); e.y = ld(q2 + e2);
-        f.x = ld(q1 + e1 + wb1); f.y = ld(q2 + e2 + wb2);
-        c.x = ld(q1 + m1); c.y = ld(q2 + m2);
-        d.x = ld(q1 + m1 + wb1); d.y = ld(q2 + m2 + wb2);
-#endif
-        const u16x2 dc = d - c, top = (a - b) + dc, bot = (f - e) - dc;
-        const float i1 = __builtin_amdgcn_rcpf((float)__umul24(w1, h1)), i2 = __builtin_amdgcn_rcpf((float)__umul24(w2, h2));
-        const int p1 = (int)__builtin_fmaf((float)((uint32_t)top.x + bot.x), i1, 0.00075f);
-        const int p2 = (int)__builtin_fmaf((float)((uint32_t)top.y + bot.y), i2, 0.00075f);
-        const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
-        return (p1 - p2) <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
 #else
         // (fields by bit-field extracts; bits of hi above 23 are the record's child offset, never read)
         const unsigned char* cb = base + __umul24(lo >> 26, (unsigned)chs2);
