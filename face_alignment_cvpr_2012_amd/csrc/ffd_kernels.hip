@@ -3126,10 +3126,14 @@ bool traverse_window_fits(TravShape g, bool hp, int step, int step_y, int lds_ca
   return traverse_lds_bytes(g, step, step_y) <= lds_cap && NCH * WH * (trav_row_pitch(WW, g.gx * step) * 2 / cb) <= ns * u;
 }
 
-// The block shapes instantiated (x x y patches): head pose 4x4, 5x4, 3x3; FFD 5x5, 4x4, 3x3.
+// The block shapes instantiated (x x y patches): head pose 4x4, 5x4, 3x3; FFD 5x5, 4x4, 3x3 (measurement builds
+// add others through FFD_TRAV_EXTRA_SHAPES, e.g. -DFFD_TRAV_EXTRA_SHAPES(X)=X(true,4,5)).
+#ifndef FFD_TRAV_EXTRA_SHAPES
+#define FFD_TRAV_EXTRA_SHAPES(X)
+#endif
 // (FFD 4x6, 480 walks with an unpadded pitch-44 window, measured 14.5 ms against 8.5 ms for 5x5.)
 #define FFD_TRAV_SHAPES(X)                                                                              \
-  X(true, 4, 4) X(true, 5, 4) X(true, 3, 3) X(false, 5, 5) X(false, 4, 4) X(false, 3, 3)
+  X(true, 4, 4) X(true, 5, 4) X(true, 3, 3) X(false, 5, 5) X(false, 4, 4) X(false, 3, 3) FFD_TRAV_EXTRA_SHAPES(X)
 
 bool traverse_shape_supported(TravShape g, bool hp) {
 #define FFD_TRAV_SUP(HPV, GXV, GYV) if (hp == HPV && g.gx == GXV && g.gy == GYV) return true;
