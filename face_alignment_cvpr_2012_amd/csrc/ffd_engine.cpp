@@ -884,6 +884,7 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
     }
     HIP_CHECK(hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&e->copy_done, hipEventDisableTiming));
+    e->warm_descriptor_slots();
     e->model_path = d->model_path;
     e->load_model(d->model_path);
     e->check_traverse_lds();
@@ -1077,7 +1078,7 @@ ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t
     // BGR2GRAY of (v,v,v) is v: (1868+9617+4899)*v + 8192 >> 14 == v for v in [0,255]
     for (int i = 0; i < W * H; i++) bgr[3 * i] = bgr[3 * i + 1] = bgr[3 * i + 2] = gray_face[i];
     e->scratch_a.ensure(bgr.size());
-    HIP_CHECK(hipMemcpyAsync(e->scratch_a.p, bgr.data(), bgr.size(), hipMemcpyHostToDevice, w.stream));
+    e->upload_pinned(e->scratch_a.p, bgr.data(), bgr.size(), w.stream);
     FaceDesc f;
     std::memset(&f, 0, sizeof(f));
     f.img_w = W; f.img_h = H; f.img_stride = 3 * W; f.bw = W; f.bh = H; f.W = W; f.H = H;
@@ -1278,7 +1279,7 @@ void run_facial_features(ffd_engine* e, Workspace& w, const FaceDesc& f, const u
   std::memset(&hs, 0, sizeof(hs));
   hs.n_trees = n_trees;
   for (int t = 0; t < n_trees; t++) hs.trees[t] = tree_ids[t];
-  HIP_CHECK(hipMemcpyAsync(w.state.p, &hs, sizeof(hs), hipMemcpyHostToDevice, w.stream));
+  e->upload_pinned(w.state.p, &hs, sizeof(hs), w.stream);
   e->out.ensure(sizeof(FaceOut));
   const int n_parts = std::max(0, std::min(o.num_parts, NPARTS));
   launch_traverse(false, dfd, 1, blocks_per_face(fv, false, g), g, e->mp_pairs.as<uint4>(), e->mp_tops.as<uint4>(),
@@ -1505,7 +1506,7 @@ ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, i
         std::memset(&hs, 0, sizeof(hs));
         hs.n_trees = n_trees;
         for (int t = 0; t < n_trees; t++) hs.trees[t] = tree_ids[t];
-        HIP_CHECK(hipMemcpyAsync(w.state.p, &hs, sizeof(hs), hipMemcpyHostToDevice, w.stream));
+        e->upload_pinned(w.state.p, &hs, sizeof(hs), w.stream);
       }
       launch_traverse(hp, w.faces.as<FaceDesc>(), 1, blocks_per_face(fv, hp, g), g,
                       hp ? e->hp_pairs.as<uint4>() : e->mp_pairs.as<uint4>(), hp ? e->hp_tops.as<uint4>() : e->mp_tops.as<uint4>(),
@@ -1583,7 +1584,7 @@ ffd_status ffd_sample_create(ffd_engine* e, const uint8_t* gray, int32_t W, int3
         p[0] = p[1] = p[2] = v;
       }
     e->scratch_a.ensure(bgr.size());
-    HIP_CHECK(hipMemcpyAsync(e->scratch_a.p, bgr.data(), bgr.size(), hipMemcpyHostToDevice, w.stream));
+    e->upload_pinned(e->scratch_a.p, bgr.data(), bgr.size(), w.stream);
     FaceDesc f;
     std::memset(&f, 0, sizeof(f));
     f.img_w = W; f.img_h = H; f.img_stride = 3 * W; f.bw = W; f.bh = H; f.W = W; f.H = H;
@@ -1596,15 +1597,25 @@ ffd_status ffd_sample_create(ffd_engine* e, const uint8_t* gray, int32_t W, int3
       w.gabor_mm.ensure(5 * 64);
       HIP_CHECK(hipMemsetAsync(w.gabor_mm.p, 0, w.gabor_mm.n, w.stream));
     }
-    std::vector<FaceDesc> one{f};
-    upload(w.faces, one, w.stream);
+    e->upload_descriptors(w.faces, std::vector<FaceDesc>{f}, w.stream);
     const FaceDesc* dfd = w.faces.as<FaceDesc>();
     launch_gray_resize(dfd, 1, e->scratch_a.as<uint8_t>(), w.gray.as<uint8_t>(), w.stream);
+    // the five Gabor scales and the integrals side by side on the workspace's fork streams, as a small batch
+    // runs them (run_chunk): one face's kernels are each a few workgroups, so in one stream they would run
+    // one after another (≈ 0.33 ms of a sample's ≈ 0.45 ms, evaluate_mt trace)
+    const int nfork = (int)w.fork.size();
+    HIP_CHECK(hipEventRecord(w.fork_ev[0], w.stream));
+    for (int i = 0; i < nfork; i++) HIP_CHECK(hipStreamWaitEvent(w.fork[i], w.fork_ev[0], 0));
+    auto cs = [&](int i) { return i % (nfork + 1) == 0 ? w.stream : w.fork[i % (nfork + 1) - 1]; };
     for (int nu = 4; nu >= 0; nu--)
       launch_gabor(nu, dfd, 1, H, w.gray.as<uint8_t>(), e->gabor_coef.as<float>(), w.mag.as<float>(),
-                   s->chan.as<uint16_t>(), w.gabor_redo.as<int>(), e->gabor_exact, w.gabor_mm.as<uint32_t>(), w.stream);
-    launch_integral(dfd, 1, H, w.gray.as<uint8_t>(), s->chan.as<uint16_t>(), w.stream);
+                   s->chan.as<uint16_t>(), w.gabor_redo.as<int>(), e->gabor_exact, w.gabor_mm.as<uint32_t>(), cs(4 - nu));
+    launch_integral(dfd, 1, H, w.gray.as<uint8_t>(), s->chan.as<uint16_t>(), cs(5));
     HIP_CHECK(hipGetLastError());
+    for (int i = 0; i < nfork; i++) {
+      HIP_CHECK(hipEventRecord(w.fork_ev[1 + i], w.fork[i]));
+      HIP_CHECK(hipStreamWaitEvent(w.stream, w.fork_ev[1 + i], 0));
+    }
     HIP_CHECK(hipStreamSynchronize(w.stream));  // bgr is released on return
     w.count = 0;
     w.pending = false;

@@ -247,9 +247,25 @@ struct ffd_engine {
   };
   PinnedSlot desc_pin[8];
   int desc_pin_next = 0;
+  // every slot's event and a first pinned buffer at engine creation: a slot's first use otherwise pays a
+  // hipHostMalloc (≈ 50 µs) inside a call (the first eight calls of a process: evaluate_mt trace)
+  void warm_descriptor_slots() {
+    for (auto& s : desc_pin) {
+      if (!s.ev) HIP_CHECK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+      if (!s.p) {
+        HIP_CHECK(hipHostMalloc(&s.p, 64 * sizeof(FaceDesc), hipHostMallocDefault));
+        s.cap = 64 * sizeof(FaceDesc);
+      }
+    }
+  }
   void upload_descriptors(DevBuf& dst, const std::vector<FaceDesc>& fds, hipStream_t st) {
     const size_t bytes = fds.size() * sizeof(FaceDesc);
     dst.ensure(bytes);
+    upload_pinned(dst.p, fds.data(), bytes, st);
+  }
+  // a small host -> device copy through the pinned slots (a pageable source is staged by the runtime on
+  // the calling thread)
+  void upload_pinned(void* dst, const void* src, size_t bytes, hipStream_t st) {
     if (!bytes) return;
     PinnedSlot& s = desc_pin[desc_pin_next++ & 7];
     if (!s.ev) HIP_CHECK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
@@ -261,8 +277,8 @@ struct ffd_engine {
       HIP_CHECK(hipHostMalloc(&s.p, bytes, hipHostMallocDefault));
       s.cap = bytes;
     }
-    std::memcpy(s.p, fds.data(), bytes);
-    HIP_CHECK(hipMemcpyAsync(dst.p, s.p, bytes, hipMemcpyHostToDevice, st));
+    std::memcpy(s.p, src, bytes);
+    HIP_CHECK(hipMemcpyAsync(dst, s.p, bytes, hipMemcpyHostToDevice, st));
     HIP_CHECK(hipEventRecord(s.ev, st));
     s.used = true;
   }
