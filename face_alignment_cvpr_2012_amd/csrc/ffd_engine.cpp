@@ -1500,7 +1500,10 @@ ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, i
       stage_desc(e, w, f);
       const TravShape g = ffd_engine::fit_shape(hp ? e->trav_g_hp : e->trav_g_mp, hp, step, step);
       std::vector<FaceDesc> fv{f};
-      int32_t* leaf_dev = hp ? w.hpleaf.as<int32_t>() : w.mpleaf.as<int32_t>();
+      // the leaves go straight to host-mapped pinned memory (no device buffer, no copy back)
+      const size_t all = (size_t)gx * gy * n_trees * 4;
+      int32_t* pin = static_cast<int32_t*>(e->pin_leaf.ensure(all));
+      int32_t* leaf_dev = pin;
       if (!hp) {
         HpState hs;
         std::memset(&hs, 0, sizeof(hs));
@@ -1515,9 +1518,6 @@ ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, i
                       hp ? e->hp_trees : 0, step, step, f.plane, s->chan.as<uint16_t>(), leaf_dev, e->trav_wg,
                       TRAV_LDS_CAP, w.stream);
       HIP_CHECK(hipGetLastError());
-      const size_t all = (size_t)gx * gy * n_trees * 4;
-      int32_t* pin = static_cast<int32_t*>(e->pin_leaf.ensure(all));
-      HIP_CHECK(hipMemcpyAsync(pin, leaf_dev, all, hipMemcpyDeviceToHost, w.stream));
       HIP_CHECK(hipStreamSynchronize(w.stream));
       for (int i = 0; i < nx; i++)  // rows of the sub-grid: patch (i, j) of the full grid is i * gy + j
         std::memcpy(leaf_ids + (size_t)i * ny * n_trees, pin + (size_t)i * gy * n_trees, (size_t)ny * n_trees * 4);

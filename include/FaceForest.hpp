@@ -556,7 +556,7 @@ template <class S> class Forest {
   static constexpr size_t npos = ~(size_t)0;
   struct Cache {
     std::mutex mu;
-    std::unordered_map<int32_t, std::unique_ptr<Leaf>> leaves;
+    std::vector<std::unique_ptr<Leaf>> leaves;  // by leaf ordinal (a lookup per patch and tree: no hashing)
     // the speculative grid evaluation of the last (sample, tree list): patches (x0 + i step, y0 + j step)
     uint64_t sample = 0;
     std::vector<int32_t> ids;
@@ -575,13 +575,14 @@ template <class S> class Forest {
     if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(engine_));
   }
   Leaf* leaf_locked(int32_t ordinal) const {
-    auto it = cache_->leaves.find(ordinal);
-    if (it != cache_->leaves.end()) return it->second.get();
+    auto& v = cache_->leaves;
+    if (ordinal >= 0 && (size_t)ordinal < v.size() && v[ordinal]) return v[ordinal].get();
     typename ForestKind<S>::Raw raw;
-    check(ffd_forest_leaves(engine_, ForestKind<S>::value, &ordinal, 1, &raw));
+    check(ffd_forest_leaves(engine_, ForestKind<S>::value, &ordinal, 1, &raw));  // (rejects a bad ordinal)
     std::unique_ptr<Leaf> l(new Leaf());
     ForestKind<S>::fill(raw, *l);
-    return (cache_->leaves[ordinal] = std::move(l)).get();
+    if ((size_t)ordinal >= v.size()) v.resize((size_t)ordinal + 1);
+    return (v[ordinal] = std::move(l)).get();
   }
   void eval_one(const S* sample, int32_t* ids) const {
     const int32_t xy[2] = {sample->roi.x, sample->roi.y};
@@ -607,13 +608,16 @@ template <class S> class Forest {
       c.grid_ids.resize((size_t)c.nx * c.ny * T);
       check(ffd_sample_eval_grid(im.handle(), ForestKind<S>::value, c.x0, c.y0, step, c.nx, c.ny, ids_.data(), T,
                                  c.grid_ids.data()));
-      // the payloads of every leaf reached, fetched once
+      // the payloads of every leaf reached, fetched once per forest cache
+      int32_t top = -1;
+      for (int32_t v : c.grid_ids) top = std::max(top, v);
+      if ((size_t)(top + 1) > c.leaves.size()) c.leaves.resize((size_t)top + 1);
       std::vector<int32_t> uniq;
       for (int32_t v : c.grid_ids)
-        if (!c.leaves.count(v)) uniq.push_back(v);
-      std::sort(uniq.begin(), uniq.end());
-      uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+        if (!c.leaves[v]) uniq.push_back(v);
       if (!uniq.empty()) {
+        std::sort(uniq.begin(), uniq.end());
+        uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
         std::vector<typename ForestKind<S>::Raw> raw(uniq.size());
         check(ffd_forest_leaves(engine_, ForestKind<S>::value, uniq.data(), (int32_t)uniq.size(), raw.data()));
         for (size_t i = 0; i < uniq.size(); i++) {
