@@ -465,12 +465,13 @@ template <class S> struct Tree {
 template <class S> class Forest {
  public:
   typedef typename S::Leaf Leaf;
-  Forest() : cache_(std::make_shared<Cache>()) {}
-  Forest(ffd_engine* e, std::vector<int32_t> trees) : engine_(e), cache_(std::make_shared<Cache>()) {
+  Forest() : list_(std::make_shared<TreeList>()), cache_(std::make_shared<Cache>()) {}
+  Forest(ffd_engine* e, std::vector<int32_t> trees)
+      : engine_(e), list_(std::make_shared<TreeList>()), cache_(std::make_shared<Cache>()) {
     for (int32_t t : trees) addTree(t);
   }
-  int numberOfTrees() const { return (int)ids_.size(); }
-  const std::vector<int32_t>& treeIds() const { return ids_; }
+  int numberOfTrees() const { return (int)list_->ids.size(); }
+  const std::vector<int32_t>& treeIds() const { return list_->ids; }
   ffd_engine* engine() const { return engine_; }
   void setParam(ForestParam fp) { param_ = fp; }
   ForestParam getParam() const { return param_; }
@@ -481,14 +482,12 @@ template <class S> class Forest {
     addTree(tree->id);
   }
   void addTree(int32_t id) {
-    ids_.push_back(id);
-    trees_.push_back(Tree<S>{id, engine_});
+    TreeList& l = mut();
+    l.ids.push_back(id);
+    l.trees.push_back(Tree<S>{id, engine_});
   }
-  Tree<S>* getTree(int idx) { return &trees_.at(idx); }
-  void cleanForest() {
-    ids_.clear();
-    trees_.clear();
-  }
+  Tree<S>* getTree(int idx) { return &mut().trees.at(idx); }
+  void cleanForest() { list_ = std::make_shared<TreeList>(); }
   // the patch grid step of the speculative evaluation (0: S::default_step)
   void setGridStep(int step) { grid_step_ = step; }
 
@@ -523,7 +522,7 @@ template <class S> class Forest {
 
   // Forest<S>::evaluateMT(const S*, S::Leaf**) (Forest.hpp:80-90): leafs[t] = the leaf tree t reaches.
   void evaluateMT(const S* sample, Leaf** leafs) const {
-    const size_t T = ids_.size();
+    const size_t T = list_->ids.size();
     std::lock_guard<std::mutex> g(cache_->mu);
     const size_t row = grid_row(sample);
     if (row != npos) {
@@ -537,7 +536,7 @@ template <class S> class Forest {
   }
   // the same with the model's leaf ordinals (ffd_forest_leaves gives their payloads)
   void evaluateMT(const S* sample, int32_t* leafs) const {
-    const size_t T = ids_.size();
+    const size_t T = list_->ids.size();
     std::lock_guard<std::mutex> g(cache_->mu);
     const size_t row = grid_row(sample);
     if (row != npos) {
@@ -564,12 +563,21 @@ template <class S> class Forest {
     std::vector<int32_t> grid_ids;  // [(i * ny + j) * T + t]
     std::vector<Leaf*> grid_leaf;   // the payloads of grid_ids
   };
+  // the tree list, shared by copies until one of them changes it (a copy per evaluateMT call, as the reference
+  // binds the forest by value into every task, then costs a reference count, not a list copy)
+  struct TreeList {
+    std::vector<int32_t> ids;
+    std::deque<Tree<S>> trees;
+  };
   ffd_engine* engine_ = nullptr;
   ForestParam param_;
-  std::vector<int32_t> ids_;
-  std::deque<Tree<S>> trees_;
+  std::shared_ptr<TreeList> list_;
   int grid_step_ = 0;
   std::shared_ptr<Cache> cache_;
+  TreeList& mut() {
+    if (list_.use_count() > 1) list_ = std::make_shared<TreeList>(*list_);
+    return *list_;
+  }
 
   void check(ffd_status st) const {
     if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(engine_));
@@ -586,27 +594,28 @@ template <class S> class Forest {
   }
   void eval_one(const S* sample, int32_t* ids) const {
     const int32_t xy[2] = {sample->roi.x, sample->roi.y};
-    check(ffd_sample_eval_leaves(sample->image->handle(), ForestKind<S>::value, xy, 1, ids_.data(),
-                                 (int32_t)ids_.size(), ids));
+    check(ffd_sample_eval_leaves(sample->image->handle(), ForestKind<S>::value, xy, 1, list_->ids.data(),
+                                 (int32_t)list_->ids.size(), ids));
   }
   // The offset of the sample patch's leaf row in the grid evaluation, evaluating the grid that contains the patch
   // first when the cache holds another sample or tree list; npos for a patch off the grid.
   size_t grid_row(const S* sample) const {
     Cache& c = *cache_;
     const ImageSample& im = *sample->image;
-    const int x = sample->roi.x, y = sample->roi.y, P = 31, T = (int)ids_.size();
-    if (c.sample != im.id() || c.ids != ids_) {
+    const std::vector<int32_t>& ids = list_->ids;
+    const int x = sample->roi.x, y = sample->roi.y, P = 31, T = (int)ids.size();
+    if (c.sample != im.id() || c.ids != ids) {
       const int step = grid_step_ > 0 ? grid_step_ : S::default_step;
       if (x < 0 || y < 0 || x + P > im.width() || y + P > im.height() || T == 0) return npos;
       c.sample = 0;
-      c.ids = ids_;
+      c.ids = ids;
       c.x0 = x % step;
       c.y0 = y % step;
       c.step = step;
       c.nx = (im.width() - P - c.x0) / step + 1;
       c.ny = (im.height() - P - c.y0) / step + 1;
       c.grid_ids.resize((size_t)c.nx * c.ny * T);
-      check(ffd_sample_eval_grid(im.handle(), ForestKind<S>::value, c.x0, c.y0, step, c.nx, c.ny, ids_.data(), T,
+      check(ffd_sample_eval_grid(im.handle(), ForestKind<S>::value, c.x0, c.y0, step, c.nx, c.ny, ids.data(), T,
                                  c.grid_ids.data()));
       // the payloads of every leaf reached, fetched once per forest cache
       int32_t top = -1;
