@@ -2434,7 +2434,7 @@ constexpr int MS_RA = FFD_MS_RA;  // serial phase: LDS reads in flight ahead of 
 #define FFD_MS_SORT 1  // k_meanshift over chains sorted by list length (k_ms_order)
 #endif
 #ifndef FFD_MS_K
-#define FFD_MS_K 4  // k_meanshift4: votes per lane per tile
+#define FFD_MS_K 2  // k_meanshift4: votes per lane per tile (C4 MeanShift: 1 8.52-8.56, 2 8.51-8.55, 4 8.68-8.71, 8 14.1 ms)
 #endif
 #ifndef FFD_VOTES_WG_MAX
 #define FFD_VOTES_WG_MAX 64  // batches of up to 64 faces: k_votes_wg (16 waves per face)
