@@ -6,8 +6,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 B=face_alignment_cvpr_2012_amd/lib/libffd.so
 FFD_LIBRARY=$PWD/$B timeout -k 10 300 python tools/leaf_ab.py --faces 4096 --out gpurun_out/ab_base_c2.npz > gpurun_out/abq.log 2>&1 || { tail -5 gpurun_out/abq.log; exit 1; }
-for v in qs13 qs7; do
+for v in qs13 qs7 noblk; do
   FFD_LIBRARY=$PWD/build/$v/libffd.so timeout -k 10 300 python tools/leaf_ab.py --faces 4096 --out gpurun_out/ab_${v}_c2.npz >> gpurun_out/abq.log 2>&1 || { tail -5 gpurun_out/abq.log; exit 1; }
   echo "$v c2: $(python tools/leaf_ab.py --compare gpurun_out/ab_base_c2.npz gpurun_out/ab_${v}_c2.npz)"
 done
-STAGES=gabor_25x25,gabor_19x19,gabor_13x13,gabor_9x9,gabor_7x7 tools/lib_variant_probe.sh build/qs13/libffd.so build/qs7/libffd.so
+STAGES=gabor_19x19,gabor_13x13,gabor_9x9,headpose_traverse,ffd_traverse tools/lib_variant_probe.sh build/qs13/libffd.so build/qs7/libffd.so build/noblk/libffd.so
