@@ -105,7 +105,7 @@ $(EXAMPLE3): examples/bench_host.cpp include/FaceForest.hpp include/ffd.h $(LIB)
 	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(PKG)/lib -lffd -Wl,-rpath,'$$ORIGIN/../../$(PKG)/lib'
 $(EXAMPLE4): examples/evaluate_mt.cpp include/FaceForest.hpp include/ffd.h $(LIB)
 	@mkdir -p $(@D)
-	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(PKG)/lib -lffd -Wl,-rpath,'$$ORIGIN/../../$(PKG)/lib'
+	$(CXX) -O2 -std=c++17 -Wall -pthread -Iinclude -o $@ $< -L$(PKG)/lib -lffd -Wl,-rpath,'$$ORIGIN/../../$(PKG)/lib'
 $(EXAMPLE5): examples/reference_main.cpp include/FaceForest.hpp include/ffd.h $(LIB)
 	@mkdir -p $(@D)
 	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -L$(PKG)/lib -lffd -Wl,-rpath,'$$ORIGIN/../../$(PKG)/lib'

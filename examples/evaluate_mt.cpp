@@ -12,13 +12,18 @@
 // $FFD_EVAL_REPS (default 3) repetitions of the whole per-face procedure (a fresh ImageSample each): the
 // ImageSample, the first evaluateMT call (the grid evaluation), the mean of the other calls, all calls, the
 // vote filter and MeanShift; plus the first repetition's first call (cold: first launches, allocations).
+// $FFD_EVAL_THREADS=N (default 0) first runs N threads that each build their own ImageSample and their own
+// Forest (separate caches, one engine) and walk every patch four times; "thread_crcs" holds each thread's leaf
+// CRC (the header serialises the engine calls of distinct objects, detail::engine_call).
 // exit: 0 ok, 2 bad arguments, 3 engine not initialised, 4 error.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #define FFD_NO_OPENCV
@@ -84,6 +89,46 @@ int main(int argc, char** argv) {
     Forest<MPSample> forest;
     forest.setParam(jungle[0].getParam());
     for (int g : tree_args) forest.addTree(jungle.at(g / 20).getTree(g % 20));
+    // threads on one engine, each with its own sample and forest (FFD_EVAL_THREADS)
+    std::string thread_json;
+    const int nthreads = std::getenv("FFD_EVAL_THREADS") ? std::max(0, std::atoi(std::getenv("FFD_EVAL_THREADS"))) : 0;
+    if (nthreads > 0) {
+      std::vector<Forest<MPSample>> own(nthreads);
+      for (auto& fk : own) {  // composed here: getTree() may copy the jungle's tree list
+        fk.setParam(jungle[0].getParam());
+        for (int g : tree_args) fk.addTree(jungle.at(g / 20).getTree(g % 20));
+      }
+      std::vector<uint32_t> crcs(nthreads, 0);
+      std::atomic<int> errors{0};
+      std::vector<std::thread> th;
+      for (int k = 0; k < nthreads; k++)
+        th.emplace_back([&, k] {
+          try {
+            const int ps = own[k].getParam().getPatchSize(), step = MultiPartEstimatorOption().step_size;
+            const int T = own[k].numberOfTrees();
+            for (int it = 0; it < 4; it++) {
+              ImageSample s(cv::Mat(h, w, px.data(), (size_t)w, 1), std::vector<int>{0, 1, 2}, true);
+              std::vector<int32_t> ids;
+              for (int x = 0; x < w - ps; x += step)
+                for (int y = 0; y < h - ps; y += step) {
+                  MPSample m(&s, cv::Rect(x, y, ps, ps));
+                  ids.resize(ids.size() + T);
+                  own[k].evaluateMT(&m, &ids[ids.size() - T]);
+                }
+              const uint32_t c = crc32(ids.data(), ids.size() * 4);
+              if (it > 0 && c != crcs[k]) errors++;
+              crcs[k] = c;
+            }
+          } catch (const std::exception& e) {
+            std::fprintf(stderr, "thread %d: %s\n", k, e.what());
+            errors++;
+          }
+        });
+      for (auto& t : th) t.join();
+      thread_json = ", \"thread_errors\": " + std::to_string(errors.load()) + ", \"thread_crcs\": [";
+      for (int k = 0; k < nthreads; k++) thread_json += (k ? ", " : "") + std::to_string(crcs[k]);
+      thread_json += "]";
+    }
     const int reps = std::getenv("FFD_EVAL_REPS") ? std::max(1, std::atoi(std::getenv("FFD_EVAL_REPS"))) : 3;
     double cold_first_ms = 0;
     for (int rep = 0; rep < reps; rep++) {
@@ -157,9 +202,10 @@ int main(int argc, char** argv) {
       for (int p = 0; p < options.num_parts; p++) std::printf(p ? ", %zu" : "%zu", votes[p].size());
       std::printf("], \"leaf_crc\": %u, \"patches\": %zu, \"trees\": %d, \"sample_ms\": %.4f, \"first_call_ms\": %.4f, "
                   "\"other_calls_mean_us\": %.4f, \"all_calls_ms\": %.4f, \"vote_filter_ms\": %.4f, \"meanshift_ms\": %.4f, "
-                  "\"cold_first_call_ms\": %.4f, \"reps\": %d}\n",
+                  "\"cold_first_call_ms\": %.4f, \"reps\": %d%s}\n",
                   crc32(ord.data(), ord.size() * 4), samples.size(), num_trees, sample_ms, first_ms,
-                  (all_ms - first_ms) * 1e3 / (double)(samples.size() - 1), all_ms, filter_ms, ms_ms, cold_first_ms, reps);
+                  (all_ms - first_ms) * 1e3 / (double)(samples.size() - 1), all_ms, filter_ms, ms_ms, cold_first_ms, reps,
+                  thread_json.c_str());
     }
   } catch (const std::exception& e) {
     std::fprintf(stderr, "evaluate_mt: %s\n", e.what());

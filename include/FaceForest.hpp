@@ -286,6 +286,25 @@ inline ForestDirs& forest_dirs() {
   static ForestDirs d;
   return d;
 }
+// Calls into an engine one at a time, with the error text read under the same lock.  The C ABI takes one
+// caller per engine at a time (ffd.h), while the reference's callers evaluate forests and samples from pool
+// threads (face_utils.cpp:210-216, 267-274) and distinct Forest / ImageSample objects share their engine.
+// Lock order: a Forest's cache or an ImageSample's state first, then the engine.
+inline std::mutex& engine_mutex(const ffd_engine* e) {
+  static std::mutex mu;
+  static std::unordered_map<const ffd_engine*, std::unique_ptr<std::mutex>> m;
+  std::lock_guard<std::mutex> g(mu);
+  std::unique_ptr<std::mutex>& p = m[e];
+  if (!p) p.reset(new std::mutex());
+  return *p;
+}
+template <class F>
+ffd_status engine_call(ffd_engine* e, std::string& err, F f) {
+  std::lock_guard<std::mutex> g(engine_mutex(e));
+  const ffd_status st = f();
+  if (st != FFD_OK) err = ffd_last_error(e);
+  return st;
+}
 inline uint64_t next_sample_id() {
   static std::atomic<uint64_t> n{0};
   return ++n;
@@ -361,8 +380,9 @@ class ImageSample {
     if (f != std::vector<int>({0, 1, 2}))
       throw std::invalid_argument("ImageSample: only features {0,1,2} are supported (the pretrained forests' channels)");
     if (!st_->engine) throw std::runtime_error("ImageSample: no FaceForest engine");
-    const ffd_status s = ffd_sample_create(st_->engine, gray, cols, rows, (int32_t)step, &st_->h);
-    if (s != FFD_OK) throw std::runtime_error(std::string("ImageSample: ") + ffd_last_error(st_->engine));
+    std::string err;
+    if (detail::engine_call(st_->engine, err, [&] { return ffd_sample_create(st_->engine, gray, cols, rows, (int32_t)step, &st_->h); }) != FFD_OK)
+      throw std::runtime_error("ImageSample: " + err);
     st_->w = cols;
     st_->hgt = rows;
     st_->id = detail::next_sample_id();
@@ -377,8 +397,11 @@ class ImageSample {
     std::lock_guard<std::mutex> g(st_->mu);
     if (st_->ch.empty()) {
       st_->ch.resize((size_t)38 * (st_->hgt + 1) * (st_->w + 1));
-      if (ffd_sample_channels(st_->h, st_->ch.data()) != FFD_OK)
-        throw std::runtime_error(std::string("ImageSample: ") + ffd_last_error(st_->engine));
+      std::string err;
+      if (detail::engine_call(st_->engine, err, [&] { return ffd_sample_channels(st_->h, st_->ch.data()); }) != FFD_OK) {
+        st_->ch.clear();
+        throw std::runtime_error("ImageSample: " + err);
+      }
     }
     return st_->ch.data();
   }
@@ -391,7 +414,11 @@ class ImageSample {
     uint64_t id = 0;
     std::mutex mu;
     std::vector<uint32_t> ch;
-    ~State() { ffd_sample_destroy(h); }
+    ~State() {
+      if (!h) return;
+      std::lock_guard<std::mutex> g(detail::engine_mutex(engine));
+      ffd_sample_destroy(h);
+    }
   };
   std::shared_ptr<State> st_;  // copies share the device sample (the reference copies cv::Mat headers)
 };
@@ -579,14 +606,16 @@ template <class S> class Forest {
     return *list_;
   }
 
-  void check(ffd_status st) const {
-    if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(engine_));
+  // an engine call under the engine's lock (detail::engine_call); a failure throws with its error text
+  template <class F> void call(ffd_engine* e, F f) const {
+    std::string err;
+    if (detail::engine_call(e, err, f) != FFD_OK) throw std::invalid_argument(err);
   }
   Leaf* leaf_locked(int32_t ordinal) const {
     auto& v = cache_->leaves;
     if (ordinal >= 0 && (size_t)ordinal < v.size() && v[ordinal]) return v[ordinal].get();
     typename ForestKind<S>::Raw raw;
-    check(ffd_forest_leaves(engine_, ForestKind<S>::value, &ordinal, 1, &raw));  // (rejects a bad ordinal)
+    call(engine_, [&] { return ffd_forest_leaves(engine_, ForestKind<S>::value, &ordinal, 1, &raw); });  // (rejects a bad ordinal)
     std::unique_ptr<Leaf> l(new Leaf());
     ForestKind<S>::fill(raw, *l);
     if ((size_t)ordinal >= v.size()) v.resize((size_t)ordinal + 1);
@@ -594,8 +623,10 @@ template <class S> class Forest {
   }
   void eval_one(const S* sample, int32_t* ids) const {
     const int32_t xy[2] = {sample->roi.x, sample->roi.y};
-    check(ffd_sample_eval_leaves(sample->image->handle(), ForestKind<S>::value, xy, 1, list_->ids.data(),
-                                 (int32_t)list_->ids.size(), ids));
+    call(sample->image->engine(), [&] {
+      return ffd_sample_eval_leaves(sample->image->handle(), ForestKind<S>::value, xy, 1, list_->ids.data(),
+                                    (int32_t)list_->ids.size(), ids);
+    });
   }
   // The offset of the sample patch's leaf row in the grid evaluation, evaluating the grid that contains the patch
   // first when the cache holds another sample or tree list; npos for a patch off the grid.
@@ -615,8 +646,10 @@ template <class S> class Forest {
       c.nx = (im.width() - P - c.x0) / step + 1;
       c.ny = (im.height() - P - c.y0) / step + 1;
       c.grid_ids.resize((size_t)c.nx * c.ny * T);
-      check(ffd_sample_eval_grid(im.handle(), ForestKind<S>::value, c.x0, c.y0, step, c.nx, c.ny, ids.data(), T,
-                                 c.grid_ids.data()));
+      call(im.engine(), [&] {
+        return ffd_sample_eval_grid(im.handle(), ForestKind<S>::value, c.x0, c.y0, step, c.nx, c.ny, ids.data(), T,
+                                    c.grid_ids.data());
+      });
       // the payloads of every leaf reached, fetched once per forest cache
       int32_t top = -1;
       for (int32_t v : c.grid_ids) top = std::max(top, v);
@@ -628,7 +661,7 @@ template <class S> class Forest {
         std::sort(uniq.begin(), uniq.end());
         uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
         std::vector<typename ForestKind<S>::Raw> raw(uniq.size());
-        check(ffd_forest_leaves(engine_, ForestKind<S>::value, uniq.data(), (int32_t)uniq.size(), raw.data()));
+        call(engine_, [&] { return ffd_forest_leaves(engine_, ForestKind<S>::value, uniq.data(), (int32_t)uniq.size(), raw.data()); });
         for (size_t i = 0; i < uniq.size(); i++) {
           std::unique_ptr<Leaf> l(new Leaf());
           ForestKind<S>::fill(raw[i], *l);
@@ -669,8 +702,9 @@ class MeanShift {
     for (size_t i = 0; i < votes.size(); i++)
       v[i] = ffd_vote{votes[i].pos.x, votes[i].pos.y, votes[i].weight, votes[i].check ? 1 : 0};
     const ffd_meanshift_option o{kernel, num_iterations, stopping_criteria};
-    if (ffd_meanshift(e, v.data(), (int32_t)v.size(), &o, mean_xy) != FFD_OK)
-      throw std::runtime_error(std::string("MeanShift: ") + ffd_last_error(e));
+    std::string err;
+    if (detail::engine_call(e, err, [&] { return ffd_meanshift(e, v.data(), (int32_t)v.size(), &o, mean_xy); }) != FFD_OK)
+      throw std::runtime_error("MeanShift: " + err);
   }
 };
 
@@ -753,8 +787,11 @@ class FaceForest {
     std::vector<ffd_face> out(64);
     int32_t n = 0;
     for (int pass = 0; pass < 2; pass++) {
-      const ffd_status st = ffd_analyze_images(engine_, &im, 1, &o, out.data(), nullptr, (int32_t)out.size(), &n);
-      if (st != FFD_OK) throw std::runtime_error(ffd_last_error(engine_));
+      std::string err;
+      if (detail::engine_call(engine_, err, [&] {
+            return ffd_analyze_images(engine_, &im, 1, &o, out.data(), nullptr, (int32_t)out.size(), &n);
+          }) != FFD_OK)
+        throw std::runtime_error(err);
       if (n <= (int32_t)out.size()) break;
       out.resize(n);
     }
@@ -778,10 +815,12 @@ class FaceForest {
     for (size_t i = 0; i < boxes.size(); i++) r[i] = {boxes[i].x, boxes[i].y, boxes[i].width, boxes[i].height};
     std::vector<int32_t> which(boxes.size(), 0);
     std::vector<ffd_face> out(boxes.size());
-    const ffd_status st =
-        ffd_analyze_faces(engine_, &im, 1, r.data(), which.data(), (int32_t)r.size(), out.data());
-    if (st == FFD_ERR_INVALID_ARGUMENT) throw std::invalid_argument(ffd_last_error(engine_));
-    if (st != FFD_OK) throw std::runtime_error(ffd_last_error(engine_));
+    std::string err;
+    const ffd_status st = detail::engine_call(engine_, err, [&] {
+      return ffd_analyze_faces(engine_, &im, 1, r.data(), which.data(), (int32_t)r.size(), out.data());
+    });
+    if (st == FFD_ERR_INVALID_ARGUMENT) throw std::invalid_argument(err);
+    if (st != FFD_OK) throw std::runtime_error(err);
     for (size_t i = 0; i < out.size(); i++) {
       if (out[i].status != FFD_OK)
         throw std::invalid_argument("face " + std::to_string(i) + ": " + ffd_status_string(out[i].status));
@@ -806,10 +845,12 @@ class FaceForest {
       r[i] = {boxes[i].x, boxes[i].y, boxes[i].width, boxes[i].height};
     }
     out_.resize(boxes.size());
-    const ffd_status st = ffd_analyze_faces(engine_, im.data(), (int32_t)im.size(), r.data(), nullptr,
-                                            (int32_t)r.size(), out_.data());
-    if (st == FFD_ERR_INVALID_ARGUMENT) throw std::invalid_argument(ffd_last_error(engine_));
-    if (st != FFD_OK) throw std::runtime_error(ffd_last_error(engine_));
+    std::string err;
+    const ffd_status st = detail::engine_call(engine_, err, [&] {
+      return ffd_analyze_faces(engine_, im.data(), (int32_t)im.size(), r.data(), nullptr, (int32_t)r.size(), out_.data());
+    });
+    if (st == FFD_ERR_INVALID_ARGUMENT) throw std::invalid_argument(err);
+    if (st != FFD_OK) throw std::runtime_error(err);
     faces.resize(out_.size());
     for (size_t i = 0; i < out_.size(); i++) {
       if (out_[i].status != FFD_OK)
@@ -845,8 +886,11 @@ class FaceForest {
                                HeadPoseEstimatorOption options, float* headpose, float* variance) {
     const ffd_rect r{face_bbox.x, face_bbox.y, face_bbox.width, face_bbox.height};
     const ffd_headpose_option o{options.num_head_pose_labels, options.step_size, options.min_foreground_probability};
-    const ffd_status st = ffd_sample_estimate_headpose(sample.handle(), &r, &o, headpose, variance);
-    if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(sample.engine()));
+    std::string err;
+    if (detail::engine_call(sample.engine(), err, [&] {
+          return ffd_sample_estimate_headpose(sample.handle(), &r, &o, headpose, variance);
+        }) != FFD_OK)
+      throw std::invalid_argument(err);
     (void)forest;
   }
 
@@ -860,9 +904,11 @@ class FaceForest {
                                  options.min_pf,    options.max_variance, 0};
     int32_t pts[FFD_NUM_LANDMARKS * 2];
     const std::vector<int32_t> ids = forest.treeIds();
-    const ffd_status st =
-        ffd_sample_estimate_facial_features(sample.handle(), &r, ids.data(), (int32_t)ids.size(), &o, pts);
-    if (st != FFD_OK) throw std::invalid_argument(ffd_last_error(sample.engine()));
+    std::string err;
+    if (detail::engine_call(sample.engine(), err, [&] {
+          return ffd_sample_estimate_facial_features(sample.handle(), &r, ids.data(), (int32_t)ids.size(), &o, pts);
+        }) != FFD_OK)
+      throw std::invalid_argument(err);
     ffd_cordinates.clear();
     for (int i = 0; i < options.num_parts && i < FFD_NUM_LANDMARKS; i++) ffd_cordinates.emplace_back(pts[2 * i], pts[2 * i + 1]);
   }
@@ -933,8 +979,9 @@ class FaceForest {
     std::vector<ffd_rect> r(64);
     int32_t n = 0;
     for (int pass = 0; pass < 2; pass++) {
-      const ffd_status st = ffd_detect_faces(e, &im, 1, &o, r.data(), nullptr, (int32_t)r.size(), &n);
-      if (st != FFD_OK) throw std::runtime_error(ffd_last_error(e));
+      std::string err;
+      if (detail::engine_call(e, err, [&] { return ffd_detect_faces(e, &im, 1, &o, r.data(), nullptr, (int32_t)r.size(), &n); }) != FFD_OK)
+        throw std::runtime_error(err);
       if (n <= (int32_t)r.size()) break;
       r.resize(n);
     }

@@ -111,14 +111,14 @@ def test_shim_analyze_image_detects(model_path, fixtures, engine, tmp_path):
         assert np.array_equal(np.array(ln[5:], np.int32).reshape(10, 2), f.ffd_cordinates)
 
 
-def _evaluate_mt(model_path, gray, trees, tmp_path):
+def _evaluate_mt(model_path, gray, trees, tmp_path, env=None):
     import json
     path = tmp_path / "face_mt.gray"
     np.ascontiguousarray(gray).tofile(path)
     h, w = gray.shape
     exe = os.path.join(REPO, "examples", "build", "evaluate_mt")
     r = subprocess.run([exe, model_path, str(path), str(w), str(h)] + [str(int(t)) for t in trees],
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=300, env=dict(os.environ, **(env or {})))
     assert r.returncode == 0, r.stderr
     return json.loads(r.stdout.strip().splitlines()[-1])
 
@@ -145,6 +145,20 @@ def test_shim_evaluate_mt_per_patch_pattern(model_path, fixtures, oracle_mod, tm
     assert d["other_calls_mean_us"] < 100.0, d
     print("evaluate_mt timings:", {key: d[key] for key in ("sample_ms", "first_call_ms", "other_calls_mean_us",
                                                            "all_calls_ms", "vote_filter_ms", "meanshift_ms")})
+
+
+@pytest.mark.gpu
+def test_shim_evaluate_mt_threads_share_engine(model_path, fixtures, oracle_mod, tmp_path):
+    """Pool threads on one engine with distinct objects (face_utils.cpp:210-216, 267-274 run evaluateMT from a
+    thread pool): 6 threads, each with its own ImageSample and its own Forest (separate caches), walk every patch
+    four times; each thread's leaf CRC equals the oracle's (the header serialises their engine calls)."""
+    import zlib
+    img, box = fixtures["images"][2], tuple(int(v) for v in fixtures["boxes"][2])
+    ref, tr = oracle_mod.analyze_face(img, box, threads=8, trace=True)
+    d = _evaluate_mt(model_path, tr["face"], tr["trees"], tmp_path, env={"FFD_EVAL_THREADS": "6", "FFD_EVAL_REPS": "1"})
+    want = zlib.crc32(np.ascontiguousarray(tr["mp_leaves"], np.int32).tobytes())
+    assert d["leaf_crc"] == want
+    assert d["thread_errors"] == 0 and d["thread_crcs"] == [want] * 6, d
 
 
 @pytest.mark.gpu
