@@ -357,7 +357,11 @@ def _image_array(images):
 
 # --------------------------------------------------------------- FaceForest --
 class FaceForest:
-    """FaceForest (include/FaceForest.hpp:81-157) on one MI355X device."""
+    """FaceForest (include/FaceForest.hpp:81-157) on one MI355X device.
+
+    One engine serves one caller at a time (include/ffd.h; the reference's analyzeFace is not reentrant
+    either), and this object, its ImageSamples and Forests take no lock (the C++ header does): Python threads
+    use one FaceForest each, or a FaceForestGroup (one host thread per device)."""
 
     def __init__(self, options=None):
         self.options = options or FaceForestOptions()
