@@ -117,9 +117,9 @@ EXPORTED_SYMBOLS = (
     "ffd_group_create", "ffd_group_destroy", "ffd_group_last_error", "ffd_group_size", "ffd_group_engine",
     "ffd_group_analyze_faces", "ffd_comm_id", "ffd_engine_join", "ffd_gather_faces", "ffd_engine_comm_info",
     "ffd_detect_options_init", "ffd_detect_faces", "ffd_detect_faces_device", "ffd_analyze_images",
-    "ffd_detect_candidates", "ffd_model_open", "ffd_model_close", "ffd_model_last_error", "ffd_model_num_trees", "ffd_model_tree_save_path",
+    "ffd_detect_candidates", "ffd_detector_create", "ffd_model_open", "ffd_model_close", "ffd_model_last_error", "ffd_model_num_trees", "ffd_model_tree_save_path",
     "ffd_model_tree_archive", "ffd_model_save_tree",
-    "ffd_train_param_init", "ffd_train_mp_tree", "ffd_train_last_error", "ffd_trained_tree_num_nodes",
+    "ffd_train_param_init", "ffd_train_mp_tree", "ffd_train_mp_tree_patches", "ffd_train_last_error", "ffd_trained_tree_num_nodes",
     "ffd_trained_tree_num_leaves", "ffd_trained_tree_arrays", "ffd_trained_tree_stats", "ffd_trained_tree_archive",
     "ffd_trained_tree_save", "ffd_trained_tree_free",
     "ffd_train_hp_param_init", "ffd_train_hp_tree", "ffd_trained_tree_kind", "ffd_trained_tree_num_samples",

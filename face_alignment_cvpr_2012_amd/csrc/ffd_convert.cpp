@@ -25,6 +25,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <cerrno>
 #include <cmath>
@@ -502,11 +503,25 @@ std::string convert_model(const ForestParam& hp, const std::string& hp_dir, cons
   put_params(m, "mp", mp, (int)mp_dirs.size());
   put_forest(m, "mp", MP, mpo);
   Cascade cas;  // FaceDetectionOption::path_face_cascade as demo.cpp:186 / eval_ffd.cpp:143 set it
-  const bool have_cascade = !cascade_xml.empty() && parse_cascade(cascade_xml, cas);
+  // a cascade that is named but cannot be read fails the conversion, as CascadeClassifier::load fails the
+  // reference's constructor (FaceForest.cpp:23-27)
+  const bool have_cascade = !cascade_xml.empty();
+  if (have_cascade && !parse_cascade(cascade_xml, cas)) throw std::runtime_error("cannot open the cascade " + cascade_xml);
   if (have_cascade) put_cascade(m, cas);
-  std::string tmp = outp + ".tmp";
-  m.save(tmp);
-  if (std::rename(tmp.c_str(), outp.c_str()) != 0) throw std::runtime_error("rename failed: " + outp);
+  // a temporary name of this process and call, renamed over the target (atomic on one file system), so
+  // concurrent conversions of the same directories (one per rank) never interleave their writes
+  static std::atomic<unsigned> seq{0};
+  const std::string tmp = outp + ".tmp." + std::to_string((long)getpid()) + "." + std::to_string(seq++);
+  try {
+    m.save(tmp);
+  } catch (...) {
+    std::remove(tmp.c_str());
+    throw;
+  }
+  if (std::rename(tmp.c_str(), outp.c_str()) != 0) {
+    std::remove(tmp.c_str());
+    throw std::runtime_error("rename failed: " + outp);
+  }
   std::string msg = "hp " + std::to_string(hpo.tree_node_off.size() - 1) + " trees " +
                     std::to_string(hpo.node_leaf.size()) + " nodes " + std::to_string(hpo.leaf_n.size()) +
                     " leaves; mp " + std::to_string(mp_dirs.size()) + " forests " +
@@ -520,6 +535,20 @@ std::string convert_model(const ForestParam& hp, const std::string& hp_dir, cons
 }
 
 thread_local std::string g_convert_error;
+
+}  // namespace
+
+namespace ffd_host {
+void cascade_arrays(const std::string& xml, ffd::ModelFile& m);  // (declared in ffd_engine_impl.hpp)
+}
+// ffd_detector_create's cascade: the XML as the "haar.*" arrays ffd_convert writes
+void ffd_host::cascade_arrays(const std::string& xml, ffd::ModelFile& m) {
+  Cascade c;
+  if (!parse_cascade(xml, c)) throw std::runtime_error("cannot open the cascade " + xml);
+  put_cascade(m, c);
+}
+
+namespace {
 
 ForestParam from_c(const ffd_forest_param& c) {
   ForestParam p;
@@ -599,8 +628,11 @@ int main(int argc, char** argv) {
       throw std::runtime_error("cannot parse config_headpose.txt");
     if (!load_config(root + "/data/config_ffd.txt", mp))
       throw std::runtime_error("cannot parse config_ffd.txt");
+    std::string cascade = root + "/data/haarcascade_frontalface_alt.xml";  // (a tree without one: no detector)
+    struct stat cst;
+    if (stat(cascade.c_str(), &cst) != 0) cascade.clear();
     const std::string msg = convert_model(hp, root + "/" + hp.tree_path, mp, sorted_subdirs(root + "/" + mp.tree_path),
-                                          root + "/data/haarcascade_frontalface_alt.xml", outp);
+                                          cascade, outp);
     std::printf("ffd_convert: %s\n", msg.c_str());
   } catch (const std::exception& e) {
     std::fprintf(stderr, "ffd_convert: ERROR: %s\n", e.what());

@@ -443,6 +443,7 @@ ffd_status ffd_detect_candidates(ffd_engine* e, const ffd_image* img, const ffd_
 
 ffd_status ffd_analyze_images(ffd_engine* e, const ffd_image* imgs, int32_t n_img, const ffd_detect_options* opt,
                               ffd_face* faces, int32_t* face_img, int32_t max_faces, int32_t* n_faces) {
+  if (e && e->detector_only) return fail(e, FFD_ERR_INVALID_ARGUMENT, "a detector-only engine (ffd_detector_create) has no forests");
   return guarded_d(e, [&]() -> ffd_status {
     if (!n_faces || max_faces < 0 || (max_faces > 0 && !faces)) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     ffd_detect_options o;

@@ -41,26 +41,22 @@ constexpr uint32_t LEAF_BIT = 0x80000000u;
 //   lo = x1 | y1 << 5 | x2 << 10 | y2 << 15 | thr[5:0] << 20 | ch << 26
 //   hi = w1 | h1 << 5 | w2 << 10 | h2 << 15 | thr[9:6] << 20
 // (rectangles patch-relative, sides 1..22, threshold 10-bit two's complement), and for a leaf
-// ch = 63 (lo >= 63 << 26) with the leaf ordinal = lo[19:0] | hi << 20.  Depth-first layout per tree: the pair of
-// c0's children is the next record, c1's children are off1 records ahead (off1 = 0: the 32-bit
-// offset is far[pair]).  Each tree starts with a root pair (root, unused leaf).
+// ch = 63 (lo >= 63 << 26) with the leaf ordinal = lo[19:0] | hi << 20.
 // Source fields: ThresholdSplit<SimplePatchFeature> (ThresholdSplit.hpp:51-67, ImageSample.hpp:83-90).
 //
-// FFD_PAIR_BLOCKS (default): the records are laid out in 128-byte blocks of 8 slots holding three pair
-// levels in heap order instead: the children pair of node s of the record in slot j <= 2 is slot 2j + 1 + s
-// of the same block; the children pairs of the nodes of slots 3..6 start new blocks, node s's at record
-// index P + off1 + 8 s (off1 = 0: far[P]; when both are internal the two blocks are adjacent).  A tree's
-// first block holds the root pair in slot 0 (root, unused leaf), so the root's children pair is slot 1.
-// A walk keeps its record's slot j; a miss brings a line that serves the next two steps of the walk
-// (the depth-first layout above serves the next step only after a left turn).
-#ifndef FFD_PAIR_BLOCKS
-#define FFD_PAIR_BLOCKS 0
-#endif
-constexpr uint32_t PAIR_SLOT_SHIFT = 29;  // tree-top pair indices carry the record's block slot in bits 29..31
+// Sibling blocks: the pair records are stored in 32-byte blocks; the block B(n) of an internal node n
+// holds P(c0(n)) in half 0 and P(c1(n)) in half 1 (P(x) = the pair record of x's children; a half whose
+// child is a leaf is unused), so a walk standing on n can request both of its children's records before
+// it knows which child it takes.  Blocks are allocated depth-first: B(n), then c0's subtree's blocks
+// (B(c0) = B(n) + 1 when it exists), then c1's, and off1 of P(n) = B(c1) - B(n) (1 when c1's children are
+// both leaves: every block index a walk computes stays inside the array, which ends with one spare block);
+// off1 = 0 means the offset exceeds 16 bits and is far[2 * block + half] of the record.  Each tree starts
+// with a block holding P(root) in half 0 (the block of a virtual parent whose only child is the root).
 
 // Tree tops (k_traverse): per tree, TOP_CAP pair records of its top levels in heap order: entry 0
-// = the root pair, entry 1 = the root's children pair, entry 2h + s (h >= 1) = the children pair of
-// node s of entry h; entries under leaves are zero (never read).  Plus each entry's pair index.
+// = the root pair (root, unused leaf), entry 1 = the root's children pair, entry 2h + s (h >= 1) = the
+// children pair of node s of entry h; entries under leaves are zero (never read).  Plus, per entry
+// P(m), the sibling-block index B(m) (entry 0: the tree's first block).
 constexpr int TOP_CAP = 64;  // levels 0..6
 
 struct FaceDesc {

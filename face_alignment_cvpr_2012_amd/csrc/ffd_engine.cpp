@@ -166,147 +166,109 @@ static void encode_test(const uint4& n, uint32_t& lo, uint32_t& hi) {
   hi = w1 | h1 << 5 | w2 << 10 | h2 << 15 | (t >> 6) << 20;  // sides as they are: no +1 in the walk
 }
 
-// Depth-first pair layout: a pair (a, b) is followed by the pair of a's children and a's whole
-// subtree, then b's children pair at offset off1 (16 bits; 0 = look up far[pair]).  Each tree starts
-// with a root pair (root, unused leaf).  Leaves keep their model ordinals; speed-neutral for parity:
+// Sibling-block layout (ffd_device.hpp "sibling blocks"): out holds 2 pair records per block; roots_out[t] =
+// tree t's first block (P(root) in half 0).  Leaves keep their model ordinals; speed-neutral for parity:
 // every walk visits the same nodes in the same order as Tree<S>::evaluateMT.
-// FFD_PAIR_BLOCKS: the blocked layout of ffd_device.hpp instead (same records, other positions).
 void ffd_host::build_pair_records(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots,
                                   std::vector<uint4>& out, std::vector<int32_t>& roots_out,
                                   std::vector<uint32_t>& far) {
   out.clear();
   roots_out.clear();
   far.clear();
-  const uint4 unused_leaf = make_uint4(LEAF_BIT, 0u, 0u, 0u);
   auto pack = [](const uint4& a, const uint4& b, uint32_t o16) {
     uint32_t lo0, hi0, lo1, hi1;
     encode_test(a, lo0, hi0);
     encode_test(b, lo1, hi1);
     return make_uint4(lo0, lo1, hi0 | (o16 & 0xFFu) << 24, hi1 | (o16 >> 8) << 24);
   };
-  if (FFD_PAIR_BLOCKS) {
-    auto alloc = [&]() {  // one 8-record block
-      const size_t at = out.size();
-      out.resize(at + 8, make_uint4(0, 0, 0, 0));
-      far.resize(at + 8, 0u);
-      return at;
-    };
-    struct Item { size_t base; int slot; uint4 a, b; };
-    std::vector<Item> st;
-    for (int32_t root : roots) {
-      const size_t b0 = alloc();
-      roots_out.push_back((int32_t)b0);
-      st.push_back({b0, 0, bfs[(uint32_t)root], unused_leaf});
-      while (!st.empty()) {  // depth-first over blocks: a block's children blocks follow it closely
-        const Item it = st.back();
-        st.pop_back();
-        const size_t idx = it.base + (size_t)it.slot;
-        const bool ia = !(it.a.x & LEAF_BIT), ib = !(it.b.x & LEAF_BIT);
-        uint32_t o16 = 0;
-        if (it.slot <= 2) {
-          if (ib) st.push_back({it.base, 2 * it.slot + 2, bfs[it.b.x], bfs[it.b.x + 1]});
-          if (ia) st.push_back({it.base, 2 * it.slot + 1, bfs[it.a.x], bfs[it.a.x + 1]});
-        } else if (ia || ib) {
-          // node a's children block at idx + off, node b's at idx + off + 8: both allocated when both are
-          // internal; for b alone, off points one block before b's (a block is allocated first only when
-          // that would not leave off >= 1)
-          size_t c0;
-          if (ia) {
-            c0 = alloc();
-            if (ib) alloc();
-          } else {
-            if (out.size() < idx + 9) alloc();
-            c0 = alloc() - 8;
-          }
-          const uint64_t off = c0 - idx;
-          if (off > 0xFFFFFFFFull) throw std::runtime_error("pair array too large");
-          o16 = off <= 0xFFFFu ? (uint32_t)off : 0u;
-          if (o16 == 0) far[idx] = (uint32_t)off;
-          if (ib) st.push_back({c0 + 8, 0, bfs[it.b.x], bfs[it.b.x + 1]});
-          if (ia) st.push_back({c0, 0, bfs[it.a.x], bfs[it.a.x + 1]});
-        }
-        out[idx] = pack(it.a, it.b, o16);
-      }
-    }
-    if (out.size() >= ((size_t)1 << PAIR_SLOT_SHIFT)) throw std::runtime_error("pair array too large");
-    return;
-  }
-  // iterative DFS: a frame places pair (a, b); phase 0 = a's children, 1 = b's children, 2 = done
-  struct Frame { uint4 a, b; size_t idx; int phase; };
+  auto internal = [](const uint4& n) { return !(n.x & LEAF_BIT); };
+  auto alloc = [&]() {
+    const size_t b = out.size() / 2;
+    out.resize(out.size() + 2, make_uint4(0, 0, 0, 0));
+    far.resize(far.size() + 2, 0u);
+    return b;
+  };
+  // Place P(n) (n internal, bfs index) at record position pos and n's subtree below it.  An explicit stack:
+  // phase 0 allocates B(n) and descends into c0, phase 1 descends into c1, phase 2 writes P(n) (off1 is
+  // known once c1's block exists).
+  struct Frame { uint32_t n; size_t pos; int64_t bn, b1; int phase; };
+  std::vector<Frame> st;
   for (int32_t root : roots) {
-    std::vector<Frame> st;
-    roots_out.push_back((int32_t)out.size());
-    st.push_back({bfs[(uint32_t)root], unused_leaf, out.size(), 0});
-    out.push_back(make_uint4(0, 0, 0, 0));
-    far.push_back(0);
+    const size_t r0 = alloc();
+    roots_out.push_back((int32_t)r0);
+    if (!internal(bfs[(uint32_t)root])) continue;  // a one-leaf tree: the tops' root entry ends every walk
+    st.push_back({(uint32_t)root, 2 * r0, -1, -1, 0});
     while (!st.empty()) {
       Frame& f = st.back();
+      const uint4& a = bfs[bfs[f.n].x];
+      const uint4& b = bfs[bfs[f.n].x + 1];
       if (f.phase == 0) {
         f.phase = 1;
-        if (!(f.a.x & LEAF_BIT)) {
-          const uint32_t c = f.a.x;
-          st.push_back({bfs[c], bfs[c + 1], out.size(), 0});
-          out.push_back(make_uint4(0, 0, 0, 0));
-          far.push_back(0);
+        if (internal(a) || internal(b)) f.bn = (int64_t)alloc();
+        if (internal(a)) {
+          const size_t pos = 2 * (size_t)f.bn;
+          st.push_back({bfs[f.n].x, pos, -1, -1, 0});
         }
         continue;
       }
       if (f.phase == 1) {
         f.phase = 2;
-        const uint64_t off1 = out.size() - f.idx;  // where b's children pair goes
-        uint32_t o16 = off1 <= 0xFFFFu ? (uint32_t)off1 : 0u;
-        if (o16 == 0 && !(f.b.x & LEAF_BIT)) far[f.idx] = (uint32_t)off1;
-        if (off1 > 0xFFFFFFFFull) throw std::runtime_error("pair array too large");
-        out[f.idx] = pack(f.a, f.b, o16);
-        if (!(f.b.x & LEAF_BIT)) {
-          const uint32_t c = f.b.x;
-          const size_t at = out.size();
-          out.push_back(make_uint4(0, 0, 0, 0));
-          far.push_back(0);
-          st.push_back({bfs[c], bfs[c + 1], at, 0});
+        if (internal(b)) {
+          const size_t pos = 2 * (size_t)f.bn + 1;
+          // B(c1) is the next block allocated (if c1 has an internal child)
+          const uint4& b0 = bfs[b.x];
+          const uint4& b1 = bfs[b.x + 1];
+          if (internal(b0) || internal(b1)) f.b1 = (int64_t)(out.size() / 2);
+          st.push_back({bfs[f.n].x + 1, pos, -1, -1, 0});
         }
         continue;
       }
+      const uint64_t off1 = f.b1 >= 0 ? (uint64_t)(f.b1 - f.bn) : 1u;
+      if (off1 > 0xFFFFFFFFull) throw std::runtime_error("pair array too large");
+      const uint32_t o16 = off1 <= 0xFFFFu ? (uint32_t)off1 : 0u;
+      if (o16 == 0) far[f.pos] = (uint32_t)off1;
+      out[f.pos] = pack(a, b, o16);
       st.pop_back();
     }
   }
-  if (out.size() >= 0x80000000ull) throw std::runtime_error("pair array too large");
+  alloc();  // the spare block (a walk may request B(last) + 1, never reads it)
+  if (out.size() / 2 >= 0x80000000ull) throw std::runtime_error("pair array too large");
 }
 
 void ffd_host::build_tree_tops(const std::vector<uint4>& pairs, const std::vector<int32_t>& proots,
-                               const std::vector<uint32_t>& far, std::vector<uint4>& tops,
+                               const std::vector<uint32_t>& far, const std::vector<uint4>& bfs,
+                               const std::vector<int32_t>& roots, std::vector<uint4>& tops,
                                std::vector<uint32_t>& top_idx) {
   tops.assign(proots.size() * TOP_CAP, make_uint4(0, 0, 0, 0));
   top_idx.assign(proots.size() * TOP_CAP, 0u);
   auto leaf = [](uint32_t lo) { return (lo >> 26) == 63u; };
-  const uint32_t pmask = (1u << PAIR_SLOT_SHIFT) - 1u;
   for (size_t t = 0; t < proots.size(); t++) {
     uint4* rec = &tops[t * TOP_CAP];
-    uint32_t* idx = &top_idx[t * TOP_CAP];  // pair index | slot << PAIR_SLOT_SHIFT (blocked layout)
+    uint32_t* idx = &top_idx[t * TOP_CAP];  // block index B(m) of entry h = P(m)
+    std::vector<size_t> pos(TOP_CAP, 0);    // record position of entry h (h >= 1)
+    // entry 0: the virtual parent's pair (root, unused leaf), whose block holds P(root)
+    {
+      uint32_t lo0, hi0, lo1, hi1;
+      encode_test(bfs[(uint32_t)roots[t]], lo0, hi0);
+      encode_test(make_uint4(LEAF_BIT, 0u, 0u, 0u), lo1, hi1);
+      rec[0] = make_uint4(lo0, lo1, hi0, hi1);
+    }
     idx[0] = (uint32_t)proots[t];
-    rec[0] = pairs[idx[0]];
     std::vector<bool> live(TOP_CAP, false);
     live[0] = true;
     for (int h = 0; h < TOP_CAP; h++) {
       if (!live[h]) continue;
       const uint4 R = rec[h];
-      const uint32_t p = idx[h] & pmask, j = idx[h] >> PAIR_SLOT_SHIFT;
       for (uint32_t s = 0; s < (h ? 2u : 1u); s++) {  // the root pair's second slot is an unused leaf
         if (leaf(s ? R.y : R.x)) continue;
         const int h2 = h ? 2 * h + (int)s : 1;
         if (h2 >= TOP_CAP) continue;
-        const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
-        uint32_t q, j2 = 0;
-        if (!FFD_PAIR_BLOCKS) {
-          q = p + (s ? (off1 ? off1 : far[p]) : 1u);
-        } else if (j <= 2) {
-          q = p + j + 1 + s;
-          j2 = 2 * j + 1 + s;
-        } else {
-          q = p + (off1 ? off1 : far[p]) + 8 * s;
-        }
+        const size_t q = 2 * (size_t)idx[h] + s;  // P(c_s(m)) is half s of B(m)
+        uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
+        if (h && s && off1 == 0) off1 = far[pos[h]];
         rec[h2] = pairs[q];
-        idx[h2] = q | j2 << PAIR_SLOT_SHIFT;
+        pos[h2] = q;
+        idx[h2] = idx[h] + (s ? off1 : 1u);  // B(c_s(m))
         live[h2] = true;
       }
     }
@@ -834,6 +796,34 @@ void ffd_engine_desc_init(ffd_engine_desc* d) {
   d->ms_option.stopping_criteria = 0.05f;
 }
 
+namespace {
+// The engine's workspaces (streams, fork streams and their events) and the host-API copy stream.
+void create_streams(ffd_engine* e) {
+  for (int i = 0; i < std::max(1, e->n_streams); i++) {
+    auto w = std::make_unique<Workspace>();
+    HIP_CHECK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&w->done, hipEventDisableTiming));
+    for (int j = 1; j < std::max(e->channel_streams, 6); j++) {
+      hipStream_t f;
+      HIP_CHECK(hipStreamCreateWithFlags(&f, hipStreamNonBlocking));
+      w->fork.push_back(f);
+    }
+    for (int j = 0; j < std::max(e->channel_streams, 6); j++) {
+      hipEvent_t ev;
+      HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      w->fork_ev.push_back(ev);
+    }
+    e->ws.push_back(std::move(w));
+  }
+  HIP_CHECK(hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
+  HIP_CHECK(hipEventCreateWithFlags(&e->copy_done, hipEventDisableTiming));
+}
+
+ffd_status no_forests(ffd_engine* e) {
+  return fail(e, FFD_ERR_INVALID_ARGUMENT, "a detector-only engine (ffd_detector_create) has no forests");
+}
+}  // namespace
+
 ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   if (!out) return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "out is NULL");
   *out = nullptr;
@@ -866,24 +856,7 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
       return fail(nullptr, FFD_ERR_DEVICE, "no HIP device available (the engine has no CPU fallback)");
     if (d->device < 0 || d->device >= ndev) return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "bad device ordinal");
     HIP_CHECK(hipSetDevice(d->device));
-    for (int i = 0; i < std::max(1, e->n_streams); i++) {
-      auto w = std::make_unique<Workspace>();
-      HIP_CHECK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
-      HIP_CHECK(hipEventCreateWithFlags(&w->done, hipEventDisableTiming));
-      for (int j = 1; j < std::max(e->channel_streams, 6); j++) {
-        hipStream_t f;
-        HIP_CHECK(hipStreamCreateWithFlags(&f, hipStreamNonBlocking));
-        w->fork.push_back(f);
-      }
-      for (int j = 0; j < std::max(e->channel_streams, 6); j++) {
-        hipEvent_t ev;
-        HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        w->fork_ev.push_back(ev);
-      }
-      e->ws.push_back(std::move(w));
-    }
-    HIP_CHECK(hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
-    HIP_CHECK(hipEventCreateWithFlags(&e->copy_done, hipEventDisableTiming));
+    create_streams(e.get());
     e->warm_descriptor_slots();
     e->model_path = d->model_path;
     e->load_model(d->model_path);
@@ -898,11 +871,48 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   return FFD_OK;
 }
 
+// FaceForest::detectFace's CascadeClassifier (FaceForest.cpp:136-159, FaceForest.hpp:125-132) on its own: an
+// engine that holds one Haar cascade, parsed from the OpenCV XML (the converter's reader), and no forests.
+ffd_status ffd_detector_create(const char* cascade_xml, int32_t device, ffd_engine** out) {
+  if (!out) return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "out is NULL");
+  *out = nullptr;
+  if (!cascade_xml || !*cascade_xml) return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "cascade_xml is empty");
+  std::unique_ptr<ffd_engine> e(new ffd_engine());
+  ffd_engine_desc_init(&e->desc);
+  e->desc.device = device;
+  e->device = device;
+  e->detector_only = true;
+  e->n_streams = 1;
+  try {
+    ffd::ModelFile m;
+    ffd_host::cascade_arrays(cascade_xml, m);  // (a missing or malformed file fails here, as CascadeClassifier::load)
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+      return fail(nullptr, FFD_ERR_DEVICE, "no HIP device available (the engine has no CPU fallback)");
+    if (device < 0 || device >= ndev) return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "bad device ordinal");
+    HIP_CHECK(hipSetDevice(device));
+    create_streams(e.get());
+    e->warm_descriptor_slots();
+    e->load_cascade(m);
+    HIP_CHECK(hipStreamSynchronize(e->main_stream()));
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    e->n_cu = std::max(1, prop.multiProcessorCount);
+  } catch (const HipError& x) {
+    return fail(nullptr, FFD_ERR_DEVICE, x.what());
+  } catch (const std::exception& x) {
+    return fail(nullptr, FFD_ERR_MODEL, x.what());
+  }
+  *out = e.release();
+  return FFD_OK;
+}
+
 void ffd_engine_destroy(ffd_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   release_comm(e);
   for (auto& w : e->ws) (void)hipStreamSynchronize(w->stream);
+  e->orphan_samples();  // samples that outlive their engine keep only their host state
   delete e;
 }
 
@@ -982,6 +992,7 @@ ffd_status ffd_face_geometry(const ffd_engine* e, int32_t bw, int32_t bh, int32_
 
 ffd_status ffd_analyze_faces(ffd_engine* e, const ffd_image* imgs, int32_t n_img, const ffd_rect* boxes,
                              const int32_t* box_img, int32_t n_faces, ffd_face* out) {
+  if (e && e->detector_only) return no_forests(e);
   return guarded(e, [&]() -> ffd_status {
     if (n_faces > 0 && !out) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     if (n_faces > 0) e->out.ensure((size_t)n_faces * sizeof(FaceOut));
@@ -998,6 +1009,7 @@ ffd_status ffd_analyze_faces(ffd_engine* e, const ffd_image* imgs, int32_t n_img
 ffd_status ffd_analyze_faces_device(ffd_engine* e, const void* d_images, int64_t image_bytes, int32_t width,
                                     int32_t height, int32_t stride, int32_t n_img, const ffd_rect* boxes,
                                     const int32_t* box_img, int32_t n_faces, void* d_out) {
+  if (e && e->detector_only) return no_forests(e);
   return guarded(e, [&]() -> ffd_status {
     if (n_faces < 0 || (n_faces > 0 && (!d_images || !boxes || !d_out)) || width <= 0 || height <= 0 ||
         stride < 3 * width || image_bytes < (int64_t)stride * height)
@@ -1015,6 +1027,7 @@ ffd_status ffd_analyze_faces_device(ffd_engine* e, const void* d_images, int64_t
 }
 
 ffd_status ffd_get_trace(ffd_engine* e, int32_t index, ffd_trace* tr) {
+  if (e && e->detector_only) return no_forests(e);
   return guarded(e, [&]() -> ffd_status {
     if (!tr) return fail(e, FFD_ERR_INVALID_ARGUMENT, "trace is NULL");
     if (e->last_ws < 0) return fail(e, FFD_ERR_INVALID_ARGUMENT, "no batch has run");
@@ -1068,6 +1081,7 @@ ffd_status ffd_get_trace(ffd_engine* e, int32_t index, ffd_trace* tr) {
 }
 
 ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t W, int32_t H, uint32_t* out) {
+  if (e && e->detector_only) return no_forests(e);
   return guarded(e, [&]() -> ffd_status {
     if (!gray_face || !out || W < 2 || H < 2 || W > PITCH - 3 || H > MAX_FACE_H_TALL)
       return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
@@ -1310,6 +1324,7 @@ extern "C" {
 ffd_status ffd_estimate_headpose(ffd_engine* e, const uint32_t* channels, int32_t W, int32_t H,
                                  const ffd_rect* region, const ffd_headpose_option* options, float* headpose,
                                  float* variance) {
+  if (e && e->detector_only) return no_forests(e);
   return guarded(e, [&]() -> ffd_status {
     if (!channels || W < 1 || H < 1) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     const ffd_rect full{0, 0, W, H};
@@ -1331,6 +1346,7 @@ ffd_status ffd_estimate_headpose(ffd_engine* e, const uint32_t* channels, int32_
 ffd_status ffd_estimate_facial_features(ffd_engine* e, const uint32_t* channels, int32_t W, int32_t H,
                                         const ffd_rect* region, const int32_t* tree_ids, int32_t n_trees,
                                         const ffd_multipart_option* options, int32_t* points) {
+  if (e && e->detector_only) return no_forests(e);
   return guarded(e, [&]() -> ffd_status {
     if (!channels || !points || W < 1 || H < 1) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     const ffd_rect full{0, 0, W, H};
@@ -1349,6 +1365,7 @@ ffd_status ffd_estimate_facial_features(ffd_engine* e, const uint32_t* channels,
 }
 
 ffd_status ffd_forest_leaves(ffd_engine* e, int32_t kind, const int32_t* leaf_ids, int32_t n, void* out) {
+  if (e && e->detector_only) return no_forests(e);
   return guarded(e, [&]() -> ffd_status {
     if ((n > 0 && (!leaf_ids || !out)) || n < 0) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     if (kind != FFD_FOREST_HEADPOSE && kind != FFD_FOREST_FFD) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad forest kind");
@@ -1394,6 +1411,7 @@ ffd_status ffd_forest_leaves(ffd_engine* e, int32_t kind, const int32_t* leaf_id
 ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* channels, int32_t W, int32_t H,
                                   const int32_t* patches_xy, int32_t n_patches, const int32_t* tree_ids, int32_t n_trees,
                                   int32_t* leaf_ids) {
+  if (e && e->detector_only) return no_forests(e);
   return guarded(e, [&]() -> ffd_status {
     if (!channels || (!patches_xy && n_patches) || (!tree_ids && n_trees) || (!leaf_ids && n_patches * n_trees) ||
         W < 1 || H < 1 || W > PITCH - 3 || H > MAX_FACE_H_TALL || n_patches < 0 || n_trees < 0)
@@ -1438,11 +1456,23 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* c
 // ------------------------------------------------------------------ image samples --
 // ImageSample kept on the device (ffd.h "Device-resident image samples").
 struct ffd_sample {
-  ffd_engine* e = nullptr;
+  ffd_engine* e = nullptr;  // nullptr once the engine was destroyed first (the sample is then orphaned)
+  int device = 0;
   int W = 0, H = 0;
   int64_t plane = 0;  // (H + 1) * PITCH
   DevBuf chan;        // u16 [NCH][H + 1][PITCH], integrals mod 2^16
 };
+
+void ffd_engine::orphan_samples() {
+  std::lock_guard<std::mutex> g(samples_mu);
+  for (ffd_sample* s : samples) {
+    if (s->chan.p) (void)hipFree(s->chan.p);
+    s->chan.p = nullptr;
+    s->chan.n = 0;
+    s->e = nullptr;
+  }
+  samples.clear();
+}
 
 namespace {
 
@@ -1452,6 +1482,10 @@ FaceDesc sample_desc(ffd_sample* s, int hp_step, int mp_step_x, int mp_step_y) {
   FaceDesc f = region_desc(s->e, full, hp_step, mp_step_x, mp_step_y);
   f.plane = s->plane;
   return f;
+}
+
+ffd_status orphaned() {
+  return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "the image sample's engine was destroyed (ffd_engine_destroy ran first)");
 }
 
 bool sample_size_ok(int W, int H) {
@@ -1562,12 +1596,14 @@ ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, i
 extern "C" {
 
 ffd_status ffd_sample_create(ffd_engine* e, const uint8_t* gray, int32_t W, int32_t H, int32_t stride, ffd_sample** out) {
+  if (e && e->detector_only) return no_forests(e);
   return guarded(e, [&]() -> ffd_status {
     if (!gray || !out || stride < W) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     *out = nullptr;
     if (!sample_size_ok(W, H)) return fail(e, FFD_ERR_UNSUPPORTED, "image sample size unsupported (2..125 wide, 255 W H < 2^24)");
     std::unique_ptr<ffd_sample> s(new ffd_sample);
     s->e = e;
+    s->device = e->device;
     s->W = W;
     s->H = H;
     s->plane = (int64_t)(H + 1) * PITCH;
@@ -1621,18 +1657,21 @@ ffd_status ffd_sample_create(ffd_engine* e, const uint8_t* gray, int32_t W, int3
     w.pending = false;
     if (e->last_ws == 0) e->last_ws = -1;
     *out = s.release();
+    e->track_sample(*out);
     return FFD_OK;
   });
 }
 
 ffd_status ffd_sample_create_from_channels(ffd_engine* e, const uint32_t* channels, int32_t W, int32_t H,
                                            ffd_sample** out) {
+  if (e && e->detector_only) return no_forests(e);
   return guarded(e, [&]() -> ffd_status {
     if (!channels || !out) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     *out = nullptr;
     if (!sample_size_ok(W, H)) return fail(e, FFD_ERR_UNSUPPORTED, "image sample size unsupported (2..125 wide, 255 W H < 2^24)");
     std::unique_ptr<ffd_sample> s(new ffd_sample);
     s->e = e;
+    s->device = e->device;
     s->W = W;
     s->H = H;
     s->plane = (int64_t)(H + 1) * PITCH;
@@ -1645,19 +1684,23 @@ ffd_status ffd_sample_create_from_channels(ffd_engine* e, const uint32_t* channe
     HIP_CHECK(hipMemcpyAsync(s->chan.p, J.data(), J.size() * 2, hipMemcpyHostToDevice, e->main_stream()));
     HIP_CHECK(hipStreamSynchronize(e->main_stream()));
     *out = s.release();
+    e->track_sample(*out);
     return FFD_OK;
   });
 }
 
 void ffd_sample_destroy(ffd_sample* s) {
   if (!s) return;
-  (void)hipSetDevice(s->e->device);
-  (void)hipStreamSynchronize(s->e->main_stream());
-  delete s;
+  (void)hipSetDevice(s->device);
+  if (s->e) {
+    s->e->untrack_sample(s);
+    (void)hipStreamSynchronize(s->e->main_stream());
+  }
+  delete s;  // (an orphaned sample's planes were freed with its engine)
 }
 
 ffd_status ffd_sample_size(const ffd_sample* s, int32_t* W, int32_t* H) {
-  if (!s) return FFD_ERR_INVALID_ARGUMENT;
+  if (!s) return FFD_ERR_INVALID_ARGUMENT;  // (valid on an orphaned sample too)
   if (W) *W = s->W;
   if (H) *H = s->H;
   return FFD_OK;
@@ -1665,6 +1708,7 @@ ffd_status ffd_sample_size(const ffd_sample* s, int32_t* W, int32_t* H) {
 
 ffd_status ffd_sample_channels(const ffd_sample* s, uint32_t* out) {
   if (!s) return FFD_ERR_INVALID_ARGUMENT;
+  if (!s->e) return orphaned();
   return guarded(s->e, [&]() -> ffd_status {
     if (!out) return fail(s->e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     std::vector<uint16_t> v((size_t)NCH * s->plane);
@@ -1678,6 +1722,7 @@ ffd_status ffd_sample_channels(const ffd_sample* s, uint32_t* out) {
 ffd_status ffd_sample_eval_leaves(ffd_sample* s, int32_t kind, const int32_t* patches_xy, int32_t n_patches,
                                   const int32_t* tree_ids, int32_t n_trees, int32_t* leaf_ids) {
   if (!s) return FFD_ERR_INVALID_ARGUMENT;
+  if (!s->e) return orphaned();
   return guarded(s->e, [&]() -> ffd_status {
     if (!patches_xy && n_patches) return fail(s->e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     static const int32_t none[2] = {0, 0};
@@ -1688,6 +1733,7 @@ ffd_status ffd_sample_eval_leaves(ffd_sample* s, int32_t kind, const int32_t* pa
 ffd_status ffd_sample_eval_grid(ffd_sample* s, int32_t kind, int32_t x0, int32_t y0, int32_t step, int32_t nx,
                                 int32_t ny, const int32_t* tree_ids, int32_t n_trees, int32_t* leaf_ids) {
   if (!s) return FFD_ERR_INVALID_ARGUMENT;
+  if (!s->e) return orphaned();
   return guarded(s->e, [&]() -> ffd_status {
     return sample_eval(s, kind, nullptr, 0, x0, y0, step, nx, ny, tree_ids, n_trees, leaf_ids);
   });
@@ -1696,6 +1742,7 @@ ffd_status ffd_sample_eval_grid(ffd_sample* s, int32_t kind, int32_t x0, int32_t
 ffd_status ffd_sample_estimate_headpose(ffd_sample* s, const ffd_rect* region, const ffd_headpose_option* options,
                                         float* headpose, float* variance) {
   if (!s) return FFD_ERR_INVALID_ARGUMENT;
+  if (!s->e) return orphaned();
   ffd_engine* e = s->e;
   return guarded(e, [&]() -> ffd_status {
     const ffd_rect full{0, 0, s->W, s->H};
@@ -1727,6 +1774,7 @@ ffd_status ffd_sample_estimate_headpose(ffd_sample* s, const ffd_rect* region, c
 ffd_status ffd_sample_estimate_facial_features(ffd_sample* s, const ffd_rect* region, const int32_t* tree_ids,
                                                int32_t n_trees, const ffd_multipart_option* options, int32_t* points) {
   if (!s) return FFD_ERR_INVALID_ARGUMENT;
+  if (!s->e) return orphaned();
   ffd_engine* e = s->e;
   return guarded(e, [&]() -> ffd_status {
     if (!points) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");

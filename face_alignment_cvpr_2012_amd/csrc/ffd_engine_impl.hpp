@@ -9,8 +9,10 @@
 #include <cstdint>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/ffd.h"
@@ -102,13 +104,15 @@ struct Workspace {
 };
 
 namespace ffd_host {
-// Re-encode breadth-first 16-byte nodes (children adjacent) as k_traverse's 16-byte pair records
-// in depth-first order (ffd_device.hpp "pair records"); roots_out[t] = tree t's root pair.
+// Re-encode breadth-first 16-byte nodes (children adjacent) as k_traverse's 16-byte pair records in
+// depth-first sibling blocks (ffd_device.hpp "pair records", "sibling blocks"); roots_out[t] = tree t's
+// first block (P(root) in half 0).
 void build_pair_records(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots, std::vector<uint4>& out,
                         std::vector<int32_t>& roots_out, std::vector<uint32_t>& far);
-// Heap-ordered tree tops (ffd_device.hpp "tree tops") of every tree: TOP_CAP records + pair indices.
+// Heap-ordered tree tops (ffd_device.hpp "tree tops") of every tree: TOP_CAP records + block indices.
 void build_tree_tops(const std::vector<uint4>& pairs, const std::vector<int32_t>& proots,
-                     const std::vector<uint32_t>& far, std::vector<uint4>& tops, std::vector<uint32_t>& top_idx);
+                     const std::vector<uint32_t>& far, const std::vector<uint4>& bfs, const std::vector<int32_t>& roots,
+                     std::vector<uint4>& tops, std::vector<uint32_t>& top_idx);
 }  // namespace ffd_host
 
 struct ffd_engine {
@@ -116,6 +120,7 @@ struct ffd_engine {
   int device = 0;
   ffd_engine_desc desc{};
   int max_chunk = 4096;
+  bool detector_only = false;  // ffd_detector_create: a Haar cascade and no forests
   int n_streams = 1;
   int gabor_exact = 0;      // FFD_GABOR_EXACT=1: every face through the exact (sqrtf) Gabor instance (tests)
   int channel_streams = 1;  // streams the channel stage is spread over (FFD_CHANNEL_STREAMS; 2-4 measured no gain)
@@ -135,10 +140,10 @@ struct ffd_engine {
 
   // device model
   DevBuf gabor_coef, hp_nodes, hp_roots, hp_sizes, hp_m, mp_nodes, mp_roots, mp_sizes, mp_rec;
-  DevBuf hp_pairs, mp_pairs;         // pair records for k_traverse (ffd_device.hpp "pair records")
-  DevBuf hp_proots, mp_proots;       // per tree: index of its root pair
-  DevBuf hp_far, mp_far;             // per pair: far offset of child 1's children (when > 65535)
-  DevBuf hp_tops, mp_tops, hp_topi, mp_topi;  // per tree: heap-ordered top pair records + their indices
+  DevBuf hp_pairs, mp_pairs;         // sibling blocks for k_traverse (ffd_device.hpp "sibling blocks")
+  DevBuf hp_proots, mp_proots;       // per tree: its first block
+  DevBuf hp_far, mp_far;             // per pair record: child 1's block offset (when > 65535)
+  DevBuf hp_tops, mp_tops, hp_topi, mp_topi;  // per tree: heap-ordered top pair records + their block indices
   int trav_top_max = TOP_CAP;        // tree-top entries staged per tree at most (FFD_TRAV_TOPMAX)
   std::vector<uint4> hp_nodes_h, mp_nodes_h;  // host copies until the walk nodes are built
   std::vector<int32_t> hp_roots_h, mp_roots_h;
@@ -190,6 +195,19 @@ struct ffd_engine {
   } pin_leaf, pin_patch;
   DevBuf sample_patches;
   int last_ws = -1;
+  // live image samples (ffd_sample_*): a sample destroyed after its engine must not touch the engine, so the
+  // engine frees the samples' device planes when it goes and marks them orphaned (ffd_engine_destroy)
+  std::mutex samples_mu;
+  std::unordered_set<ffd_sample*> samples;
+  void track_sample(ffd_sample* s) {
+    std::lock_guard<std::mutex> g(samples_mu);
+    samples.insert(s);
+  }
+  void untrack_sample(ffd_sample* s) {
+    std::lock_guard<std::mutex> g(samples_mu);
+    samples.erase(s);
+  }
+  void orphan_samples();  // ffd_engine.cpp
 
   hipStream_t main_stream() const { return ws[0]->stream; }
 
@@ -340,7 +358,7 @@ struct ffd_engine {
       std::vector<int32_t> rp;
       std::vector<uint32_t> far, topi;
       ffd_host::build_pair_records(h, roots, pr, rp, far);
-      ffd_host::build_tree_tops(pr, rp, far, tops, topi);
+      ffd_host::build_tree_tops(pr, rp, far, h, roots, tops, topi);
       upload(d, pr, main_stream());
       upload(droots, rp, main_stream());
       upload(dfar, far, main_stream());
@@ -379,6 +397,8 @@ ffd_status analyze_host(ffd_engine* e, const ffd_image* imgs, int32_t n_img, con
                         const int32_t* box_img, int32_t n_faces, void* d_out);
 // per-face descriptor of a box on an image (ffd_engine.cpp); returns the face's status
 ffd_status make_desc(const ffd_engine* e, int64_t img_off, int iw, int ih, int stride, const ffd_rect& b, FaceDesc& f);
+// a Haar cascade XML (OpenCV format) as the FFDMODEL "haar.*" arrays (ffd_convert.cpp); throws on failure
+void cascade_arrays(const std::string& xml, ffd::ModelFile& m);
 // the engine's per-rank RCCL communicator, if it joined one (ffd_group.cpp)
 void release_comm(const ffd_engine* e);
 }  // namespace ffd_host

@@ -917,12 +917,6 @@ __device__ __forceinline__ int node_off(uint32_t enc, int ld) {
   return (int)__umul24(enc >> 7, (unsigned)ld) + (int)(enc & 127u);
 }
 
-#ifndef FFD_TRAV_VOFF_ARRAY
-#define FFD_TRAV_VOFF_ARRAY 1  // precomputed staging offsets (0: rebuilt per block from 6 registers, no spill: FFD 8.39 -> 8.67 ms)
-#endif
-#ifndef FFD_TRAV_MID_ALWAYS
-#define FFD_TRAV_MID_ALWAYS 1  // 0: middle row only for area > 257 (exec-masked; measured slower: FFD 8.42 -> 8.52 ms)
-#endif
 // ImageSample::evalTest's rectangle mean over the LDS window (k_traverse): p = byte address of the
 // rectangle's top-left integral corner, ld2 = window row pitch in bytes.  The sum is taken as two
 // halves split at h >> 1 rows, each exact modulo 2^16 (rect_mean16), and the quotient
@@ -936,47 +930,11 @@ __device__ __forceinline__ int rect_mean_lds(const unsigned char* __restrict__ p
   const uint32_t area = __umul24(w, h);
   const uint32_t a = *reinterpret_cast<const uint16_t*>(p), b = *reinterpret_cast<const uint16_t*>(p + wb);
   const uint32_t f0 = *reinterpret_cast<const uint16_t*>(p + r2), f1 = *reinterpret_cast<const uint16_t*>(p + r2 + wb);
-#if FFD_TRAV_MID_ALWAYS
   const uint32_t c = *reinterpret_cast<const uint16_t*>(p + r1), d = *reinterpret_cast<const uint16_t*>(p + r1 + wb);
-#else
-  // The middle row only for rectangles whose sum can reach 2^16 (area > 257, ~15 % of the model's
-  // rectangles): below that the 4-corner sum mod 2^16 is exact, and c = a, d = b turn the formula
-  // below into it (top = 0, bot = the whole rectangle).  The reads are exec-masked, so the lanes at
-  // small rectangles take no part in their bank conflicts.
-  uint32_t c = a, d = b;
-  if (area > 257u) {
-    c = *reinterpret_cast<const uint16_t*>(p + r1);
-    d = *reinterpret_cast<const uint16_t*>(p + r1 + wb);
-  }
-#endif
   // top = (a - b) + (d - c), bot = (f1 - f0) - (d - c), each mod 2^16 (u16 arithmetic), R = top + bot
   typedef unsigned short u16;
   const u16 dc = (u16)(d - c), top = (u16)((u16)(a - b) + dc), bot = (u16)((u16)(f1 - f0) - dc);
   return (int)__builtin_fmaf((float)((uint32_t)top + bot), __builtin_amdgcn_rcpf((float)area), 0.00075f);
-}
-
-// rect_mean_lds split into its reads and its arithmetic, so that a walker can issue one walk's reads
-// and do another walk's arithmetic while they are in flight (k_traverse, FFD_TRAV_DUAL).
-struct RectRd {
-  uint32_t a, b, c, d, f0, f1;
-};
-__device__ __forceinline__ RectRd rect_read_lds(const unsigned char* __restrict__ p, uint32_t w, uint32_t h, uint32_t hh,
-                                               int ld2) {
-  const int wb = (int)(2u * w);
-  const int r1 = (int)__umul24(hh, (unsigned)ld2), r2 = (int)__umul24(h, (unsigned)ld2);
-  RectRd r;
-  r.a = *reinterpret_cast<const uint16_t*>(p);
-  r.b = *reinterpret_cast<const uint16_t*>(p + wb);
-  r.f0 = *reinterpret_cast<const uint16_t*>(p + r2);
-  r.f1 = *reinterpret_cast<const uint16_t*>(p + r2 + wb);
-  r.c = *reinterpret_cast<const uint16_t*>(p + r1);
-  r.d = *reinterpret_cast<const uint16_t*>(p + r1 + wb);
-  return r;
-}
-__device__ __forceinline__ int rect_mean_fin(const RectRd& r, uint32_t w, uint32_t h) {
-  typedef unsigned short u16;
-  const u16 dc = (u16)(r.d - r.c), top = (u16)((u16)(r.a - r.b) + dc), bot = (u16)((u16)(r.f1 - r.f0) - dc);
-  return (int)__builtin_fmaf((float)((uint32_t)top + bot), __builtin_amdgcn_rcpf((float)__umul24(w, h)), 0.00075f);
 }
 
 // Tree<S>::evaluateMT over global u16 planes (ffd_forest_eval_leaves hook).
@@ -1002,47 +960,27 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 // between blocks.  Blocks are dealt XCD-contiguously and face-major, so the 32 workgroups of an XCD
 // share one or two faces' planes in that XCD's L2.
 //
-// A walk holds the 16-byte pair record of the node it stands on (both siblings' 56-bit tests,
-// ffd_device.hpp "pair records"): the node's children pair is requested before its test is
-// evaluated (one 16-byte load per visit; the CU's vector-memory return path is the traversal's
-// bottleneck, profiles/r2a), and the test picks the child.
-#ifndef FFD_TRAV_PROBE
-#define FFD_TRAV_PROBE 0  // timing probes (tools/probe.sh): 1 = stage only, 2 = walk only, 3 = one tree per block,
-#endif                    // 4 = walk only without window reads, 5 = 4 with staging, 6 = deep records from 4096 pairs,
-                          // 7 = walk only reading rect 1 only, 8 = 7 with staging
-#define FFD_TRAV_NOSTAGE (FFD_TRAV_PROBE == 2 || FFD_TRAV_PROBE == 4 || FFD_TRAV_PROBE == 6 || FFD_TRAV_PROBE == 7)
+// Deep levels (below the LDS tree tops) read "sibling blocks" (ffd_device.hpp): the 32-byte block of a
+// node n holds the pair records of both its children.  A walk standing on node n (its test taken from
+// P(n's parent), already in registers) requests n's block before evaluating n's test; the block is used
+// one step later, when the walk stands on n's chosen child c and needs P(c) to select c's child's test.
+// So every record request has two tests' time to return from L2 instead of one (the round-4 walk
+// statistics put the wait for a record requested one test ahead at ~210 of ~1,000 cycles per step).
 // Walker threads per workgroup by patch-block edge G: a block's G*G*T walks run in one round (T = 20
 // FFD trees: 4x4 -> 320, 5x5 -> 500 of 512), the other threads stage the next window.  A block costs
 // about its longest walk chain, so the walks a window holds per block set the throughput: FFD 5x5
 // blocks with 512 walkers took the FFD pass from 10.4 to 8.6 ms at C2 (profiles/r2c).
 constexpr int TRAV_NT = 1024;
-#ifndef FFD_TRAV_DUAL
-#define FFD_TRAV_DUAL 0  // two walks per walker lane, software-pipelined (walk_block2): measured slower (FFD 8.9 -> 12.5 ms)
-#endif
-#ifndef FFD_TRAV_PAIR
-#define FFD_TRAV_PAIR 0  // two walker lanes per walk, one rectangle each: measured slower (FFD 8.5 -> 12.4 ms)
-#endif
-#if FFD_PAIR_BLOCKS && FFD_TRAV_DUAL
-#error "the dual walker follows the depth-first pair layout"
-#endif
-#ifndef FFD_TRAV_SPLIT_RECTS
-#define FFD_TRAV_SPLIT_RECTS 0  // scheduling barrier between the two rectangles' reads
-#endif
-__host__ __device__ constexpr int trav_nw(int GX, int GY, bool HP) {
-  return FFD_TRAV_DUAL ? ((GX * GY * (HP ? 15 : 20) + 1) / 2 + 63) / 64 * 64
-                       : (GX * GY * (HP ? 15 : 20) <= 320 ? 320 : 512);
-}
+constexpr int TRAV_DEEP_UNROLL = 18;  // deep steps unrolled (FFD: 3 LDS-top levels + 18 = depth 21)
+__host__ __device__ constexpr int trav_nw(int GX, int GY, bool HP) { return GX * GY * (HP ? 15 : 20) <= 320 ? 320 : 512; }
 // Window chunks held in registers per staging thread: 16-byte chunks when the window row pitch is
 // a multiple of 8 columns, else 8-byte chunks (the pitch also sets the LDS bank pattern of the
 // rectangle reads, so it is not padded up).
 template <int CB, int NS> struct TravStage;
 template <int NS> struct TravStage<8, NS> { static constexpr int U = (20480 + NS - 1) / NS; typedef uint32_t T __attribute__((ext_vector_type(2))); };
 template <int NS> struct TravStage<16, NS> { static constexpr int U = (11000 + NS - 1) / NS; typedef uint32_t T __attribute__((ext_vector_type(4))); };
-#ifndef FFD_TRAV_STAGE_ROWS
-#define FFD_TRAV_STAGE_ROWS 1  // staging threads own runs of window rows (affine offsets); 0: chunk i = s + u NS
-#endif
-// Row-run staging (FFD_TRAV_STAGE_ROWS): NS threads over NCH x nq chunk columns, nh row groups per column, RU
-// rows per group (the host checks RU <= TravStage::U, traverse_window_fits)
+// Row-run staging (FFD 16-byte-chunk windows): NS threads over NCH x nq chunk columns, nh row groups per
+// column, RU rows per group (the host checks RU <= TravStage::U, traverse_window_fits)
 __host__ __device__ constexpr int trav_stage_groups(int ns, int nq) { return ns / (NCH * nq); }
 __host__ __device__ constexpr int trav_stage_rows(int ns, int nq, int wh) {
   return trav_stage_groups(ns, nq) > 0 ? (wh + trav_stage_groups(ns, nq) - 1) / trav_stage_groups(ns, nq) : 1 << 20;
@@ -1051,12 +989,9 @@ __host__ __device__ constexpr int trav_stage_rows(int ns, int nq, int wh) {
 // LDS row pitch (u16) of a traversal window WW columns wide staged from a 4-element aligned column:
 // a block starting at patch x px0 is staged from column px0 & ~3, so a block x-stride (gx * step)
 // that is not a multiple of 4 needs up to 3 columns of slack.
-#ifndef FFD_TRAV_PITCH8
-#define FFD_TRAV_PITCH8 0  // 1: window pitch a multiple of 8 columns (16-byte staging chunks)
-#endif
 __host__ __device__ __forceinline__ int trav_row_pitch(int WW, int xstride) {
   const int pad = (xstride & 3) ? 3 : 0;
-  return FFD_TRAV_PITCH8 ? (WW + pad + 7) & ~7 : (WW + pad + 3) & ~3;
+  return (WW + pad + 3) & ~3;
 }
 __host__ __device__ __forceinline__ int trav_chunk_bytes(int WW, int xstride) { return trav_row_pitch(WW, xstride) % 8 == 0 ? 16 : 8; }
 
@@ -1067,8 +1002,8 @@ __host__ __device__ __forceinline__ int trav_window_bytes(int WW, int WH, int xs
 
 // Tree tops in LDS: for each of the block's T trees the first TOPN entries of its heap-ordered top
 // table (TOP_CAP entries per tree in HBM, ffd_device.hpp "tree tops"): a 16-byte pair record and its
-// global pair index each (20 B).  TOPN = the largest power of two <= top_max whose T tables fit in
-// the LDS left over by the window (FFD 4x4 window, 20 trees: 64 entries = levels 0..6).
+// sibling-block index each (20 B).  TOPN = the largest power of two <= top_max whose T tables fit in
+// the LDS left over by the window (FFD 5x5 window, 20 trees: 8 entries = levels 0..2).
 constexpr int TRAV_TOP_ENTRIES = 1400;  // tree-top entries a block stages at most (2 per staging thread)
 __host__ __device__ __forceinline__ int trav_top_n(int T, int free_bytes, int top_max, int cap = TRAV_TOP_ENTRIES) {
   int n = TOP_CAP;
@@ -1078,36 +1013,15 @@ __host__ __device__ __forceinline__ int trav_top_n(int T, int free_bytes, int to
 
 constexpr int BUF_WORD3 = 0x00020000;  // raw buffer resource word 3 (gfx950: 32-bit data format)
 
-// Walk statistics (measurement builds only, tools/trav_stats.py): per (workgroup, block iteration,
-// wave) one record of 8 u32 — walker waves 0..7: {t0 (shader clock, low 32 bits, after the window
-// barrier), walk cycles, visits in the LDS tops, deep visits (node fetches), longest walk of the wave,
-// walks, longest deep part, block}; slot 8 (first stager wave): {t after barrier 1, commit cycles
-// (waits for its window loads), 0, 0, 0, 0, 0, block}.
-#ifndef FFD_TRAV_STATS
-#define FFD_TRAV_STATS 0
-#endif
-#if FFD_TRAV_STATS
-constexpr int TRAV_STATS_ITERS = 1024, TRAV_STATS_SLOTS = 9;
-__device__ uint32_t* g_trav_stats[2];  // [hp]
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-  for (int o = 32; o; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o, 64));
-  return v;
-}
-#endif
-
 constexpr int TRAV_BLK_BYTES = 64;  // the block descriptor the stagers hand to the walkers (end of the LDS)
 struct TravArgs {
   const FaceDesc* faces;
   int n_faces, bpf;        // blocks per face: ceil(nx/G) * ceil(ny/G) (max over the batch)
-  const uint4* pairs;      // pair records
+  const uint4* pairs;      // sibling blocks (2 pair records each)
   const uint4* tops;       // per tree: TOP_CAP heap-ordered pair records (levels 0..6)
-  const uint32_t* top_idx; // ... and their global pair indices
+  const uint32_t* top_idx; // ... and the sibling-block index of each entry's node
   int top_free, top_max;   // LDS bytes after the window; cap on the entries staged per tree
-  const uint32_t* far;     // per pair: offset of child 1's children pair when it exceeds 16 bits
+  const uint32_t* far;     // per pair record: child 1's block offset when it exceeds 16 bits
   const HpState* hp_state; // FFD pass: selected trees; nullptr for the head-pose pass
   int ntrees_hp;           // head-pose pass: number of trees
   int step, step_y;        // patch grid steps (x, y)
@@ -1126,7 +1040,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   // tree-top entries a block stages at most: one per staging thread for the FFD 16-byte-chunk windows (the
   // 44 x 44 window leaves LDS for 8 levels-0..2 entries per tree; more registers would spill the stager role)
   constexpr int TOP_E = (!HP && CB == 16) ? NS : (TRAV_TOP_ENTRIES + NS - 1) / NS * NS;
-  constexpr bool ROWS = FFD_TRAV_STAGE_ROWS && !HP && CB == 16;  // row-run staging (below)
+  constexpr bool ROWS = !HP && CB == 16;  // row-run staging (below)
   const int tid = threadIdx.x;
   // window: WW integral columns x WH rows (steps may differ per axis: step_y, C4's (2, 1) grid)
   const int step = A.step, stepy = A.step_y, WW = 32 + step * (GX - 1), WH = 32 + stepy * (GY - 1);
@@ -1171,97 +1085,31 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     return B;
   };
 
-#if FFD_TRAV_STATS
-  uint32_t st_top = 0, st_deep = 0, st_max = 0, st_walks = 0, st_maxdeep = 0, st_ttest = 0, st_tfetch = 0;
-  uint32_t st_ph[4] = {0, 0, 0, 0};  // FFD_TRAV_STATS == 3: setup, top levels, deep levels, store (cycles)
-  uint64_t st_t0 = 0;
-#define TRAV_STAMP(v) \
-  uint64_t v;         \
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory")
-#endif
   auto walk_block = [&](const Blk& B) {
     const int items = GG * B.T, sh = B.px0 & 3;
     int32_t* out = A.leaf_out + (int64_t)(((uint64_t)(uint32_t)B.out_hi << 32) | (uint32_t)B.out_lo);
     const int ld2 = 2 * LW, chs2 = 2 * WH * LW;  // window row / channel-plane strides (bytes)
     const int topn = trav_top_n(B.T, A.top_free, A.top_max, TOP_E);
     const uint32_t* top_i = reinterpret_cast<const uint32_t*>(top_rec + B.T * topn);
-#if FFD_TRAV_PAIR
-    // pair walkers: lanes 2k and 2k + 1 walk the same (patch, tree), each reading one of the node's two
-    // rectangles (6 LDS reads per lane and step instead of 12); the means are swapped by a DPP quad permute
-    const int half = tid & 1;
-    for (int item = tid >> 1; item < items; item += NW / 2) {
-#else
     for (int item = tid; item < items; item += NW) {
-#endif
       const int t = item / GG, pl = item - t * GG;
       const int xi = B.xi0 + pl % GX, yi = B.yi0 + pl / GX;
       if (xi >= B.nx || yi >= B.ny) continue;
-#if FFD_TRAV_STATS == 3
-      TRAV_STAMP(ph_a);
-      st_ph[0] += (uint32_t)(ph_a - st_t0);
-#endif
       // byte address of the patch's top-left integral corner in channel 0's window plane
       const unsigned char* base = reinterpret_cast<const unsigned char*>(win) +
                                   2 * ((yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh);
+      // (fields by bit-field extracts; bits of hi above 23 are the record's child offset, never read)
       auto test = [&](uint32_t lo, uint32_t hi) {
-#if FFD_TRAV_PROBE == 4 || FFD_TRAV_PROBE == 5
-        return ((lo ^ (hi >> 3)) >> 9) & 1u;  // probe: no window reads
-#endif
-#if FFD_TRAV_PROBE == 9  // probe: the 12 reads at wave-uniform addresses (LDS broadcast, no conflicts), same VALU
-        auto rect9 = [&](int k, uint32_t w, uint32_t h) {
-          const unsigned char* p = reinterpret_cast<const unsigned char*>(win) + 64 * k;
-          const uint32_t area = __umul24(w, h);
-          const uint32_t a = *reinterpret_cast<const uint16_t*>(p), b = *reinterpret_cast<const uint16_t*>(p + 8);
-          const uint32_t f0 = *reinterpret_cast<const uint16_t*>(p + 16), f1 = *reinterpret_cast<const uint16_t*>(p + 24);
-          const uint32_t c = *reinterpret_cast<const uint16_t*>(p + 32), d = *reinterpret_cast<const uint16_t*>(p + 40);
-          typedef unsigned short u16;
-          const u16 dc = (u16)(d - c + w), top = (u16)((u16)(a - b) + dc), bot = (u16)((u16)(f1 - f0) - dc);
-          return (int)__builtin_fmaf((float)((uint32_t)top + bot), __builtin_amdgcn_rcpf((float)area), 0.00075f);
-        };
-        const int q1 = rect9(0, __builtin_amdgcn_ubfe(hi, 0, 5), __builtin_amdgcn_ubfe(hi, 5, 5));
-        const int q2 = rect9(1, __builtin_amdgcn_ubfe(hi, 10, 5), __builtin_amdgcn_ubfe(hi, 15, 5));
-        const int thr9 = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
-        return (q1 - q2 + (int)(lo & 31u) - 16) <= thr9 ? 0u : 1u;
-#elif FFD_TRAV_PAIR
-        // this lane's rectangle: fields at bit 0 (rectangle 1) or 10 (rectangle 2) of lo (x, y) and hi (w, h)
         const unsigned char* cb = base + __umul24(lo >> 26, (unsigned)chs2);
-        const uint32_t f = half ? 10u : 0u;
-        const int pm = rect_mean_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, f + 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, f, 5),
-                                     __builtin_amdgcn_ubfe(hi, f, 5), __builtin_amdgcn_ubfe(hi, f + 5, 5),
-                                     __builtin_amdgcn_ubfe(hi, f + 6, 4), ld2);
-        const int po = __builtin_amdgcn_mov_dpp(pm, 0xB1, 0xF, 0xF, false);  // quad_perm [1, 0, 3, 2]: the partner's mean
-        const int d12 = half ? po - pm : pm - po;                              // p1 - p2 on both lanes
-        const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
-        return d12 <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
-#else
-        // (fields by bit-field extracts; bits of hi above 23 are the record's child offset, never read)
-        const unsigned char* cb = base + __umul24(lo >> 26, (unsigned)chs2);
-#if FFD_TRAV_SPLIT_RECTS  // rectangle 1's reads issued before rectangle 2's addresses are computed
-        const uint32_t w1 = __builtin_amdgcn_ubfe(hi, 0, 5), h1 = __builtin_amdgcn_ubfe(hi, 5, 5);
-        const RectRd r1 = rect_read_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 0, 5),
-                                        w1, h1, __builtin_amdgcn_ubfe(hi, 6, 4), ld2);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t w2 = __builtin_amdgcn_ubfe(hi, 10, 5), h2 = __builtin_amdgcn_ubfe(hi, 15, 5);
-        const RectRd r2 = rect_read_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 15, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 10, 5),
-                                        w2, h2, __builtin_amdgcn_ubfe(hi, 16, 4), ld2);
-        __builtin_amdgcn_sched_barrier(0);
-        const int p1 = rect_mean_fin(r1, w1, h1), p2 = rect_mean_fin(r2, w2, h2);
-#else
         const int p1 = rect_mean_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 0, 5),
                                      __builtin_amdgcn_ubfe(hi, 0, 5), __builtin_amdgcn_ubfe(hi, 5, 5),
                                      __builtin_amdgcn_ubfe(hi, 6, 4), ld2);
-#if FFD_TRAV_PROBE == 7 || FFD_TRAV_PROBE == 8  // probe: the second rectangle is not read
-        const int p2 = (int)(hi >> 24);
-#else
         const int p2 = rect_mean_lds(cb + __umul24(__builtin_amdgcn_ubfe(lo, 15, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(lo, 10, 5),
                                      __builtin_amdgcn_ubfe(hi, 10, 5), __builtin_amdgcn_ubfe(hi, 15, 5),
                                      __builtin_amdgcn_ubfe(hi, 16, 4), ld2);
-#endif
-#endif
         // 10-bit two's complement: sign-extended thr[9:6] (hi[23:20]) above thr[5:0] (lo[25:20])
         const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(lo, 20, 6));
         return (p1 - p2) <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
-#endif
       };
       // levels 0..log2(topn): heap-ordered pair records in LDS (the children pair of node (h, s) is
       // entry 2h + s, of the root (h = 0) entry 1)
@@ -1269,288 +1117,74 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       uint32_t h = 0, s = 0;
       uint4 R = trec[0];
       uint32_t lo = R.x, hi = R.z;
-#if FFD_TRAV_STATS
-      uint32_t wt = 0, wd = 0;
-#endif
       while (lo < (63u << 26)) {  // not a leaf (ch = 63)
         const uint32_t h2 = h ? 2u * h + s : 1u;
         if (h2 >= (uint32_t)topn) break;
-        const uint4 N = trec[h2];
-#if FFD_TRAV_STATS
-        wt++;
-#endif
+        const uint4 Nr = trec[h2];
         s = test(lo, hi);
         h = h2;
-        R = N;
+        R = Nr;
         lo = s ? R.y : R.x;
         hi = s ? R.w : R.z;
       }
-      uint32_t P = top_i[t * topn + h];
-#if FFD_PAIR_BLOCKS
-      uint32_t j = P >> PAIR_SLOT_SHIFT;  // the record's block slot
-      P &= (1u << PAIR_SLOT_SHIFT) - 1u;
-#endif
-#if FFD_TRAV_STATS == 3
-      TRAV_STAMP(ph_b);
-      st_ph[1] += (uint32_t)(ph_b - ph_a);
-#endif
-#if FFD_TRAV_PROBE == 6
-      int probe_depth = 0;
-#endif
-      // deeper levels: pair records from HBM (L2), the children pair requested before the test
-      while (lo < (63u << 26)) {  // not a leaf (ch = 63)
-        // children pair of the current node: right after its pair (child 0), or off1 away (child 1)
-        const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
-#if FFD_PAIR_BLOCKS
-        // in-block children pair: slot 2j + 1 + s; from slots 3..6: block off1 (+ 8 for node 1) away
-        uint32_t Q = j <= 2u ? P + j + 1u + s : P + off1 + (s << 3);
-        if (j > 2u && off1 == 0u) Q = P + A.far[P] + (s << 3);
-        j = j <= 2u ? 2u * j + 1u + s : 0u;
-#else
-        uint32_t Q = P + (s ? off1 : 1u);
-        if (s && off1 == 0u) Q = P + A.far[P];
-#endif
-#if FFD_TRAV_PROBE == 6
-        const uint4 N = A.pairs[Q & 4095u];
-        if (++probe_depth > 24) break;
-#else
-        const uint4 N = A.pairs[Q];
-#endif
-#if FFD_TRAV_STATS
-        wd++;
-#endif
-#if FFD_TRAV_STATS == 2  // step timing: test (LDS reads + VALU) vs the wait for the fetched record
-        uint64_t ta, tb, tc;
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ta)::"memory");
-#endif
-        s = test(lo, hi);
-#if FFD_TRAV_STATS == 2
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tb) : "v"(s) : "memory");
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tc) : "v"(N.x), "v"(N.w) : "memory");
-        st_ttest += (uint32_t)(tb - ta);
-        st_tfetch += (uint32_t)(tc - tb);
-#endif
-        P = Q;
-        R = N;
-        lo = s ? R.y : R.x;
-        hi = s ? R.w : R.z;
+      if (lo < (63u << 26)) {
+        // Deep levels.  State: the current node c (its test lo / hi), bc = c's sibling block, bp = the block of
+        // c's parent m, which holds P(c) in half sp.  Entry h of the tops is P(m); its block index is
+        // top_i[h]; child 1's block offset is in the record's top bytes (0: far[] at the record's position,
+        // 2 top_i[h >> 1] + (h & 1) for a top entry, 2 bp + sp below).
+        const uint32_t* ti = top_i + t * topn;
+        uint32_t bp = ti[h], sp = s;
+        const uint32_t o = (R.z >> 24) | ((R.w >> 24) << 8);
+        uint32_t bc = bp + (s ? o : 1u);
+        if (s && o == 0u) {  // (the far value consumed inside the branch, as in step below)
+          uint32_t fo = A.far[2u * ti[h >> 1] + (h > 1u ? (h & 1u) : 0u)];
+          asm volatile("" : "+v"(fo));
+          bc = bp + fo;
+          asm volatile("" : "+v"(bc));
+        }
+        // One step: request c's block into (nl, nh), take c's test, select P(c) from the block requested one
+        // step earlier (pl, ph) and c's chosen child's test from it.  The loop is unrolled by two so the two
+        // blocks swap roles instead of being copied (a register copy of a block still in flight would wait
+        // for it, and with it for the block just requested).
+        auto step = [&](const uint4& pl, const uint4& ph, uint4& nl, uint4& nh) {
+          nl = A.pairs[2u * bc];
+          nh = A.pairs[2u * bc + 1u];
+          const uint32_t sn = test(lo, hi);
+          const uint4 P = sp ? ph : pl;  // P(c): the tests of c's two children
+          const uint32_t o1 = (P.z >> 24) | ((P.w >> 24) << 8);
+          uint32_t nb = bc + (sn ? o1 : 1u);
+          if (sn && o1 == 0u) {
+            // (rare: an offset past 16 bits.)  The far value is consumed inside the branch, so its wait stays
+            // here instead of becoming a vmcnt(0) after the join, which would also wait for c's block
+            uint32_t fo = A.far[2u * bp + sp];
+            asm volatile("" : "+v"(fo));
+            nb = bc + fo;
+            asm volatile("" : "+v"(nb));
+          }
+          lo = sn ? P.y : P.x;
+          hi = sn ? P.w : P.z;
+          bp = bc;
+          bc = nb;
+          sp = sn;
+          return lo >= (63u << 26);
+        };
+        uint4 Xl = A.pairs[2u * bp], Xh = A.pairs[2u * bp + 1u];  // m's block: P(c) in half sp
+        uint4 Yl, Yh;
+        // straight-line steps (no loop-carried block registers for the allocator to split), then a loop for
+        // walks deeper than TRAV_DEEP_UNROLL steps
+        bool fin = false;
+#pragma unroll
+        for (int d = 0; d < TRAV_DEEP_UNROLL; d += 2) {
+          if (step(Xl, Xh, Yl, Yh)) { fin = true; break; }
+          if (step(Yl, Yh, Xl, Xh)) { fin = true; break; }
+        }
+        if (!fin)
+          while (!step(Xl, Xh, Yl, Yh) && !step(Yl, Yh, Xl, Xh)) {
+          }
       }
-#if FFD_TRAV_STATS == 3
-      TRAV_STAMP(ph_c);
-      st_ph[2] += (uint32_t)(ph_c - ph_b);
-#endif
-#if FFD_TRAV_STATS
-      st_top += wt;
-      st_deep += wd;
-      st_max = max(st_max, wt + wd);
-      st_maxdeep = max(st_maxdeep, wd);
-      st_walks++;
-#endif
-#if FFD_TRAV_PAIR
-      if (!half)
-#endif
       out[(xi * B.ny + yi) * B.T + t] = (int32_t)((lo & 0xFFFFFu) | hi << 20);  // reference order
-#if FFD_TRAV_STATS == 3
-      __builtin_amdgcn_s_waitcnt(0);
-      TRAV_STAMP(ph_d);
-      st_ph[3] += (uint32_t)(ph_d - ph_c);
-#endif
     }
   };
-
-  // Two walks per walker lane (FFD_TRAV_DUAL): items tid and tid + NW.  A step of one walk is a chain
-  // of a 16-byte record fetch (L2) and twelve LDS reads followed by the test's arithmetic; the walker
-  // interleaves the two chains so that one walk's reads are in flight while the other walk's test is
-  // computed (issue A, finish B, issue B, finish A), instead of a wave waiting on its own reads with
-  // every other walker wave queued on the same LDS (tools/trav_stats.py: the window reads' bank
-  // conflicts were ~40 % of a deep step).  Finished and empty walks keep stepping on a dummy state
-  // (channel 0 at the window origin, broadcast reads; record 0) until both walks of every lane of the
-  // wave are done; each walk's leaf is stored once, after the loop.
-#if FFD_TRAV_DUAL
-  auto walk_block2 = [&](const Blk& B) {
-    const int items = GG * B.T, sh = B.px0 & 3;
-    int32_t* out = A.leaf_out + (int64_t)(((uint64_t)(uint32_t)B.out_hi << 32) | (uint32_t)B.out_lo);
-    const int ld2 = 2 * LW, chs2 = 2 * WH * LW;
-    const int topn = trav_top_n(B.T, A.top_free, A.top_max, TOP_E), lgn = __builtin_ctz(topn);
-    const uint32_t* top_i = reinterpret_cast<const uint32_t*>(top_rec + B.T * topn);
-    const unsigned char* w0 = reinterpret_cast<const unsigned char*>(win);
-    constexpr uint32_t LEAF = 63u << 26;  // lo >= LEAF: a leaf (ch = 63)
-    struct Walk {
-      const unsigned char* base;  // the patch's top-left integral corner in channel 0's window plane
-      uint32_t lo, hi;            // the node's test fields (hi[31:24]: the pair's child offset byte)
-      uint32_t P, off1, s;        // its pair record's index, child 1's children-pair offset, sibling
-      uint32_t res;               // the leaf (reference leaf word), once reached
-      int oi, t;                  // output index (reference order; -1: no walk), tree slot
-      bool live;
-    };
-    auto init = [&](int item, Walk& w) {
-      w.base = w0;
-      w.lo = w.hi = w.P = w.off1 = w.s = w.res = 0;
-      w.oi = -1;
-      w.t = 0;
-      w.live = false;
-      if (item < items) {
-        const int t = item / GG, pl = item - t * GG;
-        const int xi = B.xi0 + pl % GX, yi = B.yi0 + pl / GX;
-        if (xi < B.nx && yi < B.ny) {
-          w.base = w0 + 2 * ((yi - B.yi0) * stepy * LW + (xi - B.xi0) * step + sh);
-          w.oi = (xi * B.ny + yi) * B.T + t;
-          w.t = t;
-          w.live = true;
-        }
-      }
-    };
-    auto reads = [&](const Walk& w, RectRd& r1, RectRd& r2) {
-      const unsigned char* cb = w.base + __umul24(w.lo >> 26, (unsigned)chs2);
-      r1 = rect_read_lds(cb + __umul24(__builtin_amdgcn_ubfe(w.lo, 5, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(w.lo, 0, 5),
-                         __builtin_amdgcn_ubfe(w.hi, 0, 5), __builtin_amdgcn_ubfe(w.hi, 5, 5), __builtin_amdgcn_ubfe(w.hi, 6, 4), ld2);
-      r2 = rect_read_lds(cb + __umul24(__builtin_amdgcn_ubfe(w.lo, 15, 5), (unsigned)ld2) + 2 * __builtin_amdgcn_ubfe(w.lo, 10, 5),
-                         __builtin_amdgcn_ubfe(w.hi, 10, 5), __builtin_amdgcn_ubfe(w.hi, 15, 5), __builtin_amdgcn_ubfe(w.hi, 16, 4), ld2);
-    };
-    auto decide = [&](const Walk& w, const RectRd& r1, const RectRd& r2) -> uint32_t {
-      const int p1 = rect_mean_fin(r1, __builtin_amdgcn_ubfe(w.hi, 0, 5), __builtin_amdgcn_ubfe(w.hi, 5, 5));
-      const int p2 = rect_mean_fin(r2, __builtin_amdgcn_ubfe(w.hi, 10, 5), __builtin_amdgcn_ubfe(w.hi, 15, 5));
-      const int thr = (int)(((uint32_t)__builtin_amdgcn_sbfe((int)w.hi, 20, 4) << 6) | __builtin_amdgcn_ubfe(w.lo, 20, 6));
-      return (p1 - p2) <= thr ? 0u : 1u;  // Sample::eval: test <= threshold -> left (MPSample.cpp:77-84)
-    };
-    // a walk stands on a node: record R (its pair), s (which sibling); take that node's fields
-    auto stand = [&](Walk& w, const uint4& R, uint32_t s) {
-      w.s = s;
-      w.lo = s ? R.y : R.x;
-      w.hi = s ? R.w : R.z;
-      w.off1 = (R.z >> 24) | ((R.w >> 24) << 8);
-    };
-    // a walk that reached a leaf keeps its word and steps on the dummy state from then on
-    auto settle = [&](Walk& w) {
-      if (w.live && w.lo >= LEAF) {
-        w.res = (w.lo & 0xFFFFFu) | w.hi << 20;
-        w.live = false;
-      }
-      if (!w.live) {
-        w.base = w0;
-        w.lo = w.hi = w.s = w.off1 = w.P = 0;
-      }
-    };
-    // children pair of the node a walk stands on: right after its pair (child 0), or off1 away (child 1)
-    // (the far lookup is entered by whole waves and its result used inside: a load that may or may not have
-    // been issued before the join would make the record fetch wait for the other walk's fetch, vmcnt(0))
-    auto next_q = [&](const Walk& w) -> uint32_t {
-      uint32_t Q = w.P + (w.s ? w.off1 : 1u);
-      const bool fq = w.live && w.s && w.off1 == 0u;
-      if (__builtin_amdgcn_ballot_w64(fq)) {
-        const uint32_t fo = A.far[w.P];     // (far has an entry per pair; P of a finished walk is 0)
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), here rather than after the join
-        Q = fq ? w.P + fo : Q;
-      }
-      return w.live ? Q : 0u;
-    };
-    auto run = [&](int i0) {
-      Walk a, b;
-      init(i0 + tid, a);
-      init(i0 + tid + NW, b);
-#if FFD_TRAV_STATS
-      uint32_t la = 0, lb2 = 0, it = 0;  // visits of a / b, deep iterations
-#endif
-#if FFD_TRAV_STATS == 3
-      TRAV_STAMP(ph_a);
-      st_ph[0] += (uint32_t)(ph_a - st_t0);
-#endif
-      // levels 0..lgn-1: heap-ordered pair records in LDS (children pair of node (h, s): entry 2h + s, of the root 1)
-      {
-        const uint4* ra = top_rec + a.t * topn;
-        const uint4* rb = top_rec + b.t * topn;
-        uint32_t ha = 0, hb = 0;
-        stand(a, ra[0], 0);
-        stand(b, rb[0], 0);
-        settle(a);
-        settle(b);
-        for (int lv = 0; lv < lgn; lv++) {
-          const uint32_t h2a = ha ? 2u * ha + a.s : 1u, h2b = hb ? 2u * hb + b.s : 1u;
-          const uint4 Na = ra[a.live ? h2a : 0u], Nb = rb[b.live ? h2b : 0u];
-          RectRd a1, a2, b1, b2;
-          reads(a, a1, a2);
-          reads(b, b1, b2);
-          const uint32_t sa = decide(a, a1, a2), sb = decide(b, b1, b2);
-          if (a.live) {
-            ha = h2a;
-            stand(a, Na, sa);
-          }
-          if (b.live) {
-            hb = h2b;
-            stand(b, Nb, sb);
-          }
-          settle(a);
-          settle(b);
-        }
-        a.P = a.live ? top_i[a.t * topn + ha] : 0u;
-        b.P = b.live ? top_i[b.t * topn + hb] : 0u;
-#if FFD_TRAV_STATS
-        // (top visits: a walk that is live after the top levels made all lgn of them)
-        la = a.live ? lgn : 0;
-        lb2 = b.live ? lgn : 0;
-        st_top += la + lb2;
-#endif
-      }
-#if FFD_TRAV_STATS == 3
-      TRAV_STAMP(ph_b);
-      st_ph[1] += (uint32_t)(ph_b - ph_a);
-#endif
-      // deeper levels: pair records from L2; issue a, finish b, issue b, finish a
-      RectRd b1, b2;
-      uint32_t Qb = next_q(b);
-      uint4 Nb = A.pairs[Qb];
-      reads(b, b1, b2);
-      while (__builtin_amdgcn_ballot_w64(a.live || b.live)) {
-        const uint32_t Qa = next_q(a);
-        const uint4 Na = A.pairs[Qa];
-        RectRd a1, a2;
-        reads(a, a1, a2);
-#if FFD_TRAV_STATS
-        it++;
-        la += a.live;
-        lb2 += b.live;
-        st_deep += (uint32_t)a.live + (uint32_t)b.live;
-#endif
-        {
-          const uint32_t sb = decide(b, b1, b2);
-          if (b.live) {
-            b.P = Qb;
-            stand(b, Nb, sb);
-          }
-          settle(b);
-        }
-        Qb = next_q(b);
-        Nb = A.pairs[Qb];
-        reads(b, b1, b2);
-        {
-          const uint32_t sa = decide(a, a1, a2);
-          if (a.live) {
-            a.P = Qa;
-            stand(a, Na, sa);
-          }
-          settle(a);
-        }
-      }
-#if FFD_TRAV_STATS == 3
-      TRAV_STAMP(ph_c);
-      st_ph[2] += (uint32_t)(ph_c - ph_b);
-#endif
-      if (a.oi >= 0) out[a.oi] = (int32_t)a.res;
-      if (b.oi >= 0) out[b.oi] = (int32_t)b.res;
-#if FFD_TRAV_STATS
-      st_max = max(st_max, max(la, lb2));
-      st_maxdeep = max(st_maxdeep, it);
-      st_walks += (uint32_t)(a.oi >= 0) + (uint32_t)(b.oi >= 0);
-#endif
-#if FFD_TRAV_STATS == 3
-      __builtin_amdgcn_s_waitcnt(0);
-      TRAV_STAMP(ph_d);
-      st_ph[3] += (uint32_t)(ph_d - ph_c);
-#endif
-    };
-    for (int i0 = 0; i0 < items; i0 += 2 * NW) run(i0);
-  };
-#endif
 
   // Stager waves and walker waves run separate loops with the same barrier sequence per block
   // (waves are wholly one role), so the staging registers are live only in the stager loop and
@@ -1583,8 +1217,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     // (chunk index form) chunk (c, r, q) of this thread's first chunk and the (c, r, q) step between its chunks
     const int dq = NS % nq, dr = (NS / nq) % WH, dc = NS / (nq * WH);
     const int q0 = s0 % nq, r0 = (s0 / nq) % WH, c0 = s0 / (nq * WH);
-#if FFD_TRAV_VOFF_ARRAY  // round-2 form: the U offsets precomputed once
-    int voffs[ROWS ? 1 : U];
+    int voffs[ROWS ? 1 : U];  // the U source offsets, precomputed once
     if constexpr (!ROWS) {
       int q = q0, r = r0, c = c0;
 #pragma unroll
@@ -1599,7 +1232,6 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         c += dc + cr;
       }
     }
-#endif
     auto prefetch = [&](const Blk& B) {
       if (!B.ok) return;
       const FaceDesc& fd = A.faces[B.f];
@@ -1620,18 +1252,13 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         for (int u = 0; u < TU; u++) {
           const int e = tid - NW + u * NS;
           if (e < B.T * topn) {
-#if FFD_TRAV_PROBE == 3 || defined(FFD_TRAV_SAMETREE)  // locality probe: every tree slot walks the block's first tree
-            const int j = e >> lg, tree = HP ? 0 : A.hp_state[B.f].trees[0];
-#else
             const int j = e >> lg, tree = HP ? j : A.hp_state[B.f].trees[j];
-#endif
             const int g = tree * TOP_CAP + (e & (topn - 1));
             top_nd[u] = reinterpret_cast<const rec_t*>(A.tops)[g];
             top_p[u] = A.top_idx[g];
           }
         }
       }
-#if !FFD_TRAV_NOSTAGE
       if constexpr (ROWS) {
         const int vb = min(sc, NCH - 1) * A.plane * 2 + r_lo * (PITCH * 2) + sq * CB;
 #pragma unroll
@@ -1642,32 +1269,13 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
           }
         }
       } else {
-#if FFD_TRAV_VOFF_ARRAY
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int voff = voffs[u];
-        if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, base_b, 0);
-        else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, base_b, 0);
+        for (int u = 0; u < U; u++) {
+          const int voff = voffs[u];
+          if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, base_b, 0);
+          else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, base_b, 0);
+        }
       }
-#else
-      const int plane_b = A.plane * 2;
-      int q = q0, r = r0, c = c0;
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int voff = min(c, NCH) * plane_b + r * (PITCH * 2) + q * CB;
-        if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, base_b, 0);
-        else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, base_b, 0);
-        q += dq;
-        int cr = q >= nq;
-        q -= cr ? nq : 0;
-        r += dr + cr;
-        cr = r >= WH;
-        r -= cr ? WH : 0;
-        c += dc + cr;
-      }
-#endif
-      }
-#endif
     };
     auto commit = [&](const Blk& B) {
       if (tid == NW) *blk_lds = B;  // the walkers' block (read after the barrier)
@@ -1685,7 +1293,6 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
           }
         }
       }
-#if !FFD_TRAV_NOSTAGE  // the walk-only probes keep the tree tops (walks need valid records)
       if constexpr (ROWS) {
         unsigned char* db = smem + ((sc * WH + r_lo) * nq + sq) * CB;
 #pragma unroll
@@ -1696,29 +1303,13 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         for (int u = 0; u < U; u++)
           if (u * NS + s < total) dst[u * NS + s] = st[u];
       }
-#endif
     };
 
     Blk cur = block(lb);
     prefetch(cur);
-#if FFD_TRAV_STATS
-    int iter = 0;
-#endif
     for (; lb < end; lb += nk) {
       __syncthreads();  // the previous block's walks are done with the window
-#if FFD_TRAV_STATS
-      const uint64_t tc0 = __builtin_amdgcn_s_memtime();
-#endif
       commit(cur);
-#if FFD_TRAV_STATS
-      __builtin_amdgcn_s_waitcnt(0);
-      const uint64_t tc1 = __builtin_amdgcn_s_memtime();
-      if (tid == NW && iter < TRAV_STATS_ITERS) {
-        uint32_t* r = g_trav_stats[HP] + ((size_t)(blockIdx.x * TRAV_STATS_ITERS + iter) * TRAV_STATS_SLOTS + 8) * 8;
-        r[0] = (uint32_t)tc0; r[1] = (uint32_t)(tc1 - tc0); r[7] = (uint32_t)lb;
-      }
-      iter++;
-#endif
       __syncthreads();  // the window holds block lb
       Blk nxt;
       nxt.ok = false;
@@ -1727,49 +1318,13 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       cur = nxt;
     }
   } else {
-#if FFD_TRAV_STATS
-    int iter = 0;
-#endif
     for (; lb < end; lb += nk) {
       __syncthreads();
       __syncthreads();
-#if FFD_TRAV_STATS
-      const uint64_t t0 = __builtin_amdgcn_s_memtime();
-      st_top = st_deep = st_max = st_walks = st_maxdeep = 0;
-      st_t0 = t0;
-#endif
-#if FFD_TRAV_PROBE != 1
       Blk cur = *blk_lds;
       cur.ok = __builtin_amdgcn_readfirstlane(cur.ok);
       cur.T = __builtin_amdgcn_readfirstlane(cur.T);
-#if FFD_TRAV_DUAL
-      if (cur.ok) walk_block2(cur);
-#else
       if (cur.ok) walk_block(cur);
-#endif
-#endif
-#if FFD_TRAV_STATS
-#if FFD_TRAV_STATS == 2  // per wave: test cycles and fetch-wait cycles summed over its deep steps
-      const uint32_t a0 = wave_max(st_ttest), a1 = wave_max(st_tfetch), a2 = wave_max(st_max), a3 = wave_sum(st_walks),
-                     a4 = wave_max(st_maxdeep);
-      st_ttest = st_tfetch = 0;
-#elif FFD_TRAV_STATS == 3  // per wave: the phases (setup, top levels, deep levels, store) in fields 2, 3, 4, 6
-      const uint32_t a0 = wave_max(st_ph[0]), a1 = wave_max(st_ph[1]), a2 = wave_max(st_ph[2]), a3 = wave_sum(st_walks),
-                     a4 = wave_max(st_ph[3]);
-      st_ph[0] = st_ph[1] = st_ph[2] = st_ph[3] = 0;
-#else
-      const uint32_t a0 = wave_sum(st_top), a1 = wave_sum(st_deep), a2 = wave_max(st_max), a3 = wave_sum(st_walks),
-                     a4 = wave_max(st_maxdeep);
-#endif
-      __builtin_amdgcn_s_waitcnt(0);
-      const uint64_t t1 = __builtin_amdgcn_s_memtime();
-      if ((tid & 63) == 0 && iter < TRAV_STATS_ITERS) {
-        uint32_t* r = g_trav_stats[HP] + ((size_t)(blockIdx.x * TRAV_STATS_ITERS + iter) * TRAV_STATS_SLOTS + (tid >> 6)) * 8;
-        r[0] = (uint32_t)t0; r[1] = (uint32_t)(t1 - t0); r[2] = a0; r[3] = a1; r[4] = a2; r[5] = a3; r[6] = a4;
-        r[7] = (uint32_t)lb;
-      }
-      iter++;
-#endif
     }
   }
 }
@@ -3121,7 +2676,7 @@ bool traverse_window_fits(TravShape g, bool hp, int step, int step_y, int lds_ca
   const int cb = trav_chunk_bytes(WW, g.gx * step);
   const int ns = TRAV_NT - trav_nw(g.gx, g.gy, hp);
   const int u = cb == 16 ? (11000 + ns - 1) / ns : (20480 + ns - 1) / ns;  // TravStage<cb, ns>::U
-  if (FFD_TRAV_STAGE_ROWS && !hp && cb == 16 && trav_stage_rows(ns, trav_row_pitch(WW, g.gx * step) * 2 / cb, WH) > u)
+  if (!hp && cb == 16 && trav_stage_rows(ns, trav_row_pitch(WW, g.gx * step) * 2 / cb, WH) > u)
     return false;
   return traverse_lds_bytes(g, step, step_y) <= lds_cap && NCH * WH * (trav_row_pitch(WW, g.gx * step) * 2 / cb) <= ns * u;
 }
@@ -3178,24 +2733,6 @@ hipError_t set_gabor_lds_limit(int bytes) {
   return e;
 }
 
-#if FFD_TRAV_STATS
-// Measurement builds: allocate / read the walk statistics (tools/trav_stats.py).
-extern "C" int ffd_trav_stats_enable(void) {
-  for (int k = 0; k < 2; k++) {
-    uint32_t* p = nullptr;
-    const size_t bytes = (size_t)256 * TRAV_STATS_ITERS * TRAV_STATS_SLOTS * 8 * 4;
-    if (hipMalloc(&p, bytes) != hipSuccess || hipMemset(p, 0, bytes) != hipSuccess) return -1;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_trav_stats), &p, sizeof(p), k * sizeof(p)) != hipSuccess) return -2;
-  }
-  return 0;
-}
-extern "C" int ffd_trav_stats_read(int hp, void* dst, size_t bytes) {
-  uint32_t* p[2];
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(p, HIP_SYMBOL(g_trav_stats), sizeof(p)) != hipSuccess) return -2;
-  return hipMemcpy(dst, p[hp ? 1 : 0], bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
-}
-#endif
 
 hipError_t set_traverse_lds_limit(int bytes) {
   hipError_t e = hipSuccess;

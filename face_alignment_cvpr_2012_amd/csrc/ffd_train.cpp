@@ -222,7 +222,10 @@ void build_channels(std::vector<TrImage>& ti, const std::vector<const uint8_t*>&
 
 void put_common(ffd::ModelFile& m, const char* P, const ffd_train_param& p, int64_t i_node, uint64_t NN);
 
-ffd_status train(const ffd_train_param& P, const ffd_train_image* imgs, int n_img, ffd_trained_tree& out) {
+// fixed / n_fixed: the caller's patches as (image, x, y) triples (Tree<MPSample>(samples, ...) of a caller that drew
+// them itself, train_ffd.cpp:102-111) instead of npatches draws per image from tree_seed
+ffd_status train(const ffd_train_param& P, const ffd_train_image* imgs, int n_img, ffd_trained_tree& out,
+                 const int32_t* fixed = nullptr, int64_t n_fixed = 0) {
   const double t0 = now_ms();
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(FFD_ERR_DEVICE, "no HIP device");
@@ -248,22 +251,35 @@ ffd_status train(const ffd_train_param& P, const ffd_train_image* imgs, int n_im
       return fail(FFD_ERR_INVALID_ARGUMENT, "training image " + std::to_string(i) + ": bad size or NULL data");
     ti[i].w = im.width;
     ti[i].h = im.height;
-    for (int j = 0; j < P.npatches; j++) {
+  }
+  const int64_t n_draw = fixed ? n_fixed : (int64_t)n_img * P.npatches;
+  for (int64_t k = 0; k < n_draw; k++) {
+    {
       TrSample t;
-      t.img = i;
-      t.x = uniform_int(rng, 1, im.width - ps - 2);  // rand_x() first (train_ffd.cpp:108)
-      t.y = uniform_int(rng, 1, im.height - ps - 2);
+      if (fixed) {
+        t.img = fixed[3 * k];
+        t.x = fixed[3 * k + 1];
+        t.y = fixed[3 * k + 2];
+        if (t.img < 0 || t.img >= n_img || t.x < 0 || t.y < 0 || t.x + ps > imgs[t.img].width ||
+            t.y + ps > imgs[t.img].height)
+          return fail(FFD_ERR_INVALID_ARGUMENT, "patch " + std::to_string(k) + " outside its training image");
+      } else {
+        t.img = (int)(k / P.npatches);
+        t.x = uniform_int(rng, 1, imgs[t.img].width - ps - 2);  // rand_x() first (train_ffd.cpp:108)
+        t.y = uniform_int(rng, 1, imgs[t.img].height - ps - 2);
+      }
+      const ffd_train_image& im = imgs[t.img];
       HSample h;
       const int cx = t.x + ps / 2, cy = t.y + ps / 2;
       h.pos = false;
-      for (int k = 0; k < 10; k++) {
-        h.off[k][0] = im.parts[2 * k] - cx;
-        h.off[k][1] = im.parts[2 * k + 1] - cy;
-        const float fx = (float)h.off[k][0] / (float)P.face_size, fy = (float)h.off[k][1] / (float)P.face_size;
+      for (int q = 0; q < 10; q++) {
+        h.off[q][0] = im.parts[2 * q] - cx;
+        h.off[q][1] = im.parts[2 * q + 1] - cy;
+        const float fx = (float)h.off[q][0] / (float)P.face_size, fy = (float)h.off[q][1] / (float)P.face_size;
         const float d = (float)std::sqrt((double)fx * fx + (double)fy * fy);
-        h.prob[k] = ffd_expf(-d / LAMDA);
-        if (h.prob[k] > PATCH_CLOSE_TO_FEATURE) h.pos = true;
-        prob.push_back(h.prob[k]);
+        h.prob[q] = ffd_expf(-d / LAMDA);
+        if (h.prob[q] > PATCH_CLOSE_TO_FEATURE) h.pos = true;
+        prob.push_back(h.prob[q]);
       }
       ts.push_back(t);
       hs.push_back(h);
@@ -760,7 +776,13 @@ void ffd_train_param_init(ffd_train_param* p) {
 
 ffd_status ffd_train_mp_tree(const ffd_train_param* p, const ffd_train_image* images, int32_t n_images,
                              ffd_trained_tree** out) {
-  if (!p || !images || !out || n_images <= 0) return fail(FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+  return ffd_train_mp_tree_patches(p, images, n_images, nullptr, 0, out);
+}
+
+ffd_status ffd_train_mp_tree_patches(const ffd_train_param* p, const ffd_train_image* images, int32_t n_images,
+                                     const int32_t* patches, int64_t n_patches, ffd_trained_tree** out) {
+  if (!p || !images || !out || n_images <= 0 || n_patches < 0 || (n_patches && !patches))
+    return fail(FFD_ERR_INVALID_ARGUMENT, "bad arguments");
   *out = nullptr;
   if (p->max_depth < 1 || p->max_depth > 24 || p->min_patches < 1 || p->ntests < 1 || p->npatches < 0 ||
       p->face_size < 1 || !(p->patch_size_ratio > 0))
@@ -769,7 +791,7 @@ ffd_status ffd_train_mp_tree(const ffd_train_param* p, const ffd_train_image* im
   if (!t) return fail(FFD_ERR_OUT_OF_MEMORY, "out of host memory");
   ffd_status st;
   try {
-    st = train(*p, images, n_images, *t);
+    st = train(*p, images, n_images, *t, patches, n_patches);
   } catch (const HipError& e) {
     st = fail(FFD_ERR_DEVICE, e.what());
   } catch (const std::bad_alloc&) {

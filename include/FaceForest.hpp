@@ -20,9 +20,14 @@
 //   Forest<HeadPoseSample|MPSample>                 (Forest.hpp: load, evaluateMT(const S*, S::Leaf**),
 //                                                   numberOfTrees, getTree / addTree / cleanForest / setParam)
 //   MeanShift::shift                                (MeanShift.hpp:41-76, on the GPU)
-// With OpenCV available, Mat / Rect / Point / CascadeClassifier are OpenCV's; otherwise the minimal PODs below.
-// Define FFD_GLOBAL_NAMES (or include the forwarding headers Constants.hpp / face_utils.hpp / MeanShift.hpp of
-// this directory) for the reference's global names.
+//   loadImage, getHeadPoseVotesMT, getFacialFeaturesVotesMT, areaUnderCurve (face_utils.hpp), the Constants.hpp
+//   identifiers, Tree<MPSample>(samples, param, rng, save_path) with MPSample's training constructor (grown on the
+//   GPU, ffd_train_mp_tree_patches), CascadeClassifier::load + the static detectFace with that classifier
+// With OpenCV available, Mat / Rect / Point / CascadeClassifier are OpenCV's; otherwise minimal stand-ins with
+// OpenCV's signatures (no OpenCV is installed where this was built, so the OpenCV branch is uncompiled here).
+// The names are global, as the reference declares them; the forwarding headers of this directory (Constants.hpp,
+// face_utils.hpp, MeanShift.hpp, Forest.hpp, Tree.hpp, ImageSample.hpp, MPSample.hpp, HeadPoseSample.hpp) give a
+// reference source its own include set.  FFD_NO_GLOBAL_NAMES keeps them in namespace ffd only.
 //
 // Forest<S>::evaluateMT, the reference's per-patch call (face_utils.cpp:210-216, 267-274: one thread-pool task
 // per patch, the Forest bound BY VALUE), evaluates on the GPU: the first call for an image sample walks every
@@ -43,10 +48,13 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <ctime>
 #include <deque>
 #include <fstream>
 #include <memory>
@@ -61,6 +69,7 @@
 
 #if defined(FFD_WITH_OPENCV) || (defined(__has_include) && __has_include(<opencv2/core/core.hpp>) && !defined(FFD_NO_OPENCV))
 #include <opencv2/core/core.hpp>
+#include <opencv2/highgui/highgui.hpp>
 #include <opencv2/objdetect/objdetect.hpp>
 #define FFD_HAVE_OPENCV 1
 #endif
@@ -74,40 +83,89 @@ using Point = cv::Point;
 using CascadeClassifier = cv::CascadeClassifier;
 inline const uint8_t* mat_data(const Mat& m) { return m.data; }
 inline int mat_step(const Mat& m) { return (int)m.step; }
+using Point2f = cv::Point2f;
+using cv::norm;
 #else
+// Without OpenCV: the few cv::Mat / Rect / Point members the reference's mains and FaceForest use, with
+// OpenCV's signatures (the cv:: names below alias these).
+#ifndef CV_8UC1
+#define CV_8UC1 0
+#endif
+#ifndef CV_8UC3
+#define CV_8UC3 16
+#endif
 struct Rect {
   int x = 0, y = 0, width = 0, height = 0;
   Rect() = default;
   Rect(int x_, int y_, int w_, int h_) : x(x_), y(y_), width(w_), height(h_) {}
+  bool operator==(const Rect& o) const { return x == o.x && y == o.y && width == o.width && height == o.height; }
 };
 struct Point {
   int x = 0, y = 0;
   Point() = default;
   Point(int x_, int y_) : x(x_), y(y_) {}
   Point& operator+=(const Point& o) { x += o.x; y += o.y; return *this; }
+  Point& operator*=(float s) {  // saturate_cast<int> of the product: cvRound (half to even)
+    x = (int)std::nearbyint(x * s);
+    y = (int)std::nearbyint(y * s);
+    return *this;
+  }
+  bool operator==(const Point& o) const { return x == o.x && y == o.y; }
 };
-struct Mat {  // 8-bit image view (cv::Mat data / rows / cols / step / channels): BGR 8UC3 or gray 8UC1
-  const uint8_t* data = nullptr;
+inline Point operator-(const Point& a, const Point& b) { return Point(a.x - b.x, a.y - b.y); }
+inline Point operator+(const Point& a, const Point& b) { return Point(a.x + b.x, a.y + b.y); }
+struct Point2f {
+  float x = 0.f, y = 0.f;
+  Point2f() = default;
+  Point2f(float x_, float y_) : x(x_), y(y_) {}
+};
+inline Point2f operator-(const Point2f& a, const Point2f& b) { return Point2f(a.x - b.x, a.y - b.y); }
+inline double norm(const Point& p) { return std::sqrt((double)p.x * p.x + (double)p.y * p.y); }
+inline double norm(const Point2f& p) { return std::sqrt((double)p.x * p.x + (double)p.y * p.y); }
+// cv::Mat stand-in: an 8-bit BGR (CV_8UC3) or gray (CV_8UC1) image, a view of caller memory (the OpenCV
+// constructor Mat(rows, cols, type, data, step)) or owning its pixels (Mat(rows, cols, type), loadImage);
+// img(rect) is a view of the ROI as in OpenCV.
+struct Mat {
+  uint8_t* data = nullptr;
   int rows = 0, cols = 0;
   size_t step = 0;
   int cn = 3;
+  std::shared_ptr<std::vector<uint8_t>> own;
   Mat() = default;
-  Mat(int rows_, int cols_, const uint8_t* data_, size_t step_ = 0, int channels_ = 3)
-      : data(data_), rows(rows_), cols(cols_), step(step_ ? step_ : (size_t)cols_ * channels_), cn(channels_) {}
-  int channels() const { return cn; }
-  bool empty() const { return !data || rows <= 0 || cols <= 0; }
-};
-// cv::CascadeClassifier stand-in: remembers the XML path (the detector itself is the converted cascade of the
-// engine, ffd_detect_faces)
-struct CascadeClassifier {
-  std::string path;
-  bool load(const std::string& p) {
-    struct stat st;
-    if (stat(p.c_str(), &st) != 0) return false;
-    path = p;
-    return true;
+  Mat(int rows_, int cols_, int type, void* data_, size_t step_ = 0)
+      : data(static_cast<uint8_t*>(data_)), rows(rows_), cols(cols_), cn(channels_of(type)) {
+    step = step_ ? step_ : (size_t)cols_ * cn;
   }
-  bool empty() const { return path.empty(); }
+  Mat(int rows_, int cols_, int type) : rows(rows_), cols(cols_), cn(channels_of(type)) {
+    step = (size_t)cols_ * cn;
+    own = std::make_shared<std::vector<uint8_t>>(step * (size_t)std::max(rows_, 0));
+    data = own->data();
+  }
+  // (earlier spelling of this header: rows, cols, data, step, channels)
+  Mat(int rows_, int cols_, const uint8_t* data_, size_t step_ = 0, int channels_ = 3)
+      : data(const_cast<uint8_t*>(data_)), rows(rows_), cols(cols_),
+        step(step_ ? step_ : (size_t)cols_ * channels_), cn(channels_) {}
+  int channels() const { return cn; }
+  int type() const { return cn == 1 ? CV_8UC1 : CV_8UC3; }
+  bool empty() const { return !data || rows <= 0 || cols <= 0; }
+  Mat operator()(const Rect& r) const {
+    if (r.x < 0 || r.y < 0 || r.width < 0 || r.height < 0 || r.x + r.width > cols || r.y + r.height > rows)
+      throw std::out_of_range("Mat: ROI outside the image");
+    Mat m(*this);
+    m.data = data + (size_t)r.y * step + (size_t)r.x * cn;
+    m.rows = r.height;
+    m.cols = r.width;
+    return m;
+  }
+  Mat clone() const {
+    Mat m(rows, cols, type());
+    for (int y = 0; y < rows; y++) std::memcpy(m.data + (size_t)y * m.step, data + (size_t)y * step, (size_t)cols * cn);
+    return m;
+  }
+  static int channels_of(int type) {
+    if (type != CV_8UC1 && type != CV_8UC3) throw std::invalid_argument("Mat: only CV_8UC1 / CV_8UC3 images");
+    return type == CV_8UC1 ? 1 : 3;
+  }
 };
 inline const uint8_t* mat_data(const Mat& m) { return m.data; }
 inline int mat_step(const Mat& m) { return (int)m.step; }
@@ -128,6 +186,12 @@ struct ForestParam {  // include/Constants.hpp:24-60
   std::vector<int> features;  // feature channels
   int getPatchSize() { return static_cast<int>(std::round(face_size * patch_size_ratio)); }
 };
+
+// Class identifiers (include/Constants.hpp:61-67)
+static const float TRAIN_IMAGES_PERCENTAGE = 0.9f;
+static const int NUM_HEADPOSE_CLASSES = 5;
+static const float NORM_HEADPOSE_VARIANCE_FACTOR = 0.05f;
+static const float PATCH_CLOSE_TO_FEATURE = 0.09f;
 
 // loadConfigFile (face_utils.cpp:50-140): (caption line, value line) pairs in a fixed order; the reference's
 // defaults when the file cannot be opened (and false).
@@ -215,6 +279,51 @@ inline void enlargeFace(Mat img, Rect& enlarge_bbox, FaceAnnotation& annotation)
   enlarge_bbox = intersect(aux, Rect(0, 0, img.cols, img.rows));
   annotation.bbox = Rect(0, 0, enlarge_bbox.width, enlarge_bbox.height);
   for (auto& p : annotation.parts) p += offset;
+}
+
+// loadImage (face_utils.cpp:18-28): the file `name` in the directory of `path`, as an 8-bit BGR image; an empty
+// Mat when it cannot be read.  With OpenCV this is cv::imread; without it (image decoding is outside the
+// engine) binary PPM (P6) and PGM (P5) files are read, which is what the bundled tools write.
+inline Mat loadImage(std::string path, std::string name) {
+  const std::size_t pos = path.rfind("/") + 1;
+  const std::string filename = path.substr(0, pos) + name;
+#ifdef FFD_HAVE_OPENCV
+  return cv::imread(filename, 1);  // IMREAD_COLOR
+#else
+  std::ifstream f(filename, std::ios::binary);
+  if (!f) return Mat();
+  auto token = [&]() {
+    std::string t;
+    char c;
+    while (f.get(c)) {
+      if (c == '#') { std::string line; std::getline(f, line); continue; }
+      if (std::isspace((unsigned char)c)) { if (!t.empty()) break; continue; }
+      t.push_back(c);
+    }
+    return t;
+  };
+  const std::string magic = token();
+  if (magic != "P6" && magic != "P5") return Mat();
+  int w = 0, h = 0, mx = 0;
+  try {
+    w = std::stoi(token());
+    h = std::stoi(token());
+    mx = std::stoi(token());
+  } catch (...) {
+    return Mat();
+  }
+  if (w <= 0 || h <= 0 || mx != 255) return Mat();
+  const int cn = magic == "P6" ? 3 : 1;
+  std::vector<uint8_t> px((size_t)w * h * cn);
+  if (!f.read(reinterpret_cast<char*>(px.data()), (std::streamsize)px.size())) return Mat();
+  Mat m(h, w, CV_8UC3);
+  for (size_t i = 0; i < (size_t)w * h; i++) {
+    uint8_t* d = m.data + 3 * i;
+    if (cn == 3) { d[0] = px[3 * i + 2]; d[1] = px[3 * i + 1]; d[2] = px[3 * i]; }  // RGB -> BGR
+    else d[0] = d[1] = d[2] = px[i];
+  }
+  return m;
+#endif
 }
 
 struct FaceDetectionOption {  // include/FaceForest.hpp:21-32
@@ -358,6 +467,42 @@ inline std::vector<std::string> subdirs(const std::string& dir) {
 inline float cv_round_f(float v) { return std::nearbyint(v); }  // cvRound: round half to even
 }  // namespace detail
 
+#ifndef FFD_HAVE_OPENCV
+// cv::CascadeClassifier stand-in, the classifier the static FaceForest::detectFace takes (include/FaceForest.hpp:
+// 125-132): load() reads the XML (OpenCV's BOOST / HAAR stump format) into an engine of its own that holds only
+// that cascade on the GPU (ffd_detector_create, device $FFD_DEVICE or 0); detectFace runs it.  false (and
+// empty()) when the file cannot be read, as OpenCV's load.  Copies share the detector.
+class CascadeClassifier {
+ public:
+  CascadeClassifier() = default;
+  explicit CascadeClassifier(const std::string& filename) { load(filename); }
+  bool load(const std::string& filename) {
+    det_.reset();
+    path_.clear();
+    const char* dv = std::getenv("FFD_DEVICE");
+    ffd_engine* e = nullptr;
+    if (ffd_detector_create(filename.c_str(), dv ? std::atoi(dv) : 0, &e) != FFD_OK) {
+      err_ = ffd_last_error(nullptr);
+      return false;
+    }
+    det_ = std::shared_ptr<ffd_engine>(e, [](ffd_engine* x) {
+      std::lock_guard<std::mutex> g(detail::engine_mutex(x));
+      ffd_engine_destroy(x);
+    });
+    path_ = filename;
+    return true;
+  }
+  bool empty() const { return !det_; }
+  const std::string& path() const { return path_; }
+  const std::string& last_error() const { return err_; }
+  ffd_engine* engine() const { return det_.get(); }
+
+ private:
+  std::string path_, err_;
+  std::shared_ptr<ffd_engine> det_;
+};
+#endif
+
 // ------------------------------------------------------------------ ImageSample --
 // ImageSample (include/ImageSample.hpp:146-190, src/ImageSample.cpp:11-20,77-90): the 38 integral feature
 // channels of a scaled gray face, extracted by the engine's HIP kernels and kept in HBM (ffd_sample_create).
@@ -386,7 +531,11 @@ class ImageSample {
     st_->w = cols;
     st_->hgt = rows;
     st_->id = detail::next_sample_id();
+    st_->gray.resize((size_t)cols * rows);  // (the training images of Tree<MPSample>(samples, ...))
+    for (int y = 0; y < rows; y++) std::memcpy(&st_->gray[(size_t)y * cols], gray + (size_t)y * step, (size_t)cols);
   }
+  // the 8-bit gray image the channels were extracted from (rows x cols, row pitch cols)
+  const std::vector<uint8_t>& gray() const { return st_->gray; }
   int width() const { return st_->w; }
   int height() const { return st_->hgt; }
   ffd_engine* engine() const { return st_->engine; }
@@ -414,6 +563,7 @@ class ImageSample {
     uint64_t id = 0;
     std::mutex mu;
     std::vector<uint32_t> ch;
+    std::vector<uint8_t> gray;
     ~State() {
       if (!h) return;
       std::lock_guard<std::mutex> g(detail::engine_mutex(engine));
@@ -454,7 +604,16 @@ struct MPSample {
   const ImageSample* image;
   Rect roi;
   MPSample(const ImageSample* i, Rect r) : image(i), roi(r) {}
+  // Training (MPSample.hpp:36-44, MPSample.cpp:13-41): the annotated landmarks of the sample's image; the part
+  // offsets and probabilities are computed where the tree is grown (Tree<MPSample>(samples, ...), on the GPU)
+  MPSample(const ImageSample* i, Rect r, const std::vector<Point> annotation_parts, float face_size_, bool label_,
+           float lamda_ = 0.125f)
+      : image(i), roi(r), parts(annotation_parts), face_size(face_size_), label(label_), lamda(lamda_) {}
   Rect getPatch() const { return roi; }
+  std::vector<Point> parts;  // (training samples only)
+  float face_size = 0.f;
+  bool label = false;
+  float lamda = 0.125f;
 };
 template <class S> struct ForestKind;
 template <> struct ForestKind<HeadPoseSample> {
@@ -479,10 +638,63 @@ template <> struct ForestKind<MPSample> {
   }
 };
 
-// Tree<S> (include/Tree.hpp): a tree of the engine's model, by global id (head pose 0..14, FFD forest*20 + t).
+// Tree<S> (include/Tree.hpp): a tree of the engine's model, by global id (head pose 0..14, FFD forest*20 + t), or
+// a tree grown from training samples.
 template <class S> struct Tree {
   int32_t id = -1;
   ffd_engine* engine = nullptr;
+  Tree() = default;
+  Tree(int32_t id_, ffd_engine* e) : id(id_), engine(e) {}
+  // Training (Tree.hpp:43-64: grow from the samples, then save() to save_path), S = MPSample: the samples' images
+  // and patches go to the GPU trainer (ffd_train_mp_tree_patches); the rng's type is the caller's (the reference
+  // passes a boost::mt19937*; its draws were spent on the patches, the split search has generators of its own,
+  // seeded per stripe by std::time as SplitGen does, or by $FFD_SPLIT_SEED).  Throws on failure.
+  template <class Rng>
+  Tree(const std::vector<S*>& samples, ForestParam param, Rng* rng, std::string save_path) {
+    (void)rng;
+    std::vector<const ImageSample*> imgs;
+    std::vector<std::vector<int32_t>> parts;
+    std::vector<int32_t> patches;
+    for (const S* smp : samples) {
+      size_t k = 0;
+      while (k < imgs.size() && imgs[k] != smp->image) k++;
+      std::vector<int32_t> pv;
+      for (const Point& q : smp->parts) pv.insert(pv.end(), {q.x, q.y});
+      if (pv.size() != 2 * FFD_NUM_LANDMARKS) throw std::invalid_argument("Tree: a training sample needs 10 parts");
+      if (smp->lamda != 0.125f || (int)smp->face_size != param.face_size)
+        throw std::invalid_argument("Tree: training samples must use lamda 0.125 and the param's face_size");
+      if (k == imgs.size()) {
+        imgs.push_back(smp->image);
+        parts.push_back(pv);
+      } else if (parts[k] != pv) {
+        throw std::invalid_argument("Tree: the samples of one image must carry the same annotation");
+      }
+      patches.insert(patches.end(), {(int32_t)k, smp->roi.x, smp->roi.y});
+    }
+    std::vector<ffd_train_image> ti(imgs.size());
+    for (size_t k = 0; k < imgs.size(); k++)
+      ti[k] = ffd_train_image{imgs[k]->gray().data(), imgs[k]->width(), imgs[k]->height(), imgs[k]->width(),
+                              parts[k].data()};
+    ffd_train_param tp;
+    ffd_train_param_init(&tp);
+    tp.max_depth = param.max_depth; tp.min_patches = param.min_patches; tp.ntests = param.ntests;
+    tp.ntrees = param.ntrees; tp.nimages = param.nimages; tp.npatches = param.npatches;
+    tp.face_size = param.face_size; tp.patch_size_ratio = param.patch_size_ratio;
+    tp.tree_path = param.tree_path.c_str();
+    tp.image_path = param.image_path.c_str();
+    tp.save_path = save_path.c_str();
+    const char* seed = std::getenv("FFD_SPLIT_SEED");
+    tp.split_seed = seed ? (uint32_t)std::strtoul(seed, nullptr, 10) : (uint32_t)std::time(nullptr);
+    const char* dv = std::getenv("FFD_DEVICE");
+    tp.device = dv ? std::atoi(dv) : 0;
+    ffd_trained_tree* t = nullptr;
+    if (ffd_train_mp_tree_patches(&tp, ti.data(), (int32_t)ti.size(), patches.data(), (int64_t)(patches.size() / 3), &t) != FFD_OK)
+      throw std::runtime_error(std::string("Tree: training failed: ") + ffd_train_last_error());
+    trained.reset(t, ffd_trained_tree_free);
+    if (ffd_trained_tree_save(t, save_path.c_str()) != FFD_OK)  // Tree::save (Tree.hpp:239-256)
+      throw std::runtime_error(std::string("Tree: cannot save ") + save_path + ": " + ffd_train_last_error());
+  }
+  std::shared_ptr<ffd_trained_tree> trained;  // (a grown tree: ffd_trained_tree_* reads its nodes and leaves)
 };
 
 // Forest<S> (include/Forest.hpp): a list of the engine's trees (value semantics, as the reference's vector of
@@ -511,7 +723,7 @@ template <class S> class Forest {
   void addTree(int32_t id) {
     TreeList& l = mut();
     l.ids.push_back(id);
-    l.trees.push_back(Tree<S>{id, engine_});
+    l.trees.push_back(Tree<S>(id, engine_));
   }
   Tree<S>* getTree(int idx) { return &mut().trees.at(idx); }
   void cleanForest() { list_ = std::make_shared<TreeList>(); }
@@ -708,6 +920,87 @@ class MeanShift {
   }
 };
 
+// ------------------------------------------------------------------ face_utils --
+// getHeadPoseVotesMT (face_utils.cpp:183-242) over any head-pose forest: the patch grid of face_bbox, every tree's
+// leaf through Forest::evaluateMT (one GPU evaluation of the grid), then the reference's float sums on the host.
+inline void getHeadPoseVotesMT(const ImageSample& sample, const Forest<HeadPoseSample>& forest, Rect face_bbox,
+                               float* headpose, float* variance,
+                               HeadPoseEstimatorOption options = HeadPoseEstimatorOption()) {
+  const int patch_size = forest.getParam().getPatchSize() > 0 ? forest.getParam().getPatchSize() : 31;
+  const int num_trees = forest.numberOfTrees();
+  std::vector<HeadPoseSample> samples;
+  for (int x = face_bbox.x; x < face_bbox.x + face_bbox.width - patch_size; x += options.step_size)
+    for (int y = face_bbox.y; y < face_bbox.y + face_bbox.height - patch_size; y += options.step_size)
+      samples.push_back(HeadPoseSample(&sample, Rect(x, y, patch_size, patch_size)));
+  Forest<HeadPoseSample> f(forest);
+  f.setGridStep(options.step_size);
+  std::vector<HeadPoseLeaf*> leafs(samples.size() * num_trees);
+  for (size_t i = 0; i < samples.size(); i++) f.evaluateMT(&samples[i], &leafs[i * num_trees]);
+  float n = 0, sum = 0, sum_sq = 0;
+  for (size_t i = 0; i < leafs.size(); ++i) {
+    if (leafs[i]->hp_foreground > options.min_foreground_probability) {
+      float m = 0;  // predicted label [0..4]
+      for (int j = 0; j < options.num_head_pose_labels; j++) m += leafs[i]->hp_labels[j] * j;
+      m /= (leafs[i]->hp_nsamples * leafs[i]->hp_foreground);
+      sum += m;
+      sum_sq += m * m;
+      n++;
+    }
+  }
+  float mean = sum / n;
+  float var = (sum_sq / n) - (mean * mean);
+  mean -= 2;
+  var *= NORM_HEADPOSE_VARIANCE_FACTOR;
+  *headpose = mean;
+  *variance = var;
+}
+
+// getFacialFeaturesVotesMT (face_utils.cpp:244-302): votes[i] (the caller sizes votes to the parts) gains one
+// vote per (patch, tree) leaf that passes the option's filter, in the reference's patch-major, tree-minor order.
+inline void getFacialFeaturesVotesMT(const ImageSample& sample, const Forest<MPSample>& forest, Rect face_bbox,
+                                     std::vector<std::vector<Vote>>& votes,
+                                     MultiPartEstimatorOption options = MultiPartEstimatorOption()) {
+  const int patch_size = forest.getParam().getPatchSize() > 0 ? forest.getParam().getPatchSize() : 31;
+  std::vector<MPSample> samples;
+  for (int x = face_bbox.x; x < face_bbox.x + face_bbox.width - patch_size; x += options.step_size)
+    for (int y = face_bbox.y; y < face_bbox.y + face_bbox.height - patch_size; y += options.step_size)
+      samples.push_back(MPSample(&sample, Rect(x, y, patch_size, patch_size)));
+  const int num_trees = forest.numberOfTrees();
+  Forest<MPSample> f(forest);
+  f.setGridStep(options.step_size);
+  std::vector<MPLeaf*> leafs(samples.size() * num_trees);
+  for (size_t i = 0; i < samples.size(); i++) f.evaluateMT(&samples[i], &leafs[i * num_trees]);
+  for (size_t k = 0; k < leafs.size(); k++) {
+    const MPLeaf* l = leafs[k];
+    const int offset_x = samples[k / num_trees].getPatch().x + patch_size / 2;
+    const int offset_y = samples[k / num_trees].getPatch().y + patch_size / 2;
+    for (size_t i = 0; i < votes.size(); i++) {
+      float min_pf = options.min_pf;
+      if (i == 0 || i == 7) min_pf *= 1.5;  // probability in outer eye parts
+      if (l->mp_foreground > options.min_forground && l->mp_prob_foreground[i] > min_pf &&
+          l->mp_parts_variance[i] < options.max_variance && l->mp_samples > options.min_samples) {
+        Vote v;
+        v.pos.x = l->mp_parts_offset[i].x + offset_x;
+        v.pos.y = l->mp_parts_offset[i].y + offset_y;
+        v.weight = l->mp_foreground;
+        v.check = true;
+        votes[i].push_back(v);
+      }
+    }
+  }
+}
+
+// areaUnderCurve (face_utils.cpp:304-323): left Riemann sum of the normal density, step 0.01
+inline float areaUnderCurve(float x1, float x2, double mean, double std) {
+  double sum = 0;
+  const double step = 0.01;
+  for (double x = x1; x < x2; x += step) {
+    const double t = (x - mean) / std;
+    sum += std::exp(-0.5 * (t * t)) * step;
+  }
+  return (float)(sum * 1.0 / (std * std::sqrt(2 * M_PI)));
+}
+
 // ------------------------------------------------------------------ FaceForest --
 class FaceForest {
  public:
@@ -770,12 +1063,25 @@ class FaceForest {
   // FaceForest::detectFace (FaceForest.cpp:136-159) with this object's fd_option, on the GPU.
   void detectFace(const Mat img, std::vector<Rect>& faces_bboxes) { detect(engine_, img, fd_option_, faces_bboxes); }
 
-  // static FaceForest::detectFace (include/FaceForest.hpp:125-132): the current engine's converted cascade (the
-  // XML of FaceDetectionOption::path_face_cascade) runs in place of the CascadeClassifier argument.
+  // static FaceForest::detectFace (include/FaceForest.hpp:125-132, FaceForest.cpp:136-159) with the classifier it
+  // is given.  With OpenCV: the reference itself (the classifier's detectMultiScale on the CPU, then the widening).
+  // Without: the classifier's own detector engine (CascadeClassifier::load above) on the GPU.
   static void detectFace(const Mat& img, CascadeClassifier& face_cascade, FaceDetectionOption fd_option,
                          std::vector<Rect>& faces_bboxes) {
-    (void)face_cascade;
-    detect(detail::current_engine(), img, fd_option, faces_bboxes);
+#ifdef FFD_HAVE_OPENCV
+    const cv::Size min_feature_size(fd_option.min_feature_size, fd_option.min_feature_size);
+    face_cascade.detectMultiScale(img, faces_bboxes, fd_option.search_scale_factor, fd_option.min_neighbors, 0,
+                                  min_feature_size);
+    for (size_t i = 0; i < faces_bboxes.size(); i++) {  // the boxes are too tight for the estimators
+      const int offset_x = (int)(faces_bboxes[i].width * 0.05), offset_y = (int)(faces_bboxes[i].width * 0.15);
+      const Rect r1(faces_bboxes[i].x - offset_x, faces_bboxes[i].y, faces_bboxes[i].width + (offset_x * 2),
+                    faces_bboxes[i].height + (offset_y * 2));
+      faces_bboxes[i] = intersect(r1, Rect(0, 0, img.cols, img.rows));
+    }
+#else
+    if (face_cascade.empty()) throw std::runtime_error("detectFace: the CascadeClassifier is not loaded");
+    detect(face_cascade.engine(), img, fd_option, faces_bboxes);
+#endif
   }
 
   // FaceForest::analyzeImage (FaceForest.cpp:161-181): detectFace, then analyzeFace on every box (one
@@ -997,12 +1303,17 @@ class FaceForest {
 
 }  // namespace ffd
 
-#ifdef FFD_GLOBAL_NAMES  // drop-in: the reference's global names
+// Drop-in: the reference's global names, as its headers declare them (FaceForest.hpp, Constants.hpp,
+// face_utils.hpp, MeanShift.hpp, Forest.hpp, Tree.hpp, ImageSample.hpp, MPSample.hpp, HeadPoseSample.hpp: the
+// forwarding headers of this directory include this one).  FFD_NO_GLOBAL_NAMES keeps everything in namespace ffd.
+#ifndef FFD_NO_GLOBAL_NAMES
 #ifndef FFD_HAVE_OPENCV
 namespace cv {  // the reference spells the image types cv::Mat / cv::Rect / cv::Point (the PODs above without OpenCV)
 using ffd::CascadeClassifier;
 using ffd::Mat;
+using ffd::norm;
 using ffd::Point;
+using ffd::Point2f;
 using ffd::Rect;
 }  // namespace cv
 #endif
@@ -1025,8 +1336,16 @@ using ffd::MPSample;
 using ffd::MultiPartEstimatorOption;
 using ffd::Tree;
 using ffd::Vote;
+using ffd::areaUnderCurve;
 using ffd::enlargeFace;
+using ffd::getFacialFeaturesVotesMT;
+using ffd::getHeadPoseVotesMT;
 using ffd::intersect;
 using ffd::loadAnnotations;
 using ffd::loadConfigFile;
+using ffd::loadImage;
+using ffd::NORM_HEADPOSE_VARIANCE_FACTOR;
+using ffd::NUM_HEADPOSE_CLASSES;
+using ffd::PATCH_CLOSE_TO_FEATURE;
+using ffd::TRAIN_IMAGES_PERCENTAGE;
 #endif

@@ -334,6 +334,12 @@ ffd_status ffd_detect_faces_device(ffd_engine* engine, const void* d_images, int
                                    ffd_rect* boxes, int32_t* box_img, int32_t max_boxes, int32_t* n_boxes);
 ffd_status ffd_analyze_images(ffd_engine* engine, const ffd_image* imgs, int32_t n_img, const ffd_detect_options* opt,
                               ffd_face* faces, int32_t* face_img, int32_t max_faces, int32_t* n_faces);
+/* FaceForest::detectFace with the CascadeClassifier it is given (include/FaceForest.hpp:125-132, the static
+ * overload): an engine that holds only the Haar cascade of an OpenCV XML file (BOOST / HAAR stumps, the
+ * converter's reader) on `device`, for ffd_detect_faces / ffd_detect_faces_device / ffd_detect_candidates.
+ * The forest entry points fail on it (FFD_ERR_INVALID_ARGUMENT).  A missing or malformed file fails
+ * (FFD_ERR_MODEL), as CascadeClassifier::load returns false.  Destroy with ffd_engine_destroy. */
+ffd_status ffd_detector_create(const char* cascade_xml, int32_t device, ffd_engine** out);
 /* test hook: detectMultiScale's ungrouped candidates of one frame, in scan order */
 ffd_status ffd_detect_candidates(ffd_engine* engine, const ffd_image* img, const ffd_detect_options* opt,
                                  ffd_rect* raw, int32_t cap, int32_t* n_raw);
@@ -424,6 +430,11 @@ typedef struct ffd_trained_tree ffd_trained_tree;
 void ffd_train_param_init(ffd_train_param* p);
 ffd_status ffd_train_mp_tree(const ffd_train_param* p, const ffd_train_image* images, int32_t n_images,
                              ffd_trained_tree** out);
+/* the same with the caller's patches instead of npatches draws per image: n_patches (image, x, y) triples, each a
+ * face_size * patch_size_ratio square inside its image (Tree<MPSample>(samples, param, rng, save_path) of a caller
+ * that made its MPSamples itself, include/Tree.hpp:43-64, src/demo.cpp:48-100); tree_seed is then unused */
+ffd_status ffd_train_mp_tree_patches(const ffd_train_param* p, const ffd_train_image* images, int32_t n_images,
+                                     const int32_t* patches, int64_t n_patches, ffd_trained_tree** out);
 const char* ffd_train_last_error(void);  /* this thread's last ffd_train_* failure */
 int64_t ffd_trained_tree_num_nodes(const ffd_trained_tree* t);
 int64_t ffd_trained_tree_num_leaves(const ffd_trained_tree* t);

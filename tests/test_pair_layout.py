@@ -1,8 +1,8 @@
-"""The traversal's pair-record layout on the CPU (no device): tools/pair_layout_check.cpp re-encodes random
-breadth-first trees (one complete depth-18 tree, so child offsets pass 16 bits and take the far table) through
+"""The traversal's sibling-block layout on the CPU (no device): tools/pair_layout_check.cpp re-encodes random
+breadth-first trees (one complete depth-18 tree, so block offsets pass 16 bits and take the far table) through
 libffd.so's own ffd_host::build_pair_records / build_tree_tops and walks them the way k_traverse does (heap-ordered
-LDS tops for the first levels, then the records with the layout's child rule), against breadth-first walks with
-the same node decisions.  The GPU side of the same walks is the leaf parity of tests/test_gpu_parity.py."""
+LDS tops for the first levels, then the sibling blocks, each requested a step before its record is used), against
+breadth-first walks with the same node decisions; every requested block index must lie inside the array.  The GPU side of the same walks is the leaf parity of tests/test_gpu_parity.py."""
 import os
 import subprocess
 
@@ -23,15 +23,9 @@ def checker(tmp_path_factory):
     return exe
 
 
-def _blocked():
-    """FFD_PAIR_BLOCKS as the library was built (ffd_device.hpp's default)."""
-    src = open(os.path.join(REPO, "face_alignment_cvpr_2012_amd", "csrc", "ffd_device.hpp")).read()
-    return 1 if "#define FFD_PAIR_BLOCKS 1" in src else 0
-
-
 @pytest.mark.parametrize("top_levels", [0, 3, 6])
 def test_pair_walks_reach_the_breadth_first_leaves(checker, top_levels):
-    r = subprocess.run([checker, str(_blocked()), str(top_levels)], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([checker, str(top_levels)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert '"mismatches": 0' in r.stdout
     if top_levels == 0:

@@ -10,7 +10,7 @@ mkdir -p build/$NAME
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
   -Iinclude $X -c face_alignment_cvpr_2012_amd/csrc/ffd_kernels.hip -o build/$NAME/ffd_kernels.o
 ENG=$L/ffd_engine.o
-if [ "${ENGINE:-0}" = 1 ]; then  # flags that change the host-side encodings too (e.g. -DFFD_PAIR_BLOCKS=0)
+if [ "${ENGINE:-0}" = 1 ]; then  # flags that change the host-side encodings too (e.g. the record layout)
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
     -Iinclude $X -c face_alignment_cvpr_2012_amd/csrc/ffd_engine.cpp -o build/$NAME/ffd_engine.o
   ENG=build/$NAME/ffd_engine.o
