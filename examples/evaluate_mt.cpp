@@ -27,7 +27,6 @@
 #include <vector>
 
 #define FFD_NO_OPENCV
-#define FFD_GLOBAL_NAMES
 #include "FaceForest.hpp"
 
 using Clock = std::chrono::steady_clock;

@@ -1,4 +1,4 @@
-// reference_main.cpp — a reference main's setup, unchanged but for the include: eval_ffd's configuration
+// reference_main.cpp — a reference main's setup, unchanged (the include path decides): eval_ffd's configuration
 // (src/eval_ffd.cpp:137-174: loadConfigFile for both forests, FaceForestOptions with hp_forest_param /
 // mp_forest_param / the cascade path, FaceForest(ff_options)), then analyzeFace on one image (eval_ffd.cpp:89)
 // and the static detectFace with a CascadeClassifier (FaceForest.cpp:136-159).
@@ -12,8 +12,6 @@
 #include <string>
 #include <vector>
 
-#define FFD_NO_OPENCV
-#define FFD_GLOBAL_NAMES
 #include "FaceForest.hpp"
 
 int main(int argc, char** argv) {
@@ -46,7 +44,7 @@ int main(int argc, char** argv) {
   std::ifstream f(argv[4], std::ios::binary);
   if (!f.read(reinterpret_cast<char*>(px.data()), (std::streamsize)px.size())) return 2;
   try {
-    cv::Mat img(h, w, px.data());
+    cv::Mat img(h, w, CV_8UC3, px.data());
     Face face;
     ff.analyzeFace(img, cv::Rect(std::atoi(argv[7]), std::atoi(argv[8]), std::atoi(argv[9]), std::atoi(argv[10])), face);
     std::printf("%.9g", face.headpose);

@@ -130,7 +130,7 @@ EXPORTED_SYMBOLS = (
     "ffd_forest_subdirs", "ffd_group_debug_overlap",
 )
 COMM_ID_BYTES = 128
-STATUS_OK, STATUS_INVALID_ARGUMENT, STATUS_UNSUPPORTED = 0, 1, 7
+STATUS_OK, STATUS_INVALID_ARGUMENT, STATUS_OUT_OF_MEMORY, STATUS_UNSUPPORTED = 0, 1, 4, 7
 NUM_STAGES = 12
 
 
@@ -621,6 +621,41 @@ class FaceForest:
         bufs["trees"] = bufs["trees"][:nt]
         bufs["mp_leaves"] = bufs["mp_leaves"][: nmp * nt].reshape(nmp, nt)
         return bufs
+
+
+class _ForestParamC(ctypes.Structure):  # ffd_forest_param = ForestParam (Constants.hpp:24-60)
+    _fields_ = [("max_depth", ctypes.c_int32), ("min_patches", ctypes.c_int32), ("ntests", ctypes.c_int32),
+                ("ntrees", ctypes.c_int32), ("nimages", ctypes.c_int32), ("npatches", ctypes.c_int32),
+                ("face_size", ctypes.c_int32), ("patch_size_ratio", ctypes.c_float), ("tree_path", ctypes.c_char_p),
+                ("image_path", ctypes.c_char_p), ("features", ctypes.POINTER(ctypes.c_int32)),
+                ("n_features", ctypes.c_int32)]
+
+
+def convert_model(hp_config, ffd_config, cascade_xml, out_path):
+    """FaceForest(FaceForestOptions)'s loads (src/FaceForest.cpp:15-58) as a model file: loadConfigFile of both
+    configs, the head-pose trees of hp tree_path, the FFD trees of the sorted sub-directories of the FFD
+    tree_path, the Haar cascade (ffd_model_convert).  Returns out_path."""
+    from . import config
+    keep = []
+
+    def c_param(path):
+        ok, p = config.load_config_file(path)
+        if not ok:
+            raise FFDError(0, f"cannot read {path}")
+        feats = (ctypes.c_int32 * max(1, len(p.features)))(*p.features)
+        keep.append(feats)
+        return _ForestParamC(p.max_depth, p.min_patches, p.ntests, p.ntrees, p.nimages, p.npatches, p.face_size,
+                             p.patch_size_ratio, p.tree_path.encode(), p.image_path.encode(), feats, len(p.features))
+
+    hp, mp = c_param(hp_config), c_param(ffd_config)
+    root = mp.tree_path.decode()
+    dirs = sorted(os.path.join(root, d) for d in os.listdir(root) if os.path.isdir(os.path.join(root, d)))
+    arr = (ctypes.c_char_p * max(1, len(dirs)))(*[d.encode() for d in dirs])
+    st = lib().ffd_model_convert(ctypes.byref(hp), ctypes.byref(mp), arr, len(dirs),
+                                 cascade_xml.encode() if cascade_xml else None, str(out_path).encode())
+    if st != 0:
+        raise FFDError(st, "ffd_model_convert: " + lib().ffd_model_convert_last_error().decode())
+    return out_path
 
 
 def comm_id():

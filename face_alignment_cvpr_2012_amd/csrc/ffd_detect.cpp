@@ -244,7 +244,7 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
     e->det_clssum.ensure((size_t)nF * cap * 20);
     e->det_boxes.ensure((size_t)nF * cap * 16);
     e->det_packed.ensure((size_t)nF * cap * 20);
-    if (cap > HAAR_MAX_CAND) e->det_label.ensure((size_t)nF * cap * 4);
+    if (cap > HAAR_MAX_CAND) e->det_label.ensure(((size_t)nF * cap + 1) * 4);  // (+ the rounds' change flag)
     int max_px = 0, max_lpx = 0, max_rows = 0, max_cols = 0, max_tiles = 0, max_ystep = 1;
     for (const auto& f : frames) max_px = std::max(max_px, f.w * f.h);
     for (const auto& L : levels) {
@@ -288,9 +288,9 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
     std::vector<char> over(nF, 0);  // frames whose raw candidates exceed cap: boxes from a run of their own
     for (int k = 0; k < nF; k++) {
       if (counts[k] > cap) {
-        if (counts[k] > (1 << 24))
+        if (counts[k] > HAAR_GROUP_MAX)  // (the pair tests grow as N^2: ~1 s per round at 2^20 over the chip)
           return fail(e, FFD_ERR_UNSUPPORTED, "frame " + std::to_string(g0 + k) + ": " + std::to_string(counts[k]) +
-                                                  " raw detections");
+                                                  " raw detections (more than " + std::to_string(HAAR_GROUP_MAX) + ")");
         over[k] = 1;
       }
       total += counts[nF + k];

@@ -7,7 +7,9 @@
 //                                          every rectangle the trees read is exact, ffd_kernels.hip rect_mean16)
 //   hpleaf i32 [n_hp][15]                  head-pose leaf ordinal per (patch, tree), reference order
 //   mpleaf i32 [n_mp][T]                   FFD leaf ordinal per (patch, tree slot), reference order
-//   votes  {i16 x,y; f32 w} [10][T*n_mp]   compacted votes per landmark (MeanShift input)
+//   votes  {i16 x,y; f32 w} [10][T*n_mp]   compacted votes per landmark (MeanShift input); a face whose vote
+//                                          positions may leave int16 (FaceDesc::wide) has {i32 x,y; f32 w; pad}
+//                                          records over twice the space
 // The reference order is x-major over the patch grid (i = xi*ny + yi, face_utils.cpp:200-207),
 // tree-minor; the traversal writes its leaves there, so the order-dependent consumers (head-pose
 // sums, vote lists) read them contiguously.
@@ -24,7 +26,9 @@ constexpr int NPARTS = 10;
 constexpr int NHP_LABELS = 5;
 constexpr int MAX_TREES = 32;     // FFD_MAX_TREES
 constexpr int MAX_FACE_H = 600;   // scaled faces up to this height stage whole into the Gabor kernels' LDS (box aspect h/w <= 4.8)
-constexpr int MAX_FACE_H_TALL = 4096;  // taller ones band by band (k_gabor_sep<..., TALL>) up to this (aspect 32.8); beyond: FFD_ERR_UNSUPPORTED
+// taller ones band by band (k_gabor_sep<..., TALL>).  MAX_FACE_ROWS keeps every per-face index in 32 bits
+// (leaf lists n_patches x trees < 2^31); a face that tall needs > 50 GB of channel planes: FFD_ERR_OUT_OF_MEMORY
+constexpr int MAX_FACE_ROWS = 1 << 21;
 constexpr uint32_t LEAF_BIT = 0x80000000u;
 
 // Flattened tree node (16 B), breadth-first per tree, children adjacent:
@@ -41,22 +45,14 @@ constexpr uint32_t LEAF_BIT = 0x80000000u;
 //   lo = x1 | y1 << 5 | x2 << 10 | y2 << 15 | thr[5:0] << 20 | ch << 26
 //   hi = w1 | h1 << 5 | w2 << 10 | h2 << 15 | thr[9:6] << 20
 // (rectangles patch-relative, sides 1..22, threshold 10-bit two's complement), and for a leaf
-// ch = 63 (lo >= 63 << 26) with the leaf ordinal = lo[19:0] | hi << 20.
+// ch = 63 (lo >= 63 << 26) with the leaf ordinal = lo[19:0] | hi << 20.  Depth-first layout per tree: the pair of
+// c0's children is the next record, c1's children are off1 records ahead (off1 = 0: the 32-bit
+// offset is far[pair]).  Each tree starts with a root pair (root, unused leaf).
 // Source fields: ThresholdSplit<SimplePatchFeature> (ThresholdSplit.hpp:51-67, ImageSample.hpp:83-90).
-//
-// Sibling blocks: the pair records are stored in 32-byte blocks; the block B(n) of an internal node n
-// holds P(c0(n)) in half 0 and P(c1(n)) in half 1 (P(x) = the pair record of x's children; a half whose
-// child is a leaf is unused), so a walk standing on n can request both of its children's records before
-// it knows which child it takes.  Blocks are allocated depth-first: B(n), then c0's subtree's blocks
-// (B(c0) = B(n) + 1 when it exists), then c1's, and off1 of P(n) = B(c1) - B(n) (1 when c1's children are
-// both leaves: every block index a walk computes stays inside the array, which ends with one spare block);
-// off1 = 0 means the offset exceeds 16 bits and is far[2 * block + half] of the record.  Each tree starts
-// with a block holding P(root) in half 0 (the block of a virtual parent whose only child is the root).
 
 // Tree tops (k_traverse): per tree, TOP_CAP pair records of its top levels in heap order: entry 0
-// = the root pair (root, unused leaf), entry 1 = the root's children pair, entry 2h + s (h >= 1) = the
-// children pair of node s of entry h; entries under leaves are zero (never read).  Plus, per entry
-// P(m), the sibling-block index B(m) (entry 0: the tree's first block).
+// = the root pair, entry 1 = the root's children pair, entry 2h + s (h >= 1) = the children pair of
+// node s of entry h; entries under leaves are zero (never read).  Plus each entry's pair index.
 constexpr int TOP_CAP = 64;  // levels 0..6
 
 struct FaceDesc {
@@ -84,6 +80,8 @@ struct FaceDesc {
   int32_t fint;           // 1: an integral value may reach 2^24 (255 W H >= 2^24, a tall face), where the
                           //    reference's CV_32F integral rounds: float-accumulated integrals, and the
                           //    traversals' exact walker k_walk_fint instead of k_traverse
+  int32_t wide;           // 1: a vote position of this face may leave int16 (a face over ~32 k rows, or far leaf
+                          //    offsets): its votes are VoteW records and its MeanShift runs in k_meanshift5
 };
 
 struct FaceOut {          // == ffd_face
@@ -98,6 +96,12 @@ struct FaceOut {          // == ffd_face
 struct Vote {
   int16_t x, y;
   float w;
+};
+
+struct VoteW {            // the vote of a wide face (FaceDesc::wide): two Vote slots
+  int32_t x, y;
+  float w;
+  int32_t pad;
 };
 
 struct HpState {          // per-face head-pose result + tree selection

@@ -166,8 +166,9 @@ static void encode_test(const uint4& n, uint32_t& lo, uint32_t& hi) {
   hi = w1 | h1 << 5 | w2 << 10 | h2 << 15 | (t >> 6) << 20;  // sides as they are: no +1 in the walk
 }
 
-// Sibling-block layout (ffd_device.hpp "sibling blocks"): out holds 2 pair records per block; roots_out[t] =
-// tree t's first block (P(root) in half 0).  Leaves keep their model ordinals; speed-neutral for parity:
+// Depth-first pair layout: a pair (a, b) is followed by the pair of a's children and a's whole
+// subtree, then b's children pair at offset off1 (16 bits; 0 = look up far[pair]).  Each tree starts
+// with a root pair (root, unused leaf).  Leaves keep their model ordinals; speed-neutral for parity:
 // every walk visits the same nodes in the same order as Tree<S>::evaluateMT.
 void ffd_host::build_pair_records(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots,
                                   std::vector<uint4>& out, std::vector<int32_t>& roots_out,
@@ -175,100 +176,80 @@ void ffd_host::build_pair_records(const std::vector<uint4>& bfs, const std::vect
   out.clear();
   roots_out.clear();
   far.clear();
+  const uint4 unused_leaf = make_uint4(LEAF_BIT, 0u, 0u, 0u);
   auto pack = [](const uint4& a, const uint4& b, uint32_t o16) {
     uint32_t lo0, hi0, lo1, hi1;
     encode_test(a, lo0, hi0);
     encode_test(b, lo1, hi1);
     return make_uint4(lo0, lo1, hi0 | (o16 & 0xFFu) << 24, hi1 | (o16 >> 8) << 24);
   };
-  auto internal = [](const uint4& n) { return !(n.x & LEAF_BIT); };
-  auto alloc = [&]() {
-    const size_t b = out.size() / 2;
-    out.resize(out.size() + 2, make_uint4(0, 0, 0, 0));
-    far.resize(far.size() + 2, 0u);
-    return b;
-  };
-  // Place P(n) (n internal, bfs index) at record position pos and n's subtree below it.  An explicit stack:
-  // phase 0 allocates B(n) and descends into c0, phase 1 descends into c1, phase 2 writes P(n) (off1 is
-  // known once c1's block exists).
-  struct Frame { uint32_t n; size_t pos; int64_t bn, b1; int phase; };
-  std::vector<Frame> st;
+  // iterative DFS: a frame places pair (a, b); phase 0 = a's children, 1 = b's children, 2 = done
+  struct Frame { uint4 a, b; size_t idx; int phase; };
   for (int32_t root : roots) {
-    const size_t r0 = alloc();
-    roots_out.push_back((int32_t)r0);
-    if (!internal(bfs[(uint32_t)root])) continue;  // a one-leaf tree: the tops' root entry ends every walk
-    st.push_back({(uint32_t)root, 2 * r0, -1, -1, 0});
+    std::vector<Frame> st;
+    roots_out.push_back((int32_t)out.size());
+    st.push_back({bfs[(uint32_t)root], unused_leaf, out.size(), 0});
+    out.push_back(make_uint4(0, 0, 0, 0));
+    far.push_back(0);
     while (!st.empty()) {
       Frame& f = st.back();
-      const uint4& a = bfs[bfs[f.n].x];
-      const uint4& b = bfs[bfs[f.n].x + 1];
       if (f.phase == 0) {
         f.phase = 1;
-        if (internal(a) || internal(b)) f.bn = (int64_t)alloc();
-        if (internal(a)) {
-          const size_t pos = 2 * (size_t)f.bn;
-          st.push_back({bfs[f.n].x, pos, -1, -1, 0});
+        if (!(f.a.x & LEAF_BIT)) {
+          const uint32_t c = f.a.x;
+          st.push_back({bfs[c], bfs[c + 1], out.size(), 0});
+          out.push_back(make_uint4(0, 0, 0, 0));
+          far.push_back(0);
         }
         continue;
       }
       if (f.phase == 1) {
         f.phase = 2;
-        if (internal(b)) {
-          const size_t pos = 2 * (size_t)f.bn + 1;
-          // B(c1) is the next block allocated (if c1 has an internal child)
-          const uint4& b0 = bfs[b.x];
-          const uint4& b1 = bfs[b.x + 1];
-          if (internal(b0) || internal(b1)) f.b1 = (int64_t)(out.size() / 2);
-          st.push_back({bfs[f.n].x + 1, pos, -1, -1, 0});
+        const uint64_t off1 = out.size() - f.idx;  // where b's children pair goes
+        uint32_t o16 = off1 <= 0xFFFFu ? (uint32_t)off1 : 0u;
+        if (o16 == 0 && !(f.b.x & LEAF_BIT)) far[f.idx] = (uint32_t)off1;
+        if (off1 > 0xFFFFFFFFull) throw std::runtime_error("pair array too large");
+        out[f.idx] = pack(f.a, f.b, o16);
+        if (!(f.b.x & LEAF_BIT)) {
+          const uint32_t c = f.b.x;
+          const size_t at = out.size();
+          out.push_back(make_uint4(0, 0, 0, 0));
+          far.push_back(0);
+          st.push_back({bfs[c], bfs[c + 1], at, 0});
         }
         continue;
       }
-      const uint64_t off1 = f.b1 >= 0 ? (uint64_t)(f.b1 - f.bn) : 1u;
-      if (off1 > 0xFFFFFFFFull) throw std::runtime_error("pair array too large");
-      const uint32_t o16 = off1 <= 0xFFFFu ? (uint32_t)off1 : 0u;
-      if (o16 == 0) far[f.pos] = (uint32_t)off1;
-      out[f.pos] = pack(a, b, o16);
       st.pop_back();
     }
   }
-  alloc();  // the spare block (a walk may request B(last) + 1, never reads it)
-  if (out.size() / 2 >= 0x80000000ull) throw std::runtime_error("pair array too large");
+  if (out.size() >= 0x80000000ull) throw std::runtime_error("pair array too large");
 }
 
 void ffd_host::build_tree_tops(const std::vector<uint4>& pairs, const std::vector<int32_t>& proots,
-                               const std::vector<uint32_t>& far, const std::vector<uint4>& bfs,
-                               const std::vector<int32_t>& roots, std::vector<uint4>& tops,
+                               const std::vector<uint32_t>& far, std::vector<uint4>& tops,
                                std::vector<uint32_t>& top_idx) {
   tops.assign(proots.size() * TOP_CAP, make_uint4(0, 0, 0, 0));
   top_idx.assign(proots.size() * TOP_CAP, 0u);
   auto leaf = [](uint32_t lo) { return (lo >> 26) == 63u; };
   for (size_t t = 0; t < proots.size(); t++) {
     uint4* rec = &tops[t * TOP_CAP];
-    uint32_t* idx = &top_idx[t * TOP_CAP];  // block index B(m) of entry h = P(m)
-    std::vector<size_t> pos(TOP_CAP, 0);    // record position of entry h (h >= 1)
-    // entry 0: the virtual parent's pair (root, unused leaf), whose block holds P(root)
-    {
-      uint32_t lo0, hi0, lo1, hi1;
-      encode_test(bfs[(uint32_t)roots[t]], lo0, hi0);
-      encode_test(make_uint4(LEAF_BIT, 0u, 0u, 0u), lo1, hi1);
-      rec[0] = make_uint4(lo0, lo1, hi0, hi1);
-    }
+    uint32_t* idx = &top_idx[t * TOP_CAP];  // pair index of each entry
     idx[0] = (uint32_t)proots[t];
+    rec[0] = pairs[idx[0]];
     std::vector<bool> live(TOP_CAP, false);
     live[0] = true;
     for (int h = 0; h < TOP_CAP; h++) {
       if (!live[h]) continue;
       const uint4 R = rec[h];
+      const uint32_t p = idx[h];
       for (uint32_t s = 0; s < (h ? 2u : 1u); s++) {  // the root pair's second slot is an unused leaf
         if (leaf(s ? R.y : R.x)) continue;
         const int h2 = h ? 2 * h + (int)s : 1;
         if (h2 >= TOP_CAP) continue;
-        const size_t q = 2 * (size_t)idx[h] + s;  // P(c_s(m)) is half s of B(m)
-        uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
-        if (h && s && off1 == 0) off1 = far[pos[h]];
+        const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
+        const uint32_t q = p + (s ? (off1 ? off1 : far[p]) : 1u);
         rec[h2] = pairs[q];
-        pos[h2] = q;
-        idx[h2] = idx[h] + (s ? off1 : 1u);  // B(c_s(m))
+        idx[h2] = q;
         live[h2] = true;
       }
     }
@@ -322,6 +303,7 @@ void ffd_engine::load_model(const std::string& path) {
     vote_rec_compact = vt.compact;
     vote_bias_x = vt.bias_x;
     vote_bias_y = vt.bias_y;
+    vote_range = vt.range;
     upload(mp_rec, vt.rec, main_stream());
   }
   load_cascade(m);
@@ -381,6 +363,8 @@ ffd_host::VoteTable ffd_host::mp_vote_records(const ffd::ModelFile& m, const ffd
     mask[L] = mk;
   }
   VoteTable vt;
+  vt.range.any = mnx <= mxx;
+  if (vt.range.any) vt.range = VoteRange{true, mnx, mxx, mny, mxy};
   vt.compact = mxx - mnx <= 255 && mxy - mny <= 255;
   vt.bias_x = vt.compact && mnx <= mxx ? mnx : 0;
   vt.bias_y = vt.compact && mny <= mxy ? mny : 0;
@@ -498,12 +482,14 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   // one channel plane stride for the whole batch (the traversal's window staging assumes it)
   int64_t plane = PITCH;
   int max_h = 1;
-  bool any_fint = false;
-  for (const auto& f : fds)
+  bool any_fint = false, any_wide = false;
+  for (auto& f : fds)
     if (f.valid) {
       plane = std::max(plane, (int64_t)(f.H + 1) * PITCH);
       max_h = std::max(max_h, f.H);
       any_fint |= f.fint != 0;
+      f.wide = force_wide || votes_wide(f, desc.mp_option.step_size, mp_step_y(), patch / 2, vote_range);
+      any_wide |= f.wide != 0;
     }
   for (auto& f : fds) {
     if (!f.valid) continue;
@@ -518,8 +504,8 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
     hp_e += (int64_t)hp_trees * f.nhx * f.nhy;
     f.mp_off = mp_e;
     mp_e += (int64_t)MAX_TREES * f.nmx * f.nmy;
-    f.vote_off = vote_e;
-    vote_e += (int64_t)NPARTS * MAX_TREES * f.nmx * f.nmy;
+    f.vote_off = vote_e;  // (even: a wide face's VoteW records are 16-B aligned)
+    vote_e += align_up((int64_t)NPARTS * MAX_TREES * f.nmx * f.nmy * (f.wide ? 2 : 1), 2);
   }
   w.gray.ensure(gray_b + 256);
   w.mag.ensure((mag_e + 64) * 4);
@@ -565,11 +551,16 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
     HIP_CHECK(hipEventRecord(w.fork_ev[1 + i], w.fork[i]));
     HIP_CHECK(hipStreamWaitEvent(st, w.fork_ev[1 + i], 0));
   }
+  // block queues of the two traversals (8 per-XCD counters each) and the FFD pass's face order
+  w.trav_queue.ensure(16 * sizeof(uint32_t));
+  if (trav_sort) w.trav_order.ensure((size_t)n * sizeof(int32_t));
+  uint32_t* hp_queue = trav_queue ? w.trav_queue.as<uint32_t>() : nullptr;
+  uint32_t* mp_queue = trav_queue ? w.trav_queue.as<uint32_t>() + 8 : nullptr;
   stage(7, st, [&] {
     launch_traverse(true, dfd, n, blocks_per_face(fds, true, trav_g_hp), trav_g_hp, hp_pairs.as<uint4>(),
                     hp_tops.as<uint4>(), hp_topi.as<uint32_t>(), trav_top_max, hp_far.as<uint32_t>(), nullptr,
                     hp_trees, desc.hp_option.step_size, desc.hp_option.step_size, plane, w.chan.as<uint16_t>(),
-                    w.hpleaf.as<int32_t>(), trav_wg, TRAV_LDS_CAP, st);
+                    w.hpleaf.as<int32_t>(), trav_wg, TRAV_LDS_CAP, st, nullptr, hp_queue);
     if (any_fint)
       launch_walk_fint(true, dfd, n, hp_nodes.as<uint4>(), hp_roots.as<int32_t>(), hp_trees, nullptr,
                        desc.hp_option.step_size, desc.hp_option.step_size, w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), st);
@@ -579,10 +570,12 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
                    w.state.as<HpState>(), d_out, st);
   });
   stage(9, st, [&] {
+    if (trav_sort) launch_trav_order(w.state.as<HpState>(), n, ntrees_per_forest, w.trav_order.as<int32_t>(), st);
     launch_traverse(false, dfd, n, blocks_per_face(fds, false, trav_g_mp), trav_g_mp, mp_pairs.as<uint4>(),
                     mp_tops.as<uint4>(), mp_topi.as<uint32_t>(), trav_top_max, mp_far.as<uint32_t>(),
                     w.state.as<HpState>(), 0, desc.mp_option.step_size, mp_step_y(), plane, w.chan.as<uint16_t>(),
-                    w.mpleaf.as<int32_t>(), trav_wg, TRAV_LDS_CAP, st);
+                    w.mpleaf.as<int32_t>(), trav_wg, TRAV_LDS_CAP, st, trav_sort ? w.trav_order.as<int32_t>() : nullptr,
+                    mp_queue);
     if (any_fint)
       launch_walk_fint(false, dfd, n, mp_nodes.as<uint4>(), mp_roots.as<int32_t>(), 0, w.state.as<HpState>(),
                        desc.mp_option.step_size, mp_step_y(), w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), st);
@@ -596,18 +589,40 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   stage(11, st, [&] {
     launch_meanshift(dfd, n, w.state.as<HpState>(), MAX_TREES, n_parts, (float)desc.ms_option.kernel_size,
                      desc.ms_option.max_iterations, desc.ms_option.stopping_criteria, w.votes.as<Vote>(),
-                     w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(), d_out, w.ms_order.as<int32_t>(), st);
+                     w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(), d_out, w.ms_order.as<int32_t>(), st, any_wide);
   });
   HIP_CHECK(hipGetLastError());
 }
 
 // Split the batch into chunks, round-robin over the stream workspaces.  On return every chunk
 // is enqueued and main_stream() is ordered after all of them.
+// A chunk ends at max_chunk faces, where the faces change between ordinary and tall (H > MAX_FACE_H: a
+// chunk has one channel plane stride, so a tall face would stretch its neighbours' planes), or before its
+// buffers pass chunk_bytes (a few very tall faces).
 void ffd_engine::analyze(const uint8_t* d_images, const std::vector<FaceDesc>& all, FaceOut* d_out) {
   const int n = (int)all.size();
+  auto face_bytes = [&](const FaceDesc& f) -> int64_t {  // gray, mag, leaves, votes (VoteW past ~16 k rows)
+    const int64_t pm = (int64_t)f.nmx * f.nmy;
+    return (int64_t)f.H * PITCH * (1 + 4 * NGABOR) + 4 * ((int64_t)hp_trees * f.nhx * f.nhy + MAX_TREES * pm) +
+           (int64_t)NPARTS * MAX_TREES * pm * sizeof(Vote) * (f.H > 16000 ? 2 : 1);
+  };
   int k = 0;
-  for (int first = 0; first < n; first += max_chunk, k++) {
-    const int cnt = std::min(max_chunk, n - first);
+  for (int first = 0; first < n; k++) {
+    int cnt = 0, nvalid = 0, cls = -1;
+    int64_t plane_max = PITCH, other = 0;
+    while (first + cnt < n && cnt < max_chunk) {
+      const FaceDesc& f = all[first + cnt];
+      if (f.valid) {
+        const int c = f.H > MAX_FACE_H;
+        const int64_t pl = std::max(plane_max, (int64_t)(f.H + 1) * PITCH), o = other + face_bytes(f);
+        if (cnt > 0 && (c != cls || o + (int64_t)(nvalid + 1) * NCH * pl * 2 > chunk_bytes)) break;
+        cls = c;
+        plane_max = pl;
+        other = o;
+        nvalid++;
+      }
+      cnt++;
+    }
     Workspace& w = *ws[k % ws.size()];
     // (h_fds reaches the device through a pinned staging slot that is reused only after its copy ran,
     // upload_descriptors; the device buffers are reused in stream order, so the host need not wait for
@@ -620,6 +635,7 @@ void ffd_engine::analyze(const uint8_t* d_images, const std::vector<FaceDesc>& a
     HIP_CHECK(hipEventRecord(w.done, w.stream));
     w.pending = true;
     last_ws = (int)(k % ws.size());
+    first += cnt;
   }
   for (size_t i = 1; i < ws.size(); i++)
     if (ws[i]->pending) HIP_CHECK(hipStreamWaitEvent(main_stream(), ws[i]->done, 0));
@@ -633,8 +649,8 @@ ffd_status ffd_host::fail(ffd_engine* e, ffd_status s, const std::string& msg) {
 
 // Fill the per-face descriptor (geometry + resize parameters) for a box on an image.  Returns the
 // face's status: FFD_OK, FFD_ERR_INVALID_ARGUMENT (box outside the image or an empty scaled face:
-// the reference's cv::Mat ROI / resize assertions throw) or FFD_ERR_UNSUPPORTED (scaled face taller
-// than MAX_FACE_H_TALL).  A face on which no head-pose patch fits runs like the reference: 0/0 head pose
+// the reference's cv::Mat ROI / resize assertions throw) or FFD_ERR_OUT_OF_MEMORY (scaled face taller
+// than MAX_FACE_ROWS: FFD_ERR_OUT_OF_MEMORY).  A face on which no head-pose patch fits runs like the reference: 0/0 head pose
 // (NaN), trees 0..19 of forest 0, no votes, landmarks (0, 0); its channels are never read, so the
 // channel stage skips it.
 ffd_status ffd_host::make_desc(const ffd_engine* e, int64_t img_off, int iw, int ih, int stride, const ffd_rect& b,
@@ -649,9 +665,9 @@ ffd_status ffd_host::make_desc(const ffd_engine* e, int64_t img_off, int iw, int
     return FFD_ERR_INVALID_ARGUMENT;
   Geometry g = e->geometry(b.width, b.height);
   if (g.W < 1 || g.H < 1 || g.W > PITCH - 3) return FFD_ERR_INVALID_ARGUMENT;
-  if (g.H > MAX_FACE_H_TALL) {
-    f.reject = FFD_ERR_UNSUPPORTED;
-    return FFD_ERR_UNSUPPORTED;
+  if (g.H > MAX_FACE_ROWS) {  // > 50 GB of channel planes for this one face
+    f.reject = FFD_ERR_OUT_OF_MEMORY;
+    return FFD_ERR_OUT_OF_MEMORY;
   }
   f.W = g.W; f.H = g.H; f.scale = g.scale;
   f.fint = (int64_t)255 * g.W * g.H >= (int64_t)1 << 24 ? 1 : 0;  // an integral value may reach 2^24
@@ -767,10 +783,10 @@ const char* ffd_status_string(int32_t s) {
     case FFD_ERR_INVALID_ARGUMENT: return "invalid argument (face box outside the image or empty scaled face)";
     case FFD_ERR_MODEL: return "model file invalid or unsupported";
     case FFD_ERR_DEVICE: return "HIP device error or no HIP device";
-    case FFD_ERR_OUT_OF_MEMORY: return "out of memory";
+    case FFD_ERR_OUT_OF_MEMORY: return "out of memory (or a scaled face over 2^21 rows)";
     case FFD_ERR_NOT_INITIALIZED: return "not initialised";
     case FFD_ERR_INTERNAL: return "internal error";
-    case FFD_ERR_UNSUPPORTED: return "unsupported face geometry (scaled face taller than 4096 rows)";
+    case FFD_ERR_UNSUPPORTED: return "unsupported input (an image sample over 125 columns, or a detection frame over 2^20 raw candidates)";
     default: return "unknown status";
   }
 }
@@ -843,6 +859,10 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   if (const char* v = std::getenv("FFD_TRAV_G_FFD")) shape(v, e->trav_g_mp);
   if (const char* v = std::getenv("FFD_TRAV_WG")) e->trav_wg = std::max(8, std::atoi(v));
   if (const char* v = std::getenv("FFD_TRAV_TOPMAX")) e->trav_top_max = std::max(1, std::min(TOP_CAP, std::atoi(v)));
+  if (const char* v = std::getenv("FFD_TRAV_QUEUE")) e->trav_queue = std::atoi(v) != 0;
+  if (const char* v = std::getenv("FFD_TRAV_SORT")) e->trav_sort = std::atoi(v) != 0;
+  if (const char* v = std::getenv("FFD_VOTES_WIDE")) e->force_wide = std::atoi(v) != 0;
+  if (const char* v = std::getenv("FFD_CHUNK_BYTES")) e->chunk_bytes = std::max<int64_t>(1, std::atoll(v));
   if (const char* v = std::getenv("FFD_GABOR_EXACT")) e->gabor_exact = std::atoi(v) != 0;
   if (const char* v = std::getenv("FFD_CHANNEL_STREAMS")) e->channel_streams = std::max(1, std::min(6, std::atoi(v)));
   if (const char* v = std::getenv("FFD_SMALL_BATCH")) e->small_batch = std::max(0, std::atoi(v));
@@ -1083,7 +1103,7 @@ ffd_status ffd_get_trace(ffd_engine* e, int32_t index, ffd_trace* tr) {
 ffd_status ffd_extract_channels(ffd_engine* e, const uint8_t* gray_face, int32_t W, int32_t H, uint32_t* out) {
   if (e && e->detector_only) return no_forests(e);
   return guarded(e, [&]() -> ffd_status {
-    if (!gray_face || !out || W < 2 || H < 2 || W > PITCH - 3 || H > MAX_FACE_H_TALL)
+    if (!gray_face || !out || W < 2 || H < 2 || W > PITCH - 3 || H > MAX_FACE_ROWS)
       return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     // the face itself is the "image" (copy mode): one BGR image whose gray equals the input
     e->sync_all();
@@ -1223,9 +1243,9 @@ const float* hp_table(ffd_engine* e, const ffd_headpose_option& o) {
   }
   return e->alt.hp_m.as<float>();
 }
-const uint4* mp_table(ffd_engine* e, const ffd_multipart_option& o, bool& compact, int& bx, int& by) {
+const uint4* mp_table(ffd_engine* e, const ffd_multipart_option& o, bool& compact, int& bx, int& by, VoteRange& vr) {
   if (same(o, e->desc.mp_option)) {
-    compact = e->vote_rec_compact; bx = e->vote_bias_x; by = e->vote_bias_y;
+    compact = e->vote_rec_compact; bx = e->vote_bias_x; by = e->vote_bias_y; vr = e->vote_range;
     return e->mp_rec.as<uint4>();
   }
   if (!e->alt.mp_ok || !same(o, e->alt.mp)) {
@@ -1233,17 +1253,17 @@ const uint4* mp_table(ffd_engine* e, const ffd_multipart_option& o, bool& compac
     VoteTable vt = mp_vote_records(e->leaf_arrays(), o);
     upload(e->alt.mp_rec, vt.rec, e->main_stream());
     HIP_CHECK(hipStreamSynchronize(e->main_stream()));
-    e->alt.compact = vt.compact; e->alt.bias_x = vt.bias_x; e->alt.bias_y = vt.bias_y;
+    e->alt.compact = vt.compact; e->alt.bias_x = vt.bias_x; e->alt.bias_y = vt.bias_y; e->alt.range = vt.range;
     e->alt.mp = o;
     e->alt.mp_ok = true;
   }
-  compact = e->alt.compact; bx = e->alt.bias_x; by = e->alt.bias_y;
+  compact = e->alt.compact; bx = e->alt.bias_x; by = e->alt.bias_y; vr = e->alt.range;
   return e->alt.mp_rec.as<uint4>();
 }
 
 bool region_ok(int W, int H, const ffd_rect* r) {
   return r && r->x >= 0 && r->y >= 0 && r->width > 0 && r->height > 0 && (int64_t)r->x + r->width <= W &&
-         (int64_t)r->y + r->height <= H && r->width <= PITCH - 3 && r->height <= MAX_FACE_H_TALL;
+         (int64_t)r->y + r->height <= H && r->width <= PITCH - 3 && r->height <= MAX_FACE_ROWS;
 }
 
 // getHeadPoseVotesMT + the pose reduction (FaceForest.cpp:60-72, face_utils.cpp:183-242) on the staged
@@ -1280,12 +1300,18 @@ ffd_status check_mp_call(ffd_engine* e, const int32_t* tree_ids, int n_trees, co
 
 // getFacialFeaturesVotesMT + MeanShift (FaceForest.cpp:74-95, face_utils.cpp:244-302) on the staged one-face
 // chunk f of workspace w (planes `chan`) with the given trees; points in sample coordinates.
-void run_facial_features(ffd_engine* e, Workspace& w, const FaceDesc& f, const uint16_t* chan, const int32_t* tree_ids,
+void run_facial_features(ffd_engine* e, Workspace& w, FaceDesc f, const uint16_t* chan, const int32_t* tree_ids,
                          int n_trees, const ffd_multipart_option& o, int32_t* points) {
   const int step_y = o.step_size_y > 0 ? o.step_size_y : o.step_size;
   bool compact = false;
   int bias_x = 0, bias_y = 0;
-  const uint4* rec = mp_table(e, o, compact, bias_x, bias_y);
+  VoteRange vr;
+  const uint4* rec = mp_table(e, o, compact, bias_x, bias_y, vr);
+  f.wide = e->force_wide || votes_wide(f, o.step_size, step_y, e->patch / 2, vr);
+  if (f.wide) {  // VoteW lists: twice the vote space, and the descriptor again
+    w.votes.ensure(((size_t)2 * NPARTS * MAX_TREES * f.nmx * f.nmy + 64) * sizeof(Vote));
+    e->upload_descriptors(w.faces, std::vector<FaceDesc>{f}, w.stream);
+  }
   const TravShape g = ffd_engine::fit_shape(e->trav_g_mp, false, o.step_size, step_y);
   const FaceDesc* dfd = w.faces.as<FaceDesc>();
   std::vector<FaceDesc> fv{f};
@@ -1306,7 +1332,7 @@ void run_facial_features(ffd_engine* e, Workspace& w, const FaceDesc& f, const u
                o.step_size, step_y, e->patch / 2, n_parts, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), w.stream);
   // FaceForest::estimateFacialFeatures shifts with a default MeanShiftOption (FaceForest.cpp:89-92)
   launch_meanshift(dfd, 1, w.state.as<HpState>(), MAX_TREES, n_parts, 10.f, 7, 0.05f, w.votes.as<Vote>(),
-                   w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(), e->out.as<FaceOut>(), nullptr, w.stream);
+                   w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(), e->out.as<FaceOut>(), nullptr, w.stream, f.wide != 0);
   HIP_CHECK(hipGetLastError());
   FaceOut out;
   HIP_CHECK(hipMemcpyAsync(&out, e->out.p, sizeof(out), hipMemcpyDeviceToHost, w.stream));
@@ -1414,7 +1440,7 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* c
   if (e && e->detector_only) return no_forests(e);
   return guarded(e, [&]() -> ffd_status {
     if (!channels || (!patches_xy && n_patches) || (!tree_ids && n_trees) || (!leaf_ids && n_patches * n_trees) ||
-        W < 1 || H < 1 || W > PITCH - 3 || H > MAX_FACE_H_TALL || n_patches < 0 || n_trees < 0)
+        W < 1 || H < 1 || W > PITCH - 3 || H > MAX_FACE_ROWS || n_patches < 0 || n_trees < 0)
       return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     if (kind != FFD_FOREST_HEADPOSE && kind != FFD_FOREST_FFD) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad forest kind");
     const int ntot = kind == FFD_FOREST_HEADPOSE ? e->hp_trees : e->n_forests * e->ntrees_per_forest;
@@ -1429,10 +1455,14 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* c
     const int64_t plane = (int64_t)(H + 1) * PITCH;
     // the device keeps integrals modulo 2^16 (exact for every rectangle the trees read)
     std::vector<uint16_t> narrow((size_t)NCH * plane, 0);
+    uint32_t vmax = 0;
     for (int c = 0; c < NCH; c++)
       for (int y = 0; y <= H; y++)
-        for (int x = 0; x <= W; x++)
-          narrow[(size_t)c * plane + (size_t)y * PITCH + x] = (uint16_t)channels[((size_t)c * (H + 1) + y) * (W + 1) + x];
+        for (int x = 0; x <= W; x++) {
+          const uint32_t v = channels[((size_t)c * (H + 1) + y) * (W + 1) + x];
+          vmax = std::max(vmax, v);
+          narrow[(size_t)c * plane + (size_t)y * PITCH + x] = (uint16_t)v;
+        }
     upload(e->scratch_a, narrow, e->main_stream());
     std::vector<int32_t> pv(patches_xy, patches_xy + 2 * n_patches), tv(tree_ids, tree_ids + n_trees);
     upload(e->scratch_b, pv, e->main_stream());
@@ -1443,7 +1473,7 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* c
     launch_eval_patches(hp ? e->hp_nodes.as<uint4>() : e->mp_nodes.as<uint4>(),
                         hp ? e->hp_roots.as<int32_t>() : e->mp_roots.as<int32_t>(), e->scratch_c.as<int32_t>(), n_trees,
                         e->scratch_b.as<int32_t>(), n_patches, e->scratch_a.as<uint16_t>(), plane, outb.as<int32_t>(),
-                        e->main_stream());
+                        e->main_stream(), vmax >= (1u << 24));  // float-rounded integrals: rect_mean_fint
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipMemcpyAsync(leaf_ids, outb.p, (size_t)n_patches * n_trees * 4, hipMemcpyDeviceToHost, e->main_stream()));
     HIP_CHECK(hipStreamSynchronize(e->main_stream()));  // `narrow` outlives the upload
@@ -1460,6 +1490,7 @@ struct ffd_sample {
   int device = 0;
   int W = 0, H = 0;
   int64_t plane = 0;  // (H + 1) * PITCH
+  int fint = 0;       // float-rounded integrals (CV_32F past 2^24, FaceDesc::fint): walked by rect_mean_fint
   DevBuf chan;        // u16 [NCH][H + 1][PITCH], integrals mod 2^16
 };
 
@@ -1481,6 +1512,7 @@ FaceDesc sample_desc(ffd_sample* s, int hp_step, int mp_step_x, int mp_step_y) {
   const ffd_rect full{0, 0, s->W, s->H};
   FaceDesc f = region_desc(s->e, full, hp_step, mp_step_x, mp_step_y);
   f.plane = s->plane;
+  f.fint = s->fint;
   return f;
 }
 
@@ -1488,10 +1520,7 @@ ffd_status orphaned() {
   return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "the image sample's engine was destroyed (ffd_engine_destroy ran first)");
 }
 
-bool sample_size_ok(int W, int H) {
-  // (255 W H >= 2^24: the reference's CV_32F integrals round; the sample path walks exact integrals only)
-  return W >= 2 && H >= 2 && W <= PITCH - 3 && (int64_t)255 * W * H < ((int64_t)1 << 24);
-}
+bool sample_size_ok(int W, int H) { return W >= 2 && H >= 2 && W <= PITCH - 3 && H <= MAX_FACE_ROWS; }
 
 ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, int32_t n_patches, int x0, int y0,
                        int step, int nx, int ny, const int32_t* tree_ids, int32_t n_trees, int32_t* leaf_ids) {
@@ -1524,31 +1553,39 @@ ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, i
   // exactly the grid order; the grid asked for is a leading sub-grid of it.
   bool all_hp_trees = hp && n_trees == e->hp_trees;
   for (int t = 0; all_hp_trees && t < n_trees; t++) all_hp_trees = tree_ids[t] == t;
-  if (grid && x0 == 0 && y0 == 0 && (!hp || all_hp_trees) && step <= 32 && n_trees <= MAX_TREES) {
+  if (grid && x0 == 0 && y0 == 0 && (!hp || all_hp_trees) && step <= 32 && n_trees <= MAX_TREES && !s->fint) {
     const FaceDesc f = sample_desc(s, hp ? step : e->desc.hp_option.step_size, hp ? e->desc.mp_option.step_size : step,
                                    hp ? e->mp_step_y() : step);
     const int gx = hp ? f.nhx : f.nmx, gy = hp ? f.nhy : f.nmy;
     if (nx <= gx && ny <= gy) {
       e->sync_all();
       Workspace& w = *e->ws[0];
-      stage_desc(e, w, f);
+      w.count = 0;  // the workspace no longer holds a batch for ffd_get_trace
+      w.pending = false;
+      if (e->last_ws == 0) e->last_ws = -1;
       const TravShape g = ffd_engine::fit_shape(hp ? e->trav_g_hp : e->trav_g_mp, hp, step, step);
       std::vector<FaceDesc> fv{f};
       // the leaves go straight to host-mapped pinned memory (no device buffer, no copy back)
       const size_t all = (size_t)gx * gy * n_trees * 4;
       int32_t* pin = static_cast<int32_t*>(e->pin_leaf.ensure(all));
       int32_t* leaf_dev = pin;
-      if (!hp) {
+      // the descriptor and the tree list in one upload
+      struct {
+        FaceDesc f;
         HpState hs;
-        std::memset(&hs, 0, sizeof(hs));
-        hs.n_trees = n_trees;
-        for (int t = 0; t < n_trees; t++) hs.trees[t] = tree_ids[t];
-        e->upload_pinned(w.state.p, &hs, sizeof(hs), w.stream);
-      }
-      launch_traverse(hp, w.faces.as<FaceDesc>(), 1, blocks_per_face(fv, hp, g), g,
+      } one;
+      std::memset(&one, 0, sizeof(one));
+      one.f = f;
+      one.hs.n_trees = n_trees;
+      for (int t = 0; t < n_trees; t++) one.hs.trees[t] = tree_ids[t];
+      e->sample_args.ensure(sizeof(one));
+      e->upload_pinned(e->sample_args.p, &one, sizeof(one), w.stream);
+      const FaceDesc* d_f = e->sample_args.as<FaceDesc>();
+      const HpState* d_hs = reinterpret_cast<const HpState*>(e->sample_args.as<uint8_t>() + offsetof(decltype(one), hs));
+      launch_traverse(hp, d_f, 1, blocks_per_face(fv, hp, g), g,
                       hp ? e->hp_pairs.as<uint4>() : e->mp_pairs.as<uint4>(), hp ? e->hp_tops.as<uint4>() : e->mp_tops.as<uint4>(),
                       hp ? e->hp_topi.as<uint32_t>() : e->mp_topi.as<uint32_t>(), e->trav_top_max,
-                      hp ? e->hp_far.as<uint32_t>() : e->mp_far.as<uint32_t>(), hp ? nullptr : w.state.as<HpState>(),
+                      hp ? e->hp_far.as<uint32_t>() : e->mp_far.as<uint32_t>(), hp ? nullptr : d_hs,
                       hp ? e->hp_trees : 0, step, step, f.plane, s->chan.as<uint16_t>(), leaf_dev, e->trav_wg,
                       TRAV_LDS_CAP, w.stream);
       HIP_CHECK(hipGetLastError());
@@ -1565,6 +1602,7 @@ ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, i
   a.roots = hp ? e->hp_roots.as<int32_t>() : e->mp_roots.as<int32_t>();
   a.chan = s->chan.as<uint16_t>();
   a.plane = s->plane;
+  a.fint = s->fint;
   a.n_patches = n_patches;
   a.n_trees = n_trees;
   for (int t = 0; t < n_trees; t++) a.trees[t] = tree_ids[t];
@@ -1600,7 +1638,7 @@ ffd_status ffd_sample_create(ffd_engine* e, const uint8_t* gray, int32_t W, int3
   return guarded(e, [&]() -> ffd_status {
     if (!gray || !out || stride < W) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     *out = nullptr;
-    if (!sample_size_ok(W, H)) return fail(e, FFD_ERR_UNSUPPORTED, "image sample size unsupported (2..125 wide, 255 W H < 2^24)");
+    if (!sample_size_ok(W, H)) return fail(e, FFD_ERR_UNSUPPORTED, "image sample size unsupported (2..125 wide, 2 rows or more)");
     std::unique_ptr<ffd_sample> s(new ffd_sample);
     s->e = e;
     s->device = e->device;
@@ -1625,6 +1663,8 @@ ffd_status ffd_sample_create(ffd_engine* e, const uint8_t* gray, int32_t W, int3
     std::memset(&f, 0, sizeof(f));
     f.img_w = W; f.img_h = H; f.img_stride = 3 * W; f.bw = W; f.bh = H; f.W = W; f.H = H;
     f.scale = 1.f; f.mode = 0; f.valid = 1;
+    f.fint = (int64_t)255 * W * H >= (int64_t)1 << 24 ? 1 : 0;  // OpenCV's float integral rounds past 2^24
+    s->fint = f.fint;
     f.plane = s->plane;
     w.gray.ensure((size_t)H * PITCH + 256);
     w.mag.ensure((size_t)NGABOR * H * PITCH * 4 + 256);
@@ -1668,7 +1708,7 @@ ffd_status ffd_sample_create_from_channels(ffd_engine* e, const uint32_t* channe
   return guarded(e, [&]() -> ffd_status {
     if (!channels || !out) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     *out = nullptr;
-    if (!sample_size_ok(W, H)) return fail(e, FFD_ERR_UNSUPPORTED, "image sample size unsupported (2..125 wide, 255 W H < 2^24)");
+    if (!sample_size_ok(W, H)) return fail(e, FFD_ERR_UNSUPPORTED, "image sample size unsupported (2..125 wide, 2 rows or more)");
     std::unique_ptr<ffd_sample> s(new ffd_sample);
     s->e = e;
     s->device = e->device;
@@ -1676,10 +1716,15 @@ ffd_status ffd_sample_create_from_channels(ffd_engine* e, const uint32_t* channe
     s->H = H;
     s->plane = (int64_t)(H + 1) * PITCH;
     std::vector<uint16_t> J((size_t)NCH * s->plane, 0);
+    uint32_t vmax = 0;
     for (int c = 0; c < NCH; c++)
       for (int y = 0; y <= H; y++)
-        for (int x = 0; x <= W; x++)
-          J[(size_t)c * s->plane + (size_t)y * PITCH + x] = (uint16_t)channels[((size_t)c * (H + 1) + y) * (W + 1) + x];
+        for (int x = 0; x <= W; x++) {
+          const uint32_t v = channels[((size_t)c * (H + 1) + y) * (W + 1) + x];
+          vmax = std::max(vmax, v);
+          J[(size_t)c * s->plane + (size_t)y * PITCH + x] = (uint16_t)v;
+        }
+    s->fint = vmax >= (1u << 24) ? 1 : 0;  // float-rounded integrals (CV_32F past 2^24)
     s->chan.ensure(J.size() * 2 + 512);
     HIP_CHECK(hipMemcpyAsync(s->chan.p, J.data(), J.size() * 2, hipMemcpyHostToDevice, e->main_stream()));
     HIP_CHECK(hipStreamSynchronize(e->main_stream()));
@@ -1811,24 +1856,33 @@ ffd_status ffd_meanshift(ffd_engine* e, const ffd_vote* votes, int32_t n, const 
     if ((n && !votes) || n < 0 || !mean_xy) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     const ffd_meanshift_option o = option ? *option : e->desc.ms_option;
     if (o.max_iterations < 0 || o.kernel_size <= 0) return fail(e, FFD_ERR_INVALID_ARGUMENT, "invalid MeanShiftOption");
-    std::vector<Vote> v;
+    // positions beyond int16 (or FFD_VOTES_WIDE): the list as VoteW records (a wide face)
+    bool wide = e->force_wide;
+    for (int i = 0; i < n && !wide; i++)
+      wide = votes[i].check && (votes[i].x < -32768 || votes[i].x > 32767 || votes[i].y < -32768 || votes[i].y > 32767);
+    std::vector<VoteW> v;  // (narrow: packed as Vote below)
     v.reserve(n);
     for (int i = 0; i < n; i++) {
       if (!votes[i].check) continue;  // getMean / getWeightedMean skip unchecked votes
-      if (votes[i].x < -32768 || votes[i].x > 32767 || votes[i].y < -32768 || votes[i].y > 32767)
-        return fail(e, FFD_ERR_UNSUPPORTED, "vote position outside the 16-bit range");
-      v.push_back(Vote{(int16_t)votes[i].x, (int16_t)votes[i].y, votes[i].weight});
+      v.push_back(VoteW{votes[i].x, votes[i].y, votes[i].weight, 0});
     }
     e->sync_all();
     Workspace& w = *e->ws[0];
     FaceDesc f;
     std::memset(&f, 0, sizeof(f));
-    f.valid = 1; f.nochan = 1; f.scale = 1.f;
+    f.valid = 1; f.nochan = 1; f.scale = 1.f; f.wide = wide;
     f.nmx = std::max<int>(1, (int)v.size());
     f.nmy = 1;
     int32_t counts[NPARTS] = {(int32_t)v.size()};
-    w.votes.ensure(std::max<size_t>(1, v.size()) * sizeof(Vote));
-    if (!v.empty()) HIP_CHECK(hipMemcpyAsync(w.votes.p, v.data(), v.size() * sizeof(Vote), hipMemcpyHostToDevice, w.stream));
+    w.votes.ensure(std::max<size_t>(1, v.size()) * sizeof(VoteW));
+    if (wide) {
+      if (!v.empty()) HIP_CHECK(hipMemcpyAsync(w.votes.p, v.data(), v.size() * sizeof(VoteW), hipMemcpyHostToDevice, w.stream));
+    } else {
+      std::vector<Vote> p(v.size());
+      for (size_t i = 0; i < v.size(); i++) p[i] = Vote{(int16_t)v[i].x, (int16_t)v[i].y, v[i].w};
+      if (!p.empty()) HIP_CHECK(hipMemcpyAsync(w.votes.p, p.data(), p.size() * sizeof(Vote), hipMemcpyHostToDevice, w.stream));
+      HIP_CHECK(hipStreamSynchronize(w.stream));  // p is released on return
+    }
     w.vote_counts.ensure(sizeof(counts));
     HIP_CHECK(hipMemcpyAsync(w.vote_counts.p, counts, sizeof(counts), hipMemcpyHostToDevice, w.stream));
     w.ms_mean.ensure(NPARTS * 2 * 4);
@@ -1837,7 +1891,7 @@ ffd_status ffd_meanshift(ffd_engine* e, const ffd_vote* votes, int32_t n, const 
     upload(w.faces, one, w.stream);
     launch_meanshift(w.faces.as<FaceDesc>(), 1, nullptr, 1, 1, (float)o.kernel_size, o.max_iterations,
                      o.stopping_criteria, w.votes.as<Vote>(), w.vote_counts.as<int32_t>(), w.ms_mean.as<float>(),
-                     e->out.as<FaceOut>(), nullptr, w.stream);
+                     e->out.as<FaceOut>(), nullptr, w.stream, wide);
     HIP_CHECK(hipGetLastError());
     float m[2];
     HIP_CHECK(hipMemcpyAsync(m, w.ms_mean.p, sizeof(m), hipMemcpyDeviceToHost, w.stream));

@@ -68,6 +68,21 @@ struct Geometry {
   float scale = 0;
 };
 
+// The leaf offsets a vote table's voting parts can add to a patch centre (per axis, inclusive)
+struct VoteRange {
+  bool any = false;  // no voting offset at all: no votes
+  int lo_x = 0, hi_x = 0, lo_y = 0, hi_y = 0;
+};
+
+// 1: some vote position of face f may leave int16 (FaceDesc::wide: 16-B VoteW lists); positions are
+// vox + xi step + half + off_x, voy + yi step_y + half + off_y (face_utils.cpp:257-293)
+inline int votes_wide(const ffd::FaceDesc& f, int step, int step_y, int half, const VoteRange& r) {
+  if (!r.any || f.nmx <= 0 || f.nmy <= 0) return 0;
+  const int64_t x0 = (int64_t)f.vox + half + r.lo_x, x1 = (int64_t)f.vox + half + (int64_t)(f.nmx - 1) * step + r.hi_x;
+  const int64_t y0 = (int64_t)f.voy + half + r.lo_y, y1 = (int64_t)f.voy + half + (int64_t)(f.nmy - 1) * step_y + r.hi_y;
+  return x0 < -32768 || y0 < -32768 || x1 > 32767 || y1 > 32767;
+}
+
 }  // namespace ffd_host
 
 using namespace ffd;  // internal header: the engine's TUs work in ffd's vocabulary
@@ -92,6 +107,8 @@ struct Workspace {
   DevBuf gabor_redo;  // per scale and face: the fast Gabor instance flags faces for the exact one
   DevBuf ms_order;    // MeanShift chains sorted by list length (k_ms_order)
   DevBuf gabor_mm;    // per face and scale: the banded Gabor instances' 16-word slots (zero between launches)
+  DevBuf trav_queue;  // the traversals' per-XCD block counters (head pose 0..7, FFD 8..15)
+  DevBuf trav_order;  // the FFD pass's face order (k_trav_order)
   std::vector<FaceDesc> h_fds;  // host staging, reused only after `done`
   std::vector<FaceDesc> desc;   // descriptors of the chunk last run here (ffd_get_trace)
   int first = 0, count = 0;
@@ -104,15 +121,13 @@ struct Workspace {
 };
 
 namespace ffd_host {
-// Re-encode breadth-first 16-byte nodes (children adjacent) as k_traverse's 16-byte pair records in
-// depth-first sibling blocks (ffd_device.hpp "pair records", "sibling blocks"); roots_out[t] = tree t's
-// first block (P(root) in half 0).
+// Re-encode breadth-first 16-byte nodes (children adjacent) as k_traverse's 16-byte pair records
+// in depth-first order (ffd_device.hpp "pair records"); roots_out[t] = tree t's root pair.
 void build_pair_records(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots, std::vector<uint4>& out,
                         std::vector<int32_t>& roots_out, std::vector<uint32_t>& far);
-// Heap-ordered tree tops (ffd_device.hpp "tree tops") of every tree: TOP_CAP records + block indices.
+// Heap-ordered tree tops (ffd_device.hpp "tree tops") of every tree: TOP_CAP records + pair indices.
 void build_tree_tops(const std::vector<uint4>& pairs, const std::vector<int32_t>& proots,
-                     const std::vector<uint32_t>& far, const std::vector<uint4>& bfs, const std::vector<int32_t>& roots,
-                     std::vector<uint4>& tops, std::vector<uint32_t>& top_idx);
+                     const std::vector<uint32_t>& far, std::vector<uint4>& tops, std::vector<uint32_t>& top_idx);
 }  // namespace ffd_host
 
 struct ffd_engine {
@@ -120,6 +135,7 @@ struct ffd_engine {
   int device = 0;
   ffd_engine_desc desc{};
   int max_chunk = 4096;
+  int64_t chunk_bytes = (int64_t)40 << 30;  // a chunk's face buffers at most (FFD_CHUNK_BYTES; C2's 4,096 faces: ~26 GB)
   bool detector_only = false;  // ffd_detector_create: a Haar cascade and no forests
   int n_streams = 1;
   int gabor_exact = 0;      // FFD_GABOR_EXACT=1: every face through the exact (sqrtf) Gabor instance (tests)
@@ -133,6 +149,8 @@ struct ffd_engine {
   // Overridable with FFD_TRAV_G_{HP,FFD} / FFD_TRAV_WG / FFD_CHUNK / FFD_STREAMS.
   TravShape trav_g_hp{5, 4}, trav_g_mp{5, 5};
   int trav_wg = 256;
+  bool trav_queue = true;  // per-XCD block queues in the batch traversals (FFD_TRAV_QUEUE=0: static dealing)
+  bool trav_sort = true;   // the FFD pass walks its faces grouped by tree set (FFD_TRAV_SORT=0: batch order)
 
   // model parameters
   int face_size = 125, patch = 31, hp_trees = 0, n_forests = 0, ntrees_per_forest = 0;
@@ -140,15 +158,17 @@ struct ffd_engine {
 
   // device model
   DevBuf gabor_coef, hp_nodes, hp_roots, hp_sizes, hp_m, mp_nodes, mp_roots, mp_sizes, mp_rec;
-  DevBuf hp_pairs, mp_pairs;         // sibling blocks for k_traverse (ffd_device.hpp "sibling blocks")
-  DevBuf hp_proots, mp_proots;       // per tree: its first block
-  DevBuf hp_far, mp_far;             // per pair record: child 1's block offset (when > 65535)
-  DevBuf hp_tops, mp_tops, hp_topi, mp_topi;  // per tree: heap-ordered top pair records + their block indices
+  DevBuf hp_pairs, mp_pairs;         // pair records for k_traverse (ffd_device.hpp "pair records")
+  DevBuf hp_proots, mp_proots;       // per tree: index of its root pair
+  DevBuf hp_far, mp_far;             // per pair: far offset of child 1's children (when > 65535)
+  DevBuf hp_tops, mp_tops, hp_topi, mp_topi;  // per tree: heap-ordered top pair records + their indices
   int trav_top_max = TOP_CAP;        // tree-top entries staged per tree at most (FFD_TRAV_TOPMAX)
   std::vector<uint4> hp_nodes_h, mp_nodes_h;  // host copies until the walk nodes are built
   std::vector<int32_t> hp_roots_h, mp_roots_h;
   bool vote_rec_compact = false;     // 32-B vote records (else 64-B), see load_model
   int vote_bias_x = 0, vote_bias_y = 0;
+  ffd_host::VoteRange vote_range;    // the offsets those records can add (FaceDesc::wide)
+  bool force_wide = false;           // FFD_VOTES_WIDE=1: every face through the wide vote path (tests)
   std::string model_path;            // the FFDMODEL file (re-read for option-dependent tables)
 
   // Option-dependent leaf tables (head-pose values m, FFD vote records) for per-call estimator
@@ -161,6 +181,7 @@ struct ffd_engine {
     DevBuf hp_m, mp_rec;
     bool compact = false;
     int bias_x = 0, bias_y = 0;
+    ffd_host::VoteRange range;
   } alt;
   std::shared_ptr<ffd::ModelFile> leaf_model;  // leaf payload arrays (hp.leaf_*, mp.leaf_*), lazily
   const ffd::ModelFile& leaf_arrays();
@@ -194,6 +215,7 @@ struct ffd_engine {
     ~Pinned() { if (p) (void)hipHostFree(p); }
   } pin_leaf, pin_patch;
   DevBuf sample_patches;
+  DevBuf sample_args;  // a sample's grid evaluation: its descriptor and tree list (one upload)
   int last_ws = -1;
   // live image samples (ffd_sample_*): a sample destroyed after its engine must not touch the engine, so the
   // engine frees the samples' device planes when it goes and marks them orphaned (ffd_engine_destroy)
@@ -233,11 +255,18 @@ struct ffd_engine {
     HIP_CHECK(hipEventRecord(p.b, s));
     pending.push_back(p);
   }
-  void sync_all() {
-    if (copy_stream) HIP_CHECK(hipStreamSynchronize(copy_stream));
+  void sync_all() {  // (a stream with nothing queued answers the query at once: no wait)
+    auto idle = [](hipStream_t s) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipErrorNotReady) return false;
+      HIP_CHECK(q);
+      return true;
+    };
+    if (copy_stream && !idle(copy_stream)) HIP_CHECK(hipStreamSynchronize(copy_stream));
     for (auto& w : ws) {
-      for (auto f : w->fork) HIP_CHECK(hipStreamSynchronize(f));
-      HIP_CHECK(hipStreamSynchronize(w->stream));
+      for (auto f : w->fork)
+        if (!idle(f)) HIP_CHECK(hipStreamSynchronize(f));
+      if (!idle(w->stream)) HIP_CHECK(hipStreamSynchronize(w->stream));
     }
   }
   void resolve() {
@@ -358,7 +387,7 @@ struct ffd_engine {
       std::vector<int32_t> rp;
       std::vector<uint32_t> far, topi;
       ffd_host::build_pair_records(h, roots, pr, rp, far);
-      ffd_host::build_tree_tops(pr, rp, far, h, roots, tops, topi);
+      ffd_host::build_tree_tops(pr, rp, far, tops, topi);
       upload(d, pr, main_stream());
       upload(droots, rp, main_stream());
       upload(dfar, far, main_stream());
@@ -388,6 +417,7 @@ struct VoteTable {
   std::vector<uint32_t> rec;
   bool compact = false;
   int bias_x = 0, bias_y = 0;
+  VoteRange range;
 };
 VoteTable mp_vote_records(const ffd::ModelFile& m, const ffd_multipart_option& o);
 // status + message helpers shared by the C entry points

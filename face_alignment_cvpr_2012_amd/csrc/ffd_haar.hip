@@ -562,6 +562,7 @@ __global__ __launch_bounds__(HC_THREADS) void k_haar_group(const HaarFrame* __re
                                                             int widen, int4* __restrict__ cls_rect,
                                                             int* __restrict__ cls_sum, int4* __restrict__ boxes,
                                                             int32_t* __restrict__ n_boxes, int* __restrict__ label_g) {
+  // (GLOBAL: the labels arrive converged from k_haar_label_round / k_haar_label_jump, spread over the chip)
   __shared__ int label_s[GLOBAL ? 1 : HAAR_MAX_CAND];
   int* const labp = GLOBAL ? label_g + (int64_t)blockIdx.x * cap : label_s;
   auto lget = [&](int i) -> int {
@@ -585,8 +586,8 @@ __global__ __launch_bounds__(HC_THREADS) void k_haar_group(const HaarFrame* __re
     return;
   }
   // connected components of SimilarRects: every label converges to its component's smallest index
-  for (int i = threadIdx.x; i < N; i += HC_THREADS) lset(i, i);
-  for (;;) {
+  if (!GLOBAL) for (int i = threadIdx.x; i < N; i += HC_THREADS) lset(i, i);
+  for (; !GLOBAL;) {
     if (threadIdx.x == 0) changed = 0;
     __syncthreads();
     for (int i = threadIdx.x; i < N; i += HC_THREADS) {
@@ -742,6 +743,61 @@ void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, c
                                                                            n_stages, ww, wh, order_free, result);
 }
 
+// The grouping of a frame with more raw detections than a workgroup's LDS holds (the overflow re-run, one frame):
+// the same connected components of SimilarRects (every label the smallest index of its component), with the
+// O(N^2) pair tests spread over the whole chip.  A round: every candidate i takes the smallest label among the
+// candidates similar to it (tiles of candidates and their labels staged in LDS; labels only decrease, so reading
+// one that another workgroup is lowering at the same time only speeds convergence), then pointer jumping; the
+// host repeats rounds until one changes nothing.
+constexpr int HL_THREADS = 256;
+__global__ __launch_bounds__(HL_THREADS) void k_haar_label_init(const int32_t* __restrict__ n_cand, int cap,
+                                                              int* __restrict__ label) {
+  const int N = min(n_cand[0], cap);
+  for (int i = blockIdx.x * HL_THREADS + threadIdx.x; i < N; i += gridDim.x * HL_THREADS) label[i] = i;
+}
+__global__ __launch_bounds__(HL_THREADS) void k_haar_label_round(const int4* __restrict__ R, const int32_t* __restrict__ n_cand,
+                                                               int cap, int* __restrict__ label, int* __restrict__ changed) {
+  __shared__ int4 tr[HL_THREADS];
+  __shared__ int tl[HL_THREADS];
+  const int N = min(n_cand[0], cap);
+  const int i = blockIdx.x * HL_THREADS + threadIdx.x;
+  if (blockIdx.x * HL_THREADS >= N) return;  // (whole workgroup: the barriers below stay uniform)
+  const int4 ri = i < N ? R[i] : make_int4(0, 0, 0, 0);
+  int m = i < N ? __hip_atomic_load(&label[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  const int m0 = m;
+  for (int j0 = 0; j0 < N; j0 += HL_THREADS) {
+    const int j = j0 + threadIdx.x;
+    if (j < N) {
+      tr[threadIdx.x] = R[j];
+      tl[threadIdx.x] = __hip_atomic_load(&label[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (i < N) {
+      const int n = min(HL_THREADS, N - j0);
+      for (int k = 0; k < n; k++)
+        if (j0 + k != i && tl[k] < m && similar_rects(ri, tr[k], 0.2)) m = tl[k];
+    }
+    __syncthreads();
+  }
+  if (i < N && m < m0) {
+    __hip_atomic_fetch_min(&label[i], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(changed, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__global__ __launch_bounds__(HL_THREADS) void k_haar_label_jump(const int32_t* __restrict__ n_cand, int cap,
+                                                              int* __restrict__ label) {
+  const int N = min(n_cand[0], cap);
+  for (int i = blockIdx.x * HL_THREADS + threadIdx.x; i < N; i += gridDim.x * HL_THREADS) {
+    int l = __hip_atomic_load(&label[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      const int n = __hip_atomic_load(&label[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (n == l) break;
+      l = n;
+    }
+    __hip_atomic_fetch_min(&label[i], l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 void launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows, int32_t* rowcnt,
                        const HaarLevel* levels, const int8_t* result, int cap, int4* cand, int32_t* n_cand,
                        int min_neighbors, int widen, int4* cls_rect, int* cls_sum, int4* boxes, int32_t* n_boxes,
@@ -755,9 +811,24 @@ void launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows
   if (max_frame_rows > 0) k_haar_rowcount<<<dim3(n_frames, rb), HR_THREADS, 0, s>>>(frames, levels, result, max_frame_rows, rowcnt);
   k_haar_emit<<<dim3(n_frames, rb), HR_THREADS, 0, s>>>(frames, levels, result, max_frame_rows, rowcnt, cap, cand, n_cand);
 #endif
-  if (cap > HAAR_MAX_CAND)
+  if (cap > HAAR_MAX_CAND) {  // (one frame: the overflow re-run)
+    if (min_neighbors > 0) {
+      int* changed = label_g + cap;  // (the label buffer holds cap + 1 ints)
+      const int grid = (cap + HL_THREADS - 1) / HL_THREADS;
+      k_haar_label_init<<<std::min(grid, 1024), HL_THREADS, 0, s>>>(n_cand, cap, label_g);
+      for (int round = 0;; round++) {
+        int h = 0;
+        (void)hipMemsetAsync(changed, 0, sizeof(int), s);
+        k_haar_label_round<<<grid, HL_THREADS, 0, s>>>(cand, n_cand, cap, label_g, changed);
+        k_haar_label_jump<<<std::min(grid, 1024), HL_THREADS, 0, s>>>(n_cand, cap, label_g);
+        if (hipMemcpyAsync(&h, changed, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess || !h || round > cap)
+          break;
+      }
+    }
     k_haar_group<true><<<n_frames, HC_THREADS, 0, s>>>(frames, cap, cand, n_cand, min_neighbors, widen, cls_rect, cls_sum,
                                                      boxes, n_boxes, label_g);
+  }
   else
     k_haar_group<false><<<n_frames, HC_THREADS, 0, s>>>(frames, cap, cand, n_cand, min_neighbors, widen, cls_rect,
                                                       cls_sum, boxes, n_boxes, nullptr);

@@ -11,6 +11,7 @@
 namespace ffd {
 
 constexpr int HAAR_MAX_CAND = 8192;  // raw candidates per frame the grouping kernel holds (LDS labels)
+constexpr int HAAR_GROUP_MAX = 1 << 20;  // raw candidates of one frame grouped at all (FFD_ERR_UNSUPPORTED beyond)
 
 // One frame of a detection batch.
 struct HaarFrame {

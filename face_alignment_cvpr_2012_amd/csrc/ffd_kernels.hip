@@ -557,9 +557,6 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restric
 //   H_OFF + 16 (t + R)  t = -R..R: (hc0, hs0), (g, g), then for p = 1..3 (hc_p, hc_p, hs_p, hs_p)
 //                       [hs_p(t) odd in t]
 constexpr int GS_THREADS = 256, GS_BY = 8;
-#ifndef FFD_GABOR_PROBE
-#define FFD_GABOR_PROBE 0
-#endif
 #ifndef FFD_GS_QSPLIT
 #define FFD_GS_QSPLIT 1  // k_gabor_sep: V / H passes in two plane halves (LDS 66 -> 47 KB at 25x25: 3 WGs per CU)
 #endif
@@ -654,7 +651,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
   if (!TALL) stage_rows(yb, (ye - yb + GS_BY - 1) / GS_BY * GS_BY + 2 * R);
 
 #pragma unroll 1
-  for (int y0 = yb; y0 < (FFD_GABOR_PROBE == 5 ? 0 : ye); y0 += GS_BY) {  // probe 5: epilogue only
+  for (int y0 = yb; y0 < ye; y0 += GS_BY) {  // probe 5: epilogue only
     __syncthreads();  // the face is staged; the previous H pass is done with vg / vq
     if (TALL) {       // (the previous V pass is done with gface: the barrier before the H pass)
       stage_rows(y0, GS_BY + 2 * R);
@@ -680,7 +677,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
       constexpr int QLO = decltype(qlo_c)::value, QN = decltype(qn_c)::value;
       constexpr bool G = decltype(g_c)::value;
 #pragma unroll 1
-      for (int i = tid; i < (FFD_GABOR_PROBE == 3 ? 0 : GS_BY * C::SC); i += GS_THREADS) {
+      for (int i = tid; i < GS_BY * C::SC; i += GS_THREADS) {
         const int r = i / C::SC, cc = i - r * C::SC;
         if (cc >= NPC) continue;
         const uint8_t* col = &gface[((TALL ? 0 : y0 - yb) + r + R) * C::GP + cc];
@@ -770,7 +767,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
     } else {
     // ---- V pass
 #pragma unroll 1
-    for (int i = tid; i < (FFD_GABOR_PROBE == 3 ? 0 : GS_BY * C::SC); i += GS_THREADS) {
+    for (int i = tid; i < GS_BY * C::SC; i += GS_THREADS) {
       const int r = i / C::SC, cc = i - r * C::SC;
       if (cc >= NPC) continue;
       const uint8_t* col = &gface[((TALL ? 0 : y0 - yb) + r + R) * C::GP + cc];
@@ -864,17 +861,11 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
           minmax_update<GS_MASK>(mn[o], mx[o], m4[k], x0 + k < FW);
         }
         // columns >= W land in the row's pitch padding, never read
-#if FFD_GABOR_PROBE != 1 && FFD_GABOR_PROBE != 4  // 4: epilogue reads whatever the buffer holds
         *reinterpret_cast<float4*>(&mag[fd.mag_off + ((int64_t)(NU * 7 + o) * FH + y) * PITCH + x0]) =
             make_float4(m4[0], m4[1], m4[2], m4[3]);
-#endif
       }
     }
   }
-#if FFD_GABOR_PROBE == 1 || FFD_GABOR_PROBE == 2  // timing probes: no normalisation / integration
-  if (mn[0] == 0x12345u && mx[1] == 0x6789u) mag[0] = 0.f;
-  return;
-#endif
   if (SPLIT) {
     if (!split_finish<EXACT>(mn, mx, tiny, force, split_mm + ((int64_t)blockIdx.x * 5 + NU) * 16, nwg,
                              redo + blockIdx.x))
@@ -937,14 +928,37 @@ __device__ __forceinline__ int rect_mean_lds(const unsigned char* __restrict__ p
   return (int)__builtin_fmaf((float)((uint32_t)top + bot), __builtin_amdgcn_rcpf((float)area), 0.00075f);
 }
 
-// Tree<S>::evaluateMT over global u16 planes (ffd_forest_eval_leaves hook).
+// Rectangle means of float-integral faces (FaceDesc::fint: the reference's CV_32F integral may round,
+// FeatureChannelFactory.hpp:46-57 with OpenCV's float integral_): evalTest (ImageSample.cpp:48-63) on
+// the rounded integral values, (int)((float)(d - b - c + a) / (float)area).  A rectangle half's mod-2^16
+// combination is recovered in the window [-128, 65407]: its true value is the exact half sum (<= 61,710)
+// plus the rounding errors of at most 11 row additions in each of two columns (each <= 4 below 2^27):
+// |error| <= 88.  Sums may then be negative or exceed 255 area, so the quotient is an IEEE division
+// with truncation, as in the reference.
+__device__ __forceinline__ int rect_mean_fint(const uint16_t* __restrict__ I, int ld, int w, int h) {
+  const int h1 = h >> 1;
+  const uint32_t a = I[0], b = I[w], c = I[h1 * ld], d = I[h1 * ld + w], e = I[h * ld], f = I[h * ld + w];
+  auto half = [](uint32_t v) {
+    v &= 0xFFFFu;
+    return (int)v - (v >= 0xFF80u ? 65536 : 0);
+  };
+  const int R = half(d - c - b + a) + half(f - e - d + c);
+  return (int)((float)R / (float)(w * h));
+}
+
+// Tree<S>::evaluateMT over global u16 planes (ffd_forest_eval_leaves hook); FINT: float-rounded integrals.
+template <bool FINT = false>
 __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint32_t node,
                                            const uint16_t* __restrict__ chan, int64_t plane) {
   uint4 nd = nodes[node];
   while (!(nd.x & LEAF_BIT)) {
     const uint16_t* I = chan + (int64_t)(nd.y & 63u) * plane;
-    const int p1 = rect_mean16(I + node_off(nd.w & 0xFFFFu, PITCH), PITCH, (nd.y >> 6) & 31u, (nd.y >> 11) & 31u);
-    const int p2 = rect_mean16(I + node_off(nd.w >> 16, PITCH), PITCH, (nd.y >> 16) & 31u, (nd.y >> 21) & 31u);
+    const uint16_t* I1 = I + node_off(nd.w & 0xFFFFu, PITCH);
+    const uint16_t* I2 = I + node_off(nd.w >> 16, PITCH);
+    const int p1 = FINT ? rect_mean_fint(I1, PITCH, (nd.y >> 6) & 31u, (nd.y >> 11) & 31u)
+                        : rect_mean16(I1, PITCH, (nd.y >> 6) & 31u, (nd.y >> 11) & 31u);
+    const int p2 = FINT ? rect_mean_fint(I2, PITCH, (nd.y >> 16) & 31u, (nd.y >> 21) & 31u)
+                        : rect_mean16(I2, PITCH, (nd.y >> 16) & 31u, (nd.y >> 21) & 31u);
     node = nd.x + ((p1 - p2) <= (int)nd.z ? 0u : 1u);
     nd = nodes[node];
   }
@@ -960,18 +974,18 @@ __device__ __forceinline__ uint32_t walk16(const uint4* __restrict__ nodes, uint
 // between blocks.  Blocks are dealt XCD-contiguously and face-major, so the 32 workgroups of an XCD
 // share one or two faces' planes in that XCD's L2.
 //
-// Deep levels (below the LDS tree tops) read "sibling blocks" (ffd_device.hpp): the 32-byte block of a
-// node n holds the pair records of both its children.  A walk standing on node n (its test taken from
-// P(n's parent), already in registers) requests n's block before evaluating n's test; the block is used
-// one step later, when the walk stands on n's chosen child c and needs P(c) to select c's child's test.
-// So every record request has two tests' time to return from L2 instead of one (the round-4 walk
-// statistics put the wait for a record requested one test ahead at ~210 of ~1,000 cycles per step).
+// A walk holds the 16-byte pair record of the node it stands on (both siblings' 56-bit tests,
+// ffd_device.hpp "pair records"): the node's children pair is requested before its test is
+// evaluated (one 16-byte load per visit), and the test picks the child.  The record gathers are what
+// bounds the walk: one random 16-byte gather per lane costs the CU's vector-memory path about 2.4 cycles
+// from L2 and 7.6 from the Infinity Cache (tools/td_probe.hip, profiles/r5a), and a block needs ~6,500 of
+// them (500 walks x 13 deep levels).  Requesting both children's records a step ahead (two gathers per
+// step) was measured even (round 5, DESIGN.md tried-table).
 // Walker threads per workgroup by patch-block edge G: a block's G*G*T walks run in one round (T = 20
 // FFD trees: 4x4 -> 320, 5x5 -> 500 of 512), the other threads stage the next window.  A block costs
 // about its longest walk chain, so the walks a window holds per block set the throughput: FFD 5x5
 // blocks with 512 walkers took the FFD pass from 10.4 to 8.6 ms at C2 (profiles/r2c).
 constexpr int TRAV_NT = 1024;
-constexpr int TRAV_DEEP_UNROLL = 18;  // deep steps unrolled (FFD: 3 LDS-top levels + 18 = depth 21)
 __host__ __device__ constexpr int trav_nw(int GX, int GY, bool HP) { return GX * GY * (HP ? 15 : 20) <= 320 ? 320 : 512; }
 // Window chunks held in registers per staging thread: 16-byte chunks when the window row pitch is
 // a multiple of 8 columns, else 8-byte chunks (the pitch also sets the LDS bank pattern of the
@@ -1002,7 +1016,7 @@ __host__ __device__ __forceinline__ int trav_window_bytes(int WW, int WH, int xs
 
 // Tree tops in LDS: for each of the block's T trees the first TOPN entries of its heap-ordered top
 // table (TOP_CAP entries per tree in HBM, ffd_device.hpp "tree tops"): a 16-byte pair record and its
-// sibling-block index each (20 B).  TOPN = the largest power of two <= top_max whose T tables fit in
+// global pair index each (20 B).  TOPN = the largest power of two <= top_max whose T tables fit in
 // the LDS left over by the window (FFD 5x5 window, 20 trees: 8 entries = levels 0..2).
 constexpr int TRAV_TOP_ENTRIES = 1400;  // tree-top entries a block stages at most (2 per staging thread)
 __host__ __device__ __forceinline__ int trav_top_n(int T, int free_bytes, int top_max, int cap = TRAV_TOP_ENTRIES) {
@@ -1017,11 +1031,11 @@ constexpr int TRAV_BLK_BYTES = 64;  // the block descriptor the stagers hand to 
 struct TravArgs {
   const FaceDesc* faces;
   int n_faces, bpf;        // blocks per face: ceil(nx/G) * ceil(ny/G) (max over the batch)
-  const uint4* pairs;      // sibling blocks (2 pair records each)
+  const uint4* pairs;      // pair records
   const uint4* tops;       // per tree: TOP_CAP heap-ordered pair records (levels 0..6)
-  const uint32_t* top_idx; // ... and the sibling-block index of each entry's node
+  const uint32_t* top_idx; // ... and their global pair indices
   int top_free, top_max;   // LDS bytes after the window; cap on the entries staged per tree
-  const uint32_t* far;     // per pair record: child 1's block offset when it exceeds 16 bits
+  const uint32_t* far;     // per pair: offset of child 1's children pair when it exceeds 16 bits
   const HpState* hp_state; // FFD pass: selected trees; nullptr for the head-pose pass
   int ntrees_hp;           // head-pose pass: number of trees
   int step, step_y;        // patch grid steps (x, y)
@@ -1029,6 +1043,8 @@ struct TravArgs {
   int lds_bytes;           // dynamic LDS of the workgroup
   const uint16_t* chan;
   int32_t* leaf_out;
+  const int32_t* order;    // the faces in walking order (FFD pass: grouped by tree set, k_trav_order), or nullptr
+  uint32_t* queue;         // per XCD: blocks handed out so far (zeroed before the launch), or nullptr: static dealing
 };
 
 template <bool HP, int GX, int GY, int CB>
@@ -1056,6 +1072,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     int f, xi0, yi0, px0, py0, nx, ny, T;
     int ok;
     int out_lo, out_hi;  // element offset of the face's leaf block (FaceDesc hp_off / mp_off)
+    int more;            // 0: past the XCD's last block (every wave leaves its loop)
   };
   // The block a window holds, computed by the stagers with the window's next fill and handed to the walkers
   // through LDS at the end of the allocation (TRAV_BLK_BYTES), so the walkers start walking after the barrier
@@ -1064,8 +1081,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   auto block = [&](int lb) {
     Blk B;
     B.ok = 0;
-    B.f = lb / A.bpf;
+    B.more = lb < end;
+    B.f = B.more ? lb / A.bpf : 0;
     const int b = lb - B.f * A.bpf;
+    if (B.more && A.order) B.f = A.order[B.f];
     const FaceDesc& fd = A.faces[B.f];
     B.nx = HP ? fd.nhx : fd.nmx;
     B.ny = HP ? fd.nhy : fd.nmy;
@@ -1075,7 +1094,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     B.px0 = B.xi0 * step;
     B.py0 = B.yi0 * stepy;
     B.T = 0;
-    if (fd.valid && !fd.fint && B.nx > 0 && b < gbx * gby) {  // (float-integral faces: k_walk_fint)
+    if (B.more && fd.valid && !fd.fint && B.nx > 0 && b < gbx * gby) {  // (float-integral faces: k_walk_fint)
       B.ok = 1;
       B.T = HP ? A.ntrees_hp : A.hp_state[B.f].n_trees;
     }
@@ -1127,60 +1146,19 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         lo = s ? R.y : R.x;
         hi = s ? R.w : R.z;
       }
-      if (lo < (63u << 26)) {
-        // Deep levels.  State: the current node c (its test lo / hi), bc = c's sibling block, bp = the block of
-        // c's parent m, which holds P(c) in half sp.  Entry h of the tops is P(m); its block index is
-        // top_i[h]; child 1's block offset is in the record's top bytes (0: far[] at the record's position,
-        // 2 top_i[h >> 1] + (h & 1) for a top entry, 2 bp + sp below).
-        const uint32_t* ti = top_i + t * topn;
-        uint32_t bp = ti[h], sp = s;
-        const uint32_t o = (R.z >> 24) | ((R.w >> 24) << 8);
-        uint32_t bc = bp + (s ? o : 1u);
-        if (s && o == 0u) {  // (the far value consumed inside the branch, as in step below)
-          uint32_t fo = A.far[2u * ti[h >> 1] + (h > 1u ? (h & 1u) : 0u)];
-          asm volatile("" : "+v"(fo));
-          bc = bp + fo;
-          asm volatile("" : "+v"(bc));
-        }
-        // One step: request c's block into (nl, nh), take c's test, select P(c) from the block requested one
-        // step earlier (pl, ph) and c's chosen child's test from it.  The loop is unrolled by two so the two
-        // blocks swap roles instead of being copied (a register copy of a block still in flight would wait
-        // for it, and with it for the block just requested).
-        auto step = [&](const uint4& pl, const uint4& ph, uint4& nl, uint4& nh) {
-          nl = A.pairs[2u * bc];
-          nh = A.pairs[2u * bc + 1u];
-          const uint32_t sn = test(lo, hi);
-          const uint4 P = sp ? ph : pl;  // P(c): the tests of c's two children
-          const uint32_t o1 = (P.z >> 24) | ((P.w >> 24) << 8);
-          uint32_t nb = bc + (sn ? o1 : 1u);
-          if (sn && o1 == 0u) {
-            // (rare: an offset past 16 bits.)  The far value is consumed inside the branch, so its wait stays
-            // here instead of becoming a vmcnt(0) after the join, which would also wait for c's block
-            uint32_t fo = A.far[2u * bp + sp];
-            asm volatile("" : "+v"(fo));
-            nb = bc + fo;
-            asm volatile("" : "+v"(nb));
-          }
-          lo = sn ? P.y : P.x;
-          hi = sn ? P.w : P.z;
-          bp = bc;
-          bc = nb;
-          sp = sn;
-          return lo >= (63u << 26);
-        };
-        uint4 Xl = A.pairs[2u * bp], Xh = A.pairs[2u * bp + 1u];  // m's block: P(c) in half sp
-        uint4 Yl, Yh;
-        // straight-line steps (no loop-carried block registers for the allocator to split), then a loop for
-        // walks deeper than TRAV_DEEP_UNROLL steps
-        bool fin = false;
-#pragma unroll
-        for (int d = 0; d < TRAV_DEEP_UNROLL; d += 2) {
-          if (step(Xl, Xh, Yl, Yh)) { fin = true; break; }
-          if (step(Yl, Yh, Xl, Xh)) { fin = true; break; }
-        }
-        if (!fin)
-          while (!step(Xl, Xh, Yl, Yh) && !step(Yl, Yh, Xl, Xh)) {
-          }
+      // deeper levels: pair records from L2, the children pair requested before the test.  The children pair of
+      // the current node is right after its own pair (child 0) or off1 away (child 1; off1 = 0: far[pair])
+      uint32_t P = top_i[t * topn + h];
+      while (lo < (63u << 26)) {  // not a leaf (ch = 63)
+        const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
+        uint32_t Q = P + (s ? off1 : 1u);
+        if (s && off1 == 0u) Q = P + A.far[P];
+        const uint4 Nr = A.pairs[Q];
+        s = test(lo, hi);
+        P = Q;
+        R = Nr;
+        lo = s ? R.y : R.x;
+        hi = s ? R.w : R.z;
       }
       out[(xi * B.ny + yi) * B.T + t] = (int32_t)((lo & 0xFFFFFu) | hi << 20);  // reference order
     }
@@ -1189,8 +1167,20 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   // Stager waves and walker waves run separate loops with the same barrier sequence per block
   // (waves are wholly one role), so the staging registers are live only in the stager loop and
   // the walkers get the rest of the register file.
-  int lb = start + k;
-  if (lb >= end) return;
+  // Block sequence of this workgroup: with a queue, the next unclaimed block of the XCD's range (an XCD's 32
+  // workgroups then stay on the same one or two faces, whose planes and tree records share its L2, and the
+  // faster workgroups take more blocks); else start + k, + nk, ...  Thread NW claims block i + 2 while the window
+  // holds block i and leaves it in LDS slot i & 1 (read after the next window barrier).
+  int* q_slot = reinterpret_cast<int*>(smem + A.lds_bytes - TRAV_BLK_BYTES + 48);
+  int seq = 0;
+  auto claim = [&]() {
+    return A.queue ? start + (int)atomicAdd(&A.queue[xcd], 1u) : start + k + nk * seq++;
+  };
+  if (tid == NW) {
+    q_slot[0] = claim();
+    q_slot[1] = claim();
+  }
+  __syncthreads();
   if (tid >= NW) {
     // Staging: chunk i = (channel c, window row r, 8-column group q), i = (c * WH + r) * nq + q, goes
     // to LDS chunk i; staging thread s owns chunks s + u * NS.  Their face-relative source byte
@@ -1305,23 +1295,24 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       }
     };
 
-    Blk cur = block(lb);
+    Blk cur = block(q_slot[0]);
     prefetch(cur);
-    for (; lb < end; lb += nk) {
+    for (int it = 0;; it++) {
       __syncthreads();  // the previous block's walks are done with the window
       commit(cur);
-      __syncthreads();  // the window holds block lb
-      Blk nxt;
-      nxt.ok = false;
-      if (lb + nk < end) nxt = block(lb + nk);
+      __syncthreads();  // the window holds block `cur` (or the end marker)
+      if (!cur.more) break;
+      const Blk nxt = block(q_slot[(it + 1) & 1]);
+      if (tid == NW) q_slot[it & 1] = claim();  // block it + 2 (slot it & 1 was read before this window)
       prefetch(nxt);
       cur = nxt;
     }
   } else {
-    for (; lb < end; lb += nk) {
+    for (;;) {
       __syncthreads();
       __syncthreads();
       Blk cur = *blk_lds;
+      if (!__builtin_amdgcn_readfirstlane(cur.more)) break;
       cur.ok = __builtin_amdgcn_readfirstlane(cur.ok);
       cur.T = __builtin_amdgcn_readfirstlane(cur.T);
       if (cur.ok) walk_block(cur);
@@ -1334,12 +1325,13 @@ __global__ void k_eval_patches(const uint4* __restrict__ nodes, const int32_t* _
                                const int32_t* __restrict__ tree_ids, int n_trees,
                                const int32_t* __restrict__ patches, int n_patches,
                                const uint16_t* __restrict__ chan, int64_t plane,
-                               int32_t* __restrict__ leaf_ids) {
+                               int32_t* __restrict__ leaf_ids, int fint) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_patches * n_trees) return;
   const int p = i / n_trees, t = i % n_trees;
-  const uint16_t* I = chan + patches[2 * p + 1] * PITCH + patches[2 * p];
-  leaf_ids[i] = (int32_t)walk16(nodes, (uint32_t)roots[tree_ids[t]], I, plane);
+  const uint16_t* I = chan + (int64_t)patches[2 * p + 1] * PITCH + patches[2 * p];
+  const uint32_t root = (uint32_t)roots[tree_ids[t]];
+  leaf_ids[i] = (int32_t)(fint ? walk16<true>(nodes, root, I, plane) : walk16(nodes, root, I, plane));
 }
 
 // Forest<S>::evaluateMT on patches of a device-resident ImageSample (ffd_sample_eval_leaves): one lane
@@ -1365,7 +1357,8 @@ __global__ __launch_bounds__(256) void k_sample_eval(SampleEvalArgs A) {
     y = A.patches[2 * p + 1];
   }
   const uint16_t* I = A.chan + (int64_t)y * PITCH + x;
-  A.leaf_out[i] = (int32_t)walk16(A.nodes, (uint32_t)A.roots[A.trees[t]], I, A.plane);
+  const uint32_t root = (uint32_t)A.roots[A.trees[t]];
+  A.leaf_out[i] = (int32_t)(A.fint ? walk16<true>(A.nodes, root, I, A.plane) : walk16(A.nodes, root, I, A.plane));
 }
 
 void launch_sample_eval(const SampleEvalArgs& a, hipStream_t s) {
@@ -1374,24 +1367,8 @@ void launch_sample_eval(const SampleEvalArgs& a, hipStream_t s) {
   k_sample_eval<<<(total + 255) / 256, 256, 0, s>>>(a);
 }
 
-// The traversals of float-integral faces (FaceDesc::fint: the reference's CV_32F integral may round,
-// FeatureChannelFactory.hpp:46-57 with OpenCV's float integral_): evalTest (ImageSample.cpp:48-63) on
-// the rounded integral values, (int)((float)(d - b - c + a) / (float)area).  A rectangle half's mod-2^16
-// combination is recovered in the window [-128, 65407]: its true value is the exact half sum (<= 61,710)
-// plus the rounding errors of at most 11 row additions in each of two columns (each <= 4 below 2^27):
-// |error| <= 88.  Sums may then be negative or exceed 255 area, so the quotient is an IEEE division
-// with truncation, as in the reference.  Grid (slices, faces); other faces exit at once.
-__device__ __forceinline__ int rect_mean_fint(const uint16_t* __restrict__ I, int ld, int w, int h) {
-  const int h1 = h >> 1;
-  const uint32_t a = I[0], b = I[w], c = I[h1 * ld], d = I[h1 * ld + w], e = I[h * ld], f = I[h * ld + w];
-  auto half = [](uint32_t v) {
-    v &= 0xFFFFu;
-    return (int)v - (v >= 0xFF80u ? 65536 : 0);
-  };
-  const int R = half(d - c - b + a) + half(f - e - d + c);
-  return (int)((float)R / (float)(w * h));
-}
-
+// The traversals of float-integral faces (FaceDesc::fint, rect_mean_fint above).  Grid (slices, faces);
+// other faces exit at once.
 template <bool HP>
 __global__ __launch_bounds__(256) void k_walk_fint(const FaceDesc* __restrict__ faces, const uint4* __restrict__ nodes,
                                                   const int32_t* __restrict__ roots, int ntrees_hp,
@@ -1774,11 +1751,12 @@ __global__ __launch_bounds__(256) void k_hp_pose1(const FaceDesc* __restrict__ f
 #ifndef FFD_VOTE_U
 #define FFD_VOTE_U 2
 #endif
-template <bool compact>
+// VT: Vote, or VoteW for a wide face (FaceDesc::wide: positions beyond int16)
+template <bool compact, class VT>
 __device__ __forceinline__ void votes_range(const FaceDesc& fd, const int32_t* __restrict__ L,
                                             const uint4* __restrict__ leaf_rec, int bias_x, int bias_y, int T,
                                             int step, int step_y, int half_patch, int beg, int end,
-                                            Vote* __restrict__ V, int64_t cap, int (&cnt)[NPARTS]) {
+                                            VT* __restrict__ V, int64_t cap, int (&cnt)[NPARTS]) {
   const int lane = __lane_id();
   const int ny = fd.nmy;
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -1853,8 +1831,9 @@ __device__ __forceinline__ void votes_range(const FaceDesc& fd, const int32_t* _
         if (vote) {
           const int pos = cnt[i] + __popcll(bal & below);
           const int32_t o = (int32_t)off[i];
-          V[i * cap + pos] = Vote{(int16_t)((int)(int16_t)(o & 0xFFFF) + cur.vx0[u]),
-                                  (int16_t)((int)(int16_t)(o >> 16) + cur.vy0[u]), w};
+          const int vx = (int)(int16_t)(o & 0xFFFF) + cur.vx0[u], vy = (int)(int16_t)(o >> 16) + cur.vy0[u];
+          if constexpr (sizeof(VT) == sizeof(VoteW)) V[i * cap + pos] = VoteW{vx, vy, w, 0};
+          else V[i * cap + pos] = Vote{(int16_t)vx, (int16_t)vy, w};
         }
         cnt[i] += __popcll(bal);
       }
@@ -1882,8 +1861,12 @@ __global__ __launch_bounds__(256) void k_votes(const FaceDesc* __restrict__ face
   int cnt[NPARTS];
 #pragma unroll
   for (int i = 0; i < NPARTS; i++) cnt[i] = 0;
-  votes_range<compact>(fd, mp_leaf + fd.mp_off, leaf_rec, bias_x, bias_y, T, step, step_y, half_patch, 0, n * T,
-                       votes + fd.vote_off, (int64_t)tslots * n, cnt);
+  if (fd.wide)
+    votes_range<compact>(fd, mp_leaf + fd.mp_off, leaf_rec, bias_x, bias_y, T, step, step_y, half_patch, 0, n * T,
+                         reinterpret_cast<VoteW*>(votes + fd.vote_off), (int64_t)tslots * n, cnt);
+  else
+    votes_range<compact>(fd, mp_leaf + fd.mp_off, leaf_rec, bias_x, bias_y, T, step, step_y, half_patch, 0, n * T,
+                         votes + fd.vote_off, (int64_t)tslots * n, cnt);
   if (lane < n_parts) {
     int c = 0;
 #pragma unroll
@@ -1945,8 +1928,12 @@ __global__ __launch_bounds__(64 * VOTES_WG_WAVES) void k_votes_wg(const FaceDesc
     cnt[i] = b;
   }
   // pass 2: the votes at their final slots
-  votes_range<compact>(fd, L, leaf_rec, bias_x, bias_y, T, step, step_y, half_patch, beg, end, votes + fd.vote_off,
-                       (int64_t)tslots * n, cnt);
+  if (fd.wide)
+    votes_range<compact>(fd, L, leaf_rec, bias_x, bias_y, T, step, step_y, half_patch, beg, end,
+                         reinterpret_cast<VoteW*>(votes + fd.vote_off), (int64_t)tslots * n, cnt);
+  else
+    votes_range<compact>(fd, L, leaf_rec, bias_x, bias_y, T, step, step_y, half_patch, beg, end, votes + fd.vote_off,
+                         (int64_t)tslots * n, cnt);
   if (wv == VOTES_WG_WAVES - 1 && lane < n_parts) {
     int c = 0;
 #pragma unroll
@@ -1980,10 +1967,7 @@ constexpr int MS_FPW = (MS_FACES + 3) / 4;  // faces per wave
 #endif
 constexpr int MS_RA = FFD_MS_RA;  // serial phase: LDS reads in flight ahead of the adds
 #ifndef FFD_MS_DEFAULT
-#define FFD_MS_DEFAULT 0  // 0: chosen per batch (launch_meanshift); 1 k_meanshift, 3 k_meanshift3, 4 k_meanshift4
-#endif
-#ifndef FFD_MS_UDEF
-#define FFD_MS_UDEF 4
+#define FFD_MS_DEFAULT 0  // 0: chosen per batch (launch_meanshift); 1 k_meanshift, 4 k_meanshift4, 5 k_meanshift5
 #endif
 #ifndef FFD_MS_SORT
 #define FFD_MS_SORT 1  // k_meanshift over chains sorted by list length (k_ms_order)
@@ -1996,9 +1980,6 @@ constexpr int MS_RA = FFD_MS_RA;  // serial phase: LDS reads in flight ahead of 
 #endif
 #ifndef FFD_MS5_CHAINS
 #define FFD_MS5_CHAINS 640  // batches of up to 64 faces: k_meanshift5 (a workgroup per chain)
-#endif
-#ifndef FFD_MS_PROBE
-#define FFD_MS_PROBE 0  // timing probes (bits): 1 = no serial phase, 2 = cheap weights, 4 = no early convergence
 #endif
 
 // MeanShift::getWeightedMean's weight of one vote (MeanShift.hpp:122-124): d = cv::norm(mean - pos)
@@ -2075,7 +2056,7 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
     const int f = chain < n_chains ? (int)(chain / NPARTS) : n_faces, part = (int)(chain % NPARTS);
     int cnt = 0;
     int64_t vb = 0;
-    if (f < n_faces && faces[f].valid) {
+    if (f < n_faces && faces[f].valid && !faces[f].wide) {  // (wide faces: k_meanshift5)
       const FaceDesc& fd = faces[f];
       cnt = vote_counts[(int64_t)f * NPARTS + part];
       vb = fd.vote_off + (int64_t)part * tslots * fd.nmx * fd.nmy;
@@ -2083,7 +2064,7 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
     }
     s_cnt[tid] = cnt;
     s_vb[tid] = vb;
-    s_live[tid] = (f < n_faces && faces[f].valid) ? 1 : 0;
+    s_live[tid] = (f < n_faces && faces[f].valid && !faces[f].wide) ? 1 : 0;
     s_mx[tid] = 0.f;
     s_my[tid] = 0.f;
     atomicMax(&s_maxcnt, cnt);
@@ -2124,18 +2105,14 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         if (p >= MS_FACES || !s_live[p] || k0 + j >= s_cnt[p]) continue;
         const Vote v = vv[i];
         const float fx = (float)v.x, fy = (float)v.y;
-#if FFD_MS_PROBE & 2
-        const float w = pass < 0 ? v.w : v.w * (s_mx[p] - fx);
-#else
         const float w = pass < 0 ? v.w : ms_weight(s_mx[p], s_my[p], fx, fy, v.w, lamda, lam_y);
-#endif
         tx[j * MS_LD + p] = fx * w;
         ty[j * MS_LD + p] = fy * w;
         tw[j * MS_LD + p] = w;
       }
       if (k0 + MS_TILE < maxcnt) load_tile(k0 + MS_TILE);  // in flight during the serial phase
       __syncthreads();
-      if (!(FFD_MS_PROBE & 1) && tid < MS_FACES && s_live[tid]) {  // serial phase, in list order
+      if (tid < MS_FACES && s_live[tid]) {  // serial phase, in list order
         const int lim = min(MS_TILE, s_cnt[tid] - k0);
         int j = 0;
         for (; j + MS_RA <= lim; j += MS_RA) {  // LDS reads of MS_RA terms ahead of their in-order adds
@@ -2168,7 +2145,7 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         s_my[tid] = ay;
       } else {
         const float ddx = ax - s_mx[tid], ddy = ay - s_my[tid];
-        if (!(FFD_MS_PROBE & 4) && __builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) s_live[tid] = 0;  // converged
+        if (__builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) s_live[tid] = 0;  // converged
         s_mx[tid] = ax;
         s_my[tid] = ay;
       }
@@ -2178,152 +2155,7 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
   if (tid < MS_FACES) {
     const int chain = s_chain[tid];
     const int f = chain < n_faces * NPARTS ? chain / NPARTS : n_faces, part = chain % NPARTS;
-    if (f < n_faces && faces[f].valid) {
-      const float mx = s_mx[tid], my = s_my[tid];
-      if (part < n_parts) {
-        ms_mean[((int64_t)f * NPARTS + part) * 2] = mx;
-        ms_mean[((int64_t)f * NPARTS + part) * 2 + 1] = my;
-      }
-      const float inv = 1.0f / faces[f].scale;  // FaceForest.cpp:255-257
-      out[f].points[part][0] = part < n_parts ? cv_round((float)cv_round(mx) * inv) : 0;
-      out[f].points[part][1] = part < n_parts ? cv_round((float)cv_round(my) * inv) : 0;
-    }
-  }
-}
-
-// MeanShift, overlapped form (FFD_MS_KERNEL=3): a 256-thread workgroup runs F chains (F faces, one
-// landmark; a chain = one face's vote list for that landmark) through MeanShift::shift (MeanShift.hpp:41-135)
-// in tiles of T = 256 U / F votes per chain, double-buffered in LDS:
-//   terms   all 256 threads compute tile k + 1's per-vote terms (x*w, y*w, w) — U per thread, the votes
-//           loaded into registers a tile ahead — into one buffer,
-//   sums    while lanes 0..F-1 of wave 0 add tile k's terms (the other buffer) in list order,
-// one barrier per tile.  Every running sum is the reference's sequential float sum bit for bit; the terms
-// use ms_weight (the exact fast quotient at lamda = 10).  F is chosen per batch (launch_meanshift) so
-// that the grid still has two workgroups per CU.
-template <int F, int U>
-__global__ __launch_bounds__(256) void k_meanshift3(const FaceDesc* __restrict__ faces, int n_faces, int tslots,
-                                                   int n_parts, float lamda, float lam_y, int max_iter, float stop,
-                                                   const Vote* __restrict__ votes, const int32_t* __restrict__ vote_counts,
-                                                   float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
-  constexpr int T = 256 * U / F, CSTEP = 256 / T;  // votes per chain per tile; chain stride of a thread's items
-  static_assert(T * CSTEP == 256 && CSTEP * U == F && T >= 8, "tile shape");
-  __shared__ float4 term[2][T][F];  // [buffer][vote j][chain slot (c + j) mod F] = (x*w, y*w, w, 0)
-  __shared__ float s_mx[F], s_my[F];
-  __shared__ int s_cnt[F], s_live[F];
-  __shared__ int64_t s_vb[F];
-  __shared__ int s_maxcnt, s_any;
-  const int part = blockIdx.y, f0 = blockIdx.x * F, tid = threadIdx.x;
-  if (tid < F) {
-    const int f = f0 + tid;
-    int cnt = 0, live = 0;
-    int64_t vb = 0;
-    if (f < n_faces && faces[f].valid) {
-      const FaceDesc& fd = faces[f];
-      cnt = part < n_parts ? vote_counts[(int64_t)f * NPARTS + part] : 0;
-      vb = fd.vote_off + (int64_t)part * tslots * fd.nmx * fd.nmy;
-      live = 1;
-    }
-    s_cnt[tid] = cnt;
-    s_vb[tid] = vb;
-    s_live[tid] = live;
-    s_mx[tid] = 0.f;
-    s_my[tid] = 0.f;
-  }
-  const int j = tid % T, cb = tid / T;
-  float ax = 0, ay = 0, aw = 0;  // lane c < F of wave 0: chain c's running sums
-  for (int pass = -1; pass < max_iter; pass++) {
-    if (tid == 0) { s_maxcnt = 0; s_any = 0; }
-    __syncthreads();  // s_mx / s_my / s_live of the previous pass are final
-    if (tid < F && s_live[tid]) {
-      atomicMax(&s_maxcnt, s_cnt[tid]);
-      atomicOr(&s_any, 1);
-    }
-    __syncthreads();
-    if (!s_any) break;  // every chain converged
-    const int maxcnt = s_maxcnt;
-    ax = ay = aw = 0;
-    int lim[U];
-    float mx[U], my[U];
-    const Vote* vp[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int c = cb + CSTEP * u;
-      lim[u] = s_live[c] ? s_cnt[c] : 0;
-      mx[u] = s_mx[c];
-      my[u] = s_my[c];
-      vp[u] = votes + s_vb[c];
-    }
-    Vote v[U];
-    auto load = [&](int k0) {
-#pragma unroll
-      for (int u = 0; u < U; u++)
-        if (k0 + j < lim[u]) v[u] = vp[u][k0 + j];
-    };
-    auto terms = [&](int buf, int k0) {
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int c = cb + CSTEP * u;
-        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (k0 + j < lim[u]) {
-          const float fx = (float)v[u].x, fy = (float)v[u].y;
-          const float w = pass < 0 ? v[u].w : ms_weight(mx[u], my[u], fx, fy, v[u].w, lamda, lam_y);
-          t = make_float4(fx * w, fy * w, w, 0.f);
-        }
-        term[buf][j][(c + j) & (F - 1)] = t;
-      }
-    };
-    int buf = 0;
-    if (maxcnt > 0) {
-      load(0);
-      terms(0, 0);
-      if (T < maxcnt) load(T);
-    }
-    __syncthreads();
-    for (int k0 = 0; k0 < maxcnt; k0 += T, buf ^= 1) {
-      if (k0 + T < maxcnt) {  // the next tile's terms into the other buffer
-        terms(buf ^ 1, k0 + T);
-        if (k0 + 2 * T < maxcnt) load(k0 + 2 * T);
-      }
-      if (tid < F && s_live[tid]) {  // this tile's sums, in list order
-        const int n = min(T, s_cnt[tid] - k0);
-        int q = 0;
-        for (; q + 8 <= n; q += 8) {  // LDS reads 8 ahead of their in-order adds
-          float4 t[8];
-#pragma unroll
-          for (int e = 0; e < 8; e++) t[e] = term[buf][q + e][(tid + q + e) & (F - 1)];
-#pragma unroll
-          for (int e = 0; e < 8; e++) {
-            ax += t[e].x;
-            ay += t[e].y;
-            aw += t[e].z;
-          }
-        }
-        for (; q < n; q++) {
-          const float4 t = term[buf][q][(tid + q) & (F - 1)];
-          ax += t.x;
-          ay += t.y;
-          aw += t.z;
-        }
-      }
-      __syncthreads();  // tile k0 + T's terms are complete; tile k0's buffer is free
-    }
-    if (tid < F && s_live[tid]) {
-      if (aw > 0) { ax /= aw; ay /= aw; }
-      if (pass < 0) {
-        s_mx[tid] = ax;
-        s_my[tid] = ay;
-      } else {
-        const float ddx = ax - s_mx[tid], ddy = ay - s_my[tid];
-        if (!(FFD_MS_PROBE & 4) && __builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) s_live[tid] = 0;  // converged
-        s_mx[tid] = ax;
-        s_my[tid] = ay;
-      }
-    }
-  }
-  __syncthreads();
-  if (tid < F) {
-    const int f = f0 + tid;
-    if (f < n_faces && faces[f].valid) {
+    if (f < n_faces && faces[f].valid && !faces[f].wide) {
       const float mx = s_mx[tid], my = s_my[tid];
       if (part < n_parts) {
         ms_mean[((int64_t)f * NPARTS + part) * 2] = mx;
@@ -2374,7 +2206,7 @@ __global__ __launch_bounds__(256) void k_meanshift4(const FaceDesc* __restrict__
     if (g < n_chains) {
       const int f = (int)(g / NPARTS), part = (int)(g - (int64_t)f * NPARTS);
       const FaceDesc& fd = faces[f];
-      if (fd.valid) {
+      if (fd.valid && !fd.wide) {  // (wide faces: k_meanshift5)
         valid = 1;
         cnt = part < n_parts ? vote_counts[(int64_t)f * NPARTS + part] : 0;
         vb = fd.vote_off + (int64_t)part * tslots * fd.nmx * fd.nmy;
@@ -2449,7 +2281,7 @@ __global__ __launch_bounds__(256) void k_meanshift4(const FaceDesc* __restrict__
       if (aw > 0) { ax /= aw; ay /= aw; }
       if (pass >= 0) {
         const float ddx = ax - smx, ddy = ay - smy;
-        if (!(FFD_MS_PROBE & 4) && __builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) s_live = 0;
+        if (__builtin_sqrt((double)ddx * ddx + (double)ddy * ddy) < (double)stop) s_live = 0;
       }
       smx = ax;
       smy = ay;
@@ -2487,11 +2319,14 @@ __global__ __launch_bounds__(256) void k_meanshift4(const FaceDesc* __restrict__
 // tile k in list order (serial_sum), one barrier per tile.  The sums are the reference's sequential
 // float sums bit for bit; the terms use ms_weight.  A batch of a few faces has only 10 chains per face,
 // so what bounds the pass is one chain's serial adds, not the term arithmetic.
+// wide_only: the companion launch of a batch kernel, for the batch's wide faces (FaceDesc::wide, VoteW lists),
+// which the batch kernels skip; this form reads either list format.
 template <int U>
 __global__ __launch_bounds__(256) void k_meanshift5(const FaceDesc* __restrict__ faces, int n_faces, int tslots,
                                                    int n_parts, float lamda, float lam_y, int max_iter, float stop,
                                                    const Vote* __restrict__ votes, const int32_t* __restrict__ vote_counts,
-                                                   float* __restrict__ ms_mean, FaceOut* __restrict__ out) {
+                                                   float* __restrict__ ms_mean, FaceOut* __restrict__ out,
+                                                   int wide_only) {
   constexpr int NT = 192, T = NT * U;
   __shared__ __attribute__((aligned(16))) float tc[2][3][T];
   __shared__ float s_acc[3], s_m[2];
@@ -2499,18 +2334,29 @@ __global__ __launch_bounds__(256) void k_meanshift5(const FaceDesc* __restrict__
   const int tid = threadIdx.x, tt = tid - 64;
   const bool term_thread = tid >= 64;
   const int f = blockIdx.x / NPARTS, part = blockIdx.x - f * NPARTS;
-  if (f >= n_faces || !faces[f].valid) return;  // whole workgroup
+  if (f >= n_faces || !faces[f].valid || (wide_only && !faces[f].wide)) return;  // whole workgroup
   const FaceDesc& fd = faces[f];
   const int cnt = part < n_parts ? vote_counts[(int64_t)f * NPARTS + part] : 0;
-  const Vote* vp = votes + fd.vote_off + (int64_t)part * tslots * fd.nmx * fd.nmy;
+  const int64_t lb = (int64_t)part * tslots * fd.nmx * fd.nmy;
+  const Vote* vp = votes + fd.vote_off + lb;
+  const VoteW* vpw = reinterpret_cast<const VoteW*>(votes + fd.vote_off) + lb;
+  const bool wide = fd.wide != 0;
   float mx = 0.f, my = 0.f;
   for (int pass = -1; pass < max_iter; pass++) {
-    Vote v[U];
+    float vx[U], vy[U], vw[U];  // the vote positions as floats (exact: |position| < 2^24)
     auto load = [&](int k0) {
 #pragma unroll
       for (int u = 0; u < U; u++) {
         const int k = k0 + tt + NT * u;
-        if (k < cnt) v[u] = vp[k];
+        if (k < cnt) {
+          if (wide) {
+            const VoteW q = vpw[k];
+            vx[u] = (float)q.x; vy[u] = (float)q.y; vw[u] = q.w;
+          } else {
+            const Vote q = vp[k];
+            vx[u] = (float)q.x; vy[u] = (float)q.y; vw[u] = q.w;
+          }
+        }
       }
     };
     auto terms = [&](int buf, int k0) {
@@ -2518,8 +2364,8 @@ __global__ __launch_bounds__(256) void k_meanshift5(const FaceDesc* __restrict__
       for (int u = 0; u < U; u++) {
         const int k = k0 + tt + NT * u;
         if (k < cnt) {
-          const float fx = (float)v[u].x, fy = (float)v[u].y;
-          const float w = pass < 0 ? v[u].w : ms_weight(mx, my, fx, fy, v[u].w, lamda, lam_y);
+          const float fx = vx[u], fy = vy[u];
+          const float w = pass < 0 ? vw[u] : ms_weight(mx, my, fx, fy, vw[u], lamda, lam_y);
           tc[buf][0][tt + NT * u] = fx * w;
           tc[buf][1][tt + NT * u] = fy * w;
           tc[buf][2][tt + NT * u] = w;
@@ -2697,17 +2543,60 @@ bool traverse_shape_supported(TravShape g, bool hp) {
   return false;
 }
 
+// The FFD pass's face order (k_traverse's TravArgs::order): faces grouped by the forest that contributes most of
+// their selected trees and, within it, by how many of its trees they take (FaceForest.cpp:239-250 takes the first
+// floor(area * 20) trees of each pose forest), so the faces an XCD walks at the same time share most of their tree
+// records in its L2.  One workgroup, a counting sort.
+constexpr int TRAV_ORDER_KEYS = 5 * (MAX_TREES + 1);
+__global__ __launch_bounds__(1024) void k_trav_order(const HpState* __restrict__ state, int n_faces, int ntrees_per_forest,
+                                                     int32_t* __restrict__ order) {
+  __shared__ int hist[TRAV_ORDER_KEYS + 1];
+  const int tid = threadIdx.x;
+  auto key = [&](int f) {
+    const HpState& st = state[f];
+    int cnt[5] = {0, 0, 0, 0, 0};
+    for (int j = 0; j < st.n_trees && j < MAX_TREES; j++) {
+      const int fo = st.trees[j] / ntrees_per_forest;
+      if (fo >= 0 && fo < 5) cnt[fo]++;
+    }
+    int d = 0;
+    for (int i = 1; i < 5; i++) d = cnt[i] > cnt[d] ? i : d;
+    return d * (MAX_TREES + 1) + (MAX_TREES - min(cnt[d], MAX_TREES));
+  };
+  for (int i = tid; i <= TRAV_ORDER_KEYS; i += 1024) hist[i] = 0;
+  __syncthreads();
+  for (int f = tid; f < n_faces; f += 1024) atomicAdd(&hist[key(f)], 1);
+  __syncthreads();
+  if (tid == 0) {  // exclusive prefix over the few keys
+    int run = 0;
+    for (int i = 0; i <= TRAV_ORDER_KEYS; i++) {
+      const int v = hist[i];
+      hist[i] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  // (the order within a key is the atomics'; it changes no result: every face's leaves go to its own slots)
+  for (int f = tid; f < n_faces; f += 1024) order[atomicAdd(&hist[key(f)], 1)] = f;
+}
+
+void launch_trav_order(const HpState* state, int n, int ntrees_per_forest, int32_t* order, hipStream_t s) {
+  if (n > 0) k_trav_order<<<1, 1024, 0, s>>>(state, n, ntrees_per_forest, order);
+}
+
 void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, TravShape g, const uint4* pairs, const uint4* tops,
                      const uint32_t* top_idx, int top_max, const uint32_t* far, const HpState* state, int ntrees_hp,
                      int step, int step_y, int64_t plane, const uint16_t* chan, int32_t* leaf_out, int n_wg,
-                     int lds_cap, hipStream_t s) {
+                     int lds_cap, hipStream_t s, const int32_t* order, uint32_t* queue) {
   const int total_blocks = n * bpf;
   if (total_blocks <= 0) return;
   // the window, then as many tree-top entries as the rest of the CU's LDS holds
   const int WW = 32 + step * (g.gx - 1), WH = 32 + step_y * (g.gy - 1), lds = lds_cap;
+  if (queue) (void)hipMemsetAsync(queue, 0, 8 * sizeof(uint32_t), s);
   TravArgs A{faces, n, bpf, pairs, tops, top_idx, lds - trav_window_bytes(WW, WH, g.gx * step) - TRAV_BLK_BYTES, top_max,
-             far, state, ntrees_hp, step, step_y, (int)plane, lds, chan, leaf_out};
-  const int grid = std::max(8, n_wg & ~7);
+             far, state, ntrees_hp, step, step_y, (int)plane, lds, chan, leaf_out, order, queue};
+  // one persistent workgroup per CU, but no more than the blocks need (a one-face call has ~50 blocks)
+  const int grid = std::max(8, std::min(n_wg & ~7, (total_blocks + 7) & ~7));
   const bool c16 = trav_chunk_bytes(WW, g.gx * step) == 16;
 #define FFD_TRAV_LAUNCH(HPV, GXV, GYV)                                                    \
   if (hp == HPV && g.gx == GXV && g.gy == GYV) {                                          \
@@ -2756,11 +2645,11 @@ void launch_walk_fint(bool hp, const FaceDesc* faces, int n, const uint4* nodes,
 
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
                          const int32_t* patches, int n_patches, const uint16_t* chan, int64_t plane,
-                         int32_t* leaf_ids, hipStream_t s) {
+                         int32_t* leaf_ids, hipStream_t s, bool fint) {
   const int total = n_patches * n_trees;
   if (total <= 0) return;
   k_eval_patches<<<(total + 255) / 256, 256, 0, s>>>(nodes, roots, tree_ids, n_trees, patches, n_patches, chan,
-                                                     plane, leaf_ids);
+                                                     plane, leaf_ids, fint ? 1 : 0);
 }
 
 void launch_hp_pose(const FaceDesc* faces, int n, const int32_t* hp_leaf, const float* hp_m, int hp_trees,
@@ -2847,7 +2736,7 @@ __global__ __launch_bounds__(1024) void k_ms_order(const FaceDesc* __restrict__ 
 
 void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int tslots, int n_parts, float lamda,
                       int max_iter, float stop, const Vote* votes, const int32_t* vote_counts, float* ms_mean,
-                      FaceOut* out, int32_t* order, hipStream_t s) {
+                      FaceOut* out, int32_t* order, hipStream_t s, bool any_wide) {
   (void)state;
   // k_meanshift5 (5) for a few chains (single-face latency: one workgroup per chain); k_meanshift (1) when
   // the batch has chains for >= 4 of its workgroups per CU (C2: 2,048 workgroups, 2.45 ms, where
@@ -2866,9 +2755,12 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
   const float lam_y = lamda == 10.f ? 1.f / 10.f : 0.f;  // the verified fast quotient (ffd_div_rcp)
   if (which == 5) {
     k_meanshift5<4><<<(unsigned)chains, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes,
-                                                     vote_counts, ms_mean, out);
+                                                     vote_counts, ms_mean, out, 0);
     return;
   }
+  if (any_wide)  // the batch kernels below skip wide faces
+    k_meanshift5<4><<<(unsigned)chains, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes,
+                                                     vote_counts, ms_mean, out, 1);
   if (which == 1) {
     if (FFD_MS_SORT && order) {  // chains sorted by list length, MS_FACES per workgroup
       k_ms_order<<<1, 1024, 0, s>>>(faces, n, n_parts, vote_counts, order);
@@ -2883,21 +2775,6 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
     return;
   }
   const int64_t lists = (int64_t)n * NPARTS;
-  if (which == 3) {  // overlapped form: the most chains per workgroup that still gives >= 512 workgroups
-    static const int ms_u = [] {
-      const char* v = std::getenv("FFD_MS_U");
-      return v ? std::atoi(v) : FFD_MS_UDEF;
-    }();
-    auto grid_for = [&](int F) { return dim3((n + F - 1) / F, NPARTS); };
-#define FFD_MS3(FV, UV) k_meanshift3<FV, UV><<<grid_for(FV), 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out)
-    if (ms_u == 8) {
-      if (lists >= 64 * 512) FFD_MS3(64, 8); else if (lists >= 32 * 512) FFD_MS3(32, 8); else FFD_MS3(16, 8);
-    } else {
-      if (lists >= 64 * 512) FFD_MS3(64, 4); else if (lists >= 32 * 512) FFD_MS3(32, 4); else FFD_MS3(16, 4);
-    }
-#undef FFD_MS3
-    return;
-  }
   // wave-independent form: the most chains per wave (fewer idle lanes in the sums) that still gives
   // >= FFD_MS_WAVES waves (default 4096: four per SIMD)
   static const int64_t want = [] {

@@ -47,14 +47,17 @@ bool traverse_shape_supported(TravShape g, bool hp);  // an instantiated k_trave
 void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, TravShape g, const uint4* pairs, const uint4* tops,
                      const uint32_t* top_idx, int top_max, const uint32_t* far, const HpState* state, int ntrees_hp,
                      int step, int step_y, int64_t plane, const uint16_t* chan, int32_t* leaf_out, int n_wg,
-                     int lds_cap, hipStream_t s);
+                     int lds_cap, hipStream_t s, const int32_t* order = nullptr, uint32_t* queue = nullptr);
+// order: faces in walking order (or nullptr); queue: 8 per-XCD block counters the launch zeroes (nullptr: static
+// dealing).  launch_trav_order: the FFD pass's order, faces grouped by their selected trees (k_trav_order).
+void launch_trav_order(const HpState* state, int n, int ntrees_per_forest, int32_t* order, hipStream_t s);
 hipError_t set_traverse_lds_limit(int bytes);
 // the traversals of float-integral faces (FaceDesc::fint) over the 16-B node arrays
 void launch_walk_fint(bool hp, const FaceDesc* faces, int n, const uint4* nodes, const int32_t* roots, int ntrees_hp,
                       const HpState* state, int step, int step_y, const uint16_t* chan, int32_t* leaf_out, hipStream_t s);
 void launch_eval_patches(const uint4* nodes, const int32_t* roots, const int32_t* tree_ids, int n_trees,
                          const int32_t* patches, int n_patches, const uint16_t* chan, int64_t plane,
-                         int32_t* leaf_ids, hipStream_t s);
+                         int32_t* leaf_ids, hipStream_t s, bool fint = false);
 // Forest<S>::evaluateMT on a device-resident image sample (k_sample_eval): a patch list or a patch grid
 constexpr int SAMPLE_INLINE = 16;  // patches passed in the argument block
 struct SampleEvalArgs {
@@ -66,6 +69,7 @@ struct SampleEvalArgs {
   const int32_t* patches;  // (x, y) pairs when n_patches > SAMPLE_INLINE and not a grid
   int n_patches, n_trees;
   int grid_ny, x0, y0, step;  // grid mode when grid_ny > 0 (n_patches = grid_nx * grid_ny)
+  int fint;                // float-rounded integrals (FaceDesc::fint): rect_mean_fint
   int32_t trees[MAX_TREES];
   int32_t inl[2 * SAMPLE_INLINE];
 };
@@ -80,6 +84,6 @@ void launch_votes(const FaceDesc* faces, int n, const int32_t* mp_leaf, const ui
                   hipStream_t s);
 void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int tslots, int n_parts, float lamda,
                       int max_iter, float stop, const Vote* votes, const int32_t* vote_counts, float* ms_mean,
-                      FaceOut* out, int32_t* order, hipStream_t s);
+                      FaceOut* out, int32_t* order, hipStream_t s, bool any_wide = false);  // any_wide: a FaceDesc::wide face
 
 }  // namespace ffd

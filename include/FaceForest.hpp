@@ -45,6 +45,7 @@
 #pragma once
 
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -426,14 +427,37 @@ inline std::string model_cache_path(const std::string& key) {
   if (d.empty()) {
     const char* xdg = std::getenv("XDG_CACHE_HOME");
     const char* home = std::getenv("HOME");
-    d = xdg ? std::string(xdg) + "/ffd" : home ? std::string(home) + "/.cache/ffd" : "/tmp";
+    d = xdg ? std::string(xdg) + "/ffd" : home ? std::string(home) + "/.cache/ffd"
+                                              : "/tmp/ffd-" + std::to_string((long)getuid());  // (per user)
   }
   std::string p;
   for (size_t i = 1; i <= d.size(); i++)  // mkdir -p
-    if (i == d.size() || d[i] == '/') (void)mkdir(d.substr(0, i).c_str(), 0755);
+    if (i == d.size() || d[i] == '/') (void)mkdir(d.substr(0, i).c_str(), 0700);
   char name[64];
   std::snprintf(name, sizeof name, "/ffd_model_%016llx.bin", (unsigned long long)h);
   return d + name;
+}
+// a converted model in the cache is used only if it is a complete FFDMODEL container (its directory of arrays
+// ends inside the file): a file left by a crashed or concurrent writer is converted again
+inline bool model_file_ok(const std::string& p) {
+  std::ifstream f(p, std::ios::binary);
+  char head[16];
+  if (!f.read(head, 16) || std::string(head, 8) != "FFDMODEL") return false;
+  uint32_t ver, n;
+  std::memcpy(&ver, head + 8, 4);
+  std::memcpy(&n, head + 12, 4);
+  if (ver != 1 || n == 0 || n > 4096) return false;
+  uint64_t end = 0;
+  for (uint32_t i = 0; i < n; i++) {  // entries (ffd_model_format.h): name[48] dtype[8] ndim pad shape[4] offset nbytes
+    char e[112];
+    if (!f.read(e, 112)) return false;
+    uint64_t off, nb;
+    std::memcpy(&off, e + 96, 8);
+    std::memcpy(&nb, e + 104, 8);
+    end = std::max(end, off + nb);
+  }
+  f.seekg(0, std::ios::end);
+  return (uint64_t)f.tellg() >= end;
 }
 inline std::string file_key(const std::string& p) {
   struct stat st;
@@ -1244,12 +1268,17 @@ class FaceForest {
       }
     key += "|fd:" + detail::file_key(o.fd_option.path_face_cascade);
     model = detail::model_cache_path(key);
-    struct stat st;
-    if (stat(model.c_str(), &st) == 0) return true;
+    if (detail::model_file_ok(model)) return true;
+    if (o.fd_option.path_face_cascade.empty()) {  // CascadeClassifier::load("") fails the reference's ctor
+      err_ = "(!) Error loading cascade classifier: FaceDetectionOption::path_face_cascade is empty";
+      std::fprintf(stderr, "ERROR: %s\n", err_.c_str());
+      model.clear();
+      return false;
+    }
     const ffd_forest_param hp = detail::to_c(o.hp_forest_param), mp = detail::to_c(o.mp_forest_param);
     std::vector<const char*> dirs;
     for (const std::string& d : o.mp_forest_paths) dirs.push_back(d.c_str());
-    const char* cascade = o.fd_option.path_face_cascade.empty() ? nullptr : o.fd_option.path_face_cascade.c_str();
+    const char* cascade = o.fd_option.path_face_cascade.c_str();
     if (ffd_model_convert(&hp, &mp, dirs.data(), (int32_t)dirs.size(), cascade, model.c_str()) != FFD_OK) {
       err_ = std::string("(!) Error loading the forests: ") + ffd_model_convert_last_error();
       std::fprintf(stderr, "ERROR: %s\n", err_.c_str());

@@ -49,7 +49,7 @@ typedef enum {
   FFD_ERR_OUT_OF_MEMORY = 4,
   FFD_ERR_NOT_INITIALIZED = 5,
   FFD_ERR_INTERNAL = 6,
-  FFD_ERR_UNSUPPORTED = 7    /* per face: scaled face taller than 4,096 rows (box h/w > 32.8; the reference has no limit) */
+  FFD_ERR_UNSUPPORTED = 7    /* an image sample wider than 125 columns; a detection frame over 2^20 raw candidates */
 } ffd_status;
 
 /* Human-readable meaning of a status code (call or per-face). */
@@ -74,7 +74,8 @@ typedef struct {                                                       /* struct
   int32_t points[FFD_NUM_LANDMARKS][2]; /* Face::ffd_cordinates (bbox-relative) */
   int32_t n_trees;           /* FFD trees selected for this face (20 except edge cases) */
   int32_t status;            /* FFD_OK; FFD_ERR_INVALID_ARGUMENT: box outside the image or empty scaled
-                                face (the reference's CV_Assert); FFD_ERR_UNSUPPORTED: face too tall.
+                                face (the reference's CV_Assert); FFD_ERR_OUT_OF_MEMORY: scaled face over
+                                2^21 rows (> 50 GB of channel planes; box h/w > 16,777).
                                 A face with no head-pose patch is FFD_OK with the reference's result:
                                 NaN headpose / variance, landmarks (0, 0) */
 } ffd_face;
@@ -215,8 +216,11 @@ ffd_status ffd_forest_leaves(ffd_engine* engine, int32_t forest_kind, const int3
  * ffd_meanshift          MeanShift::shift (include/MeanShift.hpp:41-76) of one vote list on the GPU: votes
  *                        with check == 0 are skipped as in getMean / getWeightedMean; result = the mode before
  *                        rounding (the reference's Point_<int> result is cvRound of it).
- * A sample belongs to the engine that made it (destroy it before the engine).  Samples taller than 525
- * rows at width 125 (255 W H >= 2^24: the reference's float integrals round) are FFD_ERR_UNSUPPORTED. */
+ * A sample belongs to the engine that made it.  Destroying the engine first frees the sample's planes; the
+ * sample's calls then fail with FFD_ERR_INVALID_ARGUMENT and ffd_sample_destroy still releases it.  Samples
+ * whose integrals may pass 2^24 (255 W H >= 2^24: the reference's CV_32F integrals round) keep the rounded
+ * values and are walked with the reference's float rectangle means.  Samples wider than 125 columns are
+ * FFD_ERR_UNSUPPORTED (the u16 planes' pitch). */
 typedef struct ffd_sample ffd_sample;
 ffd_status ffd_sample_create(ffd_engine* engine, const uint8_t* gray, int32_t width, int32_t height, int32_t stride,
                              ffd_sample** out);
@@ -317,7 +321,8 @@ ffd_status ffd_engine_comm_info(ffd_engine* engine, int32_t* n_ranks, int32_t* r
  * Boxes beyond max_boxes / max_faces are counted in *n_boxes / *n_faces but not written.
  * Frames are grouped on the GPU with up to 8,192 raw (ungrouped) detections each in LDS; a frame with more
  * (natural 1080p frames give a few hundred) is run again on its own with a capacity that holds all of them
- * (component labels in global memory), so there is no limit but 2^24 detections per frame.
+ * (component labels in global memory, the pair tests spread over every CU); a frame with more than 2^20 raw
+ * detections fails with FFD_ERR_UNSUPPORTED.
  * Parity: bit-exact with the CPU restatement (oracle/); with OpenCV itself unpinned (no OpenCV here). */
 typedef struct {
   int32_t min_feature_size;    /* FaceDetectionOption (include/FaceForest.hpp:21-32): 30 */

@@ -76,6 +76,8 @@ def lib():
         L.oracle_exp.restype = ctypes.c_double
         L.oracle_expf.argtypes = [ctypes.c_float]
         L.oracle_expf.restype = ctypes.c_float
+        L.oracle_meanshift.argtypes = [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int32] * 3 + [ctypes.c_float,
+                                                                                                   ctypes.c_void_p]
         L.oracle_estimate_headpose.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 6 + [
             ctypes.POINTER(ctypes.c_float)] * 2
         L.oracle_estimate_facial_features.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 6 + [
@@ -241,6 +243,15 @@ def gabor_mag(face, index):
 
 def area_under_curve(x1, x2, mean, std):
     return lib().oracle_area_under_curve(x1, x2, mean, std)
+
+
+def meanshift(xy, w, kernel=10, iters=7, stop=0.05):
+    """MeanShift::shift (MeanShift.hpp:41-135) of one vote list: the mode (x, y) before cvRound."""
+    xy = np.ascontiguousarray(xy, np.int32).reshape(-1, 2)
+    w = np.ascontiguousarray(w, np.float32)
+    out = np.zeros(2, np.float32)
+    lib().oracle_meanshift(xy.ctypes.data, w.ctypes.data, len(w), kernel, iters, stop, out.ctypes.data)
+    return out
 
 
 def exp(x):

@@ -618,6 +618,35 @@ void estimate_headpose(const uint32_t* ch, int W, int H, int rx, int ry, int rw,
   *out_var = var;
 }
 
+struct MsVote { int x, y; float w; };
+
+// MeanShift::shift (MeanShift.hpp:41-135): getMean, then up to `iters` getWeightedMean passes with the
+// kernel exp(-d / lamda) until the mode moves less than `stop`; sequential float sums in list order.
+void ms_shift(const MsVote* V, int n, int kernel, int iters, float stop, float& out_x, float& out_y) {
+  float mx = 0, my = 0, sw = 0;
+  for (int k = 0; k < n; k++) { const MsVote& v = V[k]; float w = v.w; mx += v.x * w; my += v.y * w; sw += w; }
+  if (sw > 0) { mx /= sw; my /= sw; }
+  bool conv = false;
+  const float lamda = (float)kernel;
+  for (int it = 0; it < iters && !conv; it++) {
+    float sx = 0, sy = 0, s = 0;
+    for (int k = 0; k < n; k++) {
+      const MsVote& v = V[k];
+      float dx = mx - (float)v.x, dy = my - (float)v.y;
+      float d = (float)std::sqrt((double)dx * dx + (double)dy * dy);
+      d = ffd_expf(-d / lamda);
+      float w = v.w * d;
+      sx += v.x * w; sy += v.y * w; s += w;
+    }
+    if (s > 0) { sx /= s; sy /= s; }
+    float ddx = sx - mx, ddy = sy - my;
+    if (std::sqrt((double)ddx * ddx + (double)ddy * ddy) < stop) conv = true;
+    mx = sx; my = sy;
+  }
+  out_x = mx;
+  out_y = my;
+}
+
 // getFacialFeaturesVotesMT (face_utils.cpp:244-302) over the region with the given trees, then
 // MeanShift::shift per part (MeanShift.hpp:41-135; kernel `ms_kernel`, `ms_iter` iterations, stop
 // `ms_stop`: 10 / 7 / 0.05 as FaceForest::estimateFacialFeatures, FaceForest.cpp:74-95): pts = cvRound
@@ -638,8 +667,7 @@ void estimate_facial_features(const uint32_t* ch, int W, int H, int rx, int ry, 
     for (int t = 0; t < MT; t++)
       mp_leafs[i * MT + t] = walk(g_mp, g_mp.roots[trees[t]], ch, W, H, mp_patches[i].first, mp_patches[i].second);
   });
-  struct Vote { int x, y; float w; };
-  std::vector<std::vector<Vote>> votes(FFD_NUM_PARTS);
+  std::vector<std::vector<MsVote>> votes(FFD_NUM_PARTS);
   for (size_t k = 0; k < mp_leafs.size(); k++) {
     int L = mp_leafs[k];
     int ox = mp_patches[k / MT].first + P / 2, oy = mp_patches[k / MT].second + P / 2;
@@ -654,25 +682,8 @@ void estimate_facial_features(const uint32_t* ch, int W, int H, int rx, int ry, 
   for (int i = 0; i < FFD_NUM_PARTS; i++) {
     const auto& V = votes[i];
     vote_counts[i] = (int)V.size();
-    float mx = 0, my = 0, sw = 0;
-    for (const auto& v : V) { float w = v.w; mx += v.x * w; my += v.y * w; sw += w; }
-    if (sw > 0) { mx /= sw; my /= sw; }
-    bool conv = false;
-    const float lamda = (float)ms_kernel, stop = ms_stop;
-    for (int it = 0; it < ms_iter && !conv; it++) {
-      float sx = 0, sy = 0, s = 0;
-      for (const auto& v : V) {
-        float dx = mx - (float)v.x, dy = my - (float)v.y;
-        float d = (float)std::sqrt((double)dx * dx + (double)dy * dy);
-        d = ffd_expf(-d / lamda);
-        float w = v.w * d;
-        sx += v.x * w; sy += v.y * w; s += w;
-      }
-      if (s > 0) { sx /= s; sy /= s; }
-      float ddx = sx - mx, ddy = sy - my;
-      if (std::sqrt((double)ddx * ddx + (double)ddy * ddy) < stop) conv = true;
-      mx = sx; my = sy;
-    }
+    float mx, my;
+    ms_shift(V.data(), (int)V.size(), ms_kernel, ms_iter, ms_stop, mx, my);
     ms_mean[2 * i] = mx;
     ms_mean[2 * i + 1] = my;
     pts[i][0] = i < NP ? cv_round(mx) : 0;
@@ -1010,6 +1021,13 @@ int oracle_gabor_mag(const uint8_t* face, int32_t w, int32_t h, int32_t index, f
 
 double oracle_area_under_curve(float x1, float x2, double mean, double std_) {
   return area_under_curve(x1, x2, mean, std_);
+}
+
+void oracle_meanshift(const int32_t* xy, const float* w, int32_t n, int32_t kernel, int32_t iters, float stop,
+                      float* mean_xy) {
+  std::vector<MsVote> V(n);
+  for (int i = 0; i < n; i++) V[i] = MsVote{xy[2 * i], xy[2 * i + 1], w[i]};
+  ms_shift(V.data(), n, kernel, iters, stop, mean_xy[0], mean_xy[1]);
 }
 
 double oracle_exp(double x) { return ffd_exp(x); }

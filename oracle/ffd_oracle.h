@@ -145,6 +145,9 @@ int oracle_channels(const uint8_t* face, int32_t w, int32_t h, uint32_t* channel
 int oracle_gabor_kernel(int32_t index, float* real, float* imag, int32_t* width);
 int oracle_gabor_mag(const uint8_t* face, int32_t w, int32_t h, int32_t index, float* mag);
 double oracle_area_under_curve(float x1, float x2, double mean, double std_);
+/* MeanShift::shift (MeanShift.hpp:41-135) of one vote list (x, y pairs, weights): the mode before cvRound. */
+void oracle_meanshift(const int32_t* xy, const float* w, int32_t n, int32_t kernel, int32_t iters, float stop,
+                      float* mean_xy);
 double oracle_exp(double x);
 float oracle_expf(float x);
 

@@ -1,4 +1,6 @@
+import gzip
 import os
+import shutil
 import sys
 
 import numpy as np
@@ -67,3 +69,24 @@ def reference_root():
 def crops(n, seed=2012):
     from face_alignment_cvpr_2012_amd.synthetic import make_crops
     return make_crops(n, seed=seed)[0]
+
+
+@pytest.fixture(scope="session")
+def reference_tree(tmp_path_factory, model_path):
+    """data/trees_headpose + data/trees_ffd/forest_{0..4} archives, the two configs pointing at them, the cascade."""
+    from face_alignment_cvpr_2012_amd import archive
+    root = tmp_path_factory.mktemp("reference_data")
+    with archive.ModelArchive(model_path) as m:
+        m.save_all(str(root))
+    cfg = {}
+    for name, sub in (("config_headpose.txt", "data/trees_headpose"), ("config_ffd.txt", "data/trees_ffd")):
+        lines = open(os.path.join(os.path.join(REPO, "tests", "golden"), name)).read().split("\n")
+        lines[3] = str(root / sub)  # the "Path to trees" value (loadConfigFile's second pair)
+        cfg[name] = root / name
+        cfg[name].write_text("\n".join(lines))
+    xml = root / "haarcascade_frontalface_alt.xml"
+    with gzip.open(os.path.join(os.path.join(REPO, "tests", "golden"), "haarcascade_frontalface_alt.xml.gz")) as src, open(xml, "wb") as dst:
+        shutil.copyfileobj(src, dst)
+    cache = root / "cache"
+    cache.mkdir()
+    return {"root": root, "hp": cfg["config_headpose.txt"], "ffd": cfg["config_ffd.txt"], "xml": xml, "cache": cache}

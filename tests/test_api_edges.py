@@ -82,15 +82,67 @@ def test_very_tall_faces_match_oracle(engine, oracle_mod, fixtures):
         assert np.float32(f.headpose) == np.float32(ref["headpose"]), box
 
 
+def test_faces_beyond_int16_rows_match_oracle(engine, oracle_mod, fixtures):
+    """No face-height limit short of memory: a 125 x 10,416 face (past round 4's 4,096-row cap) and a 125 x 37,500
+    face whose vote positions leave int16 (FaceDesc::wide: VoteW lists, k_meanshift5), in one batch with an
+    ordinary face (the tall ones get chunks of their own), each equal to the oracle."""
+    img = np.ascontiguousarray(np.concatenate([fixtures["images"][0], fixtures["images"][1]], axis=0))
+    boxes = [(120, 0, 3, 250), (61, 72, 130, 130), (120, 0, 1, 300)]
+    faces = engine.analyzeFaces([img], boxes, [0] * len(boxes))
+    for f, box in zip(faces, boxes):
+        ref, _ = oracle_mod.analyze_face(img, box, threads=16)
+        assert f.status == 0, (box, f.status)
+        assert f.n_trees == ref["n_trees"], box
+        assert np.array_equal(f.ffd_cordinates, ref["points"]), box
+        assert np.float32(f.headpose) == np.float32(ref["headpose"]), box
+
+
+def test_wide_vote_path_equals_narrow(model_path, engine, fixtures):
+    """FFD_VOTES_WIDE=1 sends every face through the wide vote path (16-B VoteW lists, the k_meanshift5
+    companion launch): the 20 bundled faces, as a batch and one by one, equal the ordinary path's."""
+    boxes = [tuple(int(v) for v in b) for b in fixtures["boxes"]]
+    want = engine.analyzeFaces(list(fixtures["images"]), boxes)
+    os.environ["FFD_VOTES_WIDE"] = "1"
+    try:
+        wide = ffd.FaceForest(ffd.FaceForestOptions(model_path=model_path))
+    finally:
+        del os.environ["FFD_VOTES_WIDE"]
+    try:
+        got = wide.analyzeFaces(list(fixtures["images"]), boxes)
+        one = [wide.analyzeFace(img, b) for img, b in zip(fixtures["images"][:3], boxes[:3])]
+    finally:
+        wide.close()
+    for a, b in zip(got + one, want + want[:3]):
+        assert np.array_equal(a.ffd_cordinates, b.ffd_cordinates) and np.float32(a.headpose) == np.float32(b.headpose)
+
+
+def test_meanshift_votes_beyond_int16(engine, oracle_mod):
+    """ffd_meanshift (MeanShift::shift on one list) with positions far outside int16 (a wide list) and inside
+    it, equal to the oracle's restatement bit for bit; unchecked votes are skipped."""
+    rng = np.random.default_rng(5)
+    for centre, spread in (((40000, -70000), 30), ((120, 90), 12), ((5, 2_000_000), 8)):
+        n = 700
+        xy = np.stack([rng.normal(centre[0], spread, n), rng.normal(centre[1], spread, n)], 1).astype(np.int32)
+        w = rng.uniform(0.1, 1.0, n).astype(np.float32)
+        check = rng.uniform(size=n) < 0.9
+        got = ffd.meanshift(engine, [(int(x), int(y), float(ww), bool(c)) for (x, y), ww, c in zip(xy, w, check)])
+        want = oracle_mod.meanshift(xy[check], w[check])
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (centre, got, want)
+
+
 def test_rejected_boxes_get_truthful_status(engine, fixtures):
     img = fixtures["images"][0]
-    boxes = [(100, 5, 6, 240), (200, 200, 100, 100), (-1, 0, 50, 50), (61, 72, 130, 130), (10, 10, 200, 1)]
+    boxes = [(200, 200, 100, 100), (-1, 0, 50, 50), (61, 72, 130, 130), (10, 10, 200, 1)]
     faces = engine.analyzeFaces([img], boxes, [0] * len(boxes))
-    assert [f.status for f in faces] == [ffd.STATUS_UNSUPPORTED, ffd.STATUS_INVALID_ARGUMENT,
-                                        ffd.STATUS_INVALID_ARGUMENT, 0, ffd.STATUS_INVALID_ARGUMENT]
-    assert "unsupported" in ffd.status_string(faces[0].status)
-    good = engine.analyzeFace(img, boxes[3])
-    assert np.array_equal(faces[3].ffd_cordinates, good.ffd_cordinates)
+    assert [f.status for f in faces] == [ffd.STATUS_INVALID_ARGUMENT, ffd.STATUS_INVALID_ARGUMENT, 0,
+                                        ffd.STATUS_INVALID_ARGUMENT]
+    good = engine.analyzeFace(img, boxes[2])
+    assert np.array_equal(faces[2].ffd_cordinates, good.ffd_cordinates)
+    # a scaled face over MAX_FACE_ROWS (2^21 rows: > 50 GB of channel planes) is out of memory, not a crash
+    tall = np.zeros((17000, 2, 3), np.uint8)
+    f = engine.analyzeFaces([tall], [(0, 0, 1, 16800)], [0])[0]
+    assert f.status == ffd.STATUS_OUT_OF_MEMORY
+    assert "memory" in ffd.status_string(f.status)
 
 
 def test_group_on_one_device_equals_engine(model_path, engine, fixtures):

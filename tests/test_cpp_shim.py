@@ -182,3 +182,39 @@ def test_sample_eval_leaves_matches_oracle(model_path, fixtures, engine, oracle_
             xy = np.stack([rng.integers(0, w - 31 + 1, n), rng.integers(0, h - 31 + 1, n)], 1).astype(np.int32)
             want = oracle_mod.eval_patches(tr["channels"], xy, ffd.FOREST_HEADPOSE, list(range(15)))
             assert np.array_equal(s.eval_leaves(ffd.FOREST_HEADPOSE, xy, list(range(15))), want)
+
+
+@pytest.mark.gpu
+def test_tall_sample_float_integrals_match_oracle(fixtures, engine, oracle_mod):
+    """A sample whose integrals pass 2^24 (a 125 x 1500 face: 255 W H >= 2^24, where the reference's CV_32F
+    integrals round) keeps the rounded values and is walked with the float rectangle means: its channels read
+    back, the FFD grid, patch lists, the whole-sample and sub-region estimates, a sample made from those
+    channels and ffd_forest_eval_leaves on them all equal the oracle."""
+    import face_alignment_cvpr_2012_amd as ffd
+    img, box = fixtures["images"][0], (100, 5, 20, 240)
+    ref, tr = oracle_mod.analyze_face(img, box, threads=16, trace=True)
+    gray, ch = tr["face"], tr["channels"]
+    h, w = gray.shape
+    assert 255 * w * h >= 1 << 24 and ch.max() >= 1 << 24
+    rng = np.random.default_rng(9)
+    xy = np.stack([rng.integers(0, w - 31 + 1, 300), rng.integers(0, h - 31 + 1, 300)], 1).astype(np.int32)
+    want_hp = oracle_mod.eval_patches(ch, xy, ffd.FOREST_HEADPOSE, list(range(15)))
+    want_mp = oracle_mod.eval_patches(ch, xy[:12], ffd.FOREST_FFD, tr["trees"])
+    assert np.array_equal(ffd.Forest(engine, ffd.FOREST_HEADPOSE).evaluate(ch, xy, list(range(15))), want_hp)
+    for s in (ffd.ImageSample(engine, gray), ffd.ImageSample(engine, channels=ch)):
+        with s:
+            assert np.array_equal(s.channels(), ch)
+            nx, ny = len(range(0, w - 31, 3)), len(range(0, h - 31, 3))
+            got = s.eval_grid(ffd.FOREST_FFD, 0, 0, 3, nx, ny, tr["trees"])
+            assert np.array_equal(got, tr["mp_leaves"].reshape(nx * ny, -1))
+            assert np.array_equal(s.eval_leaves(ffd.FOREST_HEADPOSE, xy, list(range(15))), want_hp)
+            assert np.array_equal(s.eval_leaves(ffd.FOREST_FFD, xy[:12], tr["trees"]), want_mp)
+            hp, var = s.estimateHeadPose()
+            assert np.float32(hp) == np.float32(ref["headpose"])
+            assert np.array_equal(s.estimateFacialFeatures(None, tr["trees"]), np.rint(tr["ms_mean"]).astype(np.int32))
+            for region in ((3, 200, 110, 700), (0, 900, 125, 600)):
+                o = oracle_mod.estimate_headpose(ch, region)
+                g = s.estimateHeadPose(region)
+                assert np.float32(g[0]) == np.float32(o[0]) and np.float32(g[1]) == np.float32(o[1]), region
+                assert np.array_equal(s.estimateFacialFeatures(region, tr["trees"]),
+                                      oracle_mod.estimate_facial_features(ch, region, tr["trees"])), region

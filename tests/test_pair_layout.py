@@ -1,8 +1,8 @@
-"""The traversal's sibling-block layout on the CPU (no device): tools/pair_layout_check.cpp re-encodes random
-breadth-first trees (one complete depth-18 tree, so block offsets pass 16 bits and take the far table) through
+"""The traversal's pair-record layout on the CPU (no device): tools/pair_layout_check.cpp re-encodes random
+breadth-first trees (one complete depth-18 tree, so child offsets pass 16 bits and take the far table) through
 libffd.so's own ffd_host::build_pair_records / build_tree_tops and walks them the way k_traverse does (heap-ordered
-LDS tops for the first levels, then the sibling blocks, each requested a step before its record is used), against
-breadth-first walks with the same node decisions; every requested block index must lie inside the array.  The GPU side of the same walks is the leaf parity of tests/test_gpu_parity.py."""
+LDS tops for the first levels, then the records with the layout's child rule), against breadth-first walks with
+the same node decisions.  The GPU side of the same walks is the leaf parity of tests/test_gpu_parity.py."""
 import os
 import subprocess
 

@@ -1,10 +1,9 @@
-// pair_layout_check.cpp — CPU check of the traversal's sibling-block layout (csrc/ffd_engine.cpp
-// ffd_host::build_pair_records / build_tree_tops, ffd_device.hpp "sibling blocks"): random breadth-first trees
-// (one complete tree deep enough that block offsets exceed 16 bits and take the far table) are re-encoded by
+// pair_layout_check.cpp — CPU check of the traversal's pair-record layouts (csrc/ffd_engine.cpp
+// ffd_host::build_pair_records / build_tree_tops, ffd_device.hpp "pair records"): random breadth-first trees
+// (one complete tree deep enough that child offsets exceed 16 bits and take the far table) are re-encoded by
 // the library, then walked the way k_traverse walks them (heap-ordered tops for the first LG levels, then the
-// sibling blocks, each requested one step before its record is used) and the breadth-first way, with the same
-// node decisions; every walk must reach the same leaf, and every block index the walk requests must lie inside
-// the array.  No device is used.
+// pair records with the layout's child rule) and the breadth-first way, with the same node decisions; every walk
+// must reach the same leaf.  No device is used.
 //
 // usage: pair_layout_check [TOP_LEVELS]
 // build: hipcc -O2 -std=c++17 -Iface_alignment_cvpr_2012_amd/csrc -Iinclude tools/pair_layout_check.cpp -Lface_alignment_cvpr_2012_amd/lib -lffd
@@ -20,8 +19,7 @@ namespace ffd_host {
 void build_pair_records(const std::vector<uint4>& bfs, const std::vector<int32_t>& roots, std::vector<uint4>& out,
                         std::vector<int32_t>& roots_out, std::vector<uint32_t>& far);
 void build_tree_tops(const std::vector<uint4>& pairs, const std::vector<int32_t>& proots,
-                     const std::vector<uint32_t>& far, const std::vector<uint4>& bfs, const std::vector<int32_t>& roots,
-                     std::vector<uint4>& tops, std::vector<uint32_t>& top_idx);
+                     const std::vector<uint32_t>& far, std::vector<uint4>& tops, std::vector<uint32_t>& top_idx);
 }  // namespace ffd_host
 
 static constexpr uint32_t LEAF_BIT = 0x80000000u;
@@ -90,7 +88,7 @@ int main(int argc, char** argv) {
   std::vector<int32_t> proots;
   std::vector<uint32_t> far, topi;
   ffd_host::build_pair_records(bfs, roots, pairs, proots, far);
-  ffd_host::build_tree_tops(pairs, proots, far, bfs, roots, tops, topi);
+  ffd_host::build_tree_tops(pairs, proots, far, tops, topi);
   const int topn = 1 << lg;
   long walks = 0, bad = 0, far_used = 0;
   for (size_t t = 0; t < roots.size(); t++) {
@@ -118,36 +116,24 @@ int main(int argc, char** argv) {
         lo = s ? R.y : R.x;
         hi = s ? R.w : R.z;
       }
-      if (lo < (63u << 26)) {
-        const uint32_t nblk = (uint32_t)(pairs.size() / 2);
-        const uint32_t* ti = &topi[t * TOP_CAP];
-        uint32_t bp = ti[h], sp = s;
-        uint32_t o = (R.z >> 24) | ((R.w >> 24) << 8);
-        if (s && o == 0u) { o = far[2u * ti[h >> 1] + (h > 1u ? (h & 1u) : 0u)]; far_used++; }
-        uint32_t bc = bp + (s ? o : 1u);
-        if (bp >= nblk) { bad++; continue; }
-        uint4 Pl = pairs[2u * bp], Ph = pairs[2u * bp + 1u];
-        do {
-          if (bc >= nblk) { bad++; break; }  // the kernel requests every computed block
-          const uint4 Nl = pairs[2u * bc], Nh = pairs[2u * bc + 1u];
-          const uint32_t sn = decide(lo, hi, wk);
-          const uint4 P = sp ? Ph : Pl;
-          uint32_t o1 = (P.z >> 24) | ((P.w >> 24) << 8);
-          if (sn && o1 == 0u) { o1 = far[2u * bp + sp]; far_used++; }
-          lo = sn ? P.y : P.x;
-          hi = sn ? P.w : P.z;
-          bp = bc;
-          bc += sn ? o1 : 1u;
-          sp = sn;
-          Pl = Nl;
-          Ph = Nh;
-        } while (lo < (63u << 26));
+      uint32_t P = topi[t * TOP_CAP + h];
+      while (lo < (63u << 26)) {
+        const uint32_t off1 = (R.z >> 24) | ((R.w >> 24) << 8);
+        uint32_t Q = P + (s ? off1 : 1u);
+        if (s && off1 == 0u) { Q = P + far[P]; far_used++; }
+        if (Q >= pairs.size()) { bad++; break; }
+        const uint4 N = pairs[Q];
+        s = decide(lo, hi, wk);
+        P = Q;
+        R = N;
+        lo = s ? R.y : R.x;
+        hi = s ? R.w : R.z;
       }
       const uint32_t got = (lo & 0xFFFFFu) | hi << 20;
       if (got != want) bad++;
     }
   }
-  std::printf("{\"top_levels\": %d, \"nodes\": %zu, \"pair_slots\": %zu, \"walks\": %ld, \"far_steps\": %ld, "
+  std::printf("{\"top_levels\": %d, \"nodes\": %zu, \"pairs\": %zu, \"walks\": %ld, \"far_steps\": %ld, "
               "\"mismatches\": %ld}\n", lg, bfs.size(), pairs.size(), walks, far_used, bad);
   return bad ? 1 : 0;
 }
