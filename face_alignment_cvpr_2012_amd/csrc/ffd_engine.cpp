@@ -551,16 +551,11 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
     HIP_CHECK(hipEventRecord(w.fork_ev[1 + i], w.fork[i]));
     HIP_CHECK(hipStreamWaitEvent(st, w.fork_ev[1 + i], 0));
   }
-  // block queues of the two traversals (8 per-XCD counters each) and the FFD pass's face order
-  w.trav_queue.ensure(16 * sizeof(uint32_t));
-  if (trav_sort) w.trav_order.ensure((size_t)n * sizeof(int32_t));
-  uint32_t* hp_queue = trav_queue ? w.trav_queue.as<uint32_t>() : nullptr;
-  uint32_t* mp_queue = trav_queue ? w.trav_queue.as<uint32_t>() + 8 : nullptr;
   stage(7, st, [&] {
     launch_traverse(true, dfd, n, blocks_per_face(fds, true, trav_g_hp), trav_g_hp, hp_pairs.as<uint4>(),
                     hp_tops.as<uint4>(), hp_topi.as<uint32_t>(), trav_top_max, hp_far.as<uint32_t>(), nullptr,
                     hp_trees, desc.hp_option.step_size, desc.hp_option.step_size, plane, w.chan.as<uint16_t>(),
-                    w.hpleaf.as<int32_t>(), trav_wg, TRAV_LDS_CAP, st, nullptr, hp_queue);
+                    w.hpleaf.as<int32_t>(), trav_wg, TRAV_LDS_CAP, st);
     if (any_fint)
       launch_walk_fint(true, dfd, n, hp_nodes.as<uint4>(), hp_roots.as<int32_t>(), hp_trees, nullptr,
                        desc.hp_option.step_size, desc.hp_option.step_size, w.chan.as<uint16_t>(), w.hpleaf.as<int32_t>(), st);
@@ -570,12 +565,10 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
                    w.state.as<HpState>(), d_out, st);
   });
   stage(9, st, [&] {
-    if (trav_sort) launch_trav_order(w.state.as<HpState>(), n, ntrees_per_forest, w.trav_order.as<int32_t>(), st);
     launch_traverse(false, dfd, n, blocks_per_face(fds, false, trav_g_mp), trav_g_mp, mp_pairs.as<uint4>(),
                     mp_tops.as<uint4>(), mp_topi.as<uint32_t>(), trav_top_max, mp_far.as<uint32_t>(),
                     w.state.as<HpState>(), 0, desc.mp_option.step_size, mp_step_y(), plane, w.chan.as<uint16_t>(),
-                    w.mpleaf.as<int32_t>(), trav_wg, TRAV_LDS_CAP, st, trav_sort ? w.trav_order.as<int32_t>() : nullptr,
-                    mp_queue);
+                    w.mpleaf.as<int32_t>(), trav_wg, TRAV_LDS_CAP, st);
     if (any_fint)
       launch_walk_fint(false, dfd, n, mp_nodes.as<uint4>(), mp_roots.as<int32_t>(), 0, w.state.as<HpState>(),
                        desc.mp_option.step_size, mp_step_y(), w.chan.as<uint16_t>(), w.mpleaf.as<int32_t>(), st);
@@ -859,8 +852,6 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   if (const char* v = std::getenv("FFD_TRAV_G_FFD")) shape(v, e->trav_g_mp);
   if (const char* v = std::getenv("FFD_TRAV_WG")) e->trav_wg = std::max(8, std::atoi(v));
   if (const char* v = std::getenv("FFD_TRAV_TOPMAX")) e->trav_top_max = std::max(1, std::min(TOP_CAP, std::atoi(v)));
-  if (const char* v = std::getenv("FFD_TRAV_QUEUE")) e->trav_queue = std::atoi(v) != 0;
-  if (const char* v = std::getenv("FFD_TRAV_SORT")) e->trav_sort = std::atoi(v) != 0;
   if (const char* v = std::getenv("FFD_VOTES_WIDE")) e->force_wide = std::atoi(v) != 0;
   if (const char* v = std::getenv("FFD_CHUNK_BYTES")) e->chunk_bytes = std::max<int64_t>(1, std::atoll(v));
   if (const char* v = std::getenv("FFD_GABOR_EXACT")) e->gabor_exact = std::atoi(v) != 0;
@@ -1492,6 +1483,8 @@ struct ffd_sample {
   int64_t plane = 0;  // (H + 1) * PITCH
   int fint = 0;       // float-rounded integrals (CV_32F past 2^24, FaceDesc::fint): walked by rect_mean_fint
   DevBuf chan;        // u16 [NCH][H + 1][PITCH], integrals mod 2^16
+  DevBuf desc;        // the grid traversal's one-face descriptor, kept for the steps it was made for
+  int desc_hp = -1, desc_mp = -1;
 };
 
 void ffd_engine::orphan_samples() {
@@ -1500,6 +1493,9 @@ void ffd_engine::orphan_samples() {
     if (s->chan.p) (void)hipFree(s->chan.p);
     s->chan.p = nullptr;
     s->chan.n = 0;
+    if (s->desc.p) (void)hipFree(s->desc.p);
+    s->desc.p = nullptr;
+    s->desc.n = 0;
     s->e = nullptr;
   }
   samples.clear();
@@ -1514,6 +1510,19 @@ FaceDesc sample_desc(ffd_sample* s, int hp_step, int mp_step_x, int mp_step_y) {
   f.plane = s->plane;
   f.fint = s->fint;
   return f;
+}
+
+// The sample's one-face descriptor for the grid traversal (head-pose step khp, FFD step kmp on both axes), kept on
+// the device with the sample and uploaded again only for other steps.
+const FaceDesc* grid_desc(ffd_engine* e, ffd_sample* s, int khp, int kmp, hipStream_t st) {
+  if (s->desc_hp != khp || s->desc_mp != kmp || !s->desc.p) {
+    const FaceDesc f = sample_desc(s, khp, kmp, kmp);
+    s->desc.ensure(sizeof(FaceDesc));
+    e->upload_pinned(s->desc.p, &f, sizeof(f), st);
+    s->desc_hp = khp;
+    s->desc_mp = kmp;
+  }
+  return s->desc.as<FaceDesc>();
 }
 
 ffd_status orphaned() {
@@ -1554,8 +1563,8 @@ ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, i
   bool all_hp_trees = hp && n_trees == e->hp_trees;
   for (int t = 0; all_hp_trees && t < n_trees; t++) all_hp_trees = tree_ids[t] == t;
   if (grid && x0 == 0 && y0 == 0 && (!hp || all_hp_trees) && step <= 32 && n_trees <= MAX_TREES && !s->fint) {
-    const FaceDesc f = sample_desc(s, hp ? step : e->desc.hp_option.step_size, hp ? e->desc.mp_option.step_size : step,
-                                   hp ? e->mp_step_y() : step);
+    const int khp = hp ? step : e->desc.hp_option.step_size, kmp = hp ? e->desc.mp_option.step_size : step;
+    const FaceDesc f = sample_desc(s, khp, kmp, kmp);
     const int gx = hp ? f.nhx : f.nmx, gy = hp ? f.nhy : f.nmy;
     if (nx <= gx && ny <= gy) {
       e->sync_all();
@@ -1569,25 +1578,14 @@ ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, i
       const size_t all = (size_t)gx * gy * n_trees * 4;
       int32_t* pin = static_cast<int32_t*>(e->pin_leaf.ensure(all));
       int32_t* leaf_dev = pin;
-      // the descriptor and the tree list in one upload
-      struct {
-        FaceDesc f;
-        HpState hs;
-      } one;
-      std::memset(&one, 0, sizeof(one));
-      one.f = f;
-      one.hs.n_trees = n_trees;
-      for (int t = 0; t < n_trees; t++) one.hs.trees[t] = tree_ids[t];
-      e->sample_args.ensure(sizeof(one));
-      e->upload_pinned(e->sample_args.p, &one, sizeof(one), w.stream);
-      const FaceDesc* d_f = e->sample_args.as<FaceDesc>();
-      const HpState* d_hs = reinterpret_cast<const HpState*>(e->sample_args.as<uint8_t>() + offsetof(decltype(one), hs));
-      launch_traverse(hp, d_f, 1, blocks_per_face(fv, hp, g), g,
+      // the descriptor stays with the sample (made with it for the default steps); the tree list goes in the
+      // kernel arguments: the call is one launch and one synchronisation
+      launch_traverse(hp, grid_desc(e, s, khp, kmp, w.stream), 1, blocks_per_face(fv, hp, g), g,
                       hp ? e->hp_pairs.as<uint4>() : e->mp_pairs.as<uint4>(), hp ? e->hp_tops.as<uint4>() : e->mp_tops.as<uint4>(),
                       hp ? e->hp_topi.as<uint32_t>() : e->mp_topi.as<uint32_t>(), e->trav_top_max,
-                      hp ? e->hp_far.as<uint32_t>() : e->mp_far.as<uint32_t>(), hp ? nullptr : d_hs,
+                      hp ? e->hp_far.as<uint32_t>() : e->mp_far.as<uint32_t>(), nullptr,
                       hp ? e->hp_trees : 0, step, step, f.plane, s->chan.as<uint16_t>(), leaf_dev, e->trav_wg,
-                      TRAV_LDS_CAP, w.stream);
+                      TRAV_LDS_CAP, w.stream, tree_ids, n_trees);
       HIP_CHECK(hipGetLastError());
       HIP_CHECK(hipStreamSynchronize(w.stream));
       for (int i = 0; i < nx; i++)  // rows of the sub-grid: patch (i, j) of the full grid is i * gy + j
@@ -1692,6 +1690,7 @@ ffd_status ffd_sample_create(ffd_engine* e, const uint8_t* gray, int32_t W, int3
       HIP_CHECK(hipEventRecord(w.fork_ev[1 + i], w.fork[i]));
       HIP_CHECK(hipStreamWaitEvent(w.stream, w.fork_ev[1 + i], 0));
     }
+    grid_desc(e, s.get(), e->desc.hp_option.step_size, e->desc.mp_option.step_size, w.stream);
     HIP_CHECK(hipStreamSynchronize(w.stream));  // bgr is released on return
     w.count = 0;
     w.pending = false;
@@ -1727,6 +1726,7 @@ ffd_status ffd_sample_create_from_channels(ffd_engine* e, const uint32_t* channe
     s->fint = vmax >= (1u << 24) ? 1 : 0;  // float-rounded integrals (CV_32F past 2^24)
     s->chan.ensure(J.size() * 2 + 512);
     HIP_CHECK(hipMemcpyAsync(s->chan.p, J.data(), J.size() * 2, hipMemcpyHostToDevice, e->main_stream()));
+    grid_desc(e, s.get(), e->desc.hp_option.step_size, e->desc.mp_option.step_size, e->main_stream());
     HIP_CHECK(hipStreamSynchronize(e->main_stream()));
     *out = s.release();
     e->track_sample(*out);

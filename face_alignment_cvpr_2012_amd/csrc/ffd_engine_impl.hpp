@@ -107,8 +107,6 @@ struct Workspace {
   DevBuf gabor_redo;  // per scale and face: the fast Gabor instance flags faces for the exact one
   DevBuf ms_order;    // MeanShift chains sorted by list length (k_ms_order)
   DevBuf gabor_mm;    // per face and scale: the banded Gabor instances' 16-word slots (zero between launches)
-  DevBuf trav_queue;  // the traversals' per-XCD block counters (head pose 0..7, FFD 8..15)
-  DevBuf trav_order;  // the FFD pass's face order (k_trav_order)
   std::vector<FaceDesc> h_fds;  // host staging, reused only after `done`
   std::vector<FaceDesc> desc;   // descriptors of the chunk last run here (ffd_get_trace)
   int first = 0, count = 0;
@@ -149,8 +147,6 @@ struct ffd_engine {
   // Overridable with FFD_TRAV_G_{HP,FFD} / FFD_TRAV_WG / FFD_CHUNK / FFD_STREAMS.
   TravShape trav_g_hp{5, 4}, trav_g_mp{5, 5};
   int trav_wg = 256;
-  bool trav_queue = true;  // per-XCD block queues in the batch traversals (FFD_TRAV_QUEUE=0: static dealing)
-  bool trav_sort = true;   // the FFD pass walks its faces grouped by tree set (FFD_TRAV_SORT=0: batch order)
 
   // model parameters
   int face_size = 125, patch = 31, hp_trees = 0, n_forests = 0, ntrees_per_forest = 0;
@@ -215,7 +211,6 @@ struct ffd_engine {
     ~Pinned() { if (p) (void)hipHostFree(p); }
   } pin_leaf, pin_patch;
   DevBuf sample_patches;
-  DevBuf sample_args;  // a sample's grid evaluation: its descriptor and tree list (one upload)
   int last_ws = -1;
   // live image samples (ffd_sample_*): a sample destroyed after its engine must not touch the engine, so the
   // engine frees the samples' device planes when it goes and marks them orphaned (ffd_engine_destroy)

@@ -1043,8 +1043,8 @@ struct TravArgs {
   int lds_bytes;           // dynamic LDS of the workgroup
   const uint16_t* chan;
   int32_t* leaf_out;
-  const int32_t* order;    // the faces in walking order (FFD pass: grouped by tree set, k_trav_order), or nullptr
-  uint32_t* queue;         // per XCD: blocks handed out so far (zeroed before the launch), or nullptr: static dealing
+  int n_inl;               // FFD pass with hp_state == nullptr (one image sample): its tree list, by value
+  int32_t inl_trees[MAX_TREES];
 };
 
 template <bool HP, int GX, int GY, int CB>
@@ -1084,7 +1084,6 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     B.more = lb < end;
     B.f = B.more ? lb / A.bpf : 0;
     const int b = lb - B.f * A.bpf;
-    if (B.more && A.order) B.f = A.order[B.f];
     const FaceDesc& fd = A.faces[B.f];
     B.nx = HP ? fd.nhx : fd.nmx;
     B.ny = HP ? fd.nhy : fd.nmy;
@@ -1096,7 +1095,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     B.T = 0;
     if (B.more && fd.valid && !fd.fint && B.nx > 0 && b < gbx * gby) {  // (float-integral faces: k_walk_fint)
       B.ok = 1;
-      B.T = HP ? A.ntrees_hp : A.hp_state[B.f].n_trees;
+      B.T = HP ? A.ntrees_hp : A.hp_state ? A.hp_state[B.f].n_trees : A.n_inl;
     }
     const int64_t off = HP ? fd.hp_off : fd.mp_off;
     B.out_lo = (int)(uint32_t)off;
@@ -1166,21 +1165,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
 
   // Stager waves and walker waves run separate loops with the same barrier sequence per block
   // (waves are wholly one role), so the staging registers are live only in the stager loop and
-  // the walkers get the rest of the register file.
-  // Block sequence of this workgroup: with a queue, the next unclaimed block of the XCD's range (an XCD's 32
-  // workgroups then stay on the same one or two faces, whose planes and tree records share its L2, and the
-  // faster workgroups take more blocks); else start + k, + nk, ...  Thread NW claims block i + 2 while the window
-  // holds block i and leaves it in LDS slot i & 1 (read after the next window barrier).
-  int* q_slot = reinterpret_cast<int*>(smem + A.lds_bytes - TRAV_BLK_BYTES + 48);
-  int seq = 0;
-  auto claim = [&]() {
-    return A.queue ? start + (int)atomicAdd(&A.queue[xcd], 1u) : start + k + nk * seq++;
-  };
-  if (tid == NW) {
-    q_slot[0] = claim();
-    q_slot[1] = claim();
-  }
-  __syncthreads();
+  // the walkers get the rest of the register file.  Blocks of this workgroup: start + k, + nk, ...
   if (tid >= NW) {
     // Staging: chunk i = (channel c, window row r, 8-column group q), i = (c * WH + r) * nq + q, goes
     // to LDS chunk i; staging thread s owns chunks s + u * NS.  Their face-relative source byte
@@ -1242,7 +1227,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         for (int u = 0; u < TU; u++) {
           const int e = tid - NW + u * NS;
           if (e < B.T * topn) {
-            const int j = e >> lg, tree = HP ? j : A.hp_state[B.f].trees[j];
+            const int j = e >> lg, tree = HP ? j : A.hp_state ? A.hp_state[B.f].trees[j] : A.inl_trees[j];
             const int g = tree * TOP_CAP + (e & (topn - 1));
             top_nd[u] = reinterpret_cast<const rec_t*>(A.tops)[g];
             top_p[u] = A.top_idx[g];
@@ -1295,15 +1280,16 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       }
     };
 
-    Blk cur = block(q_slot[0]);
+    int lb = start + k;
+    Blk cur = block(lb);
     prefetch(cur);
-    for (int it = 0;; it++) {
+    for (;;) {
       __syncthreads();  // the previous block's walks are done with the window
       commit(cur);
       __syncthreads();  // the window holds block `cur` (or the end marker)
       if (!cur.more) break;
-      const Blk nxt = block(q_slot[(it + 1) & 1]);
-      if (tid == NW) q_slot[it & 1] = claim();  // block it + 2 (slot it & 1 was read before this window)
+      lb += nk;
+      const Blk nxt = block(lb);
       prefetch(nxt);
       cur = nxt;
     }
@@ -2543,58 +2529,21 @@ bool traverse_shape_supported(TravShape g, bool hp) {
   return false;
 }
 
-// The FFD pass's face order (k_traverse's TravArgs::order): faces grouped by the forest that contributes most of
-// their selected trees and, within it, by how many of its trees they take (FaceForest.cpp:239-250 takes the first
-// floor(area * 20) trees of each pose forest), so the faces an XCD walks at the same time share most of their tree
-// records in its L2.  One workgroup, a counting sort.
-constexpr int TRAV_ORDER_KEYS = 5 * (MAX_TREES + 1);
-__global__ __launch_bounds__(1024) void k_trav_order(const HpState* __restrict__ state, int n_faces, int ntrees_per_forest,
-                                                     int32_t* __restrict__ order) {
-  __shared__ int hist[TRAV_ORDER_KEYS + 1];
-  const int tid = threadIdx.x;
-  auto key = [&](int f) {
-    const HpState& st = state[f];
-    int cnt[5] = {0, 0, 0, 0, 0};
-    for (int j = 0; j < st.n_trees && j < MAX_TREES; j++) {
-      const int fo = st.trees[j] / ntrees_per_forest;
-      if (fo >= 0 && fo < 5) cnt[fo]++;
-    }
-    int d = 0;
-    for (int i = 1; i < 5; i++) d = cnt[i] > cnt[d] ? i : d;
-    return d * (MAX_TREES + 1) + (MAX_TREES - min(cnt[d], MAX_TREES));
-  };
-  for (int i = tid; i <= TRAV_ORDER_KEYS; i += 1024) hist[i] = 0;
-  __syncthreads();
-  for (int f = tid; f < n_faces; f += 1024) atomicAdd(&hist[key(f)], 1);
-  __syncthreads();
-  if (tid == 0) {  // exclusive prefix over the few keys
-    int run = 0;
-    for (int i = 0; i <= TRAV_ORDER_KEYS; i++) {
-      const int v = hist[i];
-      hist[i] = run;
-      run += v;
-    }
-  }
-  __syncthreads();
-  // (the order within a key is the atomics'; it changes no result: every face's leaves go to its own slots)
-  for (int f = tid; f < n_faces; f += 1024) order[atomicAdd(&hist[key(f)], 1)] = f;
-}
-
-void launch_trav_order(const HpState* state, int n, int ntrees_per_forest, int32_t* order, hipStream_t s) {
-  if (n > 0) k_trav_order<<<1, 1024, 0, s>>>(state, n, ntrees_per_forest, order);
-}
 
 void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, TravShape g, const uint4* pairs, const uint4* tops,
                      const uint32_t* top_idx, int top_max, const uint32_t* far, const HpState* state, int ntrees_hp,
                      int step, int step_y, int64_t plane, const uint16_t* chan, int32_t* leaf_out, int n_wg,
-                     int lds_cap, hipStream_t s, const int32_t* order, uint32_t* queue) {
+                     int lds_cap, hipStream_t s, const int32_t* inl_trees, int n_inl) {
   const int total_blocks = n * bpf;
   if (total_blocks <= 0) return;
   // the window, then as many tree-top entries as the rest of the CU's LDS holds
   const int WW = 32 + step * (g.gx - 1), WH = 32 + step_y * (g.gy - 1), lds = lds_cap;
-  if (queue) (void)hipMemsetAsync(queue, 0, 8 * sizeof(uint32_t), s);
   TravArgs A{faces, n, bpf, pairs, tops, top_idx, lds - trav_window_bytes(WW, WH, g.gx * step) - TRAV_BLK_BYTES, top_max,
-             far, state, ntrees_hp, step, step_y, (int)plane, lds, chan, leaf_out, order, queue};
+             far, state, ntrees_hp, step, step_y, (int)plane, lds, chan, leaf_out, 0, {}};
+  if (!hp && !state) {
+    A.n_inl = std::min(std::max(n_inl, 0), MAX_TREES);
+    for (int t = 0; t < A.n_inl; t++) A.inl_trees[t] = inl_trees[t];
+  }
   // one persistent workgroup per CU, but no more than the blocks need (a one-face call has ~50 blocks)
   const int grid = std::max(8, std::min(n_wg & ~7, (total_blocks + 7) & ~7));
   const bool c16 = trav_chunk_bytes(WW, g.gx * step) == 16;

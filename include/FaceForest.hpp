@@ -543,30 +543,30 @@ class ImageSample {
               bool useIntegral = true, ffd_engine* engine = nullptr)
       : st_(std::make_shared<State>()) {
     (void)useIntegral;
-    st_->engine = engine ? engine : detail::current_engine();
     std::vector<int> f(features);
     std::sort(f.begin(), f.end());
     if (f != std::vector<int>({0, 1, 2}))
       throw std::invalid_argument("ImageSample: only features {0,1,2} are supported (the pretrained forests' channels)");
-    if (!st_->engine) throw std::runtime_error("ImageSample: no FaceForest engine");
-    std::string err;
-    if (detail::engine_call(st_->engine, err, [&] { return ffd_sample_create(st_->engine, gray, cols, rows, (int32_t)step, &st_->h); }) != FFD_OK)
-      throw std::runtime_error("ImageSample: " + err);
     st_->w = cols;
     st_->hgt = rows;
     st_->id = detail::next_sample_id();
     st_->gray.resize((size_t)cols * rows);  // (the training images of Tree<MPSample>(samples, ...))
     for (int y = 0; y < rows; y++) std::memcpy(&st_->gray[(size_t)y * cols], gray + (size_t)y * step, (size_t)cols);
+    // the channels on the device now, as the reference's constructor computes them; without an engine (a training
+    // program that builds ImageSamples before any FaceForest, demo.cpp:86-96) on first use, with the engine current then
+    st_->engine = engine ? engine : detail::current_engine();
+    if (st_->engine) st_->create();
   }
   // the 8-bit gray image the channels were extracted from (rows x cols, row pitch cols)
   const std::vector<uint8_t>& gray() const { return st_->gray; }
   int width() const { return st_->w; }
   int height() const { return st_->hgt; }
-  ffd_engine* engine() const { return st_->engine; }
-  ffd_sample* handle() const { return st_->h; }
+  ffd_engine* engine() const { return ensure()->engine; }
+  ffd_sample* handle() const { return ensure()->h; }
   uint64_t id() const { return st_->id; }
   // the channels as 38 u32 integral planes [38][rows+1][cols+1] (downloaded on first use)
   const uint32_t* channels() const {
+    ensure();
     std::lock_guard<std::mutex> g(st_->mu);
     if (st_->ch.empty()) {
       st_->ch.resize((size_t)38 * (st_->hgt + 1) * (st_->w + 1));
@@ -588,6 +588,11 @@ class ImageSample {
     std::mutex mu;
     std::vector<uint32_t> ch;
     std::vector<uint8_t> gray;
+    void create() {
+      std::string err;
+      if (detail::engine_call(engine, err, [&] { return ffd_sample_create(engine, gray.data(), w, hgt, (int32_t)w, &h); }) != FFD_OK)
+        throw std::runtime_error("ImageSample: " + err);
+    }
     ~State() {
       if (!h) return;
       std::lock_guard<std::mutex> g(detail::engine_mutex(engine));
@@ -595,6 +600,15 @@ class ImageSample {
     }
   };
   std::shared_ptr<State> st_;  // copies share the device sample (the reference copies cv::Mat headers)
+  State* ensure() const {
+    std::lock_guard<std::mutex> g(st_->mu);
+    if (!st_->h) {
+      if (!st_->engine) st_->engine = detail::current_engine();
+      if (!st_->engine) throw std::runtime_error("ImageSample: no FaceForest engine");
+      st_->create();
+    }
+    return st_.get();
+  }
 };
 
 // Leaf payloads (HeadPoseSample.hpp:144-162, MPSample.hpp:137-159), same member names, so the
@@ -736,8 +750,8 @@ template <class S> class Forest {
   int numberOfTrees() const { return (int)list_->ids.size(); }
   const std::vector<int32_t>& treeIds() const { return list_->ids; }
   ffd_engine* engine() const { return engine_; }
-  void setParam(ForestParam fp) { param_ = fp; }
-  ForestParam getParam() const { return param_; }
+  void setParam(ForestParam fp) { param_ = std::make_shared<const ForestParam>(std::move(fp)); }
+  ForestParam getParam() const { return param_ ? *param_ : ForestParam(); }
   // Forest::addTree / getTree / cleanForest (Forest.hpp:41-68), as FaceForest::analyzeFace composes the
   // per-face forest from the jungle (FaceForest.cpp:239-250)
   void addTree(Tree<S>* tree) {
@@ -789,8 +803,8 @@ template <class S> class Forest {
     std::lock_guard<std::mutex> g(cache_->mu);
     const size_t row = grid_row(sample);
     if (row != npos) {
-      Leaf* const* lp = &cache_->grid_leaf[row];
-      for (size_t t = 0; t < T; t++) leafs[t] = lp[t];
+      const int32_t* id = &cache_->grid_ids[row];
+      for (size_t t = 0; t < T; t++) leafs[t] = cache_->leaves[id[t]].get();
       return;
     }
     std::vector<int32_t> ids(T);
@@ -823,8 +837,7 @@ template <class S> class Forest {
     uint64_t sample = 0;
     std::vector<int32_t> ids;
     int x0 = 0, y0 = 0, step = 0, nx = 0, ny = 0;
-    std::vector<int32_t> grid_ids;  // [(i * ny + j) * T + t]
-    std::vector<Leaf*> grid_leaf;   // the payloads of grid_ids
+    std::vector<int32_t> grid_ids;  // [(i * ny + j) * T + t]; leaves[] holds the payload of each
   };
   // the tree list, shared by copies until one of them changes it (a copy per evaluateMT call, as the reference
   // binds the forest by value into every task, then costs a reference count, not a list copy)
@@ -833,7 +846,7 @@ template <class S> class Forest {
     std::deque<Tree<S>> trees;
   };
   ffd_engine* engine_ = nullptr;
-  ForestParam param_;
+  std::shared_ptr<const ForestParam> param_;  // (shared by copies: a per-call copy allocates nothing)
   std::shared_ptr<TreeList> list_;
   int grid_step_ = 0;
   std::shared_ptr<Cache> cache_;
@@ -886,26 +899,23 @@ template <class S> class Forest {
         return ffd_sample_eval_grid(im.handle(), ForestKind<S>::value, c.x0, c.y0, step, c.nx, c.ny, ids.data(), T,
                                     c.grid_ids.data());
       });
-      // the payloads of every leaf reached, fetched once per forest cache
-      int32_t top = -1;
-      for (int32_t v : c.grid_ids) top = std::max(top, v);
-      if ((size_t)(top + 1) > c.leaves.size()) c.leaves.resize((size_t)top + 1);
+      // the payloads of every leaf reached, fetched once per forest cache (one pass over the grid)
       std::vector<int32_t> uniq;
+      const size_t have = c.leaves.size();
       for (int32_t v : c.grid_ids)
-        if (!c.leaves[v]) uniq.push_back(v);
+        if ((size_t)v >= have || !c.leaves[v]) uniq.push_back(v);
       if (!uniq.empty()) {
         std::sort(uniq.begin(), uniq.end());
         uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
         std::vector<typename ForestKind<S>::Raw> raw(uniq.size());
         call(engine_, [&] { return ffd_forest_leaves(engine_, ForestKind<S>::value, uniq.data(), (int32_t)uniq.size(), raw.data()); });
+        if ((size_t)uniq.back() >= have) c.leaves.resize((size_t)uniq.back() + 1);
         for (size_t i = 0; i < uniq.size(); i++) {
           std::unique_ptr<Leaf> l(new Leaf());
           ForestKind<S>::fill(raw[i], *l);
           c.leaves[uniq[i]] = std::move(l);
         }
       }
-      c.grid_leaf.resize(c.grid_ids.size());
-      for (size_t i = 0; i < c.grid_ids.size(); i++) c.grid_leaf[i] = c.leaves[c.grid_ids[i]].get();
       c.sample = im.id();
     }
     const int dx = x - c.x0, dy = y - c.y0;

@@ -105,17 +105,36 @@ static int eval_main(const char* hp_cfg, const char* ffd_cfg, const char* face_c
 static int analyze_main(const char* hp_cfg, const char* ffd_cfg, const char* cascade, const char* image) {
   FaceForestOptions ff_options;
   if (!options_from(hp_cfg, ffd_cfg, cascade, ff_options)) return EXIT_FAILURE;
-  FaceForest ff(ff_options);
-  if (!ff.is_initialized()) return 3;
-  cv::Mat img = loadImage(image, std::string(image).substr(std::string(image).rfind('/') + 1));
-  if (img.empty()) return 4;
-  std::vector<Face> faces;
-  ff.analyzeImage(img, faces);
-  for (const Face& f : faces) {
-    std::printf("face %d %d %d %d %.9g", f.bbox.x, f.bbox.y, f.bbox.width, f.bbox.height, f.headpose);
-    for (const cv::Point& p : f.ffd_cordinates) std::printf(" %d %d", p.x, p.y);
-    std::printf("\n");
+  std::unique_ptr<ImageSample> kept;  // made under the FaceForest below and kept past its end
+  {
+    FaceForest ff(ff_options);
+    if (!ff.is_initialized()) return 3;
+    cv::Mat img = loadImage(image, std::string(image).substr(std::string(image).rfind('/') + 1));
+    if (img.empty()) return 4;
+    std::vector<Face> faces;
+    ff.analyzeImage(img, faces);
+    for (const Face& f : faces) {
+      std::printf("face %d %d %d %d %.9g", f.bbox.x, f.bbox.y, f.bbox.width, f.bbox.height, f.headpose);
+      for (const cv::Point& p : f.ffd_cordinates) std::printf(" %d %d", p.x, p.y);
+      std::printf("\n");
+    }
+    cv::Mat gray(64, 64, CV_8UC1);
+    for (int y = 0; y < 64; y++)
+      for (int x = 0; x < 64; x++) gray.data[(size_t)y * gray.step + x] = img.data[(size_t)y * img.step + 3 * x];
+    kept.reset(new ImageSample(gray, std::vector<int>{0, 1, 2}, true));
+    (void)kept->channels();
   }
+  // the engine is gone: it freed the sample's planes, the sample's calls fail, its destructor frees host state only
+  int threw = 0;
+  try {
+    ImageSample copy = *kept;
+    std::vector<uint32_t> ch(38 * 65 * 65);
+    if (ffd_sample_channels(copy.handle(), ch.data()) != FFD_OK) threw = 1;
+  } catch (const std::exception&) {
+    threw = 1;
+  }
+  kept.reset();
+  std::printf("orphaned_sample_fails %d\n", threw);
   return EXIT_SUCCESS;
 }
 

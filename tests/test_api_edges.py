@@ -216,3 +216,28 @@ def test_mag_sqrt_exhaustive(engine):
     checked, bad = engine.check_mag_sqrt()
     assert checked == 1 + (0x7F800000 - 0x0F800000)
     assert bad == 0
+
+
+def test_engine_closed_before_its_sample(model_path, fixtures):
+    """a FaceForest closed (or its with-block left) while an ImageSample made from it lives.  The engine
+    frees the sample's planes and marks it orphaned (ffd_engine_destroy); the sample's calls then fail cleanly
+    and its close / garbage collection only releases host state."""
+    img, box = fixtures["images"][3], tuple(int(v) for v in fixtures["boxes"][3])
+    gray = np.ascontiguousarray(img[box[1]:box[1] + 100, box[0]:box[0] + 100, 1])  # any 8-bit face
+    ff = ffd.FaceForest(ffd.FaceForestOptions(model_path=model_path))
+    s = ffd.ImageSample(ff, gray)
+    hp = s.estimateHeadPose()
+    ff.close()
+    with pytest.raises(ffd.FFDError, match="destroyed"):
+        s.estimateHeadPose()
+    with pytest.raises(ffd.FFDError):
+        s.channels()
+    with pytest.raises(ffd.FFDError):
+        s.eval_leaves(ffd.FOREST_HEADPOSE, [(0, 0)], [0])
+    s.close()
+    with ffd.FaceForest(ffd.FaceForestOptions(model_path=model_path)) as ff2:
+        s2 = ffd.ImageSample(ff2, gray)
+        assert np.float32(s2.estimateHeadPose()[0]) == np.float32(hp[0])
+    with pytest.raises(ffd.FFDError):
+        s2.estimateFacialFeatures(None, list(range(20)))
+    del s2  # (garbage collected after its engine: host state only)

@@ -170,6 +170,7 @@ def test_demo_analyze_image(exe, reference_tree, image_dir, tmp_path, fixtures, 
         r = _run(exe, "analyze", hp, ffd, reference_tree["xml"], image_dir / str(fixtures["names"][k]), env=env)
         assert r.returncode == 0, r.stderr
         faces = engine.analyzeImage(fixtures["images"][k])
+        assert "orphaned_sample_fails 1" in r.stdout  # an ImageSample outliving its FaceForest
         lines = [line.split()[1:] for line in r.stdout.splitlines() if line.startswith("face")]
         assert len(lines) == len(faces) >= 1
         for v, f in zip(lines, faces):
