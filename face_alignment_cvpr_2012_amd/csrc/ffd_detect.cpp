@@ -288,7 +288,7 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
     std::vector<char> over(nF, 0);  // frames whose raw candidates exceed cap: boxes from a run of their own
     for (int k = 0; k < nF; k++) {
       if (counts[k] > cap) {
-        if (counts[k] > HAAR_GROUP_MAX)  // (the pair tests grow as N^2: ~1 s per round at 2^20 over the chip)
+        if (counts[k] > HAAR_GROUP_MAX)  // (the pair tests grow as N^2, ffd_haar.hpp)
           return fail(e, FFD_ERR_UNSUPPORTED, "frame " + std::to_string(g0 + k) + ": " + std::to_string(counts[k]) +
                                                   " raw detections (more than " + std::to_string(HAAR_GROUP_MAX) + ")");
         over[k] = 1;

@@ -779,7 +779,7 @@ const char* ffd_status_string(int32_t s) {
     case FFD_ERR_OUT_OF_MEMORY: return "out of memory (or a scaled face over 2^21 rows)";
     case FFD_ERR_NOT_INITIALIZED: return "not initialised";
     case FFD_ERR_INTERNAL: return "internal error";
-    case FFD_ERR_UNSUPPORTED: return "unsupported input (an image sample over 125 columns, or a detection frame over 2^20 raw candidates)";
+    case FFD_ERR_UNSUPPORTED: return "unsupported input (an image sample over 125 columns, or a detection frame over 2^18 raw candidates)";
     default: return "unknown status";
   }
 }
@@ -1578,14 +1578,28 @@ ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, i
       const size_t all = (size_t)gx * gy * n_trees * 4;
       int32_t* pin = static_cast<int32_t*>(e->pin_leaf.ensure(all));
       int32_t* leaf_dev = pin;
-      // the descriptor stays with the sample (made with it for the default steps); the tree list goes in the
-      // kernel arguments: the call is one launch and one synchronisation
+      // the descriptor stays with the sample (made with it for the default steps) and the tree list with the
+      // engine (uploaded when it changes: one forest's calls over many samples upload it once), so the call is
+      // one launch and one synchronisation
+      const HpState* d_hs = nullptr;
+      if (!hp) {
+        HpState hs;
+        std::memset(&hs, 0, sizeof(hs));
+        hs.n_trees = n_trees;
+        for (int t = 0; t < n_trees; t++) hs.trees[t] = tree_ids[t];
+        if (!e->sample_hs.p || std::memcmp(&hs, &e->sample_hs_host, sizeof(hs)) != 0) {
+          e->sample_hs.ensure(sizeof(HpState));
+          e->upload_pinned(e->sample_hs.p, &hs, sizeof(hs), w.stream);
+          e->sample_hs_host = hs;
+        }
+        d_hs = e->sample_hs.as<HpState>();
+      }
       launch_traverse(hp, grid_desc(e, s, khp, kmp, w.stream), 1, blocks_per_face(fv, hp, g), g,
                       hp ? e->hp_pairs.as<uint4>() : e->mp_pairs.as<uint4>(), hp ? e->hp_tops.as<uint4>() : e->mp_tops.as<uint4>(),
                       hp ? e->hp_topi.as<uint32_t>() : e->mp_topi.as<uint32_t>(), e->trav_top_max,
-                      hp ? e->hp_far.as<uint32_t>() : e->mp_far.as<uint32_t>(), nullptr,
+                      hp ? e->hp_far.as<uint32_t>() : e->mp_far.as<uint32_t>(), d_hs,
                       hp ? e->hp_trees : 0, step, step, f.plane, s->chan.as<uint16_t>(), leaf_dev, e->trav_wg,
-                      TRAV_LDS_CAP, w.stream, tree_ids, n_trees);
+                      TRAV_LDS_CAP, w.stream);
       HIP_CHECK(hipGetLastError());
       HIP_CHECK(hipStreamSynchronize(w.stream));
       for (int i = 0; i < nx; i++)  // rows of the sub-grid: patch (i, j) of the full grid is i * gy + j

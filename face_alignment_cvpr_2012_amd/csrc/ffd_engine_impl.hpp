@@ -133,6 +133,8 @@ struct ffd_engine {
   int device = 0;
   ffd_engine_desc desc{};
   int max_chunk = 4096;
+  DevBuf sample_hs;          // the FFD tree list of the last image-sample grid evaluation (ffd_sample_eval_grid)
+  HpState sample_hs_host{};  // ... and its host copy (uploaded again only when a call's list differs)
   int64_t chunk_bytes = (int64_t)40 << 30;  // a chunk's face buffers at most (FFD_CHUNK_BYTES; C2's 4,096 faces: ~26 GB)
   bool detector_only = false;  // ffd_detector_create: a Haar cascade and no forests
   int n_streams = 1;

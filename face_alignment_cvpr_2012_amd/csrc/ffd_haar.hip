@@ -198,7 +198,10 @@ __global__ __launch_bounds__(256) void k_haar_cols(const HaarLevel* __restrict__
 #define FFD_HAAR_GROUP_PASSES 1
 #endif
 #ifndef FFD_HAAR_BATCH2
-#define FFD_HAAR_BATCH2 4  // two-rectangle classifiers evaluated per step (their corner reads issued together)
+#define FFD_HAAR_BATCH2 2  // two-rectangle classifiers evaluated per step (their corner reads issued together)
+#endif
+#ifndef FFD_HAAR_BATCH3
+#define FFD_HAAR_BATCH3 2  // three-rectangle classifiers per step (2 / 2: 58 VGPRs, C3 detection 83.7 -> 81.3 ms; 4 / 4: 84)
 #endif
 #ifndef FFD_HAAR_THREADS
 #define FFD_HAAR_THREADS 256
@@ -348,7 +351,7 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
           return (double)ret * f;
         };
         auto run = [&](int i, int e, auto three) {
-          constexpr int NB = decltype(three)::value ? 4 : FFD_HAAR_BATCH2;
+          constexpr int NB = decltype(three)::value ? FFD_HAAR_BATCH3 : FFD_HAAR_BATCH2;
           for (; i + NB <= e; i += NB) {
             HaarWeak c[NB];
             double v[NB];

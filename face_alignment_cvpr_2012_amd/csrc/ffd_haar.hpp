@@ -11,7 +11,9 @@
 namespace ffd {
 
 constexpr int HAAR_MAX_CAND = 8192;  // raw candidates per frame the grouping kernel holds (LDS labels)
-constexpr int HAAR_GROUP_MAX = 1 << 20;  // raw candidates of one frame grouped at all (FFD_ERR_UNSUPPORTED beyond)
+// raw candidates of one frame grouped at all (FFD_ERR_UNSUPPORTED beyond): the min-label rounds' pair tests grow as
+// N^2; measured whole-frame detection 0.67 s at 167,103 (tools/r5_haar_bign.py), so ~1.6 s at this ceiling
+constexpr int HAAR_GROUP_MAX = 1 << 18;
 
 // One frame of a detection batch.
 struct HaarFrame {

@@ -1043,8 +1043,6 @@ struct TravArgs {
   int lds_bytes;           // dynamic LDS of the workgroup
   const uint16_t* chan;
   int32_t* leaf_out;
-  int n_inl;               // FFD pass with hp_state == nullptr (one image sample): its tree list, by value
-  int32_t inl_trees[MAX_TREES];
 };
 
 template <bool HP, int GX, int GY, int CB>
@@ -1095,7 +1093,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     B.T = 0;
     if (B.more && fd.valid && !fd.fint && B.nx > 0 && b < gbx * gby) {  // (float-integral faces: k_walk_fint)
       B.ok = 1;
-      B.T = HP ? A.ntrees_hp : A.hp_state ? A.hp_state[B.f].n_trees : A.n_inl;
+      B.T = HP ? A.ntrees_hp : A.hp_state[B.f].n_trees;
     }
     const int64_t off = HP ? fd.hp_off : fd.mp_off;
     B.out_lo = (int)(uint32_t)off;
@@ -1227,7 +1225,7 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         for (int u = 0; u < TU; u++) {
           const int e = tid - NW + u * NS;
           if (e < B.T * topn) {
-            const int j = e >> lg, tree = HP ? j : A.hp_state ? A.hp_state[B.f].trees[j] : A.inl_trees[j];
+            const int j = e >> lg, tree = HP ? j : A.hp_state[B.f].trees[j];
             const int g = tree * TOP_CAP + (e & (topn - 1));
             top_nd[u] = reinterpret_cast<const rec_t*>(A.tops)[g];
             top_p[u] = A.top_idx[g];
@@ -1952,6 +1950,12 @@ constexpr int MS_FPW = (MS_FACES + 3) / 4;  // faces per wave
 #define FFD_MS_RA 4
 #endif
 constexpr int MS_RA = FFD_MS_RA;  // serial phase: LDS reads in flight ahead of the adds
+#ifndef FFD_MS_SUM3
+#define FFD_MS_SUM3 1  // serial phase: lanes 3p, 3p + 1, 3p + 2 add face p's x / y / w terms (0: lane p adds all three)
+#endif
+// the x / y / w term planes: with SUM3 MS_LD words apart beyond the tile, so the three lanes of a face read
+// different banks (a plane is 64 x 21 words = 0 mod 64 banks)
+constexpr int MS_TSTRIDE = MS_TILE * MS_LD + (FFD_MS_SUM3 ? MS_LD : 0);
 #ifndef FFD_MS_DEFAULT
 #define FFD_MS_DEFAULT 0  // 0: chosen per batch (launch_meanshift); 1 k_meanshift, 4 k_meanshift4, 5 k_meanshift5
 #endif
@@ -2020,7 +2024,10 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                                                    const int32_t* __restrict__ vote_counts,
                                                    float* __restrict__ ms_mean, FaceOut* __restrict__ out,
                                                    const int32_t* __restrict__ order) {
-  __shared__ float tx[MS_TILE * MS_LD], ty[MS_TILE * MS_LD], tw[MS_TILE * MS_LD];
+  __shared__ float tt[3 * MS_TSTRIDE];
+  float* const tx = tt;
+  float* const ty = tt + MS_TSTRIDE;
+  float* const tw = tt + 2 * MS_TSTRIDE;
   __shared__ float s_mx[MS_FACES], s_my[MS_FACES];
   __shared__ int s_cnt[MS_FACES], s_live[MS_FACES], s_chain[MS_FACES];
   __shared__ int64_t s_vb[MS_FACES];
@@ -2057,8 +2064,10 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
   }
   __syncthreads();
   const int maxcnt = s_maxcnt;
-  // lane p of wave 0 owns chain s_chain[p]; its sums live in registers
+  // lane p of wave 0 owns chain s_chain[p]; its sums live in registers (SUM3: lanes 3p + e, component e)
   float ax = 0, ay = 0, aw = 0;
+  float acc = 0;
+  const int sp = tid / 3, se = tid - 3 * sp;  // SUM3: the face and component this lane adds
   // pass = -1: getMean (terms x*w, y*w, w); pass >= 0: getWeightedMean iteration
   for (int pass = -1; pass < max_iter; pass++) {
     if (pass >= 0) {
@@ -2069,6 +2078,7 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
       if (s_nlive == 0) break;
     }
     ax = ay = aw = 0;
+    acc = 0;
     // wave w owns faces w + 4 i (i < MS_FPW): a face's MS_TILE = 64 votes of a tile are one wave's lanes,
     // so its count, list base and mean are wave-uniform.  The votes of tile k0 are loaded into
     // registers during tile k0 - 64's serial phase (the first tile's here).
@@ -2098,7 +2108,20 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
       }
       if (k0 + MS_TILE < maxcnt) load_tile(k0 + MS_TILE);  // in flight during the serial phase
       __syncthreads();
-      if (tid < MS_FACES && s_live[tid]) {  // serial phase, in list order
+      if (FFD_MS_SUM3 && tid < 3 * MS_FACES && s_live[sp]) {  // serial phase, in list order, a component per lane
+        const int lim = min(MS_TILE, s_cnt[sp] - k0);
+        const float* src = tt + se * MS_TSTRIDE + sp;
+        int j = 0;
+        for (; j + MS_RA <= lim; j += MS_RA) {
+          float v[MS_RA];
+#pragma unroll
+          for (int q = 0; q < MS_RA; q++) v[q] = src[(j + q) * MS_LD];
+#pragma unroll
+          for (int q = 0; q < MS_RA; q++) acc += v[q];
+        }
+        for (; j < lim; j++) acc += src[j * MS_LD];
+      }
+      if (!FFD_MS_SUM3 && tid < MS_FACES && s_live[tid]) {  // serial phase, in list order
         const int lim = min(MS_TILE, s_cnt[tid] - k0);
         int j = 0;
         for (; j + MS_RA <= lim; j += MS_RA) {  // LDS reads of MS_RA terms ahead of their in-order adds
@@ -2123,6 +2146,11 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         }
       }
       __syncthreads();
+    }
+    if (FFD_MS_SUM3) {  // face tid's sums from lanes 3 tid .. 3 tid + 2 of wave 0
+      ax = __shfl(acc, 3 * tid);
+      ay = __shfl(acc, 3 * tid + 1);
+      aw = __shfl(acc, 3 * tid + 2);
     }
     if (tid < MS_FACES && s_live[tid]) {
       if (aw > 0) { ax /= aw; ay /= aw; }
@@ -2533,17 +2561,13 @@ bool traverse_shape_supported(TravShape g, bool hp) {
 void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, TravShape g, const uint4* pairs, const uint4* tops,
                      const uint32_t* top_idx, int top_max, const uint32_t* far, const HpState* state, int ntrees_hp,
                      int step, int step_y, int64_t plane, const uint16_t* chan, int32_t* leaf_out, int n_wg,
-                     int lds_cap, hipStream_t s, const int32_t* inl_trees, int n_inl) {
+                     int lds_cap, hipStream_t s) {
   const int total_blocks = n * bpf;
   if (total_blocks <= 0) return;
   // the window, then as many tree-top entries as the rest of the CU's LDS holds
   const int WW = 32 + step * (g.gx - 1), WH = 32 + step_y * (g.gy - 1), lds = lds_cap;
   TravArgs A{faces, n, bpf, pairs, tops, top_idx, lds - trav_window_bytes(WW, WH, g.gx * step) - TRAV_BLK_BYTES, top_max,
-             far, state, ntrees_hp, step, step_y, (int)plane, lds, chan, leaf_out, 0, {}};
-  if (!hp && !state) {
-    A.n_inl = std::min(std::max(n_inl, 0), MAX_TREES);
-    for (int t = 0; t < A.n_inl; t++) A.inl_trees[t] = inl_trees[t];
-  }
+             far, state, ntrees_hp, step, step_y, (int)plane, lds, chan, leaf_out};
   // one persistent workgroup per CU, but no more than the blocks need (a one-face call has ~50 blocks)
   const int grid = std::max(8, std::min(n_wg & ~7, (total_blocks + 7) & ~7));
   const bool c16 = trav_chunk_bytes(WW, g.gx * step) == 16;

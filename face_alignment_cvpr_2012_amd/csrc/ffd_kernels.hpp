@@ -47,9 +47,7 @@ bool traverse_shape_supported(TravShape g, bool hp);  // an instantiated k_trave
 void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, TravShape g, const uint4* pairs, const uint4* tops,
                      const uint32_t* top_idx, int top_max, const uint32_t* far, const HpState* state, int ntrees_hp,
                      int step, int step_y, int64_t plane, const uint16_t* chan, int32_t* leaf_out, int n_wg,
-                     int lds_cap, hipStream_t s, const int32_t* inl_trees = nullptr, int n_inl = 0);
-// inl_trees / n_inl: an FFD pass over one image sample with state == nullptr takes its tree list in the kernel
-// arguments (no upload).
+                     int lds_cap, hipStream_t s);
 hipError_t set_traverse_lds_limit(int bytes);
 // the traversals of float-integral faces (FaceDesc::fint) over the 16-B node arrays
 void launch_walk_fint(bool hp, const FaceDesc* faces, int n, const uint4* nodes, const int32_t* roots, int ntrees_hp,

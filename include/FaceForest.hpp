@@ -742,16 +742,16 @@ template <class S> struct Tree {
 template <class S> class Forest {
  public:
   typedef typename S::Leaf Leaf;
-  Forest() : list_(std::make_shared<TreeList>()), cache_(std::make_shared<Cache>()) {}
-  Forest(ffd_engine* e, std::vector<int32_t> trees)
-      : engine_(e), list_(std::make_shared<TreeList>()), cache_(std::make_shared<Cache>()) {
+  Forest() : sh_(std::make_shared<Shared>()) {}
+  Forest(ffd_engine* e, std::vector<int32_t> trees) : sh_(std::make_shared<Shared>()) {
+    engine_ = e;
     for (int32_t t : trees) addTree(t);
   }
-  int numberOfTrees() const { return (int)list_->ids.size(); }
-  const std::vector<int32_t>& treeIds() const { return list_->ids; }
+  int numberOfTrees() const { return (int)sh_->list->ids.size(); }
+  const std::vector<int32_t>& treeIds() const { return sh_->list->ids; }
   ffd_engine* engine() const { return engine_; }
-  void setParam(ForestParam fp) { param_ = std::make_shared<const ForestParam>(std::move(fp)); }
-  ForestParam getParam() const { return param_ ? *param_ : ForestParam(); }
+  void setParam(ForestParam fp) { mut_shared().param = std::make_shared<const ForestParam>(std::move(fp)); }
+  ForestParam getParam() const { return sh_->param ? *sh_->param : ForestParam(); }
   // Forest::addTree / getTree / cleanForest (Forest.hpp:41-68), as FaceForest::analyzeFace composes the
   // per-face forest from the jungle (FaceForest.cpp:239-250)
   void addTree(Tree<S>* tree) {
@@ -764,7 +764,7 @@ template <class S> class Forest {
     l.trees.push_back(Tree<S>(id, engine_));
   }
   Tree<S>* getTree(int idx) { return &mut().trees.at(idx); }
-  void cleanForest() { list_ = std::make_shared<TreeList>(); }
+  void cleanForest() { mut_shared().list = std::make_shared<TreeList>(); }
   // the patch grid step of the speculative evaluation (0: S::default_step)
   void setGridStep(int step) { grid_step_ = step; }
 
@@ -799,12 +799,12 @@ template <class S> class Forest {
 
   // Forest<S>::evaluateMT(const S*, S::Leaf**) (Forest.hpp:80-90): leafs[t] = the leaf tree t reaches.
   void evaluateMT(const S* sample, Leaf** leafs) const {
-    const size_t T = list_->ids.size();
-    std::lock_guard<std::mutex> g(cache_->mu);
+    const size_t T = sh_->list->ids.size();
+    Cache& c = *sh_->cache;
+    std::lock_guard<std::mutex> g(c.mu);
     const size_t row = grid_row(sample);
     if (row != npos) {
-      const int32_t* id = &cache_->grid_ids[row];
-      for (size_t t = 0; t < T; t++) leafs[t] = cache_->leaves[id[t]].get();
+      std::copy(&c.grid_leaf[row], &c.grid_leaf[row] + T, leafs);
       return;
     }
     std::vector<int32_t> ids(T);
@@ -813,18 +813,19 @@ template <class S> class Forest {
   }
   // the same with the model's leaf ordinals (ffd_forest_leaves gives their payloads)
   void evaluateMT(const S* sample, int32_t* leafs) const {
-    const size_t T = list_->ids.size();
-    std::lock_guard<std::mutex> g(cache_->mu);
+    const size_t T = sh_->list->ids.size();
+    Cache& c = *sh_->cache;
+    std::lock_guard<std::mutex> g(c.mu);
     const size_t row = grid_row(sample);
     if (row != npos) {
-      std::copy(&cache_->grid_ids[row], &cache_->grid_ids[row] + T, leafs);
+      std::copy(&c.grid_ids[row], &c.grid_ids[row] + T, leafs);
       return;
     }
     eval_one(sample, leafs);
   }
   // the payload of a leaf ordinal (the reference: TreeNode::getLeaf, TreeNode.hpp:61-66)
   Leaf& leaf(int32_t ordinal) const {
-    std::lock_guard<std::mutex> g(cache_->mu);
+    std::lock_guard<std::mutex> g(sh_->cache->mu);
     return *leaf_locked(ordinal);
   }
 
@@ -835,24 +836,39 @@ template <class S> class Forest {
     std::vector<std::unique_ptr<Leaf>> leaves;  // by leaf ordinal (a lookup per patch and tree: no hashing)
     // the speculative grid evaluation of the last (sample, tree list): patches (x0 + i step, y0 + j step)
     uint64_t sample = 0;
+    uint64_t list_uid = 0;  // the TreeList the grid was evaluated for
     std::vector<int32_t> ids;
     int x0 = 0, y0 = 0, step = 0, nx = 0, ny = 0;
-    std::vector<int32_t> grid_ids;  // [(i * ny + j) * T + t]; leaves[] holds the payload of each
+    std::vector<int32_t> grid_ids;  // [(i * ny + j) * T + t]
+    std::vector<Leaf*> grid_leaf;   // their payloads
   };
   // the tree list, shared by copies until one of them changes it (a copy per evaluateMT call, as the reference
   // binds the forest by value into every task, then costs a reference count, not a list copy)
   struct TreeList {
     std::vector<int32_t> ids;
     std::deque<Tree<S>> trees;
+    uint64_t uid = detail::next_sample_id();  // a new one with every change (the cache's key)
+  };
+  // what copies share: the tree list, the param and the evaluation cache behind ONE reference count, so the copy
+  // per evaluateMT call costs one atomic increment (copy-on-write: a copy that changes its list or param gets its
+  // own Shared, still over the same cache, which is keyed by the tree list)
+  struct Shared {
+    std::shared_ptr<TreeList> list = std::make_shared<TreeList>();
+    std::shared_ptr<const ForestParam> param;
+    std::shared_ptr<Cache> cache = std::make_shared<Cache>();
   };
   ffd_engine* engine_ = nullptr;
-  std::shared_ptr<const ForestParam> param_;  // (shared by copies: a per-call copy allocates nothing)
-  std::shared_ptr<TreeList> list_;
   int grid_step_ = 0;
-  std::shared_ptr<Cache> cache_;
+  std::shared_ptr<Shared> sh_;
+  Shared& mut_shared() {
+    if (sh_.use_count() > 1) sh_ = std::make_shared<Shared>(*sh_);
+    return *sh_;
+  }
   TreeList& mut() {
-    if (list_.use_count() > 1) list_ = std::make_shared<TreeList>(*list_);
-    return *list_;
+    Shared& x = mut_shared();
+    if (x.list.use_count() > 1) x.list = std::make_shared<TreeList>(*x.list);
+    x.list->uid = detail::next_sample_id();
+    return *x.list;
   }
 
   // an engine call under the engine's lock (detail::engine_call); a failure throws with its error text
@@ -861,7 +877,7 @@ template <class S> class Forest {
     if (detail::engine_call(e, err, f) != FFD_OK) throw std::invalid_argument(err);
   }
   Leaf* leaf_locked(int32_t ordinal) const {
-    auto& v = cache_->leaves;
+    auto& v = sh_->cache->leaves;
     if (ordinal >= 0 && (size_t)ordinal < v.size() && v[ordinal]) return v[ordinal].get();
     typename ForestKind<S>::Raw raw;
     call(engine_, [&] { return ffd_forest_leaves(engine_, ForestKind<S>::value, &ordinal, 1, &raw); });  // (rejects a bad ordinal)
@@ -873,22 +889,25 @@ template <class S> class Forest {
   void eval_one(const S* sample, int32_t* ids) const {
     const int32_t xy[2] = {sample->roi.x, sample->roi.y};
     call(sample->image->engine(), [&] {
-      return ffd_sample_eval_leaves(sample->image->handle(), ForestKind<S>::value, xy, 1, list_->ids.data(),
-                                    (int32_t)list_->ids.size(), ids);
+      return ffd_sample_eval_leaves(sample->image->handle(), ForestKind<S>::value, xy, 1, sh_->list->ids.data(),
+                                    (int32_t)sh_->list->ids.size(), ids);
     });
   }
   // The offset of the sample patch's leaf row in the grid evaluation, evaluating the grid that contains the patch
   // first when the cache holds another sample or tree list; npos for a patch off the grid.
   size_t grid_row(const S* sample) const {
-    Cache& c = *cache_;
+    Cache& c = *sh_->cache;
     const ImageSample& im = *sample->image;
-    const std::vector<int32_t>& ids = list_->ids;
+    const TreeList& L = *sh_->list;
+    const std::vector<int32_t>& ids = L.ids;
     const int x = sample->roi.x, y = sample->roi.y, P = 31, T = (int)ids.size();
-    if (c.sample != im.id() || c.ids != ids) {
+    if (c.list_uid != L.uid && c.ids == ids) c.list_uid = L.uid;  // another list with the same trees
+    if (c.sample != im.id() || c.list_uid != L.uid) {
       const int step = grid_step_ > 0 ? grid_step_ : S::default_step;
       if (x < 0 || y < 0 || x + P > im.width() || y + P > im.height() || T == 0) return npos;
       c.sample = 0;
       c.ids = ids;
+      c.list_uid = L.uid;
       c.x0 = x % step;
       c.y0 = y % step;
       c.step = step;
@@ -902,8 +921,13 @@ template <class S> class Forest {
       // the payloads of every leaf reached, fetched once per forest cache (one pass over the grid)
       std::vector<int32_t> uniq;
       const size_t have = c.leaves.size();
-      for (int32_t v : c.grid_ids)
-        if ((size_t)v >= have || !c.leaves[v]) uniq.push_back(v);
+      c.grid_leaf.resize(c.grid_ids.size());
+      for (size_t i = 0; i < c.grid_ids.size(); i++) {
+        const int32_t v = c.grid_ids[i];
+        Leaf* l = (size_t)v < have ? c.leaves[v].get() : nullptr;
+        c.grid_leaf[i] = l;
+        if (!l) uniq.push_back(v);
+      }
       if (!uniq.empty()) {
         std::sort(uniq.begin(), uniq.end());
         uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
@@ -915,6 +939,8 @@ template <class S> class Forest {
           ForestKind<S>::fill(raw[i], *l);
           c.leaves[uniq[i]] = std::move(l);
         }
+        for (size_t i = 0; i < c.grid_ids.size(); i++)
+          if (!c.grid_leaf[i]) c.grid_leaf[i] = c.leaves[c.grid_ids[i]].get();
       }
       c.sample = im.id();
     }

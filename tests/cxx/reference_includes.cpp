@@ -202,10 +202,11 @@ static int train_main(const char* ffd_cfg, const char* ann_path, int n_images, c
   ffd_train_param_init(&tp);
   tp.max_depth = mp_param.max_depth; tp.min_patches = mp_param.min_patches; tp.ntests = mp_param.ntests;
   tp.npatches = mp_param.npatches; tp.face_size = mp_param.face_size; tp.patch_size_ratio = mp_param.patch_size_ratio;
+  tp.ntrees = mp_param.ntrees; tp.nimages = mp_param.nimages;  // (the archive records the ForestParam, as Tree::save)
   tp.tree_seed = 100;
   tp.split_seed = (uint32_t)std::strtoul(std::getenv("FFD_SPLIT_SEED") ? std::getenv("FFD_SPLIT_SEED") : "7", nullptr, 10);
-  char tree_path[512];
-  std::snprintf(tree_path, sizeof tree_path, "%s/tree_%03d.txt", out_dir, 99);
+  char tree_path[512];  // (the path the shim's Tree below saves to: the archive records it)
+  std::snprintf(tree_path, sizeof tree_path, "%s/tree_%03d.txt", out_dir, 98);
   tp.tree_path = mp_param.tree_path.c_str();
   tp.image_path = mp_param.image_path.c_str();
   tp.save_path = tree_path;
@@ -241,7 +242,7 @@ static int train_main(const char* ffd_cfg, const char* ann_path, int n_images, c
   std::string a((size_t)sa, '\0'), b((size_t)sb, '\0');
   ffd_trained_tree_archive(ref, &a[0], sa, &sa);
   ffd_trained_tree_archive(tree->trained.get(), &b[0], sb, &sb);
-  std::printf("samples %lld nodes %lld %lld same_archive %d\n", (long long)n, (long long)ffd_trained_tree_num_nodes(ref),
+  std::printf("samples %lld nodes %lld nodes_shim %lld same_archive %d\n", (long long)n, (long long)ffd_trained_tree_num_nodes(ref),
               (long long)ffd_trained_tree_num_nodes(tree->trained.get()), a == b ? 1 : 0);
   std::ifstream saved(tree_path2, std::ios::binary);
   std::string file((std::istreambuf_iterator<char>(saved)), std::istreambuf_iterator<char>());
