@@ -804,7 +804,8 @@ template <class S> class Forest {
     std::lock_guard<std::mutex> g(c.mu);
     const size_t row = grid_row(sample);
     if (row != npos) {
-      std::copy(&c.grid_leaf[row], &c.grid_leaf[row] + T, leafs);
+      const int32_t* id = &c.grid_ids[row];
+      for (size_t t = 0; t < T; t++) leafs[t] = c.at(id[t]);
       return;
     }
     std::vector<int32_t> ids(T);
@@ -833,14 +834,34 @@ template <class S> class Forest {
   static constexpr size_t npos = ~(size_t)0;
   struct Cache {
     std::mutex mu;
-    std::vector<std::unique_ptr<Leaf>> leaves;  // by leaf ordinal (a lookup per patch and tree: no hashing)
+    // leaf payloads by ordinal in chunks of CH (stable addresses; Leaf* = chunk table + arithmetic, no per-leaf
+    // pointer to load) with a filled bit per leaf; a chunk's leaves are filled as grids reach them
+    static constexpr uint32_t CH_SHIFT = 12, CH = 1u << CH_SHIFT;
+    std::vector<std::unique_ptr<Leaf[]>> chunk;
+    std::vector<uint64_t> filled;  // one bit per ordinal
+    Leaf* at(int32_t o) const { return &chunk[(uint32_t)o >> CH_SHIFT][(uint32_t)o & (CH - 1)]; }  // (o filled)
+    bool has(int32_t o) const {
+      const uint32_t u = (uint32_t)o;
+      return (size_t)(u >> 6) < filled.size() && ((filled[u >> 6] >> (u & 63)) & 1u);
+    }
+    Leaf* put(int32_t o, const typename ForestKind<S>::Raw& r) {
+      const uint32_t u = (uint32_t)o, k = u >> CH_SHIFT;
+      if (k >= chunk.size()) {
+        chunk.resize(k + 1);
+        filled.resize((size_t)(k + 1) * (CH / 64), 0);
+      }
+      if (!chunk[k]) chunk[k].reset(new Leaf[CH]);
+      Leaf* l = &chunk[k][u & (CH - 1)];
+      ForestKind<S>::fill(r, *l);
+      filled[u >> 6] |= 1ull << (u & 63);
+      return l;
+    }
     // the speculative grid evaluation of the last (sample, tree list): patches (x0 + i step, y0 + j step)
     uint64_t sample = 0;
     uint64_t list_uid = 0;  // the TreeList the grid was evaluated for
     std::vector<int32_t> ids;
     int x0 = 0, y0 = 0, step = 0, nx = 0, ny = 0;
     std::vector<int32_t> grid_ids;  // [(i * ny + j) * T + t]
-    std::vector<Leaf*> grid_leaf;   // their payloads
   };
   // the tree list, shared by copies until one of them changes it (a copy per evaluateMT call, as the reference
   // binds the forest by value into every task, then costs a reference count, not a list copy)
@@ -877,14 +898,11 @@ template <class S> class Forest {
     if (detail::engine_call(e, err, f) != FFD_OK) throw std::invalid_argument(err);
   }
   Leaf* leaf_locked(int32_t ordinal) const {
-    auto& v = sh_->cache->leaves;
-    if (ordinal >= 0 && (size_t)ordinal < v.size() && v[ordinal]) return v[ordinal].get();
+    Cache& c = *sh_->cache;
+    if (ordinal >= 0 && c.has(ordinal)) return c.at(ordinal);
     typename ForestKind<S>::Raw raw;
     call(engine_, [&] { return ffd_forest_leaves(engine_, ForestKind<S>::value, &ordinal, 1, &raw); });  // (rejects a bad ordinal)
-    std::unique_ptr<Leaf> l(new Leaf());
-    ForestKind<S>::fill(raw, *l);
-    if ((size_t)ordinal >= v.size()) v.resize((size_t)ordinal + 1);
-    return (v[ordinal] = std::move(l)).get();
+    return c.put(ordinal, raw);
   }
   void eval_one(const S* sample, int32_t* ids) const {
     const int32_t xy[2] = {sample->roi.x, sample->roi.y};
@@ -918,29 +936,16 @@ template <class S> class Forest {
         return ffd_sample_eval_grid(im.handle(), ForestKind<S>::value, c.x0, c.y0, step, c.nx, c.ny, ids.data(), T,
                                     c.grid_ids.data());
       });
-      // the payloads of every leaf reached, fetched once per forest cache (one pass over the grid)
+      // the payloads of every leaf reached, fetched once per forest cache (one pass over the grid: bit tests)
       std::vector<int32_t> uniq;
-      const size_t have = c.leaves.size();
-      c.grid_leaf.resize(c.grid_ids.size());
-      for (size_t i = 0; i < c.grid_ids.size(); i++) {
-        const int32_t v = c.grid_ids[i];
-        Leaf* l = (size_t)v < have ? c.leaves[v].get() : nullptr;
-        c.grid_leaf[i] = l;
-        if (!l) uniq.push_back(v);
-      }
+      for (int32_t v : c.grid_ids)
+        if (!c.has(v)) uniq.push_back(v);
       if (!uniq.empty()) {
         std::sort(uniq.begin(), uniq.end());
         uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
         std::vector<typename ForestKind<S>::Raw> raw(uniq.size());
         call(engine_, [&] { return ffd_forest_leaves(engine_, ForestKind<S>::value, uniq.data(), (int32_t)uniq.size(), raw.data()); });
-        if ((size_t)uniq.back() >= have) c.leaves.resize((size_t)uniq.back() + 1);
-        for (size_t i = 0; i < uniq.size(); i++) {
-          std::unique_ptr<Leaf> l(new Leaf());
-          ForestKind<S>::fill(raw[i], *l);
-          c.leaves[uniq[i]] = std::move(l);
-        }
-        for (size_t i = 0; i < c.grid_ids.size(); i++)
-          if (!c.grid_leaf[i]) c.grid_leaf[i] = c.leaves[c.grid_ids[i]].get();
+        for (size_t i = 0; i < uniq.size(); i++) c.put(uniq[i], raw[i]);
       }
       c.sample = im.id();
     }
