@@ -127,7 +127,7 @@ EXPORTED_SYMBOLS = (
     "ffd_sample_create", "ffd_sample_create_from_channels", "ffd_sample_destroy", "ffd_sample_size",
     "ffd_sample_channels", "ffd_sample_eval_leaves", "ffd_sample_eval_grid", "ffd_sample_estimate_headpose",
     "ffd_sample_estimate_facial_features", "ffd_meanshift", "ffd_model_convert", "ffd_model_convert_last_error",
-    "ffd_forest_subdirs", "ffd_group_debug_overlap",
+    "ffd_forest_subdirs", "ffd_group_debug_overlap", "ffd_forest_tree_leaves",
 )
 COMM_ID_BYTES = 128
 STATUS_OK, STATUS_INVALID_ARGUMENT, STATUS_OUT_OF_MEMORY, STATUS_UNSUPPORTED = 0, 1, 4, 7

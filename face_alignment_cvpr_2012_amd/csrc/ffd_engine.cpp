@@ -297,6 +297,12 @@ void ffd_engine::load_model(const std::string& path) {
   // option-dependent leaf tables (head-pose values, FFD vote records) for desc's options
   hp_leaves = (int64_t)m.get("hp.leaf_n").count();
   mp_leaves = (int64_t)m.get("mp.leaf_n").count();
+  for (int k = 0; k < 2; k++) {  // per tree: its leaf ordinals [off[t], off[t + 1]) (ffd_forest_tree_leaves)
+    const std::string name = k ? "mp.tree_leaf_off" : "hp.tree_leaf_off";
+    std::vector<int64_t>& v = k ? mp_tree_leaf_off : hp_tree_leaf_off;
+    v.clear();
+    if (m.has(name)) v.assign(m.get(name).as<int64_t>(), m.get(name).as<int64_t>() + m.get(name).count());
+  }
   upload(hp_m, hp_leaf_values(m, desc.hp_option), main_stream());
   {
     VoteTable vt = mp_vote_records(m, desc.mp_option);
@@ -1377,6 +1383,19 @@ ffd_status ffd_estimate_facial_features(ffd_engine* e, const uint32_t* channels,
     Workspace& w = *e->ws[0];
     const FaceDesc f = stage_sample(e, w, channels, W, H, *region, e->desc.hp_option.step_size, o.step_size, step_y);
     run_facial_features(e, w, f, w.chan.as<uint16_t>(), tree_ids, n_trees, o, points);
+    return FFD_OK;
+  });
+}
+
+ffd_status ffd_forest_tree_leaves(ffd_engine* e, int32_t kind, int32_t tree_id, int32_t* first, int32_t* count) {
+  if (e && e->detector_only) return no_forests(e);
+  return guarded(e, [&]() -> ffd_status {
+    if (!first || !count) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (kind != FFD_FOREST_HEADPOSE && kind != FFD_FOREST_FFD) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad forest kind");
+    const std::vector<int64_t>& off = kind == FFD_FOREST_HEADPOSE ? e->hp_tree_leaf_off : e->mp_tree_leaf_off;
+    if (tree_id < 0 || (size_t)tree_id + 1 >= off.size()) return fail(e, FFD_ERR_INVALID_ARGUMENT, "tree id out of range");
+    *first = (int32_t)off[tree_id];
+    *count = (int32_t)(off[tree_id + 1] - off[tree_id]);
     return FFD_OK;
   });
 }

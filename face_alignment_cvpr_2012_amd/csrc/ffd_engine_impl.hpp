@@ -153,6 +153,7 @@ struct ffd_engine {
   // model parameters
   int face_size = 125, patch = 31, hp_trees = 0, n_forests = 0, ntrees_per_forest = 0;
   int64_t hp_leaves = 0, mp_leaves = 0;
+  std::vector<int64_t> hp_tree_leaf_off, mp_tree_leaf_off;  // per tree: first leaf ordinal (+ the total at the end)
 
   // device model
   DevBuf gabor_coef, hp_nodes, hp_roots, hp_sizes, hp_m, mp_nodes, mp_roots, mp_sizes, mp_rec;

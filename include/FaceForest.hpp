@@ -839,6 +839,7 @@ template <class S> class Forest {
     static constexpr uint32_t CH_SHIFT = 12, CH = 1u << CH_SHIFT;
     std::vector<std::unique_ptr<Leaf[]>> chunk;
     std::vector<uint64_t> filled;  // one bit per ordinal
+    std::vector<uint8_t> tree_done;  // by tree id: every leaf of the tree filled
     Leaf* at(int32_t o) const { return &chunk[(uint32_t)o >> CH_SHIFT][(uint32_t)o & (CH - 1)]; }  // (o filled)
     bool has(int32_t o) const {
       const uint32_t u = (uint32_t)o;
@@ -861,6 +862,7 @@ template <class S> class Forest {
     uint64_t list_uid = 0;  // the TreeList the grid was evaluated for
     std::vector<int32_t> ids;
     int x0 = 0, y0 = 0, step = 0, nx = 0, ny = 0;
+    std::vector<int32_t> col, row;  // patch x / y -> grid index i / j (-1: off the grid)
     std::vector<int32_t> grid_ids;  // [(i * ny + j) * T + t]
   };
   // the tree list, shared by copies until one of them changes it (a copy per evaluateMT call, as the reference
@@ -931,28 +933,35 @@ template <class S> class Forest {
       c.step = step;
       c.nx = (im.width() - P - c.x0) / step + 1;
       c.ny = (im.height() - P - c.y0) / step + 1;
+      c.col.assign((size_t)im.width(), -1);
+      c.row.assign((size_t)im.height(), -1);
+      for (int k = 0; k < c.nx; k++) c.col[(size_t)(c.x0 + k * step)] = k;
+      for (int k = 0; k < c.ny; k++) c.row[(size_t)(c.y0 + k * step)] = k;
       c.grid_ids.resize((size_t)c.nx * c.ny * T);
       call(im.engine(), [&] {
         return ffd_sample_eval_grid(im.handle(), ForestKind<S>::value, c.x0, c.y0, step, c.nx, c.ny, ids.data(), T,
                                     c.grid_ids.data());
       });
-      // the payloads of every leaf reached, fetched once per forest cache (one pass over the grid: bit tests)
-      std::vector<int32_t> uniq;
-      for (int32_t v : c.grid_ids)
-        if (!c.has(v)) uniq.push_back(v);
-      if (!uniq.empty()) {
-        std::sort(uniq.begin(), uniq.end());
-        uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
-        std::vector<typename ForestKind<S>::Raw> raw(uniq.size());
-        call(engine_, [&] { return ffd_forest_leaves(engine_, ForestKind<S>::value, uniq.data(), (int32_t)uniq.size(), raw.data()); });
-        for (size_t i = 0; i < uniq.size(); i++) c.put(uniq[i], raw[i]);
+      // every leaf payload of the list's trees, the first time a tree is used (the reference holds each loaded
+      // tree's leaves in memory, Forest::load): the grid's leaves need no check, a Leaf* is arithmetic
+      for (int32_t t : ids) {
+        if ((size_t)t < c.tree_done.size() && c.tree_done[t]) continue;
+        int32_t first = 0, count = 0;
+        call(engine_, [&] { return ffd_forest_tree_leaves(engine_, ForestKind<S>::value, t, &first, &count); });
+        std::vector<int32_t> ord((size_t)count);
+        for (int32_t i = 0; i < count; i++) ord[i] = first + i;
+        std::vector<typename ForestKind<S>::Raw> raw((size_t)count);
+        if (count) call(engine_, [&] { return ffd_forest_leaves(engine_, ForestKind<S>::value, ord.data(), count, raw.data()); });
+        for (int32_t i = 0; i < count; i++)
+          if (!c.has(first + i)) c.put(first + i, raw[i]);
+        if ((size_t)t >= c.tree_done.size()) c.tree_done.resize((size_t)t + 1, 0);
+        c.tree_done[t] = 1;
       }
       c.sample = im.id();
     }
-    const int dx = x - c.x0, dy = y - c.y0;
-    if (dx < 0 || dy < 0 || dx % c.step || dy % c.step) return npos;
-    const int i = dx / c.step, j = dy / c.step;
-    if (i >= c.nx || j >= c.ny) return npos;
+    // grid index of the patch by table (no divisions per call): col[x] = i for x = x0 + i step, else -1
+    const int i = (unsigned)x < c.col.size() ? c.col[x] : -1, j = (unsigned)y < c.row.size() ? c.row[y] : -1;
+    if (i < 0 || j < 0) return npos;
     return ((size_t)i * c.ny + j) * T;
   }
 };

@@ -199,6 +199,11 @@ typedef struct {             /* MPLeaf, include/MPSample.hpp:137-159 */
   float mp_prob_foreground[FFD_NUM_LANDMARKS];
 } ffd_mp_leaf;
 ffd_status ffd_forest_leaves(ffd_engine* engine, int32_t forest_kind, const int32_t* leaf_ids, int32_t n, void* out);
+/* The leaf ordinals of one tree (global tree id as in tree_ids): [*first, *first + *count).  What the reference holds
+ * in memory per loaded tree (Forest::load, include/Forest.hpp:103-129); the C++ header fills a forest's payloads tree
+ * by tree with it. */
+ffd_status ffd_forest_tree_leaves(ffd_engine* engine, int32_t forest_kind, int32_t tree_id, int32_t* first,
+                                  int32_t* count);
 
 /* ---- Device-resident image samples (ImageSample + Forest<S>::evaluateMT, the reference's low-level API) ----
  * ffd_sample_create      ImageSample(img, features, use_integral)     src/ImageSample.cpp:11-20,77-90: the 38

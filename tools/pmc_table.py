@@ -3,6 +3,7 @@ usage: python tools/pmc_table.py gpurun_out/pmc_TAG [kernel-substring ...]"""
 import csv
 import glob
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -16,7 +17,8 @@ def main():
             k = r["Kernel_Name"]
             if keys and not any(s in k for s in keys):
                 continue
-            acc[k.split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            m = re.search(r"(k_\w+(?:<[^>]*>)?)", k)  # (anonymous-namespace kernels: "ffd::(anonymous namespace)::k_...")
+            acc[m.group(1) if m else k.split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, cs in sorted(acc.items()):
         print(k)
         for c, v in sorted(cs.items()):
