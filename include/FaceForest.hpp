@@ -805,7 +805,11 @@ template <class S> class Forest {
     const size_t row = grid_row(sample);
     if (row != npos) {
       const int32_t* id = &c.grid_ids[row];
-      for (size_t t = 0; t < T; t++) leafs[t] = c.at(id[t]);
+      const std::unique_ptr<Leaf[]>* ch = c.chunk.data();  // (hoisted: the stores below may alias for the compiler)
+      for (size_t t = 0; t < T; t++) {
+        const uint32_t u = (uint32_t)id[t];
+        leafs[t] = &ch[u >> Cache::CH_SHIFT][u & (Cache::CH - 1)];
+      }
       return;
     }
     std::vector<int32_t> ids(T);
