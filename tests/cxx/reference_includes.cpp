@@ -295,6 +295,16 @@ static int cpu_main(const char* ann_path, const char* ppm, const char* cfg) {
   return EXIT_SUCCESS;
 }
 
+// FaceForest(FaceForestOptions) over the reference's tree directories with the given cascade path: the reference's
+// constructor returns uninitialised when the cascade does not load (FaceForest.cpp:23-27)
+static int init_main(const char* hp_cfg, const char* ffd_cfg, const char* cascade) {
+  FaceForestOptions ff_options;
+  if (!options_from(hp_cfg, ffd_cfg, cascade, ff_options)) return EXIT_FAILURE;
+  FaceForest ff(ff_options);
+  std::printf("initialized %d\n", ff.is_initialized() ? 1 : 0);
+  return EXIT_SUCCESS;
+}
+
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "";
   try {
@@ -302,6 +312,7 @@ int main(int argc, char** argv) {
     if (mode == "eval" && argc == 5) return eval_main(argv[2], argv[3], argv[4]);
     if (mode == "analyze" && argc == 6) return analyze_main(argv[2], argv[3], argv[4], argv[5]);
     if (mode == "detect" && argc == 4) return detect_main(argv[2], argv[3]);
+    if (mode == "init" && argc == 5) return init_main(argv[2], argv[3], argv[4]);
     if (mode == "train" && argc == 6) return train_main(argv[2], argv[3], std::atoi(argv[4]), argv[5]);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "exception: %s\n", e.what());

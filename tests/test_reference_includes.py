@@ -105,6 +105,24 @@ def _configs(reference_tree, image_dir, tmp):
     return out
 
 
+def test_missing_cascade_leaves_it_uninitialized(exe, reference_tree, image_dir, tmp_path):
+    """like the reference's constructor (FaceForest.cpp:23-27), a FaceForest whose cascade does not load
+    (a missing file, an empty path, a file that is not a cascade) is not initialised; no GPU is reached."""
+    hp, ffd = _configs(reference_tree, image_dir, tmp_path)
+    env = dict(os.environ, FFD_MODEL_CACHE=str(tmp_path / "cache"))
+    env.pop("FFD_MODEL", None)
+    (tmp_path / "cache").mkdir()
+    junk = tmp_path / "junk.xml"
+    junk.write_text("<opencv_storage><nothing/></opencv_storage>")
+    for cascade in (tmp_path / "missing.xml", junk):
+        r = _run(exe, "init", hp, ffd, cascade, env=env)
+        assert r.returncode == 0 and "initialized 0" in r.stdout, (cascade, r.stdout, r.stderr)
+        assert "Error loading" in r.stderr and "cascade" in r.stderr.lower(), r.stderr
+    # the bundled cascade converts (the model is built; without a device the engine itself then fails)
+    r = _run(exe, "init", hp, ffd, reference_tree["xml"], env=env)
+    assert r.returncode == 0 and "cascade" not in r.stderr.lower(), r.stderr
+
+
 @pytest.mark.gpu
 def test_eval_ffd_main(exe, reference_tree, image_dir, tmp_path, fixtures):
     from face_alignment_cvpr_2012_amd import eval as fe
