@@ -26,6 +26,8 @@ void ffd_engine::load_cascade(const ffd::ModelFile& m) {
   haar_ww = win[0];
   haar_wh = win[1];
   if (haar_ww < 3 || haar_wh < 3 || haar_ww > 255 || haar_wh > 255) throw std::runtime_error("cascade window size");
+  // the squared integral is kept modulo 2^32: exact for the normrect's sum while (ww - 2)(wh - 2) 255^2 < 2^32
+  if ((int64_t)(haar_ww - 2) * (haar_wh - 2) * 255 * 255 >= ((int64_t)1 << 32)) throw std::runtime_error("cascade window too large");
   const auto& sf = m.get("haar.stage_first");
   const auto& sn = m.get("haar.stage_ntrees");
   const auto& st = m.get("haar.stage_threshold");
@@ -260,15 +262,15 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
       upload(e->det_levels, levels, s);
       e->det_scaled.ensure(sz[1]);
       e->det_sum.ensure(sz[2] * 4);
-      e->det_sq.ensure(sz[2] * 8);
+      e->det_sq.ensure(sz[2] * 4);
       e->det_res.ensure(sz[3]);
       launch_haar_gray(e->det_frames.as<HaarFrame>(), nF, max_px, d_images, e->det_gray.as<uint8_t>(), s);
       launch_haar_pyramid(e->det_levels.as<HaarLevel>(), nL, max_lpx, max_rows, max_cols, e->det_gray.as<uint8_t>(),
-                          e->det_scaled.as<uint8_t>(), e->det_sum.as<int32_t>(), e->det_sq.as<uint64_t>(), s);
+                          e->det_scaled.as<uint8_t>(), e->det_sum.as<int32_t>(), e->det_sq.as<uint32_t>(), s);
       const int lds = haar_cascade_lds(max_ystep, e->haar_ww, e->haar_wh);
       if (lds > 64 * 1024) return fail(e, FFD_ERR_UNSUPPORTED, "cascade window too large for the LDS tile");
       launch_haar_cascade(e->det_levels.as<HaarLevel>(), nL, max_tiles, e->det_sum.as<int32_t>(),
-                          e->det_sq.as<uint64_t>(), e->haar_weak.as<HaarWeak>(), e->haar_nweak, e->haar_stage.as<HaarStage>(),
+                          e->det_sq.as<uint32_t>(), e->haar_weak.as<HaarWeak>(), e->haar_nweak, e->haar_stage.as<HaarStage>(),
                           e->haar_stages, e->haar_ww, e->haar_wh, e->haar_order_free, e->det_res.as<int8_t>(), lds, s);
     }
     int max_frame_rows = 0;

@@ -123,16 +123,18 @@ __global__ __launch_bounds__(256) void k_haar_resize(const HaarLevel* __restrict
 }
 
 // ---------------------------------------------------------------------- integrals ----
-// Pass 1: one wave per (level, row y): prefix sums of v and v*v along the row (both < 2^32 for rows
-// up to 2^16 pixels) into sum[y + 1][x + 1] / sq[y + 1][x + 1]; column 0 and row 0 are zeroed here.
+// Pass 1: one wave per (level, row y): prefix sums of v and v*v along the row into sum[y + 1][x + 1] / sq[y + 1][x + 1];
+// column 0 and row 0 are zeroed here.  The squared integral is kept modulo 2^32 (u32): the cascade only reads it
+// through the normrect's four-corner sum, whose true value is below 2^32 (ffd_detect.cpp checks the window), so the
+// modular difference is exact — half the bytes of a u64 plane in both passes and the cascade's corner reads.
 __global__ __launch_bounds__(256) void k_haar_rows(const HaarLevel* __restrict__ levels,
                                                    const uint8_t* __restrict__ scaled, int32_t* __restrict__ sum,
-                                                   uint64_t* __restrict__ sq) {
+                                                   uint32_t* __restrict__ sq) {
   const HaarLevel L = levels[blockIdx.y];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int P = L.sw + 1;
   int32_t* S = sum + L.sum_off;
-  uint64_t* Q = sq + L.sum_off;
+  uint32_t* Q = sq + L.sum_off;
   for (int y = blockIdx.x * 4 + wv; y <= L.sh; y += gridDim.x * 4) {
     if (y == 0) {
       for (int x = lane; x < P; x += 64) { S[x] = 0; Q[x] = 0; }
@@ -140,14 +142,14 @@ __global__ __launch_bounds__(256) void k_haar_rows(const HaarLevel* __restrict__
     }
     const uint8_t* row = scaled + L.img_off + (int64_t)(y - 1) * L.sw;
     int32_t* so = S + (int64_t)y * P;
-    uint64_t* qo = Q + (int64_t)y * P;
+    uint32_t* qo = Q + (int64_t)y * P;
     if (lane == 0) { so[0] = 0; qo[0] = 0; }
     uint32_t cs = 0, cq = 0;
     for (int x0 = 0; x0 < L.sw; x0 += 64) {
       const int x = x0 + lane;
       const uint32_t v = x < L.sw ? row[x] : 0u;
       const uint32_t ps = wave_scan_u32(v), pq = wave_scan_u32(v * v);
-      if (x < L.sw) { so[x + 1] = (int32_t)(cs + ps); qo[x + 1] = (uint64_t)(cq + pq); }
+      if (x < L.sw) { so[x + 1] = (int32_t)(cs + ps); qo[x + 1] = cq + pq; }
       cs += (uint32_t)__builtin_amdgcn_readlane((int)ps, 63);
       cq += (uint32_t)__builtin_amdgcn_readlane((int)pq, 63);
     }
@@ -156,18 +158,18 @@ __global__ __launch_bounds__(256) void k_haar_rows(const HaarLevel* __restrict__
 
 // Pass 2: one thread per (level, column x >= 1): running sums down the rows, 8 rows' loads in flight.
 __global__ __launch_bounds__(256) void k_haar_cols(const HaarLevel* __restrict__ levels, int32_t* __restrict__ sum,
-                                                   uint64_t* __restrict__ sq) {
+                                                   uint32_t* __restrict__ sq) {
   const HaarLevel L = levels[blockIdx.y];
   const int x = 1 + blockIdx.x * 256 + threadIdx.x;
   if (x > L.sw) return;
   const int P = L.sw + 1;
   int32_t* S = sum + L.sum_off + x;
-  uint64_t* Q = sq + L.sum_off + x;
+  uint32_t* Q = sq + L.sum_off + x;
   int32_t as = 0;
-  uint64_t aq = 0;
+  uint32_t aq = 0;
   for (int y0 = 1; y0 <= L.sh; y0 += 8) {
     int32_t vs[8];
-    uint64_t vq[8];
+    uint32_t vq[8];
 #pragma unroll
     for (int k = 0; k < 8; k++)
       if (y0 + k <= L.sh) { vs[k] = S[(int64_t)(y0 + k) * P]; vq[k] = Q[(int64_t)(y0 + k) * P]; }
@@ -217,7 +219,7 @@ __host__ __device__ constexpr int haar_win_rows(int ystep, int wh) { return HT_Y
 
 __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __restrict__ levels,
                                                              const int32_t* __restrict__ sum,
-                                                             const uint64_t* __restrict__ sq,
+                                                             const uint32_t* __restrict__ sq,
                                                              const HaarWeak* __restrict__ weak_tables, int n_weak,
                                                              const HaarStage* __restrict__ stages, int n_stages,
                                                              int ww, int wh, int order_free,
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
   const int x0 = tx * HT_X * ys, y0 = ty * HT_Y * ys;
   const HaarWeak* __restrict__ weak = weak_tables + (ys == 2 ? n_weak : 0);  // offsets for this window pitch
   const int32_t* S = sum + L.sum_off;
-  const uint64_t* Q = sq + L.sum_off;
+  const uint32_t* Q = sq + L.sum_off;
   for (int i = threadIdx.x; i < WC * WR; i += HT_THREADS) {
     const int r = i / WC, c = i - r * WC;
     const int gy = y0 + r, gx = x0 + c;
@@ -253,8 +255,8 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
     if (ix >= L.nx || iy >= L.ny) continue;
     const int o = ly * ys * WC + lx;  // window(ys ly, ys lx): see haar_window_offset
     const int valsum = win[o + na] - win[o + nb] - win[o + nc] + win[o + nd];
-    const uint64_t* q = Q + (int64_t)(y0 + ly * ys) * P + x0 + lx * ys;
-    const double valsq = (double)(int64_t)(q[qa] - q[qb] - q[qc] + q[qd]);
+    const uint32_t* q = Q + (int64_t)(y0 + ly * ys) * P + x0 + lx * ys;
+    const double valsq = (double)(uint32_t)(q[qa] - q[qb] - q[qc] + q[qd]);  // (exact modulo 2^32, see k_haar_rows)
     double nf = (double)((ww - 2) * (wh - 2)) * valsq - (double)valsum * (double)valsum;
     nf = nf > 0. ? __builtin_sqrt(nf) : 1.;
     vnf[p] = 1. / nf;
@@ -729,7 +731,7 @@ void launch_haar_gray(const HaarFrame* frames, int n_frames, int max_pixels, con
 }
 
 void launch_haar_pyramid(const HaarLevel* levels, int n_levels, int max_pixels, int max_rows, int max_cols,
-                         const uint8_t* gray, uint8_t* scaled, int32_t* sum, uint64_t* sq, hipStream_t s) {
+                         const uint8_t* gray, uint8_t* scaled, int32_t* sum, uint32_t* sq, hipStream_t s) {
   k_haar_resize<<<dim3(std::min(512, (max_pixels + 255) / 256), n_levels), 256, 0, s>>>(levels, gray, scaled);
   k_haar_rows<<<dim3(std::min(256, (max_rows + 1 + 3) / 4), n_levels), 256, 0, s>>>(levels, scaled, sum, sq);
   k_haar_cols<<<dim3((max_cols + 255) / 256, n_levels), 256, 0, s>>>(levels, sum, sq);
@@ -739,7 +741,7 @@ int haar_cascade_lds(int max_ystep, int ww, int wh) {
   return haar_win_cols(max_ystep, ww) * haar_win_rows(max_ystep, wh) * 4;
 }
 
-void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint64_t* sq,
+void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint32_t* sq,
                          const HaarWeak* weak, int n_weak, const HaarStage* stages, int n_stages, int ww, int wh,
                          int order_free, int8_t* result, int lds_bytes, hipStream_t s) {
   k_haar_cascade<<<dim3(max_tiles, n_levels), HT_THREADS, lds_bytes, s>>>(levels, sum, sq, weak, n_weak, stages,

@@ -58,7 +58,7 @@ struct HaarStage {
 void launch_haar_gray(const HaarFrame* frames, int n_frames, int max_pixels, const uint8_t* images, uint8_t* gray,
                       hipStream_t s);
 void launch_haar_pyramid(const HaarLevel* levels, int n_levels, int max_pixels, int max_rows, int max_cols,
-                         const uint8_t* gray, uint8_t* scaled, int32_t* sum, uint64_t* sq, hipStream_t s);
+                         const uint8_t* gray, uint8_t* scaled, int32_t* sum, uint32_t* sq, hipStream_t s);
 // a workgroup per 64 x 8 scan positions: max_tiles = the largest level's ceil(nx / 64) * ceil(ny / 8);
 // lds_bytes = haar_cascade_lds(largest ystep of the batch, ww, wh) (dynamic LDS: the integral window)
 #ifndef FFD_HAAR_TILE_Y
@@ -67,7 +67,7 @@ void launch_haar_pyramid(const HaarLevel* levels, int n_levels, int max_pixels, 
 constexpr int HAAR_TILE_X = 64, HAAR_TILE_Y = FFD_HAAR_TILE_Y;
 int haar_cascade_lds(int max_ystep, int ww, int wh);
 // weak: the ystep-1 table, then (at weak + n_weak) the ystep-2 table
-void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint64_t* sq,
+void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint32_t* sq,
                          const HaarWeak* weak, int n_weak, const HaarStage* stages, int n_stages, int ww, int wh,
                          int order_free, int8_t* result, int lds_bytes, hipStream_t s);
 constexpr int haar_window_cols(int ystep, int ww) { return HAAR_TILE_X * ystep + ww; }
