@@ -698,6 +698,8 @@ template <class F> ffd_status guarded(ffd_engine* e, F&& fn) {
   try {
     HIP_CHECK(hipSetDevice(e->device));
     return fn();
+  } catch (const DeviceOom& x) {
+    return fail(e, FFD_ERR_OUT_OF_MEMORY, x.what());
   } catch (const HipError& x) {
     return fail(e, FFD_ERR_DEVICE, x.what());
   } catch (const std::bad_alloc&) {

@@ -31,6 +31,9 @@ using namespace ffd;
 struct HipError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
+struct DeviceOom : HipError {  // hipMalloc found no room: FFD_ERR_OUT_OF_MEMORY, not FFD_ERR_DEVICE
+  using HipError::HipError;
+};
 
 #define HIP_CHECK(expr)                                                                        \
   do {                                                                                         \
@@ -49,7 +52,13 @@ struct DevBuf {
     if (bytes <= n) return p;
     if (p) { (void)hipFree(p); p = nullptr; n = 0; }
     size_t want = std::max<size_t>(bytes, 256);
-    HIP_CHECK(hipMalloc(&p, want));
+    const hipError_t r = hipMalloc(&p, want);
+    if (r == hipErrorOutOfMemory) {
+      (void)hipGetLastError();  // (clear the sticky error)
+      p = nullptr;
+      throw DeviceOom("device allocation of " + std::to_string(want) + " bytes failed (out of memory)");
+    }
+    HIP_CHECK(r);
     n = want;
     return p;
   }
@@ -89,6 +98,7 @@ using namespace ffd;  // internal header: the engine's TUs work in ffd's vocabul
 using ffd_host::DevBuf;
 using ffd_host::Geometry;
 using ffd_host::HipError;
+using ffd_host::DeviceOom;
 using ffd_host::upload;
 
 // Per-stream workspace: a chunk of faces runs its whole pipeline on one stream; consecutive
