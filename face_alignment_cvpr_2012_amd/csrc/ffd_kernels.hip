@@ -1950,12 +1950,11 @@ constexpr int MS_FPW = (MS_FACES + 3) / 4;  // faces per wave
 #define FFD_MS_RA 4
 #endif
 constexpr int MS_RA = FFD_MS_RA;  // serial phase: LDS reads in flight ahead of the adds
-#ifndef FFD_MS_SUM3
-#define FFD_MS_SUM3 1  // serial phase: lanes 3p, 3p + 1, 3p + 2 add face p's x / y / w terms (0: lane p adds all three)
-#endif
-// the x / y / w term planes: with SUM3 MS_LD words apart beyond the tile, so the three lanes of a face read
-// different banks (a plane is 64 x 21 words = 0 mod 64 banks)
-constexpr int MS_TSTRIDE = MS_TILE * MS_LD + (FFD_MS_SUM3 ? MS_LD : 0);
+// serial phase: lanes 3p, 3p + 1, 3p + 2 add face p's x / y / w terms (round 5: 1.93 -> 1.62 ms against one
+// lane adding all three).  Terms as [component][vote][face], MS_LD words per vote, the planes MS_TSTRIDE apart
+// (a plane is 64 x 21 words = 0 mod 64 banks, so the three lanes of a face read different banks).  (Rows per face
+// read four terms at a time with ds_read_b128, as k_meanshift4 does, measured 1.63 -> 2.05 ms here.)
+constexpr int MS_TSTRIDE = MS_TILE * MS_LD + MS_LD;
 #ifndef FFD_MS_DEFAULT
 #define FFD_MS_DEFAULT 0  // 0: chosen per batch (launch_meanshift); 1 k_meanshift, 4 k_meanshift4, 5 k_meanshift5
 #endif
@@ -2024,10 +2023,11 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
                                                    const int32_t* __restrict__ vote_counts,
                                                    float* __restrict__ ms_mean, FaceOut* __restrict__ out,
                                                    const int32_t* __restrict__ order) {
-  __shared__ float tt[3 * MS_TSTRIDE];
+  constexpr int PLANE = MS_TSTRIDE;
+  __shared__ float tt[3 * PLANE];
   float* const tx = tt;
-  float* const ty = tt + MS_TSTRIDE;
-  float* const tw = tt + 2 * MS_TSTRIDE;
+  float* const ty = tt + PLANE;
+  float* const tw = tt + 2 * PLANE;
   __shared__ float s_mx[MS_FACES], s_my[MS_FACES];
   __shared__ int s_cnt[MS_FACES], s_live[MS_FACES], s_chain[MS_FACES];
   __shared__ int64_t s_vb[MS_FACES];
@@ -2102,17 +2102,18 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         const Vote v = vv[i];
         const float fx = (float)v.x, fy = (float)v.y;
         const float w = pass < 0 ? v.w : ms_weight(s_mx[p], s_my[p], fx, fy, v.w, lamda, lam_y);
-        tx[j * MS_LD + p] = fx * w;
-        ty[j * MS_LD + p] = fy * w;
-        tw[j * MS_LD + p] = w;
+        const int at = j * MS_LD + p;
+        tx[at] = fx * w;
+        ty[at] = fy * w;
+        tw[at] = w;
       }
       if (k0 + MS_TILE < maxcnt) load_tile(k0 + MS_TILE);  // in flight during the serial phase
       __syncthreads();
-      if (FFD_MS_SUM3 && tid < 3 * MS_FACES && s_live[sp]) {  // serial phase, in list order, a component per lane
+      if (tid < 3 * MS_FACES && s_live[sp]) {  // serial phase, in list order, a component per lane
         const int lim = min(MS_TILE, s_cnt[sp] - k0);
-        const float* src = tt + se * MS_TSTRIDE + sp;
+        const float* src = tt + se * PLANE + sp;
         int j = 0;
-        for (; j + MS_RA <= lim; j += MS_RA) {
+        for (; j + MS_RA <= lim; j += MS_RA) {  // LDS reads of MS_RA terms ahead of their in-order adds
           float v[MS_RA];
 #pragma unroll
           for (int q = 0; q < MS_RA; q++) v[q] = src[(j + q) * MS_LD];
@@ -2121,37 +2122,12 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         }
         for (; j < lim; j++) acc += src[j * MS_LD];
       }
-      if (!FFD_MS_SUM3 && tid < MS_FACES && s_live[tid]) {  // serial phase, in list order
-        const int lim = min(MS_TILE, s_cnt[tid] - k0);
-        int j = 0;
-        for (; j + MS_RA <= lim; j += MS_RA) {  // LDS reads of MS_RA terms ahead of their in-order adds
-          float vx[MS_RA], vy[MS_RA], vw[MS_RA];
-#pragma unroll
-          for (int q = 0; q < MS_RA; q++) {
-            vx[q] = tx[(j + q) * MS_LD + tid];
-            vy[q] = ty[(j + q) * MS_LD + tid];
-            vw[q] = tw[(j + q) * MS_LD + tid];
-          }
-#pragma unroll
-          for (int q = 0; q < MS_RA; q++) {
-            ax += vx[q];
-            ay += vy[q];
-            aw += vw[q];
-          }
-        }
-        for (; j < lim; j++) {
-          ax += tx[j * MS_LD + tid];
-          ay += ty[j * MS_LD + tid];
-          aw += tw[j * MS_LD + tid];
-        }
-      }
       __syncthreads();
     }
-    if (FFD_MS_SUM3) {  // face tid's sums from lanes 3 tid .. 3 tid + 2 of wave 0
-      ax = __shfl(acc, 3 * tid);
-      ay = __shfl(acc, 3 * tid + 1);
-      aw = __shfl(acc, 3 * tid + 2);
-    }
+    // face tid's sums from lanes 3 tid .. 3 tid + 2 of wave 0
+    ax = __shfl(acc, 3 * tid);
+    ay = __shfl(acc, 3 * tid + 1);
+    aw = __shfl(acc, 3 * tid + 2);
     if (tid < MS_FACES && s_live[tid]) {
       if (aw > 0) { ax /= aw; ay /= aw; }
       if (pass < 0) {
@@ -2191,6 +2167,10 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
 //   sums   lane 3c + e (e = x, y, w) adds component e of chain c's V terms in list order,
 // in program order within the wave (LDS operations of one wave complete in order).  Every running sum
 // is the reference's sequential float sum bit for bit; the terms use ms_weight.
+// The wave's terms as [component][chain][vote] rows (TVP words, an odd multiple of V, so the 64 term lanes of
+// one store hit 64 banks), read four at a time with ds_read_b128 by the sum lanes (round 5: the serial phase
+// issues TV adds + TV / 4 reads per tile instead of TV + TV; C4 MeanShift 8.40 -> 7.65 ms against [vote][chain]
+// float4 terms).
 template <int C, int K>
 __global__ __launch_bounds__(256) void k_meanshift4(const FaceDesc* __restrict__ faces, int n_faces, int tslots,
                                                    int n_parts, float lamda, float lam_y, int max_iter, float stop,
@@ -2199,7 +2179,9 @@ __global__ __launch_bounds__(256) void k_meanshift4(const FaceDesc* __restrict__
                                                    const int32_t* __restrict__ order) {
   constexpr int V = 64 / C, TV = V * K;  // term lanes per chain; votes per chain per tile
   static_assert(3 * C <= 64 && V * C == 64, "chains per wave");
-  __shared__ float4 term[4][TV][C];  // per wave: [vote j][chain c] = (x*w, y*w, w, 0)
+  constexpr int TVP = K % 2 ? TV : TV + V;  // an odd multiple of V: c * TVP + tk is 64 distinct banks
+  static_assert(TVP % 4 == 0, "16-B aligned rows");
+  __shared__ __attribute__((aligned(16))) float term[4][3 * C * TVP];  // per wave: [component e][chain c][vote j]
   __shared__ float s_mean[4][C][2];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t n_chains = (int64_t)n_faces * NPARTS;
@@ -2266,23 +2248,30 @@ __global__ __launch_bounds__(256) void k_meanshift4(const FaceDesc* __restrict__
           t = make_float4(fx * w, fy * w, w, 0.f);
         }
         if (k + TV < lim) v[u] = vp[k + TV];  // the next tile's votes, in flight during the sums
-        term[wv][tk + V * u][tc] = t;
+        float* const row = &term[wv][tc * TVP + tk + V * u];
+        row[0] = t.x;
+        row[C * TVP] = t.y;
+        row[2 * C * TVP] = t.z;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (sum_lane) {
         const int n = min(TV, slim - k0);
-        const float* tp = reinterpret_cast<const float*>(&term[wv][0][sc]) + se;
+        const float* tp = &term[wv][(se * C + sc) * TVP];
         int j = 0;
-        for (; j + 4 <= n; j += 4) {  // LDS reads ahead of their in-order adds
-          const float a0 = tp[(j + 0) * C * 4], a1 = tp[(j + 1) * C * 4], a2 = tp[(j + 2) * C * 4], a3 = tp[(j + 3) * C * 4];
-          acc += a0;
-          acc += a1;
-          acc += a2;
-          acc += a3;
+        for (; j + 8 <= n; j += 8) {  // two 16-B reads ahead of their eight in-order adds
+          const float4 a = *reinterpret_cast<const float4*>(tp + j);
+          const float4 b = *reinterpret_cast<const float4*>(tp + j + 4);
+          acc += a.x; acc += a.y; acc += a.z; acc += a.w;
+          acc += b.x; acc += b.y; acc += b.z; acc += b.w;
         }
-        for (; j < n; j++) acc += tp[j * C * 4];
+        if (j + 4 <= n) {
+          const float4 a = *reinterpret_cast<const float4*>(tp + j);
+          acc += a.x; acc += a.y; acc += a.z; acc += a.w;
+          j += 4;
+        }
+        for (; j < n; j++) acc += tp[j];
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -2738,12 +2727,12 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
     if (FFD_MS_SORT && order) {  // chains sorted by list length, MS_FACES per workgroup
       k_ms_order<<<1, 1024, 0, s>>>(faces, n, n_parts, vote_counts, order);
       const dim3 grid((unsigned)((chains + MS_FACES - 1) / MS_FACES));
-      k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes,
-                                              vote_counts, ms_mean, out, order);
+      k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean,
+                                    out, order);
     } else {
       const dim3 grid((n + MS_FACES - 1) / MS_FACES, NPARTS);
-      k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes,
-                                              vote_counts, ms_mean, out, nullptr);
+      k_meanshift<<<grid, MS_THREADS, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean,
+                                    out, nullptr);
     }
     return;
   }
@@ -2762,12 +2751,14 @@ void launch_meanshift(const FaceDesc* faces, int n, const HpState* state, int ts
   auto launch4 = [&](int C) {
     const int64_t waves = (lists + C - 1) / C;
     const dim3 grid((unsigned)((waves + 3) / 4));
+    decltype(&k_meanshift4<2, FFD_MS_K>) k;
     switch (C) {
-      case 16: k_meanshift4<16, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out, ord); break;
-      case 8: k_meanshift4<8, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out, ord); break;
-      case 4: k_meanshift4<4, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out, ord); break;
-      default: k_meanshift4<2, FFD_MS_K><<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out, ord); break;
+      case 16: k = k_meanshift4<16, FFD_MS_K>; break;
+      case 8: k = k_meanshift4<8, FFD_MS_K>; break;
+      case 4: k = k_meanshift4<4, FFD_MS_K>; break;
+      default: k = k_meanshift4<2, FFD_MS_K>; break;
     }
+    k<<<grid, 256, 0, s>>>(faces, n, tslots, n_parts, lamda, lam_y, max_iter, stop, votes, vote_counts, ms_mean, out, ord);
   };
   int C = 16;
   while (C > 2 && (lists + C - 1) / C < want) C >>= 1;

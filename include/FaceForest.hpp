@@ -798,34 +798,32 @@ template <class S> class Forest {
   }
 
   // Forest<S>::evaluateMT(const S*, S::Leaf**) (Forest.hpp:80-90): leafs[t] = the leaf tree t reaches.
+  // A patch of the grid this thread read last is served from the thread's reference to that (immutable) grid,
+  // with no lock; any other call goes through the cache under its mutex.
   void evaluateMT(const S* sample, Leaf** leafs) const {
-    const size_t T = sh_->list->ids.size();
-    Cache& c = *sh_->cache;
-    std::lock_guard<std::mutex> g(c.mu);
-    const size_t row = grid_row(sample);
-    if (row != npos) {
-      const int32_t* id = &c.grid_ids[row];
-      const std::unique_ptr<Leaf[]>* ch = c.chunk.data();  // (hoisted: the stores below may alias for the compiler)
-      for (size_t t = 0; t < T; t++) {
-        const uint32_t u = (uint32_t)id[t];
-        leafs[t] = &ch[u >> Cache::CH_SHIFT][u & (Cache::CH - 1)];
-      }
+    const Grid* g = local_grid(sample);
+    const size_t row = g ? g->row_of(sample->roi.x, sample->roi.y) : npos;
+    if (row != npos) {  // Leaf* = the tree's array + (ordinal - its first ordinal), one offset per tree
+      const int32_t* id = &g->ids[row];
+      const intptr_t* off = g->off.data();
+      for (size_t t = 0; t < g->T; t++) leafs[t] = reinterpret_cast<Leaf*>(off[t] + (intptr_t)id[t] * (intptr_t)sizeof(Leaf));
       return;
     }
-    std::vector<int32_t> ids(T);
+    const std::vector<int32_t>& trees = sh_->list->ids;
+    std::vector<int32_t> ids(trees.size());
+    std::lock_guard<std::mutex> lk(sh_->cache->mu);
     eval_one(sample, ids.data());
-    for (size_t t = 0; t < T; t++) leafs[t] = leaf_locked(ids[t]);
+    for (size_t t = 0; t < trees.size(); t++) leafs[t] = leaf_of_tree(trees[t], ids[t]);
   }
   // the same with the model's leaf ordinals (ffd_forest_leaves gives their payloads)
   void evaluateMT(const S* sample, int32_t* leafs) const {
-    const size_t T = sh_->list->ids.size();
-    Cache& c = *sh_->cache;
-    std::lock_guard<std::mutex> g(c.mu);
-    const size_t row = grid_row(sample);
+    const Grid* g = local_grid(sample);
+    const size_t row = g ? g->row_of(sample->roi.x, sample->roi.y) : npos;
     if (row != npos) {
-      std::copy(&c.grid_ids[row], &c.grid_ids[row] + T, leafs);
+      std::copy(&g->ids[row], &g->ids[row] + g->T, leafs);
       return;
     }
+    std::lock_guard<std::mutex> lk(sh_->cache->mu);
     eval_one(sample, leafs);
   }
   // the payload of a leaf ordinal (the reference: TreeNode::getLeaf, TreeNode.hpp:61-66)
@@ -836,39 +834,42 @@ template <class S> class Forest {
 
  private:
   static constexpr size_t npos = ~(size_t)0;
+  struct Grid;
   struct Cache {
     std::mutex mu;
-    // leaf payloads by ordinal in chunks of CH (stable addresses; Leaf* = chunk table + arithmetic, no per-leaf
-    // pointer to load) with a filled bit per leaf; a chunk's leaves are filled as grids reach them
-    static constexpr uint32_t CH_SHIFT = 12, CH = 1u << CH_SHIFT;
-    std::vector<std::unique_ptr<Leaf[]>> chunk;
-    std::vector<uint64_t> filled;  // one bit per ordinal
-    std::vector<uint8_t> tree_done;  // by tree id: every leaf of the tree filled
-    Leaf* at(int32_t o) const { return &chunk[(uint32_t)o >> CH_SHIFT][(uint32_t)o & (CH - 1)]; }  // (o filled)
-    bool has(int32_t o) const {
-      const uint32_t u = (uint32_t)o;
-      return (size_t)(u >> 6) < filled.size() && ((filled[u >> 6] >> (u & 63)) & 1u);
-    }
-    Leaf* put(int32_t o, const typename ForestKind<S>::Raw& r) {
-      const uint32_t u = (uint32_t)o, k = u >> CH_SHIFT;
-      if (k >= chunk.size()) {
-        chunk.resize(k + 1);
-        filled.resize((size_t)(k + 1) * (CH / 64), 0);
-      }
-      if (!chunk[k]) chunk[k].reset(new Leaf[CH]);
-      Leaf* l = &chunk[k][u & (CH - 1)];
-      ForestKind<S>::fill(r, *l);
-      filled[u >> 6] |= 1ull << (u & 63);
-      return l;
-    }
-    // the speculative grid evaluation of the last (sample, tree list): patches (x0 + i step, y0 + j step)
-    uint64_t sample = 0;
-    uint64_t list_uid = 0;  // the TreeList the grid was evaluated for
-    std::vector<int32_t> ids;
-    int x0 = 0, y0 = 0, step = 0, nx = 0, ny = 0;
-    std::vector<int32_t> col, row;  // patch x / y -> grid index i / j (-1: off the grid)
-    std::vector<int32_t> grid_ids;  // [(i * ny + j) * T + t]
+    // leaf payloads tree by tree: a tree's leaves are filled together the first time one of them is asked for
+    // (the reference holds every loaded tree's leaves in memory, Forest::load), in one array per tree, so a
+    // Leaf* is the tree's array + arithmetic and stays valid while the cache lives
+    std::vector<std::unique_ptr<Leaf[]>> arr;  // by tree id
+    std::vector<int32_t> first, count;         // by tree id: leaf ordinals [first, first + count); count -1: unknown
+    std::shared_ptr<Grid> grid;  // the last (sample, tree list) evaluated
   };
+  // the speculative grid evaluation of one (sample, tree list): patches (x0 + i step, y0 + j step).  Never changed
+  // once published, so a thread holding a reference reads it without the cache's lock.
+  struct Grid {
+    uint64_t sample = 0;
+    std::vector<int32_t> trees;  // the tree list it was evaluated for
+    size_t T = 0;
+    int ny = 0;
+    std::vector<int32_t> col, row;  // patch x / y -> grid index i / j (-1: off the grid)
+    std::vector<int32_t> ids;       // leaf ordinals [(i * ny + j) * T + t]
+    std::vector<intptr_t> off;      // per tree: its leaf array's address - its first ordinal * sizeof(Leaf)
+    size_t row_of(int x, int y) const {  // by table, no divisions per call
+      const int i = (unsigned)x < col.size() ? col[x] : -1, j = (unsigned)y < row.size() ? row[y] : -1;
+      return i < 0 || j < 0 ? npos : ((size_t)i * ny + j) * T;
+    }
+  };
+  // a thread's last grid: the cache it belongs to (kept alive: the grid's Leaf* point into it), the sample and the
+  // TreeList uid it was validated for
+  struct Local {
+    std::shared_ptr<Cache> cache;
+    uint64_t sample = 0, list_uid = 0;
+    std::shared_ptr<const Grid> grid;
+  };
+  static Local& local() {
+    static thread_local Local l;
+    return l;
+  }
   // the tree list, shared by copies until one of them changes it (a copy per evaluateMT call, as the reference
   // binds the forest by value into every task, then costs a reference count, not a list copy)
   struct TreeList {
@@ -903,12 +904,58 @@ template <class S> class Forest {
     std::string err;
     if (detail::engine_call(e, err, f) != FFD_OK) throw std::invalid_argument(err);
   }
-  Leaf* leaf_locked(int32_t ordinal) const {
+  // tree t's leaf ordinal range (cached); false for a tree id the engine does not have
+  bool tree_range(int32_t t, int32_t& first, int32_t& count) const {
     Cache& c = *sh_->cache;
-    if (ordinal >= 0 && c.has(ordinal)) return c.at(ordinal);
-    typename ForestKind<S>::Raw raw;
-    call(engine_, [&] { return ffd_forest_leaves(engine_, ForestKind<S>::value, &ordinal, 1, &raw); });  // (rejects a bad ordinal)
-    return c.put(ordinal, raw);
+    if (t < 0) return false;
+    if ((size_t)t >= c.count.size()) {
+      c.first.resize((size_t)t + 1, 0);
+      c.count.resize((size_t)t + 1, -1);
+      c.arr.resize((size_t)t + 1);
+    }
+    if (c.count[t] < 0) {
+      std::string err;
+      if (detail::engine_call(engine_, err, [&] {
+            return ffd_forest_tree_leaves(engine_, ForestKind<S>::value, t, &c.first[t], &c.count[t]);
+          }) != FFD_OK) {
+        c.count[t] = -1;
+        return false;
+      }
+    }
+    first = c.first[t];
+    count = c.count[t];
+    return true;
+  }
+  // tree t's leaf array, filled on first use
+  Leaf* tree_leaves(int32_t t) const {
+    Cache& c = *sh_->cache;
+    int32_t first = 0, count = 0;
+    if (!tree_range(t, first, count)) throw std::invalid_argument("Forest: no tree " + std::to_string(t));
+    if (!c.arr[t]) {
+      std::vector<int32_t> ord((size_t)count);
+      for (int32_t i = 0; i < count; i++) ord[i] = first + i;
+      std::vector<typename ForestKind<S>::Raw> raw((size_t)count);
+      if (count) call(engine_, [&] { return ffd_forest_leaves(engine_, ForestKind<S>::value, ord.data(), count, raw.data()); });
+      std::unique_ptr<Leaf[]> a(new Leaf[(size_t)std::max(count, 1)]);
+      for (int32_t i = 0; i < count; i++) ForestKind<S>::fill(raw[i], a[i]);
+      c.arr[t] = std::move(a);
+    }
+    return c.arr[t].get();
+  }
+  Leaf* leaf_of_tree(int32_t t, int32_t ordinal) const {
+    Leaf* a = tree_leaves(t);
+    return a + (ordinal - sh_->cache->first[t]);
+  }
+  // the payload of any leaf ordinal: the tree holding it among this forest's trees, else among the engine's
+  Leaf* leaf_locked(int32_t ordinal) const {
+    int32_t first = 0, count = 0;
+    for (int32_t t : sh_->list->ids)
+      if (tree_range(t, first, count) && ordinal >= first && ordinal - first < count) return leaf_of_tree(t, ordinal);
+    for (int32_t t = 0; tree_range(t, first, count); t++)
+      if (ordinal >= first && ordinal - first < count) return leaf_of_tree(t, ordinal);
+    typename ForestKind<S>::Raw raw;  // (no tree holds it: the engine's error for a bad ordinal)
+    call(engine_, [&] { return ffd_forest_leaves(engine_, ForestKind<S>::value, &ordinal, 1, &raw); });
+    throw std::invalid_argument("Forest: no leaf " + std::to_string(ordinal));
   }
   void eval_one(const S* sample, int32_t* ids) const {
     const int32_t xy[2] = {sample->roi.x, sample->roi.y};
@@ -917,56 +964,49 @@ template <class S> class Forest {
                                     (int32_t)sh_->list->ids.size(), ids);
     });
   }
-  // The offset of the sample patch's leaf row in the grid evaluation, evaluating the grid that contains the patch
-  // first when the cache holds another sample or tree list; npos for a patch off the grid.
-  size_t grid_row(const S* sample) const {
-    Cache& c = *sh_->cache;
+  // The grid of (sample, this tree list), evaluated first when the cache holds another sample or tree list; null
+  // when the patch's grid cannot be made (a patch outside the image or no trees: evaluated alone).
+  const Grid* local_grid(const S* sample) const {
+    Local& l = local();
     const ImageSample& im = *sample->image;
     const TreeList& L = *sh_->list;
+    if (l.grid && l.cache == sh_->cache && l.sample == im.id() && l.list_uid == L.uid) return l.grid.get();
+    Cache& c = *sh_->cache;
+    std::lock_guard<std::mutex> lk(c.mu);
     const std::vector<int32_t>& ids = L.ids;
     const int x = sample->roi.x, y = sample->roi.y, P = 31, T = (int)ids.size();
-    if (c.list_uid != L.uid && c.ids == ids) c.list_uid = L.uid;  // another list with the same trees
-    if (c.sample != im.id() || c.list_uid != L.uid) {
+    if (!c.grid || c.grid->sample != im.id() || c.grid->trees != ids) {
+      if (x < 0 || y < 0 || x + P > im.width() || y + P > im.height() || T == 0) return nullptr;
       const int step = grid_step_ > 0 ? grid_step_ : S::default_step;
-      if (x < 0 || y < 0 || x + P > im.width() || y + P > im.height() || T == 0) return npos;
-      c.sample = 0;
-      c.ids = ids;
-      c.list_uid = L.uid;
-      c.x0 = x % step;
-      c.y0 = y % step;
-      c.step = step;
-      c.nx = (im.width() - P - c.x0) / step + 1;
-      c.ny = (im.height() - P - c.y0) / step + 1;
-      c.col.assign((size_t)im.width(), -1);
-      c.row.assign((size_t)im.height(), -1);
-      for (int k = 0; k < c.nx; k++) c.col[(size_t)(c.x0 + k * step)] = k;
-      for (int k = 0; k < c.ny; k++) c.row[(size_t)(c.y0 + k * step)] = k;
-      c.grid_ids.resize((size_t)c.nx * c.ny * T);
+      // the grid being replaced is rebuilt in place when no thread holds it any more (its storage is warm)
+      if (l.grid == c.grid) l.grid.reset();
+      std::shared_ptr<Grid> g = c.grid && c.grid.use_count() == 1 ? std::move(c.grid) : std::make_shared<Grid>();
+      g->sample = im.id();
+      g->trees = ids;
+      g->T = (size_t)T;
+      const int x0 = x % step, y0 = y % step, nx = (im.width() - P - x0) / step + 1;
+      g->ny = (im.height() - P - y0) / step + 1;
+      g->col.assign((size_t)im.width(), -1);
+      g->row.assign((size_t)im.height(), -1);
+      for (int k = 0; k < nx; k++) g->col[(size_t)(x0 + k * step)] = k;
+      for (int k = 0; k < g->ny; k++) g->row[(size_t)(y0 + k * step)] = k;
+      g->ids.resize((size_t)nx * g->ny * T);
       call(im.engine(), [&] {
-        return ffd_sample_eval_grid(im.handle(), ForestKind<S>::value, c.x0, c.y0, step, c.nx, c.ny, ids.data(), T,
-                                    c.grid_ids.data());
+        return ffd_sample_eval_grid(im.handle(), ForestKind<S>::value, x0, y0, step, nx, g->ny, ids.data(), T,
+                                    g->ids.data());
       });
-      // every leaf payload of the list's trees, the first time a tree is used (the reference holds each loaded
-      // tree's leaves in memory, Forest::load): the grid's leaves need no check, a Leaf* is arithmetic
-      for (int32_t t : ids) {
-        if ((size_t)t < c.tree_done.size() && c.tree_done[t]) continue;
-        int32_t first = 0, count = 0;
-        call(engine_, [&] { return ffd_forest_tree_leaves(engine_, ForestKind<S>::value, t, &first, &count); });
-        std::vector<int32_t> ord((size_t)count);
-        for (int32_t i = 0; i < count; i++) ord[i] = first + i;
-        std::vector<typename ForestKind<S>::Raw> raw((size_t)count);
-        if (count) call(engine_, [&] { return ffd_forest_leaves(engine_, ForestKind<S>::value, ord.data(), count, raw.data()); });
-        for (int32_t i = 0; i < count; i++)
-          if (!c.has(first + i)) c.put(first + i, raw[i]);
-        if ((size_t)t >= c.tree_done.size()) c.tree_done.resize((size_t)t + 1, 0);
-        c.tree_done[t] = 1;
-      }
-      c.sample = im.id();
+      // every leaf payload of the list's trees, the first time a tree is used; a grid leaf's Leaf* is then its
+      // tree's array + (ordinal - the tree's first ordinal), computed per call (no pointer table to write)
+      g->off.resize((size_t)T);
+      for (int t = 0; t < T; t++)
+        g->off[t] = (intptr_t)tree_leaves(ids[t]) - (intptr_t)c.first[ids[t]] * (intptr_t)sizeof(Leaf);
+      c.grid = std::move(g);
     }
-    // grid index of the patch by table (no divisions per call): col[x] = i for x = x0 + i step, else -1
-    const int i = (unsigned)x < c.col.size() ? c.col[x] : -1, j = (unsigned)y < c.row.size() ? c.row[y] : -1;
-    if (i < 0 || j < 0) return npos;
-    return ((size_t)i * c.ny + j) * T;
+    l.cache = sh_->cache;
+    l.sample = im.id();
+    l.list_uid = L.uid;
+    l.grid = c.grid;
+    return l.grid.get();
   }
 };
 
