@@ -213,9 +213,6 @@ __global__ __launch_bounds__(256) void k_haar_cols(const HaarLevel* __restrict__
 #ifndef FFD_HAAR_THREADS
 #define FFD_HAAR_THREADS 256
 #endif
-#ifndef FFD_HAAR_LOCAL
-#define FFD_HAAR_LOCAL 0  // 1: each tile builds a tile-local integral of the scaled image in LDS (no global integral passes)
-#endif
 constexpr int HT_X = 64, HT_Y = FFD_HAAR_TILE_Y, HT_THREADS = FFD_HAAR_THREADS, HT_POS = HT_X * HT_Y;
 #ifndef FFD_HAAR_PASSES
 #define FFD_HAAR_PASSES 5  // survivor-compaction passes over the stages (5: [0,1) [1,2) [2,4) [4,7) [7,n))
@@ -231,8 +228,7 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
                                                              const HaarWeak* __restrict__ weak_tables, int n_weak,
                                                              const HaarStage* __restrict__ stages, int n_stages,
                                                              int ww, int wh, int order_free,
-                                                             int8_t* __restrict__ result,
-                                                             const uint8_t* __restrict__ scaled) {
+                                                             int8_t* __restrict__ result) {
   extern __shared__ __attribute__((aligned(16))) int32_t win[];
   __shared__ double vnf[HT_POS];
   __shared__ uint16_t list[2][HT_POS];
@@ -250,54 +246,6 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
   // setWindow for every position of the tile: normrect (1, 1, ww - 2, wh - 2)
   const int na = haar_window_offset(ys, WC, 1, 1), nb = haar_window_offset(ys, WC, 1, ww - 1);
   const int nc = haar_window_offset(ys, WC, wh - 1, 1), nd = haar_window_offset(ys, WC, wh - 1, ww - 1);
-#if FFD_HAAR_LOCAL
-  // The tile's integral window relative to its origin (x0, y0): window (r, c) = the sum of the scaled pixels
-  // [y0, y0 + r) x [x0, x0 + c).  It differs from the frame integral at (y0 + r, x0 + c) by a term in r alone plus
-  // one in c alone, which every four-corner difference cancels, so each rectangle sum is the same integer.  Built
-  // in two passes over LDS: the exclusive row prefixes (a wave per row, DPP scans), then the column sums (a thread
-  // per column).  First the squared pixels (for the normrect's variance), then the pixels.
-  (void)S;
-  (void)Q;
-  (void)P;
-  const uint8_t* __restrict__ img = scaled + L.img_off;
-  auto build = [&](bool squares) {
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int r = wv; r < WR; r += HT_THREADS / 64) {
-      const int y = y0 + r - 1;
-      uint32_t carry = 0;
-      for (int c0 = 0; c0 < WC; c0 += 64) {
-        const int c = c0 + lane;  // pixel x0 + c, counted in window columns c + 1 ..
-        uint32_t v = (r > 0 && c < WC - 1 && y < L.sh && x0 + c < L.sw) ? (uint32_t)img[(int64_t)y * L.sw + x0 + c] : 0u;
-        if (squares) v *= v;
-        const uint32_t inc = wave_scan_u32(v) + carry;
-        if (c + 1 < WC) win[haar_window_offset(ys, WC, r, c + 1)] = (int32_t)inc;
-        carry = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-      }
-      if (lane == 0) win[haar_window_offset(ys, WC, r, 0)] = 0;
-    }
-    __syncthreads();
-    for (int c = threadIdx.x; c < WC; c += HT_THREADS) {
-      uint32_t acc = 0;
-      for (int r = 1; r < WR; r++) {
-        const int o = haar_window_offset(ys, WC, r, c);
-        acc += (uint32_t)win[o];
-        win[o] = (int32_t)acc;
-      }
-    }
-    __syncthreads();
-  };
-  build(true);
-  for (int p = threadIdx.x; p < HT_POS; p += HT_THREADS) {  // the normrect's sum of squares (exact: < 2^32)
-    const int lx = p & (HT_X - 1), ly = p / HT_X;
-    const int o = ly * ys * WC + lx;
-    vnf[p] = (double)(uint32_t)((uint32_t)win[o + na] - (uint32_t)win[o + nb] - (uint32_t)win[o + nc] + (uint32_t)win[o + nd]);
-  }
-  __syncthreads();
-  build(false);
-  if (threadIdx.x == 0) { n_list[0] = 0; n_list[1] = 0; }
-  __syncthreads();
-#else
-  (void)scaled;
   for (int i = threadIdx.x; i < WC * WR; i += HT_THREADS) {
     const int r = i / WC, c = i - r * WC;
     const int gy = y0 + r, gx = x0 + c;
@@ -306,19 +254,14 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
   if (threadIdx.x == 0) { n_list[0] = 0; n_list[1] = 0; }
   __syncthreads();
   const int qa = P + 1, qb = qa + (ww - 2), qc = (wh - 1) * P + 1, qd = qc + (ww - 2);
-#endif
   for (int p = threadIdx.x; p < HT_POS; p += HT_THREADS) {
     const int lx = p & (HT_X - 1), ly = p / HT_X;
     const int ix = tx * HT_X + lx, iy = ty * HT_Y + ly;
     if (ix >= L.nx || iy >= L.ny) continue;
     const int o = ly * ys * WC + lx;  // window(ys ly, ys lx): see haar_window_offset
     const int valsum = win[o + na] - win[o + nb] - win[o + nc] + win[o + nd];
-#if FFD_HAAR_LOCAL
-    const double valsq = vnf[p];
-#else
     const uint32_t* q = Q + (int64_t)(y0 + ly * ys) * P + x0 + lx * ys;
     const double valsq = (double)(uint32_t)(q[qa] - q[qb] - q[qc] + q[qd]);  // (exact modulo 2^32, see k_haar_rows)
-#endif
     double nf = (double)((ww - 2) * (wh - 2)) * valsq - (double)valsum * (double)valsum;
     nf = nf > 0. ? __builtin_sqrt(nf) : 1.;
     vnf[p] = 1. / nf;
@@ -792,12 +735,9 @@ void launch_haar_gray(const HaarFrame* frames, int n_frames, int max_pixels, con
   k_haar_gray<<<dim3(blocks, n_frames), 256, 0, s>>>(frames, images, gray);
 }
 
-static const uint8_t* g_scaled = nullptr;  // (A/B only: the scaled pyramid of the last launch_haar_pyramid)
 void launch_haar_pyramid(const HaarLevel* levels, int n_levels, int max_pixels, int max_rows, int max_cols,
                          const uint8_t* gray, uint8_t* scaled, int32_t* sum, uint32_t* sq, hipStream_t s) {
   k_haar_resize<<<dim3(std::min(512, (max_pixels + 255) / 256), n_levels), 256, 0, s>>>(levels, gray, scaled);
-  g_scaled = scaled;
-  if (FFD_HAAR_LOCAL) return;  // (the cascade tiles build their own integral windows)
   k_haar_rows<<<dim3(std::min(256, (max_rows + 1 + 3) / 4), n_levels), 256, 0, s>>>(levels, scaled, sum, sq);
   k_haar_cols<<<dim3((max_cols + 255) / 256, n_levels), 256, 0, s>>>(levels, sum, sq);
 }
@@ -810,7 +750,7 @@ void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, c
                          const HaarWeak* weak, int n_weak, const HaarStage* stages, int n_stages, int ww, int wh,
                          int order_free, int8_t* result, int lds_bytes, hipStream_t s) {
   k_haar_cascade<<<dim3(max_tiles, n_levels), HT_THREADS, lds_bytes, s>>>(levels, sum, sq, weak, n_weak, stages,
-                                                                           n_stages, ww, wh, order_free, result, g_scaled);
+                                                                           n_stages, ww, wh, order_free, result);
 }
 
 // The grouping of a frame with more raw detections than a workgroup's LDS holds (the overflow re-run, one frame):
