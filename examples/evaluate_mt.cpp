@@ -97,6 +97,10 @@ int main(int argc, char** argv) {
         fk.setParam(jungle[0].getParam());
         for (int g : tree_args) fk.addTree(jungle.at(g / 20).getTree(g % 20));
       }
+      // $FFD_EVAL_SHARED=1: every thread works on a copy of ONE forest (one cache), each with its own samples, so
+      // the threads replace the cache's grid while others still read the grid they hold
+      if (std::getenv("FFD_EVAL_SHARED") && std::atoi(std::getenv("FFD_EVAL_SHARED")))
+        for (int k = 1; k < nthreads; k++) own[k] = own[0];
       std::vector<uint32_t> crcs(nthreads, 0);
       std::atomic<int> errors{0};
       std::vector<std::thread> th;

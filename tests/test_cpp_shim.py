@@ -148,14 +148,17 @@ def test_shim_evaluate_mt_per_patch_pattern(model_path, fixtures, oracle_mod, tm
 
 
 @pytest.mark.gpu
-def test_shim_evaluate_mt_threads_share_engine(model_path, fixtures, oracle_mod, tmp_path):
-    """Pool threads on one engine with distinct objects (face_utils.cpp:210-216, 267-274 run evaluateMT from a
-    thread pool): 6 threads, each with its own ImageSample and its own Forest (separate caches), walk every patch
-    four times; each thread's leaf CRC equals the oracle's (the header serialises their engine calls)."""
+@pytest.mark.parametrize("shared", [0, 1])
+def test_shim_evaluate_mt_threads_share_engine(model_path, fixtures, oracle_mod, tmp_path, shared):
+    """Pool threads on one engine (face_utils.cpp:210-216, 267-274 run evaluateMT from a thread pool): 6 threads,
+    each with its own ImageSample, walk every patch four times, each with its own Forest (separate caches) or with
+    copies of one Forest (one cache: a thread replaces the cached grid while the others still read the grid they
+    hold without a lock); each thread's leaf CRC equals the oracle's."""
     import zlib
     img, box = fixtures["images"][2], tuple(int(v) for v in fixtures["boxes"][2])
     ref, tr = oracle_mod.analyze_face(img, box, threads=8, trace=True)
-    d = _evaluate_mt(model_path, tr["face"], tr["trees"], tmp_path, env={"FFD_EVAL_THREADS": "6", "FFD_EVAL_REPS": "1"})
+    d = _evaluate_mt(model_path, tr["face"], tr["trees"], tmp_path,
+                     env={"FFD_EVAL_THREADS": "6", "FFD_EVAL_REPS": "1", "FFD_EVAL_SHARED": str(shared)})
     want = zlib.crc32(np.ascontiguousarray(tr["mp_leaves"], np.int32).tobytes())
     assert d["leaf_crc"] == want
     assert d["thread_errors"] == 0 and d["thread_crcs"] == [want] * 6, d
