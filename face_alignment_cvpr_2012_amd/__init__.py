@@ -34,7 +34,7 @@ LANDMARK_NAMES = ("left eye (l)", "left eye (r)", "mouth (l)", "mouth (r)", "mou
 
 
 def library_path():
-    return os.environ.get("FFD_LIBRARY", os.path.join(HERE, "lib", "libffd.so"))
+    return os.environ.get("FFD_LIBRARY") or os.path.join(HERE, "lib", "libffd.so")  # (an empty value: the in-tree one)
 
 
 def default_model_path():
