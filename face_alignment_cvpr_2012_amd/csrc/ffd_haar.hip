@@ -471,7 +471,7 @@ __global__ __launch_bounds__(HC_THREADS) void k_haar_collect(const HaarFrame* __
 
 // Default form of the same scan, spread over (frame, block of HR_THREADS rows) workgroups: the
 // per-frame form above runs one workgroup per frame (64 per group of frames, a quarter of the CUs).
-// k_haar_rowcount walks each row once for its candidate count; k_haar_emit sums the counts of the
+// k_haar_rowcount counts each row's candidates (a wave per row; only a row holding a face is walked); k_haar_emit sums the counts of the
 // frame's earlier rows, scans its own and walks again, writing each candidate at its slot.  Same
 // walk, same candidate order, same cap rule.
 constexpr int HR_THREADS = 256;
@@ -511,10 +511,22 @@ __global__ __launch_bounds__(HR_THREADS) void k_haar_rowcount(const HaarFrame* _
                                                                const HaarLevel* __restrict__ levels,
                                                                const int8_t* __restrict__ result, int pitch,
                                                                int32_t* __restrict__ rowcnt) {
+  // a wave per scan row: the row's results read coalesced, walked (by lane 0) only when it holds a face — most rows
+  // hold none (round 5: a thread per row walking every row, C3 detection 77.1 -> 75.6 ms per 512 frames)
   const HaarFrame f = frames[blockIdx.x];
-  const int r = blockIdx.y * HR_THREADS + threadIdx.x;
-  if (r >= f.rows) return;
-  rowcnt[(int64_t)blockIdx.x * pitch + r] = haar_row_walk(f, levels, result, r, false, 0, 0, nullptr);
+  const int lane = threadIdx.x & 63, r = blockIdx.y * (HR_THREADS / 64) + (threadIdx.x >> 6);
+  if (r >= f.rows) return;  // whole wave
+  int lv = f.level0;
+  while (lv + 1 < f.level1 && levels[lv + 1].row0 <= r) lv++;
+  const HaarLevel& L = levels[lv];
+  const int8_t* row = result + L.res_off + (int64_t)(r - L.row0) * L.nx;
+  bool face = false;
+  for (int c = lane; c < L.nx; c += 64) face |= row[c] > 0;
+  if (__ballot(face) == 0ull) {  // no face in the row: the walk counts nothing
+    if (lane == 0) rowcnt[(int64_t)blockIdx.x * pitch + r] = 0;
+    return;
+  }
+  if (lane == 0) rowcnt[(int64_t)blockIdx.x * pitch + r] = haar_row_walk(f, levels, result, r, false, 0, 0, nullptr);
 }
 
 __global__ __launch_bounds__(HR_THREADS) void k_haar_emit(const HaarFrame* __restrict__ frames,
@@ -818,7 +830,8 @@ void launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows
   k_haar_collect<<<n_frames, HC_THREADS, 0, s>>>(frames, levels, result, cap, cand, n_cand);
 #else
   const int rb = std::max(1, (max_frame_rows + HR_THREADS - 1) / HR_THREADS);
-  if (max_frame_rows > 0) k_haar_rowcount<<<dim3(n_frames, rb), HR_THREADS, 0, s>>>(frames, levels, result, max_frame_rows, rowcnt);
+  const int rb_count = (max_frame_rows + HR_THREADS / 64 - 1) / (HR_THREADS / 64);  // (k_haar_rowcount: a wave per row)
+  if (max_frame_rows > 0) k_haar_rowcount<<<dim3(n_frames, rb_count), HR_THREADS, 0, s>>>(frames, levels, result, max_frame_rows, rowcnt);
   k_haar_emit<<<dim3(n_frames, rb), HR_THREADS, 0, s>>>(frames, levels, result, max_frame_rows, rowcnt, cap, cand, n_cand);
 #endif
   if (cap > HAAR_MAX_CAND) {  // (one frame: the overflow re-run)
