@@ -38,6 +38,7 @@ void ffd_engine::load_cascade(const ffd::ModelFile& m) {
     stages[s].ntrees = sn.as<int32_t>()[s];
     stages[s].thr = st.as<float>()[s] - 1e-5f;  // CascadeClassifier::Data::read THRESHOLD_EPS
     stages[s].n_two = 0;
+    stages[s].n_sh = 0;
   }
   const auto& wf = m.get("haar.weak_feature");
   const auto& wt = m.get("haar.weak_threshold");
@@ -87,6 +88,62 @@ void ffd_engine::load_cascade(const ffd::ModelFile& m) {
   // all leaves are integer multiples of 2^e (e = the smallest leaf's last mantissa bit) and the sum of
   // the largest |leaf| per classifier stays below 2^(53 + e).  A stage that fails the check keeps its
   // order (n_two = 0: every classifier through the 12-corner form, which covers rect 2 empty).
+  // Two rectangles sharing two corners (an edge segment; they then have opposite signs in both rectangles' sums
+  // tl - tr - bl + br): rewritten as HAAR_SHARED records (ffd_haar.hpp).  Corners are LDS offsets, equal offsets
+  // being the same window corner.
+  struct Corner {
+    uint32_t off;
+    int sign;
+  };
+  auto corners = [](const HaarWeak& w, int k, Corner* c) {
+    c[0] = {w.o[2 * k] & 0xFFFFu, +1};
+    c[1] = {w.o[2 * k] >> 16, -1};
+    c[2] = {w.o[2 * k + 1] & 0xFFFFu, -1};
+    c[3] = {w.o[2 * k + 1] >> 16, +1};
+  };
+  auto shared_of = [&](const HaarWeak& w, Corner* s1, Corner* s2) {  // the two shared corners, s1 added by rect 0
+    Corner a[4], b[4];
+    corners(w, 0, a);
+    corners(w, 1, b);
+    for (int i = 0; i < 4; i++)
+      for (int j = i + 1; j < 4; j++)
+        if (a[i].off == a[j].off || b[i].off == b[j].off) return false;  // (a degenerate rectangle)
+    int n = 0;
+    Corner sc[4];
+    for (const Corner& x : a)
+      for (const Corner& y : b)
+        if (x.off == y.off) sc[n++] = x;
+    if (n != 2 || sc[0].sign == sc[1].sign) return false;
+    *s1 = sc[0].sign > 0 ? sc[0] : sc[1];
+    *s2 = sc[0].sign > 0 ? sc[1] : sc[0];
+    return true;
+  };
+  auto shared_corners = [&](int64_t i) {  // both ystep tables share the pattern (same rectangles)
+    Corner s1, s2;
+    return shared_of(weak[i], &s1, &s2) && shared_of(weak[nw + i], &s1, &s2);
+  };
+  auto to_shared = [&](const HaarWeak& w) {
+    Corner s1, s2, a[4], b[4];
+    shared_of(w, &s1, &s2);
+    corners(w, 0, a);
+    corners(w, 1, b);
+    HaarWeak r = w;
+    r.o[0] = s1.off | s2.off << 16;
+    uint32_t x1 = 0, x2 = 0, y1 = 0, y2 = 0;
+    for (const Corner& c : a)  // rect 0 = S1 - S2 - X1 + X2
+      if (c.off != s1.off && c.off != s2.off) (c.sign > 0 ? x2 : x1) = c.off;
+    int sign1 = 0;  // rect 1 adds S1 (+1) or subtracts it (-1): rect 1 = sign1 (E - Y1 + Y2)
+    for (const Corner& c : b)
+      if (c.off == s1.off) sign1 = c.sign;
+    for (const Corner& c : b)
+      if (c.off != s1.off && c.off != s2.off) (c.sign * sign1 > 0 ? y2 : y1) = c.off;
+    r.o[1] = x1 | x2 << 16;
+    r.o[2] = y1 | y2 << 16;
+    r.o[3] = HAAR_SHARED;
+    r.o[4] = r.o[5] = 0;
+    r.w1 = sign1 > 0 ? w.w1 : -w.w1;  // w1 * (float)(-t) == (-w1) * (float)t exactly
+    return r;
+  };
   haar_order_free = 1;
   for (auto& st : stages) {
     int emin = INT32_MAX;
@@ -102,21 +159,26 @@ void ffd_engine::load_cascade(const ffd::ModelFile& m) {
       bound += std::max(std::fabs((double)w.leaf0), std::fabs((double)w.leaf1));
     }
     st.n_two = 0;
+    st.n_sh = 0;
     if (st.ntrees == 0 || emin == INT32_MAX) continue;  // a sum of zeros: exact in any order
     if (!(bound < std::ldexp(1.0, 52 + emin))) {
       haar_order_free = 0;
       continue;
     }
-    std::vector<int> two, three;
-    for (int i = st.first; i < st.first + st.ntrees; i++) (weak[i].w2 == 0.0f ? two : three).push_back(i);
+    // the shared-corner two-rectangle classifiers first, then the other two-rectangle ones, then the rest
+    std::vector<int> sh, two, three;
+    for (int i = st.first; i < st.first + st.ntrees; i++)
+      (weak[i].w2 != 0.0f ? three : shared_corners(i) ? sh : two).push_back(i);
     std::vector<HaarWeak> perm;
     for (int t = 0; t < 2; t++) {
       perm.clear();
+      for (int i : sh) perm.push_back(to_shared(weak[t * nw + i]));
       for (int i : two) perm.push_back(weak[t * nw + i]);
       for (int i : three) perm.push_back(weak[t * nw + i]);
       std::copy(perm.begin(), perm.end(), weak.begin() + t * nw + st.first);
     }
-    st.n_two = (int)two.size();
+    st.n_sh = (int)sh.size();
+    st.n_two = (int)(sh.size() + two.size());
   }
   upload(haar_weak, weak, main_stream());
   upload(haar_stage, stages, main_stream());

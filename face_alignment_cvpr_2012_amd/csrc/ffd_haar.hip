@@ -304,8 +304,15 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
           const int e = st.first + st.ntrees;
           for (int i = st.first + sub; i < e; i += G) {
             const HaarWeak c = weak[i];
-            float ret = c.w0 * (float)rs(c.o[0], c.o[1]) + c.w1 * (float)rs(c.o[2], c.o[3]);
-            if (c.w2 != 0.0f) ret += c.w2 * (float)rs(c.o[4], c.o[5]);  // rect 2 empty: + 0 (see above)
+            float ret;
+            if (c.o[3] == HAAR_SHARED) {  // (ffd_haar.hpp)
+              const int e = w0[c.o[0] & 0xFFFFu] - w0[c.o[0] >> 16];
+              ret = c.w0 * (float)(e - w0[c.o[1] & 0xFFFFu] + w0[c.o[1] >> 16]) +
+                    c.w1 * (float)(e - w0[c.o[2] & 0xFFFFu] + w0[c.o[2] >> 16]);
+            } else {
+              ret = c.w0 * (float)rs(c.o[0], c.o[1]) + c.w1 * (float)rs(c.o[2], c.o[3]);
+              if (c.w2 != 0.0f) ret += c.w2 * (float)rs(c.o[4], c.o[5]);  // rect 2 empty: + 0 (see above)
+            }
             const double v = (double)ret * f;
             acc += (double)(v < (double)c.thr ? c.leaf0 : c.leaf1);
           }
@@ -350,35 +357,44 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
         auto rs = [&](uint32_t ab, uint32_t cd) {  // corner offsets precomputed for this window pitch
           return w0[ab & 0xFFFFu] - w0[ab >> 16] - w0[cd & 0xFFFFu] + w0[cd >> 16];
         };
-        auto value_of = [&](const HaarWeak& c, auto three) {
-          float ret = c.w0 * (float)rs(c.o[0], c.o[1]) + c.w1 * (float)rs(c.o[2], c.o[3]);
-          if constexpr (decltype(three)::value) ret += c.w2 * (float)rs(c.o[4], c.o[5]);
+        // kind: 0 two rectangles, 1 three, 2 two sharing two corners (HAAR_SHARED: six corner reads)
+        auto value_of = [&](const HaarWeak& c, auto kind) {
+          float ret;
+          if constexpr (decltype(kind)::value == 2) {
+            const int e = w0[c.o[0] & 0xFFFFu] - w0[c.o[0] >> 16];
+            ret = c.w0 * (float)(e - w0[c.o[1] & 0xFFFFu] + w0[c.o[1] >> 16]) +
+                  c.w1 * (float)(e - w0[c.o[2] & 0xFFFFu] + w0[c.o[2] >> 16]);
+          } else {
+            ret = c.w0 * (float)rs(c.o[0], c.o[1]) + c.w1 * (float)rs(c.o[2], c.o[3]);
+            if constexpr (decltype(kind)::value == 1) ret += c.w2 * (float)rs(c.o[4], c.o[5]);
+          }
           // HaarEvaluator::operator() (cascadedetect.hpp, 2.4.9) returns double: calc() * varianceNormFactor,
           // compared unrounded with the float threshold in predictOrderedStump
           return (double)ret * f;
         };
-        auto run = [&](int i, int e, auto three) {
-          constexpr int NB = decltype(three)::value ? FFD_HAAR_BATCH3 : FFD_HAAR_BATCH2;
+        auto run = [&](int i, int e, auto kind) {
+          constexpr int NB = decltype(kind)::value == 1 ? FFD_HAAR_BATCH3 : FFD_HAAR_BATCH2;
           for (; i + NB <= e; i += NB) {
             HaarWeak c[NB];
             double v[NB];
 #pragma unroll
             for (int j = 0; j < NB; j++) c[j] = weak[i + j];
 #pragma unroll
-            for (int j = 0; j < NB; j++) v[j] = value_of(c[j], three);
+            for (int j = 0; j < NB; j++) v[j] = value_of(c[j], kind);
 #pragma unroll
             for (int j = 0; j < NB; j++) acc += (double)(v[j] < (double)c[j].thr ? c[j].leaf0 : c[j].leaf1);
           }
           for (; i < e; i++) {
             const HaarWeak c = weak[i];
-            const double v = value_of(c, three);
+            const double v = value_of(c, kind);
             acc += (double)(v < (double)c.thr ? c.leaf0 : c.leaf1);
           }
         };
         // two-rectangle features: rect 2 is empty (w2 = 0), and + 0 * 0 leaves ret unchanged up to the
         // sign of a zero, which no comparison distinguishes
-        run(st.first, st.first + st.n_two, std::false_type{});
-        run(st.first + st.n_two, st.first + st.ntrees, std::true_type{});
+        run(st.first, st.first + st.n_sh, std::integral_constant<int, 2>{});
+        run(st.first + st.n_sh, st.first + st.n_two, std::integral_constant<int, 0>{});
+        run(st.first + st.n_two, st.first + st.ntrees, std::integral_constant<int, 1>{});
         if (acc < (double)st.thr) break;
       }
       const int ix = tx * HT_X + lx, iy = ty * HT_Y + ly;

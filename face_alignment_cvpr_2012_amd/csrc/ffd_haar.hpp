@@ -53,7 +53,13 @@ struct HaarStage {
   int32_t first, ntrees;
   float thr;  // (float)stageThreshold - 1e-5f (CascadeClassifier::Data::read THRESHOLD_EPS)
   int32_t n_two;  // its first n_two classifiers are two-rectangle features (ffd_detect.cpp load_cascade)
+  int32_t n_sh;   // the first n_sh of those share two corners (HAAR_SHARED records)
 };
+// A two-rectangle classifier whose rectangles share two corners (an edge segment): o[0] = S1 | S2 << 16 (the shared
+// corners, S1 the one rect 0 adds), o[1] = X1 | X2 << 16 (rect 0's others, X2 added), o[2] = Y1 | Y2 << 16 (rect 1's,
+// Y2 added), o[3] = HAAR_SHARED; w1 carries rect 1's sign.  rect 0 = E - X1 + X2, rect 1 = E - Y1 + Y2 with
+// E = S1 - S2: the same integers from six corner reads instead of eight.
+constexpr uint32_t HAAR_SHARED = 0xFFFFFFFFu;
 
 void launch_haar_gray(const HaarFrame* frames, int n_frames, int max_pixels, const uint8_t* images, uint8_t* gray,
                       hipStream_t s);
