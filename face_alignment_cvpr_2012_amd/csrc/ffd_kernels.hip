@@ -2007,7 +2007,9 @@ __device__ __forceinline__ float ms_expf_nonpos(float xf) {
 __device__ __forceinline__ float ms_weight(float mx, float my, float x, float y, float w, float lamda, float lam_y) {
   const float dx = mx - x, dy = my - y;
   const float d = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
-  const float q = lam_y > 0.f ? ffd_div_rcp(-d, lamda, lam_y) : -d / lamda;
+  // (ffd_div_rcp_fast: no divergent branch for tiny d, the same weight bits; round 5: C2 MeanShift 1.62 -> 1.59,
+  // C4 7.60 -> 7.47 ms)
+  const float q = lam_y > 0.f ? ffd_div_rcp_fast(-d, lamda, lam_y) : -d / lamda;
   return w * ms_expf_nonpos(q);
 }
 

@@ -175,4 +175,18 @@ FFD_HD float ffd_div_rcp(float a, float b, float y) {
 #endif
 }
 
+/* ffd_div_rcp without its tiny-|a| branch (MeanShift's weights, k_meanshift / k_meanshift4): the same quotient for
+ * |a| > 2^-100; for smaller |a| a quotient of magnitude at most 2^-100 or zero, whose ffd_expf_nonpos is exactly
+ * 1.0f, as the IEEE quotient's is (tests/numerics/check_numerics.c "quot", every such a) — so the weight
+ * w * expf(-d / lamda) is the same bits, with no divergent branch on the GPU. */
+FFD_HD float ffd_div_rcp_fast(float a, float b, float y) {
+#ifdef __cplusplus
+  const float q = a * y;
+  return std::fma(std::fma(-q, b, a), y, q);
+#else
+  const float q = a * y;
+  return fmaf(fmaf(-q, b, a), y, q);
+#endif
+}
+
 #endif /* FFD_NUMERICS_H */

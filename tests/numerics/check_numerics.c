@@ -2,7 +2,9 @@
  * tests/test_numerics.py; plain C, -ffp-contract=off):
  *   div  ffd_div_rcp(a, 10, RN(1/10)) == a / 10 for every finite binary32 a >= 0 (the quotient is
  *        odd in a, so this covers the negative half too);
- *   expf ffd_expf_nonpos(x) == ffd_expf(x) bitwise for every binary32 x in [-110, 0] and the edges.
+ *   expf ffd_expf_nonpos(x) == ffd_expf(x) bitwise for every binary32 x in [-110, 0] and the edges;
+ *   quot ffd_expf_nonpos(ffd_div_rcp_fast(-d, 10, RN(1/10))) == ffd_expf_nonpos(-d / 10) bitwise for every binary32
+ *        d in [0, 2^-100] (above it the two quotients are equal: "div").
  * Work is split over threads; prints "ok" or the first mismatch. */
 #include <math.h>
 #include <pthread.h>
@@ -38,12 +40,23 @@ static void* exp_worker(void* arg) {
   return NULL;
 }
 
+static void* quot_worker(void* arg) {
+  const uint32_t t = (uint32_t)(uintptr_t)arg, hi = u_of(0x1p-100f);
+  const float y = 1.0f / 10.0f;
+  for (uint32_t u = t; u <= hi && !bad; u += NT) {
+    const float a = -f_of(u);
+    if (u_of(ffd_expf_nonpos(ffd_div_rcp_fast(a, 10.0f, y))) != u_of(ffd_expf_nonpos(a / 10.0f))) { bad = 1; bad_bits = u; }
+  }
+  return NULL;
+}
+
 int main(int argc, char** argv) {
-  const int which_div = argc > 1 && strcmp(argv[1], "div") == 0;
+  const int which_div = argc > 1 && strcmp(argv[1], "div") == 0, which_quot = argc > 1 && strcmp(argv[1], "quot") == 0;
   pthread_t th[NT];
-  for (uintptr_t t = 0; t < NT; t++) pthread_create(&th[t], NULL, which_div ? div_worker : exp_worker, (void*)t);
+  for (uintptr_t t = 0; t < NT; t++)
+    pthread_create(&th[t], NULL, which_div ? div_worker : which_quot ? quot_worker : exp_worker, (void*)t);
   for (int t = 0; t < NT; t++) pthread_join(th[t], NULL);
-  if (!which_div) {
+  if (!which_div && !which_quot) {
     const float edge[] = {-INFINITY, -1e30f, -104.0f, nextafterf(-104.0f, -INFINITY), nextafterf(-104.0f, 0.0f), -0.0f};
     for (unsigned i = 0; i < sizeof edge / sizeof edge[0]; i++)
       if (u_of(ffd_expf_nonpos(edge[i])) != u_of(ffd_expf(edge[i]))) { bad = 1; bad_bits = u_of(edge[i]); }

@@ -109,6 +109,12 @@ def test_markstein_division_by_ten_is_ieee_division():
     _run_numerics_check("div")
 
 
+def test_fast_quotient_gives_the_same_weight():
+    """ffd_div_rcp_fast (no tiny-|a| branch; k_meanshift's quotient) gives the same ffd_expf_nonpos as IEEE -d / 10 for
+    every binary32 d in [0, 2^-100]; above it the quotients are equal (the "div" check)."""
+    _run_numerics_check("quot")
+
+
 def test_expf_nonpos_equals_expf():
     """ffd_expf_nonpos == ffd_expf bitwise for every binary32 x in [-110, 0] (and -inf, -1e30)."""
     _run_numerics_check("exp")
