@@ -2004,14 +2004,14 @@ __device__ __forceinline__ float ms_expf_nonpos(float xf) {
   return under ? 0.0f : e;
 }
 
-#ifndef FFD_MS_SQRT
-#define FFD_MS_SQRT 1  // (0: the compiler's sqrt with its input scaling)
-#endif
 // sqrt of s = dx^2 + dy^2 (binary32 dx, dy): the compiler's correctly rounded binary64 sequence (rsq, then the
 // Goldschmidt / Newton steps, in its order) without its input scaling, which applies only below 2^-767 — such an
-// s is 0 or at least 2^-298 — and with s = 0 selected through (the +inf case is unreachable).
+// s is 0 or at least 2^-298 — and with s = 0 selected through (the +inf case is unreachable).  Used by k_meanshift
+// (C2 MeanShift 1.60 -> 1.53 ms); k_meanshift4 keeps the compiler's form (C4 7.54 with it, 7.84 ms without:
+// register allocation).
+template <bool UNSCALED>
 __device__ __forceinline__ double ms_sqrt_sum2(double s) {
-  if (!FFD_MS_SQRT) return __builtin_sqrt(s);
+  if (!UNSCALED) return __builtin_sqrt(s);
   const double y0 = __builtin_amdgcn_rsq(s);
   double g = s * y0, h = y0 * 0.5;
   const double r = __builtin_fma(-h, g, 0.5);
@@ -2023,9 +2023,10 @@ __device__ __forceinline__ double ms_sqrt_sum2(double s) {
   g = __builtin_fma(d, h, g);
   return s == 0.0 ? s : g;
 }
+template <bool UNSCALED = false>
 __device__ __forceinline__ float ms_weight(float mx, float my, float x, float y, float w, float lamda, float lam_y) {
   const float dx = mx - x, dy = my - y;
-  const float d = (float)ms_sqrt_sum2((double)dx * dx + (double)dy * dy);
+  const float d = (float)ms_sqrt_sum2<UNSCALED>((double)dx * dx + (double)dy * dy);
   // (ffd_div_rcp_fast: no divergent branch for tiny d, the same weight bits; round 5: C2 MeanShift 1.62 -> 1.59,
   // C4 7.60 -> 7.47 ms)
   const float q = lam_y > 0.f ? ffd_div_rcp_fast(-d, lamda, lam_y) : -d / lamda;
@@ -2122,7 +2123,7 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
         if (p >= MS_FACES || !s_live[p] || k0 + j >= s_cnt[p]) continue;
         const Vote v = vv[i];
         const float fx = (float)v.x, fy = (float)v.y;
-        const float w = pass < 0 ? v.w : ms_weight(s_mx[p], s_my[p], fx, fy, v.w, lamda, lam_y);
+        const float w = pass < 0 ? v.w : ms_weight<true>(s_mx[p], s_my[p], fx, fy, v.w, lamda, lam_y);
         const int at = j * MS_LD + p;
         tx[at] = fx * w;
         ty[at] = fy * w;
