@@ -15,6 +15,7 @@ anything touches the GPU) and exits with its status.  Rank 0 prints ONE JSON lin
 --dry-run: the launcher and the record gather without a GPU (gloo, synthetic records; tests).
 """
 import argparse
+import glob
 import hashlib
 import json
 import os
@@ -96,6 +97,39 @@ def measured_traffic(stage, faces_per_launch, workload="c2", key="traffic_bytes"
             if pre and name.startswith(pre) and v.get(key):
                 return v[key]
     return None
+
+
+def gather_figure(stage, avg_ms, faces_per_launch, n_cu):
+    """roofline.gather (VERDICT r5 "next" #3): the traversal's record gathers priced at the gather probe's cost, as a
+    fraction of the kernel's measured time.  Gathers per face (wave-level deep-loop gathers x their active lanes) come
+    from the walk statistics tools/walk_locality.py computes on C2 faces with k_traverse's lane mapping
+    (profiles/*/walk_locality.json, newest); the cost per gathered lane is tools/td_probe.hip's 16-B gather with 64
+    distinct 128-B lines per wave-instruction from a 2 MB (L2-resident) table (profiles/r5a/td_probe.json).  1.0 =
+    the kernel's whole time is its gathers' vector-memory data-path time at that rate (the walk-only probe measured
+    TD busy at that level)."""
+    kind = {"ffd_traverse": "ffd", "headpose_traverse": "hp"}.get(stage)
+    if kind is None:
+        return None
+    walk = probe = None
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "walk_locality.json")), reverse=True):
+        walk = json.load(open(path))
+        walk_src = os.path.relpath(path, REPO)
+        break
+    probe_path = os.path.join(REPO, "profiles", "r5a", "td_probe.json")
+    if os.path.exists(probe_path):
+        for line in open(probe_path):
+            r = json.loads(line)
+            if r["table_kb"] == 2048 and r["bytes"] == 16 and r["active"] == 64 and r["lines"] == 64:
+                probe = r
+    if walk is None or probe is None or kind not in walk:
+        return None
+    w = walk[kind]["dfs"]
+    lanes = w["lane_gathers_per_face"] * faces_per_launch
+    gather_ms = lanes / n_cu * probe["ns_per_lane"] / 1e6
+    return {"frac": round(gather_ms / avg_ms, 4), "gather_ms": round(gather_ms, 4), "kernel_ms": round(avg_ms, 4),
+            "lane_gathers_per_launch": int(lanes), "lines_per_instr": round(w["lines_per_instr"], 2),
+            "ns_per_lane": probe["ns_per_lane"], "cus": n_cu, "walk_stats": walk_src,
+            "probe": "profiles/r5a/td_probe.json (16 B, 64 lines, 2 MB table)"}
 
 
 def stage_work(stage, n_faces, W=125, H=125, n_hp=576, n_mp=1024, trees=20):
@@ -716,6 +750,16 @@ def main():
                                   "frac": round(value * b_face / 1e9 / HBM_PEAK_GBS, 4)},
             "stage_ms_per_step": {k: round(v[0] / max(1, args.steps), 3) for k, v in stages.items()},
         }
+        if wl.name == "c2":  # the traversals' gather-path figure beside the HBM one (VERDICT r5 "next" #3)
+            n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+            g = gather_figure(dom, avg_ms, faces_per_launch, n_cu)
+            if g is not None:
+                out["roofline"]["gather"] = g
+            hs = stages.get("headpose_traverse")
+            if hs and hs[1] > 0:
+                gh = gather_figure("headpose_traverse", hs[0] / hs[1], n * args.steps / hs[1], n_cu)
+                if gh is not None:
+                    out["roofline"]["gather_headpose"] = gh
         # the Gabor stage's FP32 fraction beside the HBM figure, per scale
         gab = {}
         for k, (ms_k, nl) in stages.items():

@@ -338,10 +338,12 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
     int max_frame_rows = 0;
     for (const auto& f : frames) max_frame_rows = std::max(max_frame_rows, f.rows);
     e->det_rowcnt.ensure((size_t)nF * std::max(1, max_frame_rows) * 4);
-    launch_haar_group(e->det_frames.as<HaarFrame>(), nF, max_frame_rows, e->det_rowcnt.as<int32_t>(), nL > 0 ? e->det_levels.as<HaarLevel>() : nullptr,
+    const int grc = launch_haar_group(e->det_frames.as<HaarFrame>(), nF, max_frame_rows, e->det_rowcnt.as<int32_t>(), nL > 0 ? e->det_levels.as<HaarLevel>() : nullptr,
                       nL > 0 ? e->det_res.as<int8_t>() : nullptr, cap, e->det_cand.as<int4>(), n_cand,
                       o.min_neighbors, o.widen, e->det_clsrect.as<int4>(), e->det_clssum.as<int>(),
                       e->det_boxes.as<int4>(), n_boxes, cap > HAAR_MAX_CAND ? e->det_label.as<int>() : nullptr, s);
+    if (grc == HAAR_GROUP_HIP_ERROR) throw HipError("detector grouping: a HIP call of the label rounds failed");
+    if (grc == HAAR_GROUP_NO_CONVERGENCE) throw std::runtime_error("detector grouping: label rounds did not converge");
     int4* packed = e->det_packed.as<int4>();
     int32_t* owner = reinterpret_cast<int32_t*>(packed + (size_t)nF * cap);
     launch_haar_pack(nF, cap, e->det_boxes.as<int4>(), n_boxes, packed, owner, s);

@@ -29,6 +29,11 @@ constexpr int MAX_FACE_H = 600;   // scaled faces up to this height stage whole 
 // taller ones band by band (k_gabor_sep<..., TALL>).  MAX_FACE_ROWS keeps every per-face index in 32 bits
 // (leaf lists n_patches x trees < 2^31); a face that tall needs > 50 GB of channel planes: FFD_ERR_OUT_OF_MEMORY
 constexpr int MAX_FACE_ROWS = 1 << 21;
+// Float-integral faces and samples (FaceDesc::fint) keep their CV_32F integrals modulo 2^16 and recover each rectangle
+// half in the window [-2048, 63488) (ffd_kernels.hip rect_mean_fint): exact while every integral value stays below
+// FINT_LIMIT (a half's rounding error is <= 2 columns x 11 row additions x 64 = 1,408 there).  Past it the call is
+// refused (FFD_ERR_UNSUPPORTED): for a 125-wide face that is a box more than 539 times taller than wide.
+constexpr uint64_t FINT_LIMIT = 1ull << 31;
 constexpr uint32_t LEAF_BIT = 0x80000000u;
 
 // Flattened tree node (16 B), breadth-first per tree, children adjacent:

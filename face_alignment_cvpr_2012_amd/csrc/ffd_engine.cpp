@@ -524,6 +524,7 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   w.vote_counts.ensure((size_t)n * NPARTS * 4);
   w.ms_order.ensure((size_t)n * NPARTS * 4);
   w.gabor_redo.ensure((size_t)n * 5 * 4);  // 5 scales
+  w.gabor_fmm.ensure((size_t)n * 5 * 64);  // per-face min / max slots of the decoupled Gabor epilogue
   if (w.gabor_mm.n < (size_t)n * 5 * 64) {  // the banded instances leave their slots zeroed
     w.gabor_mm.ensure((size_t)n * 5 * 64);
     HIP_CHECK(hipMemsetAsync(w.gabor_mm.p, 0, w.gabor_mm.n, st));
@@ -546,7 +547,8 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
     const hipStream_t s2 = cs(4 - nu);
     stage(1 + (4 - nu), s2, [&] {
       launch_gabor(nu, dfd, n, max_h, w.gray.as<uint8_t>(), gabor_coef.as<float>(), w.mag.as<float>(),
-                   w.chan.as<uint16_t>(), w.gabor_redo.as<int>(), gabor_exact, w.gabor_mm.as<uint32_t>(), s2);
+                   w.chan.as<uint16_t>(), w.gabor_redo.as<int>(), gabor_exact, w.gabor_mm.as<uint32_t>(), s2,
+                   gabor_epi_kernel ? w.gabor_fmm.as<uint32_t>() : nullptr);
     });
   }
   {
@@ -614,7 +616,7 @@ void ffd_engine::analyze(const uint8_t* d_images, const std::vector<FaceDesc>& a
       if (f.valid) {
         const int c = f.H > MAX_FACE_H;
         const int64_t pl = std::max(plane_max, (int64_t)(f.H + 1) * PITCH), o = other + face_bytes(f);
-        if (cnt > 0 && (c != cls || o + (int64_t)(nvalid + 1) * NCH * pl * 2 > chunk_bytes)) break;
+        if (nvalid > 0 && (c != cls || o + (int64_t)(nvalid + 1) * NCH * pl * 2 > chunk_bytes)) break;
         cls = c;
         plane_max = pl;
         other = o;
@@ -668,6 +670,10 @@ ffd_status ffd_host::make_desc(const ffd_engine* e, int64_t img_off, int iw, int
     f.reject = FFD_ERR_OUT_OF_MEMORY;
     return FFD_ERR_OUT_OF_MEMORY;
   }
+  if ((uint64_t)255 * g.W * g.H >= FINT_LIMIT) {  // float integrals past 2^31: rect_mean_fint is not exact there
+    f.reject = FFD_ERR_UNSUPPORTED;
+    return FFD_ERR_UNSUPPORTED;
+  }
   f.W = g.W; f.H = g.H; f.scale = g.scale;
   f.fint = (int64_t)255 * g.W * g.H >= (int64_t)1 << 24 ? 1 : 0;  // an integral value may reach 2^24
   f.nhx = g.nhx; f.nhy = g.nhy; f.nmx = g.nmx; f.nmy = g.nmy;
@@ -700,6 +706,8 @@ template <class F> ffd_status guarded(ffd_engine* e, F&& fn) {
     return fn();
   } catch (const DeviceOom& x) {
     return fail(e, FFD_ERR_OUT_OF_MEMORY, x.what());
+  } catch (const Unsupported& x) {
+    return fail(e, FFD_ERR_UNSUPPORTED, x.what());
   } catch (const HipError& x) {
     return fail(e, FFD_ERR_DEVICE, x.what());
   } catch (const std::bad_alloc&) {
@@ -863,6 +871,7 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   if (const char* v = std::getenv("FFD_VOTES_WIDE")) e->force_wide = std::atoi(v) != 0;
   if (const char* v = std::getenv("FFD_CHUNK_BYTES")) e->chunk_bytes = std::max<int64_t>(1, std::atoll(v));
   if (const char* v = std::getenv("FFD_GABOR_EXACT")) e->gabor_exact = std::atoi(v) != 0;
+  if (const char* v = std::getenv("FFD_GABOR_EPI")) e->gabor_epi_kernel = std::atoi(v) != 0;
   if (const char* v = std::getenv("FFD_CHANNEL_STREAMS")) e->channel_streams = std::max(1, std::min(6, std::atoi(v)));
   if (const char* v = std::getenv("FFD_SMALL_BATCH")) e->small_batch = std::max(0, std::atoi(v));
   if (const char* v = std::getenv("FFD_HOST_CHUNK")) e->host_chunk = std::max(1, std::atoi(v));
@@ -1199,6 +1208,7 @@ FaceDesc stage_sample(ffd_engine* e, Workspace& w, const uint32_t* ch, int W, in
             (uint16_t)(v - I[r.y * ow + r.x + x] - I[(r.y + y) * ow + r.x] + I[r.y * ow + r.x]);
       }
   }
+  if (vmax >= FINT_LIMIT) throw Unsupported("integral values of 2^31 or more (rect_mean_fint window)");
   f.fint = vmax >= (1u << 24) ? 1 : 0;  // float-rounded integrals (CV_32F past 2^24): k_walk_fint
   w.chan.ensure(J.size() * 2 + 512);  // slack: traversal windows read past a row
   HIP_CHECK(hipMemcpyAsync(w.chan.p, J.data(), J.size() * 2, hipMemcpyHostToDevice, w.stream));
@@ -1451,7 +1461,7 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* c
                                   int32_t* leaf_ids) {
   if (e && e->detector_only) return no_forests(e);
   return guarded(e, [&]() -> ffd_status {
-    if (!channels || (!patches_xy && n_patches) || (!tree_ids && n_trees) || (!leaf_ids && n_patches * n_trees) ||
+    if (!channels || (!patches_xy && n_patches) || (!tree_ids && n_trees) || (!leaf_ids && (int64_t)n_patches * n_trees) ||
         W < 1 || H < 1 || W > PITCH - 3 || H > MAX_FACE_ROWS || n_patches < 0 || n_trees < 0)
       return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     if (kind != FFD_FOREST_HEADPOSE && kind != FFD_FOREST_FFD) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad forest kind");
@@ -1464,6 +1474,8 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* c
         return fail(e, FFD_ERR_INVALID_ARGUMENT, "patch outside the image sample");
     }
     if (n_patches == 0 || n_trees == 0) return FFD_OK;
+    if ((int64_t)n_patches * n_trees >= ((int64_t)1 << 31))  // k_eval_patches indexes (patch, tree) in int
+      return fail(e, FFD_ERR_UNSUPPORTED, "patches x trees of 2^31 or more");
     const int64_t plane = (int64_t)(H + 1) * PITCH;
     // the device keeps integrals modulo 2^16 (exact for every rectangle the trees read)
     std::vector<uint16_t> narrow((size_t)NCH * plane, 0);
@@ -1475,6 +1487,7 @@ ffd_status ffd_forest_eval_leaves(ffd_engine* e, int32_t kind, const uint32_t* c
           vmax = std::max(vmax, v);
           narrow[(size_t)c * plane + (size_t)y * PITCH + x] = (uint16_t)v;
         }
+    if (vmax >= FINT_LIMIT) return fail(e, FFD_ERR_UNSUPPORTED, "integral values of 2^31 or more (rect_mean_fint window)");
     upload(e->scratch_a, narrow, e->main_stream());
     std::vector<int32_t> pv(patches_xy, patches_xy + 2 * n_patches), tv(tree_ids, tree_ids + n_trees);
     upload(e->scratch_b, pv, e->main_stream());
@@ -1550,7 +1563,9 @@ ffd_status orphaned() {
   return fail(nullptr, FFD_ERR_INVALID_ARGUMENT, "the image sample's engine was destroyed (ffd_engine_destroy ran first)");
 }
 
-bool sample_size_ok(int W, int H) { return W >= 2 && H >= 2 && W <= PITCH - 3 && H <= MAX_FACE_ROWS; }
+bool sample_size_ok(int W, int H) {
+  return W >= 2 && H >= 2 && W <= PITCH - 3 && H <= MAX_FACE_ROWS && (uint64_t)255 * W * H < FINT_LIMIT;
+}
 
 ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, int32_t n_patches, int x0, int y0,
                        int step, int nx, int ny, const int32_t* tree_ids, int32_t n_trees, int32_t* leaf_ids) {
@@ -1567,6 +1582,8 @@ ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, i
     if (nx < 0 || ny < 0 || (nx && ny && (step <= 0 || x0 < 0 || y0 < 0 || x0 + (int64_t)(nx - 1) * step + P > s->W ||
                                           y0 + (int64_t)(ny - 1) * step + P > s->H)))
       return fail(e, FFD_ERR_INVALID_ARGUMENT, "patch grid outside the image sample");
+    if ((int64_t)nx * ny * std::max(n_trees, 1) >= ((int64_t)1 << 31))  // k_sample_eval indexes (patch, tree) in int
+      return fail(e, FFD_ERR_UNSUPPORTED, "patch grid x trees of 2^31 or more");
     n_patches = nx * ny;
   } else {
     for (int p = 0; p < n_patches; p++) {
@@ -1577,6 +1594,7 @@ ffd_status sample_eval(ffd_sample* s, int32_t kind, const int32_t* patches_xy, i
   }
   if (n_patches == 0 || n_trees == 0) return FFD_OK;
   if (!leaf_ids) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
+  if ((int64_t)n_patches * n_trees >= ((int64_t)1 << 31)) return fail(e, FFD_ERR_UNSUPPORTED, "patches x trees of 2^31 or more");
   const bool hp = kind == FFD_FOREST_HEADPOSE;
   // A grid from the origin with the estimators' rule (face_utils.cpp:197-207,255-265) runs as the batch path's
   // traversal of a one-face chunk (k_traverse: LDS windows, tree tops, pair records), which writes the leaves in
@@ -1671,7 +1689,7 @@ ffd_status ffd_sample_create(ffd_engine* e, const uint8_t* gray, int32_t W, int3
   return guarded(e, [&]() -> ffd_status {
     if (!gray || !out || stride < W) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     *out = nullptr;
-    if (!sample_size_ok(W, H)) return fail(e, FFD_ERR_UNSUPPORTED, "image sample size unsupported (2..125 wide, 2 rows or more)");
+    if (!sample_size_ok(W, H)) return fail(e, FFD_ERR_UNSUPPORTED, "image sample size unsupported (2..125 wide, 2 rows or more, 255 W H < 2^31)");
     std::unique_ptr<ffd_sample> s(new ffd_sample);
     s->e = e;
     s->device = e->device;
@@ -1742,7 +1760,7 @@ ffd_status ffd_sample_create_from_channels(ffd_engine* e, const uint32_t* channe
   return guarded(e, [&]() -> ffd_status {
     if (!channels || !out) return fail(e, FFD_ERR_INVALID_ARGUMENT, "bad arguments");
     *out = nullptr;
-    if (!sample_size_ok(W, H)) return fail(e, FFD_ERR_UNSUPPORTED, "image sample size unsupported (2..125 wide, 2 rows or more)");
+    if (!sample_size_ok(W, H)) return fail(e, FFD_ERR_UNSUPPORTED, "image sample size unsupported (2..125 wide, 2 rows or more, 255 W H < 2^31)");
     std::unique_ptr<ffd_sample> s(new ffd_sample);
     s->e = e;
     s->device = e->device;
@@ -1758,6 +1776,7 @@ ffd_status ffd_sample_create_from_channels(ffd_engine* e, const uint32_t* channe
           vmax = std::max(vmax, v);
           J[(size_t)c * s->plane + (size_t)y * PITCH + x] = (uint16_t)v;
         }
+    if (vmax >= FINT_LIMIT) return fail(e, FFD_ERR_UNSUPPORTED, "integral values of 2^31 or more (rect_mean_fint window)");
     s->fint = vmax >= (1u << 24) ? 1 : 0;  // float-rounded integrals (CV_32F past 2^24)
     s->chan.ensure(J.size() * 2 + 512);
     HIP_CHECK(hipMemcpyAsync(s->chan.p, J.data(), J.size() * 2, hipMemcpyHostToDevice, e->main_stream()));

@@ -836,7 +836,7 @@ __global__ __launch_bounds__(HL_THREADS) void k_haar_label_jump(const int32_t* _
   }
 }
 
-void launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows, int32_t* rowcnt,
+int launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows, int32_t* rowcnt,
                        const HaarLevel* levels, const int8_t* result, int cap, int4* cand, int32_t* n_cand,
                        int min_neighbors, int widen, int4* cls_rect, int* cls_sum, int4* boxes, int32_t* n_boxes,
                        int* label_g, hipStream_t s) {
@@ -855,14 +855,18 @@ void launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows
       int* changed = label_g + cap;  // (the label buffer holds cap + 1 ints)
       const int grid = (cap + HL_THREADS - 1) / HL_THREADS;
       k_haar_label_init<<<std::min(grid, 1024), HL_THREADS, 0, s>>>(n_cand, cap, label_g);
+      // min-label rounds until no label changes: at most cap rounds (a label only decreases); a failed HIP call or
+      // running past that bound is reported, never taken as convergence (unconverged labels would group wrongly)
       for (int round = 0;; round++) {
+        if (round > cap) return HAAR_GROUP_NO_CONVERGENCE;
         int h = 0;
-        (void)hipMemsetAsync(changed, 0, sizeof(int), s);
+        if (hipMemsetAsync(changed, 0, sizeof(int), s) != hipSuccess) return HAAR_GROUP_HIP_ERROR;
         k_haar_label_round<<<grid, HL_THREADS, 0, s>>>(cand, n_cand, cap, label_g, changed);
         k_haar_label_jump<<<std::min(grid, 1024), HL_THREADS, 0, s>>>(n_cand, cap, label_g);
-        if (hipMemcpyAsync(&h, changed, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess || !h || round > cap)
-          break;
+        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(&h, changed, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+          return HAAR_GROUP_HIP_ERROR;
+        if (!h) break;
       }
     }
     k_haar_group<true><<<n_frames, HC_THREADS, 0, s>>>(frames, cap, cand, n_cand, min_neighbors, widen, cls_rect, cls_sum,
@@ -871,6 +875,7 @@ void launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows
   else
     k_haar_group<false><<<n_frames, HC_THREADS, 0, s>>>(frames, cap, cand, n_cand, min_neighbors, widen, cls_rect,
                                                       cls_sum, boxes, n_boxes, nullptr);
+  return HAAR_GROUP_OK;
 }
 
 }  // namespace ffd

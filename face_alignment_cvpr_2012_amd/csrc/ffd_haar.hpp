@@ -90,8 +90,10 @@ void launch_haar_pack(int n_frames, int cap, const int4* boxes, const int32_t* n
                       hipStream_t s);
 // candidates (cap per frame) in scan order, then grouped + widened boxes (cap per frame);
 // cls_rect: cap int4 per frame, cls_sum: 5 cap ints per frame (scratch); label_g: cap ints per frame, used when
-// cap > HAAR_MAX_CAND (the component labels do not fit the LDS)
-void launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows, int32_t* rowcnt,
+// cap > HAAR_MAX_CAND (the component labels do not fit the LDS).  Returns HAAR_GROUP_OK, or (the overflow re-run's
+// host-driven label rounds) HAAR_GROUP_HIP_ERROR / HAAR_GROUP_NO_CONVERGENCE.
+enum { HAAR_GROUP_OK = 0, HAAR_GROUP_HIP_ERROR = 1, HAAR_GROUP_NO_CONVERGENCE = 2 };
+int launch_haar_group(const HaarFrame* frames, int n_frames, int max_frame_rows, int32_t* rowcnt,
                        const HaarLevel* levels, const int8_t* result, int cap, int4* cand, int32_t* n_cand, int min_neighbors, int widen, int4* cls_rect, int* cls_sum,
                        int4* boxes, int32_t* n_boxes, int* label_g, hipStream_t s);
 

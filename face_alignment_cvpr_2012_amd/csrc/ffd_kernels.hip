@@ -346,6 +346,33 @@ __device__ __forceinline__ void gabor_normalise_integrate(const FaceDesc& fd, in
   }
 }
 
+// Big-batch instances (EPI = false): the workgroup's min / max bits of its 7 planes, reduced as in
+// gabor_minmax_scale, to out[0..6] (minima) and out[7..13] (maxima); k_gabor_epi normalises and integrates.
+template <int NWV>
+__device__ __forceinline__ void gabor_store_minmax(uint32_t (&mn)[7], uint32_t (&mx)[7], uint32_t* __restrict__ out) {
+  __shared__ uint32_t red[NWV][14];
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 0; o < 7; o++) {
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+      mn[o] = min(mn[o], (uint32_t)__shfl_xor((int)mn[o], sh));
+      mx[o] = max(mx[o], (uint32_t)__shfl_xor((int)mx[o], sh));
+    }
+  }
+  if (ln == 0) {
+#pragma unroll
+    for (int o = 0; o < 7; o++) { red[wv][o] = mn[o]; red[wv][7 + o] = mx[o]; }
+  }
+  __syncthreads();
+  if (threadIdx.x < 14) {
+    const int o = threadIdx.x;
+    uint32_t a = red[0][o];
+    for (int w = 1; w < NWV; w++) a = o < 7 ? min(a, red[w][o]) : max(a, red[w][o]);
+    out[o] = a;
+  }
+}
+
 // running min / max of a plane's magnitudes as their bits (unsigned order == float order for m >= +0).
 // MASK: pixels outside the face (in == false) enter as the neutral elements (all ones / zero), four
 // ALU operations with no select; else a predicated update.  Which form a kernel uses is decided per
@@ -423,7 +450,7 @@ __device__ __forceinline__ bool split_finish(uint32_t (&mn)[7], uint32_t (&mx)[7
 #endif
 constexpr int GB_TX = 64, GB_TY = 32, GB_THREADS = 512;
 
-template <bool EXACT, bool SPLIT>
+template <bool EXACT, bool SPLIT, bool EPI = true>
 __global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restrict__ faces,
                                                        const uint8_t* __restrict__ gray,
                                                        const float4* __restrict__ coef_g,
@@ -539,6 +566,10 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restric
   } else {
     mag_flag<EXACT>(tiny, redo, force);
   }
+  if (!EPI) {  // (split_mm: the batch's per-face min / max slots, k_gabor_epi)
+    gabor_store_minmax<GB_THREADS / 64>(mn, mx, split_mm + ((int64_t)blockIdx.x * 5 + 0) * 16);
+    return;
+  }
   gabor_normalise_integrate<GB_THREADS / 64>(fd, 0, mn, mx, mag, chan);
 }
 
@@ -583,7 +614,7 @@ template <int R> struct GSep {
 // TALL: the instance for faces taller than MAX_FACE_H (box aspect h/w > 4.8), whose padded face does not
 // fit the LDS: each band stages only its GS_BY + 2R rows (4x re-staging at 25x25; such faces are rare).
 // Each instance skips the other's faces.
-template <int W, bool EXACT, bool TALL, bool SPLIT = false>
+template <int W, bool EXACT, bool TALL, bool SPLIT = false, bool EPI = true>
 __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __restrict__ faces,
                                                           const uint8_t* __restrict__ gray,
                                                           const float* __restrict__ coef,
@@ -873,7 +904,65 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
   } else {
     mag_flag<EXACT>(tiny, redo, force);
   }
+  if (!EPI) {  // (split_mm: the batch's per-face min / max slots, k_gabor_epi)
+    gabor_store_minmax<GS_THREADS / 64>(mn, mx, split_mm + ((int64_t)blockIdx.x * 5 + NU) * 16);
+    return;
+  }
   gabor_normalise_integrate<GS_THREADS / 64>(fd, NU, mn, mx, mag, chan);
+}
+
+// The normalise / quantise / integrate epilogue of the big-batch Gabor instances as a kernel of its own: one wave
+// per magnitude plane (7 waves = one scale of one face), the plane's min / max from the compute instance's slot
+// (face_mm: [face][scale][16] = min bits x 7, max bits x 7), the same operations as gabor_minmax_scale /
+// gabor_normalise_integrate (FeatureChannelFactory.hpp:271-286).  The fused epilogue kept each compute workgroup
+// (2 waves per SIMD at 25x25) on its CU through the latency-bound scans over magnitudes read back from the
+// Infinity Cache / HBM; decoupled, the compute kernels run at their occupancy and the scans at this kernel's.
+// Faces taller than MAX_FACE_H keep the fused epilogue of the TALL instances.
+constexpr int GE_THREADS = 448;
+__global__ __launch_bounds__(GE_THREADS) void k_gabor_epi(const FaceDesc* __restrict__ faces, int nu,
+                                                         const uint32_t* __restrict__ face_mm,
+                                                         const float* __restrict__ mag, uint16_t* __restrict__ chan) {
+  const FaceDesc& fd = faces[blockIdx.x];
+  if (!fd.valid || fd.nochan || fd.H > MAX_FACE_H) return;
+  const int o = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t* mm = face_mm + ((int64_t)blockIdx.x * 5 + nu) * 16;
+  const double smin = (double)__uint_as_float(mm[o]), smax = (double)__uint_as_float(mm[7 + o]);
+  const double dmin = 0, dmax = 1;
+  const double scale = (dmax - dmin) * (smax - smin > 2.220446049250313e-16 ? 1. / (smax - smin) : 0);
+  const double shift = dmin - smin * scale;
+  const float sf = (float)scale, hf = (float)shift;
+  const int x0 = 2 * lane, FW = fd.W, FH = fd.H;
+  constexpr int RB = 16;
+  typedef float2 rowbuf[RB];
+  const float* m = mag + fd.mag_off + (int64_t)(nu * 7 + o) * FH * PITCH + x0;
+  uint16_t* out = chan + fd.ch_off + (int64_t)(1 + nu * 7 + o) * fd.plane;
+  for (int x = lane; x <= FW; x += 64) out[x] = 0;  // row 0 of the integral image
+  uint32_t c0 = 0, c1 = 0;
+  float f0 = 0.f, f1 = 0.f;
+  const bool fl = fd.fint != 0;
+  auto load = [&](int y0, rowbuf& mv) {
+#pragma unroll
+    for (int b = 0; b < RB; b++)
+      mv[b] = (y0 + b < FH) ? *reinterpret_cast<const float2*>(&m[(y0 + b) * PITCH]) : make_float2(0.f, 0.f);
+  };
+  auto scan = [&](int y0, const rowbuf& mv) {
+#pragma unroll
+    for (int b = 0; b < RB; b++) {
+      if (y0 + b >= FH) break;
+      const uint32_t q0 = (x0 < FW) ? gabor_quantise(mv[b].x, sf, hf) : 0u;
+      const uint32_t q1 = (x0 + 1 < FW) ? gabor_quantise(mv[b].y, sf, hf) : 0u;
+      reinterpret_cast<uint32_t*>(out + (int64_t)(y0 + b + 1) * PITCH)[lane] = integral_row(fl, q0, q1, c0, c1, f0, f1);
+    }
+  };
+  rowbuf A, B;
+  load(0, A);
+  for (int y0 = 0; y0 < FH; y0 += 2 * RB) {
+    if (y0 + RB < FH) load(y0 + RB, B);
+    scan(y0, A);
+    if (y0 + RB >= FH) break;
+    if (y0 + 2 * RB < FH) load(y0 + 2 * RB, A);
+    scan(y0 + RB, B);
+  }
 }
 
 // --------------------------------------------------------------- traversal --
@@ -931,16 +1020,17 @@ __device__ __forceinline__ int rect_mean_lds(const unsigned char* __restrict__ p
 // Rectangle means of float-integral faces (FaceDesc::fint: the reference's CV_32F integral may round,
 // FeatureChannelFactory.hpp:46-57 with OpenCV's float integral_): evalTest (ImageSample.cpp:48-63) on
 // the rounded integral values, (int)((float)(d - b - c + a) / (float)area).  A rectangle half's mod-2^16
-// combination is recovered in the window [-128, 65407]: its true value is the exact half sum (<= 61,710)
-// plus the rounding errors of at most 11 row additions in each of two columns (each <= 4 below 2^27):
-// |error| <= 88.  Sums may then be negative or exceed 255 area, so the quotient is an IEEE division
-// with truncation, as in the reference.
+// combination is recovered in the window [-2048, 63488): its true value is the exact half sum (<= 61,710)
+// plus the rounding errors of at most 11 row additions in each of two columns, each <= 64 (half an ulp)
+// while the integrals stay below 2^31 (FINT_LIMIT, enforced by the host): |error| <= 1,408, so
+// [-1,408, 63,118] lies inside the window.  Sums may then be negative or exceed 255 area, so the quotient
+// is an IEEE division with truncation, as in the reference.
 __device__ __forceinline__ int rect_mean_fint(const uint16_t* __restrict__ I, int ld, int w, int h) {
   const int h1 = h >> 1;
   const uint32_t a = I[0], b = I[w], c = I[h1 * ld], d = I[h1 * ld + w], e = I[h * ld], f = I[h * ld + w];
   auto half = [](uint32_t v) {
     v &= 0xFFFFu;
-    return (int)v - (v >= 0xFF80u ? 65536 : 0);
+    return (int)v - (v >= 0xF800u ? 65536 : 0);  // [-2048, 63488)
   };
   const int R = half(d - c - b + a) + half(f - e - d + c);
   return (int)((float)R / (float)(w * h));
@@ -1026,6 +1116,18 @@ __host__ __device__ __forceinline__ int trav_top_n(int T, int free_bytes, int to
 }
 
 constexpr int BUF_WORD3 = 0x00020000;  // raw buffer resource word 3 (gfx950: 32-bit data format)
+#ifndef FFD_TRAV_PF_DIST
+#define FFD_TRAV_PF_DIST 0  // k_traverse plane prefetch distance in block iterations (0: off; 1 and 2 measured slower)
+#endif
+#ifndef FFD_TRAV_PROBE_SAMEPLANES
+#define FFD_TRAV_PROBE_SAMEPLANES 0
+#endif
+#ifndef FFD_TRAV_PROBE_WALKONLY
+#define FFD_TRAV_PROBE_WALKONLY 0  // probe builds only: stage one window per workgroup, then walk without staging
+#endif
+#ifndef FFD_TRAV_STAGE_AUX
+#define FFD_TRAV_STAGE_AUX 0  // cache-policy bits of the window staging loads (2: nt, 16: sc1 -- bypass the CU's L1)
+#endif
 
 constexpr int TRAV_BLK_BYTES = 64;  // the block descriptor the stagers hand to the walkers (end of the LDS)
 struct TravArgs {
@@ -1205,9 +1307,16 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
         c += dc + cr;
       }
     }
+#if FFD_TRAV_PROBE_WALKONLY
+    int staged = 0, committed = 0;
+#endif
     auto prefetch = [&](const Blk& B) {
       if (!B.ok) return;
+#if FFD_TRAV_PROBE_SAMEPLANES  // probe builds only: every block stages face 0's planes (always L2 / MALL-warm)
+      const FaceDesc& fd = A.faces[0];
+#else
       const FaceDesc& fd = A.faces[B.f];
+#endif
       // the resource and the block offset must be wave-uniform (SGPRs): read them from the first lane
       const uint64_t base = (uint64_t)(A.chan + fd.ch_off);
       const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)base);
@@ -1232,21 +1341,24 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
           }
         }
       }
+#if FFD_TRAV_PROBE_WALKONLY  // probe: the window is staged once per workgroup (walks read a stale window)
+      if (staged++) return;
+#endif
       if constexpr (ROWS) {
         const int vb = min(sc, NCH - 1) * A.plane * 2 + r_lo * (PITCH * 2) + sq * CB;
 #pragma unroll
         for (int u = 0; u < U; u++) {
           if (u < r_n) {
-            if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, vb + u * (PITCH * 2), base_b, 0);
-            else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, vb + u * (PITCH * 2), base_b, 0);
+            if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, vb + u * (PITCH * 2), base_b, FFD_TRAV_STAGE_AUX);
+            else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, vb + u * (PITCH * 2), base_b, FFD_TRAV_STAGE_AUX);
           }
         }
       } else {
 #pragma unroll
         for (int u = 0; u < U; u++) {
           const int voff = voffs[u];
-          if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, base_b, 0);
-          else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, base_b, 0);
+          if constexpr (CB == 16) st[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, base_b, FFD_TRAV_STAGE_AUX);
+          else st[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, base_b, FFD_TRAV_STAGE_AUX);
         }
       }
     };
@@ -1266,6 +1378,9 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
           }
         }
       }
+#if FFD_TRAV_PROBE_WALKONLY
+      if (committed++) return;
+#endif
       if constexpr (ROWS) {
         unsigned char* db = smem + ((sc * WH + r_lo) * nq + sq) * CB;
 #pragma unroll
@@ -1278,10 +1393,54 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       }
     };
 
+    // Plane prefetch into L2 through the scalar data path (SMEM loads: no TA / TD / vector L1 involved).  The window
+    // staging loads are vector loads, returned in order through the CU's vector-memory pipeline, so one that misses
+    // L2 (a face's planes are first touched by its blocks' windows; the channel kernels wrote them long before)
+    // holds every gather behind it for an HBM round trip.  With every block staging planes already in L2 the
+    // FFD pass took 6.8 instead of 8.6 ms and head pose 3.4 instead of 4.3 (round 6 probe, profiles/r6a).  So each
+    // block iteration, the XCD's stager waves load one 4-byte word of every 128-byte line of the faces whose first
+    // block the XCD reaches FFD_TRAV_PF_DIST iterations later (the XCD's blocks are face-major, `start`..`end`),
+    // the lines of a face dealt evenly over the XCD's nk x NSW stager waves, 14 loads in flight per wave.
+    uint32_t pf_acc = 0;
+    auto plane_prefetch = [&](int it) {
+      if constexpr (FFD_TRAV_PF_DIST > 0) {
+        constexpr int NSW = NS / 64, PFB = 14;
+        const int j = __builtin_amdgcn_readfirstlane(k * NSW + ((tid - NW) >> 6)), NJ = nk * NSW;
+        const int b_lo = it == 0 ? start : start + nk * (it + FFD_TRAV_PF_DIST);
+        const int b_hi = min(end, start + nk * (it + FFD_TRAV_PF_DIST + 1));
+        if (b_lo >= b_hi) return;
+        const int f_lo = it == 0 ? b_lo / A.bpf : (b_lo + A.bpf - 1) / A.bpf;  // faces whose first block is in range
+        const int f_hi = (b_hi + A.bpf - 1) / A.bpf;
+        for (int f = f_lo; f < f_hi; f++) {
+          const FaceDesc& fd = A.faces[f];
+          if (!fd.valid || fd.fint || fd.nochan) continue;
+          const int lpc = (fd.H + 1) * (PITCH * 2 / 128);  // 128-byte lines per channel plane of the face
+          const int T = NCH * lpc, l0 = (int)((int64_t)j * T / NJ), l1 = (int)((int64_t)(j + 1) * T / NJ);
+          if (l0 >= l1) continue;
+          const uint64_t base = (uint64_t)(A.chan + fd.ch_off), cstride = (uint64_t)A.plane * 2;
+          int c = l0 / lpc, o = l0 - c * lpc;
+          for (int l = l0; l < l1; l += PFB) {
+            uint32_t v[PFB];
+#pragma unroll
+            for (int u = 0; u < PFB; u++) {
+              // (past this wave's last line: its last line again, never past the face's planes)
+              const int cc = l + u < l1 ? c : (l1 - 1) / lpc, oo = l + u < l1 ? o : (l1 - 1) - ((l1 - 1) / lpc) * lpc;
+              typedef const __attribute__((address_space(4))) uint32_t* cptr;
+              v[u] = *(cptr)(base + (uint64_t)cc * cstride + (uint64_t)oo * 128);
+              if (++o == lpc) { o = 0; c++; }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < PFB; u++) pf_acc += v[u];
+          }
+        }
+      }
+    };
+
     int lb = start + k;
     Blk cur = block(lb);
     prefetch(cur);
-    for (;;) {
+    for (int it = 0;; it++) {
       __syncthreads();  // the previous block's walks are done with the window
       commit(cur);
       __syncthreads();  // the window holds block `cur` (or the end marker)
@@ -1289,8 +1448,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       lb += nk;
       const Blk nxt = block(lb);
       prefetch(nxt);
+      plane_prefetch(it);
       cur = nxt;
     }
+    if (pf_acc == 0x9E3779B9u && A.n_faces < 0) A.leaf_out[0] = (int32_t)pf_acc;  // (keeps the prefetch loads)
   } else {
     for (;;) {
       __syncthreads();
@@ -1937,6 +2098,7 @@ __global__ __launch_bounds__(64 * VOTES_WG_WAVES) void k_votes_wg(const FaceDesc
 #ifndef FFD_MS_FACES
 #define FFD_MS_FACES 20  // 4096 faces x 10 landmarks = 2048 workgroups = one round of 8 per CU
 #endif
+static_assert(3 * FFD_MS_FACES <= 64, "k_meanshift: lanes 3p..3p+2 of wave 0 add face p (SUM3), so every face must sit in wave 0");
 #ifndef FFD_MS_TILE
 #define FFD_MS_TILE 64
 #endif
@@ -2460,7 +2622,7 @@ int gabor_face_lds(int R, int max_h) {
 }
 
 void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t* gray, const float* coef, float* mag,
-                  uint16_t* chan, int* redo, int force_exact, uint32_t* split_mm, hipStream_t s) {
+                  uint16_t* chan, int* redo, int force_exact, uint32_t* split_mm, hipStream_t s, uint32_t* face_mm) {
   if (n <= 0) return;
   const float* c = coef + GABOR_OFFS[nu];
   // small batches: a face's bands / tiles spread over workgroups (split_mm: n x 5 zeroed 16-word slots)
@@ -2469,6 +2631,7 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t
     return v ? std::atoi(v) : FFD_GABOR_SPLIT_MAX;
   }();
   const bool split = split_mm && n <= split_max && max_h <= MAX_FACE_H;
+  if (split || FFD_GABOR_BAND_ALL) face_mm = nullptr;  // (the banded / band-all instances run the fused epilogue)
   // the fast instance, then the exact one over the faces it flagged (an empty pass in practice)
   int* rd = redo + (int64_t)nu * n;  // one flag array per scale: the scales may run on fork streams
   for (int exact = 0; exact < 2; exact++) {
@@ -2494,7 +2657,11 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t
       continue;
     }
 #define FFD_GABOR_LAUNCH(WV, RV)                                                                              \
-  (exact ? k_gabor_sep<WV, true, false> : k_gabor_sep<WV, false, false>)<<<n, GS_THREADS, gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, \
+  if (face_mm)                                                                                                  \
+    (exact ? k_gabor_sep<WV, true, false, false, false> : k_gabor_sep<WV, false, false, false, false>)<<<n, GS_THREADS, \
+        gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, mag, chan, rd, force_exact, face_mm); \
+  else                                                                                                          \
+    (exact ? k_gabor_sep<WV, true, false> : k_gabor_sep<WV, false, false>)<<<n, GS_THREADS, gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, \
                                                                                                   mag, chan, rd, force_exact, nullptr); \
   if (max_h > MAX_FACE_H || FFD_GABOR_BAND_ALL)                                                                 \
     (exact ? k_gabor_sep<WV, true, true> : k_gabor_sep<WV, false, true>)<<<n, GS_THREADS, (GS_BY + 2 * RV) * ((PITCH + 2 * RV + 3) / 4 * 4), s>>>(faces, gray, c, \
@@ -2505,12 +2672,17 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t
       case 2: FFD_GABOR_LAUNCH(13, 6); break;
       case 1: FFD_GABOR_LAUNCH(9, 4); break;
       default:
-        (exact ? k_gabor7<true, false> : k_gabor7<false, false>)<<<n, GB_THREADS, 0, s>>>(faces, gray, reinterpret_cast<const float4*>(c),
-                                                                          mag, chan, rd, force_exact, nullptr);
+        if (face_mm)
+          (exact ? k_gabor7<true, false, false> : k_gabor7<false, false, false>)<<<n, GB_THREADS, 0, s>>>(
+              faces, gray, reinterpret_cast<const float4*>(c), mag, chan, rd, force_exact, face_mm);
+        else
+          (exact ? k_gabor7<true, false> : k_gabor7<false, false>)<<<n, GB_THREADS, 0, s>>>(faces, gray, reinterpret_cast<const float4*>(c),
+                                                                            mag, chan, rd, force_exact, nullptr);
         break;
     }
 #undef FFD_GABOR_LAUNCH
   }
+  if (face_mm) k_gabor_epi<<<n, GE_THREADS, 0, s>>>(faces, nu, face_mm, mag, chan);  // (not reached when split)
 }
 
 // Exhaustive device check of mag_sqrt against sqrtf (ffd_check_mag_sqrt): the n floats with bits

@@ -381,10 +381,6 @@ struct Vote {  // include/face_utils.hpp:34-42
 };
 
 namespace detail {
-inline ffd_engine*& current_engine() {  // the most recently constructed FaceForest's engine
-  static ffd_engine* e = nullptr;
-  return e;
-}
 // tree directories -> (forest kind, first global tree id) of the engine built from them (Forest<S>::load)
 struct ForestDirs {
   ffd_engine* engine = nullptr;
@@ -392,9 +388,44 @@ struct ForestDirs {
   std::vector<std::string> mp_dirs;
   int mp_ntrees = 20;
 };
-inline ForestDirs& forest_dirs() {
-  static ForestDirs d;
-  return d;
+// The live FaceForests' engines, in construction order.  The reference's ImageSample, MeanShift and Forest::load
+// signatures carry no engine (src/ImageSample.cpp:11-20, include/MeanShift.hpp:41-76, include/Forest.hpp:103-129),
+// so with ONE FaceForest alive they use its engine; with several alive a call that names no engine is ambiguous and
+// fails (default_engine) instead of binding to whichever was constructed last.
+struct Registry {
+  std::mutex mu;
+  std::vector<ForestDirs> live;
+};
+inline Registry& registry() {
+  static Registry r;
+  return r;
+}
+inline void register_engine(const ForestDirs& d) {
+  std::lock_guard<std::mutex> g(registry().mu);
+  registry().live.push_back(d);
+}
+inline void unregister_engine(ffd_engine* e) {
+  std::lock_guard<std::mutex> g(registry().mu);
+  auto& v = registry().live;
+  for (size_t i = 0; i < v.size(); i++)
+    if (v[i].engine == e) {
+      v.erase(v.begin() + (std::ptrdiff_t)i);
+      break;
+    }
+}
+inline size_t live_engines() {
+  std::lock_guard<std::mutex> g(registry().mu);
+  return registry().live.size();
+}
+// The engine a call without one uses: the only live FaceForest's, nullptr when none is alive; throws when more than
+// one is alive (`who` names the call in the message).
+inline ffd_engine* default_engine(const char* who) {
+  std::lock_guard<std::mutex> g(registry().mu);
+  const auto& v = registry().live;
+  if (v.size() > 1)
+    throw std::runtime_error(std::string(who) + ": " + std::to_string(v.size()) +
+                             " FaceForests are alive, so the engine is ambiguous; pass one explicitly");
+  return v.empty() ? nullptr : v[0].engine;
 }
 // Calls into an engine one at a time, with the error text read under the same lock.  The C ABI takes one
 // caller per engine at a time (ffd.h), while the reference's callers evaluate forests and samples from pool
@@ -554,7 +585,7 @@ class ImageSample {
     for (int y = 0; y < rows; y++) std::memcpy(&st_->gray[(size_t)y * cols], gray + (size_t)y * step, (size_t)cols);
     // the channels on the device now, as the reference's constructor computes them; without an engine (a training
     // program that builds ImageSamples before any FaceForest, demo.cpp:86-96) on first use, with the engine current then
-    st_->engine = engine ? engine : detail::current_engine();
+    st_->engine = engine ? engine : detail::default_engine("ImageSample");
     if (st_->engine) st_->create();
   }
   // the 8-bit gray image the channels were extracted from (rows x cols, row pitch cols)
@@ -603,7 +634,7 @@ class ImageSample {
   State* ensure() const {
     std::lock_guard<std::mutex> g(st_->mu);
     if (!st_->h) {
-      if (!st_->engine) st_->engine = detail::current_engine();
+      if (!st_->engine) st_->engine = detail::default_engine("ImageSample");
       if (!st_->engine) throw std::runtime_error("ImageSample: no FaceForest engine");
       st_->create();
     }
@@ -772,24 +803,44 @@ template <class S> class Forest {
   // was converted from the tree directory `path` (FaceForest(FaceForestOptions) records them), its first trees
   // as the reference's loop admits them.  false (with an ERROR line on stderr, as Forest::load_tree) when no
   // engine holds that directory.
-  bool load(std::string path, ForestParam fp, int max_trees = -1) {
+  bool load(std::string path, ForestParam fp, int max_trees = -1) { return load(path, fp, max_trees, nullptr); }
+  // ... from the trees of a given engine (nullptr: the live FaceForest whose options name the directory; with
+  // several such FaceForests alive the call fails instead of picking one)
+  bool load(std::string path, ForestParam fp, int max_trees, ffd_engine* engine) {
     setParam(fp);
     if (max_trees == -1) max_trees = fp.ntrees;
-    const detail::ForestDirs& d = detail::forest_dirs();
     auto same = [](const std::string& a, const std::string& b) {
       char ra[4096], rb[4096];
       return a == b || (realpath(a.c_str(), ra) && realpath(b.c_str(), rb) && std::string(ra) == std::string(rb));
     };
-    int base = -1;
-    if (ForestKind<S>::value == FFD_FOREST_HEADPOSE && !d.hp_dir.empty() && same(path, d.hp_dir)) base = 0;
-    if (ForestKind<S>::value == FFD_FOREST_FFD)
-      for (size_t i = 0; i < d.mp_dirs.size(); i++)
-        if (same(path, d.mp_dirs[i])) base = (int)i * d.mp_ntrees;
-    if (base < 0 || !d.engine) {
+    int base = -1, holders = 0;
+    ffd_engine* eng = nullptr;
+    {
+      std::lock_guard<std::mutex> g(detail::registry().mu);
+      for (const detail::ForestDirs& d : detail::registry().live) {
+        if (engine && d.engine != engine) continue;
+        int b = -1;
+        if (ForestKind<S>::value == FFD_FOREST_HEADPOSE && !d.hp_dir.empty() && same(path, d.hp_dir)) b = 0;
+        if (ForestKind<S>::value == FFD_FOREST_FFD)
+          for (size_t i = 0; i < d.mp_dirs.size(); i++)
+            if (same(path, d.mp_dirs[i])) b = (int)i * d.mp_ntrees;
+        if (b >= 0) {
+          holders++;
+          base = b;
+          eng = d.engine;
+        }
+      }
+    }
+    if (holders > 1) {
+      std::fprintf(stderr, "ERROR: Forest::load: %d FaceForests hold the trees of %s; pass the engine\n", holders,
+                   path.c_str());
+      return false;
+    }
+    if (base < 0 || !eng) {
       std::fprintf(stderr, "ERROR: Forest::load: no engine holds the trees of %s\n", path.c_str());
       return false;
     }
-    engine_ = d.engine;
+    engine_ = eng;
     for (int i = 0; i < fp.ntrees; i++) {
       if (numberOfTrees() > max_trees) continue;
       addTree(base + i);
@@ -1026,7 +1077,17 @@ class MeanShift {
   // the mode before rounding
   static void mode(const std::vector<Vote>& votes, float* mean_xy, int num_iterations = 7, int kernel = 10,
                    float stopping_criteria = 0.05f) {
-    ffd_engine* e = detail::current_engine();
+    mode(votes, mean_xy, num_iterations, kernel, stopping_criteria, detail::default_engine("MeanShift"));
+  }
+  // the same on a given engine (FaceForest::engine()), for a program with several FaceForests alive
+  static void shift(const std::vector<Vote>& votes, Point& result, int num_iterations, int kernel,
+                    float stopping_criteria, ffd_engine* e) {
+    float m[2];
+    mode(votes, m, num_iterations, kernel, stopping_criteria, e);
+    result = Point((int)detail::cv_round_f(m[0]), (int)detail::cv_round_f(m[1]));
+  }
+  static void mode(const std::vector<Vote>& votes, float* mean_xy, int num_iterations, int kernel,
+                   float stopping_criteria, ffd_engine* e) {
     if (!e) throw std::runtime_error("MeanShift: no FaceForest engine");
     std::vector<ffd_vote> v(votes.size());
     for (size_t i = 0; i < votes.size(); i++)
@@ -1147,12 +1208,12 @@ class FaceForest {
       std::fprintf(stderr, "ERROR: (!) Error loading the forests: %s\n", err_.c_str());
     }
     if (engine_) {
-      detail::current_engine() = engine_;
-      detail::ForestDirs& fd = detail::forest_dirs();
+      detail::ForestDirs fd;
       fd.engine = engine_;
       fd.hp_dir = options_.hp_forest_param.tree_path;
       fd.mp_dirs = options_.mp_forest_paths;
       if (options_.mp_forest_param.ntrees > 0) fd.mp_ntrees = options_.mp_forest_param.ntrees;
+      detail::register_engine(fd);
     }
     fd_option_ = option.fd_option;
   }
@@ -1162,8 +1223,7 @@ class FaceForest {
     o.engine_ = nullptr;
   }
   virtual ~FaceForest() {
-    if (engine_ && detail::current_engine() == engine_) detail::current_engine() = nullptr;
-    if (engine_ && detail::forest_dirs().engine == engine_) detail::forest_dirs() = detail::ForestDirs();
+    if (engine_) detail::unregister_engine(engine_);
     ffd_engine_destroy(engine_);
   }
 
