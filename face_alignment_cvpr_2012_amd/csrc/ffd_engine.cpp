@@ -524,7 +524,6 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   w.vote_counts.ensure((size_t)n * NPARTS * 4);
   w.ms_order.ensure((size_t)n * NPARTS * 4);
   w.gabor_redo.ensure((size_t)n * 5 * 4);  // 5 scales
-  w.gabor_fmm.ensure((size_t)n * 5 * 64);  // per-face min / max slots of the decoupled Gabor epilogue
   if (w.gabor_mm.n < (size_t)n * 5 * 64) {  // the banded instances leave their slots zeroed
     w.gabor_mm.ensure((size_t)n * 5 * 64);
     HIP_CHECK(hipMemsetAsync(w.gabor_mm.p, 0, w.gabor_mm.n, st));
@@ -547,8 +546,7 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
     const hipStream_t s2 = cs(4 - nu);
     stage(1 + (4 - nu), s2, [&] {
       launch_gabor(nu, dfd, n, max_h, w.gray.as<uint8_t>(), gabor_coef.as<float>(), w.mag.as<float>(),
-                   w.chan.as<uint16_t>(), w.gabor_redo.as<int>(), gabor_exact, w.gabor_mm.as<uint32_t>(), s2,
-                   gabor_epi_kernel ? w.gabor_fmm.as<uint32_t>() : nullptr);
+                   w.chan.as<uint16_t>(), w.gabor_redo.as<int>(), gabor_exact, w.gabor_mm.as<uint32_t>(), s2);
     });
   }
   {
@@ -871,7 +869,6 @@ ffd_status ffd_engine_create(const ffd_engine_desc* d, ffd_engine** out) {
   if (const char* v = std::getenv("FFD_VOTES_WIDE")) e->force_wide = std::atoi(v) != 0;
   if (const char* v = std::getenv("FFD_CHUNK_BYTES")) e->chunk_bytes = std::max<int64_t>(1, std::atoll(v));
   if (const char* v = std::getenv("FFD_GABOR_EXACT")) e->gabor_exact = std::atoi(v) != 0;
-  if (const char* v = std::getenv("FFD_GABOR_EPI")) e->gabor_epi_kernel = std::atoi(v) != 0;
   if (const char* v = std::getenv("FFD_CHANNEL_STREAMS")) e->channel_streams = std::max(1, std::min(6, std::atoi(v)));
   if (const char* v = std::getenv("FFD_SMALL_BATCH")) e->small_batch = std::max(0, std::atoi(v));
   if (const char* v = std::getenv("FFD_HOST_CHUNK")) e->host_chunk = std::max(1, std::atoi(v));

@@ -120,7 +120,6 @@ struct Workspace {
   DevBuf gabor_redo;  // per scale and face: the fast Gabor instance flags faces for the exact one
   DevBuf ms_order;    // MeanShift chains sorted by list length (k_ms_order)
   DevBuf gabor_mm;    // per face and scale: the banded Gabor instances' 16-word slots (zero between launches)
-  DevBuf gabor_fmm;   // per face and scale: min / max bits of the big-batch instances for k_gabor_epi
   std::vector<FaceDesc> h_fds;  // host staging, reused only after `done`
   std::vector<FaceDesc> desc;   // descriptors of the chunk last run here (ffd_get_trace)
   int first = 0, count = 0;
@@ -153,7 +152,6 @@ struct ffd_engine {
   bool detector_only = false;  // ffd_detector_create: a Haar cascade and no forests
   int n_streams = 1;
   int gabor_exact = 0;      // FFD_GABOR_EXACT=1: every face through the exact (sqrtf) Gabor instance (tests)
-  int gabor_epi_kernel = 1; // FFD_GABOR_EPI=0: big batches keep the epilogue fused into the Gabor compute workgroups
   int channel_streams = 1;  // streams the channel stage is spread over (FFD_CHANNEL_STREAMS; 2-4 measured no gain)
   int host_chunk = 1024;    // faces per upload chunk of the host-buffer API (FFD_HOST_CHUNK)
   hipStream_t copy_stream = nullptr;  // H2D of the host-buffer API's images

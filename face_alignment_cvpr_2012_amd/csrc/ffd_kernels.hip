@@ -346,33 +346,6 @@ __device__ __forceinline__ void gabor_normalise_integrate(const FaceDesc& fd, in
   }
 }
 
-// Big-batch instances (EPI = false): the workgroup's min / max bits of its 7 planes, reduced as in
-// gabor_minmax_scale, to out[0..6] (minima) and out[7..13] (maxima); k_gabor_epi normalises and integrates.
-template <int NWV>
-__device__ __forceinline__ void gabor_store_minmax(uint32_t (&mn)[7], uint32_t (&mx)[7], uint32_t* __restrict__ out) {
-  __shared__ uint32_t red[NWV][14];
-  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 0; o < 7; o++) {
-#pragma unroll
-    for (int sh = 32; sh >= 1; sh >>= 1) {
-      mn[o] = min(mn[o], (uint32_t)__shfl_xor((int)mn[o], sh));
-      mx[o] = max(mx[o], (uint32_t)__shfl_xor((int)mx[o], sh));
-    }
-  }
-  if (ln == 0) {
-#pragma unroll
-    for (int o = 0; o < 7; o++) { red[wv][o] = mn[o]; red[wv][7 + o] = mx[o]; }
-  }
-  __syncthreads();
-  if (threadIdx.x < 14) {
-    const int o = threadIdx.x;
-    uint32_t a = red[0][o];
-    for (int w = 1; w < NWV; w++) a = o < 7 ? min(a, red[w][o]) : max(a, red[w][o]);
-    out[o] = a;
-  }
-}
-
 // running min / max of a plane's magnitudes as their bits (unsigned order == float order for m >= +0).
 // MASK: pixels outside the face (in == false) enter as the neutral elements (all ones / zero), four
 // ALU operations with no select; else a predicated update.  Which form a kernel uses is decided per
@@ -450,7 +423,7 @@ __device__ __forceinline__ bool split_finish(uint32_t (&mn)[7], uint32_t (&mx)[7
 #endif
 constexpr int GB_TX = 64, GB_TY = 32, GB_THREADS = 512;
 
-template <bool EXACT, bool SPLIT, bool EPI = true>
+template <bool EXACT, bool SPLIT>
 __global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restrict__ faces,
                                                        const uint8_t* __restrict__ gray,
                                                        const float4* __restrict__ coef_g,
@@ -566,10 +539,6 @@ __global__ __launch_bounds__(GB_THREADS) void k_gabor7(const FaceDesc* __restric
   } else {
     mag_flag<EXACT>(tiny, redo, force);
   }
-  if (!EPI) {  // (split_mm: the batch's per-face min / max slots, k_gabor_epi)
-    gabor_store_minmax<GB_THREADS / 64>(mn, mx, split_mm + ((int64_t)blockIdx.x * 5 + 0) * 16);
-    return;
-  }
   gabor_normalise_integrate<GB_THREADS / 64>(fd, 0, mn, mx, mag, chan);
 }
 
@@ -614,7 +583,7 @@ template <int R> struct GSep {
 // TALL: the instance for faces taller than MAX_FACE_H (box aspect h/w > 4.8), whose padded face does not
 // fit the LDS: each band stages only its GS_BY + 2R rows (4x re-staging at 25x25; such faces are rare).
 // Each instance skips the other's faces.
-template <int W, bool EXACT, bool TALL, bool SPLIT = false, bool EPI = true>
+template <int W, bool EXACT, bool TALL, bool SPLIT = false>
 __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __restrict__ faces,
                                                           const uint8_t* __restrict__ gray,
                                                           const float* __restrict__ coef,
@@ -904,65 +873,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
   } else {
     mag_flag<EXACT>(tiny, redo, force);
   }
-  if (!EPI) {  // (split_mm: the batch's per-face min / max slots, k_gabor_epi)
-    gabor_store_minmax<GS_THREADS / 64>(mn, mx, split_mm + ((int64_t)blockIdx.x * 5 + NU) * 16);
-    return;
-  }
   gabor_normalise_integrate<GS_THREADS / 64>(fd, NU, mn, mx, mag, chan);
-}
-
-// The normalise / quantise / integrate epilogue of the big-batch Gabor instances as a kernel of its own: one wave
-// per magnitude plane (7 waves = one scale of one face), the plane's min / max from the compute instance's slot
-// (face_mm: [face][scale][16] = min bits x 7, max bits x 7), the same operations as gabor_minmax_scale /
-// gabor_normalise_integrate (FeatureChannelFactory.hpp:271-286).  The fused epilogue kept each compute workgroup
-// (2 waves per SIMD at 25x25) on its CU through the latency-bound scans over magnitudes read back from the
-// Infinity Cache / HBM; decoupled, the compute kernels run at their occupancy and the scans at this kernel's.
-// Faces taller than MAX_FACE_H keep the fused epilogue of the TALL instances.
-constexpr int GE_THREADS = 448;
-__global__ __launch_bounds__(GE_THREADS) void k_gabor_epi(const FaceDesc* __restrict__ faces, int nu,
-                                                         const uint32_t* __restrict__ face_mm,
-                                                         const float* __restrict__ mag, uint16_t* __restrict__ chan) {
-  const FaceDesc& fd = faces[blockIdx.x];
-  if (!fd.valid || fd.nochan || fd.H > MAX_FACE_H) return;
-  const int o = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t* mm = face_mm + ((int64_t)blockIdx.x * 5 + nu) * 16;
-  const double smin = (double)__uint_as_float(mm[o]), smax = (double)__uint_as_float(mm[7 + o]);
-  const double dmin = 0, dmax = 1;
-  const double scale = (dmax - dmin) * (smax - smin > 2.220446049250313e-16 ? 1. / (smax - smin) : 0);
-  const double shift = dmin - smin * scale;
-  const float sf = (float)scale, hf = (float)shift;
-  const int x0 = 2 * lane, FW = fd.W, FH = fd.H;
-  constexpr int RB = 16;
-  typedef float2 rowbuf[RB];
-  const float* m = mag + fd.mag_off + (int64_t)(nu * 7 + o) * FH * PITCH + x0;
-  uint16_t* out = chan + fd.ch_off + (int64_t)(1 + nu * 7 + o) * fd.plane;
-  for (int x = lane; x <= FW; x += 64) out[x] = 0;  // row 0 of the integral image
-  uint32_t c0 = 0, c1 = 0;
-  float f0 = 0.f, f1 = 0.f;
-  const bool fl = fd.fint != 0;
-  auto load = [&](int y0, rowbuf& mv) {
-#pragma unroll
-    for (int b = 0; b < RB; b++)
-      mv[b] = (y0 + b < FH) ? *reinterpret_cast<const float2*>(&m[(y0 + b) * PITCH]) : make_float2(0.f, 0.f);
-  };
-  auto scan = [&](int y0, const rowbuf& mv) {
-#pragma unroll
-    for (int b = 0; b < RB; b++) {
-      if (y0 + b >= FH) break;
-      const uint32_t q0 = (x0 < FW) ? gabor_quantise(mv[b].x, sf, hf) : 0u;
-      const uint32_t q1 = (x0 + 1 < FW) ? gabor_quantise(mv[b].y, sf, hf) : 0u;
-      reinterpret_cast<uint32_t*>(out + (int64_t)(y0 + b + 1) * PITCH)[lane] = integral_row(fl, q0, q1, c0, c1, f0, f1);
-    }
-  };
-  rowbuf A, B;
-  load(0, A);
-  for (int y0 = 0; y0 < FH; y0 += 2 * RB) {
-    if (y0 + RB < FH) load(y0 + RB, B);
-    scan(y0, A);
-    if (y0 + RB >= FH) break;
-    if (y0 + 2 * RB < FH) load(y0 + 2 * RB, A);
-    scan(y0 + RB, B);
-  }
 }
 
 // --------------------------------------------------------------- traversal --
@@ -1116,8 +1027,17 @@ __host__ __device__ __forceinline__ int trav_top_n(int T, int free_bytes, int to
 }
 
 constexpr int BUF_WORD3 = 0x00020000;  // raw buffer resource word 3 (gfx950: 32-bit data format)
-#ifndef FFD_TRAV_PF_DIST
-#define FFD_TRAV_PF_DIST 0  // k_traverse plane prefetch distance in block iterations (0: off; 1 and 2 measured slower)
+#ifndef FFD_TRAV_TOUCH
+#define FFD_TRAV_TOUCH 1  // k_traverse: touch the planes of the faces whose first block is this many iterations ahead (0: off)
+#endif
+#ifndef FFD_TRAV_TOUCH_SECT
+#define FFD_TRAV_TOUCH_SECT 1  // words touched per 128-byte line (1: one; 2: one per 64-byte half)
+#endif
+#ifndef FFD_TRAV_TOUCH_HP
+#define FFD_TRAV_TOUCH_HP 1  // 0: the head-pose pass does not touch
+#endif
+#ifndef FFD_TRAV_TOUCH_FIRST
+#define FFD_TRAV_TOUCH_FIRST 0  // 1: the touches are issued before the next window's staging loads
 #endif
 #ifndef FFD_TRAV_PROBE_SAMEPLANES
 #define FFD_TRAV_PROBE_SAMEPLANES 0
@@ -1164,9 +1084,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   const int total = NCH * WH * nq;  // chunks per window (host guarantees <= NS * U)
   uint4* top_rec = reinterpret_cast<uint4*>(smem + trav_window_bytes(WW, WH, GX * step));  // [t][TOPN] heap-ordered pairs
   // XCD-contiguous, face-major block range of this workgroup's XCD; workgroups of one XCD stride it
-  const int N = A.n_faces * A.bpf, xcd = blockIdx.x & 7, k = blockIdx.x >> 3, nk = gridDim.x >> 3;
+  const int N = A.n_faces * A.bpf, xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
   const int q8 = N >> 3, r8 = N & 7;
   const int start = xcd * q8 + min(xcd, r8), end = start + q8 + (xcd < r8 ? 1 : 0);
+  const int nk = gridDim.x >> 3;
 
   struct Blk {
     int f, xi0, yi0, px0, py0, nx, ny, T;
@@ -1393,45 +1314,30 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       }
     };
 
-    // Plane prefetch into L2 through the scalar data path (SMEM loads: no TA / TD / vector L1 involved).  The window
-    // staging loads are vector loads, returned in order through the CU's vector-memory pipeline, so one that misses
-    // L2 (a face's planes are first touched by its blocks' windows; the channel kernels wrote them long before)
-    // holds every gather behind it for an HBM round trip.  With every block staging planes already in L2 the
-    // FFD pass took 6.8 instead of 8.6 ms and head pose 3.4 instead of 4.3 (round 6 probe, profiles/r6a).  So each
-    // block iteration, the XCD's stager waves load one 4-byte word of every 128-byte line of the faces whose first
-    // block the XCD reaches FFD_TRAV_PF_DIST iterations later (the XCD's blocks are face-major, `start`..`end`),
-    // the lines of a face dealt evenly over the XCD's nk x NSW stager waves, 14 loads in flight per wave.
-    uint32_t pf_acc = 0;
-    auto plane_prefetch = [&](int it) {
-      if constexpr (FFD_TRAV_PF_DIST > 0) {
-        constexpr int NSW = NS / 64, PFB = 14;
-        const int j = __builtin_amdgcn_readfirstlane(k * NSW + ((tid - NW) >> 6)), NJ = nk * NSW;
-        const int b_lo = it == 0 ? start : start + nk * (it + FFD_TRAV_PF_DIST);
-        const int b_hi = min(end, start + nk * (it + FFD_TRAV_PF_DIST + 1));
+    // Plane touches (FFD_TRAV_TOUCH): a face's planes are first read by its blocks' window staging (the channel kernels
+    // wrote them long before, so they come from HBM), and every window of an iteration that overlaps a line in flight
+    // waits for it.  So each block iteration the XCD's stager lanes load one word of every 128-byte line of the faces
+    // whose first block the XCD reaches FFD_TRAV_TOUCH iterations later (the XCD's blocks are face-major), each line
+    // once over the XCD's nk x NS lanes (<= 2 loads per lane per iteration); the words are consumed after the next
+    // commit, whose wait for the staging loads covers them.  (Round-6 probes, DESIGN.md §5: the same lines fetched
+    // through the scalar path with the stager waves waiting for them, or by a prefetching workgroup per XCD, were slower.)
+    uint32_t pf_acc = 0, tv0 = 0, tv1 = 0;
+    auto touch = [&](int it) {
+      if constexpr (FFD_TRAV_TOUCH > 0 && (FFD_TRAV_TOUCH_HP || !HP)) {
+        const int b_lo = start + nk * (it + FFD_TRAV_TOUCH), b_hi = min(end, b_lo + nk);
         if (b_lo >= b_hi) return;
-        const int f_lo = it == 0 ? b_lo / A.bpf : (b_lo + A.bpf - 1) / A.bpf;  // faces whose first block is in range
-        const int f_hi = (b_hi + A.bpf - 1) / A.bpf;
+        const int f_lo = (b_lo + A.bpf - 1) / A.bpf, f_hi = min((b_hi + A.bpf - 1) / A.bpf, f_lo + 2);
+        const int j = k * NS + (tid - NW);  // (the XCD has nk x NS stager lanes; lines past them are not touched)
         for (int f = f_lo; f < f_hi; f++) {
           const FaceDesc& fd = A.faces[f];
           if (!fd.valid || fd.fint || fd.nochan) continue;
-          const int lpc = (fd.H + 1) * (PITCH * 2 / 128);  // 128-byte lines per channel plane of the face
-          const int T = NCH * lpc, l0 = (int)((int64_t)j * T / NJ), l1 = (int)((int64_t)(j + 1) * T / NJ);
-          if (l0 >= l1) continue;
-          const uint64_t base = (uint64_t)(A.chan + fd.ch_off), cstride = (uint64_t)A.plane * 2;
-          int c = l0 / lpc, o = l0 - c * lpc;
-          for (int l = l0; l < l1; l += PFB) {
-            uint32_t v[PFB];
-#pragma unroll
-            for (int u = 0; u < PFB; u++) {
-              // (past this wave's last line: its last line again, never past the face's planes)
-              const int cc = l + u < l1 ? c : (l1 - 1) / lpc, oo = l + u < l1 ? o : (l1 - 1) - ((l1 - 1) / lpc) * lpc;
-              typedef const __attribute__((address_space(4))) uint32_t* cptr;
-              v[u] = *(cptr)(base + (uint64_t)cc * cstride + (uint64_t)oo * 128);
-              if (++o == lpc) { o = 0; c++; }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < PFB; u++) pf_acc += v[u];
+          const int lpc = (fd.H + 1) * (PITCH * 2 / 128), T = NCH * lpc;  // 128-byte lines of the face's planes
+          const uint32_t* base = reinterpret_cast<const uint32_t*>(A.chan + fd.ch_off);
+          if (j < T) {
+            const int c = j / lpc, o = j - c * lpc;
+            uint32_t v = base[(int64_t)c * (A.plane / 2) + o * 32];
+            if (FFD_TRAV_TOUCH_SECT > 1) v += base[(int64_t)c * (A.plane / 2) + o * 32 + 16];
+            if (f == f_lo) tv0 = v; else tv1 = v;
           }
         }
       }
@@ -1444,11 +1350,13 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       __syncthreads();  // the previous block's walks are done with the window
       commit(cur);
       __syncthreads();  // the window holds block `cur` (or the end marker)
+      pf_acc += tv0 + tv1;  // (the last iteration's touches: complete, the commit waited for the loads before them)
       if (!cur.more) break;
       lb += nk;
       const Blk nxt = block(lb);
+      if (FFD_TRAV_TOUCH_FIRST) touch(it);
       prefetch(nxt);
-      plane_prefetch(it);
+      if (!FFD_TRAV_TOUCH_FIRST) touch(it);
       cur = nxt;
     }
     if (pf_acc == 0x9E3779B9u && A.n_faces < 0) A.leaf_out[0] = (int32_t)pf_acc;  // (keeps the prefetch loads)
@@ -2622,7 +2530,7 @@ int gabor_face_lds(int R, int max_h) {
 }
 
 void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t* gray, const float* coef, float* mag,
-                  uint16_t* chan, int* redo, int force_exact, uint32_t* split_mm, hipStream_t s, uint32_t* face_mm) {
+                  uint16_t* chan, int* redo, int force_exact, uint32_t* split_mm, hipStream_t s) {
   if (n <= 0) return;
   const float* c = coef + GABOR_OFFS[nu];
   // small batches: a face's bands / tiles spread over workgroups (split_mm: n x 5 zeroed 16-word slots)
@@ -2631,7 +2539,6 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t
     return v ? std::atoi(v) : FFD_GABOR_SPLIT_MAX;
   }();
   const bool split = split_mm && n <= split_max && max_h <= MAX_FACE_H;
-  if (split || FFD_GABOR_BAND_ALL) face_mm = nullptr;  // (the banded / band-all instances run the fused epilogue)
   // the fast instance, then the exact one over the faces it flagged (an empty pass in practice)
   int* rd = redo + (int64_t)nu * n;  // one flag array per scale: the scales may run on fork streams
   for (int exact = 0; exact < 2; exact++) {
@@ -2657,11 +2564,7 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t
       continue;
     }
 #define FFD_GABOR_LAUNCH(WV, RV)                                                                              \
-  if (face_mm)                                                                                                  \
-    (exact ? k_gabor_sep<WV, true, false, false, false> : k_gabor_sep<WV, false, false, false, false>)<<<n, GS_THREADS, \
-        gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, mag, chan, rd, force_exact, face_mm); \
-  else                                                                                                          \
-    (exact ? k_gabor_sep<WV, true, false> : k_gabor_sep<WV, false, false>)<<<n, GS_THREADS, gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, \
+  (exact ? k_gabor_sep<WV, true, false> : k_gabor_sep<WV, false, false>)<<<n, GS_THREADS, gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, \
                                                                                                   mag, chan, rd, force_exact, nullptr); \
   if (max_h > MAX_FACE_H || FFD_GABOR_BAND_ALL)                                                                 \
     (exact ? k_gabor_sep<WV, true, true> : k_gabor_sep<WV, false, true>)<<<n, GS_THREADS, (GS_BY + 2 * RV) * ((PITCH + 2 * RV + 3) / 4 * 4), s>>>(faces, gray, c, \
@@ -2672,17 +2575,12 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t
       case 2: FFD_GABOR_LAUNCH(13, 6); break;
       case 1: FFD_GABOR_LAUNCH(9, 4); break;
       default:
-        if (face_mm)
-          (exact ? k_gabor7<true, false, false> : k_gabor7<false, false, false>)<<<n, GB_THREADS, 0, s>>>(
-              faces, gray, reinterpret_cast<const float4*>(c), mag, chan, rd, force_exact, face_mm);
-        else
-          (exact ? k_gabor7<true, false> : k_gabor7<false, false>)<<<n, GB_THREADS, 0, s>>>(faces, gray, reinterpret_cast<const float4*>(c),
-                                                                            mag, chan, rd, force_exact, nullptr);
+        (exact ? k_gabor7<true, false> : k_gabor7<false, false>)<<<n, GB_THREADS, 0, s>>>(faces, gray, reinterpret_cast<const float4*>(c),
+                                                                          mag, chan, rd, force_exact, nullptr);
         break;
     }
 #undef FFD_GABOR_LAUNCH
   }
-  if (face_mm) k_gabor_epi<<<n, GE_THREADS, 0, s>>>(faces, nu, face_mm, mag, chan);  // (not reached when split)
 }
 
 // Exhaustive device check of mag_sqrt against sqrtf (ffd_check_mag_sqrt): the n floats with bits

@@ -27,11 +27,8 @@ void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uin
 // quantisation and integration of the 7 channels (one workgroup per face)
 // max_h: the tallest scaled face of the batch (sizes the padded-face LDS copy)
 void launch_check_mag_sqrt(uint32_t lo, uint32_t n, uint32_t* bad, int blocks, hipStream_t s);
-// face_mm (big batches; n x 5 x 16 words): the compute instances store each plane's min / max there and k_gabor_epi
-// normalises and integrates; nullptr: the epilogue fused into the compute workgroups (small batches, samples)
 void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t* gray, const float* coef, float* mag,
-                  uint16_t* chan, int* redo, int force_exact, uint32_t* split_mm, hipStream_t s,
-                  uint32_t* face_mm = nullptr);
+                  uint16_t* chan, int* redo, int force_exact, uint32_t* split_mm, hipStream_t s);
 hipError_t set_gabor_lds_limit(int bytes);
 // integral channels 0 (gray), 36, 37 (Sobel)
 void launch_integral(const FaceDesc* faces, int n, int max_h, const uint8_t* gray, uint16_t* chan, hipStream_t s);
