@@ -1034,7 +1034,7 @@ constexpr int BUF_WORD3 = 0x00020000;  // raw buffer resource word 3 (gfx950: 32
 #define FFD_TRAV_TOUCH_SECT 1  // words touched per 128-byte line (1: one; 2: one per 64-byte half)
 #endif
 #ifndef FFD_TRAV_TOUCH_HP
-#define FFD_TRAV_TOUCH_HP 1  // 0: the head-pose pass does not touch
+#define FFD_TRAV_TOUCH_HP 0  // 1: the head-pose pass touches too (measured 4.31 -> 4.40 ms: a face is ~1 block iteration there)
 #endif
 #ifndef FFD_TRAV_TOUCH_FIRST
 #define FFD_TRAV_TOUCH_FIRST 0  // 1: the touches are issued before the next window's staging loads
@@ -1063,11 +1063,12 @@ struct TravArgs {
   int step, step_y;        // patch grid steps (x, y)
   int plane;               // channel plane stride (elements), the same for every face of the batch
   int lds_bytes;           // dynamic LDS of the workgroup
+  int tg;                  // tree groups per block (small batches: a block's trees over tg workgroups)
   const uint16_t* chan;
   int32_t* leaf_out;
 };
 
-template <bool HP, int GX, int GY, int CB>
+template <bool HP, int GX, int GY, int CB, bool TGR = false>
 __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* win = reinterpret_cast<uint16_t*>(smem);
@@ -1084,13 +1085,16 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   const int total = NCH * WH * nq;  // chunks per window (host guarantees <= NS * U)
   uint4* top_rec = reinterpret_cast<uint4*>(smem + trav_window_bytes(WW, WH, GX * step));  // [t][TOPN] heap-ordered pairs
   // XCD-contiguous, face-major block range of this workgroup's XCD; workgroups of one XCD stride it
-  const int N = A.n_faces * A.bpf, xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+  // work unit lb = (face block, tree group): lb / tg = block, lb % tg = the group of the face's trees it walks
+  const int tg = TGR ? A.tg : 1;  // TGR: the small-batch instance (tree groups); batches keep the plain indexing
+  const int N = A.n_faces * A.bpf * tg, xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
   const int q8 = N >> 3, r8 = N & 7;
   const int start = xcd * q8 + min(xcd, r8), end = start + q8 + (xcd < r8 ? 1 : 0);
   const int nk = gridDim.x >> 3;
 
   struct Blk {
     int f, xi0, yi0, px0, py0, nx, ny, T;
+    int t0, t1;          // the trees of this work unit: [t0, t1) of the face's T
     int ok;
     int out_lo, out_hi;  // element offset of the face's leaf block (FaceDesc hp_off / mp_off)
     int more;            // 0: past the XCD's last block (every wave leaves its loop)
@@ -1098,13 +1102,15 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   // The block a window holds, computed by the stagers with the window's next fill and handed to the walkers
   // through LDS at the end of the allocation (TRAV_BLK_BYTES), so the walkers start walking after the barrier
   // instead of loading the face descriptor and tree count themselves.
+  static_assert(sizeof(Blk) <= TRAV_BLK_BYTES, "block descriptor slot");
   Blk* blk_lds = reinterpret_cast<Blk*>(smem + A.lds_bytes - TRAV_BLK_BYTES);
   auto block = [&](int lb) {
     Blk B;
     B.ok = 0;
     B.more = lb < end;
-    B.f = B.more ? lb / A.bpf : 0;
-    const int b = lb - B.f * A.bpf;
+    const int lbb = TGR ? lb / tg : lb, g = TGR ? lb - lbb * tg : 0;
+    B.f = B.more ? lbb / A.bpf : 0;
+    const int b = lbb - B.f * A.bpf;
     const FaceDesc& fd = A.faces[B.f];
     B.nx = HP ? fd.nhx : fd.nmx;
     B.ny = HP ? fd.nhy : fd.nmy;
@@ -1118,6 +1124,8 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       B.ok = 1;
       B.T = HP ? A.ntrees_hp : A.hp_state[B.f].n_trees;
     }
+    B.t0 = TGR ? g * B.T / tg : 0;
+    B.t1 = TGR ? (g + 1) * B.T / tg : B.T;
     const int64_t off = HP ? fd.hp_off : fd.mp_off;
     B.out_lo = (int)(uint32_t)off;
     B.out_hi = (int)(off >> 32);
@@ -1125,13 +1133,13 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   };
 
   auto walk_block = [&](const Blk& B) {
-    const int items = GG * B.T, sh = B.px0 & 3;
+    const int items = GG * (TGR ? B.t1 - B.t0 : B.T), sh = B.px0 & 3;
     int32_t* out = A.leaf_out + (int64_t)(((uint64_t)(uint32_t)B.out_hi << 32) | (uint32_t)B.out_lo);
     const int ld2 = 2 * LW, chs2 = 2 * WH * LW;  // window row / channel-plane strides (bytes)
     const int topn = trav_top_n(B.T, A.top_free, A.top_max, TOP_E);
     const uint32_t* top_i = reinterpret_cast<const uint32_t*>(top_rec + B.T * topn);
     for (int item = tid; item < items; item += NW) {
-      const int t = item / GG, pl = item - t * GG;
+      const int tr = item / GG, pl = item - tr * GG, t = TGR ? B.t0 + tr : tr;
       const int xi = B.xi0 + pl % GX, yi = B.yi0 + pl / GX;
       if (xi >= B.nx || yi >= B.ny) continue;
       // byte address of the patch's top-left integral corner in channel 0's window plane
@@ -1324,9 +1332,9 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     uint32_t pf_acc = 0, tv0 = 0, tv1 = 0;
     auto touch = [&](int it) {
       if constexpr (FFD_TRAV_TOUCH > 0 && (FFD_TRAV_TOUCH_HP || !HP)) {
-        const int b_lo = start + nk * (it + FFD_TRAV_TOUCH), b_hi = min(end, b_lo + nk);
+        const int b_lo = start + nk * (it + FFD_TRAV_TOUCH), b_hi = min(end, b_lo + nk), upf = A.bpf * tg;
         if (b_lo >= b_hi) return;
-        const int f_lo = (b_lo + A.bpf - 1) / A.bpf, f_hi = min((b_hi + A.bpf - 1) / A.bpf, f_lo + 2);
+        const int f_lo = (b_lo + upf - 1) / upf, f_hi = min((b_hi + upf - 1) / upf, f_lo + 2);
         const int j = k * NS + (tid - NW);  // (the XCD has nk x NS stager lanes; lines past them are not touched)
         for (int f = f_lo; f < f_hi; f++) {
           const FaceDesc& fd = A.faces[f];
@@ -1368,6 +1376,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
       if (!__builtin_amdgcn_readfirstlane(cur.more)) break;
       cur.ok = __builtin_amdgcn_readfirstlane(cur.ok);
       cur.T = __builtin_amdgcn_readfirstlane(cur.T);
+      if (TGR) {
+        cur.t0 = __builtin_amdgcn_readfirstlane(cur.t0);
+        cur.t1 = __builtin_amdgcn_readfirstlane(cur.t1);
+      }
       if (cur.ok) walk_block(cur);
     }
   }
@@ -2645,16 +2657,22 @@ void launch_traverse(bool hp, const FaceDesc* faces, int n, int bpf, TravShape g
                      int lds_cap, hipStream_t s) {
   const int total_blocks = n * bpf;
   if (total_blocks <= 0) return;
+  // a batch of a few faces has fewer blocks than CUs: a block's trees are then walked by tg workgroups, tg trees
+  // fewer per window (single-face latency: the sample grid of the per-patch evaluateMT pattern, analyzeFace)
+  const int tg = total_blocks * 2 <= n_wg ? std::max(1, std::min(hp ? 8 : 4, n_wg / total_blocks)) : 1;
   // the window, then as many tree-top entries as the rest of the CU's LDS holds
   const int WW = 32 + step * (g.gx - 1), WH = 32 + step_y * (g.gy - 1), lds = lds_cap;
   TravArgs A{faces, n, bpf, pairs, tops, top_idx, lds - trav_window_bytes(WW, WH, g.gx * step) - TRAV_BLK_BYTES, top_max,
-             far, state, ntrees_hp, step, step_y, (int)plane, lds, chan, leaf_out};
+             far, state, ntrees_hp, step, step_y, (int)plane, lds, tg, chan, leaf_out};
   // one persistent workgroup per CU, but no more than the blocks need (a one-face call has ~50 blocks)
-  const int grid = std::max(8, std::min(n_wg & ~7, (total_blocks + 7) & ~7));
+  const int grid = std::max(8, std::min(n_wg & ~7, (total_blocks * tg + 7) & ~7));
   const bool c16 = trav_chunk_bytes(WW, g.gx * step) == 16;
 #define FFD_TRAV_LAUNCH(HPV, GXV, GYV)                                                    \
   if (hp == HPV && g.gx == GXV && g.gy == GYV) {                                          \
-    if (c16) k_traverse<HPV, GXV, GYV, 16><<<grid, TRAV_NT, lds, s>>>(A);                 \
+    if (tg > 1) {                                                                         \
+      if (c16) k_traverse<HPV, GXV, GYV, 16, true><<<grid, TRAV_NT, lds, s>>>(A);         \
+      else k_traverse<HPV, GXV, GYV, 8, true><<<grid, TRAV_NT, lds, s>>>(A);              \
+    } else if (c16) k_traverse<HPV, GXV, GYV, 16><<<grid, TRAV_NT, lds, s>>>(A);          \
     else k_traverse<HPV, GXV, GYV, 8><<<grid, TRAV_NT, lds, s>>>(A);                      \
     return;                                                                               \
   }
@@ -2680,7 +2698,8 @@ hipError_t set_gabor_lds_limit(int bytes) {
 hipError_t set_traverse_lds_limit(int bytes) {
   hipError_t e = hipSuccess;
 #define FFD_TRAV_ATTR(HPV, GXV, GYV)                                                                     \
-  for (const void* f : {(const void*)k_traverse<HPV, GXV, GYV, 8>, (const void*)k_traverse<HPV, GXV, GYV, 16>}) { \
+  for (const void* f : {(const void*)k_traverse<HPV, GXV, GYV, 8>, (const void*)k_traverse<HPV, GXV, GYV, 16>,        \
+                        (const void*)k_traverse<HPV, GXV, GYV, 8, true>, (const void*)k_traverse<HPV, GXV, GYV, 16, true>}) { \
     hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);            \
     if (r != hipSuccess) e = r;                                                                          \
   }
