@@ -561,6 +561,12 @@ constexpr int GS_THREADS = 256, GS_BY = 8;
 #define FFD_GS_QSPLIT 1  // k_gabor_sep: V / H passes in two plane halves (LDS 66 -> 47 KB at 25x25: 3 WGs per CU)
 #endif
 constexpr bool GS_QSPLIT = FFD_GS_QSPLIT;
+#ifndef FFD_GS_CPT2_MASK
+#define FFD_GS_CPT2_MASK 0  // bit nu (2: 13x13, 3: 19x19, 4: 25x25): the batch instance with 2 columns per H-pass thread
+#endif
+#ifndef FFD_GS_CPT2_WAVES
+#define FFD_GS_CPT2_WAVES 4  // ... its waves per SIMD (4: <= 128 VGPRs, two 512-thread workgroups per CU)
+#endif
 #ifndef FFD_GABOR_BAND_ALL
 #define FFD_GABOR_BAND_ALL 0  // 1: every face through the band-staged (TALL) instance (LDS 66 -> 49 KB per workgroup)
 #endif
@@ -572,19 +578,26 @@ constexpr bool GS_QSPLIT = FFD_GS_QSPLIT;
 #endif
 
 
-template <int R> struct GSep {
+// CPT: output columns per H-pass thread (4: 256-thread workgroups; 2: 512 threads, half the accumulators per thread)
+template <int R, int CPT = 4> struct GSep {
   static constexpr int GP = (PITCH + 2 * R + 3) / 4 * 4;  // padded gray row pitch (bytes)
-  static constexpr int QS = 32 + ((3 + 2 * R) >> 2);      // quad-split slots per phase
-  static constexpr int VP = 4 * QS;                       // V row pitch (elements) >= W + 2R
+  static constexpr int LC = CPT == 4 ? 2 : 1;             // log2(CPT)
+  // V values "CPT-split": padded column cc at slot (cc % CPT) * QS + cc / CPT, so the lanes of an H-pass row
+  // (column groups cq, cq + 1, ...) reading column CPT * cq + u hit consecutive words
+  static constexpr int QS = 128 / CPT + ((CPT - 1 + 2 * R) >> LC);
+  static constexpr int VP = CPT * QS;                     // V row pitch (elements) >= W + 2R
   static constexpr int SC = GP;                           // staging / V-pass column range
+  static constexpr int NT = 256 * 4 / CPT;                // threads per workgroup
   static constexpr int V_OFF = 4, H_OFF = 4 + 12 * (R + 1);
 };
+__host__ __device__ constexpr int gs_threads(int cpt) { return 256 * 4 / cpt; }
 
 // TALL: the instance for faces taller than MAX_FACE_H (box aspect h/w > 4.8), whose padded face does not
 // fit the LDS: each band stages only its GS_BY + 2R rows (4x re-staging at 25x25; such faces are rare).
 // Each instance skips the other's faces.
-template <int W, bool EXACT, bool TALL, bool SPLIT = false>
-__global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __restrict__ faces,
+template <int W, bool EXACT, bool TALL, bool SPLIT = false, int CPT = 4>
+__global__ __launch_bounds__(gs_threads(CPT)) __attribute__((amdgpu_waves_per_eu(CPT == 2 ? FFD_GS_CPT2_WAVES : 1)))
+void k_gabor_sep(const FaceDesc* __restrict__ faces,
                                                           const uint8_t* __restrict__ gray,
                                                           const float* __restrict__ coef,
                                                           float* __restrict__ mag,
@@ -592,7 +605,9 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
                                                           uint32_t* __restrict__ split_mm) {
   static_assert(!(TALL && SPLIT), "tall faces are not banded across workgroups");
   constexpr int R = (W - 1) / 2;
-  using C = GSep<R>;
+  using C = GSep<R, CPT>;
+  constexpr int GS_THREADS = C::NT;
+  static_assert(CPT == 4 || (CPT == 2 && !TALL && !SPLIT), "2-column threads: the batch instance only");
   constexpr int NU = W == 9 ? 1 : W == 13 ? 2 : W == 19 ? 3 : 4;
   // magnitude sqrt / min-max forms per scale (r2e, C2, ms): 25x25 sqrtf + masked min-max 1.88 (both
   // compiler forms 1.93, both fast 2.04: SGPR spills); 19x19 both fast 1.63 (1.72); 13x13 / 9x9
@@ -602,7 +617,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
   __shared__ float vg[GS_BY * C::VP];
   // QS: the V / H passes in two plane halves (half the V-plane LDS, fewer live registers): measured faster
   // for 9x9 only (1.34 -> 1.16 ms; 13x13 / 19x19 even, 25x25 1.96 -> 2.43)
-  constexpr bool QS = GS_QSPLIT && W == 9;
+  constexpr bool QS = GS_QSPLIT && W == 9 && CPT == 4;
   __shared__ f2 vq[QS ? 2 : 4][GS_BY * C::VP];
   const FaceDesc fd = faces[blockIdx.x];
   if (!fd.valid || fd.nochan || ((FFD_GABOR_BAND_ALL && !SPLIT) ? !TALL : (fd.H > MAX_FACE_H) != TALL)) return;
@@ -657,20 +672,21 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
       stage_rows(y0, GS_BY + 2 * R);
       __syncthreads();
     }
-    // ---- H pass (below): thread = (row hr, column quad cq), outputs x = 4 cq + k
-    const int hr = tid >> 5, cq = tid & 31, y = y0 + hr, x0 = 4 * cq;
-    f2 acc0[4], acc4[4], ac[3][4], be[3][4];  // mu 0, mu 4; per horizontal set p = 1..3: (A, C), (B, E)
-    float dc[4];
+    // ---- H pass (below): thread = (row hr, column group cq), outputs x = CPT cq + k
+    constexpr int NCQ = 128 / CPT;
+    const int hr = tid / NCQ, cq = tid % NCQ, y = y0 + hr, x0 = CPT * cq;
+    f2 acc0[CPT], acc4[CPT], ac[3][CPT], be[3][CPT];  // mu 0, mu 4; per horizontal set p = 1..3: (A, C), (B, E)
+    float dc[CPT];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < CPT; k++) {
       dc[k] = 0.f;
       acc0[k] = acc4[k] = f2{0.f, 0.f};
 #pragma unroll
       for (int p = 0; p < 3; p++) ac[p][k] = be[p][k] = f2{0.f, 0.f};
     }
     const int rb = hr * C::VP + cq;
-    // V value at padded column x0 + u + R: quad-split slot (u + R) & 3, offset (u + R) >> 2
-#define GS_IDX(u) (rb + (((u) + R) & 3) * C::QS + (((u) + R) >> 2))
+    // V value at padded column x0 + u + R: slot (u + R) % CPT, offset (u + R) / CPT
+#define GS_IDX(u) (rb + (((u) + R) & (CPT - 1)) * C::QS + (((u) + R) >> C::LC))
     if constexpr (QS) {
     // ---- V pass over planes [QLO, QLO + QN) (+ Vg when G): vq slot q - QLO
     auto vpass = [&](auto qlo_c, auto qn_c, auto g_c) {
@@ -788,7 +804,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
       vgv = fmaf(cv[0], p0, vgv);
 #pragma unroll
       for (int q = 0; q < 4; q++) vqv[q] = __builtin_elementwise_fma(f2{cv[2 + 2 * q], cv[3 + 2 * q]}, f2{p0, p0}, vqv[q]);
-      const int qi = r * C::VP + (cc & 3) * C::QS + (cc >> 2);
+      const int qi = r * C::VP + (cc & (CPT - 1)) * C::QS + (cc >> C::LC);
       vg[qi] = vgv;
 #pragma unroll
       for (int q = 0; q < 4; q++) vq[q][qi] = vqv[q];
@@ -796,10 +812,10 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
     __syncthreads();  // V planes ready
     // Vg: DC term and mu 0
 #pragma unroll
-    for (int u = -R; u <= R + 3; u++) {
+    for (int u = -R; u <= R + CPT - 1; u++) {
       const float v = vg[GS_IDX(u)];
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
+      for (int k = 0; k < CPT; k++) {
         const int t = u - k;
         if (t < -R || t > R) continue;
         const float* h = chh + 16 * (t + R);
@@ -809,10 +825,10 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
     }
     // q = 4: mu 4
 #pragma unroll
-    for (int u = -R; u <= R + 3; u++) {
+    for (int u = -R; u <= R + CPT - 1; u++) {
       const f2 v = vq[3][GS_IDX(u)];
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
+      for (int k = 0; k < CPT; k++) {
         const int t = u - k;
         if (t < -R || t > R) continue;
         const float* h = chh + 16 * (t + R);
@@ -823,10 +839,10 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
 #pragma unroll
     for (int p = 0; p < 3; p++) {
 #pragma unroll
-      for (int u = -R; u <= R + 3; u++) {
+      for (int u = -R; u <= R + CPT - 1; u++) {
         const f2 v = vq[p][GS_IDX(u)], vs = f2{v.y, v.x};
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < CPT; k++) {
           const int t = u - k;
           if (t < -R || t > R) continue;
           const float* h = chh + 16 * (t + R) + 4 * (p + 1);
@@ -837,9 +853,9 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
     }
 #undef GS_IDX
     }
-    f2 acc[4][7];
+    f2 acc[CPT][7];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < CPT; k++) {
       acc[k][0] = acc0[k];
       acc[k][4] = acc4[k];
       acc[k][1] = f2{ac[0][k].x - be[0][k].x, ac[0][k].y + be[0][k].y};
@@ -852,17 +868,18 @@ __global__ __launch_bounds__(GS_THREADS) void k_gabor_sep(const FaceDesc* __rest
     if (y < FH) {
 #pragma unroll
       for (int o = 0; o < 7; o++) {
-        float m4[4];
+        float m4[CPT];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < CPT; k++) {
           const float re = fmaf(-cdc, dc[k], acc[k][o].x), im = acc[k][o].y;
           const float i2 = im * im, r2 = re * re;
           m4[k] = mag_of<EXACT, GS_FAST>(i2 + r2, tiny);
           minmax_update<GS_MASK>(mn[o], mx[o], m4[k], x0 + k < FW);
         }
         // columns >= W land in the row's pitch padding, never read
-        *reinterpret_cast<float4*>(&mag[fd.mag_off + ((int64_t)(NU * 7 + o) * FH + y) * PITCH + x0]) =
-            make_float4(m4[0], m4[1], m4[2], m4[3]);
+        float* mp = &mag[fd.mag_off + ((int64_t)(NU * 7 + o) * FH + y) * PITCH + x0];
+        if constexpr (CPT == 4) *reinterpret_cast<float4*>(mp) = make_float4(m4[0], m4[1], m4[2], m4[3]);
+        else *reinterpret_cast<float2*>(mp) = make_float2(m4[0], m4[1]);
       }
     }
   }
@@ -1333,7 +1350,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     auto touch = [&](int it) {
       if constexpr (FFD_TRAV_TOUCH > 0 && (FFD_TRAV_TOUCH_HP || !HP)) {
         const int b_lo = start + nk * (it + FFD_TRAV_TOUCH), b_hi = min(end, b_lo + nk), upf = A.bpf * tg;
-        if (b_lo >= b_hi) return;
+        // only faces that take at most two block iterations: a face's lines all requested at once then serve its
+        // next iteration; the blocks of a larger face (C4: 190 per face) come over many iterations, by which time
+        // its touched lines are gone from L2 (C4 FFD 8.42 -> 9.83 ms touching them)
+        if (b_lo >= b_hi || upf > 2 * nk) return;
         const int f_lo = (b_lo + upf - 1) / upf, f_hi = min((b_hi + upf - 1) / upf, f_lo + 2);
         const int j = k * NS + (tid - NW);  // (the XCD has nk x NS stager lanes; lines past them are not touched)
         for (int f = f_lo; f < f_hi; f++) {
@@ -2576,7 +2596,11 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t
       continue;
     }
 #define FFD_GABOR_LAUNCH(WV, RV)                                                                              \
-  (exact ? k_gabor_sep<WV, true, false> : k_gabor_sep<WV, false, false>)<<<n, GS_THREADS, gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, \
+  if ((FFD_GS_CPT2_MASK >> nu) & 1)                                                                             \
+    (exact ? k_gabor_sep<WV, true, false, false, 2> : k_gabor_sep<WV, false, false, false, 2>)<<<n, gs_threads(2), \
+        gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, mag, chan, rd, force_exact, nullptr); \
+  else                                                                                                          \
+    (exact ? k_gabor_sep<WV, true, false> : k_gabor_sep<WV, false, false>)<<<n, GS_THREADS, gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, \
                                                                                                   mag, chan, rd, force_exact, nullptr); \
   if (max_h > MAX_FACE_H || FFD_GABOR_BAND_ALL)                                                                 \
     (exact ? k_gabor_sep<WV, true, true> : k_gabor_sep<WV, false, true>)<<<n, GS_THREADS, (GS_BY + 2 * RV) * ((PITCH + 2 * RV + 3) / 4 * 4), s>>>(faces, gray, c, \
@@ -2686,6 +2710,9 @@ hipError_t set_gabor_lds_limit(int bytes) {
                        (const void*)k_gabor_sep<19, false, false>, (const void*)k_gabor_sep<25, false, false>,
                        (const void*)k_gabor_sep<9, true, false>,   (const void*)k_gabor_sep<13, true, false>,
                        (const void*)k_gabor_sep<19, true, false>,  (const void*)k_gabor_sep<25, true, false>,
+                       (const void*)k_gabor_sep<13, false, false, false, 2>, (const void*)k_gabor_sep<19, false, false, false, 2>,
+                       (const void*)k_gabor_sep<25, false, false, false, 2>, (const void*)k_gabor_sep<13, true, false, false, 2>,
+                       (const void*)k_gabor_sep<19, true, false, false, 2>,  (const void*)k_gabor_sep<25, true, false, false, 2>,
                        (const void*)k_integral<true>};
   for (const void* f : fns) {
     hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
