@@ -309,13 +309,15 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
     e->det_boxes.ensure((size_t)nF * cap * 16);
     e->det_packed.ensure((size_t)nF * cap * 20);
     if (cap > HAAR_MAX_CAND) e->det_label.ensure(((size_t)nF * cap + 1) * 4);  // (+ the rounds' change flag)
-    int max_px = 0, max_lpx = 0, max_rows = 0, max_cols = 0, max_tiles = 0, max_ystep = 1;
+    int max_px = 0, max_lpx = 0, max_rows = 0, max_cols = 0, max_ystep = 1;
     for (const auto& f : frames) max_px = std::max(max_px, f.w * f.h);
-    for (const auto& L : levels) {
+    int total_tiles = 0;  // the cascade's grid: every level's tiles, none empty (HaarLevel::tile0)
+    for (auto& L : levels) {
+      L.tile0 = total_tiles;
+      total_tiles += ((L.nx + HAAR_TILE_X - 1) / HAAR_TILE_X) * ((L.ny + HAAR_TILE_Y - 1) / HAAR_TILE_Y);
       max_lpx = std::max(max_lpx, L.sw * L.sh);
       max_rows = std::max(max_rows, L.sh);
       max_cols = std::max(max_cols, L.sw);
-      max_tiles = std::max(max_tiles, ((L.nx + HAAR_TILE_X - 1) / HAAR_TILE_X) * ((L.ny + HAAR_TILE_Y - 1) / HAAR_TILE_Y));
       max_ystep = std::max(max_ystep, L.ystep);
     }
     int32_t* n_cand = e->det_ncand.as<int32_t>();
@@ -331,7 +333,7 @@ ffd_status detect_batch(ffd_engine* e, const uint8_t* d_images, const std::vecto
                           e->det_scaled.as<uint8_t>(), e->det_sum.as<int32_t>(), e->det_sq.as<uint32_t>(), s);
       const int lds = haar_cascade_lds(max_ystep, e->haar_ww, e->haar_wh);
       if (lds > 64 * 1024) return fail(e, FFD_ERR_UNSUPPORTED, "cascade window too large for the LDS tile");
-      launch_haar_cascade(e->det_levels.as<HaarLevel>(), nL, max_tiles, e->det_sum.as<int32_t>(),
+      launch_haar_cascade(e->det_levels.as<HaarLevel>(), nL, total_tiles, e->det_sum.as<int32_t>(),
                           e->det_sq.as<uint32_t>(), e->haar_weak.as<HaarWeak>(), e->haar_nweak, e->haar_stage.as<HaarStage>(),
                           e->haar_stages, e->haar_ww, e->haar_wh, e->haar_order_free, e->det_res.as<int8_t>(), lds, s);
     }

@@ -222,7 +222,7 @@ static_assert(HT_X == HAAR_TILE_X && HT_Y == HAAR_TILE_Y, "host offset tables as
 __host__ __device__ constexpr int haar_win_cols(int ystep, int ww) { return HT_X * ystep + ww; }
 __host__ __device__ constexpr int haar_win_rows(int ystep, int wh) { return HT_Y * ystep + wh; }
 
-__global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __restrict__ levels,
+__global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __restrict__ levels, int n_levels,
                                                              const int32_t* __restrict__ sum,
                                                              const uint32_t* __restrict__ sq,
                                                              const HaarWeak* __restrict__ weak_tables, int n_weak,
@@ -233,9 +233,17 @@ __global__ __launch_bounds__(HT_THREADS) void k_haar_cascade(const HaarLevel* __
   __shared__ double vnf[HT_POS];
   __shared__ uint16_t list[2][HT_POS];
   __shared__ int n_list[2];
-  const HaarLevel L = levels[blockIdx.y];
-  const int tiles_x = (L.nx + HT_X - 1) / HT_X;
-  const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
+  // this workgroup's level: the last whose first tile is <= blockIdx.x (the grid holds every level's tiles and
+  // nothing else; a (tile, level) grid over the largest level's tile count launched ~6x as many empty workgroups)
+  int lo = 0, hi = n_levels - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (levels[mid].tile0 <= (int)blockIdx.x) lo = mid;
+    else hi = mid - 1;
+  }
+  const HaarLevel L = levels[lo];
+  const int tiles_x = (L.nx + HT_X - 1) / HT_X, tl = (int)blockIdx.x - L.tile0;
+  const int ty = tl / tiles_x, tx = tl - ty * tiles_x;
   if (ty * HT_Y >= L.ny) return;
   const int ys = L.ystep, P = L.sw + 1;
   const int WC = haar_win_cols(ys, ww), WR = haar_win_rows(ys, wh);
@@ -774,11 +782,12 @@ int haar_cascade_lds(int max_ystep, int ww, int wh) {
   return haar_win_cols(max_ystep, ww) * haar_win_rows(max_ystep, wh) * 4;
 }
 
-void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint32_t* sq,
+void launch_haar_cascade(const HaarLevel* levels, int n_levels, int total_tiles, const int32_t* sum, const uint32_t* sq,
                          const HaarWeak* weak, int n_weak, const HaarStage* stages, int n_stages, int ww, int wh,
                          int order_free, int8_t* result, int lds_bytes, hipStream_t s) {
-  k_haar_cascade<<<dim3(max_tiles, n_levels), HT_THREADS, lds_bytes, s>>>(levels, sum, sq, weak, n_weak, stages,
-                                                                           n_stages, ww, wh, order_free, result);
+  if (total_tiles <= 0 || n_levels <= 0) return;
+  k_haar_cascade<<<total_tiles, HT_THREADS, lds_bytes, s>>>(levels, n_levels, sum, sq, weak, n_weak, stages, n_stages, ww,
+                                                            wh, order_free, result);
 }
 
 // The grouping of a frame with more raw detections than a workgroup's LDS holds (the overflow re-run, one frame):

@@ -36,6 +36,7 @@ struct HaarLevel {
   int32_t mode, xv;  // resize: 0 copy, 1 bilinear, 2 area 2x; SSE2 column bound
   int32_t row0;      // first scan row of this level within its frame
   int32_t frame;
+  int32_t tile0;     // the level's first cascade tile in its launch's one-dimensional grid (k_haar_cascade)
 };
 
 // One stump weak classifier with its Haar feature (HaarEvaluator::Feature + DTreeNode + 2 leaves), its
@@ -73,7 +74,7 @@ void launch_haar_pyramid(const HaarLevel* levels, int n_levels, int max_pixels, 
 constexpr int HAAR_TILE_X = 64, HAAR_TILE_Y = FFD_HAAR_TILE_Y;
 int haar_cascade_lds(int max_ystep, int ww, int wh);
 // weak: the ystep-1 table, then (at weak + n_weak) the ystep-2 table
-void launch_haar_cascade(const HaarLevel* levels, int n_levels, int max_tiles, const int32_t* sum, const uint32_t* sq,
+void launch_haar_cascade(const HaarLevel* levels, int n_levels, int total_tiles, const int32_t* sum, const uint32_t* sq,
                          const HaarWeak* weak, int n_weak, const HaarStage* stages, int n_stages, int ww, int wh,
                          int order_free, int8_t* result, int lds_bytes, hipStream_t s);
 constexpr int haar_window_cols(int ystep, int ww) { return HAAR_TILE_X * ystep + ww; }

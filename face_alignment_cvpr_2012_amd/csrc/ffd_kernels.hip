@@ -562,7 +562,7 @@ constexpr int GS_THREADS = 256, GS_BY = 8;
 #endif
 constexpr bool GS_QSPLIT = FFD_GS_QSPLIT;
 #ifndef FFD_GS_CPT2_MASK
-#define FFD_GS_CPT2_MASK 0  // bit nu (2: 13x13, 3: 19x19, 4: 25x25): the batch instance with 2 columns per H-pass thread
+#define FFD_GS_CPT2_MASK 12  // bit nu (2: 13x13, 3: 19x19, 4: 25x25): the batch instance with 2 columns per H-pass thread (25x25: spills at 128 VGPRs, 1.93 -> 2.68 ms)
 #endif
 #ifndef FFD_GS_CPT2_WAVES
 #define FFD_GS_CPT2_WAVES 4  // ... its waves per SIMD (4: <= 128 VGPRs, two 512-thread workgroups per CU)
@@ -1051,7 +1051,10 @@ constexpr int BUF_WORD3 = 0x00020000;  // raw buffer resource word 3 (gfx950: 32
 #define FFD_TRAV_TOUCH_SECT 1  // words touched per 128-byte line (1: one; 2: one per 64-byte half)
 #endif
 #ifndef FFD_TRAV_TOUCH_HP
-#define FFD_TRAV_TOUCH_HP 0  // 1: the head-pose pass touches too (measured 4.31 -> 4.40 ms: a face is ~1 block iteration there)
+#define FFD_TRAV_TOUCH_HP 0  // 1: the head-pose pass touches too (4.34 -> 4.40 ms face-major, 4.48 with interleaved pairs)
+#endif
+#ifndef FFD_TRAV_ILV_HP
+#define FFD_TRAV_ILV_HP 1  // head-pose faces dealt in interleaved groups of this many (2: 4.34 -> 4.44 ms without touches)
 #endif
 #ifndef FFD_TRAV_TOUCH_FIRST
 #define FFD_TRAV_TOUCH_FIRST 0  // 1: the touches are issued before the next window's staging loads
@@ -1104,6 +1107,10 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
   // XCD-contiguous, face-major block range of this workgroup's XCD; workgroups of one XCD stride it
   // work unit lb = (face block, tree group): lb / tg = block, lb % tg = the group of the face's trees it walks
   const int tg = TGR ? A.tg : 1;  // TGR: the small-batch instance (tree groups); batches keep the plain indexing
+  // ILV: the head-pose pass deals the blocks of two faces interleaved, so a face (30 blocks) spans two block
+  // iterations of its XCD (32 workgroups) instead of one, and the plane touches of its first iteration (below) serve
+  // its second
+  constexpr int ILV = (HP && !TGR) ? FFD_TRAV_ILV_HP : 1;
   const int N = A.n_faces * A.bpf * tg, xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
   const int q8 = N >> 3, r8 = N & 7;
   const int start = xcd * q8 + min(xcd, r8), end = start + q8 + (xcd < r8 ? 1 : 0);
@@ -1126,8 +1133,15 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     B.ok = 0;
     B.more = lb < end;
     const int lbb = TGR ? lb / tg : lb, g = TGR ? lb - lbb * tg : 0;
-    B.f = B.more ? lbb / A.bpf : 0;
-    const int b = lbb - B.f * A.bpf;
+    int b;
+    if constexpr (ILV > 1) {  // faces in groups of ILV, their blocks interleaved (the last group may be smaller)
+      const int grp = lbb / (ILV * A.bpf), q = lbb - grp * (ILV * A.bpf), r = min(ILV, A.n_faces - grp * ILV);
+      B.f = B.more ? grp * ILV + q % r : 0;
+      b = B.more ? q / r : 0;
+    } else {
+      B.f = B.more ? lbb / A.bpf : 0;
+      b = lbb - B.f * A.bpf;
+    }
     const FaceDesc& fd = A.faces[B.f];
     B.nx = HP ? fd.nhx : fd.nmx;
     B.ny = HP ? fd.nhy : fd.nmy;
@@ -1348,13 +1362,15 @@ __global__ __launch_bounds__(TRAV_NT) void k_traverse(TravArgs A) {
     // through the scalar path with the stager waves waiting for them, or by a prefetching workgroup per XCD, were slower.)
     uint32_t pf_acc = 0, tv0 = 0, tv1 = 0;
     auto touch = [&](int it) {
-      if constexpr (FFD_TRAV_TOUCH > 0 && (FFD_TRAV_TOUCH_HP || !HP)) {
-        const int b_lo = start + nk * (it + FFD_TRAV_TOUCH), b_hi = min(end, b_lo + nk), upf = A.bpf * tg;
-        // only faces that take at most two block iterations: a face's lines all requested at once then serve its
-        // next iteration; the blocks of a larger face (C4: 190 per face) come over many iterations, by which time
-        // its touched lines are gone from L2 (C4 FFD 8.42 -> 9.83 ms touching them)
+      // (not in the 8-byte-chunk instances: C4's (2, 1) grid, whose stager registers already spill)
+      if constexpr (FFD_TRAV_TOUCH > 0 && (FFD_TRAV_TOUCH_HP || !HP) && CB == 16) {
+        const int b_lo = start + nk * (it + FFD_TRAV_TOUCH), b_hi = min(end, b_lo + nk), upf = A.bpf * tg * ILV;
+        // only faces (groups of ILV faces) that take at most two block iterations: their lines all requested at once
+        // then serve the next iteration; the blocks of a larger face (C4: 190 per face) come over many iterations,
+        // by which time its touched lines are gone from L2 (C4 FFD 8.42 -> 9.83 ms touching them)
         if (b_lo >= b_hi || upf > 2 * nk) return;
-        const int f_lo = (b_lo + upf - 1) / upf, f_hi = min((b_hi + upf - 1) / upf, f_lo + 2);
+        const int g_lo = (b_lo + upf - 1) / upf, g_hi = (b_hi + upf - 1) / upf;  // groups starting in the iteration
+        const int f_lo = g_lo * ILV, f_hi = min(min(g_hi * ILV, A.n_faces), f_lo + 2);
         const int j = k * NS + (tid - NW);  // (the XCD has nk x NS stager lanes; lines past them are not touched)
         for (int f = f_lo; f < f_hi; f++) {
           const FaceDesc& fd = A.faces[f];
@@ -2295,8 +2311,12 @@ __global__ __launch_bounds__(MS_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8
 // one store hit 64 banks), read four at a time with ds_read_b128 by the sum lanes (round 5: the serial phase
 // issues TV adds + TV / 4 reads per tile instead of TV + TV; C4 MeanShift 8.40 -> 7.65 ms against [vote][chain]
 // float4 terms).
+#ifndef FFD_MS4_WAVES
+#define FFD_MS4_WAVES 1  // k_meanshift4: minimum waves per SIMD the register allocation must allow (8: <= 64 VGPRs)
+#endif
 template <int C, int K>
-__global__ __launch_bounds__(256) void k_meanshift4(const FaceDesc* __restrict__ faces, int n_faces, int tslots,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FFD_MS4_WAVES)))
+void k_meanshift4(const FaceDesc* __restrict__ faces, int n_faces, int tslots,
                                                    int n_parts, float lamda, float lam_y, int max_iter, float stop,
                                                    const Vote* __restrict__ votes, const int32_t* __restrict__ vote_counts,
                                                    float* __restrict__ ms_mean, FaceOut* __restrict__ out,
