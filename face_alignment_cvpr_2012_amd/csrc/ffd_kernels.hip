@@ -193,24 +193,11 @@ __device__ __forceinline__ void integral_scan(uint16_t* __restrict__ out, int W,
 // integrated by the Gabor kernels themselves.  One 4-wave workgroup per face (the 4th wave idles).
 // STAGE (small batches): the face's gray rows are first copied to LDS by all four waves, so the three
 // sequential scans read their values at LDS rather than L2 latency.
-template <bool STAGE>
-__global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ faces,
-                                                  const uint8_t* __restrict__ gray,
-                                                  uint16_t* __restrict__ chan) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t s_gray[];  // STAGE: H x PITCH
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const FaceDesc fd = faces[blockIdx.x];
-  if (!fd.valid || fd.nochan) return;
+// One of the non-Gabor integral channels (c = 0 gray, 36 Sobel d/dy, 37 Sobel d/dx) of a face, by one wave; g: the
+// face's gray rows (global, or staged in LDS).
+__device__ __forceinline__ void integral_channel(const FaceDesc& fd, const uint8_t* g, uint16_t* __restrict__ chan,
+                                                 int c, int lane) {
   const int W = fd.W, H = fd.H, x0 = 2 * lane;
-  const uint8_t* g = gray + fd.gray_off;
-  if (STAGE) {
-    for (int i = threadIdx.x; i < H * (PITCH / 16); i += 256)
-      reinterpret_cast<uint4*>(s_gray)[i] = reinterpret_cast<const uint4*>(g)[i];
-    __syncthreads();
-    g = s_gray;
-  }
-  if (wv >= 3) return;
-  const int c = wv == 0 ? 0 : 35 + wv;
   integral_scan(chan + fd.ch_off + (int64_t)c * fd.plane, W, H, lane, fd.fint != 0, [&](int y0, uint32_t* v0, uint32_t* v1) {
 #pragma unroll
     for (int b = 0; b < 8; b++) {
@@ -219,6 +206,36 @@ __global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ f
       v1[b] = (uint32_t)chan_value(c, g, W, H, y, x0 + 1);
     }
   });
+}
+
+#ifndef FFD_GS_CPT2_MASK
+#define FFD_GS_CPT2_MASK 12  // bit nu (2: 13x13, 3: 19x19, 4: 25x25): the batch instance with 2 columns per H-pass thread (25x25: spills at 128 VGPRs, 1.93 -> 2.68 ms)
+#endif
+#ifndef FFD_GS_CPT2_WAVES
+#define FFD_GS_CPT2_WAVES 4  // ... its waves per SIMD (4: <= 128 VGPRs, two 512-thread workgroups per CU)
+#endif
+#ifndef FFD_GABOR_BAND_ALL
+#define FFD_GABOR_BAND_ALL 0  // 1: every face through the band-staged (TALL) instance (LDS 66 -> 49 KB per workgroup)
+#endif
+
+template <bool STAGE>
+__global__ __launch_bounds__(256) void k_integral(const FaceDesc* __restrict__ faces,
+                                                  const uint8_t* __restrict__ gray,
+                                                  uint16_t* __restrict__ chan) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_gray[];  // STAGE: H x PITCH
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const FaceDesc fd = faces[blockIdx.x];
+  if (!fd.valid || fd.nochan) return;
+  const int H = fd.H;
+  const uint8_t* g = gray + fd.gray_off;
+  if (STAGE) {
+    for (int i = threadIdx.x; i < H * (PITCH / 16); i += 256)
+      reinterpret_cast<uint4*>(s_gray)[i] = reinterpret_cast<const uint4*>(g)[i];
+    __syncthreads();
+    g = s_gray;
+  }
+  if (wv >= 3) return;
+  integral_channel(fd, g, chan, wv == 0 ? 0 : 35 + wv, lane);
 }
 
 // ------------------------------------------------------------------ Gabor --
@@ -561,15 +578,6 @@ constexpr int GS_THREADS = 256, GS_BY = 8;
 #define FFD_GS_QSPLIT 1  // k_gabor_sep: V / H passes in two plane halves (LDS 66 -> 47 KB at 25x25: 3 WGs per CU)
 #endif
 constexpr bool GS_QSPLIT = FFD_GS_QSPLIT;
-#ifndef FFD_GS_CPT2_MASK
-#define FFD_GS_CPT2_MASK 12  // bit nu (2: 13x13, 3: 19x19, 4: 25x25): the batch instance with 2 columns per H-pass thread (25x25: spills at 128 VGPRs, 1.93 -> 2.68 ms)
-#endif
-#ifndef FFD_GS_CPT2_WAVES
-#define FFD_GS_CPT2_WAVES 4  // ... its waves per SIMD (4: <= 128 VGPRs, two 512-thread workgroups per CU)
-#endif
-#ifndef FFD_GABOR_BAND_ALL
-#define FFD_GABOR_BAND_ALL 0  // 1: every face through the band-staged (TALL) instance (LDS 66 -> 49 KB per workgroup)
-#endif
 #ifndef FFD_GABOR_SPLIT_MAX
 #define FFD_GABOR_SPLIT_MAX 16  // batches of up to 16 faces: banded Gabor instances (SPLIT)
 #endif
@@ -2581,16 +2589,21 @@ int gabor_face_lds(int R, int max_h) {
   return ((max_h + GS_BY - 1) / GS_BY * GS_BY + 2 * R) * ((PITCH + 2 * R + 3) / 4 * 4);
 }
 
+// the banded (SPLIT) Gabor instances for a batch of n faces of at most max_h rows
+bool gabor_split(int n, int max_h) {
+  static const int split_max = [] {
+    const char* v = std::getenv("FFD_GABOR_SPLIT_MAX");
+    return v ? std::atoi(v) : FFD_GABOR_SPLIT_MAX;
+  }();
+  return n <= split_max && max_h <= MAX_FACE_H;
+}
+
 void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t* gray, const float* coef, float* mag,
                   uint16_t* chan, int* redo, int force_exact, uint32_t* split_mm, hipStream_t s) {
   if (n <= 0) return;
   const float* c = coef + GABOR_OFFS[nu];
   // small batches: a face's bands / tiles spread over workgroups (split_mm: n x 5 zeroed 16-word slots)
-  static const int split_max = [] {
-    const char* v = std::getenv("FFD_GABOR_SPLIT_MAX");
-    return v ? std::atoi(v) : FFD_GABOR_SPLIT_MAX;
-  }();
-  const bool split = split_mm && n <= split_max && max_h <= MAX_FACE_H;
+  const bool split = split_mm && gabor_split(n, max_h);
   // the fast instance, then the exact one over the faces it flagged (an empty pass in practice)
   int* rd = redo + (int64_t)nu * n;  // one flag array per scale: the scales may run on fork streams
   for (int exact = 0; exact < 2; exact++) {
