@@ -211,6 +211,12 @@ __device__ __forceinline__ void integral_channel(const FaceDesc& fd, const uint8
 #ifndef FFD_GS_CPT2_MASK
 #define FFD_GS_CPT2_MASK 12  // bit nu (2: 13x13, 3: 19x19, 4: 25x25): the batch instance with 2 columns per H-pass thread (25x25: spills at 128 VGPRs, 1.93 -> 2.68 ms)
 #endif
+#ifndef FFD_GS_CPT2S_MASK
+#define FFD_GS_CPT2S_MASK 16  // bit nu: the 2-column instance in 256-thread workgroups (4-row bands; 25x25 1.91 -> 1.74 ms)
+#endif
+#ifndef FFD_GS_CPT2S_WAVES
+#define FFD_GS_CPT2S_WAVES 3  // ... its waves per SIMD (3: <= 168 VGPRs, three workgroups per CU)
+#endif
 #ifndef FFD_GS_CPT2_WAVES
 #define FFD_GS_CPT2_WAVES 4  // ... its waves per SIMD (4: <= 128 VGPRs, two 512-thread workgroups per CU)
 #endif
@@ -595,16 +601,17 @@ template <int R, int CPT = 4> struct GSep {
   static constexpr int QS = 128 / CPT + ((CPT - 1 + 2 * R) >> LC);
   static constexpr int VP = CPT * QS;                     // V row pitch (elements) >= W + 2R
   static constexpr int SC = GP;                           // staging / V-pass column range
-  static constexpr int NT = 256 * 4 / CPT;                // threads per workgroup
   static constexpr int V_OFF = 4, H_OFF = 4 + 12 * (R + 1);
 };
-__host__ __device__ constexpr int gs_threads(int cpt) { return 256 * 4 / cpt; }
+// threads of a k_gabor_sep workgroup: BY rows x 128 / CPT column groups
+__host__ __device__ constexpr int gs_threads(int cpt, int by = 8) { return by * 128 / cpt; }
 
 // TALL: the instance for faces taller than MAX_FACE_H (box aspect h/w > 4.8), whose padded face does not
 // fit the LDS: each band stages only its GS_BY + 2R rows (4x re-staging at 25x25; such faces are rare).
 // Each instance skips the other's faces.
-template <int W, bool EXACT, bool TALL, bool SPLIT = false, int CPT = 4>
-__global__ __launch_bounds__(gs_threads(CPT)) __attribute__((amdgpu_waves_per_eu(CPT == 2 ? FFD_GS_CPT2_WAVES : 1)))
+template <int W, bool EXACT, bool TALL, bool SPLIT = false, int CPT = 4, int BY = GS_BY>
+__global__ __launch_bounds__(gs_threads(CPT, BY))
+__attribute__((amdgpu_waves_per_eu(CPT == 2 ? (BY == GS_BY ? FFD_GS_CPT2_WAVES : FFD_GS_CPT2S_WAVES) : 1)))
 void k_gabor_sep(const FaceDesc* __restrict__ faces,
                                                           const uint8_t* __restrict__ gray,
                                                           const float* __restrict__ coef,
@@ -614,19 +621,20 @@ void k_gabor_sep(const FaceDesc* __restrict__ faces,
   static_assert(!(TALL && SPLIT), "tall faces are not banded across workgroups");
   constexpr int R = (W - 1) / 2;
   using C = GSep<R, CPT>;
-  constexpr int GS_THREADS = C::NT;
+  constexpr int GS_THREADS = gs_threads(CPT, BY);
   static_assert(CPT == 4 || (CPT == 2 && !TALL && !SPLIT), "2-column threads: the batch instance only");
+  static_assert(GS_BY % BY == 0, "bands: the staged rows are allocated for whole bands of 8 rows");
   constexpr int NU = W == 9 ? 1 : W == 13 ? 2 : W == 19 ? 3 : 4;
   // magnitude sqrt / min-max forms per scale (r2e, C2, ms): 25x25 sqrtf + masked min-max 1.88 (both
   // compiler forms 1.93, both fast 2.04: SGPR spills); 19x19 both fast 1.63 (1.72); 13x13 / 9x9
   // mag_sqrt + predicated min-max 1.44 / 1.30 (1.54 / 1.34; masked: SGPR spills, 2.8 / 1.7)
   constexpr bool GS_FAST = W != 25, GS_MASK = W == 25 || W == 19;
   extern __shared__ __attribute__((aligned(16))) uint8_t gface[];  // (H + 2R) x GP reflect-101 padded face
-  __shared__ float vg[GS_BY * C::VP];
+  __shared__ float vg[BY * C::VP];
   // QS: the V / H passes in two plane halves (half the V-plane LDS, fewer live registers): measured faster
   // for 9x9 only (1.34 -> 1.16 ms; 13x13 / 19x19 even, 25x25 1.96 -> 2.43)
   constexpr bool QS = GS_QSPLIT && W == 9 && CPT == 4;
-  __shared__ f2 vq[QS ? 2 : 4][GS_BY * C::VP];
+  __shared__ f2 vq[QS ? 2 : 4][BY * C::VP];
   const FaceDesc fd = faces[blockIdx.x];
   if (!fd.valid || fd.nochan || ((FFD_GABOR_BAND_ALL && !SPLIT) ? !TALL : (fd.H > MAX_FACE_H) != TALL)) return;
   if (EXACT && !redo[blockIdx.x]) return;  // the fast instance's mag_sqrt was exact for this face
@@ -663,21 +671,21 @@ void k_gabor_sep(const FaceDesc* __restrict__ faces,
   // this workgroup's rows [yb, ye): the whole face, or (SPLIT) its share of the face's bands
   int yb = 0, ye = FH, nwg = 1;
   if (SPLIT) {
-    const int nbands = (FH + GS_BY - 1) / GS_BY, per = (nbands + gridDim.y - 1) / gridDim.y;
+    const int nbands = (FH + BY - 1) / BY, per = (nbands + gridDim.y - 1) / gridDim.y;
     nwg = (nbands + per - 1) / per;
     if ((int)blockIdx.y >= nwg) return;
-    yb = blockIdx.y * per * GS_BY;
-    ye = min(FH, yb + per * GS_BY);
+    yb = blockIdx.y * per * BY;
+    ye = min(FH, yb + per * BY);
   }
   // the padded rows of those bands, once: up to the last band's end (whole bands + 2R: every row the V
   // pass reads is staged)
-  if (!TALL) stage_rows(yb, (ye - yb + GS_BY - 1) / GS_BY * GS_BY + 2 * R);
+  if (!TALL) stage_rows(yb, (ye - yb + BY - 1) / BY * BY + 2 * R);
 
 #pragma unroll 1
-  for (int y0 = yb; y0 < ye; y0 += GS_BY) {  // probe 5: epilogue only
+  for (int y0 = yb; y0 < ye; y0 += BY) {  // probe 5: epilogue only
     __syncthreads();  // the face is staged; the previous H pass is done with vg / vq
     if (TALL) {       // (the previous V pass is done with gface: the barrier before the H pass)
-      stage_rows(y0, GS_BY + 2 * R);
+      stage_rows(y0, BY + 2 * R);
       __syncthreads();
     }
     // ---- H pass (below): thread = (row hr, column group cq), outputs x = CPT cq + k
@@ -701,7 +709,7 @@ void k_gabor_sep(const FaceDesc* __restrict__ faces,
       constexpr int QLO = decltype(qlo_c)::value, QN = decltype(qn_c)::value;
       constexpr bool G = decltype(g_c)::value;
 #pragma unroll 1
-      for (int i = tid; i < GS_BY * C::SC; i += GS_THREADS) {
+      for (int i = tid; i < BY * C::SC; i += GS_THREADS) {
         const int r = i / C::SC, cc = i - r * C::SC;
         if (cc >= NPC) continue;
         const uint8_t* col = &gface[((TALL ? 0 : y0 - yb) + r + R) * C::GP + cc];
@@ -791,7 +799,7 @@ void k_gabor_sep(const FaceDesc* __restrict__ faces,
     } else {
     // ---- V pass
 #pragma unroll 1
-    for (int i = tid; i < GS_BY * C::SC; i += GS_THREADS) {
+    for (int i = tid; i < BY * C::SC; i += GS_THREADS) {
       const int r = i / C::SC, cc = i - r * C::SC;
       if (cc >= NPC) continue;
       const uint8_t* col = &gface[((TALL ? 0 : y0 - yb) + r + R) * C::GP + cc];
@@ -2629,7 +2637,11 @@ void launch_gabor(int nu, const FaceDesc* faces, int n, int max_h, const uint8_t
       continue;
     }
 #define FFD_GABOR_LAUNCH(WV, RV)                                                                              \
-  if ((FFD_GS_CPT2_MASK >> nu) & 1)                                                                             \
+  if ((FFD_GS_CPT2S_MASK >> nu) & 1)                                                                            \
+    (exact ? k_gabor_sep<WV, true, false, false, 2, 4> : k_gabor_sep<WV, false, false, false, 2, 4>)<<<n,        \
+        gs_threads(2, 4), gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, mag, chan, rd,     \
+                                                                                force_exact, nullptr);         \
+  else if ((FFD_GS_CPT2_MASK >> nu) & 1)                                                                        \
     (exact ? k_gabor_sep<WV, true, false, false, 2> : k_gabor_sep<WV, false, false, false, 2>)<<<n, gs_threads(2), \
         gabor_face_lds(RV, std::min(max_h, MAX_FACE_H)), s>>>(faces, gray, c, mag, chan, rd, force_exact, nullptr); \
   else                                                                                                          \
@@ -2746,6 +2758,9 @@ hipError_t set_gabor_lds_limit(int bytes) {
                        (const void*)k_gabor_sep<13, false, false, false, 2>, (const void*)k_gabor_sep<19, false, false, false, 2>,
                        (const void*)k_gabor_sep<25, false, false, false, 2>, (const void*)k_gabor_sep<13, true, false, false, 2>,
                        (const void*)k_gabor_sep<19, true, false, false, 2>,  (const void*)k_gabor_sep<25, true, false, false, 2>,
+                       (const void*)k_gabor_sep<13, false, false, false, 2, 4>, (const void*)k_gabor_sep<19, false, false, false, 2, 4>,
+                       (const void*)k_gabor_sep<25, false, false, false, 2, 4>, (const void*)k_gabor_sep<13, true, false, false, 2, 4>,
+                       (const void*)k_gabor_sep<19, true, false, false, 2, 4>,  (const void*)k_gabor_sep<25, true, false, false, 2, 4>,
                        (const void*)k_integral<true>};
   for (const void* f : fns) {
     hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
