@@ -58,58 +58,71 @@ __global__ __launch_bounds__(256) void k_haar_gray(const HaarFrame* __restrict__
   const HaarFrame f = frames[blockIdx.y];
   const uint8_t* img = images + f.img_off;
   uint8_t* g = gray + f.gray_off;
-  const int n = f.w * f.h;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const int y = i / f.w, x = i - y * f.w;
+  const int cpr = (f.w + 255) / 256, n = cpr * f.h;  // steps of 256 pixels of one row (the row index wave-uniform)
+  for (int t = blockIdx.x; t < n; t += gridDim.x) {
+    const int y = t / cpr, x = (t - y * cpr) * 256 + threadIdx.x;
+    if (x >= f.w) continue;
     const uint8_t* p = img + (int64_t)y * f.stride + 3 * x;
-    g[i] = (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14);
+    g[(int64_t)y * f.w + x] = (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14);
   }
 }
 
 // ------------------------------------------------------------------------ resize ----
 // resize(INTER_LINEAR) 8U as oracle cv_resize (OpenCV 2.4.9 fixed point: 11-bit horizontal
 // coefficients, SSE2 vertical pass on columns [0, xv), scalar tail); mode 0 copy, 2 area 2x.
+// A workgroup step is a tile of 256 columns x HZ_ROWS rows: each thread's column coefficients (source column,
+// 11-bit weights) are computed once for the tile's rows, each row's (wave-uniform) once per row — the same
+// expressions as per pixel, hoisted (round 6: a thread per pixel with an integer division and both coefficient sets
+// per pixel, C3 377 us per 64 frames).
+#ifndef FFD_HAAR_RESIZE_ROWS
+#define FFD_HAAR_RESIZE_ROWS 8
+#endif
+constexpr int HZ_ROWS = FFD_HAAR_RESIZE_ROWS;
 __global__ __launch_bounds__(256) void k_haar_resize(const HaarLevel* __restrict__ levels,
                                                      const uint8_t* __restrict__ gray, uint8_t* __restrict__ scaled) {
   const HaarLevel L = levels[blockIdx.y];
   const uint8_t* src = gray + L.gray_off;
   uint8_t* dst = scaled + L.img_off;
-  const int sw = L.src_w, sh = L.src_h, n = L.sw * L.sh;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const int dy = i / L.sw, dx = i - dy * L.sw;
-    int v;
+  const int sw = L.src_w, sh = L.src_h;
+  const int ncb = (L.sw + 255) / 256, tiles = ncb * ((L.sh + HZ_ROWS - 1) / HZ_ROWS);
+  for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int rb = t / ncb, dx = (t - rb * ncb) * 256 + threadIdx.x, y0 = rb * HZ_ROWS, y1 = min(L.sh, y0 + HZ_ROWS);
+    if (dx >= L.sw) continue;
+    uint8_t* out = dst + (int64_t)y0 * L.sw + dx;
     if (L.mode == 0) {
-      v = src[(int64_t)dy * sw + dx];
-    } else if (L.mode == 2) {
-      const uint8_t* s0 = src + (int64_t)(2 * dy) * sw + 2 * dx;
-      v = (s0[0] + s0[1] + s0[sw] + s0[sw + 1] + 2) >> 2;
-    } else {
-      float fx = (float)((dx + 0.5) * L.scale_x - 0.5);
-      int sx = (int)floorf(fx);
-      fx -= sx;
-      if (sx < 0) fx = 0, sx = 0;
-      bool right = false;
-      if (sx + 1 >= sw) {
-        right = true;
-        if (sx >= sw - 1) fx = 0, sx = sw - 1;
+      for (int dy = y0; dy < y1; dy++, out += L.sw) *out = src[(int64_t)dy * sw + dx];
+      continue;
+    }
+    if (L.mode == 2) {
+      for (int dy = y0; dy < y1; dy++, out += L.sw) {
+        const uint8_t* s0 = src + (int64_t)(2 * dy) * sw + 2 * dx;
+        *out = (uint8_t)((s0[0] + s0[1] + s0[sw] + s0[sw + 1] + 2) >> 2);
       }
-      const int a0 = hsat_s16(hround((1.f - fx) * 2048.f)), a1 = hsat_s16(hround(fx * 2048.f));
+      continue;
+    }
+    float fx = (float)((dx + 0.5) * L.scale_x - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= sx;
+    if (sx < 0) fx = 0, sx = 0;
+    bool right = false;
+    if (sx + 1 >= sw) {
+      right = true;
+      if (sx >= sw - 1) fx = 0, sx = sw - 1;
+    }
+    const int a0 = right ? 2048 : hsat_s16(hround((1.f - fx) * 2048.f)), a1 = right ? 0 : hsat_s16(hround(fx * 2048.f));
+    const int sx1 = right ? sx : sx + 1;  // (right: r = p[sx] * 2048, as a0 = 2048, a1 = 0 gives)
+    const bool vec = dx < L.xv;
+    for (int dy = y0; dy < y1; dy++, out += L.sw) {
       float fy = (float)((dy + 0.5) * L.scale_y - 0.5);
       const int sy = (int)floorf(fy);
       fy -= sy;
       const int b0 = hsat_s16(hround((1.f - fy) * 2048.f)), b1 = hsat_s16(hround(fy * 2048.f));
-      const int y0 = min(max(sy, 0), sh - 1), y1 = min(max(sy + 1, 0), sh - 1);
-      const uint8_t* r0p = src + (int64_t)y0 * sw;
-      const uint8_t* r1p = src + (int64_t)y1 * sw;
-      int r0, r1;
-      if (right) {
-        r0 = r0p[sx] * 2048;
-        r1 = r1p[sx] * 2048;
-      } else {
-        r0 = r0p[sx] * a0 + r0p[sx + 1] * a1;
-        r1 = r1p[sx] * a0 + r1p[sx + 1] * a1;
-      }
-      if (dx < L.xv) {
+      const int yy0 = min(max(sy, 0), sh - 1), yy1 = min(max(sy + 1, 0), sh - 1);
+      const uint8_t* r0p = src + (int64_t)yy0 * sw;
+      const uint8_t* r1p = src + (int64_t)yy1 * sw;
+      const int r0 = r0p[sx] * a0 + r0p[sx1] * a1, r1 = r1p[sx] * a0 + r1p[sx1] * a1;
+      int v;
+      if (vec) {
         const int s0 = max(-32768, min(32767, r0 >> 4)), s1 = max(-32768, min(32767, r1 >> 4));
         int m = max(-32768, min(32767, ((s0 * b0) >> 16) + ((s1 * b1) >> 16)));
         m = max(-32768, min(32767, m + 2)) >> 2;
@@ -117,8 +130,8 @@ __global__ __launch_bounds__(256) void k_haar_resize(const HaarLevel* __restrict
       } else {
         v = hsat_u8((b0 * r0 + b1 * r1 + (1 << 21)) >> 22);
       }
+      *out = (uint8_t)v;
     }
-    dst[i] = (uint8_t)v;
   }
 }
 
@@ -773,7 +786,8 @@ void launch_haar_gray(const HaarFrame* frames, int n_frames, int max_pixels, con
 
 void launch_haar_pyramid(const HaarLevel* levels, int n_levels, int max_pixels, int max_rows, int max_cols,
                          const uint8_t* gray, uint8_t* scaled, int32_t* sum, uint32_t* sq, hipStream_t s) {
-  k_haar_resize<<<dim3(std::min(512, (max_pixels + 255) / 256), n_levels), 256, 0, s>>>(levels, gray, scaled);
+  k_haar_resize<<<dim3(std::min(512, (max_pixels + 256 * HZ_ROWS - 1) / (256 * HZ_ROWS) + 1), n_levels), 256, 0, s>>>(levels, gray,
+                                                                                                         scaled);
   k_haar_rows<<<dim3(std::min(256, (max_rows + 1 + 3) / 4), n_levels), 256, 0, s>>>(levels, scaled, sum, sq);
   k_haar_cols<<<dim3((max_cols + 255) / 256, n_levels), 256, 0, s>>>(levels, sum, sq);
 }
