@@ -955,10 +955,11 @@ __device__ __forceinline__ int rect_mean_lds(const unsigned char* __restrict__ p
   const uint32_t a = *reinterpret_cast<const uint16_t*>(p), b = *reinterpret_cast<const uint16_t*>(p + wb);
   const uint32_t f0 = *reinterpret_cast<const uint16_t*>(p + r2), f1 = *reinterpret_cast<const uint16_t*>(p + r2 + wb);
   const uint32_t c = *reinterpret_cast<const uint16_t*>(p + r1), d = *reinterpret_cast<const uint16_t*>(p + r1 + wb);
-  // top = (a - b) + (d - c), bot = (f1 - f0) - (d - c), each mod 2^16 (u16 arithmetic), R = top + bot
-  typedef unsigned short u16;
-  const u16 dc = (u16)(d - c), top = (u16)((u16)(a - b) + dc), bot = (u16)((u16)(f1 - f0) - dc);
-  return (int)__builtin_fmaf((float)((uint32_t)top + bot), __builtin_amdgcn_rcpf((float)area), 0.00075f);
+  // top = (a - b) + (d - c), bot = (f1 - f0) - (d - c), each mod 2^16, R = top + bot — in 32-bit registers, masked:
+  // as u16 arithmetic the SLP vectorizer pairs a test's two rectangles into v_pk_sub_i16 / v_pk_add_u16 with
+  // v_perm_b32 repacks and a v_pk_fma_f32 (round 6: FFD traversal 8.02-8.07 -> 7.94-7.99 ms)
+  const uint32_t dc = d - c, top = (a - b + dc) & 0xFFFFu, bot = (f1 - f0 - dc) & 0xFFFFu;
+  return (int)__builtin_fmaf((float)(top + bot), __builtin_amdgcn_rcpf((float)area), 0.00075f);
 }
 
 // Rectangle means of float-integral faces (FaceDesc::fint: the reference's CV_32F integral may round,
