@@ -57,7 +57,7 @@ def main():
         alts = [prefix, prefix.replace(", 4, 8>", ">")]  # (a demangler may print default template arguments or not)
         tkey = next((k for a in alts for k in traffic if k.startswith(a + "(")), None)
         t = traffic.get(tkey, {})
-        per_launch = t.get("traffic_bytes", 0) / max(1, t.get("launches", 1))
+        per_launch = t.get("traffic_bytes", 0)  # (tools/pmc_traffic.py: already the average per launch)
         rows.append({
             "scale": scale, "kernel": name, "ms": stages.get("gabor_" + scale), "threads": threads,
             "vgprs": r["vgprs"], "sgprs": r["sgprs"], "sgpr_spills": r["sgpr_spills"], "vgpr_spills": r["vgpr_spills"],
