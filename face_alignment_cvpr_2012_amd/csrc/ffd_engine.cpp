@@ -488,11 +488,13 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   // one channel plane stride for the whole batch (the traversal's window staging assumes it)
   int64_t plane = PITCH;
   int max_h = 1;
+  int64_t max_src = 0;
   bool any_fint = false, any_wide = false;
   for (auto& f : fds)
     if (f.valid) {
       plane = std::max(plane, (int64_t)(f.H + 1) * PITCH);
       max_h = std::max(max_h, f.H);
+      if (!f.nochan) max_src = std::max(max_src, (int64_t)f.bw * f.bh);
       any_fint |= f.fint != 0;
       f.wide = force_wide || votes_wide(f, desc.mp_option.step_size, mp_step_y(), patch / 2, vote_range);
       any_wide |= f.wide != 0;
@@ -532,7 +534,9 @@ void ffd_engine::run_chunk(Workspace& w, const uint8_t* d_images, FaceOut* d_out
   HIP_CHECK(hipMemsetAsync(d_out, 0, (size_t)n * sizeof(FaceOut), st));
 
   const FaceDesc* dfd = w.faces.as<FaceDesc>();
-  stage(0, st, [&] { launch_gray_resize(dfd, n, d_images, w.gray.as<uint8_t>(), st); });
+  stage(0, st, [&] {
+    launch_gray_resize(dfd, n, d_images, w.gray.as<uint8_t>(), st, max_src > (int64_t)1 << 30 ? 0 : (int)max_src);
+  });
   // channel stage: Gabor scales 4..0 and the gray / Sobel integrals, dealt over the fork streams
   // (a large chunk fills the chip with one kernel at a time, so it forks only when FFD_CHANNEL_STREAMS
   // asks; a small one runs all six channel kernels side by side: single-face latency)

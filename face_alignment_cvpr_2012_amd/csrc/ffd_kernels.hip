@@ -64,58 +64,94 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
 // ------------------------------------------------------ gray + ROI + resize --
 // One workgroup per face; OpenCV 2.4.9 resize(INTER_LINEAR) 8U fixed-point path
 // (HResizeLinear + VResizeLinearVec_32s8u SSE2 columns [0, xv) + scalar tail).
+// STAGED (batches, source box <= the launch's dynamic LDS): the face's source box is first converted to gray into
+// LDS (each source pixel once, coalesced BGR reads), then each thread owns one output column (its horizontal
+// coefficients computed once) and walks every other row — the same expressions as the per-pixel form (round 6: C2
+// 0.32 ms with each output pixel converting its four source pixels and dividing its index).
+template <bool STAGED = false>
 __global__ __launch_bounds__(256) void k_gray_resize(const FaceDesc* __restrict__ faces,
                                                      const uint8_t* __restrict__ images,
-                                                     uint8_t* __restrict__ gray) {
+                                                     uint8_t* __restrict__ gray, int lds_cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_src[];
   const FaceDesc fd = faces[blockIdx.x];
   if (!fd.valid || fd.nochan) return;
   const uint8_t* img = images + fd.img_off;
   uint8_t* out = gray + fd.gray_off;
+  const int sw = fd.bw, sh = fd.bh;
+  const bool st = STAGED && sw * sh <= lds_cap;  // (a larger box: the per-pixel form below)
+  if (st) {  // 8 pixels per thread per step, all their loads issued before the LDS stores (HBM latency, not bytes)
+    const int n = sw * sh;
+    for (int i0 = 0; i0 < n; i0 += 8 * 256) {
+      uint8_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = min(i0 + k * 256 + (int)threadIdx.x, n - 1), y = i / sw, x = i - y * sw;
+        v[k] = gray_px(img + (int64_t)(fd.by + y) * fd.img_stride + 3 * (fd.bx + x));
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (i0 + k * 256 + (int)threadIdx.x < n) s_src[i0 + k * 256 + threadIdx.x] = v[k];
+    }
+    __syncthreads();
+  }
   auto G = [&](int y, int x) -> int {
+    if (st) return s_src[y * sw + x];
     return gray_px(img + (int64_t)(fd.by + y) * fd.img_stride + 3 * (fd.bx + x));
   };
-  const int sw = fd.bw, sh = fd.bh;
+  // horizontal / vertical coefficients of the bilinear mode (OpenCV 2.4.9 fixed point, as oracle cv_resize)
+  auto xcoef = [&](int dx, int& sx, int& a0, int& a1, bool& right) {
+    float fx = (float)((dx + 0.5) * fd.scale_x - 0.5);
+    sx = (int)floorf(fx);
+    fx -= sx;
+    if (sx < 0) fx = 0, sx = 0;
+    right = false;
+    if (sx + 1 >= sw) {
+      right = true;
+      if (sx >= sw - 1) fx = 0, sx = sw - 1;
+    }
+    a0 = sat_s16(cv_round((1.f - fx) * 2048.f));
+    a1 = sat_s16(cv_round(fx * 2048.f));
+  };
+  auto pixel = [&](int dy, int dx, int sx, int a0, int a1, bool right) -> int {
+    if (fd.mode == 0) return G(dy, dx);
+    if (fd.mode == 2)
+      return (G(2 * dy, 2 * dx) + G(2 * dy, 2 * dx + 1) + G(2 * dy + 1, 2 * dx) + G(2 * dy + 1, 2 * dx + 1) + 2) >> 2;
+    float fy = (float)((dy + 0.5) * fd.scale_y - 0.5);
+    int sy = (int)floorf(fy);
+    fy -= sy;
+    int b0 = sat_s16(cv_round((1.f - fy) * 2048.f)), b1 = sat_s16(cv_round(fy * 2048.f));
+    int y0 = min(max(sy, 0), sh - 1), y1 = min(max(sy + 1, 0), sh - 1);
+    int r0, r1;
+    if (right) {
+      r0 = G(y0, sx) * 2048;
+      r1 = G(y1, sx) * 2048;
+    } else {
+      r0 = G(y0, sx) * a0 + G(y0, sx + 1) * a1;
+      r1 = G(y1, sx) * a0 + G(y1, sx + 1) * a1;
+    }
+    if (dx < fd.xv) {
+      int s0 = max(-32768, min(32767, r0 >> 4)), s1 = max(-32768, min(32767, r1 >> 4));
+      int m = max(-32768, min(32767, ((s0 * b0) >> 16) + ((s1 * b1) >> 16)));
+      m = max(-32768, min(32767, m + 2)) >> 2;
+      return sat_u8(m);
+    }
+    return sat_u8((b0 * r0 + b1 * r1 + (1 << 21)) >> 22);
+  };
+  if (st) {  // a thread per output column (W <= 125 < 128), two rows per pass
+    const int dx = threadIdx.x & 127;
+    if (dx >= fd.W) return;
+    int sx = 0, a0 = 0, a1 = 0;
+    bool right = false;
+    if (fd.mode == 1) xcoef(dx, sx, a0, a1, right);
+    for (int dy = threadIdx.x >> 7; dy < fd.H; dy += 2) out[dy * PITCH + dx] = (uint8_t)pixel(dy, dx, sx, a0, a1, right);
+    return;
+  }
   for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < fd.W * fd.H; i += gridDim.y * blockDim.x) {
     int dy = i / fd.W, dx = i % fd.W;
-    int v;
-    if (fd.mode == 0) {
-      v = G(dy, dx);
-    } else if (fd.mode == 2) {
-      v = (G(2 * dy, 2 * dx) + G(2 * dy, 2 * dx + 1) + G(2 * dy + 1, 2 * dx) + G(2 * dy + 1, 2 * dx + 1) + 2) >> 2;
-    } else {
-      float fx = (float)((dx + 0.5) * fd.scale_x - 0.5);
-      int sx = (int)floorf(fx);
-      fx -= sx;
-      if (sx < 0) fx = 0, sx = 0;
-      bool right = false;
-      if (sx + 1 >= sw) {
-        right = true;
-        if (sx >= sw - 1) fx = 0, sx = sw - 1;
-      }
-      int a0 = sat_s16(cv_round((1.f - fx) * 2048.f)), a1 = sat_s16(cv_round(fx * 2048.f));
-      float fy = (float)((dy + 0.5) * fd.scale_y - 0.5);
-      int sy = (int)floorf(fy);
-      fy -= sy;
-      int b0 = sat_s16(cv_round((1.f - fy) * 2048.f)), b1 = sat_s16(cv_round(fy * 2048.f));
-      int y0 = min(max(sy, 0), sh - 1), y1 = min(max(sy + 1, 0), sh - 1);
-      int r0, r1;
-      if (right) {
-        r0 = G(y0, sx) * 2048;
-        r1 = G(y1, sx) * 2048;
-      } else {
-        r0 = G(y0, sx) * a0 + G(y0, sx + 1) * a1;
-        r1 = G(y1, sx) * a0 + G(y1, sx + 1) * a1;
-      }
-      if (dx < fd.xv) {
-        int s0 = max(-32768, min(32767, r0 >> 4)), s1 = max(-32768, min(32767, r1 >> 4));
-        int m = max(-32768, min(32767, ((s0 * b0) >> 16) + ((s1 * b1) >> 16)));
-        m = max(-32768, min(32767, m + 2)) >> 2;
-        v = sat_u8(m);
-      } else {
-        v = sat_u8((b0 * r0 + b1 * r1 + (1 << 21)) >> 22);
-      }
-    }
-    out[dy * PITCH + dx] = (uint8_t)v;
+    int sx = 0, a0 = 0, a1 = 0;
+    bool right = false;
+    if (fd.mode == 1) xcoef(dx, sx, a0, a1, right);
+    out[dy * PITCH + dx] = (uint8_t)pixel(dy, dx, sx, a0, a1, right);
   }
 }
 
@@ -193,17 +229,56 @@ __device__ __forceinline__ void integral_scan(uint16_t* __restrict__ out, int W,
 // integrated by the Gabor kernels themselves.  One 4-wave workgroup per face (the 4th wave idles).
 // STAGE (small batches): the face's gray rows are first copied to LDS by all four waves, so the three
 // sequential scans read their values at LDS rather than L2 latency.
+#ifndef FFD_SOBEL_ROWS
+#define FFD_SOBEL_ROWS 1  // Sobel values from each batch's source rows read once (0: six neighbour reads per value)
+#endif
+#ifndef FFD_INTEGRAL_STAGE_ALL
+#define FFD_INTEGRAL_STAGE_ALL 1  // batches too stage the face's gray rows in LDS (0: small batches only)
+#endif
 // One of the non-Gabor integral channels (c = 0 gray, 36 Sobel d/dy, 37 Sobel d/dx) of a face, by one wave; g: the
 // face's gray rows (global, or staged in LDS).
 __device__ __forceinline__ void integral_channel(const FaceDesc& fd, const uint8_t* g, uint16_t* __restrict__ chan,
                                                  int c, int lane) {
   const int W = fd.W, H = fd.H, x0 = 2 * lane;
-  integral_scan(chan + fd.ch_off + (int64_t)c * fd.plane, W, H, lane, fd.fint != 0, [&](int y0, uint32_t* v0, uint32_t* v1) {
+  uint16_t* out = chan + fd.ch_off + (int64_t)c * fd.plane;
+  if (c == 0 || !FFD_SOBEL_ROWS) {
+    integral_scan(out, W, H, lane, fd.fint != 0, [&](int y0, uint32_t* v0, uint32_t* v1) {
 #pragma unroll
-    for (int b = 0; b < 8; b++) {
-      const int y = min(y0 + b, H - 1);
-      v0[b] = (uint32_t)chan_value(c, g, W, H, y, x0);
-      v1[b] = (uint32_t)chan_value(c, g, W, H, y, x0 + 1);
+      for (int b = 0; b < 8; b++) {
+        const int y = min(y0 + b, H - 1);
+        v0[b] = (uint32_t)chan_value(c, g, W, H, y, x0);
+        v1[b] = (uint32_t)chan_value(c, g, W, H, y, x0 + 1);
+      }
+    });
+    return;
+  }
+  // Sobel (chan_value's arithmetic): a batch of 8 rows reads its 10 source rows (reflect-101) once, at the lane's
+  // four columns x0 - 1, x0, x0 + 1, x0 + 2 (reflect-101), instead of six neighbours per value (12 per row)
+  const int xs = min(x0, W - 1);  // (lanes past the face read valid columns; their values are 0)
+  const int ca = reflect101(xs - 1, W), cb = xs, cc = reflect101(xs + 1, W), cd = reflect101(xs + 2, W);
+  const bool in0 = x0 < W, in1 = x0 + 1 < W;
+  integral_scan(out, W, H, lane, fd.fint != 0, [&](int y0, uint32_t* v0, uint32_t* v1) {
+    int A[10], B[10], C[10], D[10];
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+      const uint8_t* row = g + reflect101(min(y0 - 1 + k, H), H) * PITCH;  // (rows past H - 1: unused values)
+      A[k] = row[ca];
+      B[k] = row[cb];
+      C[k] = row[cc];
+      D[k] = row[cd];
+    }
+#pragma unroll
+    for (int b = 0; b < 8; b++) {  // rows ym = b, y = b + 1, yp = b + 2 of the arrays
+      int s0, s1;
+      if (c == 36) {  // Sobel(0,1): d/dy
+        s0 = (A[b + 2] + 2 * B[b + 2] + C[b + 2]) - (A[b] + 2 * B[b] + C[b]);
+        s1 = (B[b + 2] + 2 * C[b + 2] + D[b + 2]) - (B[b] + 2 * C[b] + D[b]);
+      } else {        // Sobel(1,0): d/dx
+        s0 = (C[b] + 2 * C[b + 1] + C[b + 2]) - (A[b] + 2 * A[b + 1] + A[b + 2]);
+        s1 = (D[b] + 2 * D[b + 1] + D[b + 2]) - (B[b] + 2 * B[b + 1] + B[b + 2]);
+      }
+      v0[b] = in0 ? (uint32_t)sat_u8(s0) : 0u;
+      v1[b] = in1 ? (uint32_t)sat_u8(s1) : 0u;
     }
   });
 }
@@ -212,7 +287,7 @@ __device__ __forceinline__ void integral_channel(const FaceDesc& fd, const uint8
 #define FFD_GS_CPT2_MASK 12  // bit nu (2: 13x13, 3: 19x19, 4: 25x25): the batch instance with 2 columns per H-pass thread (25x25: spills at 128 VGPRs, 1.93 -> 2.68 ms)
 #endif
 #ifndef FFD_GS_CPT2S_MASK
-#define FFD_GS_CPT2S_MASK 16  // bit nu: the 2-column instance in 256-thread workgroups (4-row bands; 25x25 1.91 -> 1.74 ms)
+#define FFD_GS_CPT2S_MASK 18  // bit nu: the 2-column instance in 256-thread workgroups (4-row bands; 25x25 1.91 -> 1.74, 9x9 1.20 -> 1.16 ms)
 #endif
 #ifndef FFD_GS_CPT2S_WAVES
 #define FFD_GS_CPT2S_WAVES 3  // ... its waves per SIMD (3: <= 168 VGPRs, three workgroups per CU)
@@ -2587,9 +2662,15 @@ __global__ __launch_bounds__(256) void k_meanshift5(const FaceDesc* __restrict__
 }
 
 // ------------------------------------------------------------------ launch --
-void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s) {
+#ifndef FFD_GRAY_STAGE_MAX
+#define FFD_GRAY_STAGE_MAX 48 * 1024  // batches whose largest source box is at most this many pixels: k_gray_resize<true>
+#endif
+void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s, int max_src) {
   // small batches: a face's pixels spread over 8 workgroups (single-face latency)
-  k_gray_resize<<<dim3(n, n <= FFD_GABOR_SPLIT_MAX ? 8 : 1), 256, 0, s>>>(faces, images, gray);
+  if (n <= FFD_GABOR_SPLIT_MAX || max_src <= 0 || max_src > FFD_GRAY_STAGE_MAX)
+    k_gray_resize<false><<<dim3(n, n <= FFD_GABOR_SPLIT_MAX ? 8 : 1), 256, 0, s>>>(faces, images, gray, 0);
+  else
+    k_gray_resize<true><<<n, 256, (max_src + 15) / 16 * 16, s>>>(faces, images, gray, max_src);
 }
 
 // dynamic LDS of k_gabor_sep: the padded u8 face of the tallest face of the batch, its rows rounded up
@@ -2683,7 +2764,9 @@ void launch_check_mag_sqrt(uint32_t lo, uint32_t n, uint32_t* bad, int blocks, h
 
 void launch_integral(const FaceDesc* faces, int n, int max_h, const uint8_t* gray, uint16_t* chan, hipStream_t s) {
   if (n <= 0) return;
-  if (n <= FFD_GABOR_SPLIT_MAX && max_h <= MAX_FACE_H)  // small batches: the face staged in LDS (<= 75 KB)
+  // the face's gray rows staged in LDS (<= 75 KB): small batches, and batches (FFD_INTEGRAL_STAGE_ALL: the byte reads
+  // of the three scans at LDS rather than the texture path)
+  if ((n <= FFD_GABOR_SPLIT_MAX || FFD_INTEGRAL_STAGE_ALL) && max_h <= MAX_FACE_H)
     k_integral<true><<<n, 256, (size_t)max_h * PITCH, s>>>(faces, gray, chan);
   else
     k_integral<false><<<n, 256, 0, s>>>(faces, gray, chan);
@@ -2759,6 +2842,7 @@ hipError_t set_gabor_lds_limit(int bytes) {
                        (const void*)k_gabor_sep<13, false, false, false, 2>, (const void*)k_gabor_sep<19, false, false, false, 2>,
                        (const void*)k_gabor_sep<25, false, false, false, 2>, (const void*)k_gabor_sep<13, true, false, false, 2>,
                        (const void*)k_gabor_sep<19, true, false, false, 2>,  (const void*)k_gabor_sep<25, true, false, false, 2>,
+                       (const void*)k_gabor_sep<9, false, false, false, 2, 4>, (const void*)k_gabor_sep<9, true, false, false, 2, 4>,
                        (const void*)k_gabor_sep<13, false, false, false, 2, 4>, (const void*)k_gabor_sep<19, false, false, false, 2, 4>,
                        (const void*)k_gabor_sep<25, false, false, false, 2, 4>, (const void*)k_gabor_sep<13, true, false, false, 2, 4>,
                        (const void*)k_gabor_sep<19, true, false, false, 2, 4>,  (const void*)k_gabor_sep<25, true, false, false, 2, 4>,

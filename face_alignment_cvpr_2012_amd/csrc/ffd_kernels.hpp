@@ -22,7 +22,9 @@ constexpr int GABOR_OFF4 = GABOR_OFF3 + gabor_sep_block(9);
 constexpr int GABOR_COEF_TOTAL = GABOR_OFF4 + gabor_sep_block(12);
 constexpr int GABOR_OFFS[5] = {GABOR_OFF0, GABOR_OFF1, GABOR_OFF2, GABOR_OFF3, GABOR_OFF4};
 
-void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s);
+// max_src: the largest valid face's source box (bw x bh pixels) of the batch, 0 = unknown (the per-pixel form)
+void launch_gray_resize(const FaceDesc* faces, int n, const uint8_t* images, uint8_t* gray, hipStream_t s,
+                        int max_src = 0);
 // Gabor scale nu (0..4): magnitudes of the 7 orientations, face-wide min-max normalisation,
 // quantisation and integration of the 7 channels (one workgroup per face)
 // max_h: the tallest scaled face of the batch (sizes the padded-face LDS copy)

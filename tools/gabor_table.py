@@ -18,10 +18,10 @@ import sys
 
 LDS_CU = 160 * 1024
 PITCH = 128  # ffd_device.hpp
-# the batch instance each scale launches at C2 (FFD_GS_CPT2S_MASK 16, FFD_GS_CPT2_MASK 12)
+# the batch instance each scale launches at C2 (FFD_GS_CPT2S_MASK 18, FFD_GS_CPT2_MASK 12)
 INSTANCE = {
     "7x7": ("void ffd::k_gabor7<false, false>", 512),
-    "9x9": ("void ffd::k_gabor_sep<9, false, false, false, 4, 8>", 256),
+    "9x9": ("void ffd::k_gabor_sep<9, false, false, false, 2, 4>", 256),
     "13x13": ("void ffd::k_gabor_sep<13, false, false, false, 2, 8>", 512),
     "19x19": ("void ffd::k_gabor_sep<19, false, false, false, 2, 8>", 512),
     "25x25": ("void ffd::k_gabor_sep<25, false, false, false, 2, 4>", 256),
