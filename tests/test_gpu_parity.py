@@ -121,3 +121,25 @@ def test_batch_order_independence(engine, fixtures):
     for i in range(6):
         np.testing.assert_array_equal(a[i].ffd_cordinates, b[5 - i].ffd_cordinates)
         assert a[i].headpose == b[5 - i].headpose
+
+
+@pytest.fixture(scope="module")
+def batch_staged(engine, oracle_mod, fixtures):
+    """The same cases without the 250 x 250 box: every source box is at most 48 K pixels, so the batch (more than 16
+    faces) runs k_gray_resize<true> (the source box converted to gray into LDS first; copy, bilinear up- and
+    down-scale, tall and wide boxes) — the full batch above takes the per-pixel form because of its 2x box."""
+    cases = [c for c in _cases(fixtures) if c[1][2] * c[1][3] <= 48 * 1024]
+    assert len(cases) > 16 and len(cases) == len(_cases(fixtures)) - 1
+    engine.analyzeFaces([c[0] for c in cases], [c[1] for c in cases])
+    traces = [engine.trace(i, c[1][2], c[1][3]) for i, c in enumerate(cases)]
+    ref = [oracle_mod.analyze_face(c[0], c[1], threads=8, trace=True) for c in cases]
+    return cases, traces, ref
+
+
+def test_gray_face_and_channels_bit_exact_lds_staged(batch_staged):
+    cases, traces, ref = batch_staged
+    for i in range(len(cases)):
+        np.testing.assert_array_equal(traces[i]["face"], ref[i][1]["face"], err_msg=f"case {i}")
+        g, o = traces[i]["channels"], ref[i][1]["channels"]
+        bad = [c for c in range(38) if not np.array_equal(g[c], o[c])]
+        assert not bad, f"case {i}: channels differ {bad}"
